@@ -1,0 +1,243 @@
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE itself.
+
+Runs only in the build container (``/root/reference`` does not exist on the GPU box):
+
+    python tests/golden/make_golden.py
+
+The reference is imported read-only with the two in-process shims SURVEY.md §8(c)
+documents (no file of the reference is modified or copied):
+  1. ``sys.modules['cv2']`` = empty module: custom_model.py:6 / data_process.py:18 import
+     cv2, but the v0.4.0 model path never calls it;
+  2. ``transformers.utils.backbone_utils.load_backbone`` aliased to the transformers 5.15
+     location (custom_model.py:13 expects the 4.47 one).
+Weights come from the deterministic generator (rgbd_amd.init); inputs from the seeded
+synthetic-scene generator (rgbd_amd.synthetic).  Each fixture stores inputs (or the
+sha256 of regenerated inputs) and the reference's outputs.
+
+Fixtures (SURVEY.md §8(c) "Golden vectors"):
+  g1_decompose.npz   a2 + a5-a8: grey, histogram, modes, windows, region codes, pooled codes
+  g2_dsam.npz        a4: DSAModule forward at reduced channels (8->16, 16->32)
+  g3_dggm.npz        a9: DepthGradientInjectionResidual forward at channels [4,8,16,32]
+  g4_ratio.npz       a3: EnhancedDepthImageRatioPredictor eval at 240x320, B=2
+  g5_model.npz       a1+a12: full model eval forward at 320x240 (ratio, logits, sampled features)
+  g6_grads.npz       one loss.backward() at 320x240 B=2 (eval mode): hot-path grad stats
+"""
+import hashlib
+import json
+import sys
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+REPO = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(REPO))
+import _rgbd_import  # noqa: E402,F401  (registers rgbd_amd)
+from rgbd_amd import init as winit, synthetic  # noqa: E402
+from oracle import dggm_pre  # noqa: E402
+
+OUT = Path(__file__).resolve().parent
+REF = "/root/reference"
+
+
+def import_reference():
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    import transformers.utils.backbone_utils as bu
+    from transformers.backbone_utils import load_backbone
+    bu.load_backbone = load_backbone
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import mask2former.utils.custom_model as cm
+    return cm
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ----------------------------------------------------------------------------- inputs
+def decomposition_cases():
+    """List of (name, depth3 f32 [3,H,W], ratio).  Regenerated identically by the tests."""
+    return golden_inputs.decomposition_cases()
+
+
+def main():
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    cm = import_reference()
+    gray = cm.CustomMask2FormerPixelLevelModule.to_grayscale
+
+    # ------------------------------------------------------------------ G1
+    cases = golden_inputs.decomposition_cases()
+    dsam = cm.DSAModule(8, 16)
+    rec = {"names": [], "shapes": [], "ratios": [], "input_sha": [], "n_modes": [],
+           "centers": [], "peak_hist": [], "windows": [], "hist": [], "edges": [],
+           "grey_sha": [], "code": [], "pooled": [], "error": []}
+    for name, d3, r in cases:
+        H, W = d3.shape[1:]
+        g = gray(None, torch.from_numpy(d3))
+        gnp = g.squeeze().cpu().detach().numpy()
+        rec["names"].append(name); rec["shapes"].append((H, W)); rec["ratios"].append(r)
+        rec["input_sha"].append(sha(d3)); rec["grey_sha"].append(sha(gnp))
+        try:
+            hist, edges = dsam._calculate_depth_histogram(gnp)
+        except ValueError as e:
+            rec["error"].append(str(e))
+            for k in ("n_modes", "centers", "peak_hist", "windows", "hist", "edges", "code", "pooled"):
+                rec[k].append(None)
+            continue
+        rec["error"].append("")
+        modes = dsam._select_depth_distribution_modes(hist, edges, num_modes=3)
+        if modes:
+            wins = dsam._define_depth_interval_windows(modes, window_size_ratio=r)
+            masks = dsam._generate_depth_region_masks(gnp, wins)
+        else:
+            wins = []
+            masks = [np.zeros_like(gnp, dtype=bool)] * 4
+        code = np.zeros((H, W), np.uint8)
+        for i, m in enumerate(masks):
+            code |= m.astype(np.uint8) << i
+        pooled = []
+        for (oh, ow) in golden_inputs.pool_sizes(H, W):
+            pc = np.zeros((oh, ow), np.uint8)
+            for i, m in enumerate(masks):
+                t = torch.from_numpy(m).float()[None, None]
+                pm = F.adaptive_max_pool2d(t, (oh, ow))[0, 0].numpy()
+                pc |= (pm > 0).astype(np.uint8) << i
+            pooled.append(pc)
+        rec["n_modes"].append(len(modes)); rec["centers"].append(np.array(modes, np.float32))
+        rec["peak_hist"].append(np.array([0], np.int64))
+        rec["windows"].append(np.array([[float(a), float(b)] for a, b in wins], np.float64).reshape(-1, 2))
+        rec["hist"].append(hist.astype(np.int64)); rec["edges"].append(edges.astype(np.float32))
+        rec["code"].append(code); rec["pooled"].append(pooled)
+    save_g1(rec)
+
+    # ------------------------------------------------------------------ G2
+    g2 = {}
+    for tag, (cin, cout) in {"a": (8, 16), "b": (16, 32)}.items():
+        mod = cm.DSAModule(cin, cout)
+        winit.init_deterministic(mod, prefix=f"g2.{tag}.")
+        for ci, case_idx in enumerate(golden_inputs.G2_CASES):
+            name, d3, r = cases[case_idx]
+            H, W = d3.shape[1:]
+            h, w = (H + 3) // 4, (W + 3) // 4
+            x = golden_inputs.feature(f"g2.{tag}.{ci}", (1, cin, h, w))
+            g = gray(None, torch.from_numpy(d3))
+            with torch.no_grad():
+                y = mod(torch.from_numpy(x), g, r)
+            g2[f"{tag}_{ci}_x"] = x
+            g2[f"{tag}_{ci}_y"] = y.numpy()
+            g2[f"{tag}_{ci}_case"] = np.array(case_idx)
+    np.savez_compressed(OUT / "g2_dsam.npz", **g2)
+
+    # ------------------------------------------------------------------ G3
+    mod = cm.DepthGradientInjectionResidual([4, 8, 16, 32], 3)
+    winit.init_deterministic(mod, prefix="g3.")
+    H, W = 64, 96
+    planes = np.stack([dggm_pre.dggm_planes(synthetic.make_scene(9000 + b, H, W)["depth_u8"])
+                       for b in range(2)])
+    grad, mask = planes[:, 0:3], planes[:, 3:4]
+    cols = [golden_inputs.feature(f"g3.c{i}", (2, c, (H + s - 1) // s, (W + s - 1) // s))
+            for i, (c, s) in enumerate(zip([4, 8, 16, 32], [4, 8, 16, 32]))]
+    with torch.no_grad():
+        outs = mod([torch.from_numpy(c) for c in cols], torch.from_numpy(grad), torch.from_numpy(mask))
+    g3 = {"grad": grad, "mask": mask}
+    for i in range(4):
+        g3[f"color{i}"] = cols[i]
+        g3[f"out{i}"] = outs[i].numpy()
+    np.savez_compressed(OUT / "g3_dggm.npz", **g3)
+
+    # ------------------------------------------------------------------ G4
+    rp = cm.EnhancedDepthImageRatioPredictor(3)
+    winit.init_deterministic(rp, prefix="model.pixel_level_module.ratio_predictor.")
+    rp.eval()
+    pv = golden_inputs.pixel_values(4, 2, 240, 320)
+    feats = {}
+    rp.feature_extractor[3].register_forward_hook(lambda m, i, o: feats.__setitem__("pool4", o))
+    with torch.no_grad():
+        ratio = rp(torch.from_numpy(pv[:, 3:6]))
+    np.savez_compressed(OUT / "g4_ratio.npz", ratio=ratio.numpy(), pool4=feats["pool4"].numpy(),
+                        input_sha=np.array(sha(pv)))
+
+    # ------------------------------------------------------------------ G5 / G6
+    model = build_model(cm)
+    pv = golden_inputs.pixel_values(1, 1, 240, 320)
+    caps = {}
+    plm = model.model.pixel_level_module
+    plm.ratio_predictor.register_forward_hook(lambda m, i, o: caps.__setitem__("ratio", o.detach().clone()))
+    plm.decoder.register_forward_pre_hook(lambda m, a: caps.__setitem__("bb", [t.detach().clone() for t in a[0]]))
+    plm.encoder.register_forward_hook(lambda m, i, o: caps.__setitem__("sw", [t.detach().clone() for t in o.feature_maps]))
+    model.eval()
+    with torch.no_grad():
+        out = model(pixel_values=torch.from_numpy(pv))
+    g5 = {"input_sha": np.array(sha(pv)), "ratio": caps["ratio"].numpy(),
+          "class_logits": out.class_queries_logits.numpy(),
+          "mask_logits": out.masks_queries_logits.numpy()}
+    for k in range(4):
+        for tag, lst in (("bb", caps["bb"]), ("sw", caps["sw"])):
+            t = lst[k].numpy().ravel()
+            idx = golden_inputs.sample_index(f"g5.{tag}{k}", t.size, 4096)
+            g5[f"{tag}{k}_idx"] = idx
+            g5[f"{tag}{k}_val"] = t[idx]
+            g5[f"{tag}{k}_sum"] = np.array(t.astype(np.float64).sum())
+            g5[f"{tag}{k}_abs"] = np.array(np.abs(t.astype(np.float64)).sum())
+    np.savez_compressed(OUT / "g5_model.npz", **g5)
+
+    pv2 = golden_inputs.pixel_values(6, 2, 240, 320)
+    labels = golden_inputs.labels(6, 2, 240, 320)
+    model.zero_grad()
+    out = model(pixel_values=torch.from_numpy(pv2),
+                mask_labels=[torch.from_numpy(m) for m in labels[0]],
+                class_labels=[torch.from_numpy(c) for c in labels[1]])
+    out.loss.backward()
+    g6 = {"input_sha": np.array(sha(pv2)), "loss": np.array(out.loss.item())}
+    names = []
+    for n, p in model.named_parameters():
+        if ".dsam" in n or "depth_gradient_injection" in n:
+            names.append(n)
+            g = p.grad.numpy().ravel()
+            idx = golden_inputs.sample_index("g6." + n, g.size, 1024)
+            g6[n + "|norm"] = np.array(float(np.linalg.norm(g.astype(np.float64))))
+            g6[n + "|sum"] = np.array(float(g.astype(np.float64).sum()))
+            g6[n + "|idx"] = idx
+            g6[n + "|val"] = g[idx]
+        elif ("ratio_predictor" in n or "pixel_level_module.encoder." in n) and p.grad is not None:
+            raise AssertionError(f"unexpected grad on {n} (Q1/Q2)")
+    g6["names"] = np.array(names)
+    np.savez_compressed(OUT / "g6_grads.npz", **g6)
+    print("golden fixtures written to", OUT)
+
+
+def build_model(cm):
+    from transformers import Mask2FormerConfig  # noqa: F401
+    cfg = cm.CustomConfig.from_pretrained(f"{REF}/mask2former/checkpoints/standard",
+                                          **golden_inputs.label_kwargs())
+    model = cm.CustomMask2FormerForUniversalSegmentation(cfg, version="0.4.0")
+    winit.init_deterministic(model)
+    return model
+
+
+def save_g1(rec):
+    out = {"names": np.array(rec["names"]), "shapes": np.array(rec["shapes"]),
+           "ratios": np.array(rec["ratios"], np.float64), "input_sha": np.array(rec["input_sha"]),
+           "grey_sha": np.array(rec["grey_sha"]), "error": np.array(rec["error"])}
+    for i in range(len(rec["names"])):
+        if rec["error"][i]:
+            continue
+        out[f"{i}_n_modes"] = np.array(rec["n_modes"][i])
+        out[f"{i}_centers"] = rec["centers"][i]
+        out[f"{i}_windows"] = rec["windows"][i]
+        out[f"{i}_hist"] = rec["hist"][i]
+        out[f"{i}_edges"] = rec["edges"][i]
+        out[f"{i}_code"] = rec["code"][i]
+        for s, pc in enumerate(rec["pooled"][i]):
+            out[f"{i}_pooled{s}"] = pc
+    np.savez_compressed(OUT / "g1_decompose.npz", **out)
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    import golden_inputs  # noqa: E402
+    main()
