@@ -1,0 +1,145 @@
+/*
+ * rgbd_hip.h — C ABI of librgbd_hip.so, the MI355X (gfx950) kernels of the RGB-D
+ * DGGM + E-DSAM hot path (reference: TheoBald200814/RGB-D-Instance-Segmentation,
+ * mask2former/utils/custom_model.py v0.4.0 and data_process.py).
+ *
+ * Conventions (SURVEY.md §8(b) "What the C-ABI replacement must export"):
+ *   - every pointer is a DEVICE pointer unless the name ends in _host;
+ *   - no entry point allocates: callers pass a workspace sized by the matching
+ *     *_workspace_size() query (bytes, 256-aligned internally);
+ *   - all work is enqueued on `stream` (a hipStream_t passed as void*), nothing
+ *     synchronises, so every entry point is hipGraph-capturable;
+ *   - return 0 on success, a positive hipError_t on a launch/runtime error, or a
+ *     negative RGBD_E* code on a bad argument (checked on the host before any launch).
+ *   - dtype: RGBD_F32 (exact-f32 MFMA, the parity mode) or RGBD_BF16 (bf16 MFMA with
+ *     f32 accumulation).  Depth planes, DGGM planes, ratios and every discrete
+ *     decision are always float32 (SURVEY §7 hard part (i)).
+ * Layouts: NCHW = [B][C][H][W]; NHWC = [B][H][W][C]; both dense.
+ */
+#ifndef RGBD_HIP_H
+#define RGBD_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RGBD_OK 0
+#define RGBD_E_ARG (-1)      /* null pointer / non-positive size */
+#define RGBD_E_SHAPE (-2)    /* shape combination the kernel does not support */
+#define RGBD_E_DTYPE (-3)
+
+#define RGBD_F32 0
+#define RGBD_BF16 1
+
+#define RGBD_NBINS 512
+#define RGBD_MAX_MODES 3
+
+/* Per-image result of the E-DSAM depth decomposition (device memory, one per image).
+ * status: 0 ok; 1 histogram range not finite (all-NaN / inf depth: numpy raises
+ * "supplied range ... is not finite"); 2 "Too many bins for data range" (numpy
+ * ValueError).  Reference: custom_model.py:701-798. */
+typedef struct rgbd_decomp_info {
+  int32_t status;
+  int32_t n_modes;            /* 0..3 selected depth modes (custom_model.py:720-752)   */
+  int32_t n_masks;            /* len(region_masks): n_modes+1, or 4 when no mode      */
+  int32_t peak_bin[RGBD_MAX_MODES];
+  float first_edge, last_edge;/* histogram range after numpy's +-0.5 expansion        */
+  float center[RGBD_MAX_MODES];
+  float lo[RGBD_MAX_MODES], hi[RGBD_MAX_MODES];  /* interval windows (:754-772)      */
+  int32_t hist[RGBD_NBINS];   /* np.histogram counts (:714-718)                      */
+} rgbd_decomp_info;
+
+const char* rgbd_version(void);
+
+/* ---------------------------------------------------------------- K1 DGGM-pre
+ * Replaces calculate_gradient_features (data_process.py:1247-1305) as called by
+ * map_10channel_case2 (dataloader.py:414-421), fused with the 10-channel assembly:
+ *   pv[b,0:3]  = (rgb/255 - mean)/std          (image-processor rescale+normalise)
+ *   pv[b,3:6]  = (depth/255 - mean)/std        (depth as RGB, :389-410)
+ *   pv[b,6:9]  = normalised Sobel magnitude x3 (:415-417)
+ *   pv[b,9]    = valid-gradient mask           (:420)
+ * rgb_u8: [B][H][W][3] (may be NULL: channels 0:3 untouched); depth_u8: [B][H][W];
+ * pv: float32 [B][10][H][W].  Bit-exact to the oracle (IEEE sqrt/div, no FMA). */
+size_t rgbd_assemble_workspace_size(int B);
+int rgbd_assemble_pixel_values(const uint8_t* rgb_u8, const uint8_t* depth_u8, int B, int H, int W,
+                               float* pv, void* ws, void* stream);
+
+/* ---------------------------------------------------------------- K3 E-DSAM decomposition
+ * Replaces, per image and ONCE for all three DSAMs, DSAModule.forward lines 661-687:
+ * to_grayscale (custom_model.py:466-480) -> nanmin/nanmax -> np.histogram(512) ->
+ * find_peaks(prominence=0.01*max) -> top-3 modes -> windows(ratio) -> region masks ->
+ * adaptive_max_pool2d to each DSAM input resolution.
+ * depth3: float32 NCHW planes, image b channel c at depth3 + b*batch_stride + c*H*W;
+ * depth_channels 3 = ImageNet-normalised depth-as-RGB (grey computed, the v0.4.0 call
+ * site :339-350), 1 = an already-grey map (DSAModule.forward called directly).
+ * ratio: float32 [B] (device; the predicted window-size ratio, never synced to host).
+ * codes[s]: uint8 [B][out_h[s]][out_w[s]], bit i = pooled region mask i (conv_layers[i]).
+ * info: rgbd_decomp_info [B]. */
+size_t rgbd_edsam_decompose_workspace_size(int B);
+int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
+                         const float* ratio, int n_scales, const int* out_h_host,
+                         const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
+                         void* ws, void* stream);
+
+/* ---------------------------------------------------------------- K2 DGGM gated fusion
+ * Replaces DepthGradientInjectionResidual.forward (custom_model.py:1204-1269) for one
+ * scale, fused with the final sum (custom_model.py:355):
+ *   out = cp1 + (color + ReLU(W . (bilinear(grad) * nearest(mask)) + b))
+ * cp1/color/out: dtype NCHW [B][C][h][w] (cp1 may equal color; cp1 NULL gives the bare
+ * module output color + ReLU(...)); grad: float32 planes
+ * (3 channels) and mask (1 channel) at grad/mask + b*pv_batch_stride + c*H*W;
+ * weight float32 [C][3]; bias float32 [C]. */
+int rgbd_dggm_fuse_fwd(int dtype, const void* cp1, const void* color, const float* grad,
+                       const float* mask, long long pv_batch_stride, int B, int H, int W, int C,
+                       int h, int w, const float* weight, const float* bias, void* out,
+                       void* stream);
+/* Backward of the gated branch: dW[C][3] and db[C] (float32, OVERWRITTEN) from the
+ * upstream gradient dout (dtype NCHW).  The residual paths are identity. */
+size_t rgbd_dggm_fuse_bwd_workspace_size(int B, int C, int h, int w);
+int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const float* mask,
+                       long long pv_batch_stride, int B, int H, int W, int C, int h, int w,
+                       const float* weight, const float* bias, float* dweight, float* dbias,
+                       void* ws, void* stream);
+
+/* ---------------------------------------------------------------- layout helpers */
+int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H, int W,
+                      void* stream);
+/* Packs DSAModule weights (conv_layers[0..3].weight, rgb_projection.weight; float32
+ * [4][Cout][Cin][3][3] and [Cout][Cin][3][3]) into the implicit-GEMM B operands:
+ *   wfwd [Cout][5][9][Cin]  (forward: k = (seg, tap, ci))
+ *   wbwd [Cin][5][9][Cout]  (dX: k = (seg, tap, co), taps NOT flipped; see csrc)   */
+int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, int Cin,
+                           int Cout, void* wfwd, void* wbwd, void* stream);
+
+/* ---------------------------------------------------------------- K5 DSAM masked conv
+ * Forward of one DSAModule for the whole batch (replaces the per-sample Python loop of
+ * custom_model.py:339-352 and DSAModule.forward :682-699):
+ *   out = residual + sum_{i<4} Conv3x3s2_i(x * m_i) + sum_{i<n_masks[b]} b_i + Proj3x3s2(x)
+ * x_nhwc: dtype [B][h][w][Cin]; code: uint8 [B][h][w] (pooled region codes at x's
+ * resolution); bias float32 [4][Cout]; residual/out_nchw: dtype [B][Cout][ho][wo];
+ * out_nhwc (optional, may be NULL): dtype [B][ho][wo][Cout]. */
+int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                  int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
+                  const void* residual, void* out_nchw, void* out_nhwc, void* stream);
+/* dX of one DSAModule, plus the upstream gradient of its input's other consumer:
+ *   dx = gin + sum_i m_i * ConvT_i(gout) + ConvT_proj(gout)
+ * gout_nhwc: dtype [B][ho][wo][Cout]; gin_nchw: dtype [B][Cin][h][w];
+ * dx_nchw (dtype [B][Cin][h][w]) and dx_nhwc (optional) are written. */
+int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
+                       int w, int Cout, const void* wbwd, const void* gin_nchw, void* dx_nchw,
+                       void* dx_nhwc, void* stream);
+/* dW / db of one DSAModule: dconv_w float32 [4][Cout][Cin][3][3], dproj_w float32
+ * [Cout][Cin][3][3], dbias float32 [4][Cout] (all OVERWRITTEN).  gout_nchw: dtype
+ * [B][Cout][ho][wo]; x_nhwc as in the forward. */
+size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout);
+int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, const uint8_t* code,
+                         const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
+                         float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RGBD_HIP_H */

@@ -181,6 +181,10 @@ def region_code(masks) -> np.ndarray:
 
 def pooled_codes(code: np.ndarray, oh: int, ow: int) -> np.ndarray:
     """OR-pool of the packed region code == per-mask adaptive max pool, packed."""
+    H, W = code.shape
+    if H % oh == 0 and W % ow == 0:  # exact bins: same result, vectorised
+        blocks = code.reshape(oh, H // oh, ow, W // ow)
+        return np.bitwise_or.reduce(np.bitwise_or.reduce(blocks, axis=3), axis=1).astype(np.uint8)
     out = np.zeros((oh, ow), dtype=np.uint8)
     for bit in range(4):
         out |= adaptive_max_pool_bool(((code >> bit) & 1).astype(bool), oh, ow).astype(np.uint8) << bit

@@ -1,0 +1,84 @@
+"""ctypes binding of librgbd_hip.so (the C ABI declared in include/rgbd_hip.h).
+
+There is no fallback: if the library is missing or fails to load, every op raises.
+``import torch`` happens first so that torch's HIP runtime (soname libamdhip64.so.7) is the
+one the library binds to — one HIP runtime per process.
+"""
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "librgbd_hip.so"
+
+RGBD_F32 = 0
+RGBD_BF16 = 1
+NBINS = 512
+
+# rgbd_decomp_info (include/rgbd_hip.h) as a numpy structured dtype: 2116 bytes, no padding
+DECOMP_INFO_DTYPE = np.dtype([
+    ("status", "<i4"), ("n_modes", "<i4"), ("n_masks", "<i4"), ("peak_bin", "<i4", 3),
+    ("first_edge", "<f4"), ("last_edge", "<f4"), ("center", "<f4", 3),
+    ("lo", "<f4", 3), ("hi", "<f4", 3), ("hist", "<i4", NBINS)])
+assert DECOMP_INFO_DTYPE.itemsize == 2116
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_LL = ctypes.c_longlong
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must list every symbol the header declares
+SIGNATURES = {
+    "rgbd_version": (ctypes.c_char_p, []),
+    "rgbd_assemble_workspace_size": (_SZ, [_I]),
+    "rgbd_assemble_pixel_values": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
+    "rgbd_edsam_decompose_workspace_size": (_SZ, [_I]),
+    "rgbd_edsam_decompose": (_I, [_P, _LL, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "rgbd_dggm_fuse_fwd": (_I, [_I, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "rgbd_dggm_fuse_bwd_workspace_size": (_SZ, [_I, _I, _I, _I]),
+    "rgbd_dggm_fuse_bwd": (_I, [_I, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "rgbd_nchw_to_nhwc": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
+    "rgbd_dsam_pack_weights": (_I, [_I, _P, _P, _I, _I, _P, _P, _P]),
+    "rgbd_dsam_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "rgbd_dsam_bwd_data": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "rgbd_dsam_bwd_weight_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
+    "rgbd_dsam_bwd_weight": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+class RgbdHipError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the CDLL with argtypes set.  Raises if unavailable."""
+    global _lib
+    if _lib is None:
+        import torch  # noqa: F401  (bind to torch's HIP runtime)
+        if not LIB_PATH.exists():
+            raise RgbdHipError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback for the rgbd_amd kernels)")
+        h = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        kind = {-1: "bad argument", -2: "unsupported shape", -3: "unsupported dtype"}.get(rc, "HIP error")
+        raise RgbdHipError(f"{what} failed: {kind} (code {rc})")
+
+
+def header_symbols():
+    """Function names declared in include/rgbd_hip.h (parsed, for the export test)."""
+    import re
+    hdr = Path(__file__).resolve().parents[1] / "include" / "rgbd_hip.h"
+    txt = hdr.read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(rgbd_\w+)\s*\(", txt, flags=re.M)))

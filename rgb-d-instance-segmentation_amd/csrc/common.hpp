@@ -1,0 +1,68 @@
+// Shared helpers for the gfx950 kernels of librgbd_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "../../include/rgbd_hip.h"
+
+#define RGBD_CHECK_LAUNCH()                                  \
+  do {                                                       \
+    hipError_t e__ = hipGetLastError();                      \
+    if (e__ != hipSuccess) return (int)e__;                  \
+  } while (0)
+
+#define RGBD_REQUIRE(cond, code) \
+  do {                           \
+    if (!(cond)) return (code);  \
+  } while (0)
+
+namespace rgbd {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+
+typedef uint16_t bf16_t;  // raw bfloat16 storage (same bits as torch.bfloat16)
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);  // round-to-nearest-even, NaN-preserving
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+template <typename T> struct Num;
+template <> struct Num<float> {
+  static __device__ __forceinline__ float load(const float* p) { return *p; }
+  static __device__ __forceinline__ float to_f(float v) { return v; }
+  static __device__ __forceinline__ float from_f(float v) { return v; }
+};
+template <> struct Num<bf16_t> {
+  static __device__ __forceinline__ float to_f(bf16_t v) { return bf16_to_f32(v); }
+  static __device__ __forceinline__ bf16_t from_f(float v) { return f32_to_bf16(v); }
+};
+
+// Order-preserving float <-> uint32 key (for atomicMin/atomicMax on floats of any sign).
+__device__ __forceinline__ uint32_t f32_key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_f32(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace rgbd

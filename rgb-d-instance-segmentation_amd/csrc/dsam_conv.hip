@@ -1,0 +1,488 @@
+// K5: DSAM masked 3x3/stride-2 convolutions as MFMA implicit GEMMs (gfx950).
+//
+// Reference: DSAModule.forward (mask2former/utils/custom_model.py:682-699) evaluates, per
+// sample, four Conv3x3s2 on rgb_features * pooled_mask_i plus a bias-free projection conv,
+// i.e. five convolutions at batch 1 (and the Python loop of :339-352 repeats it per sample).
+// Here one launch covers the whole batch and all five convolutions:
+//
+//   out[m, n] = sum_{seg<5} sum_{tap<9} sum_{c<Cin} Wseg[n, c, tap] * x[src(m, tap), c] * bit_seg
+//
+// with K = 5*9*Cin ordered (seg, tap, c): the A operand (im2col of the NHWC input) is loaded
+// once per (tap, 32-channel chunk) and re-used by all five segments; segment `seg` < 4 keeps
+// an element only where bit `seg` of the pooled region code of its SOURCE pixel is set
+// (x * mask, :689).  A segment whose bit is absent from every pixel of a wave's 32 rows is
+// skipped (its contribution is exactly zero), which removes most masked FLOPs on real scenes.
+//
+// dX (training) is the transposed convolution with the same packed structure: output pixels
+// are split into the four stride-2 parity classes so only live taps are visited, and the
+// mask bit is taken at the OUTPUT pixel (d(x*m)/dx = m).  dW contracts over pixels with an
+// LDS-staged im2col tile.
+#include "mfma.hpp"
+
+using namespace rgbd;
+
+namespace {
+
+enum { MASK_NONE = 0, MASK_SRC = 1, MASK_DST = 2 };
+
+struct ConvArgs {
+  const void* x;          // NHWC [B][Hi][Wi][C]
+  const uint8_t* code;    // region codes: [B][Hi][Wi] (MASK_SRC) or [B][Ho][Wo] (MASK_DST)
+  const void* w;          // packed B operand [N][nseg * KH*KW * C]
+  int B, Hi, Wi, C;
+  int Ho, Wo, N;
+  int KH, KW, stride, pad;
+  int nseg, mask_mode, transposed;
+  const float* bias4;               // DSAM conv biases [4][N] (summed over i < n_masks[b])
+  const rgbd_decomp_info* info;
+  const void* residual;             // NCHW [B][N][Ho][Wo] added in the epilogue (optional)
+  void* out_nchw;                   // optional
+  void* out_nhwc;                   // optional
+};
+
+constexpr int BM = 64, BN = 64;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  int py = 0, px = 0, Hc = a.Ho, Wc = a.Wo;
+  if (a.transposed) {
+    py = blockIdx.z >> 1;
+    px = blockIdx.z & 1;
+    Hc = (a.Ho - py + 1) >> 1;
+    Wc = (a.Wo - px + 1) >> 1;
+  }
+  const long long HWc = (long long)Hc * Wc;
+  const long long Mtot = (long long)a.B * HWc;
+  const long long mbase = (long long)blockIdx.x * BM + wm * 32;
+  const int nbase = blockIdx.y * BN + wn * 32;
+  if (mbase >= Mtot) return;  // wave-uniform
+
+  int rb[2], roy[2], rox[2];
+  bool rvalid[2];
+  uint32_t rcode[2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const long long m = mbase + 16 * mi + r;
+    rvalid[mi] = m < Mtot;
+    const long long mm = rvalid[mi] ? m : 0;
+    rb[mi] = (int)(mm / HWc);
+    const int rem = (int)(mm % HWc);
+    const int i = rem / Wc, j = rem % Wc;
+    roy[mi] = a.transposed ? 2 * i + py : i;
+    rox[mi] = a.transposed ? 2 * j + px : j;
+    rcode[mi] = (a.mask_mode == MASK_DST && rvalid[mi])
+                    ? a.code[((long long)rb[mi] * a.Ho + roy[mi]) * a.Wo + rox[mi]]
+                    : 0xffu;
+  }
+  const int ntap = a.KH * a.KW;
+  const long long ktot = (long long)a.nseg * ntap * a.C;
+  const T* wp = (const T*)a.w;
+  const T* xp = (const T*)a.x;
+  bool nvalid[2];
+  const T* wrow[2];
+#pragma unroll
+  for (int nj = 0; nj < 2; ++nj) {
+    const int n = nbase + 16 * nj + r;
+    nvalid[nj] = n < a.N;
+    wrow[nj] = wp + (long long)(nvalid[nj] ? n : 0) * ktot + 8 * g;
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int ky = 0; ky < a.KH; ++ky) {
+    if (a.transposed && ((py + a.pad - ky) & 1)) continue;
+    for (int kx = 0; kx < a.KW; ++kx) {
+      if (a.transposed && ((px + a.pad - kx) & 1)) continue;
+      const int tap = ky * a.KW + kx;
+      const T* src[2];
+      bool inb[2];
+      uint32_t scode[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        int iy, ix;
+        if (a.transposed) {
+          iy = (roy[mi] + a.pad - ky) >> 1;
+          ix = (rox[mi] + a.pad - kx) >> 1;
+        } else {
+          iy = roy[mi] * a.stride - a.pad + ky;
+          ix = rox[mi] * a.stride - a.pad + kx;
+        }
+        inb[mi] = rvalid[mi] && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+        const long long pix = inb[mi] ? ((long long)rb[mi] * a.Hi + iy) * a.Wi + ix : 0;
+        src[mi] = xp + pix * a.C + 8 * g;
+        scode[mi] = (a.mask_mode == MASK_SRC) ? (inb[mi] ? a.code[pix] : 0u) : rcode[mi];
+      }
+      for (int c0 = 0; c0 < a.C; c0 += 32) {
+        const bool cok = c0 + 8 * g < a.C;  // C % 8 == 0: a lane's 8-chunk is all in or all out
+        Frag<T> A[2];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          if (inb[mi] && cok)
+            A[mi].load(src[mi] + c0);
+          else
+            A[mi].zero();
+        }
+        for (int seg = 0; seg < a.nseg; ++seg) {
+          bool keep[2] = {true, true};
+          if (a.mask_mode != MASK_NONE && seg < 4) {
+            keep[0] = (scode[0] >> seg) & 1u;
+            keep[1] = (scode[1] >> seg) & 1u;
+            if (!__any(keep[0] || keep[1])) continue;  // all-zero segment for this wave
+          }
+          Frag<T> As[2] = {A[0], A[1]};
+          As[0].select(keep[0]);
+          As[1].select(keep[1]);
+          const long long koff = ((long long)seg * ntap + tap) * a.C + c0;
+#pragma unroll
+          for (int nj = 0; nj < 2; ++nj) {
+            Frag<T> Bf;
+            if (nvalid[nj] && cok)
+              Bf.load(wrow[nj] + koff);
+            else
+              Bf.zero();
+            mma(acc[0][nj], As[0], Bf);
+            mma(acc[1][nj], As[1], Bf);
+          }
+        }
+      }
+    }
+  }
+
+  // epilogue: D[m = row][n = col], row = 4g + reg, col = r
+  const T* res = (const T*)a.residual;
+  T* onchw = (T*)a.out_nchw;
+  T* onhwc = (T*)a.out_nhwc;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const long long m = mbase + 16 * mi + 4 * g + reg;
+      if (m >= Mtot) continue;
+      const int b = (int)(m / HWc);
+      const int rem = (int)(m % HWc);
+      const int i = rem / Wc, j = rem % Wc;
+      const int oy = a.transposed ? 2 * i + py : i;
+      const int ox = a.transposed ? 2 * j + px : j;
+      int nmask = 0;
+      if (a.info) nmask = a.info[b].n_masks;
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj) {
+        const int n = nbase + 16 * nj + r;
+        if (n >= a.N) continue;
+        float v = acc[mi][nj][reg];
+        if (a.bias4) {
+          float bs = 0.f;
+          for (int s = 0; s < nmask; ++s) bs += a.bias4[s * a.N + n];
+          v += bs;
+        }
+        const long long o_nchw = (((long long)b * a.N + n) * a.Ho + oy) * a.Wo + ox;
+        if (res) v = Num<T>::to_f(res[o_nchw]) + v;
+        const T tv = Num<T>::from_f(v);
+        if (onchw) onchw[o_nchw] = tv;
+        if (onhwc) onhwc[(((long long)b * a.Ho + oy) * a.Wo + ox) * a.N + n] = tv;
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void k_pack_dsam(const float* __restrict__ conv_w, const float* __restrict__ proj_w, int Cin,
+                            int Cout, T* __restrict__ wfwd, T* __restrict__ wbwd) {
+  // element (seg, o, c, tap) of W_seg
+  const long long total = 5ll * Cout * Cin * 9;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int tap = (int)(e % 9);
+    const int c = (int)((e / 9) % Cin);
+    const int o = (int)((e / (9ll * Cin)) % Cout);
+    const int seg = (int)(e / (9ll * Cin * Cout));
+    const float v = seg < 4 ? conv_w[(((long long)seg * Cout + o) * Cin + c) * 9 + tap]
+                            : proj_w[((long long)o * Cin + c) * 9 + tap];
+    const T tv = Num<T>::from_f(v);
+    if (wfwd) wfwd[(long long)o * 45 * Cin + ((long long)seg * 9 + tap) * Cin + c] = tv;
+    if (wbwd) wbwd[(long long)c * 45 * Cout + ((long long)seg * 9 + tap) * Cout + o] = tv;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_nchw_to_nhwc(const T* __restrict__ src, T* __restrict__ dst, int C,
+                                                      int HW) {
+  __shared__ T tile[32][33];
+  const int b = blockIdx.z;
+  const int p0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, p = p0 + tx;
+    if (c < C && p < HW) tile[k][tx] = src[((long long)b * C + c) * HW + p];
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int p = p0 + k, c = c0 + tx;
+    if (c < C && p < HW) dst[((long long)b * HW + p) * C + c] = tile[tx][k];
+  }
+}
+
+// ----------------------------------------------------------------------- dW
+// D[o][kk] = sum_m G[m][o] * X[m][kk],  kk = (seg*9 + tap)*Cin + c,  per split z (images).
+template <typename T>
+__global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, const T* __restrict__ x,
+                                                    const uint8_t* __restrict__ code, int B, int Cin,
+                                                    int h, int w, int Cout, int splits,
+                                                    float* __restrict__ partial) {
+  __shared__ T Gs[64][32 + 8];   // [o][px]
+  __shared__ T Xs[32][64 + 8];   // [px][kk]
+  const int ho = (h + 1) / 2, wo = (w + 1) / 2;  // 3x3 s2 p1
+  const int hwo = ho * wo;
+  const int KK = 45 * Cin;
+  const int kk0 = blockIdx.x * 64, o0 = blockIdx.y * 64, z = blockIdx.z;
+  const int b0 = (int)((long long)z * B / splits), b1 = (int)((long long)(z + 1) * B / splits);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // staging roles
+  const int go = threadIdx.x >> 2, gp = (threadIdx.x & 3) * 8;     // G: o row, 8 px
+  const int xpx = threadIdx.x >> 3, xk = (threadIdx.x & 7) * 8;     // X: px row, 8 kk
+  const int kk = kk0 + xk;
+  const bool kk_ok = kk < KK;
+  const int seg = kk_ok ? kk / (9 * Cin) : 0;
+  const int tap = kk_ok ? (kk / Cin) % 9 : 0;
+  const int cc = kk_ok ? kk % Cin : 0;
+  const int ky = tap / 3, kx = tap % 3;
+  for (int b = b0; b < b1; ++b) {
+    for (int p0 = 0; p0 < hwo; p0 += 32) {
+      __syncthreads();
+      {  // stage G^T tile
+        const int o = o0 + go;
+        for (int j = 0; j < 8; ++j) {
+          const int p = p0 + gp + j;
+          Gs[go][gp + j] = (o < Cout && p < hwo) ? gout[((long long)b * Cout + o) * hwo + p] : (T)0;
+        }
+      }
+      {  // stage im2col tile
+        const int p = p0 + xpx;
+        bool ok = kk_ok && p < hwo;
+        int iy = 0, ix = 0;
+        if (ok) {
+          iy = 2 * (p / wo) - 1 + ky;
+          ix = 2 * (p % wo) - 1 + kx;
+          ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+        }
+        const long long pix = ((long long)b * h + iy) * w + ix;
+        if (ok && seg < 4) ok = (code[pix] >> seg) & 1u;
+        for (int j = 0; j < 8; ++j) Xs[xpx][xk + j] = ok ? x[pix * Cin + cc + j] : (T)0;
+      }
+      __syncthreads();
+      Frag<T> Af[2], Bf[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int o = wm * 32 + 16 * mi + r;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Af[mi].set(j, Num<T>::to_f(Gs[o][8 * g + j]));
+      }
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj) {
+        const int c = wn * 32 + 16 * nj + r;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Bf[nj].set(j, Num<T>::to_f(Xs[8 * g + j][c]));
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) mma(acc[mi][nj], Af[mi], Bf[nj]);
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int o = o0 + wm * 32 + 16 * mi + 4 * g + reg;
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj) {
+        const int c = kk0 + wn * 32 + 16 * nj + r;
+        if (o < Cout && c < KK) partial[((long long)z * Cout + o) * KK + c] = acc[mi][nj][reg];
+      }
+    }
+}
+
+__global__ void k_dsam_wgrad_final(const float* __restrict__ partial, int splits, int Cin, int Cout,
+                                   float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
+  const long long KK = 45ll * Cin;
+  const long long total = (long long)Cout * KK;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += partial[(long long)z * total + e];  // fixed order
+    const int o = (int)(e / KK);
+    const int kk = (int)(e % KK);
+    const int seg = kk / (9 * Cin), tap = (kk / Cin) % 9, c = kk % Cin;
+    if (seg < 4)
+      dconv_w[(((long long)seg * Cout + o) * Cin + c) * 9 + tap] = s;
+    else
+      dproj_w[((long long)o * Cin + c) * 9 + tap] = s;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_chan_sum(const T* __restrict__ g, int HW, float* __restrict__ out) {
+  // out[b*C + c] = sum_p g[b][c][p]   (one block per (b, c))
+  __shared__ float red[4];
+  const long long base = (long long)blockIdx.x * HW;
+  float s = 0.f;
+  for (int p = threadIdx.x; p < HW; p += 256) s += Num<T>::to_f(g[base + p]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_decomp_info* info, int B,
+                                 int Cout, float* __restrict__ dbias) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // (i, o)
+  if (t >= 4 * Cout) return;
+  const int i = t / Cout, o = t % Cout;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b)
+    if (i < info[b].n_masks) s += csum[b * Cout + o];  // conv_layers[i] used only if i < len(masks)
+  dbias[t] = s;
+}
+
+template <typename T>
+int launch_conv(const ConvArgs& a, hipStream_t s) {
+  int nclass = a.transposed ? 4 : 1;
+  long long Mmax = (long long)a.B * a.Ho * a.Wo;
+  if (a.transposed) Mmax = (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2);
+  dim3 grid(ceil_div(Mmax, BM), ceil_div(a.N, BN), nclass);
+  k_conv_igemm<T><<<grid, 256, 0, s>>>(a);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int dsam_wgrad_splits(int B, int Cin, int Cout) {
+  const long long tiles = (long long)ceil_div(45ll * Cin, 64) * ceil_div(Cout, 64);
+  int sp = (int)std::min<long long>(B, std::max<long long>(1, ceil_div(1024, tiles)));
+  return sp < 1 ? 1 : sp;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rgbd_version(void) { return "rgbd_hip 0.1.0 (gfx950)"; }
+
+int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H, int W, void* stream) {
+  RGBD_REQUIRE(src && dst && B > 0 && C > 0 && H > 0 && W > 0, RGBD_E_ARG);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(ceil_div((long long)H * W, 32), ceil_div(C, 32), B);
+  if (dtype == RGBD_F32)
+    k_nchw_to_nhwc<float><<<grid, 256, 0, s>>>((const float*)src, (float*)dst, C, H * W);
+  else if (dtype == RGBD_BF16)
+    k_nchw_to_nhwc<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)src, (bf16_t*)dst, C, H * W);
+  else
+    return RGBD_E_DTYPE;
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, int Cin, int Cout,
+                           void* wfwd, void* wbwd, void* stream) {
+  RGBD_REQUIRE(conv_w && proj_w && (wfwd || wbwd) && Cin > 0 && Cout > 0, RGBD_E_ARG);
+  hipStream_t s = (hipStream_t)stream;
+  const long long total = 45ll * Cin * Cout;
+  const int nb = (int)std::min<long long>(ceil_div(total, 256), 4096);
+  if (dtype == RGBD_F32)
+    k_pack_dsam<float><<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (float*)wfwd, (float*)wbwd);
+  else if (dtype == RGBD_BF16)
+    k_pack_dsam<bf16_t><<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (bf16_t*)wfwd, (bf16_t*)wbwd);
+  else
+    return RGBD_E_DTYPE;
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                  int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
+                  const void* residual, void* out_nchw, void* out_nhwc, void* stream) {
+  RGBD_REQUIRE(x_nhwc && code && info && wfwd && bias && (out_nchw || out_nhwc), RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
+  ConvArgs a = {};
+  a.x = x_nhwc; a.code = code; a.w = wfwd;
+  a.B = B; a.Hi = h; a.Wi = w; a.C = Cin;
+  a.Ho = (h + 1) / 2; a.Wo = (w + 1) / 2; a.N = Cout;
+  a.KH = 3; a.KW = 3; a.stride = 2; a.pad = 1;
+  a.nseg = 5; a.mask_mode = MASK_SRC; a.transposed = 0;
+  a.bias4 = bias; a.info = info; a.residual = residual; a.out_nchw = out_nchw; a.out_nhwc = out_nhwc;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_F32) return launch_conv<float>(a, s);
+  if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);
+  return RGBD_E_DTYPE;
+}
+
+int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
+                       int w, int Cout, const void* wbwd, const void* gin_nchw, void* dx_nchw,
+                       void* dx_nhwc, void* stream) {
+  RGBD_REQUIRE(gout_nhwc && code && wbwd && (dx_nchw || dx_nhwc), RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(Cout % 8 == 0, RGBD_E_SHAPE);
+  ConvArgs a = {};
+  a.x = gout_nhwc; a.code = code; a.w = wbwd;
+  a.B = B; a.Hi = (h + 1) / 2; a.Wi = (w + 1) / 2; a.C = Cout;
+  a.Ho = h; a.Wo = w; a.N = Cin;
+  a.KH = 3; a.KW = 3; a.stride = 2; a.pad = 1;
+  a.nseg = 5; a.mask_mode = MASK_DST; a.transposed = 1;
+  a.residual = gin_nchw; a.out_nchw = dx_nchw; a.out_nhwc = dx_nhwc;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_F32) return launch_conv<float>(a, s);
+  if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);
+  return RGBD_E_DTYPE;
+}
+
+size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout) {
+  (void)dtype; (void)h; (void)w;
+  const int sp = dsam_wgrad_splits(B, Cin, Cout);
+  return align256(sizeof(float) * (size_t)sp * Cout * 45 * Cin) + align256(sizeof(float) * (size_t)B * Cout);
+}
+
+int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, const uint8_t* code,
+                         const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
+                         float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream) {
+  RGBD_REQUIRE(gout_nchw && x_nhwc && code && info && dconv_w && dproj_w && dbias && ws, RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
+  hipStream_t s = (hipStream_t)stream;
+  const int sp = dsam_wgrad_splits(B, Cin, Cout);
+  float* partial = (float*)ws;
+  float* csum = (float*)((char*)ws + align256(sizeof(float) * (size_t)sp * Cout * 45 * Cin));
+  dim3 grid(ceil_div(45ll * Cin, 64), ceil_div(Cout, 64), sp);
+  const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
+  if (dtype == RGBD_F32) {
+    k_dsam_wgrad<float><<<grid, 256, 0, s>>>((const float*)gout_nchw, (const float*)x_nhwc, code, B, Cin, h, w,
+                                             Cout, sp, partial);
+    k_chan_sum<float><<<B * Cout, 256, 0, s>>>((const float*)gout_nchw, hwo, csum);
+  } else if (dtype == RGBD_BF16) {
+    k_dsam_wgrad<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)gout_nchw, (const bf16_t*)x_nhwc, code, B, Cin,
+                                              h, w, Cout, sp, partial);
+    k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
+  } else {
+    return RGBD_E_DTYPE;
+  }
+  const long long total = 45ll * Cin * Cout;
+  k_dsam_wgrad_final<<<(int)std::min<long long>(ceil_div(total, 256), 4096), 256, 0, s>>>(
+      partial, sp, Cin, Cout, dconv_w, dproj_w);
+  k_dsam_bias_grad<<<ceil_div(4 * Cout, 256), 256, 0, s>>>(csum, info, B, Cout, dbias);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+}  // extern "C"

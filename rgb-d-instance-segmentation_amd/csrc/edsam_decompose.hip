@@ -1,0 +1,327 @@
+// K3: E-DSAM depth decomposition on device, once per image for all three DSAMs.
+//
+// Reference: DSAModule (mask2former/utils/custom_model.py:622-798), which per sample and per
+// DSAM copies the grey depth to the host, runs np.histogram(512) + scipy find_peaks, builds
+// full-resolution numpy masks and copies them back.  Here the same discrete decisions are
+// made on device in four stream-ordered launches (no host sync):
+//   1. k_grey_minmax : grey = 0.299 d0 + 0.587 d1 + 0.114 d2 (f32, one rounding per op,
+//                      :466-480) and nanmin/nanmax via order-preserving uint atomics (:715)
+//   2. k_hist        : numpy's uniform-bin fast path (index = int((x-first)/(last-first)*512)
+//                      with the +-1 edge corrections), LDS-privatised 512-bin histogram
+//   3. k_peaks       : one 512-thread workgroup per image: plateau-aware local maxima
+//                      (scipy _local_maxima_1d), wave-cooperative prominence search
+//                      (scipy _peak_prominences, wlen = whole signal), threshold
+//                      0.01*max(hist) in float64, top-3 by (count, centre), windows (:754-772)
+//   4. k_codes_pool  : per-pixel 4-bit region code (bit i <-> conv_layers[i], :774-798) OR-pooled
+//                      over the adaptive_max_pool2d bins of each DSAM input resolution (:687)
+// Every float op that feeds a discrete decision uses an explicitly rounded intrinsic, so the
+// result is bit-exact to the numpy 2.2 / scipy 1.15 reference.
+#include "common.hpp"
+
+using namespace rgbd;
+
+namespace {
+
+struct DecWs {
+  uint32_t min_key, max_key;
+};
+
+__device__ __forceinline__ float grey_at(const float* __restrict__ d, long long HW, long long p, int nch) {
+  if (nch == 1) return d[p];  // already grey (DSAModule called with a 1-channel depth map)
+  const float a = __fmul_rn(0.299f, d[p]);
+  const float b = __fmul_rn(0.587f, d[HW + p]);
+  const float c = __fmul_rn(0.114f, d[2 * HW + p]);
+  return __fadd_rn(__fadd_rn(a, b), c);
+}
+
+struct Range {
+  float first, last, step, denom;
+  int status;  // 0 ok, 1 non-finite / empty, 2 too many bins
+};
+
+__device__ __forceinline__ Range make_range(const DecWs& w) {
+  Range r;
+  r.status = 0;
+  if (w.min_key == 0xffffffffu && w.max_key == 0u) {  // every value NaN
+    r.status = 1;
+    r.first = r.last = 0.f;
+  } else {
+    r.first = key_f32(w.min_key);
+    r.last = key_f32(w.max_key);
+  }
+  if (r.status == 0 && (isinf(r.first) || isinf(r.last))) r.status = 1;
+  if (r.status == 0 && r.first == r.last) {  // numpy _get_outer_edges: expand by +-0.5
+    r.first = __fsub_rn(r.first, 0.5f);
+    r.last = __fadd_rn(r.last, 0.5f);
+  }
+  r.denom = __fsub_rn(r.last, r.first);
+  r.step = __fdiv_rn(r.denom, 512.f);  // linspace: (stop - start) / 512
+  if (r.status == 0 && r.step == 0.f) r.status = 2;
+  return r;
+}
+
+// np.linspace(first, last, 513, dtype=f32)[i] = i*step + first, last edge forced to `last`.
+__device__ __forceinline__ float edge_at(const Range& r, int i) {
+  return i == RGBD_NBINS ? r.last : __fadd_rn(__fmul_rn((float)i, r.step), r.first);
+}
+
+__global__ void k_init(DecWs* ws, rgbd_decomp_info* info, int B) {
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  if (threadIdx.x == 0) {
+    ws[b].min_key = 0xffffffffu;
+    ws[b].max_key = 0u;
+  }
+  for (int i = threadIdx.x; i < RGBD_NBINS; i += blockDim.x) info[b].hist[i] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_grey_minmax(const float* __restrict__ depth3, long long bstride,
+                                                     long long HW, int nch, DecWs* ws) {
+  const int b = blockIdx.y;
+  const float* d = depth3 + b * bstride;
+  uint32_t kmin = 0xffffffffu, kmax = 0u;
+  for (long long p = blockIdx.x * 256ll + threadIdx.x; p < HW; p += 256ll * gridDim.x) {
+    const float g = grey_at(d, HW, p, nch);
+    if (!isnan(g)) {  // np.nanmin / np.nanmax
+      const uint32_t k = f32_key(g);
+      kmin = min(kmin, k);
+      kmax = max(kmax, k);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&ws[b].min_key, kmin);
+    atomicMax(&ws[b].max_key, kmax);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_hist(const float* __restrict__ depth3, long long bstride,
+                                              long long HW, int nch, const DecWs* ws, rgbd_decomp_info* info) {
+  __shared__ uint32_t h[RGBD_NBINS];
+  const int b = blockIdx.y;
+  const Range r = make_range(ws[b]);
+  if (r.status != 0) return;  // uniform per block
+  for (int i = threadIdx.x; i < RGBD_NBINS; i += 256) h[i] = 0;
+  __syncthreads();
+  const float* d = depth3 + b * bstride;
+  for (long long p = blockIdx.x * 256ll + threadIdx.x; p < HW; p += 256ll * gridDim.x) {
+    const float g = grey_at(d, HW, p, nch);
+    if (!(g >= r.first && g <= r.last)) continue;  // `keep` mask (drops NaN)
+    const float f = __fmul_rn(__fdiv_rn(__fsub_rn(g, r.first), r.denom), 512.f);
+    int idx = (int)f;
+    if (idx == RGBD_NBINS) idx -= 1;
+    if (g < edge_at(r, idx)) idx -= 1;
+    if (g >= edge_at(r, idx + 1) && idx != RGBD_NBINS - 1) idx += 1;
+    atomicAdd(&h[idx], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < RGBD_NBINS; i += 256)
+    if (h[i]) atomicAdd((uint32_t*)&info[b].hist[i], h[i]);
+}
+
+__device__ __forceinline__ long long wave_max_i64(long long v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const int lo = __shfl_xor((int)(v & 0xffffffff), o);
+    const int hi = __shfl_xor((int)(v >> 32), o);
+    const long long u = ((long long)hi << 32) | (uint32_t)lo;
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(512) void k_peaks(const DecWs* ws, const float* __restrict__ ratio,
+                                               rgbd_decomp_info* info) {
+  __shared__ int x[RGBD_NBINS];
+  __shared__ int peaks[RGBD_NBINS];
+  __shared__ int is_kept[RGBD_NBINS];
+  __shared__ int npeaks, bad;
+  __shared__ long long red[8];
+  __shared__ int sel[RGBD_MAX_MODES];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  rgbd_decomp_info* out = info + b;
+  Range r = make_range(ws[b]);
+  x[t] = out->hist[t];
+  is_kept[t] = 0;
+  if (t == 0) {
+    npeaks = 0;
+    bad = 0;
+  }
+  __syncthreads();
+  // linspace monotonicity check (numpy raises "Too many bins for data range")
+  if (r.status == 0 && !(edge_at(r, t) < edge_at(r, t + 1))) atomicOr(&bad, 1);
+  __syncthreads();
+  if (r.status == 0 && bad) r.status = 2;
+  if (r.status != 0) {
+    if (t == 0) {
+      out->status = r.status;
+      out->n_modes = 0;
+      out->n_masks = RGBD_MAX_MODES + 1;
+      out->first_edge = r.first;
+      out->last_edge = r.last;
+    }
+    return;
+  }
+  // --- local maxima (scipy _local_maxima_1d): plateau starts are x[i-1] < x[i]
+  if (t >= 1 && t < RGBD_NBINS - 1 && x[t - 1] < x[t]) {
+    int j = t + 1;
+    while (j < RGBD_NBINS - 1 && x[j] == x[t]) ++j;
+    if (x[j] < x[t]) peaks[atomicAdd(&npeaks, 1)] = (t + j - 1) >> 1;
+  }
+  // --- max(hist)
+  long long mv = wave_max_i64((long long)x[t]);
+  if (lane == 0) red[wave] = mv;
+  __syncthreads();
+  long long hmax = red[0];
+  for (int i = 1; i < 8; ++i) hmax = red[i] > hmax ? red[i] : hmax;
+  const double pmin = 0.01 * (double)hmax;  // prominence threshold, float64 (:738)
+  const int np_ = npeaks;
+  // --- prominences, one wave per peak (scipy _peak_prominences, wlen=-1)
+  for (int k = wave; k < np_; k += 8) {
+    const int p = peaks[k];
+    const int v = x[p];
+    int lmin = v;
+    for (int base = p - 1; base >= 0; base -= 64) {
+      const int idx = base - lane;
+      const bool in = idx >= 0;
+      const int xv = in ? x[idx] : 0;
+      const unsigned long long hm = __ballot(in && xv > v);
+      const int stop = hm ? __ffsll((long long)hm) - 1 : 64;  // first higher bin (closest to p)
+      int cand = (in && lane < stop) ? xv : v;
+      for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o));
+      lmin = min(lmin, cand);
+      if (hm) break;
+    }
+    int rmin = v;
+    for (int base = p + 1; base < RGBD_NBINS; base += 64) {
+      const int idx = base + lane;
+      const bool in = idx < RGBD_NBINS;
+      const int xv = in ? x[idx] : 0;
+      const unsigned long long hm = __ballot(in && xv > v);
+      const int stop = hm ? __ffsll((long long)hm) - 1 : 64;
+      int cand = (in && lane < stop) ? xv : v;
+      for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o));
+      rmin = min(rmin, cand);
+      if (hm) break;
+    }
+    const int prom = v - max(lmin, rmin);
+    if (lane == 0 && pmin <= (double)prom) is_kept[p] = 1;
+  }
+  __syncthreads();
+  // --- top-3 by (count, centre) == (count, bin) descending (:744-750)
+  for (int m = 0; m < RGBD_MAX_MODES; ++m) {
+    long long key = is_kept[t] ? (((long long)x[t] << 10) | t) : -1ll;
+    key = wave_max_i64(key);
+    if (lane == 0) red[wave] = key;
+    __syncthreads();
+    if (t == 0) {
+      long long best = red[0];
+      for (int i = 1; i < 8; ++i) best = red[i] > best ? red[i] : best;
+      sel[m] = best < 0 ? -1 : (int)(best & 1023);
+      if (best >= 0) is_kept[best & 1023] = 0;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float rr = ratio[b];
+    int n = 0;
+    for (int m = 0; m < RGBD_MAX_MODES; ++m) {
+      const int p = sel[m];
+      if (p < 0) break;
+      const float e0 = edge_at(r, p), e1 = edge_at(r, p + 1);
+      const float c = __fadd_rn(e0, __fmul_rn(__fsub_rn(e1, e0), 0.5f));  // edge + diff/2 (:745)
+      const float half = __fmul_rn(__fmul_rn(c, rr), 0.5f);                // c * r / 2 (:768)
+      float lo = __fsub_rn(c, half);
+      if (!(lo > 0.f)) lo = 0.f;                                            // max(0, .) (:769)
+      out->peak_bin[m] = p;
+      out->center[m] = c;
+      out->lo[m] = lo;
+      out->hi[m] = __fadd_rn(c, half);                                       // (:770)
+      ++n;
+    }
+    for (int m = n; m < RGBD_MAX_MODES; ++m) {
+      out->peak_bin[m] = -1;
+      out->center[m] = out->lo[m] = out->hi[m] = 0.f;
+    }
+    out->status = 0;
+    out->n_modes = n;
+    out->n_masks = n ? n + 1 : RGBD_MAX_MODES + 1;
+    out->first_edge = r.first;
+    out->last_edge = r.last;
+  }
+}
+
+__device__ __forceinline__ uint32_t pixel_code(float g, int n, const float* lo, const float* hi) {
+  if (n == 0) return 0u;  // no mode: four all-zero masks (:676-678)
+  uint32_t c = 0u;
+  for (int t = 0; t < n; ++t)
+    if (g >= lo[t] && g <= hi[t]) c |= 1u << t;  // (d >= lo) & (d <= hi) (:790)
+  if (c == 0u) c = 1u << n;                      // remaining region ~union (:795)
+  return c;
+}
+
+__global__ __launch_bounds__(256) void k_codes_pool(const float* __restrict__ depth3, long long bstride,
+                                                    int H, int W, int nch, int oh, int ow,
+                                                    const rgbd_decomp_info* info, uint8_t* __restrict__ code) {
+  const int b = blockIdx.y;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= oh * ow) return;
+  const int i = q / ow, j = q % ow;
+  const int n = info[b].n_modes;
+  float lo[RGBD_MAX_MODES], hi[RGBD_MAX_MODES];
+  for (int t = 0; t < RGBD_MAX_MODES; ++t) {
+    lo[t] = info[b].lo[t];
+    hi[t] = info[b].hi[t];
+  }
+  // adaptive_max_pool2d bins: [floor(i*H/oh), ceil((i+1)*H/oh))
+  const int y0 = (i * H) / oh, y1 = ((i + 1) * H + oh - 1) / oh;
+  const int x0 = (j * W) / ow, x1 = ((j + 1) * W + ow - 1) / ow;
+  const long long HW = (long long)H * W;
+  const float* d = depth3 + b * bstride;
+  uint32_t c = 0u;
+  if (n > 0)
+    for (int y = y0; y < y1; ++y)
+      for (int x = x0; x < x1; ++x) c |= pixel_code(grey_at(d, HW, (long long)y * W + x, nch), n, lo, hi);
+  code[(long long)b * oh * ow + q] = (uint8_t)c;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t rgbd_edsam_decompose_workspace_size(int B) { return align256(sizeof(DecWs) * (size_t)(B > 0 ? B : 1)); }
+
+int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
+                         const float* ratio, int n_scales, const int* out_h_host,
+                         const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
+                         void* ws, void* stream) {
+  RGBD_REQUIRE(depth3 && ratio && info && ws, RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && n_scales >= 0 && n_scales <= 8, RGBD_E_ARG);
+  RGBD_REQUIRE(depth_channels == 1 || depth_channels == 3, RGBD_E_SHAPE);
+  const int nch = depth_channels;
+  for (int s = 0; s < n_scales; ++s) {
+    RGBD_REQUIRE(out_h_host && out_w_host && codes_host && codes_host[s], RGBD_E_ARG);
+    RGBD_REQUIRE(out_h_host[s] > 0 && out_w_host[s] > 0 && out_h_host[s] <= H && out_w_host[s] <= W,
+                 RGBD_E_SHAPE);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  DecWs* w = (DecWs*)ws;
+  const long long HW = (long long)H * W;
+  k_init<<<B, 256, 0, st>>>(w, info, B);
+  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 512), B);
+  k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w);
+  k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w, info);
+  k_peaks<<<B, 512, 0, st>>>(w, ratio, info);
+  for (int s = 0; s < n_scales; ++s) {
+    dim3 g2(ceil_div((long long)out_h_host[s] * out_w_host[s], 256), B);
+    k_codes_pool<<<g2, 256, 0, st>>>(depth3, batch_stride, H, W, nch, out_h_host[s], out_w_host[s], info,
+                                     codes_host[s]);
+  }
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// MFMA fragment helpers shared by the implicit-GEMM kernels.
+//
+// Both precisions use the 16x16 output tile (C/D map: col = lane&15, row = 4*(lane>>4)+reg)
+// and the same per-lane K slice: lane (r = lane&15, g = lane>>4) holds 8 consecutive
+// reduction elements k = 8g .. 8g+7 of a 32-wide K step for its A row / B column.
+//   bf16: one v_mfma_f32_16x16x32_bf16 (lane map A[r][8g+j], B[8g+j][r]  — exact match)
+//   f32 : eight v_mfma_f32_16x16x4_f32; step j uses element j, i.e. the instruction's
+//         k index l>>4 = g stands for reduction element 8g+j.  A and B apply the same
+//         permutation, so the sum is the same 32-term dot product (exact f32 products,
+//         f32 accumulation: the parity mode).
+#pragma once
+#include "common.hpp"
+
+namespace rgbd {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 mbf16x8;
+
+template <typename T> struct Frag;
+
+template <> struct Frag<bf16_t> {
+  uint4 v;  // 8 x bf16
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void zero() { v = make_uint4(0u, 0u, 0u, 0u); }
+  __device__ __forceinline__ void select(bool keep) {
+    if (!keep) zero();
+  }
+  __device__ __forceinline__ void set(int j, float f) {
+    uint32_t h = f32_to_bf16(f);
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+    w[j >> 1] = (j & 1) ? ((w[j >> 1] & 0xffffu) | (h << 16)) : ((w[j >> 1] & 0xffff0000u) | h);
+  }
+  __device__ __forceinline__ void set_raw(int j, bf16_t h) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+    w[j >> 1] = (j & 1) ? ((w[j >> 1] & 0xffffu) | ((uint32_t)h << 16)) : ((w[j >> 1] & 0xffff0000u) | h);
+  }
+};
+
+template <> struct Frag<float> {
+  float4 lo, hi;  // 8 x f32
+  __device__ __forceinline__ void load(const float* p) {
+    lo = *reinterpret_cast<const float4*>(p);
+    hi = *reinterpret_cast<const float4*>(p + 4);
+  }
+  __device__ __forceinline__ void zero() {
+    lo = make_float4(0.f, 0.f, 0.f, 0.f);
+    hi = lo;
+  }
+  __device__ __forceinline__ void select(bool keep) {
+    if (!keep) zero();
+  }
+  __device__ __forceinline__ void set(int j, float f) {
+    float* e = j < 4 ? reinterpret_cast<float*>(&lo) : reinterpret_cast<float*>(&hi);
+    e[j & 3] = f;
+  }
+};
+
+__device__ __forceinline__ void mma(f32x4& acc, const Frag<bf16_t>& a, const Frag<bf16_t>& b) {
+  mbf16x8 av, bv;
+  __builtin_memcpy(&av, &a.v, 16);
+  __builtin_memcpy(&bv, &b.v, 16);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ void mma(f32x4& acc, const Frag<float>& a, const Frag<float>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.x, b.lo.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.y, b.lo.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.z, b.lo.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo.w, b.lo.w, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.x, b.hi.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.y, b.hi.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.z, b.hi.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi.w, b.hi.w, acc, 0, 0, 0);
+}
+
+}  // namespace rgbd

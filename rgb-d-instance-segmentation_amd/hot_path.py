@@ -1,0 +1,120 @@
+"""The fused v0.4.0 hot path as one autograd Function over the HIP kernels.
+
+Reference (mask2former/utils/custom_model.py:324-355), per step:
+    cp1 = cp2 = detached clones of the 4 Swin maps                          (:332-333, Q1)
+    r   = ratio_predictor(depth) -> .item() per sample (no grad)            (:336, :339-351, Q2)
+    for k in 0..2: cp1[k+1] += stack_b dsam_k(cp1[k][b], grey(depth[b]), r[b])   (:339-352, Q4)
+    cp2 = DGGM(cp2, grad, mask)                                             (:354)
+    out = [cp1_k + cp2_k]                                                   (:355, Q3)
+Here:
+    decomposition once per image for the three DSAM input resolutions (K3),
+    dsam_k over the whole batch in one masked implicit-GEMM launch whose epilogue adds the
+      residual colour map (cp1[k+1] = colour[k+1] + dsam_k) and writes the NHWC copy the next
+      DSAM reads (K5),
+    DGGM gate + final sum in one elementwise pass per scale (K2).
+Backward produces exactly the gradients the reference graph has: DSAM / DGGM parameters,
+nothing for the colour maps (detached) or the ratio (left the graph via .item()).
+"""
+import torch
+
+from . import ops
+
+DSAM_PARAMS_PER_MODULE = 9  # conv_layers.{0..3}.{weight,bias}, rgb_projection.weight
+
+
+class _PackCache:
+    """Packed implicit-GEMM weights, re-packed only when a parameter changes."""
+
+    def __init__(self):
+        self.key = None
+        self.val = None
+
+    def get(self, conv_ws, proj_w, dtype):
+        key = (dtype, proj_w.data_ptr(), proj_w._version) + tuple((w.data_ptr(), w._version) for w in conv_ws)
+        if key != self.key:
+            self.val = ops.dsam_pack(torch.stack([w.detach() for w in conv_ws]), proj_w.detach(), dtype)
+            self.key = key
+        return self.val
+
+
+class HotPathFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pixel_values, ratio, cfg, c0, c1, c2, c3, *params):
+        dtype = cfg["dtype"]
+        colors = [c.detach().to(dtype).contiguous() for c in (c0, c1, c2, c3)]
+        dsam_p = [params[9 * k:9 * k + 9] for k in range(3)]
+        dggm_p = params[27:35]
+        sizes = [tuple(c.shape[2:]) for c in colors[:3]]
+        codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
+        if cfg.get("check_status"):
+            ops.raise_on_status(info)
+        packs = [cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype) for k in range(3)]
+        x_nhwc = [ops.nchw_to_nhwc(colors[0])]
+        cp1 = [colors[0]]
+        for k in range(3):
+            bias4 = torch.stack([b.detach() for b in dsam_p[k][1:8:2]])
+            out, out_nhwc = ops.dsam_fwd(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual=colors[k + 1],
+                                         want_nhwc=(k < 2))
+            cp1.append(out)
+            if k < 2:
+                x_nhwc.append(out_nhwc)
+        outs = [ops.dggm_fuse_fwd(cp1[k], colors[k], pixel_values, dggm_p[2 * k], dggm_p[2 * k + 1])
+                for k in range(4)]
+        ctx.cfg = cfg
+        ctx.codes = codes
+        ctx.info = info
+        ctx.x_nhwc = x_nhwc
+        ctx.packs = packs
+        ctx.save_for_backward(pixel_values, *dggm_p)
+        ctx.dtype = dtype
+        ctx.in_dtypes = [c.dtype for c in (c0, c1, c2, c3)]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, g0, g1, g2, g3):
+        pixel_values, *dggm_p = ctx.saved_tensors
+        dtype = ctx.dtype
+        G = []
+        for k, g in enumerate((g0, g1, g2, g3)):
+            if g is None:
+                shape = ctx.x_nhwc[0].shape if k == 0 else None
+                raise RuntimeError("hot-path backward needs gradients for all four backbone features"
+                                   if shape is None else "missing gradient for scale 0")
+            G.append(g.to(dtype).contiguous())
+        grads_dggm = []
+        for k in range(4):
+            dw, db = ops.dggm_fuse_bwd(G[k], pixel_values, dggm_p[2 * k], dggm_p[2 * k + 1])
+            grads_dggm += [dw.reshape(dggm_p[2 * k].shape).to(dggm_p[2 * k].dtype), db.to(dggm_p[2 * k + 1].dtype)]
+        # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}
+        dcp = G[3]
+        dcp_nhwc = ops.nchw_to_nhwc(dcp)
+        grads_dsam = [None, None, None]
+        for k in (2, 1, 0):
+            dconv, dproj, dbias = ops.dsam_bwd_weight(dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info)
+            gk = []
+            for i in range(4):
+                gk += [dconv[i], dbias[i]]
+            gk.append(dproj)
+            grads_dsam[k] = gk
+            if k > 0:
+                dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k],
+                                                  want_nhwc=(k > 1))
+        pgrads = grads_dsam[0] + grads_dsam[1] + grads_dsam[2] + grads_dggm
+        return (None, None, None, None, None, None, None, *pgrads)
+
+
+def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch.float32, check_status=False):
+    """Run the fused hot path.  ``dsam_modules``: the three DSAModule instances;
+    ``dggm_module``: the DepthGradientInjectionResidual instance."""
+    params = []
+    for m in dsam_modules:
+        for i in range(4):
+            params += [m.conv_layers[i].weight, m.conv_layers[i].bias]
+        params.append(m.rgb_projection.weight)
+    for i in range(4):
+        conv = dggm_module.depth_enhancement_layers[i][0]
+        params += [conv.weight, conv.bias]
+    cfg = {"dtype": dtype, "check_status": check_status,
+           "pack_cache": [m._pack_cache for m in dsam_modules]}
+    pv = pixel_values.detach().float().contiguous()
+    return list(HotPathFunction.apply(pv, ratio, cfg, *colors, *params))

@@ -1,0 +1,236 @@
+"""Torch-facing wrappers of the librgbd_hip.so entry points (one per C-ABI function).
+
+Every wrapper validates shapes/devices on the host, allocates outputs with torch (device
+memory is plumbing), passes raw pointers + the current HIP stream to the C ABI and raises
+``RgbdHipError`` on a non-zero return.  Nothing here synchronises with the device except
+``decode_info`` (explicitly a host read-back for tests/diagnostics).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import RGBD_BF16, RGBD_F32, DECOMP_INFO_DTYPE, check
+
+_ws_cache = {}
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return RGBD_F32
+    if t.dtype == torch.bfloat16:
+        return RGBD_BF16
+    raise TypeError(f"rgbd_amd kernels take float32 or bfloat16 tensors, got {t.dtype}")
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("rgbd_amd ops run on the GPU only (no CPU fallback); got a CPU tensor")
+        if t is not None and not t.is_contiguous():
+            raise RuntimeError("rgbd_amd ops expect contiguous tensors")
+
+
+def _workspace(dev, nbytes: int, tag: str):
+    key = (dev, tag)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+        _ws_cache[key] = buf
+    return buf
+
+
+# ------------------------------------------------------------------ K1 DGGM-pre / assembly
+def assemble_pixel_values(depth_u8: torch.Tensor, rgb_u8: torch.Tensor = None, out: torch.Tensor = None):
+    """depth_u8 [B,H,W] uint8 (+ rgb_u8 [B,H,W,3]) -> pixel_values float32 [B,10,H,W]
+    (map_10channel_case2 layout, dataloader.py:386-425; DGGM-pre data_process.py:1247-1305)."""
+    _need_cuda(depth_u8, rgb_u8)
+    if depth_u8.dtype != torch.uint8 or depth_u8.dim() != 3:
+        raise ValueError("depth_u8 must be uint8 [B,H,W]")
+    B, H, W = depth_u8.shape
+    if rgb_u8 is not None and (rgb_u8.dtype != torch.uint8 or tuple(rgb_u8.shape) != (B, H, W, 3)):
+        raise ValueError("rgb_u8 must be uint8 [B,H,W,3]")
+    if out is None:
+        out = torch.zeros((B, 10, H, W), dtype=torch.float32, device=depth_u8.device)
+    L = _lib.lib()
+    ws = _workspace(depth_u8.device, L.rgbd_assemble_workspace_size(B), "assemble")
+    check(L.rgbd_assemble_pixel_values(_p(rgb_u8), _p(depth_u8), B, H, W, _p(out), _p(ws),
+                                       _stream(depth_u8.device)), "rgbd_assemble_pixel_values")
+    return out
+
+
+# ------------------------------------------------------------------ K3 decomposition
+def edsam_decompose(pixel_values: torch.Tensor, ratio: torch.Tensor, sizes):
+    """Depth decomposition of every image, once for all DSAMs.
+
+    pixel_values: float32 [B,C>=6,H,W] (depth planes = channels 3:6, custom_model.py:326), a
+    [B,3,H,W] depth tensor, or a [B,1,H,W] already-grey map; ratio: float32 [B] or [B,1] on device; sizes: list of (h, w).
+    Returns (codes list of uint8 [B,h,w], info uint8 [B, 2116] device tensor)."""
+    _need_cuda(pixel_values, ratio)
+    if pixel_values.dtype != torch.float32:
+        raise TypeError("the decomposition consumes float32 depth (SURVEY §7 (i))")
+    B, C, H, W = pixel_values.shape
+    nch = 1 if C == 1 else 3
+    depth3 = pixel_values if C in (1, 3) else pixel_values[:, 3:6]
+    r = ratio.reshape(-1).to(torch.float32).contiguous()
+    if r.numel() != B:
+        raise ValueError("one ratio per image expected")
+    dev = pixel_values.device
+    codes = [torch.empty((B, h, w), dtype=torch.uint8, device=dev) for (h, w) in sizes]
+    info = torch.empty((B, DECOMP_INFO_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    n = len(sizes)
+    oh = (ctypes.c_int * max(n, 1))(*[s[0] for s in sizes])
+    ow = (ctypes.c_int * max(n, 1))(*[s[1] for s in sizes])
+    cp = (ctypes.c_void_p * max(n, 1))(*[c.data_ptr() for c in codes])
+    L = _lib.lib()
+    ws = _workspace(dev, L.rgbd_edsam_decompose_workspace_size(B), "decompose")
+    check(L.rgbd_edsam_decompose(ctypes.c_void_p(depth3.data_ptr()), depth3.stride(0), nch, B, H, W, _p(r), n,
+                                 oh, ow, cp, _p(info), _p(ws), _stream(dev)), "rgbd_edsam_decompose")
+    return codes, info
+
+
+def decode_info(info: torch.Tensor) -> np.ndarray:
+    """Host copy of the per-image decomposition records (synchronises)."""
+    return info.cpu().numpy().view(DECOMP_INFO_DTYPE).reshape(-1)
+
+
+def raise_on_status(info: torch.Tensor):
+    """Mirror the reference's ValueError for degenerate histograms (numpy raises inside
+    DSAModule._calculate_depth_histogram, custom_model.py:717).  Synchronises."""
+    rec = decode_info(info)
+    for b, s in enumerate(rec["status"]):
+        if s == 1:
+            raise ValueError(f"image {b}: supplied range of depth is not finite (np.histogram)")
+        if s == 2:
+            raise ValueError(f"image {b}: Too many bins for data range. Cannot create 512 finite-sized bins.")
+
+
+# ------------------------------------------------------------------ K2 DGGM fusion
+def _grad_mask(pv):
+    if pv.dtype != torch.float32 or pv.shape[1] not in (4, 10):
+        raise ValueError("DGGM planes must be float32 [B,10,H,W] pixel_values or [B,4,H,W] (grad x3, mask)")
+    return (pv[:, 6:9], pv[:, 9:10]) if pv.shape[1] == 10 else (pv[:, 0:3], pv[:, 3:4])
+
+
+def dggm_fuse_fwd(cp1, color, pixel_values, weight, bias):
+    """out = cp1 + (color + ReLU(W . (bilinear(grad) * nearest(mask)) + b)), one scale
+    (cp1=None: out = color + ReLU(...), the bare DepthGradientInjectionResidual output).
+    ``pixel_values``: float32 [B, >=4, H, W] holding grad planes at channels -4:-1 and the
+    mask at channel -1 when it has 4 channels, or the full 10-channel tensor."""
+    _need_cuda(cp1, color, pixel_values, weight, bias)
+    B, C, h, w = color.shape
+    _, _, H, W = pixel_values.shape
+    if cp1 is not None and (cp1.shape != color.shape or cp1.dtype != color.dtype):
+        raise ValueError("cp1/color mismatch")
+    if weight.shape[0] != C or bias.shape[0] != C:
+        raise AssertionError(f"Expected {C} channels in the DGGM projection")
+    out = torch.empty_like(color)
+    wt = weight.reshape(C, 3).float().contiguous()
+    bs = bias.float().contiguous()
+    grad, mask = _grad_mask(pixel_values)
+    check(_lib.lib().rgbd_dggm_fuse_fwd(_dtype_code(color), _p(cp1), _p(color), ctypes.c_void_p(grad.data_ptr()),
+                                        ctypes.c_void_p(mask.data_ptr()), pixel_values.stride(0), B, H, W, C,
+                                        h, w, _p(wt), _p(bs), _p(out), _stream(color.device)),
+          "rgbd_dggm_fuse_fwd")
+    return out
+
+
+def dggm_fuse_bwd(dout, pixel_values, weight, bias):
+    _need_cuda(dout, pixel_values, weight, bias)
+    B, C, h, w = dout.shape
+    _, _, H, W = pixel_values.shape
+    wt = weight.reshape(C, 3).float().contiguous()
+    bs = bias.float().contiguous()
+    dw = torch.empty((C, 3), dtype=torch.float32, device=dout.device)
+    db = torch.empty((C,), dtype=torch.float32, device=dout.device)
+    L = _lib.lib()
+    ws = _workspace(dout.device, L.rgbd_dggm_fuse_bwd_workspace_size(B, C, h, w), "dggm_bwd")
+    grad, mask = _grad_mask(pixel_values)
+    check(L.rgbd_dggm_fuse_bwd(_dtype_code(dout), _p(dout), ctypes.c_void_p(grad.data_ptr()),
+                               ctypes.c_void_p(mask.data_ptr()), pixel_values.stride(0), B, H, W, C, h, w,
+                               _p(wt), _p(bs), _p(dw), _p(db), _p(ws), _stream(dout.device)),
+          "rgbd_dggm_fuse_bwd")
+    return dw, db
+
+
+# ------------------------------------------------------------------ layout / packing
+def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    _need_cuda(x)
+    B, C, H, W = x.shape
+    y = torch.empty((B, H, W, C), dtype=x.dtype, device=x.device)
+    check(_lib.lib().rgbd_nchw_to_nhwc(_dtype_code(x), _p(x), _p(y), B, C, H, W, _stream(x.device)),
+          "rgbd_nchw_to_nhwc")
+    return y
+
+
+def dsam_pack(conv_w: torch.Tensor, proj_w: torch.Tensor, dtype: torch.dtype):
+    """conv_w float32 [4,Co,Ci,3,3], proj_w [Co,Ci,3,3] -> (wfwd [Co,45*Ci], wbwd [Ci,45*Co])."""
+    cw = conv_w.detach().float().contiguous()
+    pw = proj_w.detach().float().contiguous()
+    _need_cuda(cw, pw)
+    Co, Ci = pw.shape[:2]
+    wfwd = torch.empty((Co, 45 * Ci), dtype=dtype, device=cw.device)
+    wbwd = torch.empty((Ci, 45 * Co), dtype=dtype, device=cw.device)
+    check(_lib.lib().rgbd_dsam_pack_weights(_dtype_code(wfwd), _p(cw), _p(pw), Ci, Co, _p(wfwd), _p(wbwd),
+                                            _stream(cw.device)), "rgbd_dsam_pack_weights")
+    return wfwd, wbwd
+
+
+# ------------------------------------------------------------------ K5 DSAM convs
+def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
+    """x_nhwc [B,h,w,Ci] -> (out_nchw [B,Co,ho,wo], out_nhwc or None)."""
+    _need_cuda(x_nhwc, code, info, wfwd, bias4, residual)
+    B, h, w, Ci = x_nhwc.shape
+    Co = wfwd.shape[0]
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    if tuple(code.shape) != (B, h, w):
+        raise ValueError(f"region code {tuple(code.shape)} does not match features {(B, h, w)}")
+    if residual is not None and tuple(residual.shape) != (B, Co, ho, wo):
+        raise ValueError(f"residual {tuple(residual.shape)} != {(B, Co, ho, wo)}")
+    out = torch.empty((B, Co, ho, wo), dtype=x_nhwc.dtype, device=x_nhwc.device)
+    out_nhwc = torch.empty((B, ho, wo, Co), dtype=x_nhwc.dtype, device=x_nhwc.device) if want_nhwc else None
+    b4 = bias4.detach().float().contiguous()
+    check(_lib.lib().rgbd_dsam_fwd(_dtype_code(x_nhwc), _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co,
+                                   _p(wfwd), _p(b4), _p(residual), _p(out), _p(out_nhwc),
+                                   _stream(x_nhwc.device)), "rgbd_dsam_fwd")
+    return out, out_nhwc
+
+
+def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False):
+    _need_cuda(gout_nhwc, code, wbwd, gin_nchw)
+    B, ho, wo, Co = gout_nhwc.shape
+    Ci = wbwd.shape[0]
+    _, h, w = code.shape
+    if gin_nchw is not None and tuple(gin_nchw.shape) != (B, Ci, h, w):
+        raise ValueError("gin shape mismatch")
+    dx = torch.empty((B, Ci, h, w), dtype=gout_nhwc.dtype, device=gout_nhwc.device)
+    dx_nhwc = torch.empty((B, h, w, Ci), dtype=gout_nhwc.dtype, device=gout_nhwc.device) if want_nhwc else None
+    check(_lib.lib().rgbd_dsam_bwd_data(_dtype_code(gout_nhwc), _p(gout_nhwc), _p(code), B, Ci, h, w, Co,
+                                        _p(wbwd), _p(gin_nchw), _p(dx), _p(dx_nhwc), _stream(gout_nhwc.device)),
+          "rgbd_dsam_bwd_data")
+    return dx, dx_nhwc
+
+
+def dsam_bwd_weight(gout_nchw, x_nhwc, code, info):
+    _need_cuda(gout_nchw, x_nhwc, code, info)
+    B, Co, ho, wo = gout_nchw.shape
+    _, h, w, Ci = x_nhwc.shape
+    dev = gout_nchw.device
+    dconv = torch.empty((4, Co, Ci, 3, 3), dtype=torch.float32, device=dev)
+    dproj = torch.empty((Co, Ci, 3, 3), dtype=torch.float32, device=dev)
+    dbias = torch.empty((4, Co), dtype=torch.float32, device=dev)
+    dt = _dtype_code(gout_nchw)
+    L = _lib.lib()
+    ws = _workspace(dev, L.rgbd_dsam_bwd_weight_workspace_size(dt, B, Ci, h, w, Co), "dsam_wgrad")
+    check(L.rgbd_dsam_bwd_weight(dt, _p(gout_nchw), _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co,
+                                 _p(dconv), _p(dproj), _p(dbias), _p(ws), _stream(dev)), "rgbd_dsam_bwd_weight")
+    return dconv, dproj, dbias
