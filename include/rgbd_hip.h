@@ -139,6 +139,29 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, c
                          const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
                          float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream);
 
+/* ---------------------------------------------------------------- K4 ratio predictor
+ * EnhancedDepthImageRatioPredictor.forward (custom_model.py:1444-1487) for the batch:
+ * depth3 (float32 planes as for the decomposition) -> ratio float32 [B] in [0.01, 0.5],
+ * left on device (the reference's k.item() host sync of :339-351 is gone).
+ * Weights (they receive no gradient in v0.4.0, Q2) are packed once:
+ *   weights_host: RGBD_RATIO_NW device pointers to the float32 state_dict tensors, order
+ *     scale1_conv.0.{weight,bias}, scale2_conv.0.*, scale3_conv.0.*, feature_fusion.0.*,
+ *     attention.0.*, attention.2.*, feature_extractor.0.*, feature_extractor.4.*,
+ *     fc_layers.0.*, fc_layers.3.*, fc_layers.6.*, fc_layers.8.*
+ *   bn_host: RGBD_RATIO_NBN x {weight, bias, running_mean, running_var} device pointers for
+ *     scale1_conv.1, scale2_conv.1, scale3_conv.1, feature_fusion.1, feature_extractor.1,
+ *     feature_extractor.5.  training=1 uses batch statistics and updates the running stats
+ *     in place (torch semantics, `momentum`), and applies dropout with a counter hash of
+ *     `seed`; training=0 uses the running stats.  B <= 32. */
+#define RGBD_RATIO_NW 24
+#define RGBD_RATIO_NBN 6
+size_t rgbd_ratio_packed_size(int dtype);
+int rgbd_ratio_pack(int dtype, const float* const* weights_host, void* packed, void* stream);
+size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W);
+int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
+                       int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
+                       float* ratio, void* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

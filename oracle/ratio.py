@@ -42,3 +42,16 @@ def ratio_forward(depth: torch.Tensor, p: dict, training: bool = False) -> torch
     h = F.relu(F.linear(h, p["fc_layers.6.weight"], p["fc_layers.6.bias"]))
     raw = F.linear(h, p["fc_layers.8.weight"], p["fc_layers.8.bias"])     # :1482
     return 0.01 + (0.5 - 0.01) * torch.sigmoid(raw)                       # :1485
+
+
+def ratio_forward_modules(m, depth):
+    """Same forward through the nn.Module tree of an (identically keyed) module on the CPU —
+    the plain PyTorch fp32 reference used to check train-mode BatchNorm running-stat updates
+    (Dropout modules are skipped so the comparison is deterministic)."""
+    s = torch.cat([m.scale1_conv(depth), m.scale2_conv(depth), m.scale3_conv(depth)], dim=1)
+    f = m.feature_fusion(s)
+    e = m.feature_extractor(f * m.attention(f))
+    g = F.adaptive_avg_pool2d(e, 1).flatten(1)
+    fc = m.fc_layers
+    h = fc[8](fc[7](fc[6](fc[4](fc[3](fc[1](fc[0](g)))))))
+    return 0.01 + (0.5 - 0.01) * torch.sigmoid(h)

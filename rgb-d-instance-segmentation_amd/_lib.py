@@ -43,6 +43,11 @@ SIGNATURES = {
     "rgbd_dsam_bwd_data": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_weight_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rgbd_dsam_bwd_weight": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "rgbd_ratio_packed_size": (_SZ, [_I]),
+    "rgbd_ratio_pack": (_I, [_I, _P, _P, _P]),
+    "rgbd_ratio_workspace_size": (_SZ, [_I, _I, _I, _I]),
+    "rgbd_ratio_forward": (_I, [_I, _I, ctypes.c_float, _P, _LL, _I, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P,
+                                _P]),
 }
 
 _lib = None

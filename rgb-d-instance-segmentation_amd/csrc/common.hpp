@@ -53,6 +53,13 @@ __device__ __forceinline__ float key_f32(uint32_t k) {
   return __uint_as_float(u);
 }
 
+// Correctly rounded float32 division / sqrt.  HIP's default f32 `/` and sqrtf are not
+// IEEE-rounded on gfx950 (measured: 28 of 256 quotients off by 1 ulp vs numpy), so every
+// op that must match numpy bit-for-bit goes through double: for / and sqrt of float32
+// operands, rounding the f64 result to f32 is exact rounding (53 >= 2*24+2 bits).
+__device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
+__device__ __forceinline__ float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
+
 __device__ __forceinline__ float wave_min(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
   return v;
@@ -60,6 +67,15 @@ __device__ __forceinline__ float wave_min(float v) {
 __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
+}
+
+// Hide a loop-invariant pointer from LICM: without it hipcc hoists every weight-fragment load
+// of a persistent tile loop out of the loop and spills them all to scratch.
+template <class P>
+__device__ __forceinline__ P opaque(P p) {
+  uintptr_t u = (uintptr_t)p;
+  asm volatile("" : "+s"(u));
+  return (P)u;
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }

@@ -41,7 +41,7 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 __device__ __forceinline__ float norm_u8(uint8_t v, int c) {
   // numpy: (x.astype(f32) * f32(1/255) - mean_c) / std_c, one rounding per op
   float x = __fmul_rn((float)v, 0.003921568859368563f);
-  return __fdiv_rn(__fsub_rn(x, kMean[c]), kStd[c]);
+  return div_rn(__fsub_rn(x, kMean[c]), kStd[c]);
 }
 
 __global__ __launch_bounds__(256) void k_prep_pass1(const uint8_t* __restrict__ rgb,
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void k_prep_pass1(const uint8_t* __restrict__ 
     auto at = [&](int yy, int xx) { return (int)d[(long long)yy * W + xx]; };
     const int gx = (at(ym, xp) - at(ym, xm)) + 2 * (at(y, xp) - at(y, xm)) + (at(yp, xp) - at(yp, xm));
     const int gy = (at(yp, xm) - at(ym, xm)) + 2 * (at(yp, x) - at(ym, x)) + (at(yp, xp) - at(ym, xp));
-    float mag = __fsqrt_rn((float)(gx * gx + gy * gy));  // exact integer argument (< 2^24)
+    float mag = sqrt_rn((float)(gx * gx + gy * gy));  // exact integer argument (< 2^24)
     if (dv == 0) mag = 0.f;                               // invalid depth (:1265, :1278)
     out[6 * HW + p] = mag;                                // scratch until pass 2
     out[9 * HW + p] = mag > 0.f ? 1.f : 0.f;              // valid-gradient mask (:1282)
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void k_prep_pass2(int H, int W, float* __restr
   const float den = __fsub_rn(mx, mn);
   for (long long p = blockIdx.x * 256ll + threadIdx.x; p < HW; p += 256ll * gridDim.x) {
     const float mag = out[6 * HW + p];
-    const float v = scale ? __fdiv_rn(__fsub_rn(mag, mn), den) : 0.f;
+    const float v = scale ? div_rn(__fsub_rn(mag, mn), den) : 0.f;
     out[6 * HW + p] = v;
     out[7 * HW + p] = v;
     out[8 * HW + p] = v;

@@ -55,7 +55,7 @@ __device__ __forceinline__ Range make_range(const DecWs& w) {
     r.last = __fadd_rn(r.last, 0.5f);
   }
   r.denom = __fsub_rn(r.last, r.first);
-  r.step = __fdiv_rn(r.denom, 512.f);  // linspace: (stop - start) / 512
+  r.step = div_rn(r.denom, 512.f);  // linspace: (stop - start) / 512
   if (r.status == 0 && r.step == 0.f) r.status = 2;
   return r;
 }
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void k_hist(const float* __restrict__ depth3, 
   for (long long p = blockIdx.x * 256ll + threadIdx.x; p < HW; p += 256ll * gridDim.x) {
     const float g = grey_at(d, HW, p, nch);
     if (!(g >= r.first && g <= r.last)) continue;  // `keep` mask (drops NaN)
-    const float f = __fmul_rn(__fdiv_rn(__fsub_rn(g, r.first), r.denom), 512.f);
+    const float f = __fmul_rn(div_rn(__fsub_rn(g, r.first), r.denom), 512.f);
     int idx = (int)f;
     if (idx == RGBD_NBINS) idx -= 1;
     if (g < edge_at(r, idx)) idx -= 1;

@@ -24,14 +24,23 @@ template <> struct Frag<bf16_t> {
   __device__ __forceinline__ void select(bool keep) {
     if (!keep) zero();
   }
-  __device__ __forceinline__ void set(int j, float f) {
-    uint32_t h = f32_to_bf16(f);
-    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
-    w[j >> 1] = (j & 1) ? ((w[j >> 1] & 0xffffu) | (h << 16)) : ((w[j >> 1] & 0xffff0000u) | h);
-  }
+  // element setters: j must be a compile-time constant after unrolling (switch keeps the
+  // fragment in registers; a pointer into it would force scratch)
+  __device__ __forceinline__ void set(int j, float f) { set_raw(j, f32_to_bf16(f)); }
   __device__ __forceinline__ void set_raw(int j, bf16_t h) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
-    w[j >> 1] = (j & 1) ? ((w[j >> 1] & 0xffffu) | ((uint32_t)h << 16)) : ((w[j >> 1] & 0xffff0000u) | h);
+    const uint32_t hv = h;
+    switch (j >> 1) {
+      case 0: v.x = (j & 1) ? ((v.x & 0xffffu) | (hv << 16)) : ((v.x & 0xffff0000u) | hv); break;
+      case 1: v.y = (j & 1) ? ((v.y & 0xffffu) | (hv << 16)) : ((v.y & 0xffff0000u) | hv); break;
+      case 2: v.z = (j & 1) ? ((v.z & 0xffffu) | (hv << 16)) : ((v.z & 0xffff0000u) | hv); break;
+      default: v.w = (j & 1) ? ((v.w & 0xffffu) | (hv << 16)) : ((v.w & 0xffff0000u) | hv); break;
+    }
+  }
+  __device__ __forceinline__ void from8(const float (&f)[8]) {
+    v.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
+    v.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
+    v.z = (uint32_t)f32_to_bf16(f[4]) | ((uint32_t)f32_to_bf16(f[5]) << 16);
+    v.w = (uint32_t)f32_to_bf16(f[6]) | ((uint32_t)f32_to_bf16(f[7]) << 16);
   }
 };
 
@@ -49,8 +58,20 @@ template <> struct Frag<float> {
     if (!keep) zero();
   }
   __device__ __forceinline__ void set(int j, float f) {
-    float* e = j < 4 ? reinterpret_cast<float*>(&lo) : reinterpret_cast<float*>(&hi);
-    e[j & 3] = f;
+    switch (j) {
+      case 0: lo.x = f; break;
+      case 1: lo.y = f; break;
+      case 2: lo.z = f; break;
+      case 3: lo.w = f; break;
+      case 4: hi.x = f; break;
+      case 5: hi.y = f; break;
+      case 6: hi.z = f; break;
+      default: hi.w = f; break;
+    }
+  }
+  __device__ __forceinline__ void from8(const float (&f)[8]) {
+    lo = make_float4(f[0], f[1], f[2], f[3]);
+    hi = make_float4(f[4], f[5], f[6], f[7]);
   }
 };
 

@@ -1,0 +1,766 @@
+// K4: EnhancedDepthImageRatioPredictor (mask2former/utils/custom_model.py:1363-1487) on gfx950.
+//
+// 216 GFLOP/img at 640x480 — the FLOP-dominant row of the hot path (SURVEY Finding 1).
+// Stages (one float32 depth image [3,H,W] in, one ratio out):
+//   chain  : per pixel, fully in registers, three chained MFMA GEMMs (k_rp_chain):
+//            stem   = the three 'same' convs 3x3 / 5x5 / 7x7 (3->64 each, :1378-1394) merged into
+//                     ONE 7x7 conv 3->192 (3x3 and 5x5 kernels embedded at the centre, zero
+//                     elsewhere; torch.cat order of :1463 preserved), implicit GEMM K=147->160
+//            fusion = 1x1 192->128 (:1397-1401), attention 1x1 128->64 ->ReLU-> 64->128 ->sigmoid
+//                     and the gate (:1404-1470).  Each GEMM's accumulator (channel in the
+//                     registers, pixel on the lane) is directly the next GEMM's B operand; the
+//                     packed weights use the matching k permutation, so nothing touches LDS.
+//   conv5  : 3x3 128->256 (:1413), 84 % of the FLOPs, LDS-tiled implicit GEMM (k_rp_conv3x3):
+//            a 4x32-pixel tile and its 6x34 halo are staged per 32-channel chunk and reused by
+//            all 9 taps; output y (NHWC) + per-workgroup BN partial sums.
+//   pool   : BN + ReLU + AdaptiveAvgPool(4) streamed over y (k_rp_bn_relu_pool)
+//   tail   : 3x3 256->512 on 4x4 + BN + ReLU + GAP (k_rp_tail_conv), MLP + dropout + sigmoid
+//            (k_rp_tail_mlp), ratio = 0.01 + 0.49 sigmoid(raw) (:1485).
+// BatchNorm: eval mode uses running stats (folded into per-channel scale/shift); train mode
+// uses batch statistics (three recompute passes of the chain for the stem / fusion BNs,
+// deterministic fixed-order reductions in double) and updates running stats like torch
+// (momentum, unbiased variance).  Dropout uses a counter-hash RNG (train mode only).
+#include "mfma.hpp"
+
+using namespace rgbd;
+
+namespace {
+
+constexpr int STEM_K = 160, STEM_C = 192, FUS_C = 128, ATT_C = 64, C5 = 256, C6 = 512;
+constexpr int NBN = 6;  // BN layers: scale1, scale2, scale3, fusion, fe.1, fe.5
+constexpr float BN_EPS = 1e-5f;
+
+struct Layout {  // byte offsets into the packed blob
+  size_t w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, w7, b7, w8, b8, w9, b9, w10, b10, total;
+};
+
+inline Layout make_layout(int es) {
+  Layout L;
+  size_t o = 0;
+  auto seg = [&](size_t bytes) {
+    size_t r = o;
+    o += align256(bytes);
+    return r;
+  };
+  L.w1 = seg((size_t)STEM_C * STEM_K * es);
+  L.b1 = seg(STEM_C * 4);
+  L.w2 = seg((size_t)FUS_C * STEM_C * es);
+  L.b2 = seg(FUS_C * 4);
+  L.w3 = seg((size_t)ATT_C * FUS_C * es);
+  L.b3 = seg(ATT_C * 4);
+  L.w4 = seg((size_t)FUS_C * ATT_C * es);
+  L.b4 = seg(FUS_C * 4);
+  L.w5 = seg((size_t)C5 * 9 * FUS_C * es);
+  L.b5 = seg(C5 * 4);
+  L.w6 = seg((size_t)C6 * C5 * 9 * 4);
+  L.b6 = seg(C6 * 4);
+  L.w7 = seg(128 * 512 * 4);
+  L.b7 = seg(128 * 4);
+  L.w8 = seg(64 * 128 * 4);
+  L.b8 = seg(64 * 4);
+  L.w9 = seg(32 * 64 * 4);
+  L.b9 = seg(32 * 4);
+  L.w10 = seg(32 * 4);
+  L.b10 = seg(4);
+  L.total = o;
+  return L;
+}
+
+// chained-operand permutation: packed position (g, e) of a 32-wide k step <-> channel
+__host__ __device__ __forceinline__ int chain_perm(int g, int e) { return e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4); }
+
+struct WPtrs {  // reference-layout float32 weights (device), order of RGBD_RATIO_NW
+  const float* p[RGBD_RATIO_NW];
+};
+struct BnPtrs {  // per BN layer: weight, bias, running_mean, running_var
+  float* p[NBN * 4];
+};
+
+// ------------------------------------------------------------------ packing
+template <typename T>
+__global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  T* w1 = (T*)(blob + L.w1);
+  float* b1 = (float*)(blob + L.b1);
+  for (int e = tid; e < STEM_C * STEM_K; e += nth) {  // stem: k = tap*3 + c over a 7x7 window
+    const int o = e / STEM_K, k = e % STEM_K;
+    float v = 0.f;
+    if (k < 147) {
+      const int tap = k / 3, c = k % 3, ky = tap / 7, kx = tap % 7;
+      const int br = o / 64, oo = o % 64, ks = 3 + 2 * br, off = 3 - ks / 2;  // 3x3 / 5x5 / 7x7
+      const int y = ky - off, x = kx - off;
+      if (y >= 0 && y < ks && x >= 0 && x < ks) v = w.p[2 * br][((oo * 3 + c) * ks + y) * ks + x];
+    }
+    w1[e] = Num<T>::from_f(v);
+  }
+  for (int e = tid; e < STEM_C; e += nth) b1[e] = w.p[2 * (e / 64) + 1][e % 64];
+  // chained 1x1 layers: packed[o][32s + 8g + e] = W[o][32s + perm(g, e)]
+  auto pack_chain = [&](const float* src, T* dst, int O, int K) {
+    for (int e = tid; e < O * K; e += nth) {
+      const int o = e / K, kk = e % K, s = kk / 32, g = (kk % 32) / 8, ee = kk % 8;
+      dst[e] = Num<T>::from_f(src[o * K + 32 * s + chain_perm(g, ee)]);
+    }
+  };
+  pack_chain(w.p[6], (T*)(blob + L.w2), FUS_C, STEM_C);
+  pack_chain(w.p[8], (T*)(blob + L.w3), ATT_C, FUS_C);
+  pack_chain(w.p[10], (T*)(blob + L.w4), FUS_C, ATT_C);
+  for (int e = tid; e < FUS_C; e += nth) ((float*)(blob + L.b2))[e] = w.p[7][e];
+  for (int e = tid; e < ATT_C; e += nth) ((float*)(blob + L.b3))[e] = w.p[9][e];
+  for (int e = tid; e < FUS_C; e += nth) ((float*)(blob + L.b4))[e] = w.p[11][e];
+  // conv5 [256][9][128] (k = tap*128 + c) from [256][128][3][3]
+  T* w5 = (T*)(blob + L.w5);
+  for (int e = tid; e < C5 * 9 * FUS_C; e += nth) {
+    const int o = e / (9 * FUS_C), tap = (e / FUS_C) % 9, c = e % FUS_C;
+    w5[e] = Num<T>::from_f(w.p[12][(o * FUS_C + c) * 9 + tap]);
+  }
+  for (int e = tid; e < C5; e += nth) ((float*)(blob + L.b5))[e] = w.p[13][e];
+  // tail + MLP stay float32 in reference layout
+  auto copy = [&](const float* src, size_t off, int n) {
+    for (int e = tid; e < n; e += nth) ((float*)(blob + off))[e] = src[e];
+  };
+  copy(w.p[14], L.w6, C6 * C5 * 9);
+  copy(w.p[15], L.b6, C6);
+  copy(w.p[16], L.w7, 128 * 512);
+  copy(w.p[17], L.b7, 128);
+  copy(w.p[18], L.w8, 64 * 128);
+  copy(w.p[19], L.b8, 64);
+  copy(w.p[20], L.w9, 32 * 64);
+  copy(w.p[21], L.b9, 32);
+  copy(w.p[22], L.w10, 32);
+  copy(w.p[23], L.b10, 1);
+}
+
+// ------------------------------------------------------------------ BN affine
+// scale/shift per channel: eval from running stats; train from a stats slab [nslab][C][2]
+// (sum, sum of squares), reduced in fixed order in double; running stats updated like torch.
+__global__ void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off, int C, double count,
+                            int training, float momentum, const float* gamma, const float* beta, float* run_mean,
+                            float* run_var, float2* __restrict__ affine) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < nslab; ++i) {  // fixed order: deterministic
+      s += (double)slab[((long long)i * row + c_off + c) * 2 + 0];
+      q += (double)slab[((long long)i * row + c_off + c) * 2 + 1];
+    }
+    const double m = s / count;
+    double v = q / count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    const double unb = count > 1.0 ? v * count / (count - 1.0) : v;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  } else {
+    mean = run_mean[c];
+    var = run_var[c];
+  }
+  const float sc = gamma[c] / sqrtf(var + BN_EPS);
+  affine[c] = make_float2(sc, beta[c] - mean * sc);
+}
+
+// ------------------------------------------------------------------ chain (stem, fusion, attention)
+constexpr int CH_TW = 16, CH_TH = 4;                    // tile: 4 rows x 16 cols, one row per wave
+constexpr int PATCH_H = CH_TH + 6, PATCH_W = CH_TW + 6;  // 7x7 halo
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <typename T>
+__device__ __forceinline__ Frag<T> load_w(const T* base, int row, int K, int s, int g) {
+  Frag<T> f;
+  f.load(base + (long long)row * K + 32 * s + 8 * g);
+  return f;
+}
+
+// PHASE 0: stem stats; 1: fusion stats; 2: write gated attention features (NHWC)
+template <typename T, int PHASE>
+__global__ __launch_bounds__(256) void k_rp_chain(const float* __restrict__ depth3, long long bstride, int B,
+                                                  int H, int W, const char* __restrict__ blob, Layout L,
+                                                  const float2* __restrict__ aff1, const float2* __restrict__ aff2,
+                                                  float* __restrict__ slab, T* __restrict__ att) {
+  __shared__ float patch[3][PATCH_H][PATCH_W];
+  __shared__ short ktab[STEM_K];  // k -> (c, ky, kx) offset into patch, -1 for the zero pad
+  __shared__ float st[4][STEM_C][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  constexpr int NST = PHASE == 0 ? STEM_C : FUS_C;
+  for (int k = threadIdx.x; k < STEM_K; k += 256) {
+    short v = -1;
+    if (k < 147) {
+      const int tap = k / 3, c = k % 3;
+      v = (short)((c * PATCH_H + tap / 7) * PATCH_W + tap % 7);
+    }
+    ktab[k] = v;
+  }
+  for (int i = threadIdx.x; i < 4 * STEM_C * 2; i += 256) (&st[0][0][0])[i] = 0.f;
+  const int tiles_x = (W + CH_TW - 1) / CH_TW, tiles_y = (H + CH_TH - 1) / CH_TH;
+  const long long ntiles = (long long)B * tiles_x * tiles_y;
+  const long long HW = (long long)H * W;
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
+    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
+    const int y0 = (trem / tiles_x) * CH_TH, x0 = (trem % tiles_x) * CH_TW;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * PATCH_H * PATCH_W; i += 256) {
+      const int c = i / (PATCH_H * PATCH_W), yy = (i / PATCH_W) % PATCH_H, xx = i % PATCH_W;
+      const int y = y0 + yy - 3, x = x0 + xx - 3;
+      (&patch[0][0][0])[i] =
+          (y >= 0 && y < H && x >= 0 && x < W) ? depth3[b * bstride + c * HW + (long long)y * W + x] : 0.f;
+    }
+    __syncthreads();
+    const int py = y0 + wave, px = x0 + r;
+    const bool pvalid = py < H && px < W;
+    const char* bl = opaque(blob);  // re-derived per tile: no LICM of the weight loads
+    const T* w1 = (const T*)(bl + L.w1);
+    const T* w2 = (const T*)(bl + L.w2);
+    const T* w3 = (const T*)(bl + L.w3);
+    const T* w4 = (const T*)(bl + L.w4);
+    const float* b1 = (const float*)(bl + L.b1);
+    const float* b2 = (const float*)(bl + L.b2);
+    const float* b3 = (const float*)(bl + L.b3);
+    const float* b4 = (const float*)(bl + L.b4);
+    const float2* af1 = opaque(aff1);
+    const float2* af2 = opaque(aff2);
+    // ---- stem: D1[192 ch][16 px]
+    f32x4 a1[12];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) a1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      Frag<T> bfr;
+      {
+        float vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int off = ktab[32 * s + 8 * g + e];
+          vv[e] = off >= 0 ? (&patch[0][0][0])[off + wave * PATCH_W + r] : 0.f;
+        }
+        bfr.from8(vv);
+      }
+#pragma unroll
+      for (int t = 0; t < 12; ++t) {
+        // the 3x3 / 5x5 branches have all-zero weights outside k in [48,99) / [24,123)
+        if (t < 4 && (s == 0 || s == 4)) continue;
+        if (t >= 4 && t < 8 && s == 4) continue;
+        mma(a1[t], load_w(w1, 16 * t + r, STEM_K, s, g), bfr);
+        __builtin_amdgcn_sched_barrier(0);  // keep weight loads from being hoisted (VGPR budget)
+      }
+    }
+    // z1 = a1 + b1 ; stats or BN+ReLU -> chained operand
+#pragma unroll
+    for (int t = 0; t < 12; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a1[t][j] += b1[16 * t + 4 * g + j];
+    if constexpr (PHASE == 0) {
+#pragma unroll
+      for (int t = 0; t < 12; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = pvalid ? a1[t][j] : 0.f, q = v * v;
+          for (int o = 1; o < 16; o <<= 1) {
+            v += __shfl_xor(v, o);
+            q += __shfl_xor(q, o);
+          }
+          if (r == 0) {
+            st[wave][16 * t + 4 * g + j][0] += v;
+            st[wave][16 * t + 4 * g + j][1] += q;
+          }
+        }
+      continue;
+    }
+    Frag<T> f1[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      float vv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int t = 2 * s + (e >> 2), j = e & 3, ch = 16 * t + 4 * g + j;
+        const float2 af = af1[ch];
+        vv[e] = fmaxf(a1[t][j] * af.x + af.y, 0.f);
+      }
+      f1[s].from8(vv);
+    }
+    // ---- fusion: D2[128][16 px]
+    f32x4 a2[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      a2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 6; ++s) mma(a2[t], load_w(w2, 16 * t + r, STEM_C, s, g), f1[s]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a2[t][j] += b2[16 * t + 4 * g + j];
+    }
+    if constexpr (PHASE == 1) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = pvalid ? a2[t][j] : 0.f, q = v * v;
+          for (int o = 1; o < 16; o <<= 1) {
+            v += __shfl_xor(v, o);
+            q += __shfl_xor(q, o);
+          }
+          if (r == 0) {
+            st[wave][16 * t + 4 * g + j][0] += v;
+            st[wave][16 * t + 4 * g + j][1] += q;
+          }
+        }
+      continue;
+    }
+    if constexpr (PHASE == 2) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float2 af = af2[16 * t + 4 * g + j];
+          a2[t][j] = fmaxf(a2[t][j] * af.x + af.y, 0.f);  // fused = ReLU(BN(z2))
+        }
+      Frag<T> f2[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vv[e] = a2[2 * s + (e >> 2)][e & 3];
+        f2[s].from8(vv);
+      }
+      // ---- attention 1: D3[64][16 px], ReLU
+      f32x4 a3[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a3[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) mma(a3[t], load_w(w3, 16 * t + r, FUS_C, s, g), f2[s]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a3[t][j] = fmaxf(a3[t][j] + b3[16 * t + 4 * g + j], 0.f);
+      }
+      Frag<T> f3[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vv[e] = a3[2 * s + (e >> 2)][e & 3];
+        f3[s].from8(vv);
+      }
+      // ---- attention 2 + sigmoid gate, store NHWC
+      T* orow = att + ((long long)b * HW + (long long)py * W + px) * FUS_C;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) mma(a4, load_w(w4, 16 * t + r, ATT_C, s, g), f3[s]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (pvalid) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ch = 16 * t + 4 * g + j;
+            orow[ch] = Num<T>::from_f(a2[t][j] * sigmoidf_(a4[j] + b4[ch]));
+          }
+        }
+      }
+    }
+  }
+  if constexpr (PHASE < 2) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < NST; c += 256)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        slab[((long long)blockIdx.x * NST + c) * 2 + q] = ((st[0][c][q] + st[1][c][q]) + st[2][c][q]) + st[3][c][q];
+  }
+}
+
+// ------------------------------------------------------------------ conv5: 3x3 128->256
+constexpr int CV_TH = 4, CV_TW = 32;             // 128-pixel tile
+constexpr int CV_PH = CV_TH + 2, CV_PW = CV_TW + 2;
+constexpr int CV_BN = 128;                       // output channels per workgroup
+constexpr int CV_CPAD = 40;                      // 32 channels + 8 pad (80-byte rows)
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_rp_conv3x3(const T* __restrict__ x, int B, int H, int W,
+                                                    const char* __restrict__ blob, Layout L, T* __restrict__ y,
+                                                    float* __restrict__ slab) {
+  // x: NHWC [B][H][W][128]; y: NHWC [B][H][W][256]; slab: [grid][256][2] (sum, sumsq of y)
+  __shared__ T patch[CV_PH * CV_PW][CV_CPAD];
+  __shared__ float st[4][64][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;   // wave tile: 64 px (2 tile rows) x 64 ch
+  const int n0 = blockIdx.y * CV_BN + wn * 64;
+  const T* w5 = (const T*)(blob + L.w5);
+  const float* b5 = (const float*)(blob + L.b5);
+  const int tiles_x = (W + CV_TW - 1) / CV_TW, tiles_y = (H + CV_TH - 1) / CV_TH;
+  const long long ntiles = (long long)B * tiles_x * tiles_y;
+  for (int i = threadIdx.x; i < 4 * 64 * 2; i += 256) (&st[0][0][0])[i] = 0.f;
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
+    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
+    const int y0 = (trem / tiles_x) * CV_TH, x0 = (trem % tiles_x) * CV_TW;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < FUS_C; c0 += 32) {
+      __syncthreads();
+      // stage the 6x34 halo x 32 channels: 204 pixels x 4 chunks of 8 channels
+      for (int i = threadIdx.x; i < CV_PH * CV_PW * 4; i += 256) {
+        const int pp = i >> 2, q = i & 3;
+        const int yy = y0 + pp / CV_PW - 1, xx = x0 + pp % CV_PW - 1;
+        Frag<T> f;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          f.load(x + (((long long)b * H + yy) * W + xx) * FUS_C + c0 + 8 * q);
+        else
+          f.zero();
+        *reinterpret_cast<Frag<T>*>(&patch[pp][8 * q]) = f;
+      }
+      __syncthreads();
+#pragma unroll 1
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+        Frag<T> bf[4];
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj)
+          bf[nj].load(w5 + (long long)(n0 + 16 * nj + r) * (9 * FUS_C) + tap * FUS_C + c0 + 8 * g);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          // rows of this 16-px tile: tile row (wm*2 + mi/2), cols (mi%2)*16 + r
+          const int ty = wm * 2 + (mi >> 1), tx = (mi & 1) * 16 + r;
+          Frag<T> af = *reinterpret_cast<const Frag<T>*>(&patch[(ty + ky) * CV_PW + tx + kx][8 * g]);
+#pragma unroll
+          for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], af, bf[nj]);
+        }
+      }
+    }
+    // epilogue: y = acc + b5 (NHWC), BN partial sums
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      const int n = n0 + 16 * nj + r;
+      const float bias = b5[n];
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int ty = wm * 2 + (mi >> 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int tx = (mi & 1) * 16 + 4 * g + j;
+          const int yy = y0 + ty, xx = x0 + tx;
+          const float v = acc[mi][nj][j] + bias;
+          if (yy < H && xx < W) {
+            const T tv = Num<T>::from_f(v);
+            y[(((long long)b * H + yy) * W + xx) * C5 + n] = tv;
+            const float vr = Num<T>::to_f(tv);  // statistics of the stored values
+            s += vr;
+            q += vr * vr;
+          }
+        }
+      }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (g == 0) {
+        st[wave][16 * nj + r][0] += s;
+        st[wave][16 * nj + r][1] += q;
+      }
+    }
+  }
+  __syncthreads();
+  // waves (wm=0,1) with the same wn own the same 64 channels
+  for (int i = threadIdx.x; i < CV_BN; i += 256) {
+    const int wnn = i / 64, c = i % 64;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      slab[((long long)blockIdx.x * C5 + blockIdx.y * CV_BN + i) * 2 + q] =
+          st[2 * wnn][c][q] + st[2 * wnn + 1][c][q];
+  }
+}
+
+// ------------------------------------------------------------------ BN + ReLU + AdaptiveAvgPool(4)
+constexpr int POOL_SPLIT = 8;  // row chunks per pool region
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y, int H, int W,
+                                                         const float2* __restrict__ aff,
+                                                         float* __restrict__ part) {
+  // grid: (16 regions * POOL_SPLIT, B); thread = channel; part[b][region][split][256]
+  const int b = blockIdx.y, reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
+  const int i = reg / 4, j = reg % 4, c = threadIdx.x;
+  const int ya = (i * H) / 4, yb = ((i + 1) * H + 3) / 4, xa = (j * W) / 4, xb = ((j + 1) * W + 3) / 4;
+  const int rows = yb - ya;
+  const int r0 = ya + (rows * sp) / POOL_SPLIT, r1 = ya + (rows * (sp + 1)) / POOL_SPLIT;
+  const float2 af = aff[c];
+  float s = 0.f;
+  for (int yy = r0; yy < r1; ++yy)
+    for (int xx = xa; xx < xb; ++xx) {
+      const float v = Num<T>::to_f(y[(((long long)b * H + yy) * W + xx) * C5 + c]);
+      s += fmaxf(v * af.x + af.y, 0.f);
+    }
+  part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = s;
+}
+
+// ------------------------------------------------------------------ tail: conv 256->512 on 4x4
+__global__ void k_rp_pool_finish(const float* __restrict__ part, int B, int H, int W, float* __restrict__ pooled) {
+  // pooled[b][256][16] = mean over the region = sum of the split partials / count
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * C5 * 16) return;
+  const int bb = e / (C5 * 16), c = (e / 16) % C5, reg = e % 16;
+  const int i = reg / 4, j = reg % 4;
+  const int cnt = (((i + 1) * H + 3) / 4 - (i * H) / 4) * (((j + 1) * W + 3) / 4 - (j * W) / 4);
+  float s = 0.f;
+  for (int sp = 0; sp < POOL_SPLIT; ++sp) s += part[(((long long)bb * 16 + reg) * POOL_SPLIT + sp) * C5 + c];
+  pooled[e] = s / (float)cnt;
+}
+
+__global__ __launch_bounds__(256) void k_rp_tail_conv(const float* __restrict__ pooled, int B,
+                                                      const char* __restrict__ blob, Layout L,
+                                                      float* __restrict__ z6) {
+  // z6[b][512][16] = conv3x3 pad1 (pooled 4x4) + b6 ; grid.x = 512/8 output-channel groups,
+  // thread = (b, pos) pair (B*16 <= 512 threads handled by a 2-pass loop)
+  const float* w6 = (const float*)(blob + L.w6);
+  const float* b6 = (const float*)(blob + L.b6);
+  const int o0 = blockIdx.x * 8;
+  for (int bp = threadIdx.x; bp < B * 16; bp += 256) {
+    const int bb = bp / 16, pos = bp % 16, py = pos / 4, px = pos % 4;
+    float acc[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) acc[o] = b6[o0 + o];
+    for (int c = 0; c < C5; ++c)
+      for (int ky = 0; ky < 3; ++ky) {
+        const int yy = py + ky - 1;
+        if (yy < 0 || yy >= 4) continue;
+        for (int kx = 0; kx < 3; ++kx) {
+          const int xx = px + kx - 1;
+          if (xx < 0 || xx >= 4) continue;
+          const float v = pooled[((long long)bb * C5 + c) * 16 + yy * 4 + xx];
+#pragma unroll
+          for (int o = 0; o < 8; ++o) acc[o] += w6[(((long long)(o0 + o) * C5 + c) * 3 + ky) * 3 + kx] * v;
+        }
+      }
+#pragma unroll
+    for (int o = 0; o < 8; ++o) z6[((long long)bb * C6 + o0 + o) * 16 + pos] = acc[o];
+  }
+}
+
+__device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned long long idx) {
+  unsigned long long z = seed + idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// BN(512, batch or running stats) + ReLU + GAP + MLP + sigmoid; one workgroup
+__global__ __launch_bounds__(512) void k_rp_tail_mlp(const float* __restrict__ z6, int B, int training,
+                                                     float momentum, const char* __restrict__ blob, Layout L,
+                                                     BnPtrs bn, unsigned long long seed,
+                                                     float* __restrict__ ratio) {
+  __shared__ float feat[32][C6];
+  __shared__ float h1[32][128], h2[32][64], h3[32][32];
+  const int c = threadIdx.x;  // 512 threads = channels
+  {
+    float* gamma = bn.p[5 * 4 + 0];
+    float* beta = bn.p[5 * 4 + 1];
+    float* rm = bn.p[5 * 4 + 2];
+    float* rv = bn.p[5 * 4 + 3];
+    float mean, var;
+    if (training) {
+      double s = 0.0, q = 0.0;
+      for (int bb = 0; bb < B; ++bb)
+        for (int p = 0; p < 16; ++p) {
+          const double v = z6[((long long)bb * C6 + c) * 16 + p];
+          s += v;
+          q += v * v;
+        }
+      const double n = 16.0 * B, m = s / n;
+      double v = q / n - m * m;
+      if (v < 0.0) v = 0.0;
+      mean = (float)m;
+      var = (float)v;
+      const double unb = n > 1.0 ? v * n / (n - 1.0) : v;
+      rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
+      rv[c] = (1.f - momentum) * rv[c] + momentum * (float)unb;
+    } else {
+      mean = rm[c];
+      var = rv[c];
+    }
+    const float sc = gamma[c] / sqrtf(var + BN_EPS), sh = beta[c] - mean * sc;
+    for (int bb = 0; bb < B; ++bb) {
+      float s = 0.f;
+      for (int p = 0; p < 16; ++p) s += fmaxf(z6[((long long)bb * C6 + c) * 16 + p] * sc + sh, 0.f);
+      feat[bb][c] = s / 16.f;  // AdaptiveAvgPool2d(1)
+    }
+  }
+  __syncthreads();
+  const float* w7 = (const float*)(blob + L.w7);
+  const float* b7 = (const float*)(blob + L.b7);
+  const float* w8 = (const float*)(blob + L.w8);
+  const float* b8 = (const float*)(blob + L.b8);
+  const float* w9 = (const float*)(blob + L.w9);
+  const float* b9 = (const float*)(blob + L.b9);
+  const float* w10 = (const float*)(blob + L.w10);
+  const float* b10 = (const float*)(blob + L.b10);
+  for (int e = threadIdx.x; e < B * 128; e += 512) {
+    const int bb = e / 128, o = e % 128;
+    float s = b7[o];
+    for (int k = 0; k < 512; ++k) s += w7[o * 512 + k] * feat[bb][k];
+    s = fmaxf(s, 0.f);
+    if (training) s = hash_uniform(seed, e) < 0.3f ? 0.f : s / 0.7f;  // Dropout(0.3)
+    h1[bb][o] = s;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < B * 64; e += 512) {
+    const int bb = e / 64, o = e % 64;
+    float s = b8[o];
+    for (int k = 0; k < 128; ++k) s += w8[o * 128 + k] * h1[bb][k];
+    s = fmaxf(s, 0.f);
+    if (training) s = hash_uniform(seed ^ 0x5555ull, e) < 0.2f ? 0.f : s / 0.8f;  // Dropout(0.2)
+    h2[bb][o] = s;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < B * 32; e += 512) {
+    const int bb = e / 32, o = e % 32;
+    float s = b9[o];
+    for (int k = 0; k < 64; ++k) s += w9[o * 64 + k] * h2[bb][k];
+    h3[bb][o] = fmaxf(s, 0.f);
+  }
+  __syncthreads();
+  if (threadIdx.x < B) {
+    const int bb = threadIdx.x;
+    float s = b10[0];
+    for (int k = 0; k < 32; ++k) s += w10[k] * h3[bb][k];
+    ratio[bb] = 0.01f + (0.5f - 0.01f) * (1.f / (1.f + expf(-s)));
+  }
+}
+
+struct Ws {  // workspace carve
+  size_t aff1, aff2, aff5, slab, att, y, part, pooled, z6, total;
+};
+
+inline int chain_grid(int B, int H, int W) {
+  const long long nt = (long long)B * ((W + CH_TW - 1) / CH_TW) * ((H + CH_TH - 1) / CH_TH);
+  return (int)std::min<long long>(nt, 2048);
+}
+inline int conv_grid(int B, int H, int W) {
+  const long long nt = (long long)B * ((W + CV_TW - 1) / CV_TW) * ((H + CV_TH - 1) / CV_TH);
+  return (int)std::min<long long>(nt, 1024);
+}
+
+inline Ws make_ws(int es, int B, int H, int W) {
+  Ws w;
+  size_t o = 0;
+  auto seg = [&](size_t bytes) {
+    size_t r = o;
+    o += align256(bytes);
+    return r;
+  };
+  const size_t P = (size_t)B * H * W;
+  const int slab_rows = std::max(chain_grid(B, H, W), conv_grid(B, H, W));
+  w.aff1 = seg(STEM_C * sizeof(float2));
+  w.aff2 = seg(FUS_C * sizeof(float2));
+  w.aff5 = seg(C5 * sizeof(float2));
+  w.slab = seg((size_t)slab_rows * C5 * 2 * sizeof(float));
+  w.att = seg(P * FUS_C * es);
+  w.y = seg(P * C5 * es);
+  w.part = seg((size_t)B * 16 * POOL_SPLIT * C5 * sizeof(float));
+  w.pooled = seg((size_t)B * C5 * 16 * sizeof(float));
+  w.z6 = seg((size_t)B * C6 * 16 * sizeof(float));
+  w.total = o;
+  return w;
+}
+
+template <typename T>
+int ratio_forward(int training, float momentum, const float* depth3, long long bstride, int B, int H, int W,
+                  const char* blob, const BnPtrs& bn, unsigned long long seed, float* ratio, char* ws,
+                  hipStream_t s) {
+  const Layout L = make_layout(sizeof(T));
+  const Ws w = make_ws(sizeof(T), B, H, W);
+  float2* aff1 = (float2*)(ws + w.aff1);
+  float2* aff2 = (float2*)(ws + w.aff2);
+  float2* aff5 = (float2*)(ws + w.aff5);
+  float* slab = (float*)(ws + w.slab);
+  T* att = (T*)(ws + w.att);
+  T* y = (T*)(ws + w.y);
+  float* part = (float*)(ws + w.part);
+  float* pooled = (float*)(ws + w.pooled);
+  float* z6 = (float*)(ws + w.z6);
+  const double P = (double)B * H * W;
+  const int gch = chain_grid(B, H, W);
+  // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
+  if (training)
+    k_rp_chain<T, 0><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, nullptr, nullptr, slab, nullptr);
+  for (int l = 0; l < 3; ++l)
+    k_bn_affine<<<1, 64, 0, s>>>(slab, gch, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
+                                 bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
+  // fusion BN
+  if (training)
+    k_rp_chain<T, 1><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, aff1, nullptr, slab, nullptr);
+  k_bn_affine<<<1, 128, 0, s>>>(slab, gch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
+                                bn.p[15], aff2);
+  // gated attention features
+  k_rp_chain<T, 2><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, aff1, aff2, nullptr, att);
+  // conv5 + its BN statistics
+  const int gcv = conv_grid(B, H, W);
+  k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
+  k_bn_affine<<<1, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
+                                bn.p[19], aff5);
+  k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), C5, 0, s>>>(y, H, W, aff5, part);
+  k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
+  k_rp_tail_conv<<<C6 / 8, 256, 0, s>>>(pooled, B, blob, L, z6);
+  k_rp_tail_mlp<<<1, 512, 0, s>>>(z6, B, training, momentum, blob, L, bn, seed, ratio);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t rgbd_ratio_packed_size(int dtype) { return make_layout(dtype == RGBD_BF16 ? 2 : 4).total; }
+
+int rgbd_ratio_pack(int dtype, const float* const* weights_host, void* packed, void* stream) {
+  RGBD_REQUIRE(weights_host && packed, RGBD_E_ARG);
+  WPtrs w;
+  for (int i = 0; i < RGBD_RATIO_NW; ++i) {
+    RGBD_REQUIRE(weights_host[i], RGBD_E_ARG);
+    w.p[i] = weights_host[i];
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_F32)
+    k_rp_pack<float><<<1024, 256, 0, s>>>(w, (char*)packed, make_layout(4));
+  else if (dtype == RGBD_BF16)
+    k_rp_pack<bf16_t><<<1024, 256, 0, s>>>(w, (char*)packed, make_layout(2));
+  else
+    return RGBD_E_DTYPE;
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W) {
+  return make_ws(dtype == RGBD_BF16 ? 2 : 4, B > 0 ? B : 1, H > 0 ? H : 1, W > 0 ? W : 1).total;
+}
+
+int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
+                       int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
+                       float* ratio, void* ws, void* stream) {
+  RGBD_REQUIRE(depth3 && packed && bn_host && ratio && ws, RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(B <= 32, RGBD_E_SHAPE);  // one workgroup runs the batch-wide tail (BN over B*16)
+  BnPtrs bn;
+  for (int i = 0; i < RGBD_RATIO_NBN * 4; ++i) {
+    RGBD_REQUIRE(bn_host[i], RGBD_E_ARG);
+    bn.p[i] = bn_host[i];
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_F32)
+    return ratio_forward<float>(training, momentum, depth3, batch_stride, B, H, W, (const char*)packed, bn, seed,
+                                ratio, (char*)ws, s);
+  if (dtype == RGBD_BF16)
+    return ratio_forward<bf16_t>(training, momentum, depth3, batch_stride, B, H, W, (const char*)packed, bn, seed,
+                                 ratio, (char*)ws, s);
+  return RGBD_E_DTYPE;
+}
+
+}  // extern "C"

@@ -1,0 +1,114 @@
+"""Drop-in replacements for the reference model classes (mask2former/utils/custom_model.py:18-53,
+56-143, 324-390), with the v0.4.0 pixel-level body running on the HIP kernels.
+
+Same class names, constructor signatures (``version`` kwarg), ``config_class``,
+``main_input_name``, forward signatures, output dataclass and state_dict keys, so a
+checkpoint of the reference loads unchanged.  Everything outside the hot path (Swin
+encoder, MSDeformAttn pixel decoder, masked-attention transformer decoder, loss) is the
+installed Hugging Face Mask2Former, exactly as in the reference (SURVEY §8(f) rows are the
+next milestones).
+"""
+import random
+
+import numpy as np
+import torch
+from torch import Tensor
+from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation, Mask2FormerModel
+from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
+                                                                  Mask2FormerPixelLevelModuleOutput)
+
+from .hot_path import hot_path
+from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
+
+SUPPORTED_VERSIONS = ("0.4.0", "0.0.0")
+
+
+def set_seed(seed=42):
+    """custom_model.py:18-25."""
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+
+
+class CustomConfig(Mask2FormerConfig):
+    model_type = "mask2former"
+
+    def __init__(self, attribute=1, **kwargs):
+        self.attribute = attribute
+        super().__init__(**kwargs)
+
+
+class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
+    """v0.4.0: 10-channel input (RGB, depth x3, DGGM gradient x3, DGGM mask); version 0.0.0:
+    plain RGB (the baseline branch, custom_model.py:145-146)."""
+    main_input_name = "pixel_values"
+
+    def __init__(self, config, version):
+        super().__init__(config)
+        if version not in SUPPORTED_VERSIONS:
+            raise NotImplementedError(
+                f"version {version!r}: only the paper model 0.4.0 (and the RGB baseline 0.0.0) are built "
+                "MI355X-native; the abandoned variants of custom_model.py are out of scope (SURVEY §2 row 1x)")
+        self.version = version
+        # bf16 MFMA for the DSAM / ratio-predictor GEMMs; float32 is the exact parity mode
+        self.compute_dtype = torch.float32
+        if version == "0.4.0":
+            self.ratio_predictor = EnhancedDepthImageRatioPredictor(3)
+            self.dsam0 = DSAModule(in_channels=96, out_channels=192, num_depth_regions=3)
+            self.dsam1 = DSAModule(in_channels=192, out_channels=384, num_depth_regions=3)
+            self.dsam2 = DSAModule(in_channels=384, out_channels=768, num_depth_regions=3)
+            self.depth_gradient_injection = DepthGradientInjectionResidual([96, 192, 384, 768], 3)
+
+    def set_compute_dtype(self, dtype):
+        self.compute_dtype = dtype
+        for m in self.modules():
+            if hasattr(m, "compute_dtype"):
+                m.compute_dtype = dtype
+        return self
+
+    def hot_path_features(self, pixel_values: Tensor, color_feature_map, ratios=None):
+        """custom_model.py:325-355 on the HIP kernels: returns the 4 backbone features."""
+        if ratios is None:
+            ratios = self.ratio_predictor(pixel_values[:, 3:6])       # :336 (no grad, Q2)
+        feats = hot_path(pixel_values, ratios, list(color_feature_map), [self.dsam0, self.dsam1, self.dsam2],
+                         self.depth_gradient_injection, dtype=self.compute_dtype)
+        dt = color_feature_map[0].dtype
+        return [f.to(dt) for f in feats]
+
+    def forward(self, pixel_values: Tensor, output_hidden_states: bool = False) -> Mask2FormerPixelLevelModuleOutput:
+        if self.version == "0.0.0":
+            backbone_features = list(self.encoder(pixel_values).feature_maps)
+        else:
+            rgb = pixel_values[:, 0:3, :, :]
+            color_feature_map = self.encoder(rgb).feature_maps          # :330 (Swin, HF)
+            backbone_features = self.hot_path_features(pixel_values, color_feature_map)
+        decoder_output = self.decoder(backbone_features, output_hidden_states=output_hidden_states)
+        return Mask2FormerPixelLevelModuleOutput(
+            encoder_last_hidden_state=backbone_features[-1],
+            encoder_hidden_states=tuple(backbone_features) if output_hidden_states else None,
+            decoder_last_hidden_state=decoder_output.mask_features,
+            decoder_hidden_states=decoder_output.multi_scale_features,
+        )
+
+
+class CustomMask2FormerModel(Mask2FormerModel):
+    main_input_name = "pixel_values"
+
+    def __init__(self, config, version):
+        super().__init__(config)
+        self.pixel_level_module = CustomMask2FormerPixelLevelModule(config, version=version)
+
+
+class CustomMask2FormerForUniversalSegmentation(Mask2FormerForUniversalSegmentation):
+    main_input_name = "pixel_values"
+    config_class = CustomConfig
+
+    def __init__(self, config, version="0.0.0"):
+        super().__init__(config)
+        set_seed(42)                                                    # Q17: after HF init
+        self.model = CustomMask2FormerModel(config, version=version)
+
+    def set_compute_dtype(self, dtype):
+        self.model.pixel_level_module.set_compute_dtype(dtype)
+        return self

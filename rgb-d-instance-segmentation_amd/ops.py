@@ -53,6 +53,8 @@ def _workspace(dev, nbytes: int, tag: str):
 def assemble_pixel_values(depth_u8: torch.Tensor, rgb_u8: torch.Tensor = None, out: torch.Tensor = None):
     """depth_u8 [B,H,W] uint8 (+ rgb_u8 [B,H,W,3]) -> pixel_values float32 [B,10,H,W]
     (map_10channel_case2 layout, dataloader.py:386-425; DGGM-pre data_process.py:1247-1305)."""
+    depth_u8 = depth_u8.contiguous()
+    rgb_u8 = None if rgb_u8 is None else rgb_u8.contiguous()
     _need_cuda(depth_u8, rgb_u8)
     if depth_u8.dtype != torch.uint8 or depth_u8.dim() != 3:
         raise ValueError("depth_u8 must be uint8 [B,H,W]")

@@ -1,0 +1,90 @@
+"""Host side of K4, the EnhancedDepthImageRatioPredictor forward (custom_model.py:1444-1487).
+
+The predictor never receives gradients in v0.4.0 (its output leaves autograd through
+``.item()``, custom_model.py:339-351, quirk Q2), so the forward is a plain device call that
+returns a float32 [B,1] tensor on the GPU; nothing is synchronised.  Weights are packed once
+per parameter version; BatchNorm buffers are read (eval) or updated in place (train) by the
+kernels through raw pointers.
+"""
+import ctypes
+import itertools
+
+import torch
+
+from . import _lib
+from ._lib import check
+from .ops import _dtype_code, _p, _stream, _workspace
+
+_W_KEYS = ["scale1_conv.0", "scale2_conv.0", "scale3_conv.0", "feature_fusion.0", "attention.0", "attention.2",
+           "feature_extractor.0", "feature_extractor.4", "fc_layers.0", "fc_layers.3", "fc_layers.6", "fc_layers.8"]
+_BN_KEYS = ["scale1_conv.1", "scale2_conv.1", "scale3_conv.1", "feature_fusion.1", "feature_extractor.1",
+            "feature_extractor.5"]
+_seed_counter = itertools.count(1)
+
+
+def _weights(module):
+    mods = dict(module.named_modules())
+    out = []
+    for k in _W_KEYS:
+        out += [mods[k].weight, mods[k].bias]
+    return out
+
+
+def _bns(module):
+    mods = dict(module.named_modules())
+    return [mods[k] for k in _BN_KEYS]
+
+
+def _packed(module, dtype):
+    ws = _weights(module)
+    key = (dtype,) + tuple((w.data_ptr(), w._version) for w in ws)
+    cache = getattr(module, "_rgbd_pack", None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    dev = ws[0].device
+    L = _lib.lib()
+    code = 1 if dtype == torch.bfloat16 else 0
+    blob = torch.empty(L.rgbd_ratio_packed_size(code), dtype=torch.uint8, device=dev)
+    src = [w.detach().float().contiguous() for w in ws]
+    arr = (ctypes.c_void_p * len(src))(*[t.data_ptr() for t in src])
+    check(L.rgbd_ratio_pack(code, arr, _p(blob), _stream(dev)), "rgbd_ratio_pack")
+    module._rgbd_pack = (key, blob, src)  # keep the float32 copies alive until the pack ran
+    return blob
+
+
+def ratio_predictor_forward(module, depth_image: torch.Tensor) -> torch.Tensor:
+    """depth_image: [B,3,H,W] (may be the pixel_values[:,3:6] view) -> ratio float32 [B,1]."""
+    if not depth_image.is_cuda:
+        raise RuntimeError("rgbd_amd ops run on the GPU only (no CPU fallback); got a CPU tensor")
+    d = depth_image.detach()
+    if d.dtype != torch.float32:
+        d = d.float()
+    if d.stride(1) != d.shape[2] * d.shape[3] or d.stride(3) != 1 or d.stride(2) != d.shape[3]:
+        d = d.contiguous()
+    B, _, H, W = d.shape
+    dtype = module.compute_dtype
+    blob = _packed(module, dtype)
+    bns = _bns(module)
+    for bn in bns:
+        for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var):
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError("BatchNorm parameters/buffers must be contiguous float32")
+    ptrs = []
+    for bn in bns:
+        ptrs += [bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr()]
+    bn_arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    training = bool(module.training)
+    momentum = bns[0].momentum if bns[0].momentum is not None else 0.1
+    ratio = torch.empty((B,), dtype=torch.float32, device=d.device)
+    L = _lib.lib()
+    code = _dtype_code(torch.empty(0, dtype=dtype))
+    ws = _workspace(d.device, L.rgbd_ratio_workspace_size(code, B, H, W), "ratio")
+    seed = (torch.initial_seed() * 1000003 + next(_seed_counter)) & 0xFFFFFFFFFFFF
+    check(L.rgbd_ratio_forward(code, int(training), ctypes.c_float(momentum), ctypes.c_void_p(d.data_ptr()),
+                               d.stride(0), B, H, W, _p(blob), bn_arr, ctypes.c_ulonglong(seed), _p(ratio), _p(ws),
+                               _stream(d.device)), "rgbd_ratio_forward")
+    if training:
+        with torch.no_grad():
+            for bn in bns:
+                bn.num_batches_tracked.add_(1)
+    return ratio.reshape(B, 1)

@@ -188,6 +188,7 @@ def main():
     pv2 = golden_inputs.pixel_values(6, 2, 240, 320)
     labels = golden_inputs.labels(6, 2, 240, 320)
     model.zero_grad()
+    torch.manual_seed(1234)  # the loss samples points with torch.rand (importance sampling)
     out = model(pixel_values=torch.from_numpy(pv2),
                 mask_labels=[torch.from_numpy(m) for m in labels[0]],
                 class_labels=[torch.from_numpy(c) for c in labels[1]])
@@ -211,10 +212,19 @@ def main():
 
 
 def build_model(cm):
-    from transformers import Mask2FormerConfig  # noqa: F401
-    cfg = cm.CustomConfig.from_pretrained(f"{REF}/mask2former/checkpoints/standard",
-                                          **golden_inputs.label_kwargs())
+    """Reference model on the restated config (rgbd_amd.config), after checking that the
+    restatement builds exactly the parameter shapes of the reference's standard config."""
+    from rgbd_amd.config import standard_config
+    ref_cfg = cm.CustomConfig.from_pretrained(f"{REF}/mask2former/checkpoints/standard",
+                                              **golden_inputs.label_kwargs())
+    cfg = standard_config(48)
     model = cm.CustomMask2FormerForUniversalSegmentation(cfg, version="0.4.0")
+    ref_model = cm.CustomMask2FormerForUniversalSegmentation(ref_cfg, version="0.4.0")
+    a = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    b = {k: tuple(v.shape) for k, v in ref_model.state_dict().items()}
+    assert a == b, "restated config differs from checkpoints/standard/config.json"
+    assert cfg.backbone_config.drop_path_rate == ref_cfg.backbone_config.drop_path_rate
+    del ref_model
     winit.init_deterministic(model)
     return model
 

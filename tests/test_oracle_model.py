@@ -1,0 +1,77 @@
+"""Pins the oracle's composition (ratio predictor + decomposition + DSAM cascade + DGGM,
+custom_model.py:324-355) and the drop-in model's module tree against G5 / G6, the full
+reference model run in the build container: the drop-in model is run on the CPU with its
+hot path replaced by the oracle (test-only monkeypatch; the product has no CPU path)."""
+import numpy as np
+import pytest
+import torch
+
+import golden_inputs as gi
+from oracle import hot_path as hot_o
+from rgbd_amd import init as winit
+
+pytestmark = pytest.mark.slow
+
+
+def _model():
+    from rgbd_amd.config import standard_config
+    from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
+    m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
+    missing = winit.init_deterministic(m)
+    assert not missing.unexpected_keys
+    return m
+
+
+def _oracle_hot(plm, captured):
+    sd = {k: v for k, v in plm.state_dict().items()}
+    named = dict(plm.named_parameters())
+    sd.update(named)  # parameters as leaves so grads flow (G6)
+
+    def hot(pixel_values, color_feature_map, ratios=None):
+        feats, r, _ = hot_o.hot_path_forward(list(color_feature_map), pixel_values, sd, training=False)
+        captured["ratio"] = r
+        return feats
+    return hot
+
+
+def test_state_dict_keys_match_reference_layout():
+    from rgbd_amd import params
+    m = _model()
+    keys = set(m.state_dict())
+    for k in params.hot_path_shapes():
+        assert params.PLM_PREFIX + k in keys, k
+
+
+def test_oracle_full_model_matches_g5(golden):
+    g5 = golden("g5_model")
+    m = _model().eval()
+    cap = {}
+    m.model.pixel_level_module.hot_path_features = _oracle_hot(m.model.pixel_level_module, cap)
+    pv = gi.pixel_values(1, 1, 240, 320)
+    import hashlib
+    assert hashlib.sha256(pv.tobytes()).hexdigest() == str(g5["input_sha"])
+    with torch.no_grad():
+        out = m(pixel_values=torch.from_numpy(pv))
+    np.testing.assert_allclose(cap["ratio"].numpy(), g5["ratio"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(out.masks_queries_logits.numpy(), g5["mask_logits"], atol=1e-3, rtol=1e-4)
+
+
+def test_oracle_grads_match_g6(golden):
+    g6 = golden("g6_grads")
+    m = _model().eval()
+    m.model.pixel_level_module.hot_path_features = _oracle_hot(m.model.pixel_level_module, {})
+    pv = gi.pixel_values(6, 2, 240, 320)
+    masks, classes = gi.labels(6, 2, 240, 320)
+    torch.manual_seed(1234)
+    out = m(pixel_values=torch.from_numpy(pv), mask_labels=[torch.from_numpy(x) for x in masks],
+            class_labels=[torch.from_numpy(c) for c in classes])
+    np.testing.assert_allclose(out.loss.item(), float(g6["loss"]), rtol=1e-5)
+    out.loss.backward()
+    named = dict(m.named_parameters())
+    for n in g6["names"]:
+        n = str(n)
+        g = named[n].grad.numpy().ravel()
+        ref_norm = float(g6[n + "|norm"])
+        assert abs(np.linalg.norm(g.astype(np.float64)) - ref_norm) <= 1e-3 * ref_norm + 1e-9, n
+        np.testing.assert_allclose(g[g6[n + "|idx"]], g6[n + "|val"], rtol=1e-3, atol=1e-3 * (ref_norm / np.sqrt(g.size) + 1e-12))
