@@ -162,6 +162,15 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        float* ratio, void* ws, void* stream);
 
+/* ---------------------------------------------------------------- kernel timing (bench only)
+ * When enabled, launch functions bracket their main kernel with hipEvents recorded on the
+ * launch stream; rgbd_timing_read synchronises those events and returns the summed
+ * milliseconds and launch count for one kernel name ("rp_conv3x3", "rp_chain", "dsam_fwd",
+ * "dsam_dx", "dsam_wgrad", "decompose", "dggm_fwd", "dggm_bwd", "assemble"), then resets.
+ * Do not enable while a stream is being captured into a graph. */
+int rgbd_timing_enable(int on);
+double rgbd_timing_read(const char* name, int* count);
+
 #ifdef __cplusplus
 }
 #endif

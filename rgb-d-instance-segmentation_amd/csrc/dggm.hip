@@ -10,6 +10,7 @@
 // pixel and walks a channel chunk, so the resampled gate (3 bilinear taps x 4 + 1 nearest) is
 // computed once per pixel and the NCHW planes are streamed with coalesced accesses.
 #include "common.hpp"
+#include "timing.hpp"
 
 using namespace rgbd;
 
@@ -236,6 +237,7 @@ int rgbd_assemble_pixel_values(const uint8_t* rgb_u8, const uint8_t* depth_u8, i
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   PrepWs* w = (PrepWs*)ws;
+  TimerScope ts("assemble", s);
   k_prep_init<<<ceil_div(B, 64), 64, 0, s>>>(w, B);
   const long long HW = (long long)H * W;
   dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 1024), B);
@@ -253,6 +255,7 @@ int rgbd_dggm_fuse_fwd(int dtype, const void* cp1, const void* color, const floa
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0 && h > 0 && w > 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(ceil_div((long long)h * w, 256), ceil_div(C, kFuseCh), B);
+  TimerScope ts("dggm_fwd", s);
   if (dtype == RGBD_F32)
     k_dggm_fuse_fwd<float><<<grid, 256, 0, s>>>((const float*)cp1, (const float*)color, grad, mask,
                                                 pv_batch_stride, H, W, C, h, w, weight, bias, (float*)out);
@@ -279,6 +282,7 @@ int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const flo
   RGBD_REQUIRE(dout && grad && mask && weight && bias && dweight && dbias && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0 && h > 0 && w > 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
+  TimerScope ts("dggm_bwd", s);
   const int ntiles = dggm_bwd_tiles(B, h, w);
   dim3 grid(ntiles, ceil_div(C, kFuseCh));
   float* partial = (float*)ws;

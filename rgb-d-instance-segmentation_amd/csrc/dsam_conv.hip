@@ -18,6 +18,7 @@
 // mask bit is taken at the OUTPUT pixel (d(x*m)/dx = m).  dW contracts over pixels with an
 // LDS-staged im2col tile.
 #include "mfma.hpp"
+#include "timing.hpp"
 
 using namespace rgbd;
 
@@ -359,6 +360,7 @@ __global__ void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_deco
 
 template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
+  TimerScope ts(a.transposed ? "dsam_dx" : "dsam_fwd", s);
   int nclass = a.transposed ? 4 : 1;
   long long Mmax = (long long)a.B * a.Ho * a.Wo;
   if (a.transposed) Mmax = (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2);
@@ -464,6 +466,7 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, c
   const int sp = dsam_wgrad_splits(B, Cin, Cout);
   float* partial = (float*)ws;
   float* csum = (float*)((char*)ws + align256(sizeof(float) * (size_t)sp * Cout * 45 * Cin));
+  TimerScope ts("dsam_wgrad", s);
   dim3 grid(ceil_div(45ll * Cin, 64), ceil_div(Cout, 64), sp);
   const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
   if (dtype == RGBD_F32) {

@@ -17,6 +17,7 @@
 // Every float op that feeds a discrete decision uses an explicitly rounded intrinsic, so the
 // result is bit-exact to the numpy 2.2 / scipy 1.15 reference.
 #include "common.hpp"
+#include "timing.hpp"
 
 using namespace rgbd;
 
@@ -310,6 +311,7 @@ int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_
   hipStream_t st = (hipStream_t)stream;
   DecWs* w = (DecWs*)ws;
   const long long HW = (long long)H * W;
+  TimerScope ts("decompose", st);
   k_init<<<B, 256, 0, st>>>(w, info, B);
   dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 512), B);
   k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w);

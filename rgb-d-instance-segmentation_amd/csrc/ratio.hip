@@ -21,6 +21,7 @@
 // deterministic fixed-order reductions in double) and updates running stats like torch
 // (momentum, unbiased variance).  Dropout uses a counter-hash RNG (train mode only).
 #include "mfma.hpp"
+#include "timing.hpp"
 
 using namespace rgbd;
 
@@ -700,10 +701,16 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   k_bn_affine<<<1, 128, 0, s>>>(slab, gch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
                                 bn.p[15], aff2);
   // gated attention features
-  k_rp_chain<T, 2><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, aff1, aff2, nullptr, att);
+  {
+    TimerScope ts("rp_chain", s);
+    k_rp_chain<T, 2><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, aff1, aff2, nullptr, att);
+  }
   // conv5 + its BN statistics
   const int gcv = conv_grid(B, H, W);
-  k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
+  {
+    TimerScope ts("rp_conv3x3", s);
+    k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
+  }
   k_bn_affine<<<1, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
                                 bn.p[19], aff5);
   k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), C5, 0, s>>>(y, H, W, aff5, part);
