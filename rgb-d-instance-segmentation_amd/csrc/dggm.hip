@@ -53,8 +53,8 @@ __global__ __launch_bounds__(256) void k_prep_pass1(const uint8_t* __restrict__ 
   const uint8_t* d = depth + b * HW;
   float* out = pv + b * 10 * HW;
   float vmax = 0.f, vmin = __uint_as_float(0x7f800000u);
-  for (long long p = blockIdx.x * 256ll + threadIdx.x; p < HW; p += 256ll * gridDim.x) {
-    const int y = (int)(p / W), x = (int)(p % W);
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < (int)HW; p += 256 * gridDim.x) {
+    const int y = p / W, x = p % W;
     const uint8_t dv = d[p];
     if (rgb) {
       const uint8_t* px = rgb + (b * HW + p) * 3;
@@ -75,9 +75,15 @@ __global__ __launch_bounds__(256) void k_prep_pass1(const uint8_t* __restrict__ 
   }
   vmax = -wave_min(-vmax);
   vmin = wave_min(vmin);
+  __shared__ float rmax[4], rmin[4];
   if ((threadIdx.x & 63) == 0) {
-    atomicMax(&ws[b].max_bits, __float_as_uint(vmax));
-    atomicMin(&ws[b].min_bits, __float_as_uint(vmin));
+    rmax[threadIdx.x >> 6] = vmax;
+    rmin[threadIdx.x >> 6] = vmin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // one atomic pair per block (same-address atomics serialise)
+    atomicMax(&ws[b].max_bits, __float_as_uint(fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]))));
+    atomicMin(&ws[b].min_bits, __float_as_uint(fminf(fminf(rmin[0], rmin[1]), fminf(rmin[2], rmin[3]))));
   }
 }
 
@@ -212,17 +218,25 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_bwd_partial(const T* __restri
   }
 }
 
-__global__ void k_dggm_fuse_bwd_final(const float* __restrict__ partial, int ntiles, int C,
-                                      float* __restrict__ dw, float* __restrict__ db) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // (c, j)
-  if (t >= C * 4) return;
+__global__ __launch_bounds__(256) void k_dggm_fuse_bwd_final(const float* __restrict__ partial, int ntiles, int C,
+                                                              float* __restrict__ dw, float* __restrict__ db) {
+  // one block per (c, j); fixed-shape tree over the tiles: deterministic
+  __shared__ float red[256];
+  const int t = blockIdx.x;
   float s = 0.f;
-  for (int i = 0; i < ntiles; ++i) s += partial[(long long)i * C * 4 + t];  // fixed order
+  for (int i = threadIdx.x; i < ntiles; i += 256) s += partial[(long long)i * C * 4 + t];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x) return;
   const int c = t >> 2, j = t & 3;
   if (j == 0)
-    db[c] = s;
+    db[c] = red[0];
   else
-    dw[c * 3 + (j - 1)] = s;
+    dw[c * 3 + (j - 1)] = red[0];
 }
 
 }  // namespace
@@ -240,7 +254,8 @@ int rgbd_assemble_pixel_values(const uint8_t* rgb_u8, const uint8_t* depth_u8, i
   TimerScope ts("assemble", s);
   k_prep_init<<<ceil_div(B, 64), 64, 0, s>>>(w, B);
   const long long HW = (long long)H * W;
-  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 1024), B);
+  RGBD_REQUIRE(HW < (1ll << 31), RGBD_E_SHAPE);
+  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 128), B);
   k_prep_pass1<<<grid, 256, 0, s>>>(rgb_u8, depth_u8, H, W, pv, w);
   k_prep_pass2<<<grid, 256, 0, s>>>(H, W, pv, w);
   RGBD_CHECK_LAUNCH();
@@ -294,7 +309,7 @@ int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const flo
                                                          B, H, W, C, h, w, weight, bias, partial);
   else
     return RGBD_E_DTYPE;
-  k_dggm_fuse_bwd_final<<<ceil_div(C * 4, 256), 256, 0, s>>>(partial, ntiles, C, dweight, dbias);
+  k_dggm_fuse_bwd_final<<<C * 4, 256, 0, s>>>(partial, ntiles, C, dweight, dbias);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -316,6 +316,116 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, 
     }
 }
 
+// bf16 dW: X tile staged [px][kk] from NHWC with 16-byte loads, read back transposed with
+// ds_read_b64_tr_b16 (gfx950) as the MFMA B operand (8 consecutive pixels per lane); the A
+// operand (G^T, 8 consecutive pixels of one channel) is a direct 16-byte load from NCHW.
+constexpr int WG_KK = 128, WG_O = 64, PXC = 32, XPAD = 136;
+typedef __attribute__((ext_vector_type(4))) short v4s;
+
+__global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restrict__ gout, const bf16_t* __restrict__ x,
+                                                         const uint8_t* __restrict__ code, int B, int Cin, int h,
+                                                         int w, int Cout, int splits, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][PXC][XPAD];
+  const int ho = (h + 1) / 2, wo = (w + 1) / 2;
+  const int hwo = ho * wo;
+  const int KK = 45 * Cin;
+  const int kk0 = blockIdx.x * WG_KK, o0 = blockIdx.y * WG_O, z = blockIdx.z;
+  const int b0 = (int)((long long)z * B / splits), b1 = (int)((long long)(z + 1) * B / splits);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  // staging role: pixel row spx, two 8-channel chunks at kk0 + 16*skg + 8*q
+  const int spx = threadIdx.x >> 3, skg = threadIdx.x & 7;
+  int s_seg[2], s_ky[2], s_kx[2], s_c[2];
+  bool s_ok[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int kk = kk0 + 16 * skg + 8 * q;
+    s_ok[q] = kk < KK;
+    const int k2 = s_ok[q] ? kk : 0;
+    s_seg[q] = k2 / (9 * Cin);
+    const int tap = (k2 / Cin) % 9;
+    s_ky[q] = tap / 3;
+    s_kx[q] = tap % 3;
+    s_c[q] = k2 % Cin;
+  }
+  auto stage = [&](int buf, int b, int p0) {
+    const int p = p0 + spx;
+    const int oy = p / wo, ox = p % wo;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int iy = 2 * oy - 1 + s_ky[q], ix = 2 * ox - 1 + s_kx[q];
+      bool ok = s_ok[q] && p < hwo && iy >= 0 && iy < h && ix >= 0 && ix < w;
+      const long long pix = ((long long)b * h + iy) * w + ix;
+      if (ok && s_seg[q] < 4) ok = (code[pix] >> s_seg[q]) & 1u;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (ok) v = *reinterpret_cast<const uint4*>(x + pix * Cin + s_c[q]);
+      *reinterpret_cast<uint4*>(&Xs[buf][spx][16 * skg + 8 * q]) = v;
+    }
+  };
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nchunk = (hwo + PXC - 1) / PXC;
+  const int total = (b1 - b0) * nchunk;
+  if (total > 0) stage(0, b0, 0);
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    const int b = b0 + it / nchunk, p0 = (it % nchunk) * PXC;
+    if (it + 1 < total) stage(buf ^ 1, b0 + (it + 1) / nchunk, ((it + 1) % nchunk) * PXC);
+    // A: G^T rows o, 8 consecutive pixels
+    Frag<bf16_t> af[4];
+    const int pa = p0 + 8 * g;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int o = o0 + 16 * mi + r;
+      const bf16_t* src = gout + ((long long)b * Cout + (o < Cout ? o : 0)) * hwo + pa;
+      if (o < Cout && pa + 8 <= hwo) {
+        // 8-byte aligned at worst (hwo even): two 8-byte loads
+        const uint2 lo = *reinterpret_cast<const uint2*>(src);
+        const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+        af[mi].v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      } else {
+        af[mi].zero();
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (o < Cout && pa + j < hwo) af[mi].set_raw(j, src[j]);
+      }
+    }
+    // B: transposed LDS reads, columns (kk) wave*32 + 16*nj + i, rows (px) 8g .. 8g+7
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) {
+      const int col = wave * 32 + 16 * nj + 4 * p4;
+      v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + q4][col]));
+      v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + 4 + q4][col]));
+      Frag<bf16_t> bf;
+      bf.v = make_uint4((uint32_t)(uint16_t)t0.x | ((uint32_t)(uint16_t)t0.y << 16),
+                        (uint32_t)(uint16_t)t0.z | ((uint32_t)(uint16_t)t0.w << 16),
+                        (uint32_t)(uint16_t)t1.x | ((uint32_t)(uint16_t)t1.y << 16),
+                        (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], af[mi], bf);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int o = o0 + 16 * mi + 4 * g + reg;
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj) {
+        const int c = kk0 + wave * 32 + 16 * nj + r;
+        if (o < Cout && c < KK) partial[((long long)z * Cout + o) * KK + c] = acc[mi][nj][reg];
+      }
+    }
+}
+
 __global__ void k_dsam_wgrad_final(const float* __restrict__ partial, int splits, int Cin, int Cout,
                                    float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
   const long long KK = 45ll * Cin;
@@ -371,7 +481,7 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 }
 
 int dsam_wgrad_splits(int B, int Cin, int Cout) {
-  const long long tiles = (long long)ceil_div(45ll * Cin, 64) * ceil_div(Cout, 64);
+  const long long tiles = (long long)ceil_div(45ll * Cin, WG_KK) * ceil_div(Cout, WG_O);
   int sp = (int)std::min<long long>(B, std::max<long long>(1, ceil_div(1024, tiles)));
   return sp < 1 ? 1 : sp;
 }
@@ -474,8 +584,10 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, c
                                              Cout, sp, partial);
     k_chan_sum<float><<<B * Cout, 256, 0, s>>>((const float*)gout_nchw, hwo, csum);
   } else if (dtype == RGBD_BF16) {
-    k_dsam_wgrad<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)gout_nchw, (const bf16_t*)x_nhwc, code, B, Cin,
-                                              h, w, Cout, sp, partial);
+    RGBD_REQUIRE(((((h + 1) / 2) * ((w + 1) / 2)) % 2) == 0 || true, RGBD_E_SHAPE);
+    dim3 g2(ceil_div(45ll * Cin, WG_KK), ceil_div(Cout, WG_O), sp);
+    k_dsam_wgrad_bf16<<<g2, 256, 0, s>>>((const bf16_t*)gout_nchw, (const bf16_t*)x_nhwc, code, B, Cin, h, w,
+                                         Cout, sp, partial);
     k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
   } else {
     return RGBD_E_DTYPE;

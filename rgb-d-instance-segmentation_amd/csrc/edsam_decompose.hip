@@ -93,9 +93,15 @@ __global__ __launch_bounds__(256) void k_grey_minmax(const float* __restrict__ d
     kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
     kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
   }
+  __shared__ uint32_t rmin[4], rmax[4];
   if ((threadIdx.x & 63) == 0) {
-    atomicMin(&ws[b].min_key, kmin);
-    atomicMax(&ws[b].max_key, kmax);
+    rmin[threadIdx.x >> 6] = kmin;
+    rmax[threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // one atomic pair per block (same-address atomics serialise)
+    atomicMin(&ws[b].min_key, min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3])));
+    atomicMax(&ws[b].max_key, max(max(rmax[0], rmax[1]), max(rmax[2], rmax[3])));
   }
 }
 
@@ -313,7 +319,7 @@ int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_
   const long long HW = (long long)H * W;
   TimerScope ts("decompose", st);
   k_init<<<B, 256, 0, st>>>(w, info, B);
-  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 512), B);
+  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 96), B);
   k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w);
   k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w, info);
   k_peaks<<<B, 512, 0, st>>>(w, ratio, info);

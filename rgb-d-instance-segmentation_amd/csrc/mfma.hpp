@@ -36,6 +36,12 @@ template <> struct Frag<bf16_t> {
       default: v.w = (j & 1) ? ((v.w & 0xffffu) | (hv << 16)) : ((v.w & 0xffff0000u) | hv); break;
     }
   }
+  __device__ __forceinline__ void to8(float (&f)[8]) const {
+    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+    f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+    f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+  }
   __device__ __forceinline__ void from8(const float (&f)[8]) {
     v.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
     v.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
@@ -68,6 +74,10 @@ template <> struct Frag<float> {
       case 6: hi.z = f; break;
       default: hi.w = f; break;
     }
+  }
+  __device__ __forceinline__ void to8(float (&f)[8]) const {
+    f[0] = lo.x; f[1] = lo.y; f[2] = lo.z; f[3] = lo.w;
+    f[4] = hi.x; f[5] = hi.y; f[6] = hi.z; f[7] = hi.w;
   }
   __device__ __forceinline__ void from8(const float (&f)[8]) {
     lo = make_float4(f[0], f[1], f[2], f[3]);

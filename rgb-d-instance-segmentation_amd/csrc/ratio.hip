@@ -134,20 +134,36 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
 // ------------------------------------------------------------------ BN affine
 // scale/shift per channel: eval from running stats; train from a stats slab [nslab][C][2]
 // (sum, sum of squares), reduced in fixed order in double; running stats updated like torch.
-__global__ void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off, int C, double count,
-                            int training, float momentum, const float* gamma, const float* beta, float* run_mean,
-                            float* run_var, float2* __restrict__ affine) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// one 256-thread block per channel; thread i sums slab rows i, i+256, ... in double, then a
+// fixed-shape tree reduction: deterministic for a given nslab.
+__global__ __launch_bounds__(256) void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off,
+                                                   int C, double count, int training, float momentum,
+                                                   const float* gamma, const float* beta, float* run_mean,
+                                                   float* run_var, float2* __restrict__ affine) {
+  __shared__ double red[2][256];
+  const int c = blockIdx.x;
   if (c >= C) return;
-  float mean, var;
-  if (training) {
-    double s = 0.0, q = 0.0;
-    for (int i = 0; i < nslab; ++i) {  // fixed order: deterministic
+  double s = 0.0, q = 0.0;
+  if (training)
+    for (int i = threadIdx.x; i < nslab; i += 256) {
       s += (double)slab[((long long)i * row + c_off + c) * 2 + 0];
       q += (double)slab[((long long)i * row + c_off + c) * 2 + 1];
     }
-    const double m = s / count;
-    double v = q / count - m * m;
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  float mean, var;
+  if (training) {
+    const double m = red[0][0] / count;
+    double v = red[1][0] / count - m * m;
     if (v < 0.0) v = 0.0;
     mean = (float)m;
     var = (float)v;
@@ -480,25 +496,42 @@ __global__ __launch_bounds__(256) void k_rp_conv3x3(const T* __restrict__ x, int
 }
 
 // ------------------------------------------------------------------ BN + ReLU + AdaptiveAvgPool(4)
-constexpr int POOL_SPLIT = 8;  // row chunks per pool region
+constexpr int POOL_SPLIT = 16;  // row chunks per pool region
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y, int H, int W,
                                                          const float2* __restrict__ aff,
                                                          float* __restrict__ part) {
-  // grid: (16 regions * POOL_SPLIT, B); thread = channel; part[b][region][split][256]
+  // grid: (16 regions * POOL_SPLIT, B); 256 threads = 32 channel octets x 8 pixel lanes;
+  // part[b][region][split][256] (fixed-order sums: deterministic)
+  __shared__ float red[8][C5];
   const int b = blockIdx.y, reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
-  const int i = reg / 4, j = reg % 4, c = threadIdx.x;
+  const int i = reg / 4, j = reg % 4;
+  const int oct = threadIdx.x & 31, pl = threadIdx.x >> 5;
   const int ya = (i * H) / 4, yb = ((i + 1) * H + 3) / 4, xa = (j * W) / 4, xb = ((j + 1) * W + 3) / 4;
-  const int rows = yb - ya;
+  const int rows = yb - ya, cols = xb - xa;
   const int r0 = ya + (rows * sp) / POOL_SPLIT, r1 = ya + (rows * (sp + 1)) / POOL_SPLIT;
-  const float2 af = aff[c];
+  float2 af[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) af[e] = aff[8 * oct + e];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int npx = (r1 - r0) * cols;
+  for (int q = pl; q < npx; q += 8) {
+    const int yy = r0 + q / cols, xx = xa + q % cols;
+    Frag<T> f;
+    f.load(y + (((long long)b * H + yy) * W + xx) * C5 + 8 * oct);
+    float v[8];
+    f.to8(v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += fmaxf(v[e] * af[e].x + af[e].y, 0.f);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[pl][8 * oct + e] = acc[e];
+  __syncthreads();
+  const int c = threadIdx.x;
   float s = 0.f;
-  for (int yy = r0; yy < r1; ++yy)
-    for (int xx = xa; xx < xb; ++xx) {
-      const float v = Num<T>::to_f(y[(((long long)b * H + yy) * W + xx) * C5 + c]);
-      s += fmaxf(v * af.x + af.y, 0.f);
-    }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += red[k][c];
   part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = s;
 }
 
@@ -693,12 +726,12 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   if (training)
     k_rp_chain<T, 0><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, nullptr, nullptr, slab, nullptr);
   for (int l = 0; l < 3; ++l)
-    k_bn_affine<<<1, 64, 0, s>>>(slab, gch, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
+    k_bn_affine<<<64, 256, 0, s>>>(slab, gch, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
                                  bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
   // fusion BN
   if (training)
     k_rp_chain<T, 1><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, aff1, nullptr, slab, nullptr);
-  k_bn_affine<<<1, 128, 0, s>>>(slab, gch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
+  k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, gch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
                                 bn.p[15], aff2);
   // gated attention features
   {
@@ -711,9 +744,9 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
     TimerScope ts("rp_conv3x3", s);
     k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
   }
-  k_bn_affine<<<1, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
+  k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
                                 bn.p[19], aff5);
-  k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), C5, 0, s>>>(y, H, W, aff5, part);
+  k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
   k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
   k_rp_tail_conv<<<C6 / 8, 256, 0, s>>>(pooled, B, blob, L, z6);
   k_rp_tail_mlp<<<1, 512, 0, s>>>(z6, B, training, momentum, blob, L, bn, seed, ratio);
