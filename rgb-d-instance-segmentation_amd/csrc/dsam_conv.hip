@@ -382,8 +382,8 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restric
     for (int mi = 0; mi < 4; ++mi) {
       const int o = o0 + 16 * mi + r;
       const bf16_t* src = gout + ((long long)b * Cout + (o < Cout ? o : 0)) * hwo + pa;
-      if (o < Cout && pa + 8 <= hwo) {
-        // 8-byte aligned at worst (hwo even): two 8-byte loads
+      if (o < Cout && pa + 8 <= hwo && (hwo & 3) == 0) {
+        // 8-byte aligned (hwo % 4 == 0, pa % 8 == 0): two 8-byte loads
         const uint2 lo = *reinterpret_cast<const uint2*>(src);
         const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
         af[mi].v = make_uint4(lo.x, lo.y, hi.x, hi.y);
@@ -584,7 +584,6 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, c
                                              Cout, sp, partial);
     k_chan_sum<float><<<B * Cout, 256, 0, s>>>((const float*)gout_nchw, hwo, csum);
   } else if (dtype == RGBD_BF16) {
-    RGBD_REQUIRE(((((h + 1) / 2) * ((w + 1) / 2)) % 2) == 0 || true, RGBD_E_SHAPE);
     dim3 g2(ceil_div(45ll * Cin, WG_KK), ceil_div(Cout, WG_O), sp);
     k_dsam_wgrad_bf16<<<g2, 256, 0, s>>>((const bf16_t*)gout_nchw, (const bf16_t*)x_nhwc, code, B, Cin, h, w,
                                          Cout, sp, partial);

@@ -389,6 +389,293 @@ __global__ __launch_bounds__(256) void k_rp_chain(const float* __restrict__ dept
   }
 }
 
+// ------------------------------------------------------------------ chain v2 (bf16)
+// 512 threads = 8 waves; persistent; ALL chain weights (143 KB bf16) live in LDS for the
+// workgroup's lifetime; a wave owns 32 pixels (one row of a 8x32 tile, two 16-px MFMA
+// columns) so every weight fragment read from LDS feeds two MFMAs.  BN statistics (phases
+// 0/1) are reduced across the wave's 32 pixels and kept per lane in registers, then written
+// as one slab row per wave: deterministic.
+constexpr int C2W_TH = 8, C2W_TW = 32, C2W_PH = C2W_TH + 6, C2W_PW = C2W_TW + 6;
+// LDS weight rows padded by 16 bytes: row strides of 336/400/272/144 B put the 16 rows a
+// ds_read_b128 lane group touches on distinct banks (unpadded 256-B rows are 16-way).
+constexpr int C2W_S1 = STEM_K + 8, C2W_S2 = STEM_C + 8, C2W_S3 = FUS_C + 8, C2W_S4 = ATT_C + 8;
+constexpr size_t C2W_OFF_W1 = 0;
+constexpr size_t C2W_OFF_W2 = C2W_OFF_W1 + (size_t)STEM_C * C2W_S1 * 2;
+constexpr size_t C2W_OFF_W3 = C2W_OFF_W2 + (size_t)FUS_C * C2W_S2 * 2;
+constexpr size_t C2W_OFF_W4 = C2W_OFF_W3 + (size_t)ATT_C * C2W_S3 * 2;
+constexpr size_t C2W_OFF_B = C2W_OFF_W4 + (size_t)FUS_C * C2W_S4 * 2;             // b1 b2 b3 b4 (f32)
+constexpr size_t C2W_OFF_AFF = C2W_OFF_B + (size_t)(STEM_C + FUS_C + ATT_C + FUS_C) * 4;  // aff1, aff2
+constexpr size_t C2W_OFF_PATCH = C2W_OFF_AFF + (size_t)(STEM_C + FUS_C) * 8;
+constexpr size_t C2W_OFF_KTAB = C2W_OFF_PATCH + (size_t)3 * C2W_PH * C2W_PW * 4;
+constexpr size_t C2W_SMEM = C2W_OFF_KTAB + STEM_K * 2;
+static_assert(C2W_SMEM <= 163840, "chain v2 LDS budget");
+
+template <int PHASE>
+__global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ depth3, long long bstride, int B,
+                                                     int H, int W, const char* __restrict__ blob, Layout L,
+                                                     const float2* __restrict__ aff1, const float2* __restrict__ aff2,
+                                                     float* __restrict__ slab, bf16_t* __restrict__ att) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bf16_t* sW1 = (const bf16_t*)(smem + C2W_OFF_W1);
+  const bf16_t* sW2 = (const bf16_t*)(smem + C2W_OFF_W2);
+  const bf16_t* sW3 = (const bf16_t*)(smem + C2W_OFF_W3);
+  const bf16_t* sW4 = (const bf16_t*)(smem + C2W_OFF_W4);
+  float* sb = (float*)(smem + C2W_OFF_B);
+  float* sb1 = sb;
+  float* sb2 = sb1 + STEM_C;
+  float* sb3 = sb2 + FUS_C;
+  float* sb4 = sb3 + ATT_C;
+  float2* saf1 = (float2*)(smem + C2W_OFF_AFF);
+  float2* saf2 = saf1 + STEM_C;
+  float* patch = (float*)(smem + C2W_OFF_PATCH);
+  short* ktab = (short*)(smem + C2W_OFF_KTAB);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  // ---- one-time LDS fill: weights, biases, BN affines, im2col table
+  {
+    const size_t wbytes = C2W_OFF_B;  // W1..W4 are contiguous in the blob too? copy each
+    (void)wbytes;
+    auto copy_rows = [&](size_t dst, size_t src, int rows, int k, int stride) {  // 16-byte pieces
+      const int per = k / 8;
+      for (int i = tid; i < rows * per; i += 512) {
+        const int rr = i / per, q = i % per;
+        *reinterpret_cast<uint4*>(smem + dst + ((size_t)rr * stride + 8 * q) * 2) =
+            *reinterpret_cast<const uint4*>(blob + src + ((size_t)rr * k + 8 * q) * 2);
+      }
+    };
+    copy_rows(C2W_OFF_W1, L.w1, STEM_C, STEM_K, C2W_S1);
+    copy_rows(C2W_OFF_W2, L.w2, FUS_C, STEM_C, C2W_S2);
+    copy_rows(C2W_OFF_W3, L.w3, ATT_C, FUS_C, C2W_S3);
+    copy_rows(C2W_OFF_W4, L.w4, FUS_C, ATT_C, C2W_S4);
+    for (int i = tid; i < STEM_C; i += 512) sb1[i] = ((const float*)(blob + L.b1))[i];
+    for (int i = tid; i < FUS_C; i += 512) sb2[i] = ((const float*)(blob + L.b2))[i];
+    for (int i = tid; i < ATT_C; i += 512) sb3[i] = ((const float*)(blob + L.b3))[i];
+    for (int i = tid; i < FUS_C; i += 512) sb4[i] = ((const float*)(blob + L.b4))[i];
+    if (PHASE >= 1)
+      for (int i = tid; i < STEM_C; i += 512) saf1[i] = aff1[i];
+    if (PHASE >= 2)
+      for (int i = tid; i < FUS_C; i += 512) saf2[i] = aff2[i];
+    for (int k = tid; k < STEM_K; k += 512) {
+      short v = -1;
+      if (k < 147) {
+        const int tap = k / 3, c = k % 3;
+        v = (short)((c * C2W_PH + tap / 7) * C2W_PW + tap % 7);
+      }
+      ktab[k] = v;
+    }
+  }
+  constexpr int NST = PHASE == 0 ? 12 : 8;  // channel tiles whose stats this phase collects
+  float ssum[NST][4], ssq[NST][4];
+#pragma unroll
+  for (int t = 0; t < NST; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ssum[t][j] = ssq[t][j] = 0.f;
+  const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
+  const long long ntiles = (long long)B * tiles_x * tiles_y;
+  const long long HW = (long long)H * W;
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
+    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
+    const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
+    __syncthreads();
+    for (int i = tid; i < 3 * C2W_PH * C2W_PW; i += 512) {
+      const int c = i / (C2W_PH * C2W_PW), yy = (i / C2W_PW) % C2W_PH, xx = i % C2W_PW;
+      const int yv = y0 + yy - 3, xv = x0 + xx - 3;
+      patch[i] = (yv >= 0 && yv < H && xv >= 0 && xv < W) ? depth3[b * bstride + c * HW + (long long)yv * W + xv] : 0.f;
+    }
+    __syncthreads();
+    const int py = y0 + wave;
+    bool pv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) pv[u] = py < H && x0 + 16 * u + r < W;
+    // ---- stem
+    f32x4 a1[12][2];
+#pragma unroll
+    for (int t = 0; t < 12; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) a1[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      Frag<bf16_t> bfr[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int off = ktab[32 * s + 8 * g + e];
+          vv[e] = off >= 0 ? patch[off + wave * C2W_PW + 16 * u + r] : 0.f;
+        }
+        bfr[u].from8(vv);
+      }
+#pragma unroll
+      for (int t = 0; t < 12; ++t) {
+        if (t < 4 && (s == 0 || s == 4)) continue;
+        if (t >= 4 && t < 8 && s == 4) continue;
+        Frag<bf16_t> af;
+        af.v = *reinterpret_cast<const uint4*>(sW1 + (16 * t + r) * C2W_S1 + 32 * s + 8 * g);
+        mma(a1[t][0], af, bfr[0]);
+        mma(a1[t][1], af, bfr[1]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 12; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float bb = sb1[16 * t + 4 * g + j];
+        a1[t][0][j] += bb;
+        a1[t][1][j] += bb;
+      }
+    if constexpr (PHASE == 0) {
+#pragma unroll
+      for (int t = 0; t < 12; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v0 = pv[0] ? a1[t][0][j] : 0.f, v1 = pv[1] ? a1[t][1][j] : 0.f;
+          ssum[t][j] += v0 + v1;
+          ssq[t][j] += v0 * v0 + v1 * v1;
+        }
+      continue;
+    }
+    Frag<bf16_t> f1[6][2];
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int t = 2 * s + (e >> 2), j = e & 3;
+          const float2 af = saf1[16 * t + 4 * g + j];
+          vv[e] = fmaxf(a1[t][u][j] * af.x + af.y, 0.f);
+        }
+        f1[s][u].from8(vv);
+      }
+    // ---- fusion
+    f32x4 a2[8][2];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      a2[t][0] = a2[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        Frag<bf16_t> af;
+        af.v = *reinterpret_cast<const uint4*>(sW2 + (16 * t + r) * C2W_S2 + 32 * s + 8 * g);
+        mma(a2[t][0], af, f1[s][0]);
+        mma(a2[t][1], af, f1[s][1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float bb = sb2[16 * t + 4 * g + j];
+        a2[t][0][j] += bb;
+        a2[t][1][j] += bb;
+      }
+    }
+    if constexpr (PHASE == 1) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v0 = pv[0] ? a2[t][0][j] : 0.f, v1 = pv[1] ? a2[t][1][j] : 0.f;
+          ssum[t][j] += v0 + v1;
+          ssq[t][j] += v0 * v0 + v1 * v1;
+        }
+      continue;
+    }
+    if constexpr (PHASE == 2) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float2 af = saf2[16 * t + 4 * g + j];
+          a2[t][0][j] = fmaxf(a2[t][0][j] * af.x + af.y, 0.f);
+          a2[t][1][j] = fmaxf(a2[t][1][j] * af.x + af.y, 0.f);
+        }
+      Frag<bf16_t> f2[4][2];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float vv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vv[e] = a2[2 * s + (e >> 2)][u][e & 3];
+          f2[s][u].from8(vv);
+        }
+      f32x4 a3[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a3[t][0] = a3[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          Frag<bf16_t> af;
+          af.v = *reinterpret_cast<const uint4*>(sW3 + (16 * t + r) * C2W_S3 + 32 * s + 8 * g);
+          mma(a3[t][0], af, f2[s][0]);
+          mma(a3[t][1], af, f2[s][1]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float bb = sb3[16 * t + 4 * g + j];
+          a3[t][0][j] = fmaxf(a3[t][0][j] + bb, 0.f);
+          a3[t][1][j] = fmaxf(a3[t][1][j] + bb, 0.f);
+        }
+      }
+      Frag<bf16_t> f3[2][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float vv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vv[e] = a3[2 * s + (e >> 2)][u][e & 3];
+          f3[s][u].from8(vv);
+        }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        f32x4 a4[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          Frag<bf16_t> af;
+          af.v = *reinterpret_cast<const uint4*>(sW4 + (16 * t + r) * C2W_S4 + 32 * s + 8 * g);
+          mma(a4[0], af, f3[s][0]);
+          mma(a4[1], af, f3[s][1]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (!pv[u]) continue;
+          uint2 pk;
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ch = 16 * t + 4 * g + j;
+            o[j] = a2[t][u][j] * sigmoidf_(a4[u][j] + sb4[ch]);
+          }
+          pk.x = (uint32_t)f32_to_bf16(o[0]) | ((uint32_t)f32_to_bf16(o[1]) << 16);
+          pk.y = (uint32_t)f32_to_bf16(o[2]) | ((uint32_t)f32_to_bf16(o[3]) << 16);
+          *reinterpret_cast<uint2*>(att + ((long long)b * HW + (long long)py * W + x0 + 16 * u + r) * FUS_C + 16 * t +
+                                    4 * g) = pk;
+        }
+      }
+    }
+  }
+  if constexpr (PHASE < 2) {
+    // reduce each lane's channel sums over the 16 pixel lanes; lanes r == 0 write the slab
+    const long long row = (long long)blockIdx.x * 8 + wave;
+    constexpr int NC = PHASE == 0 ? STEM_C : FUS_C;
+#pragma unroll
+    for (int t = 0; t < NST; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = ssum[t][j], q = ssq[t][j];
+        for (int o = 1; o < 16; o <<= 1) {
+          v += __shfl_xor(v, o);
+          q += __shfl_xor(q, o);
+        }
+        if (r == 0) {
+          slab[(row * NC + 16 * t + 4 * g + j) * 2 + 0] = v;
+          slab[(row * NC + 16 * t + 4 * g + j) * 2 + 1] = q;
+        }
+      }
+  }
+}
+
 // ------------------------------------------------------------------ conv5: 3x3 128->256
 constexpr int CV_TH = 4, CV_TW = 32;             // 128-pixel tile
 constexpr int CV_PH = CV_TH + 2, CV_PW = CV_TW + 2;
@@ -494,6 +781,154 @@ __global__ __launch_bounds__(256) void k_rp_conv3x3(const T* __restrict__ x, int
           st[2 * wnn][c][q] + st[2 * wnn + 1][c][q];
   }
 }
+
+// ------------------------------------------------------------------ conv5 v2 (bf16)
+// 512 threads = 8 waves as 2 (pixels) x 4 (channels); workgroup tile 128 px (4x32) x all 256
+// output channels; wave tile 64 px x 64 ch (4x4 MFMA 16x16x32).  K = 36 steps of (tap, 32-ch
+// chunk).  Both operands staged in LDS with 80-byte rows (conflict-free ds_read_b128 for a
+// 16-row fragment), B (weights) double-buffered per step, A (6x34 halo patch) per chunk;
+// the next step's global loads are issued before the current step's MFMAs and written to LDS
+// after them (register staging, one barrier per step).  Epilogue: bias, BN partial sums, and
+// y (NHWC bf16) re-laid out through LDS so each lane stores 16 contiguous bytes.
+constexpr int V2_ROW = 40;  // 32 ch + 8 pad = 80-byte rows
+constexpr int V2_NPIX = CV_PH * CV_PW;  // 204 halo pixels
+
+__global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict__ x, int B, int H, int W,
+                                                       const char* __restrict__ blob, Layout L,
+                                                       bf16_t* __restrict__ y, float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t(*sA)[V2_NPIX][V2_ROW] = reinterpret_cast<bf16_t(*)[V2_NPIX][V2_ROW]>(smem);
+  bf16_t(*sB)[C5][V2_ROW] = reinterpret_cast<bf16_t(*)[C5][V2_ROW]>(smem + 2 * V2_NPIX * V2_ROW * 2);
+  float(*st)[C5][2] = reinterpret_cast<float(*)[C5][2]>(smem + 2 * V2_NPIX * V2_ROW * 2 + 2 * C5 * V2_ROW * 2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  const bf16_t* w5 = (const bf16_t*)(blob + L.w5);
+  const float* b5 = (const float*)(blob + L.b5);
+  const int tiles_x = (W + CV_TW - 1) / CV_TW, tiles_y = (H + CV_TH - 1) / CV_TH;
+  const long long ntiles = (long long)B * tiles_x * tiles_y;
+  for (int i = tid; i < 2 * C5 * 2; i += 512) (&st[0][0][0])[i] = 0.f;
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
+    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
+    const int y0 = (trem / tiles_x) * CV_TH, x0 = (trem % tiles_x) * CV_TW;
+    // staging: A pieces (halo pixel, 8-ch chunk) and B pieces (n, 8-ch chunk), ids tid and tid+512
+    uint4 ra0, ra1, rb0, rb1;
+#define V2_LOAD_A1(ID, R, CHUNK)                                                                      \
+  {                                                                                                   \
+    R = make_uint4(0u, 0u, 0u, 0u);                                                                   \
+    if ((ID) < V2_NPIX * 4) {                                                                         \
+      const int pp = (ID) >> 2, q = (ID)&3;                                                           \
+      const int yy = y0 + pp / CV_PW - 1, xx = x0 + pp % CV_PW - 1;                                   \
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W)                                                     \
+        R = *reinterpret_cast<const uint4*>(x + (((long long)b * H + yy) * W + xx) * FUS_C + (CHUNK)*32 + 8 * q); \
+    }                                                                                                 \
+  }
+#define V2_STORE_A1(ID, R, BUF) \
+  if ((ID) < V2_NPIX * 4) *reinterpret_cast<uint4*>(&sA[BUF][(ID) >> 2][8 * ((ID)&3)]) = R;
+#define V2_LOAD_B1(ID, R, STEP) \
+  R = *reinterpret_cast<const uint4*>(w5 + (long long)((ID) >> 2) * (9 * FUS_C) + ((STEP) % 9) * FUS_C + ((STEP) / 9) * 32 + 8 * ((ID)&3));
+#define V2_STORE_B1(ID, R, BUF) *reinterpret_cast<uint4*>(&sB[BUF][(ID) >> 2][8 * ((ID)&3)]) = R;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();  // previous tile's epilogue done with the LDS
+    V2_LOAD_A1(tid, ra0, 0);
+    V2_LOAD_A1(tid + 512, ra1, 0);
+    V2_LOAD_B1(tid, rb0, 0);
+    V2_LOAD_B1(tid + 512, rb1, 0);
+    V2_STORE_A1(tid, ra0, 0);
+    V2_STORE_A1(tid + 512, ra1, 0);
+    V2_STORE_B1(tid, rb0, 0);
+    V2_STORE_B1(tid + 512, rb1, 0);
+    __syncthreads();
+#pragma unroll 1
+    for (int step = 0; step < 36; ++step) {
+      const int chunk = step / 9, tap = step % 9;
+      const bool more = step + 1 < 36;
+      if (more) {
+        V2_LOAD_B1(tid, rb0, step + 1);
+        V2_LOAD_B1(tid + 512, rb1, step + 1);
+      }
+      if (tap == 0 && chunk + 1 < 4) {
+        V2_LOAD_A1(tid, ra0, chunk + 1);
+        V2_LOAD_A1(tid + 512, ra1, chunk + 1);
+      }
+      const int ky = tap / 3, kx = tap % 3;
+      Frag<bf16_t> af[4], bfr[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int ty = wm * 2 + (mi >> 1), tx = (mi & 1) * 16 + r;
+        af[mi].v = *reinterpret_cast<const uint4*>(&sA[chunk & 1][(ty + ky) * CV_PW + tx + kx][8 * g]);
+      }
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj)
+        bfr[nj].v = *reinterpret_cast<const uint4*>(&sB[step & 1][wn * 64 + 16 * nj + r][8 * g]);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], af[mi], bfr[nj]);
+      if (more) {
+        V2_STORE_B1(tid, rb0, (step + 1) & 1);
+        V2_STORE_B1(tid + 512, rb1, (step + 1) & 1);
+      }
+      if (tap == 8 && chunk + 1 < 4) {
+        V2_STORE_A1(tid, ra0, (chunk + 1) & 1);
+        V2_STORE_A1(tid + 512, ra1, (chunk + 1) & 1);
+      }
+      __syncthreads();
+    }
+    // ---- epilogue: bias + stats, stage the bf16 tile in LDS as [px][256] (row 528 B)
+    bf16_t(*sY)[C5 + 8] = reinterpret_cast<bf16_t(*)[C5 + 8]>(smem);
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      const int n = wn * 64 + 16 * nj + r;
+      const float bias = b5[n];
+      float sum = 0.f, sq = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int ty = wm * 2 + (mi >> 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int tx = (mi & 1) * 16 + 4 * g + j;
+          const bf16_t tv = f32_to_bf16(acc[mi][nj][j] + bias);
+          sY[ty * CV_TW + tx][n] = tv;
+          if (y0 + ty < H && x0 + tx < W) {
+            const float vr = bf16_to_f32(tv);  // statistics of the stored values
+            sum += vr;
+            sq += vr * vr;
+          }
+        }
+      }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      sq += __shfl_xor(sq, 16);
+      sq += __shfl_xor(sq, 32);
+      if (g == 0) {
+        st[wm][n][0] += sum;
+        st[wm][n][1] += sq;
+      }
+    }
+    __syncthreads();
+    // 128 px x 512 B = 4096 16-byte pieces
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int id = tid + 512 * i;
+      const int px = id >> 5, q = id & 31;
+      const int yy = y0 + px / CV_TW, xx = x0 + px % CV_TW;
+      if (yy < H && xx < W)
+        *reinterpret_cast<uint4*>(y + (((long long)b * H + yy) * W + xx) * C5 + 8 * q) =
+            *reinterpret_cast<const uint4*>(&sY[px][8 * q]);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < C5; i += 512)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) slab[((long long)blockIdx.x * C5 + i) * 2 + q] = st[0][i][q] + st[1][i][q];
+}
+constexpr size_t V2_SMEM = 2 * V2_NPIX * V2_ROW * 2 + 2 * C5 * V2_ROW * 2 + 2 * C5 * 2 * 4;
 
 // ------------------------------------------------------------------ BN + ReLU + AdaptiveAvgPool(4)
 constexpr int POOL_SPLIT = 16;  // row chunks per pool region
@@ -677,9 +1112,13 @@ inline int chain_grid(int B, int H, int W) {
   const long long nt = (long long)B * ((W + CH_TW - 1) / CH_TW) * ((H + CH_TH - 1) / CH_TH);
   return (int)std::min<long long>(nt, 2048);
 }
+inline int chain_grid_v2(int B, int H, int W) {  // one 512-thread workgroup per CU (LDS-resident weights)
+  const long long nt = (long long)B * ((W + C2W_TW - 1) / C2W_TW) * ((H + C2W_TH - 1) / C2W_TH);
+  return (int)std::min<long long>(nt, 256);
+}
 inline int conv_grid(int B, int H, int W) {
   const long long nt = (long long)B * ((W + CV_TW - 1) / CV_TW) * ((H + CV_TH - 1) / CV_TH);
-  return (int)std::min<long long>(nt, 1024);
+  return (int)std::min<long long>(nt, 512);
 }
 
 inline Ws make_ws(int es, int B, int H, int W) {
@@ -691,7 +1130,7 @@ inline Ws make_ws(int es, int B, int H, int W) {
     return r;
   };
   const size_t P = (size_t)B * H * W;
-  const int slab_rows = std::max(chain_grid(B, H, W), conv_grid(B, H, W));
+  const int slab_rows = std::max(std::max(chain_grid(B, H, W), 8 * chain_grid_v2(B, H, W)), conv_grid(B, H, W));
   w.aff1 = seg(STEM_C * sizeof(float2));
   w.aff2 = seg(FUS_C * sizeof(float2));
   w.aff5 = seg(C5 * sizeof(float2));
@@ -721,28 +1160,50 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   float* pooled = (float*)(ws + w.pooled);
   float* z6 = (float*)(ws + w.z6);
   const double P = (double)B * H * W;
-  const int gch = chain_grid(B, H, W);
+  const bool v2 = sizeof(T) == 2;
+  const int gch = v2 ? chain_grid_v2(B, H, W) : chain_grid(B, H, W);
+  const int nslab_ch = v2 ? gch * 8 : gch;  // v2 writes one slab row per wave
+  if (v2) {
+    static const hipError_t attr[3] = {
+        hipFuncSetAttribute((const void*)k_rp_chain_v2<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C2W_SMEM),
+        hipFuncSetAttribute((const void*)k_rp_chain_v2<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C2W_SMEM),
+        hipFuncSetAttribute((const void*)k_rp_chain_v2<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C2W_SMEM)};
+    for (int i = 0; i < 3; ++i)
+      if (attr[i] != hipSuccess) return (int)attr[i];
+  }
+#define CHAIN_LAUNCH(PH, A1, A2, SL, OUT)                                                                          \
+  do {                                                                                                            \
+    if (v2)                                                                                                       \
+      k_rp_chain_v2<PH><<<gch, 512, C2W_SMEM, s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, (bf16_t*)(OUT)); \
+    else                                                                                                          \
+      k_rp_chain<T, PH><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, (T*)(OUT));            \
+  } while (0)
   // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
-  if (training)
-    k_rp_chain<T, 0><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, nullptr, nullptr, slab, nullptr);
+  if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
   for (int l = 0; l < 3; ++l)
-    k_bn_affine<<<64, 256, 0, s>>>(slab, gch, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
+    k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
                                  bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
   // fusion BN
-  if (training)
-    k_rp_chain<T, 1><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, aff1, nullptr, slab, nullptr);
-  k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, gch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
+  if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, nullptr);
+  k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, nslab_ch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
                                 bn.p[15], aff2);
   // gated attention features
   {
     TimerScope ts("rp_chain", s);
-    k_rp_chain<T, 2><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, aff1, aff2, nullptr, att);
+    CHAIN_LAUNCH(2, aff1, aff2, nullptr, att);
   }
   // conv5 + its BN statistics
   const int gcv = conv_grid(B, H, W);
   {
     TimerScope ts("rp_conv3x3", s);
-    k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
+    if constexpr (sizeof(T) == 2) {
+      static const hipError_t attr = hipFuncSetAttribute(
+          (const void*)k_rp_conv3x3_v2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)V2_SMEM);
+      if (attr != hipSuccess) return (int)attr;
+      k_rp_conv3x3_v2<<<gcv, 512, V2_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+    }
+    else
+      k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
   }
   k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
                                 bn.p[19], aff5);
