@@ -96,10 +96,9 @@ def build(args, dev):
 def make_step(ctx, world, inference=False):
     from rgbd_amd import ops
     from rgbd_amd.hot_path import hot_path
+    from rgbd_amd.distributed import GradBucket
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
-    flat = None
-    if world > 1:
-        flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=params[0].device)
+    bucket = GradBucket(params) if world > 1 else None
 
     def step():
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
@@ -110,15 +109,8 @@ def make_step(ctx, world, inference=False):
         ratio = ctx["rp"](pv[:, 3:6])
         feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"])
         torch.autograd.backward(feats, ctx["gouts"])
-        if world > 1:  # DDP gradient exchange of the hot-path parameters (RCCL over xGMI)
-            torch.cat([p.grad.reshape(-1) for p in params], out=flat)
-            dist.all_reduce(flat)
-            flat.div_(world)
-            off = 0
-            for p in params:
-                n = p.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p))
-                off += n
+        if bucket is not None:  # DDP gradient exchange of the hot-path parameters (RCCL over xGMI)
+            bucket.allreduce_mean()
         for p in params:
             p.grad = None
         return feats
