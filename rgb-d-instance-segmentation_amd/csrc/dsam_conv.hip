@@ -348,6 +348,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restric
     s_kx[q] = tap % 3;
     s_c[q] = k2 % Cin;
   }
+  int staged_any = 0;  // does the staged chunk hold any unmasked element?
   auto stage = [&](int buf, int b, int p0) {
     const int p = p0 + spx;
     const int oy = p / wo, ox = p % wo;
@@ -359,6 +360,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restric
       if (ok && s_seg[q] < 4) ok = (code[pix] >> s_seg[q]) & 1u;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (ok) v = *reinterpret_cast<const uint4*>(x + pix * Cin + s_c[q]);
+      staged_any |= ok ? 1 : 0;
       *reinterpret_cast<uint4*>(&Xs[buf][spx][16 * skg + 8 * q]) = v;
     }
   };
@@ -370,11 +372,16 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restric
   const int nchunk = (hwo + PXC - 1) / PXC;
   const int total = (b1 - b0) * nchunk;
   if (total > 0) stage(0, b0, 0);
-  __syncthreads();
+  int live = __syncthreads_or(staged_any);
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
     const int b = b0 + it / nchunk, p0 = (it % nchunk) * PXC;
+    staged_any = 0;
     if (it + 1 < total) stage(buf ^ 1, b0 + (it + 1) / nchunk, ((it + 1) % nchunk) * PXC);
+    if (!live) {  // every im2col element of this chunk is masked out: contribution is zero
+      live = __syncthreads_or(staged_any);
+      continue;
+    }
     // A: G^T rows o, 8 consecutive pixels
     Frag<bf16_t> af[4];
     const int pa = p0 + 8 * g;
@@ -411,7 +418,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restric
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], af[mi], bf);
     }
-    __syncthreads();
+    live = __syncthreads_or(staged_any);
   }
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
@@ -468,12 +475,212 @@ __global__ void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_deco
   dbias[t] = s;
 }
 
+// ----------------------------------------------------------------------- bf16 v2
+// Workgroup tile 128 output pixels (flattened over batch x grid, or over one stride-2 parity
+// class for dX) x 128 output channels; 4 waves as 2x2, wave tile 64 px x 64 ch (4x4 MFMA).
+// A (im2col rows) is gathered straight from NHWC global memory, 8 channels (16 B) per lane,
+// once per (tap, 32-ch chunk) and re-used by every live segment; B (packed weights) is staged
+// per (tap, chunk, segment) step through a double-buffered LDS tile shared by the 4 waves.
+// A segment whose mask bit is absent from every pixel the workgroup reads is skipped for
+// the whole K loop (exact: its contribution is zero).
+constexpr int V2M = 128, V2N = 128, V2BROW = 40;  // 80-byte LDS rows (conflict-free b128 reads)
+
+__global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t sB[2][V2N][V2BROW];
+  __shared__ uint32_t seg_or;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave & 1, wn = wave >> 1;
+  int py = 0, px = 0, Hc = a.Ho, Wc = a.Wo;
+  if (a.transposed) {
+    py = blockIdx.z >> 1;
+    px = blockIdx.z & 1;
+    Hc = (a.Ho - py + 1) >> 1;
+    Wc = (a.Wo - px + 1) >> 1;
+  }
+  const long long HWc = (long long)Hc * Wc;
+  const long long Mtot = (long long)a.B * HWc;
+  const long long mblk = (long long)blockIdx.x * V2M;
+  if (mblk >= Mtot) return;  // whole workgroup
+  const int n0 = blockIdx.y * V2N;
+  const bf16_t* xp = (const bf16_t*)a.x;
+  const bf16_t* wp = (const bf16_t*)a.w;
+  const long long ktot = 5ll * 9 * a.C;
+  // rows owned by this lane: m = mblk + wm*64 + 16*mi + r
+  int rb[4], roy[4], rox[4];
+  bool rvalid[4];
+  uint32_t rcode[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const long long m = mblk + wm * 64 + 16 * mi + r;
+    rvalid[mi] = m < Mtot;
+    const long long mm = rvalid[mi] ? m : 0;
+    rb[mi] = (int)(mm / HWc);
+    const int rem = (int)(mm % HWc);
+    const int i = rem / Wc, j = rem % Wc;
+    roy[mi] = a.transposed ? 2 * i + py : i;
+    rox[mi] = a.transposed ? 2 * j + px : j;
+    rcode[mi] = (a.mask_mode == MASK_DST && rvalid[mi])
+                    ? a.code[((long long)rb[mi] * a.Ho + roy[mi]) * a.Wo + rox[mi]]
+                    : 0u;
+  }
+  // ---- live segments of the workgroup (OR of every code any of its rows reads)
+  if (tid == 0) seg_or = 0u;
+  __syncthreads();
+  {
+    uint32_t o = 0u;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      if (!rvalid[mi]) continue;
+      if (a.mask_mode == MASK_DST) {
+        o |= rcode[mi];
+      } else {
+        for (int t = 0; t < 9; ++t) {
+          const int iy = roy[mi] * 2 - 1 + t / 3, ix = rox[mi] * 2 - 1 + t % 3;
+          if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi)
+            o |= a.code[((long long)rb[mi] * a.Hi + iy) * a.Wi + ix];
+        }
+      }
+    }
+    if (o) atomicOr(&seg_or, o);
+  }
+  __syncthreads();
+  const uint32_t live = (seg_or & 0xfu) | 0x10u;  // segment 4 (projection) always live
+  int segs[5], nseg = 0;
+  for (int sgi = 0; sgi < 5; ++sgi)
+    if ((live >> sgi) & 1u) segs[nseg++] = sgi;
+  // ---- K steps = (tap, chunk) x live segments
+  int taps[9], ntap = 0;
+  for (int ky = 0; ky < 3; ++ky)
+    for (int kx = 0; kx < 3; ++kx) {
+      if (a.transposed && (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1))) continue;
+      taps[ntap++] = ky * 3 + kx;
+    }
+  const int nchunk = a.C / 32;
+  const int nsteps = ntap * nchunk * nseg;
+  // B staging: 128 rows (n) x 4 pieces of 8 channels; thread -> pieces tid, tid + 256
+  uint4 rbv[2];
+#define V2_BLOAD(STEP)                                                                            \
+  {                                                                                               \
+    const int st_ = (STEP);                                                                       \
+    const int sg_ = segs[st_ % nseg], tc_ = st_ / nseg;                                           \
+    const int tap_ = taps[tc_ / nchunk], ch_ = tc_ % nchunk;                                      \
+    const long long koff_ = ((long long)sg_ * 9 + tap_) * a.C + ch_ * 32;                         \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                               \
+      const int id = tid + 256 * i, n = n0 + (id >> 2);                                          \
+      rbv[i] = n < a.N ? *reinterpret_cast<const uint4*>(wp + (long long)n * ktot + koff_ + 8 * (id & 3)) \
+                       : make_uint4(0u, 0u, 0u, 0u);                                              \
+    }                                                                                             \
+  }
+#define V2_BSTORE(BUF)                                                                    \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                         \
+    const int id = tid + 256 * i;                                                         \
+    *reinterpret_cast<uint4*>(&sB[BUF][id >> 2][8 * (id & 3)]) = rbv[i];                  \
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  V2_BLOAD(0);
+  V2_BSTORE(0);
+  __syncthreads();
+  Frag<bf16_t> A[4];
+  uint32_t scode[4];
+  for (int st = 0; st < nsteps; ++st) {
+    const int sgi = st % nseg, tc = st / nseg;
+    const int seg = segs[sgi];
+    if (st + 1 < nsteps) V2_BLOAD(st + 1);
+    if (sgi == 0) {  // new (tap, chunk): gather the A rows
+      const int tap = taps[tc / nchunk], ch = tc % nchunk;
+      const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        int iy, ix;
+        if (a.transposed) {
+          iy = (roy[mi] + 1 - ky) >> 1;
+          ix = (rox[mi] + 1 - kx) >> 1;
+        } else {
+          iy = roy[mi] * 2 - 1 + ky;
+          ix = rox[mi] * 2 - 1 + kx;
+        }
+        const bool inb = rvalid[mi] && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+        const long long pix = inb ? ((long long)rb[mi] * a.Hi + iy) * a.Wi + ix : 0;
+        if (inb)
+          A[mi].load(xp + pix * a.C + ch * 32 + 8 * g);
+        else
+          A[mi].zero();
+        scode[mi] = a.mask_mode == MASK_SRC ? (inb ? a.code[pix] : 0u) : rcode[mi];
+      }
+    }
+    Frag<bf16_t> As[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      As[mi] = A[mi];
+      if (seg < 4) As[mi].select((scode[mi] >> seg) & 1u);
+    }
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      Frag<bf16_t> bf;
+      bf.v = *reinterpret_cast<const uint4*>(&sB[st & 1][wn * 64 + 16 * nj + r][8 * g]);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], As[mi], bf);
+    }
+    if (st + 1 < nsteps) V2_BSTORE((st + 1) & 1);
+    __syncthreads();
+  }
+#undef V2_BLOAD
+#undef V2_BSTORE
+  // ---- epilogue (same contract as k_conv_igemm)
+  const bf16_t* res = (const bf16_t*)a.residual;
+  bf16_t* onchw = (bf16_t*)a.out_nchw;
+  bf16_t* onhwc = (bf16_t*)a.out_nhwc;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const long long m = mblk + wm * 64 + 16 * mi + 4 * g + reg;
+      if (m >= Mtot) continue;
+      const int b = (int)(m / HWc);
+      const int rem = (int)(m % HWc);
+      const int i = rem / Wc, j = rem % Wc;
+      const int oy = a.transposed ? 2 * i + py : i;
+      const int ox = a.transposed ? 2 * j + px : j;
+      const int nmask = a.info ? a.info[b].n_masks : 0;
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) {
+        const int n = n0 + wn * 64 + 16 * nj + r;
+        if (n >= a.N) continue;
+        float v = acc[mi][nj][reg];
+        if (a.bias4) {
+          float bs = 0.f;
+          for (int sb = 0; sb < nmask; ++sb) bs += a.bias4[sb * a.N + n];
+          v += bs;
+        }
+        const long long o_nchw = (((long long)b * a.N + n) * a.Ho + oy) * a.Wo + ox;
+        if (res) v = bf16_to_f32(res[o_nchw]) + v;
+        const bf16_t tv = f32_to_bf16(v);
+        if (onchw) onchw[o_nchw] = tv;
+        if (onhwc) onhwc[(((long long)b * a.Ho + oy) * a.Wo + ox) * a.N + n] = tv;
+      }
+    }
+  }
+}
+
 template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   TimerScope ts(a.transposed ? "dsam_dx" : "dsam_fwd", s);
   int nclass = a.transposed ? 4 : 1;
   long long Mmax = (long long)a.B * a.Ho * a.Wo;
   if (a.transposed) Mmax = (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2);
+  if constexpr (sizeof(T) == 2) {
+    if (a.C % 32 == 0 && a.nseg == 5) {
+      dim3 grid2(ceil_div(Mmax, V2M), ceil_div(a.N, V2N), nclass);
+      k_conv_igemm_v2<<<grid2, 256, 0, s>>>(a);
+      RGBD_CHECK_LAUNCH();
+      return RGBD_OK;
+    }
+  }
   dim3 grid(ceil_div(Mmax, BM), ceil_div(a.N, BN), nclass);
   k_conv_igemm<T><<<grid, 256, 0, s>>>(a);
   RGBD_CHECK_LAUNCH();
