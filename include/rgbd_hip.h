@@ -120,17 +120,19 @@ int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, 
  *   out = residual + sum_{i<4} Conv3x3s2_i(x * m_i) + sum_{i<n_masks[b]} b_i + Proj3x3s2(x)
  * x_nhwc: dtype [B][h][w][Cin]; code: uint8 [B][h][w] (pooled region codes at x's
  * resolution); bias float32 [4][Cout]; residual/out_nchw: dtype [B][Cout][ho][wo];
- * out_nhwc (optional, may be NULL): dtype [B][ho][wo][Cout]. */
+ * out_nhwc (optional, may be NULL): dtype [B][ho][wo][Cout].  ws: workspace of
+ * rgbd_dsam_conv_workspace_size bytes (split-K slabs of the bf16 path). */
+size_t rgbd_dsam_conv_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout);
 int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
                   int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
-                  const void* residual, void* out_nchw, void* out_nhwc, void* stream);
+                  const void* residual, void* out_nchw, void* out_nhwc, void* ws, void* stream);
 /* dX of one DSAModule, plus the upstream gradient of its input's other consumer:
  *   dx = gin + sum_i m_i * ConvT_i(gout) + ConvT_proj(gout)
  * gout_nhwc: dtype [B][ho][wo][Cout]; gin_nchw: dtype [B][Cin][h][w];
  * dx_nchw (dtype [B][Cin][h][w]) and dx_nhwc (optional) are written. */
 int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
                        int w, int Cout, const void* wbwd, const void* gin_nchw, void* dx_nchw,
-                       void* dx_nhwc, void* stream);
+                       void* dx_nhwc, void* ws, void* stream);
 /* dW / db of one DSAModule: dconv_w float32 [4][Cout][Cin][3][3], dproj_w float32
  * [Cout][Cin][3][3], dbias float32 [4][Cout] (all OVERWRITTEN).  gout_nchw: dtype
  * [B][Cout][ho][wo]; x_nhwc as in the forward. */

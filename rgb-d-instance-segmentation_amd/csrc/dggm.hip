@@ -180,35 +180,43 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_bwd_partial(const T* __restri
                                                                const float* __restrict__ wt,
                                                                const float* __restrict__ bias,
                                                                float* __restrict__ partial) {
-  // partial[tile][c][4] = sum over the tile's pixels of dout*relu'(pre) * (1, g0, g1, g2)
+  // partial[tile][c][4] = sum over the tile's pixels of dout*relu'(pre) * (1, g0, g1, g2).
+  // A "tile" is the pixel range [tile*ppt, (tile+1)*ppt): each thread accumulates its pixels in
+  // registers first, then one block reduction per channel (fixed order: deterministic).
   __shared__ float red[4][kFuseCh][4];
   const int hw = h * w;
   const long long P = (long long)B * hw;
-  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
-  const bool live = q < P;
-  const int b = live ? (int)(q / hw) : 0;
-  const int p = live ? (int)(q % hw) : 0;
-  Gate gt = {{0.f, 0.f, 0.f}};
-  if (live) gt = gate_at(grad + b * pvs, mask + b * pvs, H, W, h, w, p / w, p % w);
+  const long long ppt = ((P + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+  const long long q0 = (long long)blockIdx.x * ppt;
   const int c0 = blockIdx.y * kFuseCh;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int cc = 0; cc < kFuseCh; ++cc) {
-    const int c = c0 + cc;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (live && c < C) {
+  float acc[kFuseCh][4];
+#pragma unroll
+  for (int cc = 0; cc < kFuseCh; ++cc)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[cc][j] = 0.f;
+  for (long long q = q0 + threadIdx.x; q < q0 + ppt && q < P; q += 256) {
+    const int b = (int)(q / hw), p = (int)(q % hw);
+    const Gate gt = gate_at(grad + b * pvs, mask + b * pvs, H, W, h, w, p / w, p % w);
+#pragma unroll
+    for (int cc = 0; cc < kFuseCh; ++cc) {
+      const int c = c0 + cc;
+      if (c >= C) break;
       const float pre = bias[c] + wt[c * 3 + 0] * gt.g[0] + wt[c * 3 + 1] * gt.g[1] + wt[c * 3 + 2] * gt.g[2];
       const float d = pre > 0.f ? Num<T>::to_f(dout[((long long)b * C + c) * hw + p]) : 0.f;
-      v[0] = d;
-      v[1] = d * gt.g[0];
-      v[2] = d * gt.g[1];
-      v[3] = d * gt.g[2];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float s = wave_sum(v[j]);
-      if (lane == 0) red[wave][cc][j] = s;
+      acc[cc][0] += d;
+      acc[cc][1] += d * gt.g[0];
+      acc[cc][2] += d * gt.g[1];
+      acc[cc][3] += d * gt.g[2];
     }
   }
+#pragma unroll
+  for (int cc = 0; cc < kFuseCh; ++cc)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float s = wave_sum(acc[cc][j]);
+      if (lane == 0) red[wave][cc][j] = s;
+    }
   __syncthreads();
   if (threadIdx.x < kFuseCh * 4) {
     const int cc = threadIdx.x >> 2, j = threadIdx.x & 3;
@@ -284,7 +292,7 @@ int rgbd_dggm_fuse_fwd(int dtype, const void* cp1, const void* color, const floa
   return RGBD_OK;
 }
 
-static int dggm_bwd_tiles(int B, int h, int w) { return ceil_div((long long)B * h * w, 256); }
+static int dggm_bwd_tiles(int B, int h, int w) { return std::min(ceil_div((long long)B * h * w, 256), 64); }
 
 size_t rgbd_dggm_fuse_bwd_workspace_size(int B, int C, int h, int w) {
   return align256(sizeof(float) * 4 * (size_t)C * dggm_bwd_tiles(B, h, w));

@@ -39,6 +39,8 @@ struct ConvArgs {
   const void* residual;             // NCHW [B][N][Ho][Wo] added in the epilogue (optional)
   void* out_nchw;                   // optional
   void* out_nhwc;                   // optional
+  int ksplit;                       // v2 only: K split over (tap, chunk) ranges (1 = none)
+  float* partial;                   // v2 split-K slabs: f32 [ksplit][B][Ho][Wo][N]
 };
 
 constexpr int BM = 64, BN = 64;
@@ -491,10 +493,12 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave & 1, wn = wave >> 1;
+  const int nclass = a.transposed ? 4 : 1;
+  const int cls = blockIdx.z % nclass, split = blockIdx.z / nclass;
   int py = 0, px = 0, Hc = a.Ho, Wc = a.Wo;
   if (a.transposed) {
-    py = blockIdx.z >> 1;
-    px = blockIdx.z & 1;
+    py = cls >> 1;
+    px = cls & 1;
     Hc = (a.Ho - py + 1) >> 1;
     Wc = (a.Wo - px + 1) >> 1;
   }
@@ -557,13 +561,16 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
       taps[ntap++] = ky * 3 + kx;
     }
   const int nchunk = a.C / 32;
-  const int nsteps = ntap * nchunk * nseg;
+  // this split's (tap, chunk) range
+  const int tc_total = ntap * nchunk;
+  const int tc0 = (int)((long long)split * tc_total / a.ksplit), tc1 = (int)((long long)(split + 1) * tc_total / a.ksplit);
+  const int nsteps = (tc1 - tc0) * nseg;
   // B staging: 128 rows (n) x 4 pieces of 8 channels; thread -> pieces tid, tid + 256
   uint4 rbv[2];
 #define V2_BLOAD(STEP)                                                                            \
   {                                                                                               \
     const int st_ = (STEP);                                                                       \
-    const int sg_ = segs[st_ % nseg], tc_ = st_ / nseg;                                           \
+    const int sg_ = segs[st_ % nseg], tc_ = tc0 + st_ / nseg;                                     \
     const int tap_ = taps[tc_ / nchunk], ch_ = tc_ % nchunk;                                      \
     const long long koff_ = ((long long)sg_ * 9 + tap_) * a.C + ch_ * 32;                         \
     _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                               \
@@ -582,13 +589,15 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  V2_BLOAD(0);
-  V2_BSTORE(0);
+  if (nsteps > 0) {
+    V2_BLOAD(0);
+    V2_BSTORE(0);
+  }
   __syncthreads();
   Frag<bf16_t> A[4];
   uint32_t scode[4];
   for (int st = 0; st < nsteps; ++st) {
-    const int sgi = st % nseg, tc = st / nseg;
+    const int sgi = st % nseg, tc = tc0 + st / nseg;
     const int seg = segs[sgi];
     if (st + 1 < nsteps) V2_BLOAD(st + 1);
     if (sgi == 0) {  // new (tap, chunk): gather the A rows
@@ -631,6 +640,27 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
   }
 #undef V2_BLOAD
 #undef V2_BSTORE
+  if (a.ksplit > 1) {  // split-K: f32 slab, reduced + finished by k_splitk_finish
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const long long m = mblk + wm * 64 + 16 * mi + 4 * g + reg;
+        if (m >= Mtot) continue;
+        const int b = (int)(m / HWc);
+        const int rem = (int)(m % HWc);
+        const int i = rem / Wc, j = rem % Wc;
+        const int oy = a.transposed ? 2 * i + py : i;
+        const int ox = a.transposed ? 2 * j + px : j;
+        float* dst = a.partial + ((((long long)split * a.B + b) * a.Ho + oy) * a.Wo + ox) * a.N;
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) {
+          const int n = n0 + wn * 64 + 16 * nj + r;
+          if (n < a.N) dst[n] = acc[mi][nj][reg];
+        }
+      }
+    return;
+  }
   // ---- epilogue (same contract as k_conv_igemm)
   const bf16_t* res = (const bf16_t*)a.residual;
   bf16_t* onchw = (bf16_t*)a.out_nchw;
@@ -667,6 +697,63 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
   }
 }
 
+// split-K finish: sum the slabs in fixed order, add biases / residual, write NCHW (+NHWC) bf16.
+// One block per 32 pixels x 32 channels, transposed through LDS so both stores coalesce.
+__global__ __launch_bounds__(256) void k_splitk_finish(ConvArgs a) {
+  __shared__ float tile[32][33];
+  const long long P = (long long)a.B * a.Ho * a.Wo;
+  const long long p0 = (long long)blockIdx.x * 32;
+  const int n0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const long long HW = (long long)a.Ho * a.Wo;
+  for (int k = ty; k < 32; k += 8) {  // k: pixel within tile, tx: channel
+    const long long p = p0 + k;
+    const int n = n0 + tx;
+    float v = 0.f;
+    if (p < P && n < a.N) {
+      for (int sp = 0; sp < a.ksplit; ++sp) v += a.partial[((long long)sp * P + p) * a.N + n];
+      const int b = (int)(p / HW);
+      if (a.bias4) {
+        const int nm = a.info[b].n_masks;
+        float bs = 0.f;
+        for (int i = 0; i < nm; ++i) bs += a.bias4[i * a.N + n];
+        v += bs;
+      }
+      if (a.out_nhwc) {
+        // NHWC store wants the residual too: read it (NCHW, strided) here
+        if (a.residual) v += bf16_to_f32(((const bf16_t*)a.residual)[((long long)b * a.N + n) * HW + (p % HW)]);
+        ((bf16_t*)a.out_nhwc)[p * a.N + n] = f32_to_bf16(v);
+      } else if (a.residual) {
+        v += bf16_to_f32(((const bf16_t*)a.residual)[((long long)b * a.N + n) * HW + (p % HW)]);
+      }
+    }
+    tile[k][tx] = v;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {  // k: channel within tile, tx: pixel
+    const long long p = p0 + tx;
+    const int n = n0 + k;
+    if (p < P && n < a.N && a.out_nchw) {
+      const int b = (int)(p / HW);
+      ((bf16_t*)a.out_nchw)[((long long)b * a.N + n) * HW + (p % HW)] = f32_to_bf16(tile[tx][k]);
+    }
+  }
+}
+
+// split-K factor of the bf16 v2 path: enough workgroups to cover the chip ~3x
+int v2_ksplit(long long Mmax, int N, int nclass, int C, int transposed) {
+  const long long wgs = (long long)ceil_div(Mmax, V2M) * ceil_div(N, V2N) * nclass;
+  const int tc_min = (transposed ? 1 : 9) * (C / 32);
+  return (int)std::max<long long>(1, std::min<long long>(std::min(tc_min, 8), ceil_div(768, wgs)));
+}
+long long conv_mmax(const ConvArgs& a) {
+  return a.transposed ? (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2) : (long long)a.B * a.Ho * a.Wo;
+}
+size_t v2_partial_bytes(const ConvArgs& a) {
+  const int ks = v2_ksplit(conv_mmax(a), a.N, a.transposed ? 4 : 1, a.C, a.transposed);
+  return ks > 1 ? align256((size_t)ks * a.B * a.Ho * a.Wo * a.N * sizeof(float)) : 0;
+}
+
 template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   TimerScope ts(a.transposed ? "dsam_dx" : "dsam_fwd", s);
@@ -675,8 +762,14 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   if (a.transposed) Mmax = (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2);
   if constexpr (sizeof(T) == 2) {
     if (a.C % 32 == 0 && a.nseg == 5) {
-      dim3 grid2(ceil_div(Mmax, V2M), ceil_div(a.N, V2N), nclass);
-      k_conv_igemm_v2<<<grid2, 256, 0, s>>>(a);
+      ConvArgs b = a;
+      b.ksplit = v2_ksplit(Mmax, a.N, nclass, a.C, a.transposed);
+      dim3 grid2(ceil_div(Mmax, V2M), ceil_div(a.N, V2N), nclass * b.ksplit);
+      k_conv_igemm_v2<<<grid2, 256, 0, s>>>(b);
+      if (b.ksplit > 1) {
+        dim3 g3(ceil_div((long long)a.B * a.Ho * a.Wo, 32), ceil_div(a.N, 32));
+        k_splitk_finish<<<g3, 256, 0, s>>>(b);
+      }
       RGBD_CHECK_LAUNCH();
       return RGBD_OK;
     }
@@ -729,19 +822,40 @@ int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, 
   return RGBD_OK;
 }
 
-int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
-                  int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
-                  const void* residual, void* out_nchw, void* out_nhwc, void* stream) {
-  RGBD_REQUIRE(x_nhwc && code && info && wfwd && bias && (out_nchw || out_nhwc), RGBD_E_ARG);
-  RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
-  RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
+static ConvArgs fwd_args(int B, int Cin, int h, int w, int Cout) {
   ConvArgs a = {};
-  a.x = x_nhwc; a.code = code; a.w = wfwd;
   a.B = B; a.Hi = h; a.Wi = w; a.C = Cin;
   a.Ho = (h + 1) / 2; a.Wo = (w + 1) / 2; a.N = Cout;
   a.KH = 3; a.KW = 3; a.stride = 2; a.pad = 1;
-  a.nseg = 5; a.mask_mode = MASK_SRC; a.transposed = 0;
+  a.nseg = 5; a.mask_mode = MASK_SRC; a.transposed = 0; a.ksplit = 1;
+  return a;
+}
+static ConvArgs dx_args(int B, int Cin, int h, int w, int Cout) {
+  ConvArgs a = {};
+  a.B = B; a.Hi = (h + 1) / 2; a.Wi = (w + 1) / 2; a.C = Cout;
+  a.Ho = h; a.Wo = w; a.N = Cin;
+  a.KH = 3; a.KW = 3; a.stride = 2; a.pad = 1;
+  a.nseg = 5; a.mask_mode = MASK_DST; a.transposed = 1; a.ksplit = 1;
+  return a;
+}
+
+size_t rgbd_dsam_conv_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout) {
+  if (dtype != RGBD_BF16 || B <= 0 || h <= 0 || w <= 0) return 256;
+  return std::max<size_t>(256, std::max(v2_partial_bytes(fwd_args(B, Cin, h, w, Cout)),
+                                        v2_partial_bytes(dx_args(B, Cin, h, w, Cout))));
+}
+
+int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                  int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
+                  const void* residual, void* out_nchw, void* out_nhwc, void* ws, void* stream) {
+  RGBD_REQUIRE(x_nhwc && code && info && wfwd && bias && (out_nchw || out_nhwc), RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
+  ConvArgs a = fwd_args(B, Cin, h, w, Cout);
+  a.x = x_nhwc; a.code = code; a.w = wfwd;
   a.bias4 = bias; a.info = info; a.residual = residual; a.out_nchw = out_nchw; a.out_nhwc = out_nhwc;
+  a.partial = (float*)ws;
+  RGBD_REQUIRE(ws || dtype != RGBD_BF16 || v2_partial_bytes(a) == 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32) return launch_conv<float>(a, s);
   if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);
@@ -750,17 +864,15 @@ int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd
 
 int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
                        int w, int Cout, const void* wbwd, const void* gin_nchw, void* dx_nchw,
-                       void* dx_nhwc, void* stream) {
+                       void* dx_nhwc, void* ws, void* stream) {
   RGBD_REQUIRE(gout_nhwc && code && wbwd && (dx_nchw || dx_nhwc), RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
   RGBD_REQUIRE(Cout % 8 == 0, RGBD_E_SHAPE);
-  ConvArgs a = {};
+  ConvArgs a = dx_args(B, Cin, h, w, Cout);
   a.x = gout_nhwc; a.code = code; a.w = wbwd;
-  a.B = B; a.Hi = (h + 1) / 2; a.Wi = (w + 1) / 2; a.C = Cout;
-  a.Ho = h; a.Wo = w; a.N = Cin;
-  a.KH = 3; a.KW = 3; a.stride = 2; a.pad = 1;
-  a.nseg = 5; a.mask_mode = MASK_DST; a.transposed = 1;
   a.residual = gin_nchw; a.out_nchw = dx_nchw; a.out_nhwc = dx_nhwc;
+  a.partial = (float*)ws;
+  RGBD_REQUIRE(ws || dtype != RGBD_BF16 || v2_partial_bytes(a) == 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32) return launch_conv<float>(a, s);
   if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);

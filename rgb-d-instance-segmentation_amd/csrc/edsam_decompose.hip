@@ -295,6 +295,20 @@ __global__ __launch_bounds__(256) void k_codes_pool(const float* __restrict__ de
   code[(long long)b * oh * ow + q] = (uint8_t)c;
 }
 
+// OR-pool a finer code plane into a coarser one when the adaptive bins nest exactly
+// (H_in % H_out == 0, W_in % W_out == 0): identical to pooling the full-resolution masks.
+__global__ __launch_bounds__(256) void k_codes_or_pool(const uint8_t* __restrict__ fine, int fh, int fw,
+                                                       int oh, int ow, uint8_t* __restrict__ code) {
+  const int b = blockIdx.y;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= oh * ow) return;
+  const int i = q / ow, j = q % ow, sy = fh / oh, sx = fw / ow;
+  uint32_t c = 0u;
+  for (int y = i * sy; y < (i + 1) * sy; ++y)
+    for (int x = j * sx; x < (j + 1) * sx; ++x) c |= fine[((long long)b * fh + y) * fw + x];
+  code[(long long)b * oh * ow + q] = (uint8_t)c;
+}
+
 }  // namespace
 
 extern "C" {
@@ -324,9 +338,18 @@ int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_
   k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w, info);
   k_peaks<<<B, 512, 0, st>>>(w, ratio, info);
   for (int s = 0; s < n_scales; ++s) {
-    dim3 g2(ceil_div((long long)out_h_host[s] * out_w_host[s], 256), B);
-    k_codes_pool<<<g2, 256, 0, st>>>(depth3, batch_stride, H, W, nch, out_h_host[s], out_w_host[s], info,
-                                     codes_host[s]);
+    const int oh = out_h_host[s], ow = out_w_host[s];
+    dim3 g2(ceil_div((long long)oh * ow, 256), B);
+    // a previous (finer) scale whose bins nest exactly into this one's: pool its codes
+    int src = -1;
+    for (int t = 0; t < s; ++t) {
+      const int fh = out_h_host[t], fw = out_w_host[t];
+      if (fh >= oh && fw >= ow && fh % oh == 0 && fw % ow == 0 && H % fh == 0 && W % fw == 0) src = t;
+    }
+    if (src >= 0)
+      k_codes_or_pool<<<g2, 256, 0, st>>>(codes_host[src], out_h_host[src], out_w_host[src], oh, ow, codes_host[s]);
+    else
+      k_codes_pool<<<g2, 256, 0, st>>>(depth3, batch_stride, H, W, nch, oh, ow, info, codes_host[s]);
   }
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;

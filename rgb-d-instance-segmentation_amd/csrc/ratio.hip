@@ -983,33 +983,51 @@ __global__ void k_rp_pool_finish(const float* __restrict__ part, int B, int H, i
   pooled[e] = s / (float)cnt;
 }
 
-__global__ __launch_bounds__(256) void k_rp_tail_conv(const float* __restrict__ pooled, int B,
+__global__ __launch_bounds__(512) void k_rp_tail_conv(const float* __restrict__ pooled, int B,
                                                       const char* __restrict__ blob, Layout L,
                                                       float* __restrict__ z6) {
-  // z6[b][512][16] = conv3x3 pad1 (pooled 4x4) + b6 ; grid.x = 512/8 output-channel groups,
-  // thread = (b, pos) pair (B*16 <= 512 threads handled by a 2-pass loop)
+  // z6[b][512][16] = conv3x3 pad1 (pooled 4x4) + b6.  grid.x = 512/8 output-channel groups;
+  // thread = ((b, pos) pair, input-channel quarter); the 4 quarters are summed in fixed order.
+  __shared__ float red[4][128][8];
   const float* w6 = (const float*)(blob + L.w6);
   const float* b6 = (const float*)(blob + L.b6);
   const int o0 = blockIdx.x * 8;
-  for (int bp = threadIdx.x; bp < B * 16; bp += 256) {
-    const int bb = bp / 16, pos = bp % 16, py = pos / 4, px = pos % 4;
+  const int kq = threadIdx.x >> 7, lbp = threadIdx.x & 127;
+  for (int base = 0; base < B * 16; base += 128) {
+    const int bp = base + lbp;
     float acc[8];
 #pragma unroll
-    for (int o = 0; o < 8; ++o) acc[o] = b6[o0 + o];
-    for (int c = 0; c < C5; ++c)
-      for (int ky = 0; ky < 3; ++ky) {
-        const int yy = py + ky - 1;
-        if (yy < 0 || yy >= 4) continue;
-        for (int kx = 0; kx < 3; ++kx) {
-          const int xx = px + kx - 1;
-          if (xx < 0 || xx >= 4) continue;
-          const float v = pooled[((long long)bb * C5 + c) * 16 + yy * 4 + xx];
+    for (int o = 0; o < 8; ++o) acc[o] = 0.f;
+    if (bp < B * 16) {
+      const int bb = bp / 16, pos = bp % 16, py = pos / 4, px = pos % 4;
+      for (int c = kq * 64; c < kq * 64 + 64; ++c) {
+        const float* pin = pooled + ((long long)bb * C5 + c) * 16;
 #pragma unroll
-          for (int o = 0; o < 8; ++o) acc[o] += w6[(((long long)(o0 + o) * C5 + c) * 3 + ky) * 3 + kx] * v;
+        for (int ky = 0; ky < 3; ++ky) {
+          const int yy = py + ky - 1;
+          if (yy < 0 || yy >= 4) continue;
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int xx = px + kx - 1;
+            if (xx < 0 || xx >= 4) continue;
+            const float v = pin[yy * 4 + xx];
+#pragma unroll
+            for (int o = 0; o < 8; ++o) acc[o] += w6[(((long long)(o0 + o) * C5 + c) * 3 + ky) * 3 + kx] * v;
+          }
         }
       }
+    }
 #pragma unroll
-    for (int o = 0; o < 8; ++o) z6[((long long)bb * C6 + o0 + o) * 16 + pos] = acc[o];
+    for (int o = 0; o < 8; ++o) red[kq][lbp][o] = acc[o];
+    __syncthreads();
+    if (kq == 0 && bp < B * 16) {
+      const int bb = bp / 16, pos = bp % 16;
+#pragma unroll
+      for (int o = 0; o < 8; ++o)
+        z6[((long long)bb * C6 + o0 + o) * 16 + pos] =
+            b6[o0 + o] + (((red[0][lbp][o] + red[1][lbp][o]) + red[2][lbp][o]) + red[3][lbp][o]);
+    }
+    __syncthreads();
   }
 }
 
@@ -1209,7 +1227,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
                                 bn.p[19], aff5);
   k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
   k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
-  k_rp_tail_conv<<<C6 / 8, 256, 0, s>>>(pooled, B, blob, L, z6);
+  k_rp_tail_conv<<<C6 / 8, 512, 0, s>>>(pooled, B, blob, L, z6);
   k_rp_tail_mlp<<<1, 512, 0, s>>>(z6, B, training, momentum, blob, L, bn, seed, ratio);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;

@@ -201,9 +201,11 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     out = torch.empty((B, Co, ho, wo), dtype=x_nhwc.dtype, device=x_nhwc.device)
     out_nhwc = torch.empty((B, ho, wo, Co), dtype=x_nhwc.dtype, device=x_nhwc.device) if want_nhwc else None
     b4 = bias4.detach().float().contiguous()
-    check(_lib.lib().rgbd_dsam_fwd(_dtype_code(x_nhwc), _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co,
-                                   _p(wfwd), _p(b4), _p(residual), _p(out), _p(out_nhwc),
-                                   _stream(x_nhwc.device)), "rgbd_dsam_fwd")
+    L = _lib.lib()
+    dt = _dtype_code(x_nhwc)
+    ws = _workspace(x_nhwc.device, L.rgbd_dsam_conv_workspace_size(dt, B, Ci, h, w, Co), "dsam_conv")
+    check(L.rgbd_dsam_fwd(dt, _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co, _p(wfwd), _p(b4), _p(residual),
+                          _p(out), _p(out_nhwc), _p(ws), _stream(x_nhwc.device)), "rgbd_dsam_fwd")
     return out, out_nhwc
 
 
@@ -216,9 +218,11 @@ def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False):
         raise ValueError("gin shape mismatch")
     dx = torch.empty((B, Ci, h, w), dtype=gout_nhwc.dtype, device=gout_nhwc.device)
     dx_nhwc = torch.empty((B, h, w, Ci), dtype=gout_nhwc.dtype, device=gout_nhwc.device) if want_nhwc else None
-    check(_lib.lib().rgbd_dsam_bwd_data(_dtype_code(gout_nhwc), _p(gout_nhwc), _p(code), B, Ci, h, w, Co,
-                                        _p(wbwd), _p(gin_nchw), _p(dx), _p(dx_nhwc), _stream(gout_nhwc.device)),
-          "rgbd_dsam_bwd_data")
+    L = _lib.lib()
+    dt = _dtype_code(gout_nhwc)
+    ws = _workspace(gout_nhwc.device, L.rgbd_dsam_conv_workspace_size(dt, B, Ci, h, w, Co), "dsam_conv")
+    check(L.rgbd_dsam_bwd_data(dt, _p(gout_nhwc), _p(code), B, Ci, h, w, Co, _p(wbwd), _p(gin_nchw), _p(dx),
+                               _p(dx_nhwc), _p(ws), _stream(gout_nhwc.device)), "rgbd_dsam_bwd_data")
     return dx, dx_nhwc
 
 

@@ -27,10 +27,10 @@ def test_argument_validation_without_device():
     null = ctypes.c_void_p(0)
     # null pointers / bad sizes are rejected on the host with RGBD_E_ARG, nothing launched
     assert L.rgbd_assemble_pixel_values(null, null, 1, 4, 4, null, null, null) == -1
-    assert L.rgbd_dsam_fwd(0, null, null, null, 1, 32, 8, 8, 64, null, null, null, null, null, null) == -1
+    assert L.rgbd_dsam_fwd(0, null, null, null, 1, 32, 8, 8, 64, null, null, null, null, null, null, null) == -1
     fake = ctypes.c_void_p(0x1000)
     # Cin not a multiple of 8 -> unsupported shape
-    assert L.rgbd_dsam_fwd(0, fake, fake, fake, 1, 12, 8, 8, 64, fake, fake, null, fake, null, null) == -2
+    assert L.rgbd_dsam_fwd(0, fake, fake, fake, 1, 12, 8, 8, 64, fake, fake, null, fake, null, null, null) == -2
     # unknown dtype
     assert L.rgbd_nchw_to_nhwc(7, fake, fake, 1, 1, 1, 1, null) == -3
 
