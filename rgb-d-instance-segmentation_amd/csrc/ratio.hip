@@ -812,8 +812,10 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict_
     const int b = (int)(tile / ((long long)tiles_x * tiles_y));
     const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
     const int y0 = (trem / tiles_x) * CV_TH, x0 = (trem % tiles_x) * CV_TW;
-    // staging: A pieces (halo pixel, 8-ch chunk) and B pieces (n, 8-ch chunk), ids tid and tid+512
-    uint4 ra0, ra1, rb0, rb1;
+    // staging: A pieces (halo pixel, 8-ch chunk) and B pieces (n, 8-ch chunk), ids tid and tid+512.
+    // B is prefetched two steps ahead through a 2-deep register ring (sets E/O for even/odd
+    // steps; the step loop is unrolled by 2 so the ring index is static).
+    uint4 ra0, ra1, rbE0, rbE1, rbO0, rbO1;
 #define V2_LOAD_A1(ID, R, CHUNK)                                                                      \
   {                                                                                                   \
     R = make_uint4(0u, 0u, 0u, 0u);                                                                   \
@@ -837,49 +839,53 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict_
     __syncthreads();  // previous tile's epilogue done with the LDS
     V2_LOAD_A1(tid, ra0, 0);
     V2_LOAD_A1(tid + 512, ra1, 0);
-    V2_LOAD_B1(tid, rb0, 0);
-    V2_LOAD_B1(tid + 512, rb1, 0);
+    V2_LOAD_B1(tid, rbE0, 0);
+    V2_LOAD_B1(tid + 512, rbE1, 0);
+    V2_LOAD_B1(tid, rbO0, 1);
+    V2_LOAD_B1(tid + 512, rbO1, 1);
     V2_STORE_A1(tid, ra0, 0);
     V2_STORE_A1(tid + 512, ra1, 0);
-    V2_STORE_B1(tid, rb0, 0);
-    V2_STORE_B1(tid + 512, rb1, 0);
+    V2_STORE_B1(tid, rbE0, 0);
+    V2_STORE_B1(tid + 512, rbE1, 0);
     __syncthreads();
+#define V2_STEP(STEP, CUR0, CUR1, NXT0, NXT1)                                                   \
+  {                                                                                             \
+    const int step_ = (STEP);                                                                   \
+    const int chunk = step_ / 9, tap = step_ % 9;                                               \
+    if (step_ + 2 < 36) {                                                                       \
+      V2_LOAD_B1(tid, CUR0, step_ + 2);                                                         \
+      V2_LOAD_B1(tid + 512, CUR1, step_ + 2);                                                   \
+    }                                                                                           \
+    if (tap == 0 && chunk + 1 < 4) {                                                            \
+      V2_LOAD_A1(tid, ra0, chunk + 1);                                                          \
+      V2_LOAD_A1(tid + 512, ra1, chunk + 1);                                                    \
+    }                                                                                           \
+    const int ky = tap / 3, kx = tap % 3;                                                       \
+    Frag<bf16_t> af[4], bfr[4];                                                                 \
+    _Pragma("unroll") for (int mi = 0; mi < 4; ++mi) {                                          \
+      const int ty = wm * 2 + (mi >> 1), tx = (mi & 1) * 16 + r;                                \
+      af[mi].v = *reinterpret_cast<const uint4*>(&sA[chunk & 1][(ty + ky) * CV_PW + tx + kx][8 * g]); \
+    }                                                                                           \
+    _Pragma("unroll") for (int nj = 0; nj < 4; ++nj)                                            \
+      bfr[nj].v = *reinterpret_cast<const uint4*>(&sB[step_ & 1][wn * 64 + 16 * nj + r][8 * g]); \
+    _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                            \
+      _Pragma("unroll") for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], af[mi], bfr[nj]);       \
+    if (step_ + 1 < 36) {                                                                       \
+      V2_STORE_B1(tid, NXT0, (step_ + 1) & 1);                                                  \
+      V2_STORE_B1(tid + 512, NXT1, (step_ + 1) & 1);                                            \
+    }                                                                                           \
+    if (tap == 8 && chunk + 1 < 4) {                                                            \
+      V2_STORE_A1(tid, ra0, (chunk + 1) & 1);                                                   \
+      V2_STORE_A1(tid + 512, ra1, (chunk + 1) & 1);                                             \
+    }                                                                                           \
+    __syncthreads();                                                                            \
+  }
 #pragma unroll 1
-    for (int step = 0; step < 36; ++step) {
-      const int chunk = step / 9, tap = step % 9;
-      const bool more = step + 1 < 36;
-      if (more) {
-        V2_LOAD_B1(tid, rb0, step + 1);
-        V2_LOAD_B1(tid + 512, rb1, step + 1);
-      }
-      if (tap == 0 && chunk + 1 < 4) {
-        V2_LOAD_A1(tid, ra0, chunk + 1);
-        V2_LOAD_A1(tid + 512, ra1, chunk + 1);
-      }
-      const int ky = tap / 3, kx = tap % 3;
-      Frag<bf16_t> af[4], bfr[4];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int ty = wm * 2 + (mi >> 1), tx = (mi & 1) * 16 + r;
-        af[mi].v = *reinterpret_cast<const uint4*>(&sA[chunk & 1][(ty + ky) * CV_PW + tx + kx][8 * g]);
-      }
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj)
-        bfr[nj].v = *reinterpret_cast<const uint4*>(&sB[step & 1][wn * 64 + 16 * nj + r][8 * g]);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], af[mi], bfr[nj]);
-      if (more) {
-        V2_STORE_B1(tid, rb0, (step + 1) & 1);
-        V2_STORE_B1(tid + 512, rb1, (step + 1) & 1);
-      }
-      if (tap == 8 && chunk + 1 < 4) {
-        V2_STORE_A1(tid, ra0, (chunk + 1) & 1);
-        V2_STORE_A1(tid + 512, ra1, (chunk + 1) & 1);
-      }
-      __syncthreads();
+    for (int step = 0; step < 36; step += 2) {
+      V2_STEP(step, rbE0, rbE1, rbO0, rbO1);      // even step: ring slot E refills with step+2
+      V2_STEP(step + 1, rbO0, rbO1, rbE0, rbE1);  // odd step: slot O refills with step+3
     }
+#undef V2_STEP
     // ---- epilogue: bias + stats, stage the bf16 tile in LDS as [px][256] (row 528 B)
     bf16_t(*sY)[C5 + 8] = reinterpret_cast<bf16_t(*)[C5 + 8]>(smem);
 #pragma unroll
