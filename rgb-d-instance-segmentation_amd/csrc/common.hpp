@@ -78,6 +78,15 @@ __device__ __forceinline__ P opaque(P p) {
   return (P)u;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads/stores (__syncthreads() also drains vmcnt, which would serialise
+// every register-prefetched global load and every epilogue store with the barrier).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 

@@ -593,7 +593,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
     V2_BLOAD(0);
     V2_BSTORE(0);
   }
-  __syncthreads();
+  lds_barrier();
   Frag<bf16_t> A[4];
   uint32_t scode[4];
   for (int st = 0; st < nsteps; ++st) {
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
       for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], As[mi], bf);
     }
     if (st + 1 < nsteps) V2_BSTORE((st + 1) & 1);
-    __syncthreads();
+    lds_barrier();
   }
 #undef V2_BLOAD
 #undef V2_BSTORE

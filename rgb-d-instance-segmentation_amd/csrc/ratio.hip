@@ -836,7 +836,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict_
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __syncthreads();  // previous tile's epilogue done with the LDS
+    lds_barrier();  // previous tile's epilogue done with the LDS
     V2_LOAD_A1(tid, ra0, 0);
     V2_LOAD_A1(tid + 512, ra1, 0);
     V2_LOAD_B1(tid, rbE0, 0);
@@ -847,7 +847,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict_
     V2_STORE_A1(tid + 512, ra1, 0);
     V2_STORE_B1(tid, rbE0, 0);
     V2_STORE_B1(tid + 512, rbE1, 0);
-    __syncthreads();
+    lds_barrier();
 #define V2_STEP(STEP, CUR0, CUR1, NXT0, NXT1)                                                   \
   {                                                                                             \
     const int step_ = (STEP);                                                                   \
@@ -878,7 +878,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict_
       V2_STORE_A1(tid, ra0, (chunk + 1) & 1);                                                   \
       V2_STORE_A1(tid + 512, ra1, (chunk + 1) & 1);                                             \
     }                                                                                           \
-    __syncthreads();                                                                            \
+    lds_barrier();                                                                            \
   }
 #pragma unroll 1
     for (int step = 0; step < 36; step += 2) {
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict_
         st[wm][n][1] += sq;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // 128 px x 512 B = 4096 16-byte pieces
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -929,7 +929,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict_
             *reinterpret_cast<const uint4*>(&sY[px][8 * q]);
     }
   }
-  __syncthreads();
+  lds_barrier();
   for (int i = tid; i < C5; i += 512)
 #pragma unroll
     for (int q = 0; q < 2; ++q) slab[((long long)blockIdx.x * C5 + i) * 2 + q] = st[0][i][q] + st[1][i][q];
