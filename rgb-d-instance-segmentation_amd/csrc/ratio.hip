@@ -389,6 +389,24 @@ __global__ __launch_bounds__(256) void k_rp_chain(const float* __restrict__ dept
   }
 }
 
+// Butterfly reduce-scatter of N per-lane values over the 16 lanes sharing lane>>4: after the
+// call, v[i] (i < N/16) of lane r holds the 16-lane sum of original value
+// (r&1)N/2 + ((r>>1)&1)N/4 + ((r>>2)&1)N/8 + ((r>>3)&1)N/16 + i.
+template <int N>
+__device__ __forceinline__ void reduce_scatter16(float (&v)[N], int r) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int n = N >> k, half = n >> 1;
+    const bool hi = (r >> k) & 1;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float a = v[i], b = v[i + half];
+      const float keep = hi ? b : a, send = hi ? a : b;
+      v[i] = keep + __shfl_xor(send, 1 << k);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ chain v2 (bf16)
 // 512 threads = 8 waves; persistent; ALL chain weights (143 KB bf16) live in LDS for the
 // workgroup's lifetime; a wave owns 32 pixels (one row of a 8x32 tile, two 16-px MFMA
@@ -464,26 +482,49 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
       ktab[k] = v;
     }
   }
+  // BN statistics (phases 0/1): per tile, each lane's (channel, {sum, sumsq}) values are
+  // reduce-scattered over the 16 pixel lanes (4 butterfly rounds), so a lane keeps only
+  // NV/16 running sums across tiles instead of NV.
   constexpr int NST = PHASE == 0 ? 12 : 8;  // channel tiles whose stats this phase collects
-  float ssum[NST][4], ssq[NST][4];
+  constexpr int NV = NST * 4 * 2, NKEEP = NV / 16;
+  float stat[NKEEP];
 #pragma unroll
-  for (int t = 0; t < NST; ++t)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) ssum[t][j] = ssq[t][j] = 0.f;
+  for (int i = 0; i < NKEEP; ++i) stat[i] = 0.f;
   const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
   const long long ntiles = (long long)B * tiles_x * tiles_y;
   const long long HW = (long long)H * W;
+  // the next tile's depth patch is prefetched into registers while the current one computes
+  constexpr int PATCH_N = 3 * C2W_PH * C2W_PW, PATCH_PER = (PATCH_N + 511) / 512;
+  float pre[PATCH_PER];
+  auto fetch_patch = [&](long long t) {
+    const int b = (int)(t / ((long long)tiles_x * tiles_y));
+    const int trem = (int)(t % ((long long)tiles_x * tiles_y));
+    const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
+#pragma unroll
+    for (int k = 0; k < PATCH_PER; ++k) {
+      const int i = tid + 512 * k;
+      float v = 0.f;
+      if (i < PATCH_N && t < ntiles) {
+        const int c = i / (C2W_PH * C2W_PW), yy = (i / C2W_PW) % C2W_PH, xx = i % C2W_PW;
+        const int yv = y0 + yy - 3, xv = x0 + xx - 3;
+        if (yv >= 0 && yv < H && xv >= 0 && xv < W) v = depth3[b * bstride + c * HW + (long long)yv * W + xv];
+      }
+      pre[k] = v;
+    }
+  };
+  fetch_patch(blockIdx.x);
   for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int b = (int)(tile / ((long long)tiles_x * tiles_y));
     const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
     const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
-    __syncthreads();
-    for (int i = tid; i < 3 * C2W_PH * C2W_PW; i += 512) {
-      const int c = i / (C2W_PH * C2W_PW), yy = (i / C2W_PW) % C2W_PH, xx = i % C2W_PW;
-      const int yv = y0 + yy - 3, xv = x0 + xx - 3;
-      patch[i] = (yv >= 0 && yv < H && xv >= 0 && xv < W) ? depth3[b * bstride + c * HW + (long long)yv * W + xv] : 0.f;
+    lds_barrier();  // everyone is done with the previous patch
+#pragma unroll
+    for (int k = 0; k < PATCH_PER; ++k) {
+      const int i = tid + 512 * k;
+      if (i < PATCH_N) patch[i] = pre[k];
     }
-    __syncthreads();
+    lds_barrier();
+    fetch_patch(tile + gridDim.x);
     const int py = y0 + wave;
     bool pv[2];
 #pragma unroll
@@ -526,14 +567,18 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
         a1[t][1][j] += bb;
       }
     if constexpr (PHASE == 0) {
+      float v[NV];
 #pragma unroll
       for (int t = 0; t < 12; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float v0 = pv[0] ? a1[t][0][j] : 0.f, v1 = pv[1] ? a1[t][1][j] : 0.f;
-          ssum[t][j] += v0 + v1;
-          ssq[t][j] += v0 * v0 + v1 * v1;
+          v[(t * 4 + j) * 2 + 0] = v0 + v1;
+          v[(t * 4 + j) * 2 + 1] = v0 * v0 + v1 * v1;
         }
+      reduce_scatter16<NV>(v, r);
+#pragma unroll
+      for (int i = 0; i < NKEEP; ++i) stat[i] += v[i];
       continue;
     }
     Frag<bf16_t> f1[6][2];
@@ -570,14 +615,18 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
       }
     }
     if constexpr (PHASE == 1) {
+      float v[NV];
 #pragma unroll
       for (int t = 0; t < 8; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float v0 = pv[0] ? a2[t][0][j] : 0.f, v1 = pv[1] ? a2[t][1][j] : 0.f;
-          ssum[t][j] += v0 + v1;
-          ssq[t][j] += v0 * v0 + v1 * v1;
+          v[(t * 4 + j) * 2 + 0] = v0 + v1;
+          v[(t * 4 + j) * 2 + 1] = v0 * v0 + v1 * v1;
         }
+      reduce_scatter16<NV>(v, r);
+#pragma unroll
+      for (int i = 0; i < NKEEP; ++i) stat[i] += v[i];
       continue;
     }
     if constexpr (PHASE == 2) {
@@ -656,23 +705,17 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
     }
   }
   if constexpr (PHASE < 2) {
-    // reduce each lane's channel sums over the 16 pixel lanes; lanes r == 0 write the slab
+    // lane (r, g) holds original values [base, base + NKEEP) of the (t, j, q) ordering
     const long long row = (long long)blockIdx.x * 8 + wave;
     constexpr int NC = PHASE == 0 ? STEM_C : FUS_C;
+    const int base = ((r & 1) * (NV / 2)) + (((r >> 1) & 1) * (NV / 4)) + (((r >> 2) & 1) * (NV / 8)) +
+                     (((r >> 3) & 1) * (NV / 16));
 #pragma unroll
-    for (int t = 0; t < NST; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = ssum[t][j], q = ssq[t][j];
-        for (int o = 1; o < 16; o <<= 1) {
-          v += __shfl_xor(v, o);
-          q += __shfl_xor(q, o);
-        }
-        if (r == 0) {
-          slab[(row * NC + 16 * t + 4 * g + j) * 2 + 0] = v;
-          slab[(row * NC + 16 * t + 4 * g + j) * 2 + 1] = q;
-        }
-      }
+    for (int i = 0; i < NKEEP; ++i) {
+      const int L = base + i, tj = L >> 1, q = L & 1;
+      const int ch = 16 * (tj >> 2) + 4 * g + (tj & 3);
+      slab[(row * NC + ch) * 2 + q] = stat[i];
+    }
   }
 }
 
