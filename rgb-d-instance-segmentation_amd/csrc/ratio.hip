@@ -32,7 +32,9 @@ constexpr int NBN = 6;  // BN layers: scale1, scale2, scale3, fusion, fe.1, fe.5
 constexpr float BN_EPS = 1e-5f;
 
 struct Layout {  // byte offsets into the packed blob
-  size_t w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, w7, b7, w8, b8, w9, b9, w10, b10, total;
+  size_t w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, w7, b7, w8, b8, w9, b9, w10, b10;
+  size_t w5s, zero;  // bf16: conv5 weights in LDS-DMA step order; 256 zero bytes (padding source)
+  size_t total;
 };
 
 inline Layout make_layout(int es) {
@@ -63,6 +65,8 @@ inline Layout make_layout(int es) {
   L.b9 = seg(32 * 4);
   L.w10 = seg(32 * 4);
   L.b10 = seg(4);
+  L.w5s = seg(es == 2 ? (size_t)C5 * 9 * FUS_C * 2 : 0);
+  L.zero = seg(256);
   L.total = o;
   return L;
 }
@@ -115,6 +119,18 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
     w5[e] = Num<T>::from_f(w.p[12][(o * FUS_C + c) * 9 + tap]);
   }
   for (int e = tid; e < C5; e += nth) ((float*)(blob + L.b5))[e] = w.p[13][e];
+  if constexpr (sizeof(T) == 2) {
+    // K-step order for k_rp_conv3x3_v3: [step = half*9 + tap][n][64 ch], each 128-byte row
+    // holding its 16-byte chunks in the LDS swizzle order (slot q <- chunk q ^ (n & 6)), so one
+    // LDS-DMA copy of a step is linear.
+    bf16_t* w5s = (bf16_t*)(blob + L.w5s);
+    for (int e = tid; e < C5 * 9 * FUS_C; e += nth) {
+      const int st = e / (C5 * 64), n = (e / 64) % C5, q = (e % 64) / 8, k = e % 8;
+      const int half = st / 9, tap = st % 9, c = 64 * half + 8 * (q ^ (n & 6)) + k;
+      w5s[e] = f32_to_bf16(w.p[12][(n * FUS_C + c) * 9 + tap]);
+    }
+  }
+  for (int e = tid; e < 64; e += nth) ((float*)(blob + L.zero))[e] = 0.f;
   // tail + MLP stay float32 in reference layout
   auto copy = [&](const float* src, size_t off, int n) {
     for (int e = tid; e < n; e += nth) ((float*)(blob + off))[e] = src[e];
@@ -825,160 +841,6 @@ __global__ __launch_bounds__(256) void k_rp_conv3x3(const T* __restrict__ x, int
   }
 }
 
-// ------------------------------------------------------------------ conv5 v2 (bf16)
-// 512 threads = 8 waves as 2 (pixels) x 4 (channels); workgroup tile 128 px (4x32) x all 256
-// output channels; wave tile 64 px x 64 ch (4x4 MFMA 16x16x32).  K = 36 steps of (tap, 32-ch
-// chunk).  Both operands staged in LDS with 80-byte rows (conflict-free ds_read_b128 for a
-// 16-row fragment), B (weights) double-buffered per step, A (6x34 halo patch) per chunk;
-// the next step's global loads are issued before the current step's MFMAs and written to LDS
-// after them (register staging, one barrier per step).  Epilogue: bias, BN partial sums, and
-// y (NHWC bf16) re-laid out through LDS so each lane stores 16 contiguous bytes.
-constexpr int V2_ROW = 40;  // 32 ch + 8 pad = 80-byte rows
-constexpr int V2_NPIX = CV_PH * CV_PW;  // 204 halo pixels
-
-__global__ __launch_bounds__(512) void k_rp_conv3x3_v2(const bf16_t* __restrict__ x, int B, int H, int W,
-                                                       const char* __restrict__ blob, Layout L,
-                                                       bf16_t* __restrict__ y, float* __restrict__ slab) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t(*sA)[V2_NPIX][V2_ROW] = reinterpret_cast<bf16_t(*)[V2_NPIX][V2_ROW]>(smem);
-  bf16_t(*sB)[C5][V2_ROW] = reinterpret_cast<bf16_t(*)[C5][V2_ROW]>(smem + 2 * V2_NPIX * V2_ROW * 2);
-  float(*st)[C5][2] = reinterpret_cast<float(*)[C5][2]>(smem + 2 * V2_NPIX * V2_ROW * 2 + 2 * C5 * V2_ROW * 2);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int wm = wave & 1, wn = wave >> 1;
-  const bf16_t* w5 = (const bf16_t*)(blob + L.w5);
-  const float* b5 = (const float*)(blob + L.b5);
-  const int tiles_x = (W + CV_TW - 1) / CV_TW, tiles_y = (H + CV_TH - 1) / CV_TH;
-  const long long ntiles = (long long)B * tiles_x * tiles_y;
-  for (int i = tid; i < 2 * C5 * 2; i += 512) (&st[0][0][0])[i] = 0.f;
-  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
-    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
-    const int y0 = (trem / tiles_x) * CV_TH, x0 = (trem % tiles_x) * CV_TW;
-    // staging: A pieces (halo pixel, 8-ch chunk) and B pieces (n, 8-ch chunk), ids tid and tid+512.
-    // B is prefetched two steps ahead through a 2-deep register ring (sets E/O for even/odd
-    // steps; the step loop is unrolled by 2 so the ring index is static).
-    uint4 ra0, ra1, rbE0, rbE1, rbO0, rbO1;
-#define V2_LOAD_A1(ID, R, CHUNK)                                                                      \
-  {                                                                                                   \
-    R = make_uint4(0u, 0u, 0u, 0u);                                                                   \
-    if ((ID) < V2_NPIX * 4) {                                                                         \
-      const int pp = (ID) >> 2, q = (ID)&3;                                                           \
-      const int yy = y0 + pp / CV_PW - 1, xx = x0 + pp % CV_PW - 1;                                   \
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W)                                                     \
-        R = *reinterpret_cast<const uint4*>(x + (((long long)b * H + yy) * W + xx) * FUS_C + (CHUNK)*32 + 8 * q); \
-    }                                                                                                 \
-  }
-#define V2_STORE_A1(ID, R, BUF) \
-  if ((ID) < V2_NPIX * 4) *reinterpret_cast<uint4*>(&sA[BUF][(ID) >> 2][8 * ((ID)&3)]) = R;
-#define V2_LOAD_B1(ID, R, STEP) \
-  R = *reinterpret_cast<const uint4*>(w5 + (long long)((ID) >> 2) * (9 * FUS_C) + ((STEP) % 9) * FUS_C + ((STEP) / 9) * 32 + 8 * ((ID)&3));
-#define V2_STORE_B1(ID, R, BUF) *reinterpret_cast<uint4*>(&sB[BUF][(ID) >> 2][8 * ((ID)&3)]) = R;
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    lds_barrier();  // previous tile's epilogue done with the LDS
-    V2_LOAD_A1(tid, ra0, 0);
-    V2_LOAD_A1(tid + 512, ra1, 0);
-    V2_LOAD_B1(tid, rbE0, 0);
-    V2_LOAD_B1(tid + 512, rbE1, 0);
-    V2_LOAD_B1(tid, rbO0, 1);
-    V2_LOAD_B1(tid + 512, rbO1, 1);
-    V2_STORE_A1(tid, ra0, 0);
-    V2_STORE_A1(tid + 512, ra1, 0);
-    V2_STORE_B1(tid, rbE0, 0);
-    V2_STORE_B1(tid + 512, rbE1, 0);
-    lds_barrier();
-#define V2_STEP(STEP, CUR0, CUR1, NXT0, NXT1)                                                   \
-  {                                                                                             \
-    const int step_ = (STEP);                                                                   \
-    const int chunk = step_ / 9, tap = step_ % 9;                                               \
-    if (step_ + 2 < 36) {                                                                       \
-      V2_LOAD_B1(tid, CUR0, step_ + 2);                                                         \
-      V2_LOAD_B1(tid + 512, CUR1, step_ + 2);                                                   \
-    }                                                                                           \
-    if (tap == 0 && chunk + 1 < 4) {                                                            \
-      V2_LOAD_A1(tid, ra0, chunk + 1);                                                          \
-      V2_LOAD_A1(tid + 512, ra1, chunk + 1);                                                    \
-    }                                                                                           \
-    const int ky = tap / 3, kx = tap % 3;                                                       \
-    Frag<bf16_t> af[4], bfr[4];                                                                 \
-    _Pragma("unroll") for (int mi = 0; mi < 4; ++mi) {                                          \
-      const int ty = wm * 2 + (mi >> 1), tx = (mi & 1) * 16 + r;                                \
-      af[mi].v = *reinterpret_cast<const uint4*>(&sA[chunk & 1][(ty + ky) * CV_PW + tx + kx][8 * g]); \
-    }                                                                                           \
-    _Pragma("unroll") for (int nj = 0; nj < 4; ++nj)                                            \
-      bfr[nj].v = *reinterpret_cast<const uint4*>(&sB[step_ & 1][wn * 64 + 16 * nj + r][8 * g]); \
-    _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                            \
-      _Pragma("unroll") for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], af[mi], bfr[nj]);       \
-    if (step_ + 1 < 36) {                                                                       \
-      V2_STORE_B1(tid, NXT0, (step_ + 1) & 1);                                                  \
-      V2_STORE_B1(tid + 512, NXT1, (step_ + 1) & 1);                                            \
-    }                                                                                           \
-    if (tap == 8 && chunk + 1 < 4) {                                                            \
-      V2_STORE_A1(tid, ra0, (chunk + 1) & 1);                                                   \
-      V2_STORE_A1(tid + 512, ra1, (chunk + 1) & 1);                                             \
-    }                                                                                           \
-    lds_barrier();                                                                            \
-  }
-#pragma unroll 1
-    for (int step = 0; step < 36; step += 2) {
-      V2_STEP(step, rbE0, rbE1, rbO0, rbO1);      // even step: ring slot E refills with step+2
-      V2_STEP(step + 1, rbO0, rbO1, rbE0, rbE1);  // odd step: slot O refills with step+3
-    }
-#undef V2_STEP
-    // ---- epilogue: bias + stats, stage the bf16 tile in LDS as [px][256] (row 528 B)
-    bf16_t(*sY)[C5 + 8] = reinterpret_cast<bf16_t(*)[C5 + 8]>(smem);
-#pragma unroll
-    for (int nj = 0; nj < 4; ++nj) {
-      const int n = wn * 64 + 16 * nj + r;
-      const float bias = b5[n];
-      float sum = 0.f, sq = 0.f;
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int ty = wm * 2 + (mi >> 1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int tx = (mi & 1) * 16 + 4 * g + j;
-          const bf16_t tv = f32_to_bf16(acc[mi][nj][j] + bias);
-          sY[ty * CV_TW + tx][n] = tv;
-          if (y0 + ty < H && x0 + tx < W) {
-            const float vr = bf16_to_f32(tv);  // statistics of the stored values
-            sum += vr;
-            sq += vr * vr;
-          }
-        }
-      }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
-      sq += __shfl_xor(sq, 16);
-      sq += __shfl_xor(sq, 32);
-      if (g == 0) {
-        st[wm][n][0] += sum;
-        st[wm][n][1] += sq;
-      }
-    }
-    lds_barrier();
-    // 128 px x 512 B = 4096 16-byte pieces
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int id = tid + 512 * i;
-      const int px = id >> 5, q = id & 31;
-      const int yy = y0 + px / CV_TW, xx = x0 + px % CV_TW;
-      if (yy < H && xx < W)
-        *reinterpret_cast<uint4*>(y + (((long long)b * H + yy) * W + xx) * C5 + 8 * q) =
-            *reinterpret_cast<const uint4*>(&sY[px][8 * q]);
-    }
-  }
-  lds_barrier();
-  for (int i = tid; i < C5; i += 512)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) slab[((long long)blockIdx.x * C5 + i) * 2 + q] = st[0][i][q] + st[1][i][q];
-}
-constexpr size_t V2_SMEM = 2 * V2_NPIX * V2_ROW * 2 + 2 * C5 * V2_ROW * 2 + 2 * C5 * 2 * 4;
-
 // ------------------------------------------------------------------ BN + ReLU + AdaptiveAvgPool(4)
 constexpr int POOL_SPLIT = 16;  // row chunks per pool region
 
@@ -1017,6 +879,249 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y
 #pragma unroll
   for (int k = 0; k < 8; ++k) s += red[k][c];
   part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = s;
+}
+
+// ---- conv5 v3 (bf16): 256 px (8x32) x 256 ch per workgroup, 8 waves as 4 (pixel-row pairs) x
+// 2 (128-channel halves); wave tile 64 px x 128 ch = 4x8 MFMA 16x16x32, K step 64 (18 steps of
+// (channel half, tap)).  All LDS staging is LDS-DMA (global_load_lds_dwordx4, no VGPR round
+// trip): the whole 10x34 halo patch of one channel half (43 KB) is resident per half and the
+// weights of one step (32 KB) double-buffered.  Rows are 128 B, 16-byte chunk q stored at slot
+// q ^ (row & 6): conflict-free ds_read_b128 for 16 consecutive rows from any start row (the
+// patch rows of tap kx), pre-applied in the weight blob and on the per-lane DMA source address.
+// Pipeline (one barrier per step): step s issues the DMA of B(s+1) (or the next tile's B(0)),
+// one piece of A (this tile's half 1 during steps 0-5, the next tile's half 0 during 9-14),
+// runs its 64 MFMAs, waits for its own DMA except the A piece just issued, barrier.
+// Epilogue straight from the accumulators: y is written in a fragment-native layout
+// [tile][wave][mi][nj][lane][4 px] (512 contiguous bytes per store instruction; read back by
+// k_rp_bn_relu_pool_frag) and the BN statistics of the stored bf16 values accumulate in
+// registers across tiles.
+constexpr int C3_TH = 8, C3_TW = 32;
+constexpr int C3_PW = C3_TW + 2, C3_NPIX = (C3_TH + 2) * C3_PW;  // 340 halo pixels
+constexpr int C3_APIX = 344, C3_APIECES = C3_APIX / 8;            // whole 1 KiB DMA pieces
+constexpr int C3_STEPS = 18;
+constexpr int C3_A_BYTES = 2 * C3_APIX * 128;
+constexpr int C3_B_OFF = C3_A_BYTES, C3_B_BYTES = 2 * C5 * 128;
+constexpr int C3_BIAS_OFF = C3_B_OFF + C3_B_BYTES;
+constexpr size_t C3_SMEM = C3_BIAS_OFF + C5 * 4;
+static_assert(C3_SMEM <= 163840, "conv5 v3 LDS budget");
+
+__device__ __forceinline__ uint32_t c3_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 6)); }
+
+// one LDS-DMA wave instruction: 64 lanes x 16 B from per-lane sources to lds_base + 16 * lane
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_base)
+               : "memory");
+}
+
+struct C3Tile {
+  int b, y0, x0;
+};
+__device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y) {
+  C3Tile o;
+  const long long per = (long long)tiles_x * tiles_y;
+  o.b = (int)(t / per);
+  const int rem = (int)(t % per);
+  o.y0 = (rem / tiles_x) * C3_TH;
+  o.x0 = (rem % tiles_x) * C3_TW;
+  return o;
+}
+
+__global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
+                                                       const char* __restrict__ blob, Layout L,
+                                                       bf16_t* __restrict__ y, float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = wave & 3, wn = wave >> 2;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const char* w5s = blob + L.w5s;
+  const char* zero16 = blob + L.zero;
+  float* sbias = (float*)(smem + C3_BIAS_OFF);
+  for (int i = tid; i < C5; i += 512) sbias[i] = ((const float*)(blob + L.b5))[i];
+  const int tiles_x = (W + C3_TW - 1) / C3_TW, tiles_y = (H + C3_TH - 1) / C3_TH;
+  const long long ntiles = (long long)B * tiles_x * tiles_y;
+
+  // A piece j of channel half h for tile t: pixel p = 8j + lane/8, slot lane%8
+  auto issue_a = [&](const C3Tile& t, int h, int j) {
+    const int p = 8 * j + (lane >> 3), q = lane & 7;
+    const int hy = p / C3_PW, hx = p % C3_PW;
+    const int yy = t.y0 + hy - 1, xx = t.x0 + hx - 1;
+    const char* src = zero16;
+    if (p < C3_NPIX && yy >= 0 && yy < H && xx >= 0 && xx < W)
+      src = (const char*)(x + (((long long)t.b * H + yy) * W + xx) * FUS_C + 64 * h + 8 * (q ^ (p & 6)));
+    glds16(src, lds0 + h * (C3_APIX * 128) + j * 1024);
+  };
+  // B pieces of step st: 32 x 1 KiB, wave w copies pieces 4w..4w+3
+  auto issue_b = [&](int st) {
+    const char* src = w5s + (size_t)st * (C5 * 128) + wave * 4096 + 16 * lane;
+    const uint32_t dst = lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 4096;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) glds16(src + 1024 * k, dst + 1024 * k);
+  };
+
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int nj = 0; nj < 8; ++nj) ssum[nj] = ssq[nj] = 0.f;
+
+  long long tile = blockIdx.x;
+  if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
+    const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
+    for (int j = wave; j < C3_APIECES; j += 8) issue_a(t, 0, j);
+    issue_b(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (; tile < ntiles; tile += gridDim.x) {
+    const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
+    const long long ntile = tile + gridDim.x;
+    const bool has_next = ntile < ntiles;
+    const C3Tile tn = c3_tile(has_next ? ntile : tile, tiles_x, tiles_y);
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 8; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+    for (int st = 0; st < C3_STEPS; ++st) {
+      if (st + 1 < C3_STEPS)
+        issue_b(st + 1);
+      else if (has_next)
+        issue_b(0);
+      bool a_issued = false;
+      if (st < 6) {
+        const int j = wave + 8 * st;
+        if (j < C3_APIECES) {
+          issue_a(t, 1, j);
+          a_issued = true;
+        }
+      } else if (st >= 9 && st < 15 && has_next) {
+        const int j = wave + 8 * (st - 9);
+        if (j < C3_APIECES) {
+          issue_a(tn, 0, j);
+          a_issued = true;
+        }
+      }
+      const int h = st >= 9, tap = st - 9 * h, ky = tap / 3, kx = tap % 3;
+      const char* sa = smem + h * (C3_APIX * 128);
+      const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        Frag<bf16_t> fa[4], fb[8];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const int p = (2 * wm + (mi >> 1) + ky) * C3_PW + (mi & 1) * 16 + r + kx;
+          fa[mi].v = *reinterpret_cast<const uint4*>(sa + c3_off(p, 4 * ks + g));
+        }
+#pragma unroll
+        for (int nj = 0; nj < 8; ++nj)
+          fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, 4 * ks + g));
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
+      }
+      // own DMA landed (except the A piece just issued), own LDS reads done, then the barrier
+      if (a_issued)
+        asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // ---- epilogue: bias, bf16, fragment-native y store, statistics of the stored values
+    bf16_t* yt = y + (((tile * 8 + wave) * 4) * 8) * 256;  // [mi][nj][lane][4]
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const bool row_ok = t.y0 + 2 * wm + (mi >> 1) < H;
+      const int xb = t.x0 + (mi & 1) * 16 + 4 * g;
+#pragma unroll
+      for (int nj = 0; nj < 8; ++nj) {
+        const float bias = sbias[wn * 128 + 16 * nj + r];
+        uint32_t hv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16_t tv = f32_to_bf16(acc[mi][nj][j] + bias);
+          hv[j] = (uint32_t)tv;
+          if (row_ok && xb + j < W) {
+            const float vr = bf16_to_f32(tv);
+            ssum[nj] += vr;
+            ssq[nj] += vr * vr;
+          }
+        }
+        *reinterpret_cast<uint2*>(yt + ((mi * 8 + nj) * 64 + lane) * 4) =
+            make_uint2(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16));
+      }
+    }
+  }
+  // ---- statistics: lanes of equal r, then the 4 row-pair waves in fixed order
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* red = (float*)smem;  // [4 wm][256 n][2]
+#pragma unroll
+  for (int nj = 0; nj < 8; ++nj) {
+    float a = ssum[nj], q = ssq[nj];
+    a += __shfl_xor(a, 16);
+    a += __shfl_xor(a, 32);
+    q += __shfl_xor(q, 16);
+    q += __shfl_xor(q, 32);
+    if (g == 0) {
+      const int n = wn * 128 + 16 * nj + r;
+      red[(wm * C5 + n) * 2] = a;
+      red[(wm * C5 + n) * 2 + 1] = q;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < C5 * 2; i += 512)
+    slab[(long long)blockIdx.x * C5 * 2 + i] = red[i] + red[C5 * 2 + i] + red[2 * C5 * 2 + i] + red[3 * C5 * 2 + i];
+}
+
+// BN + ReLU + AdaptiveAvgPool(4) partial sums over the fragment-native y of k_rp_conv3x3_v3.
+// grid: (16 regions * POOL_SPLIT, B); 256 threads = 128 channel pairs x 2 quad lanes; a quad is
+// 4 x-consecutive pixels (never straddles a 32-px tile); one 16-byte load = 2 channels x 4 px.
+__global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __restrict__ y, int H, int W,
+                                                              const float2* __restrict__ aff,
+                                                              float* __restrict__ part) {
+  __shared__ float red[2][C5];
+  const int b = blockIdx.y, reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
+  const int i = reg / 4, j = reg % 4;
+  const int cp = threadIdx.x & 127, ql = threadIdx.x >> 7;
+  const int n0 = 2 * cp, wn = n0 >> 7, nj = (n0 & 127) >> 4, r = n0 & 15;
+  const int ya = (i * H) / 4, yb = ((i + 1) * H + 3) / 4, xa = (j * W) / 4, xb = ((j + 1) * W + 3) / 4;
+  const int rows = yb - ya;
+  const int r0 = ya + (rows * sp) / POOL_SPLIT, r1 = ya + (rows * (sp + 1)) / POOL_SPLIT;
+  const int qa = xa >> 2, nq = ((xb + 3) >> 2) - qa;
+  const int tiles_x = (W + C3_TW - 1) / C3_TW, tiles_y = (H + C3_TH - 1) / C3_TH;
+  const float2 a0 = aff[n0], a1 = aff[n0 + 1];
+  float s0 = 0.f, s1 = 0.f;
+  const int nquads = (r1 - r0) * nq;
+  for (int q = ql; q < nquads; q += 2) {
+    const int yy = r0 + q / nq, xq = (qa + q % nq) * 4;
+    const long long tile = ((long long)b * tiles_y + yy / C3_TH) * tiles_x + xq / C3_TW;
+    const int ly = yy % C3_TH, lx = xq % C3_TW;
+    const int wave = wn * 4 + (ly >> 1), mi = (ly & 1) * 2 + (lx >> 4), g = (lx & 15) >> 2;
+    const uint4 v = *reinterpret_cast<const uint4*>(
+        y + ((((tile * 8 + wave) * 4 + mi) * 8 + nj) * 64 + g * 16 + r) * 4);
+    const uint32_t w0[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int xx = xq + e;
+      if (xx >= xa && xx < xb) {
+        const float c0 = bf16_to_f32((bf16_t)(e & 1 ? w0[e >> 1] >> 16 : w0[e >> 1] & 0xffff));
+        const float c1 = bf16_to_f32((bf16_t)(e & 1 ? w0[2 + (e >> 1)] >> 16 : w0[2 + (e >> 1)] & 0xffff));
+        s0 += fmaxf(c0 * a0.x + a0.y, 0.f);
+        s1 += fmaxf(c1 * a1.x + a1.y, 0.f);
+      }
+    }
+  }
+  red[ql][n0] = s0;
+  red[ql][n0 + 1] = s1;
+  __syncthreads();
+  const int c = threadIdx.x;
+  part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = red[0][c] + red[1][c];
 }
 
 // ------------------------------------------------------------------ tail: conv 256->512 on 4x4
@@ -1187,6 +1292,21 @@ inline int conv_grid(int B, int H, int W) {
   const long long nt = (long long)B * ((W + CV_TW - 1) / CV_TW) * ((H + CV_TH - 1) / CV_TH);
   return (int)std::min<long long>(nt, 512);
 }
+inline long long conv3_tiles(int B, int H, int W) {
+  return (long long)B * ((W + C3_TW - 1) / C3_TW) * ((H + C3_TH - 1) / C3_TH);
+}
+inline int device_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+inline int conv3_grid(int B, int H, int W) {  // persistent, one 161 KB-LDS workgroup per CU
+  return (int)std::min<long long>(conv3_tiles(B, H, W), device_cus());
+}
 
 inline Ws make_ws(int es, int B, int H, int W) {
   Ws w;
@@ -1197,13 +1317,14 @@ inline Ws make_ws(int es, int B, int H, int W) {
     return r;
   };
   const size_t P = (size_t)B * H * W;
-  const int slab_rows = std::max(std::max(chain_grid(B, H, W), 8 * chain_grid_v2(B, H, W)), conv_grid(B, H, W));
+  const int slab_rows = std::max(std::max(chain_grid(B, H, W), 8 * chain_grid_v2(B, H, W)),
+                                 std::max(conv_grid(B, H, W), conv3_grid(B, H, W)));
   w.aff1 = seg(STEM_C * sizeof(float2));
   w.aff2 = seg(FUS_C * sizeof(float2));
   w.aff5 = seg(C5 * sizeof(float2));
   w.slab = seg((size_t)slab_rows * C5 * 2 * sizeof(float));
   w.att = seg(P * FUS_C * es);
-  w.y = seg(P * C5 * es);
+  w.y = seg(es == 2 ? (size_t)conv3_tiles(B, H, W) * C3_TH * C3_TW * C5 * 2 : P * C5 * es);
   w.part = seg((size_t)B * 16 * POOL_SPLIT * C5 * sizeof(float));
   w.pooled = seg((size_t)B * C5 * 16 * sizeof(float));
   w.z6 = seg((size_t)B * C6 * 16 * sizeof(float));
@@ -1260,21 +1381,26 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
     CHAIN_LAUNCH(2, aff1, aff2, nullptr, att);
   }
   // conv5 + its BN statistics
-  const int gcv = conv_grid(B, H, W);
+  int gcv;
   {
     TimerScope ts("rp_conv3x3", s);
     if constexpr (sizeof(T) == 2) {
       static const hipError_t attr = hipFuncSetAttribute(
-          (const void*)k_rp_conv3x3_v2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)V2_SMEM);
+          (const void*)k_rp_conv3x3_v3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       if (attr != hipSuccess) return (int)attr;
-      k_rp_conv3x3_v2<<<gcv, 512, V2_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
-    }
-    else
+      gcv = conv3_grid(B, H, W);
+      k_rp_conv3x3_v3<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+    } else {
+      gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
+    }
   }
   k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
                                 bn.p[19], aff5);
-  k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
+  if constexpr (sizeof(T) == 2)
+    k_rp_bn_relu_pool_frag<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
+  else
+    k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
   k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
   k_rp_tail_conv<<<C6 / 8, 512, 0, s>>>(pooled, B, blob, L, z6);
   k_rp_tail_mlp<<<1, 512, 0, s>>>(z6, B, training, momentum, blob, L, bn, seed, ratio);

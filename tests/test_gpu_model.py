@@ -34,6 +34,21 @@ def test_ratio_predictor_eval_golden(golden):
     np.testing.assert_allclose(r, g4["ratio"], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("H,W", [(90, 125), (64, 96)])
+def test_ratio_predictor_eval_bf16_ragged(H, W):
+    """bf16 eval ratio on shapes with partial conv tiles / overlapping pool regions vs the fp32
+    CPU module tree (same bf16 tolerance as the golden case)."""
+    pv = gi.pixel_values(5, 2, H, W)
+    m_cpu = _ratio_module().eval()
+    m = copy.deepcopy(m_cpu)
+    m.compute_dtype = torch.bfloat16
+    m = m.to(DEV).eval()
+    r = m(torch.from_numpy(pv).to(DEV)[:, 3:6]).cpu().numpy()
+    with torch.no_grad():
+        ref = ratio_o.ratio_forward_modules(m_cpu, torch.from_numpy(pv[:, 3:6]))
+    np.testing.assert_allclose(r, np.asarray(ref, dtype=np.float32).reshape(r.shape), atol=5e-3)
+
+
 def test_ratio_predictor_eval_bf16(golden):
     g4 = golden("g4_ratio")
     pv = gi.pixel_values(4, 2, 240, 320)
@@ -67,10 +82,12 @@ def _full_model(dtype=torch.float32):
     return m.set_compute_dtype(dtype).to(DEV)
 
 
-def test_bf16_train_mode_batchnorm_stats():
-    """The bf16 chain/conv5 kernels (LDS-resident weights, v2) in train mode: running stats of
-    all six BN layers within bf16 tolerance of the PyTorch-CPU fp32 module tree."""
-    pv = gi.pixel_values(8, 2, 240, 320)
+@pytest.mark.parametrize("H,W", [(240, 320), (90, 125)])
+def test_bf16_train_mode_batchnorm_stats(H, W):
+    """The bf16 chain/conv5 kernels (LDS-resident weights, LDS-DMA conv5) in train mode: running
+    stats of all six BN layers within bf16 tolerance of the PyTorch-CPU fp32 module tree.  90x125
+    leaves partial 8x32 conv tiles and overlapping adaptive-pool regions."""
+    pv = gi.pixel_values(8, 2, H, W)
     m_cpu = _ratio_module().train()
     m = copy.deepcopy(m_cpu)
     m.compute_dtype = torch.bfloat16
