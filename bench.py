@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0
 CONV5_FLOP_PER_PX = 2 * 128 * 9 * 256  # 3x3 128->256 (custom_model.py:1413)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-sample", type=int, default=1, help="images in the bounded CPU sample")
     ap.add_argument("--inference", type=int, default=1, help="also report forward-only img/s")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def build(args, dev):

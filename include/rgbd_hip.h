@@ -108,9 +108,15 @@ int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const flo
 int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H, int W,
                       void* stream);
 /* Packs DSAModule weights (conv_layers[0..3].weight, rgb_projection.weight; float32
- * [4][Cout][Cin][3][3] and [Cout][Cin][3][3]) into the implicit-GEMM B operands:
+ * [4][Cout][Cin][3][3] and [Cout][Cin][3][3]) into the implicit-GEMM B operands.
+ * RGBD_F32 (segment form):
  *   wfwd [Cout][5][9][Cin]  (forward: k = (seg, tap, ci))
- *   wbwd [Cin][5][9][Cout]  (dX: k = (seg, tap, co), taps NOT flipped; see csrc)   */
+ *   wbwd [Cin][5][9][Cout]  (dX: k = (seg, tap, co), taps NOT flipped; see csrc)
+ * RGBD_BF16 (code-merged form, Cin and Cout multiples of 32): for each 4-bit region code k
+ * the merged filter W_k = proj + sum_{i in k} conv_i,
+ *   wfwd [16][Cout][9][Cin],  wbwd [16][Cin][9][Cout].
+ * rgbd_dsam_packed_elems gives the element count of each of wfwd / wbwd. */
+long long rgbd_dsam_packed_elems(int dtype, int Cin, int Cout);
 int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, int Cin,
                            int Cout, void* wfwd, void* wbwd, void* stream);
 

@@ -38,6 +38,7 @@ SIGNATURES = {
     "rgbd_dggm_fuse_bwd_workspace_size": (_SZ, [_I, _I, _I, _I]),
     "rgbd_dggm_fuse_bwd": (_I, [_I, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_nchw_to_nhwc": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
+    "rgbd_dsam_packed_elems": (_LL, [_I, _I, _I]),
     "rgbd_dsam_pack_weights": (_I, [_I, _P, _P, _I, _I, _P, _P, _P]),
     "rgbd_dsam_conv_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rgbd_dsam_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
@@ -89,4 +90,4 @@ def header_symbols():
     import re
     hdr = Path(__file__).resolve().parents[1] / "include" / "rgbd_hip.h"
     txt = hdr.read_text()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(rgbd_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:\w+\*?\s+)+\*?(rgbd_\w+)\s*\(", txt, flags=re.M)))

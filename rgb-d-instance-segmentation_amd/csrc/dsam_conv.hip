@@ -41,6 +41,7 @@ struct ConvArgs {
   void* out_nhwc;                   // optional
   int ksplit;                       // v2 only: K split over (tap, chunk) ranges (1 = none)
   float* partial;                   // v2 split-K slabs: f32 [ksplit][B][Ho][Wo][N]
+  uint16_t* tile_codes;             // bf16: [nclass][M tiles][9] codes present per tap
 };
 
 constexpr int BM = 64, BN = 64;
@@ -213,6 +214,34 @@ __global__ void k_pack_dsam(const float* __restrict__ conv_w, const float* __res
   }
 }
 
+// bf16 code-merged filters: W_k = proj + sum_{i in k} conv_i for every 4-bit code k (fixed
+// summation order: proj, then conv_0..conv_3, in f32, rounded once).  wfwd[k][o][tap*Cin + c],
+// wbwd[k][c][tap*Cout + o].
+__global__ void k_pack_dsam_codes(const float* __restrict__ conv_w, const float* __restrict__ proj_w, int Cin,
+                                  int Cout, bf16_t* __restrict__ wfwd, bf16_t* __restrict__ wbwd) {
+  const long long per = (long long)Cout * Cin * 9;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < per;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int tap = (int)(e % 9);
+    const int c = (int)((e / 9) % Cin);
+    const int o = (int)(e / (9ll * Cin));
+    float w4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w4[i] = conv_w[(((long long)i * Cout + o) * Cin + c) * 9 + tap];
+    const float wp = proj_w[e];
+#pragma unroll 1
+    for (int k = 0; k < 16; ++k) {
+      float v = wp;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((k >> i) & 1) v += w4[i];
+      const bf16_t tv = f32_to_bf16(v);
+      if (wfwd) wfwd[((long long)k * Cout + o) * 9 * Cin + (long long)tap * Cin + c] = tv;
+      if (wbwd) wbwd[((long long)k * Cin + c) * 9 * Cout + (long long)tap * Cout + o] = tv;
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_nchw_to_nhwc(const T* __restrict__ src, T* __restrict__ dst, int C,
                                                       int HW) {
@@ -318,75 +347,100 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, 
     }
 }
 
-// bf16 dW: X tile staged [px][kk] from NHWC with 16-byte loads, read back transposed with
-// ds_read_b64_tr_b16 (gfx950) as the MFMA B operand (8 consecutive pixels per lane); the A
-// operand (G^T, 8 consecutive pixels of one channel) is a direct 16-byte load from NCHW.
+// bf16 dW, code-merged (see k_conv_codes): the workgroup for code k accumulates
+//   dW_k[o][tap][c] = sum over output px p with code(src(p, tap)) == k of G[p][o] X[src][c]
+// over its batch split, skipping every 32-px chunk whose rows never meet code k (presence table
+// from k_code_presence: no loads at all); k_dsam_wgrad_combine folds dW_k into the five filters
+// (conv_i gets the codes with bit i, proj gets all).  Work ~ one dense dW instead of
+// popcount + 1 of them.  X tile staged [px][kk] from NHWC with 16-byte loads, read back transposed
+// with ds_read_b64_tr_b16 (gfx950) as the MFMA B operand; the A operand (G^T, 8 consecutive
+// pixels of one channel, NCHW) is loaded one chunk ahead into registers.
 constexpr int WG_KK = 128, WG_O = 64, PXC = 32, XPAD = 136;
 typedef __attribute__((ext_vector_type(4))) short v4s;
 
+__global__ void k_code_presence(const uint8_t* __restrict__ code, int B, int h, int w,
+                                uint16_t* __restrict__ pres, uint32_t* __restrict__ gmask) {
+  // one 32-lane group per (b, 32-px output chunk): OR of 1 << code over the chunk's 9-tap sources
+  const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo, nchunk = (hwo + PXC - 1) / PXC;
+  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long grp = t >> 5;
+  const int l = (int)(t & 31);
+  uint32_t m = 0u;
+  if (grp < (long long)B * nchunk) {
+    const int b = (int)(grp / nchunk), p = (int)(grp % nchunk) * PXC + l;
+    if (p < hwo) {
+      const int oy = p / wo, ox = p % wo;
+      for (int tap = 0; tap < 9; ++tap) {
+        const int iy = 2 * oy - 1 + tap / 3, ix = 2 * ox - 1 + tap % 3;
+        if (iy >= 0 && iy < h && ix >= 0 && ix < w) m |= 1u << code[((long long)b * h + iy) * w + ix];
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+  if (l == 0 && grp < (long long)B * nchunk) {
+    pres[grp] = (uint16_t)m;
+    if (m) atomicOr(gmask, m);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restrict__ gout, const bf16_t* __restrict__ x,
-                                                         const uint8_t* __restrict__ code, int B, int Cin, int h,
+                                                         const uint8_t* __restrict__ code,
+                                                         const uint16_t* __restrict__ pres,
+                                                         const uint32_t* __restrict__ gmask, int B, int Cin, int h,
                                                          int w, int Cout, int splits, float* __restrict__ partial) {
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][PXC][XPAD];
+  const int kcode = blockIdx.z & 15, split = blockIdx.z >> 4;
+  if (!((*gmask >> kcode) & 1u)) return;  // code absent from the batch: no partial, combine skips it
   const int ho = (h + 1) / 2, wo = (w + 1) / 2;
   const int hwo = ho * wo;
-  const int KK = 45 * Cin;
-  const int kk0 = blockIdx.x * WG_KK, o0 = blockIdx.y * WG_O, z = blockIdx.z;
-  const int b0 = (int)((long long)z * B / splits), b1 = (int)((long long)(z + 1) * B / splits);
+  const int KK = 9 * Cin;
+  const int kk0 = blockIdx.x * WG_KK, o0 = blockIdx.y * WG_O;
+  const int b0 = (int)((long long)split * B / splits), b1 = (int)((long long)(split + 1) * B / splits);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   // staging role: pixel row spx, two 8-channel chunks at kk0 + 16*skg + 8*q
   const int spx = threadIdx.x >> 3, skg = threadIdx.x & 7;
-  int s_seg[2], s_ky[2], s_kx[2], s_c[2];
+  int s_ky[2], s_kx[2], s_c[2];
   bool s_ok[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int kk = kk0 + 16 * skg + 8 * q;
     s_ok[q] = kk < KK;
     const int k2 = s_ok[q] ? kk : 0;
-    s_seg[q] = k2 / (9 * Cin);
-    const int tap = (k2 / Cin) % 9;
+    const int tap = k2 / Cin;
     s_ky[q] = tap / 3;
     s_kx[q] = tap % 3;
     s_c[q] = k2 % Cin;
   }
-  int staged_any = 0;  // does the staged chunk hold any unmasked element?
-  auto stage = [&](int buf, int b, int p0) {
-    const int p = p0 + spx;
+  const int nchunk = (hwo + PXC - 1) / PXC;
+  const int total = (b1 - b0) * nchunk;
+  auto chunk_live = [&](int it) {
+    return (pres[(long long)(b0 + it / nchunk) * nchunk + it % nchunk] >> kcode) & 1u;
+  };
+  auto next_live = [&](int it) {
+    while (it < total && !chunk_live(it)) ++it;
+    return it;
+  };
+  int staged_any = 0;  // does the staged chunk hold any element of code k?
+  auto stage = [&](int buf, int it) {
+    const int b = b0 + it / nchunk, p = (it % nchunk) * PXC + spx;
     const int oy = p / wo, ox = p % wo;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int iy = 2 * oy - 1 + s_ky[q], ix = 2 * ox - 1 + s_kx[q];
       bool ok = s_ok[q] && p < hwo && iy >= 0 && iy < h && ix >= 0 && ix < w;
       const long long pix = ((long long)b * h + iy) * w + ix;
-      if (ok && s_seg[q] < 4) ok = (code[pix] >> s_seg[q]) & 1u;
+      if (ok) ok = code[pix] == kcode;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (ok) v = *reinterpret_cast<const uint4*>(x + pix * Cin + s_c[q]);
       staged_any |= ok ? 1 : 0;
       *reinterpret_cast<uint4*>(&Xs[buf][spx][16 * skg + 8 * q]) = v;
     }
   };
-  f32x4 acc[4][2];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nchunk = (hwo + PXC - 1) / PXC;
-  const int total = (b1 - b0) * nchunk;
-  if (total > 0) stage(0, b0, 0);
-  int live = __syncthreads_or(staged_any);
-  for (int it = 0; it < total; ++it) {
-    const int buf = it & 1;
-    const int b = b0 + it / nchunk, p0 = (it % nchunk) * PXC;
-    staged_any = 0;
-    if (it + 1 < total) stage(buf ^ 1, b0 + (it + 1) / nchunk, ((it + 1) % nchunk) * PXC);
-    if (!live) {  // every im2col element of this chunk is masked out: contribution is zero
-      live = __syncthreads_or(staged_any);
-      continue;
-    }
-    // A: G^T rows o, 8 consecutive pixels
-    Frag<bf16_t> af[4];
-    const int pa = p0 + 8 * g;
+  // A: G^T rows o, 8 consecutive pixels of chunk it
+  auto load_a = [&](Frag<bf16_t>* af, int it) {
+    const int b = b0 + it / nchunk, pa = (it % nchunk) * PXC + 8 * g;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const int o = o0 + 16 * mi + r;
@@ -403,25 +457,52 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restric
           if (o < Cout && pa + j < hwo) af[mi].set_raw(j, src[j]);
       }
     }
-    // B: transposed LDS reads, columns (kk) wave*32 + 16*nj + i, rows (px) 8g .. 8g+7
-    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+  };
+  f32x4 acc[4][2];
 #pragma unroll
-    for (int nj = 0; nj < 2; ++nj) {
-      const int col = wave * 32 + 16 * nj + 4 * p4;
-      v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + q4][col]));
-      v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + 4 + q4][col]));
-      Frag<bf16_t> bf;
-      bf.v = make_uint4((uint32_t)(uint16_t)t0.x | ((uint32_t)(uint16_t)t0.y << 16),
-                        (uint32_t)(uint16_t)t0.z | ((uint32_t)(uint16_t)t0.w << 16),
-                        (uint32_t)(uint16_t)t1.x | ((uint32_t)(uint16_t)t1.y << 16),
-                        (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
+  for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], af[mi], bf);
-    }
-    live = __syncthreads_or(staged_any);
+    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag<bf16_t> af[4], afn[4];
+  int cur = next_live(0), buf = 0;
+  if (cur < total) {
+    stage(0, cur);
+    load_a(af, cur);
   }
+  int live = __syncthreads_or(staged_any);
+  while (cur < total) {
+    const int nxt = next_live(cur + 1);
+    staged_any = 0;
+    if (nxt < total) {
+      stage(buf ^ 1, nxt);
+      load_a(afn, nxt);
+    }
+    if (live) {
+      // B: transposed LDS reads, columns (kk) wave*32 + 16*nj + i, rows (px) 8g .. 8g+7
+      const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj) {
+        const int col = wave * 32 + 16 * nj + 4 * p4;
+        v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + q4][col]));
+        v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + 4 + q4][col]));
+        Frag<bf16_t> bf;
+        bf.v = make_uint4((uint32_t)(uint16_t)t0.x | ((uint32_t)(uint16_t)t0.y << 16),
+                          (uint32_t)(uint16_t)t0.z | ((uint32_t)(uint16_t)t0.w << 16),
+                          (uint32_t)(uint16_t)t1.x | ((uint32_t)(uint16_t)t1.y << 16),
+                          (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], af[mi], bf);
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) af[mi] = afn[mi];
+    live = __syncthreads_or(staged_any);
+    buf ^= 1;
+    cur = nxt;
+  }
+  float* dst = partial + ((long long)(split * 16 + kcode) * Cout) * KK;
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -430,9 +511,37 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restric
 #pragma unroll
       for (int nj = 0; nj < 2; ++nj) {
         const int c = kk0 + wave * 32 + 16 * nj + r;
-        if (o < Cout && c < KK) partial[((long long)z * Cout + o) * KK + c] = acc[mi][nj][reg];
+        if (o < Cout && c < KK) dst[(long long)o * KK + c] = acc[mi][nj][reg];
       }
     }
+}
+
+// dW_k (present codes, split partials) -> the reference filters, fixed summation order
+__global__ void k_dsam_wgrad_combine(const float* __restrict__ partial, int splits,
+                                     const uint32_t* __restrict__ gmask, int Cin, int Cout,
+                                     float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
+  const long long KK = 9ll * Cin;
+  const long long total = (long long)Cout * KK;
+  const uint32_t m = *gmask;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    float seg[4] = {0.f, 0.f, 0.f, 0.f}, pr = 0.f;
+    for (int k = 0; k < 16; ++k) {
+      if (!((m >> k) & 1u)) continue;
+      float v = 0.f;
+      for (int sp = 0; sp < splits; ++sp) v += partial[(long long)(sp * 16 + k) * total + e];
+      pr += v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((k >> i) & 1) seg[i] += v;
+    }
+    const int o = (int)(e / KK);
+    const int kk = (int)(e % KK);
+    const int tap = kk / Cin, c = kk % Cin;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dconv_w[(((long long)i * Cout + o) * Cin + c) * 9 + tap] = seg[i];
+    dproj_w[((long long)o * Cin + c) * 9 + tap] = pr;
+  }
 }
 
 __global__ void k_dsam_wgrad_final(const float* __restrict__ partial, int splits, int Cin, int Cout,
@@ -477,19 +586,72 @@ __global__ void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_deco
   dbias[t] = s;
 }
 
-// ----------------------------------------------------------------------- bf16 v2
+// ----------------------------------------------------------------------- bf16: code-merged
+// The masked sum  sum_i conv_i(x * m_i) + proj(x)  is regrouped by region CODE (the 4-bit
+// pooled mask pattern of a source pixel, bit i = m_i): a source pixel with code k meets the
+// merged filter  W_k = proj + sum_{i in k} conv_i  (packed per code by k_pack_dsam_codes), so
+// each im2col row is multiplied by ONE filter instead of popcount(k) + 1 of them.
+//
 // Workgroup tile 128 output pixels (flattened over batch x grid, or over one stride-2 parity
 // class for dX) x 128 output channels; 4 waves as 2x2, wave tile 64 px x 64 ch (4x4 MFMA).
-// A (im2col rows) is gathered straight from NHWC global memory, 8 channels (16 B) per lane,
-// once per (tap, 32-ch chunk) and re-used by every live segment; B (packed weights) is staged
-// per (tap, chunk, segment) step through a double-buffered LDS tile shared by the 4 waves.
-// A segment whose mask bit is absent from every pixel the workgroup reads is skipped for
-// the whole K loop (exact: its contribution is zero).
-constexpr int V2M = 128, V2N = 128, V2BROW = 40;  // 80-byte LDS rows (conflict-free b128 reads)
+// The K loop runs over (tap, code present among the tile's rows at that tap, 32-ch chunk);
+// a row whose code differs from the step's contributes zero (register select).  A (im2col rows,
+// 16 B per lane straight from NHWC) and B (W_k rows) of step s+1 are loaded while step s runs;
+// B goes through a double-buffered LDS tile with 64-byte rows XOR-swizzled by row bit 2
+// (conflict-free ds_read_b128 / ds_write_b128).
+constexpr int V2M = 128, V2N = 128;
+__device__ __forceinline__ int cm_slot(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 1) & 2)); }
 
-__global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t sB[2][V2N][V2BROW];
-  __shared__ uint32_t seg_or;
+// Pre-pass of k_conv_codes: for each 128-row tile (and stride-2 parity class of dX), the set
+// of region codes its rows meet at each tap (one thread per row; computed once per conv instead
+// of once per (N tile, K split) workgroup).
+__global__ __launch_bounds__(128) void k_conv_tile_codes(ConvArgs a) {
+  __shared__ uint32_t sm[9];
+  const int nclass = a.transposed ? 4 : 1;
+  const int cls = blockIdx.z;
+  int py = 0, px = 0, Hc = a.Ho, Wc = a.Wo;
+  if (a.transposed) {
+    py = cls >> 1;
+    px = cls & 1;
+    Hc = (a.Ho - py + 1) >> 1;
+    Wc = (a.Wo - px + 1) >> 1;
+  }
+  if (threadIdx.x < 9) sm[threadIdx.x] = 0u;
+  __syncthreads();
+  const long long HWc = (long long)Hc * Wc, Mtot = (long long)a.B * HWc;
+  const long long m = (long long)blockIdx.x * V2M + threadIdx.x;
+  if (m < Mtot) {
+    const int b = (int)(m / HWc), rem = (int)(m % HWc), i = rem / Wc, j = rem % Wc;
+    const int oy = a.transposed ? 2 * i + py : i, ox = a.transposed ? 2 * j + px : j;
+    const uint32_t rc = a.mask_mode == MASK_DST ? a.code[((long long)b * a.Ho + oy) * a.Wo + ox] : 0u;
+    int t = 0;
+    for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx) {
+        if (a.transposed && (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1))) continue;
+        int iy, ix;
+        if (a.transposed) {
+          iy = (oy + 1 - ky) >> 1;
+          ix = (ox + 1 - kx) >> 1;
+        } else {
+          iy = oy * 2 - 1 + ky;
+          ix = ox * 2 - 1 + kx;
+        }
+        if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi) {
+          const uint32_t c = a.mask_mode == MASK_SRC ? a.code[((long long)b * a.Hi + iy) * a.Wi + ix] : rc;
+          atomicOr(&sm[t], 1u << c);
+        }
+        ++t;
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) a.tile_codes[((long long)cls * gridDim.x + blockIdx.x) * 9 + threadIdx.x] = (uint16_t)sm[threadIdx.x];
+  (void)nclass;
+}
+
+__global__ __launch_bounds__(256) void k_conv_codes(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t sB[2][V2N * 32];
+  __shared__ uint8_t tcl[9 * 16], tcnt[9], tfirst[9];
+  __shared__ int tbase[10], tdelta[9], ttap[9];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave & 1, wn = wave >> 1;
@@ -502,161 +664,214 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
     Hc = (a.Ho - py + 1) >> 1;
     Wc = (a.Wo - px + 1) >> 1;
   }
-  const long long HWc = (long long)Hc * Wc;
-  const long long Mtot = (long long)a.B * HWc;
-  const long long mblk = (long long)blockIdx.x * V2M;
+  const int HWc = Hc * Wc;
+  const int Mtot = a.B * HWc;
+  const int mblk = blockIdx.x * V2M;
   if (mblk >= Mtot) return;  // whole workgroup
   const int n0 = blockIdx.y * V2N;
   const bf16_t* xp = (const bf16_t*)a.x;
   const bf16_t* wp = (const bf16_t*)a.w;
-  const long long ktot = 5ll * 9 * a.C;
-  // rows owned by this lane: m = mblk + wm*64 + 16*mi + r
-  int rb[4], roy[4], rox[4];
-  bool rvalid[4];
-  uint32_t rcode[4];
+  const int krow = 9 * a.C;  // one code's packed row (elements)
+  // ---- tap table (uniform): origin-relative source offset of each tap, in pixels
+  if (tid == 0) {
+    int n = 0, base = 0, t = 0;
+    const int nchunk = a.C / 32;
+    for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx) {
+        int dy = ky, dx = kx;  // forward: origin (2oy-1, 2ox-1)
+        if (a.transposed) {
+          if (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1)) continue;
+          dy = (py + 1 - ky) >> 1;  // dX: origin (i, j) of the parity-class grid
+          dx = (px + 1 - kx) >> 1;
+        }
+        uint32_t msk = a.tile_codes[((long long)cls * gridDim.x + blockIdx.x) * 9 + t];
+        ttap[t] = ky * 3 + kx;
+        tdelta[t] = dy * a.Wi + dx;
+        tfirst[t] = (uint8_t)n;
+        tbase[t] = base;
+        const int cnt = __popc(msk);
+        tcnt[t] = (uint8_t)cnt;
+        base += cnt * nchunk;
+        while (msk) {
+          const int k = __ffs(msk) - 1;
+          msk &= msk - 1u;
+          tcl[n++] = (uint8_t)k;
+        }
+        ++t;
+      }
+    for (int q = t; q < 9; ++q) tcnt[q] = 0;
+    tbase[t] = base;
+    for (int q = t + 1; q < 10; ++q) tbase[q] = base;
+  }
+  // ---- rows owned by this lane: m = mblk + wm*64 + 16*mi + r.  Per row: origin pixel index,
+  // 9-bit mask of in-bounds taps and the 4-bit code each tap meets (SRC: source pixel's code;
+  // DST: the row's own code).  Taps are indexed by position t in the tap table.
+  int rorg[4];
+  uint32_t rvalid[4], rc_lo[4], rc_hi[4];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
-    const long long m = mblk + wm * 64 + 16 * mi + r;
-    rvalid[mi] = m < Mtot;
-    const long long mm = rvalid[mi] ? m : 0;
-    rb[mi] = (int)(mm / HWc);
-    const int rem = (int)(mm % HWc);
-    const int i = rem / Wc, j = rem % Wc;
-    roy[mi] = a.transposed ? 2 * i + py : i;
-    rox[mi] = a.transposed ? 2 * j + px : j;
-    rcode[mi] = (a.mask_mode == MASK_DST && rvalid[mi])
-                    ? a.code[((long long)rb[mi] * a.Ho + roy[mi]) * a.Wo + rox[mi]]
-                    : 0u;
-  }
-  // ---- live segments of the workgroup (OR of every code any of its rows reads)
-  if (tid == 0) seg_or = 0u;
-  __syncthreads();
-  {
-    uint32_t o = 0u;
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      if (!rvalid[mi]) continue;
-      if (a.mask_mode == MASK_DST) {
-        o |= rcode[mi];
+    const int m = mblk + wm * 64 + 16 * mi + r;
+    rvalid[mi] = 0u;
+    rc_lo[mi] = rc_hi[mi] = 0u;
+    rorg[mi] = 0;
+    if (m < Mtot) {
+      const int b = m / HWc, rem = m % HWc, i = rem / Wc, j = rem % Wc;
+      int t = 0;
+      if (a.transposed) {
+        const int oy = 2 * i + py, ox = 2 * j + px;
+        const uint32_t rc = a.code[((long long)b * a.Ho + oy) * a.Wo + ox];
+        rorg[mi] = (b * a.Hi + i) * a.Wi + j;
+        for (int ky = 0; ky < 3; ++ky)
+          for (int kx = 0; kx < 3; ++kx) {
+            if (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1)) continue;
+            const int iy = i + ((py + 1 - ky) >> 1), ix = j + ((px + 1 - kx) >> 1);
+            if (iy < a.Hi && ix < a.Wi) {
+              rvalid[mi] |= 1u << t;
+              if (t < 8) rc_lo[mi] |= rc << (4 * t); else rc_hi[mi] |= rc;
+            }
+            ++t;
+          }
       } else {
-        for (int t = 0; t < 9; ++t) {
-          const int iy = roy[mi] * 2 - 1 + t / 3, ix = rox[mi] * 2 - 1 + t % 3;
-          if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi)
-            o |= a.code[((long long)rb[mi] * a.Hi + iy) * a.Wi + ix];
-        }
+        const int oy = i, ox = j;
+        rorg[mi] = (b * a.Hi + 2 * oy - 1) * a.Wi + 2 * ox - 1;
+        const uint8_t* cb = a.code + (long long)b * a.Hi * a.Wi;
+        for (int ky = 0; ky < 3; ++ky)
+          for (int kx = 0; kx < 3; ++kx) {
+            const int iy = 2 * oy - 1 + ky, ix = 2 * ox - 1 + kx;
+            if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi) {
+              const uint32_t c = cb[iy * a.Wi + ix];
+              rvalid[mi] |= 1u << t;
+              if (t < 8) rc_lo[mi] |= c << (4 * t); else rc_hi[mi] |= c;
+            }
+            ++t;
+          }
       }
     }
-    if (o) atomicOr(&seg_or, o);
   }
   __syncthreads();
-  const uint32_t live = (seg_or & 0xfu) | 0x10u;  // segment 4 (projection) always live
-  int segs[5], nseg = 0;
-  for (int sgi = 0; sgi < 5; ++sgi)
-    if ((live >> sgi) & 1u) segs[nseg++] = sgi;
-  // ---- K steps = (tap, chunk) x live segments
-  int taps[9], ntap = 0;
-  for (int ky = 0; ky < 3; ++ky)
-    for (int kx = 0; kx < 3; ++kx) {
-      if (a.transposed && (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1))) continue;
-      taps[ntap++] = ky * 3 + kx;
-    }
   const int nchunk = a.C / 32;
-  // this split's (tap, chunk) range
-  const int tc_total = ntap * nchunk;
-  const int tc0 = (int)((long long)split * tc_total / a.ksplit), tc1 = (int)((long long)(split + 1) * tc_total / a.ksplit);
-  const int nsteps = (tc1 - tc0) * nseg;
-  // B staging: 128 rows (n) x 4 pieces of 8 channels; thread -> pieces tid, tid + 256
+  const int T = tbase[9];
+  const int s0 = (int)((long long)split * T / a.ksplit), s1 = (int)((long long)(split + 1) * T / a.ksplit);
+  // B staging rows: thread -> pieces tid, tid + 256 (row id>>2, 16-byte chunk id&3)
+  int boff[2];
+  bool bok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + 256 * i, n = n0 + (id >> 2);
+    bok[i] = n < a.N;
+    boff[i] = (bok[i] ? n : 0) * krow + 8 * (id & 3);
+  }
   uint4 rbv[2];
-#define V2_BLOAD(STEP)                                                                            \
-  {                                                                                               \
-    const int st_ = (STEP);                                                                       \
-    const int sg_ = segs[st_ % nseg], tc_ = tc0 + st_ / nseg;                                     \
-    const int tap_ = taps[tc_ / nchunk], ch_ = tc_ % nchunk;                                      \
-    const long long koff_ = ((long long)sg_ * 9 + tap_) * a.C + ch_ * 32;                         \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                               \
-      const int id = tid + 256 * i, n = n0 + (id >> 2);                                          \
-      rbv[i] = n < a.N ? *reinterpret_cast<const uint4*>(wp + (long long)n * ktot + koff_ + 8 * (id & 3)) \
-                       : make_uint4(0u, 0u, 0u, 0u);                                              \
-    }                                                                                             \
-  }
-#define V2_BSTORE(BUF)                                                                    \
-  _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                         \
-    const int id = tid + 256 * i;                                                         \
-    *reinterpret_cast<uint4*>(&sB[BUF][id >> 2][8 * (id & 3)]) = rbv[i];                  \
-  }
+  // step state (wave-uniform): tap position, chunk, code index within the tap
+  int st_t = 0, st_ch = 0, st_ci = 0;
+  auto seek = [&](int st) {
+    int t = 0;
+    while (st >= tbase[t + 1]) ++t;
+    const int rel = st - tbase[t], cnt = tcnt[t];
+    st_t = t;
+    st_ch = rel / cnt;
+    st_ci = rel - st_ch * cnt;
+  };
+  auto advance = [&]() {
+    if (++st_ci == tcnt[st_t]) {
+      st_ci = 0;
+      if (++st_ch == nchunk) {
+        st_ch = 0;
+        do ++st_t; while (st_t < 9 && tcnt[st_t] == 0);
+      }
+    }
+  };
+  auto bload = [&](int t, int ch, int code) {
+    const int koff = __builtin_amdgcn_readfirstlane(code * a.N * krow + ttap[t] * a.C + ch * 32);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      rbv[i] = bok[i] ? *reinterpret_cast<const uint4*>(wp + koff + boff[i]) : make_uint4(0u, 0u, 0u, 0u);
+  };
+  auto bstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 256 * i;
+      *reinterpret_cast<uint4*>(&sB[buf][cm_slot(id >> 2, id & 3)]) = rbv[i];
+    }
+  };
+  auto aload = [&](int t, int ch, Frag<bf16_t>* af, uint32_t& rq) {
+    const int d = __builtin_amdgcn_readfirstlane(tdelta[t]);
+    const int coff = ch * 32 + 8 * g;
+    rq = 0u;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const bool v = (rvalid[mi] >> t) & 1u;
+      const int pix = v ? rorg[mi] + d : 0;
+      af[mi].load(xp + (long long)pix * a.C + coff);
+      const uint32_t c = v ? ((t < 8 ? rc_lo[mi] >> (4 * t) : rc_hi[mi]) & 15u) : 0xffu;
+      rq |= c << (8 * mi);
+    }
+  };
   f32x4 acc[4][4];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nsteps > 0) {
-    V2_BLOAD(0);
-    V2_BSTORE(0);
+  int ccode = 0;
+  Frag<bf16_t> Ac[4], An[4];
+  uint32_t rqc = 0u, rqn = 0u;  // byte mi: code met by row mi at the step's tap (0xff: none)
+  if (s0 < s1) {
+    seek(s0);
+    ccode = tcl[tfirst[st_t] + st_ci];
+    bload(st_t, st_ch, ccode);
+    aload(st_t, st_ch, Ac, rqc);
+    bstore(0);
   }
   lds_barrier();
-  Frag<bf16_t> A[4];
-  uint32_t scode[4];
-  for (int st = 0; st < nsteps; ++st) {
-    const int sgi = st % nseg, tc = tc0 + st / nseg;
-    const int seg = segs[sgi];
-    if (st + 1 < nsteps) V2_BLOAD(st + 1);
-    if (sgi == 0) {  // new (tap, chunk): gather the A rows
-      const int tap = taps[tc / nchunk], ch = tc % nchunk;
-      const int ky = tap / 3, kx = tap % 3;
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        int iy, ix;
-        if (a.transposed) {
-          iy = (roy[mi] + 1 - ky) >> 1;
-          ix = (rox[mi] + 1 - kx) >> 1;
-        } else {
-          iy = roy[mi] * 2 - 1 + ky;
-          ix = rox[mi] * 2 - 1 + kx;
-        }
-        const bool inb = rvalid[mi] && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
-        const long long pix = inb ? ((long long)rb[mi] * a.Hi + iy) * a.Wi + ix : 0;
-        if (inb)
-          A[mi].load(xp + pix * a.C + ch * 32 + 8 * g);
-        else
-          A[mi].zero();
-        scode[mi] = a.mask_mode == MASK_SRC ? (inb ? a.code[pix] : 0u) : rcode[mi];
-      }
+  for (int st = s0; st < s1; ++st) {
+    int ncode = 0;
+    bool fresh = false;
+    if (st + 1 < s1) {  // prefetch step st+1: B always, A rows when its (tap, chunk) is new
+      advance();
+      ncode = tcl[tfirst[st_t] + st_ci];
+      bload(st_t, st_ch, ncode);
+      fresh = st_ci == 0;
+      if (fresh) aload(st_t, st_ch, An, rqn);
     }
     Frag<bf16_t> As[4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
-      As[mi] = A[mi];
-      if (seg < 4) As[mi].select((scode[mi] >> seg) & 1u);
+      As[mi] = Ac[mi];
+      As[mi].select(((rqc >> (8 * mi)) & 0xffu) == (uint32_t)ccode);
     }
+    const int buf = (st - s0) & 1;
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) {
       Frag<bf16_t> bf;
-      bf.v = *reinterpret_cast<const uint4*>(&sB[st & 1][wn * 64 + 16 * nj + r][8 * g]);
+      bf.v = *reinterpret_cast<const uint4*>(&sB[buf][cm_slot(wn * 64 + 16 * nj + r, g)]);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], As[mi], bf);
     }
-    if (st + 1 < nsteps) V2_BSTORE((st + 1) & 1);
+    if (st + 1 < s1) bstore(buf ^ 1);
+    if (fresh) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) Ac[mi] = An[mi];
+      rqc = rqn;
+    }
+    ccode = ncode;
     lds_barrier();
   }
-#undef V2_BLOAD
-#undef V2_BSTORE
-  if (a.ksplit > 1) {  // split-K: f32 slab, reduced + finished by k_splitk_finish
+  if (a.ksplit > 1) {  // split-K: f32 slab [split][class][m][N], reduced by k_splitk_finish
+    // slab rows: [split][class (in order)][m] = [split][B*Ho*Wo] in total
+    long long coff = 0;
+    for (int c = 0; c < cls; ++c)
+      coff += (long long)a.B * ((a.Ho - (c >> 1) + 1) >> 1) * ((a.Wo - (c & 1) + 1) >> 1);
+    float* slab = a.partial + ((long long)split * a.B * a.Ho * a.Wo + coff) * a.N;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
-        const long long m = mblk + wm * 64 + 16 * mi + 4 * g + reg;
+        const int m = mblk + wm * 64 + 16 * mi + 4 * g + reg;
         if (m >= Mtot) continue;
-        const int b = (int)(m / HWc);
-        const int rem = (int)(m % HWc);
-        const int i = rem / Wc, j = rem % Wc;
-        const int oy = a.transposed ? 2 * i + py : i;
-        const int ox = a.transposed ? 2 * j + px : j;
-        float* dst = a.partial + ((((long long)split * a.B + b) * a.Ho + oy) * a.Wo + ox) * a.N;
 #pragma unroll
         for (int nj = 0; nj < 4; ++nj) {
           const int n = n0 + wn * 64 + 16 * nj + r;
-          if (n < a.N) dst[n] = acc[mi][nj][reg];
+          if (n < a.N) slab[(long long)m * a.N + n] = acc[mi][nj][reg];
         }
       }
     return;
@@ -698,7 +913,8 @@ __global__ __launch_bounds__(256) void k_conv_igemm_v2(ConvArgs a) {
 }
 
 // split-K finish: sum the slabs in fixed order, add biases / residual, write NCHW (+NHWC) bf16.
-// One block per 32 pixels x 32 channels, transposed through LDS so both stores coalesce.
+// Slabs are [split][class][m][N] in k_conv_codes' row order (m over the batch x parity-class
+// grid).  One block per 32 pixels x 32 channels, transposed through LDS so both stores coalesce.
 __global__ __launch_bounds__(256) void k_splitk_finish(ConvArgs a) {
   __shared__ float tile[32][33];
   const long long P = (long long)a.B * a.Ho * a.Wo;
@@ -711,21 +927,31 @@ __global__ __launch_bounds__(256) void k_splitk_finish(ConvArgs a) {
     const int n = n0 + tx;
     float v = 0.f;
     if (p < P && n < a.N) {
-      for (int sp = 0; sp < a.ksplit; ++sp) v += a.partial[((long long)sp * P + p) * a.N + n];
-      const int b = (int)(p / HW);
+      const int b = (int)(p / HW), rem = (int)(p % HW), oy = rem / a.Wo, ox = rem % a.Wo;
+      int cls = 0, Hc = a.Ho, Wc = a.Wo, i = oy, j = ox;
+      if (a.transposed) {
+        cls = (oy & 1) * 2 + (ox & 1);
+        Hc = (a.Ho - (oy & 1) + 1) >> 1;
+        Wc = (a.Wo - (ox & 1) + 1) >> 1;
+        i = oy >> 1;
+        j = ox >> 1;
+      }
+      const long long m = ((long long)b * Hc + i) * Wc + j;
+      // class c's slab offset: sum of the row counts of classes < c
+      long long coff = 0;
+      for (int c = 0; c < cls; ++c) {
+        const int hc = (a.Ho - (c >> 1) + 1) >> 1, wc = (a.Wo - (c & 1) + 1) >> 1;
+        coff += (long long)a.B * hc * wc;
+      }
+      for (int sp = 0; sp < a.ksplit; ++sp) v += a.partial[((long long)sp * P + coff + m) * a.N + n];
       if (a.bias4) {
         const int nm = a.info[b].n_masks;
         float bs = 0.f;
-        for (int i = 0; i < nm; ++i) bs += a.bias4[i * a.N + n];
+        for (int q = 0; q < nm; ++q) bs += a.bias4[q * a.N + n];
         v += bs;
       }
-      if (a.out_nhwc) {
-        // NHWC store wants the residual too: read it (NCHW, strided) here
-        if (a.residual) v += bf16_to_f32(((const bf16_t*)a.residual)[((long long)b * a.N + n) * HW + (p % HW)]);
-        ((bf16_t*)a.out_nhwc)[p * a.N + n] = f32_to_bf16(v);
-      } else if (a.residual) {
-        v += bf16_to_f32(((const bf16_t*)a.residual)[((long long)b * a.N + n) * HW + (p % HW)]);
-      }
+      if (a.residual) v += bf16_to_f32(((const bf16_t*)a.residual)[((long long)b * a.N + n) * HW + rem]);
+      if (a.out_nhwc) ((bf16_t*)a.out_nhwc)[p * a.N + n] = f32_to_bf16(v);
     }
     tile[k][tx] = v;
   }
@@ -753,6 +979,9 @@ size_t v2_partial_bytes(const ConvArgs& a) {
   const int ks = v2_ksplit(conv_mmax(a), a.N, a.transposed ? 4 : 1, a.C, a.transposed);
   return ks > 1 ? align256((size_t)ks * a.B * a.Ho * a.Wo * a.N * sizeof(float)) : 0;
 }
+size_t tile_codes_bytes(const ConvArgs& a) {
+  return align256((size_t)(a.transposed ? 4 : 1) * ceil_div(conv_mmax(a), V2M) * 9 * sizeof(uint16_t));
+}
 
 template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
@@ -761,11 +990,15 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   long long Mmax = (long long)a.B * a.Ho * a.Wo;
   if (a.transposed) Mmax = (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2);
   if constexpr (sizeof(T) == 2) {
-    if (a.C % 32 == 0 && a.nseg == 5) {
+    RGBD_REQUIRE(a.C % 32 == 0 && a.N % 32 == 0, RGBD_E_SHAPE);  // code-merged bf16 path only
+    {
       ConvArgs b = a;
       b.ksplit = v2_ksplit(Mmax, a.N, nclass, a.C, a.transposed);
+      // workspace: [split-K slabs | tile code sets]
+      b.tile_codes = (uint16_t*)((char*)a.partial + v2_partial_bytes(a));
+      k_conv_tile_codes<<<dim3(ceil_div(Mmax, V2M), 1, nclass), V2M, 0, s>>>(b);
       dim3 grid2(ceil_div(Mmax, V2M), ceil_div(a.N, V2N), nclass * b.ksplit);
-      k_conv_igemm_v2<<<grid2, 256, 0, s>>>(b);
+      k_conv_codes<<<grid2, 256, 0, s>>>(b);
       if (b.ksplit > 1) {
         dim3 g3(ceil_div((long long)a.B * a.Ho * a.Wo, 32), ceil_div(a.N, 32));
         k_splitk_finish<<<g3, 256, 0, s>>>(b);
@@ -780,6 +1013,11 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   return RGBD_OK;
 }
 
+int dsam_wgrad_splits_codes(int B, int Cin, int Cout) {
+  // ~4 codes present per batch is typical; aim at ~3 live workgroups per CU
+  const long long tiles = (long long)ceil_div(9ll * Cin, WG_KK) * ceil_div(Cout, WG_O) * 4;
+  return (int)std::max<long long>(1, std::min<long long>(B, ceil_div(768, tiles)));
+}
 int dsam_wgrad_splits(int B, int Cin, int Cout) {
   const long long tiles = (long long)ceil_div(45ll * Cin, WG_KK) * ceil_div(Cout, WG_O);
   int sp = (int)std::min<long long>(B, std::max<long long>(1, ceil_div(1024, tiles)));
@@ -806,18 +1044,27 @@ int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H
   return RGBD_OK;
 }
 
+long long rgbd_dsam_packed_elems(int dtype, int Cin, int Cout) {
+  if (Cin <= 0 || Cout <= 0) return 0;
+  if (dtype == RGBD_F32) return 45ll * Cin * Cout;
+  if (dtype == RGBD_BF16) return 144ll * Cin * Cout;
+  return 0;
+}
+
 int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, int Cin, int Cout,
                            void* wfwd, void* wbwd, void* stream) {
   RGBD_REQUIRE(conv_w && proj_w && (wfwd || wbwd) && Cin > 0 && Cout > 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
-  const long long total = 45ll * Cin * Cout;
-  const int nb = (int)std::min<long long>(ceil_div(total, 256), 4096);
-  if (dtype == RGBD_F32)
+  if (dtype == RGBD_F32) {
+    const int nb = (int)std::min<long long>(ceil_div(45ll * Cin * Cout, 256), 4096);
     k_pack_dsam<float><<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (float*)wfwd, (float*)wbwd);
-  else if (dtype == RGBD_BF16)
-    k_pack_dsam<bf16_t><<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (bf16_t*)wfwd, (bf16_t*)wbwd);
-  else
+  } else if (dtype == RGBD_BF16) {
+    RGBD_REQUIRE(Cin % 32 == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
+    const int nb = (int)std::min<long long>(ceil_div(9ll * Cin * Cout, 256), 4096);
+    k_pack_dsam_codes<<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (bf16_t*)wfwd, (bf16_t*)wbwd);
+  } else {
     return RGBD_E_DTYPE;
+  }
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -841,8 +1088,9 @@ static ConvArgs dx_args(int B, int Cin, int h, int w, int Cout) {
 
 size_t rgbd_dsam_conv_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout) {
   if (dtype != RGBD_BF16 || B <= 0 || h <= 0 || w <= 0) return 256;
-  return std::max<size_t>(256, std::max(v2_partial_bytes(fwd_args(B, Cin, h, w, Cout)),
-                                        v2_partial_bytes(dx_args(B, Cin, h, w, Cout))));
+  const ConvArgs f = fwd_args(B, Cin, h, w, Cout), d = dx_args(B, Cin, h, w, Cout);
+  return std::max<size_t>(256, std::max(v2_partial_bytes(f) + tile_codes_bytes(f),
+                                        v2_partial_bytes(d) + tile_codes_bytes(d)));
 }
 
 int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
@@ -855,7 +1103,7 @@ int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd
   a.x = x_nhwc; a.code = code; a.w = wfwd;
   a.bias4 = bias; a.info = info; a.residual = residual; a.out_nchw = out_nchw; a.out_nhwc = out_nhwc;
   a.partial = (float*)ws;
-  RGBD_REQUIRE(ws || dtype != RGBD_BF16 || v2_partial_bytes(a) == 0, RGBD_E_ARG);
+  RGBD_REQUIRE(ws || dtype != RGBD_BF16, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32) return launch_conv<float>(a, s);
   if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);
@@ -872,17 +1120,39 @@ int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, in
   a.x = gout_nhwc; a.code = code; a.w = wbwd;
   a.residual = gin_nchw; a.out_nchw = dx_nchw; a.out_nhwc = dx_nhwc;
   a.partial = (float*)ws;
-  RGBD_REQUIRE(ws || dtype != RGBD_BF16 || v2_partial_bytes(a) == 0, RGBD_E_ARG);
+  RGBD_REQUIRE(ws || dtype != RGBD_BF16, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32) return launch_conv<float>(a, s);
   if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);
   return RGBD_E_DTYPE;
 }
 
+// bf16 workspace: [splits][16 codes][Cout][9 Cin] f32 partials | [B] f32 x Cout channel sums |
+// presence table [B][chunks] u16 | global code mask u32
+struct WgradWs {
+  size_t partial, csum, pres, gmask, total;
+};
+static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
+  WgradWs o;
+  size_t off = 0;
+  const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
+  const size_t part = dtype == RGBD_BF16 ? (size_t)dsam_wgrad_splits_codes(B, Cin, Cout) * 16 * Cout * 9 * Cin
+                                         : (size_t)dsam_wgrad_splits(B, Cin, Cout) * Cout * 45 * Cin;
+  o.partial = off;
+  off += align256(sizeof(float) * part);
+  o.csum = off;
+  off += align256(sizeof(float) * (size_t)B * Cout);
+  o.pres = off;
+  off += align256(sizeof(uint16_t) * (size_t)B * ((hwo + PXC - 1) / PXC));
+  o.gmask = off;
+  off += 256;
+  o.total = off;
+  return o;
+}
+
 size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout) {
-  (void)dtype; (void)h; (void)w;
-  const int sp = dsam_wgrad_splits(B, Cin, Cout);
-  return align256(sizeof(float) * (size_t)sp * Cout * 45 * Cin) + align256(sizeof(float) * (size_t)B * Cout);
+  if (B <= 0 || h <= 0 || w <= 0 || Cin <= 0 || Cout <= 0) return 256;
+  return wgrad_ws(dtype, B, Cin, h, w, Cout).total;
 }
 
 int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, const uint8_t* code,
@@ -892,27 +1162,39 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, c
   RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
   RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
-  const int sp = dsam_wgrad_splits(B, Cin, Cout);
-  float* partial = (float*)ws;
-  float* csum = (float*)((char*)ws + align256(sizeof(float) * (size_t)sp * Cout * 45 * Cin));
+  const WgradWs L = wgrad_ws(dtype, B, Cin, h, w, Cout);
+  float* partial = (float*)((char*)ws + L.partial);
+  float* csum = (float*)((char*)ws + L.csum);
   TimerScope ts("dsam_wgrad", s);
-  dim3 grid(ceil_div(45ll * Cin, 64), ceil_div(Cout, 64), sp);
   const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
   if (dtype == RGBD_F32) {
+    const int sp = dsam_wgrad_splits(B, Cin, Cout);
+    dim3 grid(ceil_div(45ll * Cin, 64), ceil_div(Cout, 64), sp);
     k_dsam_wgrad<float><<<grid, 256, 0, s>>>((const float*)gout_nchw, (const float*)x_nhwc, code, B, Cin, h, w,
                                              Cout, sp, partial);
     k_chan_sum<float><<<B * Cout, 256, 0, s>>>((const float*)gout_nchw, hwo, csum);
+    const long long total = 45ll * Cin * Cout;
+    k_dsam_wgrad_final<<<(int)std::min<long long>(ceil_div(total, 256), 4096), 256, 0, s>>>(
+        partial, sp, Cin, Cout, dconv_w, dproj_w);
   } else if (dtype == RGBD_BF16) {
-    dim3 g2(ceil_div(45ll * Cin, WG_KK), ceil_div(Cout, WG_O), sp);
-    k_dsam_wgrad_bf16<<<g2, 256, 0, s>>>((const bf16_t*)gout_nchw, (const bf16_t*)x_nhwc, code, B, Cin, h, w,
-                                         Cout, sp, partial);
+    RGBD_REQUIRE(Cin % 32 == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
+    const int spc = dsam_wgrad_splits_codes(B, Cin, Cout);
+    uint16_t* pres = (uint16_t*)((char*)ws + L.pres);
+    uint32_t* gmask = (uint32_t*)((char*)ws + L.gmask);
+    const hipError_t me = hipMemsetAsync(gmask, 0, sizeof(uint32_t), s);
+    if (me != hipSuccess) return (int)me;
+    const long long nthr = (long long)B * ((hwo + PXC - 1) / PXC) * 32;
+    k_code_presence<<<(int)ceil_div(nthr, 256), 256, 0, s>>>(code, B, h, w, pres, gmask);
+    dim3 g2(ceil_div(9ll * Cin, WG_KK), ceil_div(Cout, WG_O), spc * 16);
+    k_dsam_wgrad_bf16<<<g2, 256, 0, s>>>((const bf16_t*)gout_nchw, (const bf16_t*)x_nhwc, code, pres, gmask, B,
+                                         Cin, h, w, Cout, spc, partial);
     k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
+    const long long total = 9ll * Cin * Cout;
+    k_dsam_wgrad_combine<<<(int)std::min<long long>(ceil_div(total, 256), 4096), 256, 0, s>>>(
+        partial, spc, gmask, Cin, Cout, dconv_w, dproj_w);
   } else {
     return RGBD_E_DTYPE;
   }
-  const long long total = 45ll * Cin * Cout;
-  k_dsam_wgrad_final<<<(int)std::min<long long>(ceil_div(total, 256), 4096), 256, 0, s>>>(
-      partial, sp, Cin, Cout, dconv_w, dproj_w);
   k_dsam_bias_grad<<<ceil_div(4 * Cout, 256), 256, 0, s>>>(csum, info, B, Cout, dbias);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;

@@ -6,8 +6,10 @@ memory is plumbing), passes raw pointers + the current HIP stream to the C ABI a
 ``decode_info`` (explicitly a host read-back for tests/diagnostics).
 """
 import ctypes
+import math
 
 import numpy as np
+
 import torch
 
 from . import _lib
@@ -175,13 +177,23 @@ def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
 
 
 def dsam_pack(conv_w: torch.Tensor, proj_w: torch.Tensor, dtype: torch.dtype):
-    """conv_w float32 [4,Co,Ci,3,3], proj_w [Co,Ci,3,3] -> (wfwd [Co,45*Ci], wbwd [Ci,45*Co])."""
+    """conv_w float32 [4,Co,Ci,3,3], proj_w [Co,Ci,3,3] -> (wfwd, wbwd):
+    float32 segment form wfwd [Co,45*Ci], wbwd [Ci,45*Co]; bfloat16 code-merged form
+    wfwd [16,Co,9*Ci], wbwd [16,Ci,9*Co] (include/rgbd_hip.h)."""
     cw = conv_w.detach().float().contiguous()
     pw = proj_w.detach().float().contiguous()
     _need_cuda(cw, pw)
     Co, Ci = pw.shape[:2]
-    wfwd = torch.empty((Co, 45 * Ci), dtype=dtype, device=cw.device)
-    wbwd = torch.empty((Ci, 45 * Co), dtype=dtype, device=cw.device)
+    if dtype == torch.bfloat16:
+        if Ci % 32 or Co % 32:
+            raise ValueError(f"bfloat16 DSAM needs channel counts that are multiples of 32, got {Ci}->{Co}")
+        fshape, bshape = (16, Co, 9 * Ci), (16, Ci, 9 * Co)
+    else:
+        fshape, bshape = (Co, 45 * Ci), (Ci, 45 * Co)
+    n = _lib.lib().rgbd_dsam_packed_elems(_dtype_code(torch.empty(0, dtype=dtype)), Ci, Co)
+    assert n == math.prod(fshape) == math.prod(bshape), (n, fshape, bshape)
+    wfwd = torch.empty(fshape, dtype=dtype, device=cw.device)
+    wbwd = torch.empty(bshape, dtype=dtype, device=cw.device)
     check(_lib.lib().rgbd_dsam_pack_weights(_dtype_code(wfwd), _p(cw), _p(pw), Ci, Co, _p(wfwd), _p(wbwd),
                                             _stream(cw.device)), "rgbd_dsam_pack_weights")
     return wfwd, wbwd
@@ -192,7 +204,7 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     """x_nhwc [B,h,w,Ci] -> (out_nchw [B,Co,ho,wo], out_nhwc or None)."""
     _need_cuda(x_nhwc, code, info, wfwd, bias4, residual)
     B, h, w, Ci = x_nhwc.shape
-    Co = wfwd.shape[0]
+    Co = wfwd.shape[-2]
     ho, wo = (h + 1) // 2, (w + 1) // 2
     if tuple(code.shape) != (B, h, w):
         raise ValueError(f"region code {tuple(code.shape)} does not match features {(B, h, w)}")
@@ -212,7 +224,7 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
 def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False):
     _need_cuda(gout_nhwc, code, wbwd, gin_nchw)
     B, ho, wo, Co = gout_nhwc.shape
-    Ci = wbwd.shape[0]
+    Ci = wbwd.shape[-2]
     _, h, w = code.shape
     if gin_nchw is not None and tuple(gin_nchw.shape) != (B, Ci, h, w):
         raise ValueError("gin shape mismatch")

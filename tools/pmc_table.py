@@ -1,10 +1,16 @@
-"""Average PMC counter values per kernel from a rocprofv3 counter_collection CSV."""
+"""Average PMC counter values per (kernel, grid) from rocprofv3 counter_collection CSVs."""
 import collections, csv, sys
-rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for r in rows:
-    agg[r['Kernel_Name'].split('(')[0][-40:]][r['Counter_Name']].append(float(r['Counter_Value']))
-for k, d in agg.items():
-    if 'rocclr' in k or 'at::native' in k:
-        continue
-    print(f"{k:40s}", {c: f"{sum(v) / len(v):.4g}" for c, v in d.items()})
+order = []
+for path in sys.argv[1:]:
+    for r in csv.DictReader(open(path)):
+        n = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '')
+        if 'rocclr' in n or 'at::native' in n:
+            continue
+        key = (n[-28:], r['Grid_Size'])
+        if key not in agg:
+            order.append(key)
+        agg[key][r['Counter_Name']].append(float(r['Counter_Value']))
+for k in order:
+    d = agg[k]
+    print(f"{k[0]:28s} {k[1]:>9s}", " ".join(f"{c}={sum(v) / len(v):.4g}" for c, v in d.items()))
