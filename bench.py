@@ -39,6 +39,23 @@ import _rgbd_import  # noqa: E402,F401
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip table)
 HBM_PEAK_GBS = 8000.0
 CONV5_FLOP_PER_PX = 2 * 128 * 9 * 256  # 3x3 128->256 (custom_model.py:1413)
+CONV5_KERNEL = "k_rp_conv3x3_v3"
+
+
+def pmc_traffic(kernel, default_shape):
+    """HBM bytes per launch of ``kernel`` from the newest committed PMC table
+    (profiles/*/pmc_traffic.json, written by tools/gpu_traffic.sh + tools/traffic_table.py over
+    this bench's default step: FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE).
+    rocprofv3 cannot run inside this process, so the counters come from their own passes; the
+    value is null for a non-default shape or when no table holds this kernel."""
+    if not default_shape:
+        return None
+    best = None
+    for path in sorted((REPO / "profiles").glob("*/pmc_traffic.json")):
+        for key, row in json.loads(path.read_text()).items():
+            if key.split(" grid=")[0] == kernel and "hbm_bytes" in row:
+                best = (row["hbm_bytes"], str(path.relative_to(REPO)))
+    return best
 
 
 def parse(argv=None):
@@ -207,6 +224,7 @@ def main():
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     flop = CONV5_FLOP_PER_PX * B * args.height * args.width
     achieved = flop / (conv_avg_ms * 1e-3) / 1e12
+    traffic = pmc_traffic(CONV5_KERNEL, (B, args.height, args.width, args.dtype) == (8, 480, 640, "bf16"))
     out = {
         "metric": "NYUv2 640x480 RGB-D img/s (fwd+bwd) of the DGGM+E-DSAM hot path",
         "value": round(value, 2),
@@ -228,7 +246,10 @@ def main():
         "kernel_ms": dict(rp_conv3x3=round(conv_avg_ms, 4), **others),
         "roofline": {"bound": "mfma", "kernel": "k_rp_conv3x3 (3x3 128->256, custom_model.py:1413)",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None},
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
+                     "traffic": None if traffic is None else round(traffic[0]),
+                     "traffic_unit": "bytes/launch", "traffic_source": None if traffic is None else traffic[1],
+                     "algorithmic_bytes": (128 + 256) * 2 * B * args.height * args.width},
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, args)
