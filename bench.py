@@ -9,7 +9,9 @@ a batch of synthetic NYUv2-shaped frames (640x480, 8 images per GPU, bf16 MFMA):
   -> DSAM x3 masked implicit GEMMs (cascade) + DGGM + sum     (K5, K2)
   -> backward from a fixed synthetic upstream gradient of the 4 backbone features:
      DSAM dW/db/dX cascade + DGGM dW/db                        (K5, K2)
-  -> (N > 1) RCCL all-reduce of the hot-path parameter gradients (DDP semantics).
+  -> (N > 1) RCCL all-reduce of the hot-path parameter gradients (DDP semantics)
+  -> AdamW step on the hot-path parameters (HF Trainer's optimizer; lr 1e-5 constant,
+     mask2former/config.json), so every step re-packs the changed DSAM filters.
 The Swin encoder / pixel decoder / transformer decoder are outside the hot path (SURVEY §8(f)
 "next"); their colour-feature inputs are synthetic tensors of the Swin-T shapes.
 
@@ -116,6 +118,7 @@ def make_step(ctx, world, inference=False):
     from rgbd_amd.distributed import GradBucket
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
     bucket = GradBucket(params) if world > 1 else None
+    opt = None if inference else torch.optim.AdamW(params, lr=1e-5, fused=True)
 
     def step():
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
@@ -128,8 +131,8 @@ def make_step(ctx, world, inference=False):
         torch.autograd.backward(feats, ctx["gouts"])
         if bucket is not None:  # DDP gradient exchange of the hot-path parameters (RCCL over xGMI)
             bucket.allreduce_mean()
-        for p in params:
-            p.grad = None
+        opt.step()
+        opt.zero_grad(set_to_none=True)
         return feats
     return step
 
@@ -239,7 +242,7 @@ def main():
         "dtype": "bf16" if args.dtype == "bf16" else "f32",
         "data": "synthetic (seeded NYUv2-shaped RGB-D scenes; deterministic random-init weights)",
         "config": {"workload": f"hot-path train step (ratio predictor train-mode + decomposition + DSAM x3 + "
-                               f"DGGM, fwd+bwd), {args.width}x{args.height}, batch {B}/GPU",
+                               f"DGGM, fwd+bwd + AdamW), {args.width}x{args.height}, batch {B}/GPU",
                    "global_batch": B * world, "height": args.height, "width": args.width,
                    "parallelism": f"dp{world}"},
         "inference_img_s": inf,

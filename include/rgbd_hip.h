@@ -113,12 +113,20 @@ int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H
  *   wfwd [Cout][5][9][Cin]  (forward: k = (seg, tap, ci))
  *   wbwd [Cin][5][9][Cout]  (dX: k = (seg, tap, co), taps NOT flipped; see csrc)
  * RGBD_BF16 (code-merged form, Cin and Cout multiples of 32): for each 4-bit region code k
- * the merged filter W_k = proj + sum_{i in k} conv_i,
- *   wfwd [16][Cout][9][Cin],  wbwd [16][Cin][9][Cout].
+ * the merged filter W_k = proj + sum_{i in k} conv_i, as contiguous per-(code, tap, 32-channel
+ * chunk) tiles with the 16-byte chunks of each 64-byte row XOR-swizzled by (row >> 2) & 3,
+ *   wfwd [16 k][9 tap][Cin/32][Cout][32],  wbwd [16 k][9 tap][Cout/32][Cin][32],
+ * each followed by a 192x32-element tail pad;
+ * only the codes whose bit is set in *code_mask (a device uint32, e.g. from
+ * rgbd_dsam_code_masks; NULL = all 16) are written, and wbwd may be NULL (inference).
  * rgbd_dsam_packed_elems gives the element count of each of wfwd / wbwd. */
 long long rgbd_dsam_packed_elems(int dtype, int Cin, int Cout);
 int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, int Cin,
-                           int Cout, void* wfwd, void* wbwd, void* stream);
+                           int Cout, const uint32_t* code_mask, void* wfwd, void* wbwd, void* stream);
+/* masks[i] (device uint32, OVERWRITTEN) = OR over the bytes of code map i of (1 << code):
+ * the region codes present at one DSAM input resolution (n <= 8 maps). */
+int rgbd_dsam_code_masks(int n, const uint8_t* const* codes_host, const long long* nbytes_host,
+                         uint32_t* masks, void* stream);
 
 /* ---------------------------------------------------------------- K5 DSAM masked conv
  * Forward of one DSAModule for the whole batch (replaces the per-sample Python loop of
@@ -141,11 +149,13 @@ int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, in
                        void* dx_nhwc, void* ws, void* stream);
 /* dW / db of one DSAModule: dconv_w float32 [4][Cout][Cin][3][3], dproj_w float32
  * [Cout][Cin][3][3], dbias float32 [4][Cout] (all OVERWRITTEN).  gout_nchw: dtype
- * [B][Cout][ho][wo]; x_nhwc as in the forward. */
+ * [B][Cout][ho][wo]; gout_nhwc: the same gradient as [B][ho][wo][Cout] (required for
+ * RGBD_BF16, ignored for RGBD_F32); x_nhwc as in the forward. */
 size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout);
-int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, const uint8_t* code,
-                         const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
-                         float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream);
+int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
+                         const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h,
+                         int w, int Cout, float* dconv_w, float* dproj_w, float* dbias, void* ws,
+                         void* stream);
 
 /* ---------------------------------------------------------------- K4 ratio predictor
  * EnhancedDepthImageRatioPredictor.forward (custom_model.py:1444-1487) for the batch:

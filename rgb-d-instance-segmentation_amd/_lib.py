@@ -39,12 +39,13 @@ SIGNATURES = {
     "rgbd_dggm_fuse_bwd": (_I, [_I, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_nchw_to_nhwc": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
     "rgbd_dsam_packed_elems": (_LL, [_I, _I, _I]),
-    "rgbd_dsam_pack_weights": (_I, [_I, _P, _P, _I, _I, _P, _P, _P]),
+    "rgbd_dsam_pack_weights": (_I, [_I, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "rgbd_dsam_code_masks": (_I, [_I, _P, _P, _P, _P]),
     "rgbd_dsam_conv_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rgbd_dsam_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_data": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_weight_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
-    "rgbd_dsam_bwd_weight": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "rgbd_dsam_bwd_weight": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_timing_enable": (_I, [_I]),
     "rgbd_timing_read": (ctypes.c_double, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "rgbd_ratio_packed_size": (_SZ, [_I]),

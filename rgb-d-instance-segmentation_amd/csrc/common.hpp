@@ -87,6 +87,44 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// One LDS-DMA wave instruction: 64 lanes x 16 B from per-lane global sources to
+// lds_base + 16 * lane (lds_base wave-uniform; it goes through M0).
+__device__ __forceinline__ void dma_lds16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_base)
+               : "memory");
+}
+
+// Ring-pipeline hand-off: this wave's DMA pieces older than the newest N have landed and its LDS
+// reads are done, then the workgroup barrier (no compiler-visible global loads may be in flight
+// in such a loop: they share vmcnt with the DMA).
+template <int N>
+__device__ __forceinline__ void vm_wait_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// vm_wait_barrier for a run-time count (wave-uniform); counts past 23 wait for 23 (more waiting,
+// never less).
+__device__ __forceinline__ void vm_wait_barrier_dyn(int n) {
+  switch (n) {
+#define RGBD_VMW_CASE(k) \
+  case k:                \
+    vm_wait_barrier<k>(); \
+    break;
+    RGBD_VMW_CASE(0) RGBD_VMW_CASE(1) RGBD_VMW_CASE(2) RGBD_VMW_CASE(3) RGBD_VMW_CASE(4) RGBD_VMW_CASE(5)
+    RGBD_VMW_CASE(6) RGBD_VMW_CASE(7) RGBD_VMW_CASE(8) RGBD_VMW_CASE(9) RGBD_VMW_CASE(10) RGBD_VMW_CASE(11)
+    RGBD_VMW_CASE(12) RGBD_VMW_CASE(13) RGBD_VMW_CASE(14) RGBD_VMW_CASE(15) RGBD_VMW_CASE(16) RGBD_VMW_CASE(17)
+    RGBD_VMW_CASE(18) RGBD_VMW_CASE(19) RGBD_VMW_CASE(20) RGBD_VMW_CASE(21) RGBD_VMW_CASE(22)
+#undef RGBD_VMW_CASE
+    default:
+      vm_wait_barrier<23>();
+      break;
+  }
+}
+
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 

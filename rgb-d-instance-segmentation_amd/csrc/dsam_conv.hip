@@ -17,6 +17,8 @@
 // are split into the four stride-2 parity classes so only live taps are visited, and the
 // mask bit is taken at the OUTPUT pixel (d(x*m)/dx = m).  dW contracts over pixels with an
 // LDS-staged im2col tile.
+#include <cstdlib>
+
 #include "mfma.hpp"
 #include "timing.hpp"
 
@@ -39,9 +41,15 @@ struct ConvArgs {
   const void* residual;             // NCHW [B][N][Ho][Wo] added in the epilogue (optional)
   void* out_nchw;                   // optional
   void* out_nhwc;                   // optional
-  int ksplit;                       // v2 only: K split over (tap, chunk) ranges (1 = none)
-  float* partial;                   // v2 split-K slabs: f32 [ksplit][B][Ho][Wo][N]
-  uint16_t* tile_codes;             // bf16: [nclass][M tiles][9] codes present per tap
+  int ksplit;                       // unused (1)
+  int dbg;                          // diagnostics (RGBD_DSAM_DBG): 1 skip steps
+  uint16_t* tmasks;                 // bf16: [class][tile][16] per-tap code sets (k_dsam_plan)
+  int* items;                       // bf16: work list of k_dsam_lds (k_dsam_items)
+  int* nitems;
+  int* tickets;                     // bf16: per (class, tile, N tile) chunk counter, zeroed by k_dsam_plan
+  int ntiles0;                      // bf16: tiles of the largest class
+  int chunk_len;                    // bf16: steps per workgroup chunk of a tile
+  float* partial;                   // bf16: partial tiles of multi-chunk tiles (reduced by their last chunk)
 };
 
 constexpr int BM = 64, BN = 64;
@@ -214,32 +222,80 @@ __global__ void k_pack_dsam(const float* __restrict__ conv_w, const float* __res
   }
 }
 
-// bf16 code-merged filters: W_k = proj + sum_{i in k} conv_i for every 4-bit code k (fixed
-// summation order: proj, then conv_0..conv_3, in f32, rounded once).  wfwd[k][o][tap*Cin + c],
-// wbwd[k][c][tap*Cout + o].
-__global__ void k_pack_dsam_codes(const float* __restrict__ conv_w, const float* __restrict__ proj_w, int Cin,
-                                  int Cout, bf16_t* __restrict__ wfwd, bf16_t* __restrict__ wbwd) {
-  const long long per = (long long)Cout * Cin * 9;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < per;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int tap = (int)(e % 9);
-    const int c = (int)((e / 9) % Cin);
-    const int o = (int)(e / (9ll * Cin));
-    float w4[4];
+// bf16 code-merged filters W_k = proj + sum_{i in k} conv_i (fixed summation order: proj, then
+// conv_0..conv_3, in f32, rounded once), packed for the codes present in the batch only (bit k of
+// *code_mask; all 16 when code_mask is NULL), as the B tiles of k_dsam_lds:
+//   wfwd [16 code][9 tap][Cin/32 chunk][Cout n][32 c]   (forward: rows n = output channels)
+//   wbwd [16 code][9 tap][Cout/32 chunk][Cin n][32 o]   (dX: rows n = input channels)
+// so the tile of one (code, tap, chunk) is contiguous (one linear LDS-DMA stream), with the four
+// 16-byte chunks of each 64-byte row stored XOR-swizzled by (n >> 2) & 3 (the LDS image the
+// MFMA fragment reads want).  A one-tile tail pad keeps an over-reading last N tile in bounds.
+__device__ __forceinline__ int pk_pos(int n, int c) { return ((((c >> 3) ^ (n >> 2)) & 3) << 3) | (c & 7); }
+
+__global__ __launch_bounds__(256) void k_pack_fwd_codes(const float* __restrict__ conv_w, const float* __restrict__ proj_w,
+                                                        int Cin, int Cout, const uint32_t* __restrict__ code_mask,
+                                                        bf16_t* __restrict__ wfwd) {
+  extern __shared__ float srow[];  // [5][Cin*9] OIHW rows of output channel o: conv_0..3, proj
+  const int o = blockIdx.x, KK = 9 * Cin, nch = Cin / 32;
+  const uint32_t m = code_mask ? *code_mask : 0xffffu;
+  for (int e = threadIdx.x; e < KK; e += 256) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w4[i] = conv_w[(((long long)i * Cout + o) * Cin + c) * 9 + tap];
-    const float wp = proj_w[e];
-#pragma unroll 1
-    for (int k = 0; k < 16; ++k) {
-      float v = wp;
+    for (int i = 0; i < 4; ++i) srow[i * KK + e] = conv_w[((long long)i * Cout + o) * KK + e];
+    srow[4 * KK + e] = proj_w[(long long)o * KK + e];
+  }
+  __syncthreads();
+  for (int k = 0; k < 16; ++k) {
+    if (!((m >> k) & 1u)) continue;
+    for (int e2 = threadIdx.x; e2 < KK / 2; e2 += 256) {  // element pair (tap, c), (tap, c+1)
+      const int e = 2 * e2, tap = e / Cin, c = e % Cin;
+      float v[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if ((k >> i) & 1) v += w4[i];
-      const bf16_t tv = f32_to_bf16(v);
-      if (wfwd) wfwd[((long long)k * Cout + o) * 9 * Cin + (long long)tap * Cin + c] = tv;
-      if (wbwd) wbwd[((long long)k * Cin + c) * 9 * Cout + (long long)tap * Cout + o] = tv;
+      for (int h = 0; h < 2; ++h) {
+        const int src = (c + h) * 9 + tap;
+        float s = srow[4 * KK + src];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if ((k >> i) & 1) s += srow[i * KK + src];
+        v[h] = s;
+      }
+      const long long tile = ((long long)(k * 9 + tap) * nch + (c >> 5)) * Cout + o;
+      *reinterpret_cast<uint32_t*>(wfwd + tile * 32 + pk_pos(o, c & 31)) =
+          (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
     }
   }
+}
+
+// wbwd from wfwd: per (code, tap, 32x32 (o, c) block) an LDS transpose
+__global__ __launch_bounds__(256) void k_pack_bwd_codes(const bf16_t* __restrict__ wfwd, int Cin, int Cout,
+                                                        const uint32_t* __restrict__ code_mask,
+                                                        bf16_t* __restrict__ wbwd) {
+  __shared__ bf16_t tile[32][34];
+  const int k = blockIdx.z / 9, tap = blockIdx.z % 9;
+  const uint32_t m = code_mask ? *code_mask : 0xffffu;
+  if (!((m >> k) & 1u)) return;
+  const int cch = blockIdx.x, och = blockIdx.y, nci = Cin / 32, nco = Cout / 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const bf16_t* src = wfwd + (((long long)(k * 9 + tap) * nci + cch) * Cout + och * 32) * 32;
+  for (int i = ty; i < 32; i += 8) tile[i][tx] = src[i * 32 + pk_pos(och * 32 + i, tx)];  // [o][c]
+  __syncthreads();
+  bf16_t* dst = wbwd + (((long long)(k * 9 + tap) * nco + och) * Cin + cch * 32) * 32;
+  for (int i = ty; i < 32; i += 8) dst[i * 32 + pk_pos(cch * 32 + i, tx)] = tile[tx][i];  // [c][o]
+}
+
+// OR of (1 << code) over each code map (codes present per DSAM input resolution).
+struct CodeMaps {
+  const uint8_t* p[8];
+  long long n[8];
+};
+__global__ __launch_bounds__(256) void k_code_masks(CodeMaps cm, uint32_t* __restrict__ masks) {
+  const int y = blockIdx.y;
+  const uint8_t* p = cm.p[y];
+  const long long n = cm.n[y];
+  uint32_t m = 0u;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) m |= 1u << (p[i] & 15);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+  if ((threadIdx.x & 63) == 0 && m) atomicOr(masks + y, m);
 }
 
 template <typename T>
@@ -347,27 +403,69 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, 
     }
 }
 
-// bf16 dW, code-merged (see k_conv_codes): the workgroup for code k accumulates
+// bf16 dW, code-merged: the workgroup for code k accumulates
 //   dW_k[o][tap][c] = sum over output px p with code(src(p, tap)) == k of G[p][o] X[src][c]
-// over its batch split, skipping every 32-px chunk whose rows never meet code k (presence table
-// from k_code_presence: no loads at all); k_dsam_wgrad_combine folds dW_k into the five filters
-// (conv_i gets the codes with bit i, proj gets all).  Work ~ one dense dW instead of
-// popcount + 1 of them.  X tile staged [px][kk] from NHWC with 16-byte loads, read back transposed
-// with ds_read_b64_tr_b16 (gfx950) as the MFMA B operand; the A operand (G^T, 8 consecutive
-// pixels of one channel, NCHW) is loaded one chunk ahead into registers.
-constexpr int WG_KK = 128, WG_O = 64, PXC = 32, XPAD = 136;
+// over a contiguous range of 64-px units (unit = 64 raster-consecutive output pixels of one
+// image), visiting only the units whose sources meet code k (presence table of
+// k_code_presence, compacted into an LDS list in the prologue).  k_dsam_wgrad_combine folds the
+// dW_k into the five filters (conv_i gets the codes with bit i, proj gets all): work ~ one dense
+// dW instead of popcount + 1 of them.
+//
+// Tile: 32*FM output channels (o) x 128 kk (kk = tap*Cin + c: four 32-wide blocks, each inside
+// one tap) per workgroup, 4 waves as 2x2 (wave tile 16*FM x 64); 64 px per step = two MFMA
+// k-blocks.  Per step the operands arrive by LDS-DMA in an S-deep ring, S-1 steps ahead:
+//   G  [64 px][32*FM o] from the NHWC upstream gradient (FM blocks of 64-byte rows),
+//   X  [64 px][4 x 32 c] im2col rows from the NHWC input.  A row whose source pixel is outside
+//      the input, has a region code other than k, or lies past the image's last output pixel
+//      still copies a valid (clamped) pixel; its 64-px x 4-block mask is published through LDS
+//      and applied to the X fragments in registers (a zero-line source for masked lanes would
+//      be an L2-channel hot spot).
+// The region codes the step needs are read from an LDS copy of the code rows the workgroup's
+// units can reach (no compiler-visible global load in the step loop).  Both MFMA operands
+// are read with ds_read_b64_tr_b16 ([px][col] -> k-major fragments); rows are XOR-swizzled by
+// row bit 3 so the 32-lane halves of a transposed read fall on disjoint banks.
+constexpr int WPX = 64;             // output pixels per unit / step
+constexpr int WCODE_BYTES = 16384;  // LDS budget for the code rows
+constexpr int WLIST_MAX = 2048;     // units per workgroup (u16 list)
+constexpr int WIMG_MAX = 32;        // images per workgroup
 typedef __attribute__((ext_vector_type(4))) short v4s;
 
-__global__ void k_code_presence(const uint8_t* __restrict__ code, int B, int h, int w,
-                                uint16_t* __restrict__ pres, uint32_t* __restrict__ gmask) {
-  // one 32-lane group per (b, 32-px output chunk): OR of 1 << code over the chunk's 9-tap sources
-  const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo, nchunk = (hwo + PXC - 1) / PXC;
-  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  const long long grp = t >> 5;
-  const int l = (int)(t & 31);
+template <int FM>
+struct WgCfg {
+  static constexpr int S = FM == 6 ? 3 : 4;
+  static constexpr int NBLK = FM + 4;            // 4 KB blocks per stage: FM of G, 4 of X
+  static constexpr int STAGE = NBLK * WPX * 64;
+  static constexpr int PER = NBLK;               // DMA pieces per wave per step
+  static constexpr int OFF_CODES = S * STAGE;
+  static constexpr int OFF_LIST = OFF_CODES + WCODE_BYTES;
+  static constexpr int OFF_TAB = OFF_LIST + 2 * WLIST_MAX;
+  static constexpr int OFF_MASK = OFF_TAB + 8 * WIMG_MAX + 64;  // [S][4 blocks][4 waves] u16
+  static constexpr size_t SMEM = (size_t)OFF_MASK + 32 * S;
+  static_assert(SMEM <= 163840, "dW LDS budget");
+};
+
+__device__ __forceinline__ int wg_swz(int row) { return ((row >> 3) & 1) << 1; }
+
+struct WgArgs {
+  const bf16_t* gout;     // NHWC [B][ho][wo][Cout]
+  const bf16_t* x;        // NHWC [B][h][w][Cin]
+  const uint8_t* code;    // [B][h][w]
+  const uint16_t* pres;   // [B * nunit] bit k: code k met by the unit's sources
+  const uint32_t* gmask;  // codes present in the batch
+  int B, Cin, h, w, Cout, ho, wo, nunit, splits;
+  float inv_wo;
+  float* partial;         // [splits][16][Cout][9*Cin] f32
+};
+
+__global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict__ code, int B, int h, int w,
+                                                       uint16_t* __restrict__ pres, uint32_t* __restrict__ gmask) {
+  // one wave per 64-px unit: OR of 1 << code over its 9-tap sources
+  const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo, nunit = (hwo + WPX - 1) / WPX;
+  const long long u = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+  const int l = threadIdx.x & 63;
   uint32_t m = 0u;
-  if (grp < (long long)B * nchunk) {
-    const int b = (int)(grp / nchunk), p = (int)(grp % nchunk) * PXC + l;
+  if (u < (long long)B * nunit) {
+    const int b = (int)(u / nunit), p = (int)(u % nunit) * WPX + l;
     if (p < hwo) {
       const int oy = p / wo, ox = p % wo;
       for (int tap = 0; tap < 9; ++tap) {
@@ -377,170 +475,241 @@ __global__ void k_code_presence(const uint8_t* __restrict__ code, int B, int h, 
     }
   }
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o);
-  if (l == 0 && grp < (long long)B * nchunk) {
-    pres[grp] = (uint16_t)m;
+  for (int o = 1; o < 64; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+  if (l == 0 && u < (long long)B * nunit) {
+    pres[u] = (uint16_t)m;
     if (m) atomicOr(gmask, m);
   }
 }
 
-__global__ __launch_bounds__(256) void k_dsam_wgrad_bf16(const bf16_t* __restrict__ gout, const bf16_t* __restrict__ x,
-                                                         const uint8_t* __restrict__ code,
-                                                         const uint16_t* __restrict__ pres,
-                                                         const uint32_t* __restrict__ gmask, int B, int Cin, int h,
-                                                         int w, int Cout, int splits, float* __restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][PXC][XPAD];
+// input rows of image b reachable from output units [uf, ul] of that image (3x3 s2 p1)
+__device__ __forceinline__ void wg_rows(const WgArgs& a, int b, int u0, int u1, int& r0, int& r1) {
+  const int uf = max(u0, b * a.nunit), ul = min(u1, (b + 1) * a.nunit) - 1;
+  const int pf = (uf - b * a.nunit) * WPX, pl = min(a.ho * a.wo, (ul - b * a.nunit + 1) * WPX) - 1;
+  r0 = max(0, 2 * (pf / a.wo) - 1);
+  r1 = min(a.h, 2 * (pl / a.wo) + 2);
+}
+
+template <int FM>
+__global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
+  using Cfg = WgCfg<FM>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int kcode = blockIdx.z & 15, split = blockIdx.z >> 4;
-  if (!((*gmask >> kcode) & 1u)) return;  // code absent from the batch: no partial, combine skips it
-  const int ho = (h + 1) / 2, wo = (w + 1) / 2;
-  const int hwo = ho * wo;
-  const int KK = 9 * Cin;
-  const int kk0 = blockIdx.x * WG_KK, o0 = blockIdx.y * WG_O;
-  const int b0 = (int)((long long)split * B / splits), b1 = (int)((long long)(split + 1) * B / splits);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (!((*a.gmask >> kcode) & 1u)) return;  // code absent from the batch: combine skips it
+  uint8_t* scode = (uint8_t*)(smem + Cfg::OFF_CODES);
+  uint16_t* slist = (uint16_t*)(smem + Cfg::OFF_LIST);
+  int* img_off = (int*)(smem + Cfg::OFF_TAB);   // [WIMG_MAX] LDS offset of image b0+i's first row
+  int* img_row0 = img_off + WIMG_MAX;           // [WIMG_MAX] first input row held
+  int* wave_cnt = img_row0 + WIMG_MAX;          // [4] + total
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
-  // staging role: pixel row spx, two 8-channel chunks at kk0 + 16*skg + 8*q
-  const int spx = threadIdx.x >> 3, skg = threadIdx.x & 7;
-  int s_ky[2], s_kx[2], s_c[2];
-  bool s_ok[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int kk = kk0 + 16 * skg + 8 * q;
-    s_ok[q] = kk < KK;
-    const int k2 = s_ok[q] ? kk : 0;
-    const int tap = k2 / Cin;
-    s_ky[q] = tap / 3;
-    s_kx[q] = tap % 3;
-    s_c[q] = k2 % Cin;
-  }
-  const int nchunk = (hwo + PXC - 1) / PXC;
-  const int total = (b1 - b0) * nchunk;
-  auto chunk_live = [&](int it) {
-    return (pres[(long long)(b0 + it / nchunk) * nchunk + it % nchunk] >> kcode) & 1u;
-  };
-  auto next_live = [&](int it) {
-    while (it < total && !chunk_live(it)) ++it;
-    return it;
-  };
-  int staged_any = 0;  // does the staged chunk hold any element of code k?
-  auto stage = [&](int buf, int it) {
-    const int b = b0 + it / nchunk, p = (it % nchunk) * PXC + spx;
-    const int oy = p / wo, ox = p % wo;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int iy = 2 * oy - 1 + s_ky[q], ix = 2 * ox - 1 + s_kx[q];
-      bool ok = s_ok[q] && p < hwo && iy >= 0 && iy < h && ix >= 0 && ix < w;
-      const long long pix = ((long long)b * h + iy) * w + ix;
-      if (ok) ok = code[pix] == kcode;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (ok) v = *reinterpret_cast<const uint4*>(x + pix * Cin + s_c[q]);
-      staged_any |= ok ? 1 : 0;
-      *reinterpret_cast<uint4*>(&Xs[buf][spx][16 * skg + 8 * q]) = v;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int KK = 9 * a.Cin, hwo = a.ho * a.wo;
+  const int kk0 = blockIdx.x * 128, o0 = blockIdx.y * 32 * FM;
+  const int U = a.B * a.nunit;
+  const int u0 = (int)((long long)split * U / a.splits), u1 = (int)((long long)(split + 1) * U / a.splits);
+  const int b0 = u0 / a.nunit, b1 = u1 > u0 ? (u1 - 1) / a.nunit : b0;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  uint16_t* smask = (uint16_t*)(smem + Cfg::OFF_MASK);
+  // ---- prologue 1: code rows of every image the units reach
+  if (tid == 0) {
+    int off = 0;
+    for (int b = b0; b <= b1 && u1 > u0; ++b) {
+      int r0, r1;
+      wg_rows(a, b, u0, u1, r0, r1);
+      img_off[b - b0] = off - r0 * a.w;  // LDS index of (row, col) = img_off + row*w + col
+      img_row0[b - b0] = r0;
+      off += (r1 - r0) * a.w;
     }
-  };
-  // A: G^T rows o, 8 consecutive pixels of chunk it
-  auto load_a = [&](Frag<bf16_t>* af, int it) {
-    const int b = b0 + it / nchunk, pa = (it % nchunk) * PXC + 8 * g;
+  }
+  __syncthreads();
+  for (int b = b0; b <= b1 && u1 > u0; ++b) {
+    int r0, r1;
+    wg_rows(a, b, u0, u1, r0, r1);
+    const uint8_t* src = a.code + ((long long)b * a.h + r0) * a.w;
+    uint8_t* dst = scode + img_off[b - b0] + r0 * a.w;
+    const int n = (r1 - r0) * a.w;
+    for (int i0 = 0; i0 < n; i0 += 256 * 16) {  // 16 independent loads per thread, then the stores
+      uint8_t v[16];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int o = o0 + 16 * mi + r;
-      const bf16_t* src = gout + ((long long)b * Cout + (o < Cout ? o : 0)) * hwo + pa;
-      if (o < Cout && pa + 8 <= hwo && (hwo & 3) == 0) {
-        // 8-byte aligned (hwo % 4 == 0, pa % 8 == 0): two 8-byte loads
-        const uint2 lo = *reinterpret_cast<const uint2*>(src);
-        const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
-        af[mi].v = make_uint4(lo.x, lo.y, hi.x, hi.y);
-      } else {
-        af[mi].zero();
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + q * 256 + tid;
+        v[q] = i < n ? src[i] : 0;
+      }
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (o < Cout && pa + j < hwo) af[mi].set_raw(j, src[j]);
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + q * 256 + tid;
+        if (i < n) dst[i] = v[q];
       }
     }
+  }
+  // ---- prologue 2: ordered list of the units meeting code k
+  int count = 0;
+  for (int ub = u0; ub < u1; ub += 256) {
+    const int u = ub + tid;
+    const bool live = u < u1 && ((a.pres[u] >> kcode) & 1u);
+    const unsigned long long bal = __ballot(live);
+    __syncthreads();
+    if (lane == 0) wave_cnt[wave] = __popcll(bal);
+    __syncthreads();
+    int before = count;
+    for (int w2 = 0; w2 < wave; ++w2) before += wave_cnt[w2];
+    if (live) slist[before + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(u - u0);
+    count += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+  }
+  __syncthreads();
+  // ---- per-lane copy roles: pixel row pr of every block, 16-byte chunk q
+  const int pr = 16 * wave + (lane >> 2);
+  const int qch = 8 * ((lane & 3) ^ wg_swz(pr));
+  int xky[4], xkx[4], xc[4];
+  bool xok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kk = kk0 + 32 * j;
+    xok[j] = kk < KK;
+    const int tap = xok[j] ? kk / a.Cin : 0;
+    xky[j] = tap / 3;
+    xkx[j] = tap % 3;
+    xc[j] = xok[j] ? kk % a.Cin : 0;
+  }
+  auto issue = [&](int slot, int it) {
+    const int u = u0 + (int)slist[it];
+    const int b = u / a.nunit;
+    const int p = (u - b * a.nunit) * WPX + pr;
+    const bool pv = p < hwo;
+    const int pc = pv ? p : hwo - 1;
+    const int oy = (int)(((float)pc + 0.5f) * a.inv_wo), ox = pc - oy * a.wo;
+    const uint32_t sb = lds0 + slot * Cfg::STAGE + wave * 1024;
+    const bf16_t* gsrc = a.gout + ((long long)b * hwo + pc) * a.Cout + qch;
+#pragma unroll
+    for (int ob = 0; ob < FM; ++ob) dma_lds16(gsrc + min(o0 + 32 * ob, a.Cout - 32), sb + ob * 4096);
+    const int ib = b - b0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int iy = 2 * oy - 1 + xky[j], ix = 2 * ox - 1 + xkx[j];
+      const bool inb = iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+      const int iyc = min(max(iy, 0), a.h - 1), ixc = min(max(ix, 0), a.w - 1);
+      const bool ok = pv && xok[j] && inb && scode[img_off[ib] + iyc * a.w + ixc] == kcode;
+      dma_lds16(a.x + (((long long)b * a.h + iyc) * a.w + ixc) * a.Cin + xc[j] + qch, sb + (FM + j) * 4096);
+      // 16-bit row mask of this wave's 16 rows (lanes 4i..4i+3 share row i)
+      unsigned long long m = __ballot(ok) & 0x1111111111111111ull;
+      m = (m | (m >> 3)) & 0x0303030303030303ull;
+      m = (m | (m >> 6)) & 0x000F000F000F000Full;
+      m = (m | (m >> 12)) & 0x000000FF000000FFull;
+      m = (m | (m >> 24)) & 0xFFFFull;
+      if (lane == 0) smask[(slot * 4 + j) * 4 + wave] = (uint16_t)m;
+    }
   };
-  f32x4 acc[4][2];
+  f32x4 acc[FM][4];
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < FM; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < 2; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Frag<bf16_t> af[4], afn[4];
-  int cur = next_live(0), buf = 0;
-  if (cur < total) {
-    stage(0, cur);
-    load_a(af, cur);
-  }
-  int live = __syncthreads_or(staged_any);
-  while (cur < total) {
-    const int nxt = next_live(cur + 1);
-    staged_any = 0;
-    if (nxt < total) {
-      stage(buf ^ 1, nxt);
-      load_a(afn, nxt);
-    }
-    if (live) {
-      // B: transposed LDS reads, columns (kk) wave*32 + 16*nj + i, rows (px) 8g .. 8g+7
-      const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+    for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // transposed fragment [k = 8g + j][col = c0 + r] of a [64 px][32 col] block (64-byte rows)
+  const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+  auto trfrag = [&](const char* blk, int kb, int c0) {
+    const int col = c0 + 4 * p4, ch = col >> 3, off = (col & 7) * 2;
+    const int row0 = 32 * kb + 8 * g + q4, row1 = row0 + 4;
+    v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)(blk + row0 * 64 + 16 * (ch ^ wg_swz(row0)) + off));
+    v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)(blk + row1 * 64 + 16 * (ch ^ wg_swz(row1)) + off));
+    Frag<bf16_t> f;
+    f.v = make_uint4((uint32_t)(uint16_t)t0.x | ((uint32_t)(uint16_t)t0.y << 16),
+                     (uint32_t)(uint16_t)t0.z | ((uint32_t)(uint16_t)t0.w << 16),
+                     (uint32_t)(uint16_t)t1.x | ((uint32_t)(uint16_t)t1.y << 16),
+                     (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
+    return f;
+  };
+  const int nst = count;
+  const int npro = nst < Cfg::S - 1 ? nst : Cfg::S - 1;
+  for (int i = 0; i < npro; ++i) issue(i, i);
+  if (npro >= 3) vm_wait_barrier<2 * Cfg::PER>();
+  else if (npro == 2) vm_wait_barrier<Cfg::PER>();
+  else vm_wait_barrier<0>();
+#pragma unroll 1
+  for (int s = 0; s < nst; ++s) {
+    if (s + Cfg::S - 1 < nst) issue((s + Cfg::S - 1) % Cfg::S, s + Cfg::S - 1);
+    const int slot = s % Cfg::S;
+    const char* st = smem + slot * Cfg::STAGE;
 #pragma unroll
-      for (int nj = 0; nj < 2; ++nj) {
-        const int col = wave * 32 + 16 * nj + 4 * p4;
-        v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + q4][col]));
-        v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s*)(&Xs[buf][8 * g + 4 + q4][col]));
-        Frag<bf16_t> bf;
-        bf.v = make_uint4((uint32_t)(uint16_t)t0.x | ((uint32_t)(uint16_t)t0.y << 16),
-                          (uint32_t)(uint16_t)t0.z | ((uint32_t)(uint16_t)t0.w << 16),
-                          (uint32_t)(uint16_t)t1.x | ((uint32_t)(uint16_t)t1.y << 16),
-                          (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
+    for (int kb = 0; kb < 2; ++kb) {
+      Frag<bf16_t> fa[FM], fb[4];
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], af[mi], bf);
+      for (int mi = 0; mi < FM; ++mi) {
+        const int ol = wm * 16 * FM + 16 * mi;
+        fa[mi] = trfrag(st + (ol >> 5) * 4096, kb, ol & 31);
       }
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) {
+        const int kl = wn * 64 + 16 * nj;
+        fb[nj] = trfrag(st + (FM + (kl >> 5)) * 4096, kb, kl & 31);
+        // rows 32kb + 8g .. +7 of block kl/32: keep only the rows whose mask bit is set
+        const uint32_t bits =
+            (uint32_t)(smask[(slot * 4 + (kl >> 5)) * 4 + 2 * kb + (g >> 1)] >> (8 * (g & 1))) & 0xFFu;
+        if (bits != 0xFFu) {
+          auto hm = [&](int e) { return ((bits >> e) & 1u) ? 0xFFFFu : 0u; };
+          fb[nj].v.x &= hm(0) | (hm(1) << 16);
+          fb[nj].v.y &= hm(2) | (hm(3) << 16);
+          fb[nj].v.z &= hm(4) | (hm(5) << 16);
+          fb[nj].v.w &= hm(6) | (hm(7) << 16);
+        }
+      }
+#pragma unroll
+      for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
     }
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) af[mi] = afn[mi];
-    live = __syncthreads_or(staged_any);
-    buf ^= 1;
-    cur = nxt;
+    const int ahead = (nst - 1 < s + Cfg::S - 1 ? nst - 1 : s + Cfg::S - 1) - (s + 1);
+    if (ahead >= 2) vm_wait_barrier<2 * Cfg::PER>();
+    else if (ahead == 1) vm_wait_barrier<Cfg::PER>();
+    else vm_wait_barrier<0>();
   }
-  float* dst = partial + ((long long)(split * 16 + kcode) * Cout) * KK;
+  float* dst = a.partial + ((long long)(split * 16 + kcode) * a.Cout) * KK;
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < FM; ++mi)
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
-      const int o = o0 + 16 * mi + 4 * g + reg;
+      const int o = o0 + wm * 16 * FM + 16 * mi + 4 * g + reg;
 #pragma unroll
-      for (int nj = 0; nj < 2; ++nj) {
-        const int c = kk0 + wave * 32 + 16 * nj + r;
-        if (o < Cout && c < KK) dst[(long long)o * KK + c] = acc[mi][nj][reg];
+      for (int nj = 0; nj < 4; ++nj) {
+        const int c = kk0 + wn * 64 + 16 * nj + r;
+        if (o < a.Cout && c < KK) dst[(long long)o * KK + c] = acc[mi][nj][reg];
       }
     }
 }
 
-// dW_k (present codes, split partials) -> the reference filters, fixed summation order
-__global__ void k_dsam_wgrad_combine(const float* __restrict__ partial, int splits,
-                                     const uint32_t* __restrict__ gmask, int Cin, int Cout,
-                                     float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
-  const long long KK = 9ll * Cin;
-  const long long total = (long long)Cout * KK;
+// dW_k (present codes, split partials) -> the reference filters, fixed summation order.  One
+// block per output channel o: the five sums of the row are formed in (tap, c) order (coalesced
+// partial reads), parked in LDS, then written in the OIHW (c, tap) order (coalesced writes).
+__global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restrict__ partial, int splits,
+                                                            const uint32_t* __restrict__ gmask, int Cin, int Cout,
+                                                            float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
+  extern __shared__ float srow[];  // [5][9*Cin]
+  const int KK = 9 * Cin, o = blockIdx.x;
   const uint32_t m = *gmask;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
+  for (int kk = threadIdx.x; kk < KK; kk += 256) {
     float seg[4] = {0.f, 0.f, 0.f, 0.f}, pr = 0.f;
     for (int k = 0; k < 16; ++k) {
       if (!((m >> k) & 1u)) continue;
       float v = 0.f;
-      for (int sp = 0; sp < splits; ++sp) v += partial[(long long)(sp * 16 + k) * total + e];
+      for (int sp = 0; sp < splits; ++sp) v += partial[((long long)(sp * 16 + k) * Cout + o) * KK + kk];
       pr += v;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if ((k >> i) & 1) seg[i] += v;
     }
-    const int o = (int)(e / KK);
-    const int kk = (int)(e % KK);
-    const int tap = kk / Cin, c = kk % Cin;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dconv_w[(((long long)i * Cout + o) * Cin + c) * 9 + tap] = seg[i];
-    dproj_w[((long long)o * Cin + c) * 9 + tap] = pr;
+    for (int i = 0; i < 4; ++i) srow[i * KK + kk] = seg[i];
+    srow[4 * KK + kk] = pr;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < KK; e += 256) {  // e = c*9 + tap (OIHW order)
+    const int c = e / 9, tap = e % 9, kk = tap * Cin + c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dconv_w[((long long)i * Cout + o) * KK + e] = srow[i * KK + kk];
+    dproj_w[(long long)o * KK + e] = srow[4 * KK + kk];
   }
 }
 
@@ -589,423 +758,595 @@ __global__ void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_deco
 // ----------------------------------------------------------------------- bf16: code-merged
 // The masked sum  sum_i conv_i(x * m_i) + proj(x)  is regrouped by region CODE (the 4-bit
 // pooled mask pattern of a source pixel, bit i = m_i): a source pixel with code k meets the
-// merged filter  W_k = proj + sum_{i in k} conv_i  (packed per code by k_pack_dsam_codes), so
-// each im2col row is multiplied by ONE filter instead of popcount(k) + 1 of them.
-//
-// Workgroup tile 128 output pixels (flattened over batch x grid, or over one stride-2 parity
-// class for dX) x 128 output channels; 4 waves as 2x2, wave tile 64 px x 64 ch (4x4 MFMA).
-// The K loop runs over (tap, code present among the tile's rows at that tap, 32-ch chunk);
-// a row whose code differs from the step's contributes zero (register select).  A (im2col rows,
-// 16 B per lane straight from NHWC) and B (W_k rows) of step s+1 are loaded while step s runs;
-// B goes through a double-buffered LDS tile with 64-byte rows XOR-swizzled by row bit 2
-// (conflict-free ds_read_b128 / ds_write_b128).
-constexpr int V2M = 128, V2N = 128;
-__device__ __forceinline__ int cm_slot(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 1) & 2)); }
+// merged filter  W_k = proj + sum_{i in k} conv_i  (packed per code by k_pack_fwd_codes), so
+// each im2col row is multiplied by ONE filter instead of popcount(k) + 1 of them.  Rows are
+// output pixels flattened over batch x grid (forward) or over one stride-2 parity class of the
+// input grid (dX, where only the taps of that class are live).
 
-// Pre-pass of k_conv_codes: for each 128-row tile (and stride-2 parity class of dX), the set
-// of region codes its rows meet at each tap (one thread per row; computed once per conv instead
-// of once per (N tile, K split) workgroup).
-__global__ __launch_bounds__(128) void k_conv_tile_codes(ConvArgs a) {
-  __shared__ uint32_t sm[9];
-  const int nclass = a.transposed ? 4 : 1;
-  const int cls = blockIdx.z;
-  int py = 0, px = 0, Hc = a.Ho, Wc = a.Wo;
+// Code-merged masked conv, bf16 (fwd and dX).  Workgroup = 8 waves (2 along M x 4 along N),
+// tile 8 x 16 output pixels (128 rows) x 192 columns, wave tile 64 x 48 (4 x 3 MFMA 16x16x32).
+// Steps run over (tap, group of KC 32-channel chunks, region code present among the tile's
+// rows at that tap); each step's operands arrive by LDS-DMA in an S-stage ring, S-1 steps ahead:
+//   A  the 128 im2col rows x KC*64 B (a row whose tap falls outside the input re-reads an
+//      in-bounds pixel of its own row; rows whose code differs from the step's code, or whose
+//      tap is outside, are zeroed in registers after the fragment read);
+//   B  the KC contiguous 192-row x 64-B tiles of the packed W_code (k_pack_fwd_codes /
+//      k_pack_bwd_codes layout): linear copies.
+// Load balance: a tile's step count is 9 x (codes per tap) x chunk groups, 1x..5x a dense tile
+// on real scenes (region boundaries), so k_dsam_plan records each tile's per-tap code sets
+// and the tile's steps are cut into nc = ceil(steps / chunk_len) equal chunks, one workgroup
+// each; the last chunk of a multi-chunk tile to finish sums the f32 partials in chunk order.
+constexpr int LD_BM = 128, LD_BN = 192, LD_CH = 8;  // tile rows, tile columns, max chunks per tile
+constexpr int LD_A1 = LD_BM * 64;   // 8 KB per chunk
+constexpr int LD_B1 = LD_BN * 64;   // 12 KB per chunk
+template <int KC>
+struct LdCfg {
+  static constexpr int S = KC == 3 ? 2 : 3;
+  static constexpr int A = KC * LD_A1;
+  static constexpr int STAGE = KC * (LD_A1 + LD_B1);
+  static constexpr int ROWTAB = S * STAGE;                // [128] int4 row table
+  static constexpr int ROWOUT = ROWTAB + LD_BM * 16;      // [128] int4 NCHW base, NHWC pixel, n_masks
+  static constexpr int TMASK = ROWOUT + LD_BM * 16;       // [9] u32 code set per tap, [9][16] u8 code list
+  static constexpr int BSUM = TMASK + 64 + 160;           // [5][192] f32 bias prefix sums
+  static constexpr size_t SMEM = BSUM + 5 * LD_BN * 4;
+  static_assert(SMEM <= 163840, "LDS budget");
+};
+constexpr int LD_EPI_LD = LD_BM + 4;  // epilogue LDS tile [96 n][132] f32 (two halves)
+
+struct LdGeom {
+  int py, px, Hc, Wc, nyl, nxl, ntap, tiles_x, tiles_y, ntiles;
+};
+__device__ __forceinline__ LdGeom ld_geom(const ConvArgs& a, int cls) {
+  LdGeom G;
+  G.py = G.px = 0;
+  G.Hc = a.Ho;
+  G.Wc = a.Wo;
   if (a.transposed) {
-    py = cls >> 1;
-    px = cls & 1;
-    Hc = (a.Ho - py + 1) >> 1;
-    Wc = (a.Wo - px + 1) >> 1;
+    G.py = cls >> 1;
+    G.px = cls & 1;
+    G.Hc = (a.Ho - G.py + 1) >> 1;
+    G.Wc = (a.Wo - G.px + 1) >> 1;
   }
-  if (threadIdx.x < 9) sm[threadIdx.x] = 0u;
-  __syncthreads();
-  const long long HWc = (long long)Hc * Wc, Mtot = (long long)a.B * HWc;
-  const long long m = (long long)blockIdx.x * V2M + threadIdx.x;
-  if (m < Mtot) {
-    const int b = (int)(m / HWc), rem = (int)(m % HWc), i = rem / Wc, j = rem % Wc;
-    const int oy = a.transposed ? 2 * i + py : i, ox = a.transposed ? 2 * j + px : j;
-    const uint32_t rc = a.mask_mode == MASK_DST ? a.code[((long long)b * a.Ho + oy) * a.Wo + ox] : 0u;
-    int t = 0;
-    for (int ky = 0; ky < 3; ++ky)
-      for (int kx = 0; kx < 3; ++kx) {
-        if (a.transposed && (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1))) continue;
-        int iy, ix;
-        if (a.transposed) {
-          iy = (oy + 1 - ky) >> 1;
-          ix = (ox + 1 - kx) >> 1;
-        } else {
-          iy = oy * 2 - 1 + ky;
-          ix = ox * 2 - 1 + kx;
-        }
-        if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi) {
-          const uint32_t c = a.mask_mode == MASK_SRC ? a.code[((long long)b * a.Hi + iy) * a.Wi + ix] : rc;
-          atomicOr(&sm[t], 1u << c);
-        }
-        ++t;
-      }
+  G.nyl = a.transposed ? (G.py ? 2 : 1) : 3;
+  G.nxl = a.transposed ? (G.px ? 2 : 1) : 3;
+  G.ntap = G.nyl * G.nxl;
+  G.tiles_x = (G.Wc + 15) >> 4;
+  G.tiles_y = (G.Hc + 7) >> 3;
+  G.ntiles = a.B * G.tiles_x * G.tiles_y;
+  return G;
+}
+// live tap t of the class -> kernel tap (ky, kx) and source offset (dy, dx) from the row origin
+__device__ __forceinline__ void ld_tap(const ConvArgs& a, const LdGeom& G, int t, int& ky, int& kx, int& dy,
+                                       int& dx) {
+  const int iy = t / G.nxl, ix = t - iy * G.nxl;
+  if (a.transposed) {
+    ky = G.py ? 2 * iy : 1;
+    kx = G.px ? 2 * ix : 1;
+    dy = (G.py + 1 - ky) >> 1;
+    dx = (G.px + 1 - kx) >> 1;
+  } else {
+    ky = dy = iy;
+    kx = dx = ix;
   }
-  __syncthreads();
-  if (threadIdx.x < 9) a.tile_codes[((long long)cls * gridDim.x + blockIdx.x) * 9 + threadIdx.x] = (uint16_t)sm[threadIdx.x];
-  (void)nclass;
+}
+// Row ml of tile `tile`: pixel (ty*8 + ml/16, tx*16 + ml%16) of the class grid.  Returns whether
+// the row exists; org = origin pixel of its taps, rv = in-bounds taps, lo/hi = 4-bit code per tap.
+__device__ __forceinline__ bool ld_row(const ConvArgs& a, const LdGeom& G, int tile, int ml, int& b, int& i,
+                                       int& j, int& org, uint32_t& rv, uint32_t& lo, uint32_t& hi) {
+  b = tile / (G.tiles_x * G.tiles_y);
+  const int trem = tile - b * G.tiles_x * G.tiles_y;
+  const int iq = (trem / G.tiles_x) * 8 + (ml >> 4), jq = (trem % G.tiles_x) * 16 + (ml & 15);
+  const bool mv = b < a.B && iq < G.Hc && jq < G.Wc;
+  b = mv ? b : 0;
+  i = mv ? iq : 0;
+  j = mv ? jq : 0;
+  rv = lo = hi = 0u;
+  uint32_t cv[9];
+  if (a.transposed) {
+    const uint32_t rc = a.code[((long long)b * a.Ho + 2 * i + G.py) * a.Wo + 2 * j + G.px];
+    org = mv ? (b * a.Hi + i) * a.Wi + j : 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      int ky, kx, dy, dx;
+      ld_tap(a, G, t < G.ntap ? t : 0, ky, kx, dy, dx);
+      if (mv && t < G.ntap && i + dy < a.Hi && j + dx < a.Wi) rv |= 1u << t;
+      cv[t] = rc;
+    }
+  } else {
+    org = mv ? (b * a.Hi + 2 * i - 1) * a.Wi + 2 * j - 1 : 0;
+    int off[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = 2 * i - 1 + t / 3, ix = 2 * j - 1 + t % 3;
+      const bool inb = mv && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+      if (inb) rv |= 1u << t;
+      off[t] = inb ? org + (t / 3) * a.Wi + t % 3 : 0;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) cv[t] = a.code[off[t]];
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    if ((rv >> t) & 1u) {
+      const uint32_t c = cv[t] & 15u;
+      if (t < 8) lo |= c << (4 * t); else hi |= c;
+    }
+  return mv;
+}
+__device__ __forceinline__ int ld_steps(const uint16_t* tm, int ntap, int ncg) {
+  int s = 0;
+  for (int t = 0; t < ntap; ++t) s += __popc((uint32_t)tm[t]) * ncg;
+  return s;
+}
+__device__ __forceinline__ int ld_nchunks(int steps, int len) {
+  const int n = (steps + len - 1) / len;
+  return n < 1 ? 1 : (n > LD_CH ? LD_CH : n);
 }
 
-__global__ __launch_bounds__(256) void k_conv_codes(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t sB[2][V2N * 32];
-  __shared__ uint8_t tcl[9 * 16], tcnt[9], tfirst[9];
-  __shared__ int tbase[10], tdelta[9], ttap[9];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// Plan: per (class, tile) the set of region codes the tile's rows meet at each live tap,
+// tmasks[(cls * ntiles0 + tile) * 16 + t] (u16).  One 128-thread workgroup per tile.
+__global__ __launch_bounds__(128) void k_dsam_plan(ConvArgs a, int ntiles0, int ntn) {
+  __shared__ uint32_t tm_s[9];
+  const int cls = blockIdx.z, tile = blockIdx.x, tid = threadIdx.x;
+  const LdGeom G = ld_geom(a, cls);
+  if (tile >= G.ntiles) return;
+  if (tid < 9) tm_s[tid] = 0u;
+  __syncthreads();
+  int b, i, j, org;
+  uint32_t rv, lo, hi;
+  ld_row(a, G, tile, tid, b, i, j, org, rv, lo, hi);
+  uint32_t tm[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    if ((rv >> t) & 1u) {
+      const uint32_t c = (t < 8 ? lo >> (4 * t) : hi) & 15u;
+      tm[t >> 1] |= (1u << c) << (16 * (t & 1));
+    }
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) tm[q] |= (uint32_t)__shfl_xor((int)tm[q], o);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const uint32_t v = (tm[t >> 1] >> (16 * (t & 1))) & 0xffffu;
+      if (v) atomicOr(&tm_s[t], v);
+    }
+  __syncthreads();
+  if (tid < 16) a.tmasks[((long long)cls * ntiles0 + tile) * 16 + tid] = tid < 9 ? (uint16_t)tm_s[tid] : 0;
+  for (int q = tid; q < ntn; q += 128) a.tickets[((long long)cls * ntiles0 + tile) * ntn + q] = 0;
+}
+
+// Work list: per (class, tile) the chunk count, compacted into items (cls | chunk << 2 |
+// tile << 5) in (class, tile, chunk) order by one workgroup; a[*nitems] = count.
+__global__ __launch_bounds__(1024) void k_dsam_items(ConvArgs a, int ntiles0, int ncg) {
+  __shared__ int wsum[16];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nclass = a.transposed ? 4 : 1, total = nclass * ntiles0;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int e0 = 0; e0 < total; e0 += 1024) {
+    const int e = e0 + tid;
+    int nc = 0;
+    if (e < total) {
+      const int cls = e / ntiles0, tile = e - cls * ntiles0;
+      const LdGeom G = ld_geom(a, cls);
+      if (tile < G.ntiles) nc = ld_nchunks(ld_steps(a.tmasks + (long long)e * 16, G.ntap, ncg), a.chunk_len);
+    }
+    // block exclusive scan of nc
+    int x = nc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int before = base_s;
+    for (int q = 0; q < w; ++q) before += wsum[q];
+    const int off = before + x - nc;
+    if (e < total) {
+      const int cls = e / ntiles0, tile = e - cls * ntiles0;
+      for (int c = 0; c < nc; ++c) a.items[off + c] = cls | (c << 2) | (tile << 5);
+    }
+    __syncthreads();
+    if (tid == 1023) base_s = off + nc;
+    __syncthreads();
+  }
+  if (tid == 0) *a.nitems = base_s;
+}
+
+// One (tile, chunk) item of k_dsam_lds for N tile ntile (of ntn).
+template <int KC>
+__device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, int chunk, int ntile, int ntn) {
+  using Cfg = LdCfg<KC>;
+  constexpr int S = Cfg::S;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  int4* rowtab = (int4*)(smem + Cfg::ROWTAB);
+  int4* rowout = (int4*)(smem + Cfg::ROWOUT);
+  uint8_t* tcl = (uint8_t*)(smem + Cfg::TMASK + 64);  // [9][16]
+  float* bsum = (float*)(smem + Cfg::BSUM);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave & 1, wn = wave >> 1;
-  const int nclass = a.transposed ? 4 : 1;
-  const int cls = blockIdx.z % nclass, split = blockIdx.z / nclass;
-  int py = 0, px = 0, Hc = a.Ho, Wc = a.Wo;
-  if (a.transposed) {
-    py = cls >> 1;
-    px = cls & 1;
-    Hc = (a.Ho - py + 1) >> 1;
-    Wc = (a.Wo - px + 1) >> 1;
-  }
-  const int HWc = Hc * Wc;
-  const int Mtot = a.B * HWc;
-  const int mblk = blockIdx.x * V2M;
-  if (mblk >= Mtot) return;  // whole workgroup
-  const int n0 = blockIdx.y * V2N;
+  const LdGeom G = ld_geom(a, cls);
+  const int ncg = a.C / (32 * KC);  // chunk groups
+  const uint16_t* tmg = a.tmasks + ((long long)cls * a.ntiles0 + tile) * 16;
+  uint32_t tmask[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) tmask[t] = t < G.ntap ? (uint32_t)tmg[t] : 0u;
+  int tb[10];
+  tb[0] = 0;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) tb[t + 1] = tb[t] + __popc(tmask[t]) * ncg;
+  const int total = tb[9];
+  const int nc = ld_nchunks(total, a.chunk_len);
+  const int n0 = ntile * LD_BN;
   const bf16_t* xp = (const bf16_t*)a.x;
   const bf16_t* wp = (const bf16_t*)a.w;
-  const int krow = 9 * a.C;  // one code's packed row (elements)
-  // ---- tap table (uniform): origin-relative source offset of each tap, in pixels
-  if (tid == 0) {
-    int n = 0, base = 0, t = 0;
-    const int nchunk = a.C / 32;
-    for (int ky = 0; ky < 3; ++ky)
-      for (int kx = 0; kx < 3; ++kx) {
-        int dy = ky, dx = kx;  // forward: origin (2oy-1, 2ox-1)
-        if (a.transposed) {
-          if (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1)) continue;
-          dy = (py + 1 - ky) >> 1;  // dX: origin (i, j) of the parity-class grid
-          dx = (px + 1 - kx) >> 1;
-        }
-        uint32_t msk = a.tile_codes[((long long)cls * gridDim.x + blockIdx.x) * 9 + t];
-        ttap[t] = ky * 3 + kx;
-        tdelta[t] = dy * a.Wi + dx;
-        tfirst[t] = (uint8_t)n;
-        tbase[t] = base;
-        const int cnt = __popc(msk);
-        tcnt[t] = (uint8_t)cnt;
-        base += cnt * nchunk;
-        while (msk) {
-          const int k = __ffs(msk) - 1;
-          msk &= msk - 1u;
-          tcl[n++] = (uint8_t)k;
-        }
-        ++t;
-      }
-    for (int q = t; q < 9; ++q) tcnt[q] = 0;
-    tbase[t] = base;
-    for (int q = t + 1; q < 10; ++q) tbase[q] = base;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  // ---- prologue: row table (threads 0..127), code lists per tap, bias prefix sums of this N tile
+  for (int e = tid; e < 5 * LD_BN; e += 512) {
+    const int k = e / LD_BN, nl = e - k * LD_BN, n = n0 + nl;
+    float s = 0.f;
+    if (a.bias4 && n < a.N)
+      for (int sb = 0; sb < k; ++sb) s += a.bias4[sb * a.N + n];
+    bsum[e] = s;
   }
-  // ---- rows owned by this lane: m = mblk + wm*64 + 16*mi + r.  Per row: origin pixel index,
-  // 9-bit mask of in-bounds taps and the 4-bit code each tap meets (SRC: source pixel's code;
-  // DST: the row's own code).  Taps are indexed by position t in the tap table.
-  int rorg[4];
-  uint32_t rvalid[4], rc_lo[4], rc_hi[4];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int m = mblk + wm * 64 + 16 * mi + r;
-    rvalid[mi] = 0u;
-    rc_lo[mi] = rc_hi[mi] = 0u;
-    rorg[mi] = 0;
-    if (m < Mtot) {
-      const int b = m / HWc, rem = m % HWc, i = rem / Wc, j = rem % Wc;
-      int t = 0;
-      if (a.transposed) {
-        const int oy = 2 * i + py, ox = 2 * j + px;
-        const uint32_t rc = a.code[((long long)b * a.Ho + oy) * a.Wo + ox];
-        rorg[mi] = (b * a.Hi + i) * a.Wi + j;
-        for (int ky = 0; ky < 3; ++ky)
-          for (int kx = 0; kx < 3; ++kx) {
-            if (((py + 1 - ky) & 1) || ((px + 1 - kx) & 1)) continue;
-            const int iy = i + ((py + 1 - ky) >> 1), ix = j + ((px + 1 - kx) >> 1);
-            if (iy < a.Hi && ix < a.Wi) {
-              rvalid[mi] |= 1u << t;
-              if (t < 8) rc_lo[mi] |= rc << (4 * t); else rc_hi[mi] |= rc;
-            }
-            ++t;
-          }
-      } else {
-        const int oy = i, ox = j;
-        rorg[mi] = (b * a.Hi + 2 * oy - 1) * a.Wi + 2 * ox - 1;
-        const uint8_t* cb = a.code + (long long)b * a.Hi * a.Wi;
-        for (int ky = 0; ky < 3; ++ky)
-          for (int kx = 0; kx < 3; ++kx) {
-            const int iy = 2 * oy - 1 + ky, ix = 2 * ox - 1 + kx;
-            if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi) {
-              const uint32_t c = cb[iy * a.Wi + ix];
-              rvalid[mi] |= 1u << t;
-              if (t < 8) rc_lo[mi] |= c << (4 * t); else rc_hi[mi] |= c;
-            }
-            ++t;
-          }
-      }
+  if (tid < 9) {
+    uint32_t msk = tmask[tid];
+    int n = 0;
+    while (msk) {
+      tcl[tid * 16 + n++] = (uint8_t)(__ffs(msk) - 1);
+      msk &= msk - 1u;
     }
+  }
+  if (tid < LD_BM) {
+    int b, i, j, org;
+    uint32_t rv, lo, hi;
+    const bool mv = ld_row(a, G, tile, tid, b, i, j, org, rv, lo, hi);
+    rowtab[tid] = make_int4(org, (int)rv, (int)lo, (int)hi);
+    int obase = -1, opix = 0, nmk = 0;
+    if (mv) {
+      const int oy = a.transposed ? 2 * i + G.py : i, ox = a.transposed ? 2 * j + G.px : j;
+      opix = (b * a.Ho + oy) * a.Wo + ox;
+      obase = (b * a.N * a.Ho + oy) * a.Wo + ox;
+      nmk = a.info ? a.info[b].n_masks : 0;
+    }
+    rowout[tid] = make_int4(obase, opix, nmk, 0);
   }
   __syncthreads();
-  const int nchunk = a.C / 32;
-  const int T = tbase[9];
-  const int s0 = (int)((long long)split * T / a.ksplit), s1 = (int)((long long)(split + 1) * T / a.ksplit);
-  // B staging rows: thread -> pieces tid, tid + 256 (row id>>2, 16-byte chunk id&3)
-  int boff[2];
-  bool bok[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int id = tid + 256 * i, n = n0 + (id >> 2);
-    bok[i] = n < a.N;
-    boff[i] = (bok[i] ? n : 0) * krow + 8 * (id & 3);
+  // DMA role: A rows 16*wave + lane/4 of every chunk, slot lane%4
+  const int R = 16 * wave + (lane >> 2);
+  int aorg, afall, achk;
+  uint32_t aval;
+  {
+    const int4 e = rowtab[R];
+    aorg = e.x;
+    aval = (uint32_t)e.y;
+    afall = e.y == 0 ? 0 : (a.transposed ? e.x : e.x + a.Wi + 1);
+    achk = 8 * ((lane & 3) ^ ((R >> 2) & 3));
   }
-  uint4 rbv[2];
-  // step state (wave-uniform): tap position, chunk, code index within the tap
-  int st_t = 0, st_ch = 0, st_ci = 0;
-  auto seek = [&](int st) {
+  uint32_t cval[4], clo[4], chi[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int4 e = rowtab[wm * 64 + 16 * mi + r];
+    cval[mi] = (uint32_t)e.y;
+    clo[mi] = (uint32_t)e.z;
+    chi[mi] = (uint32_t)e.w;
+  }
+  const int s0 = (int)((long long)chunk * total / nc), s1 = (int)((long long)(chunk + 1) * total / nc);
+  const int nst = (a.dbg & 1) ? 0 : s1 - s0;
+  int st_t[S], st_code[S];
+  auto issue = [&](int slot, int s) {  // step s (absolute)
     int t = 0;
-    while (st >= tbase[t + 1]) ++t;
-    const int rel = st - tbase[t], cnt = tcnt[t];
-    st_t = t;
-    st_ch = rel / cnt;
-    st_ci = rel - st_ch * cnt;
-  };
-  auto advance = [&]() {
-    if (++st_ci == tcnt[st_t]) {
-      st_ci = 0;
-      if (++st_ch == nchunk) {
-        st_ch = 0;
-        do ++st_t; while (st_t < 9 && tcnt[st_t] == 0);
+#pragma unroll
+    for (int q = 1; q < 9; ++q) t += s >= tb[q] ? 1 : 0;
+    t = __builtin_amdgcn_readfirstlane(t);
+    const int cnt = __popc(tmask[t]);
+    const int rel = s - tb[t], cg = rel / cnt, ci = rel - cg * cnt;
+    const int code = __builtin_amdgcn_readfirstlane((int)tcl[t * 16 + ci]);
+    int ky, kx, dy, dx;
+    ld_tap(a, G, t, ky, kx, dy, dx);
+    const int delta = dy * a.Wi + dx, tap = ky * 3 + kx;
+    const uint32_t sb = lds0 + slot * Cfg::STAGE;
+    const int pix = ((aval >> t) & 1u) ? aorg + delta : afall;
+    const bf16_t* asrc = xp + (long long)pix * a.C + cg * 32 * KC + achk;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) dma_lds16(asrc + kc * 32, sb + kc * LD_A1 + wave * 1024);
+    const long long tstride = (long long)a.N * 32;  // one (code, tap, chunk) tile, elements
+    const bf16_t* bsrc = wp + ((long long)(code * 9 + tap) * (a.C / 32) + cg * KC) * tstride + (long long)n0 * 32 + lane * 8;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const bf16_t* tbk = bsrc + kc * tstride;
+      const uint32_t db = sb + Cfg::A + kc * LD_B1;
+      dma_lds16(tbk + wave * 512, db + wave * 1024);
+      if (wave < 4) dma_lds16(tbk + (wave + 8) * 512, db + (wave + 8) * 1024);
+    }
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+      if (q == slot) {
+        st_t[q] = t;
+        st_code[q] = code;
       }
-    }
   };
-  auto bload = [&](int t, int ch, int code) {
-    const int koff = __builtin_amdgcn_readfirstlane(code * a.N * krow + ttap[t] * a.C + ch * 32);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      rbv[i] = bok[i] ? *reinterpret_cast<const uint4*>(wp + koff + boff[i]) : make_uint4(0u, 0u, 0u, 0u);
-  };
-  auto bstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + 256 * i;
-      *reinterpret_cast<uint4*>(&sB[buf][cm_slot(id >> 2, id & 3)]) = rbv[i];
-    }
-  };
-  auto aload = [&](int t, int ch, Frag<bf16_t>* af, uint32_t& rq) {
-    const int d = __builtin_amdgcn_readfirstlane(tdelta[t]);
-    const int coff = ch * 32 + 8 * g;
-    rq = 0u;
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const bool v = (rvalid[mi] >> t) & 1u;
-      const int pix = v ? rorg[mi] + d : 0;
-      af[mi].load(xp + (long long)pix * a.C + coff);
-      const uint32_t c = v ? ((t < 8 ? rc_lo[mi] >> (4 * t) : rc_hi[mi]) & 15u) : 0xffu;
-      rq |= c << (8 * mi);
-    }
-  };
-  f32x4 acc[4][4];
+  const int cnt = KC * (wave < 4 ? 3 : 2);  // DMA instructions of this wave per step
+  f32x4 acc[4][3];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int ccode = 0;
-  Frag<bf16_t> Ac[4], An[4];
-  uint32_t rqc = 0u, rqn = 0u;  // byte mi: code met by row mi at the step's tap (0xff: none)
-  if (s0 < s1) {
-    seek(s0);
-    ccode = tcl[tfirst[st_t] + st_ci];
-    bload(st_t, st_ch, ccode);
-    aload(st_t, st_ch, Ac, rqc);
-    bstore(0);
-  }
-  lds_barrier();
-  for (int st = s0; st < s1; ++st) {
-    int ncode = 0;
-    bool fresh = false;
-    if (st + 1 < s1) {  // prefetch step st+1: B always, A rows when its (tap, chunk) is new
-      advance();
-      ncode = tcl[tfirst[st_t] + st_ci];
-      bload(st_t, st_ch, ncode);
-      fresh = st_ci == 0;
-      if (fresh) aload(st_t, st_ch, An, rqn);
-    }
-    Frag<bf16_t> As[4];
+    for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int npro = nst < S - 1 ? nst : S - 1;
+  for (int i = 0; i < npro; ++i) issue(i, s0 + i);
+  if (npro >= 2) vm_wait_barrier_dyn(cnt);
+  else vm_wait_barrier<0>();
+#pragma unroll 1
+  for (int s = 0; s < nst; ++s) {
+    if (s + S - 1 < nst) issue((s + S - 1) % S, s0 + s + S - 1);
+    const int slot = s % S;
+    int t = 0, code = 0;
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+      if (q == slot) {
+        t = st_t[q];
+        code = st_code[q];
+      }
+    uint32_t keep = 0u;  // bit mi: row mi's code at tap t is the step's code
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
-      As[mi] = Ac[mi];
-      As[mi].select(((rqc >> (8 * mi)) & 0xffu) == (uint32_t)ccode);
+      const uint32_t c = (t < 8 ? clo[mi] >> (4 * t) : chi[mi]) & 15u;
+      keep |= (((cval[mi] >> t) & 1u) && c == (uint32_t)code) ? 1u << mi : 0u;
     }
-    const int buf = (st - s0) & 1;
+    const char* sa = smem + slot * Cfg::STAGE;
 #pragma unroll
-    for (int nj = 0; nj < 4; ++nj) {
-      Frag<bf16_t> bf;
-      bf.v = *reinterpret_cast<const uint4*>(&sB[buf][cm_slot(wn * 64 + 16 * nj + r, g)]);
+    for (int kc = 0; kc < KC; ++kc) {
+      Frag<bf16_t> fa[4], fb[3];
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], As[mi], bf);
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = wm * 64 + 16 * mi + r;
+        fa[mi].v = *reinterpret_cast<const uint4*>(sa + kc * LD_A1 + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+        fa[mi].select((keep >> mi) & 1u);
+      }
+#pragma unroll
+      for (int nj = 0; nj < 3; ++nj) {
+        const int row = wn * 48 + 16 * nj + r;
+        fb[nj].v = *reinterpret_cast<const uint4*>(sa + Cfg::A + kc * LD_B1 + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 3; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
     }
-    if (st + 1 < s1) bstore(buf ^ 1);
-    if (fresh) {
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) Ac[mi] = An[mi];
-      rqc = rqn;
-    }
-    ccode = ncode;
-    lds_barrier();
+    // own DMA of step s+1 landed (only later steps' may stay in flight), LDS reads done, barrier
+    const int ahead = (nst - 1 < s + S - 1 ? nst - 1 : s + S - 1) - (s + 1);
+    if (ahead <= 0) vm_wait_barrier<0>();
+    else if (ahead == 1) vm_wait_barrier_dyn(cnt);
+    else vm_wait_barrier_dyn(2 * cnt);
   }
-  if (a.ksplit > 1) {  // split-K: f32 slab [split][class][m][N], reduced by k_splitk_finish
-    // slab rows: [split][class (in order)][m] = [split][B*Ho*Wo] in total
-    long long coff = 0;
-    for (int c = 0; c < cls; ++c)
-      coff += (long long)a.B * ((a.Ho - (c >> 1) + 1) >> 1) * ((a.Wo - (c & 1) + 1) >> 1);
-    float* slab = a.partial + ((long long)split * a.B * a.Ho * a.Wo + coff) * a.N;
+  if (nc > 1) {
+    // Multi-chunk tile: publish this chunk's fragment-native partial ([wave][mi][nj][lane][4] f32),
+    // take a ticket; the chunk that draws nc-1 sums all partials in chunk order (deterministic)
+    // and runs the epilogue.  Agent-scope release / acquire per cdna_hip_programming.md
+    // (in-launch split-K reduction, Guideline 16): correct for any placement of the chunks.
+    const long long tslab = (((long long)cls * a.ntiles0 + tile) * ntn + ntile) * LD_CH;
+    float* slab = a.partial + (tslab + chunk) * (LD_BN * LD_BM);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int m = mblk + wm * 64 + 16 * mi + 4 * g + reg;
-        if (m >= Mtot) continue;
+      for (int nj = 0; nj < 3; ++nj)
+        *reinterpret_cast<f32x4*>(slab + (((wave * 4 + mi) * 3 + nj) * 64 + lane) * 4) = acc[mi][nj];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last_s = (int*)(smem + Cfg::TMASK);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(a.tickets + tslab / LD_CH, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last_s = old == nc - 1;
+    }
+    __syncthreads();
+    if (!*last_s) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const float* base = a.partial + tslab * (LD_BN * LD_BM);
 #pragma unroll
-        for (int nj = 0; nj < 4; ++nj) {
-          const int n = n0 + wn * 64 + 16 * nj + r;
-          if (n < a.N) slab[(long long)m * a.N + n] = acc[mi][nj][reg];
-        }
-      }
-    return;
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nc; ++c)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 3; ++nj)
+          acc[mi][nj] += *reinterpret_cast<const f32x4*>(base + (long long)c * (LD_BN * LD_BM) +
+                                                         (((wave * 4 + mi) * 3 + nj) * 64 + lane) * 4);
   }
-  // ---- epilogue (same contract as k_conv_igemm)
+  // ---- epilogue (same contract as k_conv_igemm), staged through LDS in two 96-column halves:
+  // pass 1 runs along pixels (NCHW residual loads and stores), pass 2 along channels (NHWC);
+  // every thread's loads of a pass are independent and issued together.
+  float* et = (float*)smem;  // [96 n][LD_EPI_LD] f32
   const bf16_t* res = (const bf16_t*)a.residual;
   bf16_t* onchw = (bf16_t*)a.out_nchw;
   bf16_t* onhwc = (bf16_t*)a.out_nhwc;
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  constexpr int HN = LD_BN / 2;
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();  // ring reads / previous half done
+    if ((wn >> 1) == half)
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
+      for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const long long m = mblk + wm * 64 + 16 * mi + 4 * g + reg;
-      if (m >= Mtot) continue;
-      const int b = (int)(m / HWc);
-      const int rem = (int)(m % HWc);
-      const int i = rem / Wc, j = rem % Wc;
-      const int oy = a.transposed ? 2 * i + py : i;
-      const int ox = a.transposed ? 2 * j + px : j;
-      const int nmask = a.info ? a.info[b].n_masks : 0;
+        for (int nj = 0; nj < 3; ++nj)
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        const int n = n0 + wn * 64 + 16 * nj + r;
-        if (n >= a.N) continue;
-        float v = acc[mi][nj][reg];
-        if (a.bias4) {
-          float bs = 0.f;
-          for (int sb = 0; sb < nmask; ++sb) bs += a.bias4[sb * a.N + n];
-          v += bs;
+          for (int reg = 0; reg < 4; ++reg)
+            et[((wn & 1) * 48 + 16 * nj + r) * LD_EPI_LD + wm * 64 + 16 * mi + 4 * g + reg] = acc[mi][nj][reg];
+    __syncthreads();
+    const int nh = n0 + half * HN;
+    // pass 1: items (channel, 4 consecutive tile rows = 4 consecutive pixels of one tile row);
+    // forward rows are contiguous in NCHW (8-byte residual loads / stores), dX rows are not
+    constexpr int NQ = HN * LD_BM / 4 / 512;  // 6 items per thread
+    float4 rq[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {  // residual loads, all in flight
+      const int it = tid + 512 * q, nl = it / (LD_BM / 4), ml = (it % (LD_BM / 4)) * 4, n = nh + nl;
+      rq[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!res || n >= a.N) continue;
+      const int4 r0 = rowout[ml], r3 = rowout[ml + 3];
+      const long long o = r0.x + (long long)n * HoWo;
+      if (!a.transposed && r0.x >= 0 && r3.x == r0.x + 3) {
+        const uint2 u = *reinterpret_cast<const uint2*>(res + o);
+        rq[q] = make_float4(bf16_to_f32((bf16_t)u.x), bf16_to_f32((bf16_t)(u.x >> 16)), bf16_to_f32((bf16_t)u.y),
+                            bf16_to_f32((bf16_t)(u.y >> 16)));
+      } else {
+        float t4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int4 re = rowout[ml + e];
+          t4[e] = re.x >= 0 ? bf16_to_f32(res[re.x + (long long)n * HoWo]) : 0.f;
         }
-        const long long o_nchw = (((long long)b * a.N + n) * a.Ho + oy) * a.Wo + ox;
-        if (res) v = bf16_to_f32(res[o_nchw]) + v;
-        const bf16_t tv = f32_to_bf16(v);
-        if (onchw) onchw[o_nchw] = tv;
-        if (onhwc) onhwc[(((long long)b * a.Ho + oy) * a.Wo + ox) * a.N + n] = tv;
+        rq[q] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int it = tid + 512 * q, nl = it / (LD_BM / 4), ml = (it % (LD_BM / 4)) * 4, n = nh + nl;
+      if (n >= a.N) continue;
+      const float rr[4] = {rq[q].x, rq[q].y, rq[q].z, rq[q].w};
+      bf16_t tv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int4 re = rowout[ml + e];
+        float v = et[nl * LD_EPI_LD + ml + e] + bsum[re.z * LD_BN + half * HN + nl];
+        if (res) v = rr[e] + v;
+        tv[e] = f32_to_bf16(v);
+        et[nl * LD_EPI_LD + ml + e] = bf16_to_f32(tv[e]);
+      }
+      if (onchw) {
+        const int4 r0 = rowout[ml], r3 = rowout[ml + 3];
+        if (!a.transposed && r0.x >= 0 && r3.x == r0.x + 3) {
+          *reinterpret_cast<uint2*>(onchw + r0.x + (long long)n * HoWo) =
+              make_uint2((uint32_t)tv[0] | ((uint32_t)tv[1] << 16), (uint32_t)tv[2] | ((uint32_t)tv[3] << 16));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int4 re = rowout[ml + e];
+            if (re.x >= 0) onchw[re.x + (long long)n * HoWo] = tv[e];
+          }
+        }
+      }
+    }
+    if (onhwc) {  // pass 2: items (tile row, 8 consecutive channels) -> one 16-byte store
+      __syncthreads();
+      for (int it = tid; it < LD_BM * (HN / 8); it += 512) {
+        const int ml = it / (HN / 8), nl = (it % (HN / 8)) * 8, n = nh + nl;
+        const int4 ro = rowout[ml];
+        if (ro.x < 0 || n >= a.N) continue;
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          w4[e] = (uint32_t)f32_to_bf16(et[(nl + 2 * e) * LD_EPI_LD + ml]) |
+                  ((uint32_t)f32_to_bf16(et[(nl + 2 * e + 1) * LD_EPI_LD + ml]) << 16);
+        *reinterpret_cast<uint4*>(onhwc + (long long)ro.y * a.N + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
       }
     }
   }
 }
 
-// split-K finish: sum the slabs in fixed order, add biases / residual, write NCHW (+NHWC) bf16.
-// Slabs are [split][class][m][N] in k_conv_codes' row order (m over the batch x parity-class
-// grid).  One block per 32 pixels x 32 channels, transposed through LDS so both stores coalesce.
-__global__ __launch_bounds__(256) void k_splitk_finish(ConvArgs a) {
-  __shared__ float tile[32][33];
-  const long long P = (long long)a.B * a.Ho * a.Wo;
-  const long long p0 = (long long)blockIdx.x * 32;
-  const int n0 = blockIdx.y * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  const long long HW = (long long)a.Ho * a.Wo;
-  for (int k = ty; k < 32; k += 8) {  // k: pixel within tile, tx: channel
-    const long long p = p0 + k;
-    const int n = n0 + tx;
-    float v = 0.f;
-    if (p < P && n < a.N) {
-      const int b = (int)(p / HW), rem = (int)(p % HW), oy = rem / a.Wo, ox = rem % a.Wo;
-      int cls = 0, Hc = a.Ho, Wc = a.Wo, i = oy, j = ox;
-      if (a.transposed) {
-        cls = (oy & 1) * 2 + (ox & 1);
-        Hc = (a.Ho - (oy & 1) + 1) >> 1;
-        Wc = (a.Wo - (ox & 1) + 1) >> 1;
-        i = oy >> 1;
-        j = ox >> 1;
-      }
-      const long long m = ((long long)b * Hc + i) * Wc + j;
-      // class c's slab offset: sum of the row counts of classes < c
-      long long coff = 0;
-      for (int c = 0; c < cls; ++c) {
-        const int hc = (a.Ho - (c >> 1) + 1) >> 1, wc = (a.Wo - (c & 1) + 1) >> 1;
-        coff += (long long)a.B * hc * wc;
-      }
-      for (int sp = 0; sp < a.ksplit; ++sp) v += a.partial[((long long)sp * P + coff + m) * a.N + n];
-      if (a.bias4) {
-        const int nm = a.info[b].n_masks;
-        float bs = 0.f;
-        for (int q = 0; q < nm; ++q) bs += a.bias4[q * a.N + n];
-        v += bs;
-      }
-      if (a.residual) v += bf16_to_f32(((const bf16_t*)a.residual)[((long long)b * a.N + n) * HW + rem]);
-      if (a.out_nhwc) ((bf16_t*)a.out_nhwc)[p * a.N + n] = f32_to_bf16(v);
-    }
-    tile[k][tx] = v;
-  }
-  __syncthreads();
-  for (int k = ty; k < 32; k += 8) {  // k: channel within tile, tx: pixel
-    const long long p = p0 + tx;
-    const int n = n0 + k;
-    if (p < P && n < a.N && a.out_nchw) {
-      const int b = (int)(p / HW);
-      ((bf16_t*)a.out_nchw)[((long long)b * a.N + n) * HW + (p % HW)] = f32_to_bf16(tile[tx][k]);
-    }
+// Persistent: grid (workgroups, N tiles); each workgroup walks the item list.
+template <int KC>
+__global__ __launch_bounds__(512, 1) void k_dsam_lds(ConvArgs a) {
+  const int nitems = *a.nitems;
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int v = a.items[it];
+    ld_item<KC>(a, v & 3, v >> 5, (v >> 2) & 7, blockIdx.y, gridDim.y);
+    __syncthreads();  // LDS of this item no longer read
   }
 }
 
-// split-K factor of the bf16 v2 path: enough workgroups to cover the chip ~3x
-int v2_ksplit(long long Mmax, int N, int nclass, int C, int transposed) {
-  const long long wgs = (long long)ceil_div(Mmax, V2M) * ceil_div(N, V2N) * nclass;
-  const int tc_min = (transposed ? 1 : 9) * (C / 32);
-  return (int)std::max<long long>(1, std::min<long long>(std::min(tc_min, 8), ceil_div(768, wgs)));
-}
+
 long long conv_mmax(const ConvArgs& a) {
   return a.transposed ? (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2) : (long long)a.B * a.Ho * a.Wo;
 }
-size_t v2_partial_bytes(const ConvArgs& a) {
-  const int ks = v2_ksplit(conv_mmax(a), a.N, a.transposed ? 4 : 1, a.C, a.transposed);
-  return ks > 1 ? align256((size_t)ks * a.B * a.Ho * a.Wo * a.N * sizeof(float)) : 0;
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
 }
-size_t tile_codes_bytes(const ConvArgs& a) {
-  return align256((size_t)(a.transposed ? 4 : 1) * ceil_div(conv_mmax(a), V2M) * 9 * sizeof(uint16_t));
+int ld_kc(int C) {
+  static const int force = env_int("RGBD_DSAM_KC", 0);  // tuning override
+  if (force == 1 || (force == 2 && C % 64 == 0) || (force == 3 && C % 96 == 0)) return force;
+  return C % 96 == 0 ? 3 : (C % 64 == 0 ? 2 : 1);
+}
+// k_dsam_lds tiling of a conv: tiles of the largest parity class, N tiles
+struct LdPlan {
+  int ntiles0, ntn, kc, chunk_len;
+  size_t tmask_bytes, items_bytes, ticket_bytes, partial_bytes;
+};
+LdPlan ld_plan(const ConvArgs& a) {
+  LdPlan p;
+  const int Hc0 = a.transposed ? (a.Ho + 1) / 2 : a.Ho, Wc0 = a.transposed ? (a.Wo + 1) / 2 : a.Wo;
+  const int nclass = a.transposed ? 4 : 1;
+  p.ntiles0 = a.B * ((Hc0 + 7) / 8) * ((Wc0 + 15) / 16);
+  p.ntn = ceil_div(a.N, LD_BN);
+  p.kc = ld_kc(a.C);
+  // chunk length in steps: pct % of a dense tile (one code per tap); tuning override
+  static const int pct = env_int("RGBD_DSAM_CHUNK_PCT", 100);
+  const int ntap = a.transposed ? 4 : 9;  // class 3 of dX has 4 live taps
+  p.chunk_len = std::max(1, (ntap * (a.C / (32 * p.kc)) * pct + 99) / 100);
+  p.tmask_bytes = align256((size_t)nclass * p.ntiles0 * 16 * sizeof(uint16_t));
+  p.items_bytes = align256(((size_t)nclass * p.ntiles0 * LD_CH + 1) * sizeof(int));
+  p.ticket_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * sizeof(int));
+  p.partial_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * LD_CH * LD_BN * LD_BM * sizeof(float));
+  return p;
+}
+size_t v2_partial_bytes(const ConvArgs& a) {
+  const LdPlan p = ld_plan(a);
+  return p.tmask_bytes + p.items_bytes + p.ticket_bytes + p.partial_bytes;
+}
+
+template <int KC>
+hipError_t launch_ld(const ConvArgs& b, dim3 grid, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_dsam_lds<KC>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)LdCfg<KC>::SMEM);
+  if (attr != hipSuccess) return attr;
+  k_dsam_items<<<1, 1024, 0, s>>>(b, b.ntiles0, b.C / (32 * KC));
+  k_dsam_lds<KC><<<grid, 512, LdCfg<KC>::SMEM, s>>>(b);
+  return hipSuccess;
 }
 
 template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   TimerScope ts(a.transposed ? "dsam_dx" : "dsam_fwd", s);
   int nclass = a.transposed ? 4 : 1;
-  long long Mmax = (long long)a.B * a.Ho * a.Wo;
-  if (a.transposed) Mmax = (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2);
+  const long long Mmax = conv_mmax(a);
   if constexpr (sizeof(T) == 2) {
     RGBD_REQUIRE(a.C % 32 == 0 && a.N % 32 == 0, RGBD_E_SHAPE);  // code-merged bf16 path only
-    {
-      ConvArgs b = a;
-      b.ksplit = v2_ksplit(Mmax, a.N, nclass, a.C, a.transposed);
-      // workspace: [split-K slabs | tile code sets]
-      b.tile_codes = (uint16_t*)((char*)a.partial + v2_partial_bytes(a));
-      k_conv_tile_codes<<<dim3(ceil_div(Mmax, V2M), 1, nclass), V2M, 0, s>>>(b);
-      dim3 grid2(ceil_div(Mmax, V2M), ceil_div(a.N, V2N), nclass * b.ksplit);
-      k_conv_codes<<<grid2, 256, 0, s>>>(b);
-      if (b.ksplit > 1) {
-        dim3 g3(ceil_div((long long)a.B * a.Ho * a.Wo, 32), ceil_div(a.N, 32));
-        k_splitk_finish<<<g3, 256, 0, s>>>(b);
-      }
-      RGBD_CHECK_LAUNCH();
-      return RGBD_OK;
-    }
+    RGBD_REQUIRE((long long)a.B * a.Hi * a.Wi < (1ll << 31) && Mmax < (1ll << 31), RGBD_E_SHAPE);
+    ConvArgs b = a;
+    static const int dbg = env_int("RGBD_DSAM_DBG", 0);
+    b.dbg = dbg;
+    const LdPlan P = ld_plan(a);
+    // workspace: [per-tile code sets | partial tiles of multi-chunk tiles]
+    b.tmasks = (uint16_t*)a.partial;
+    b.items = (int*)((char*)a.partial + P.tmask_bytes);
+    b.nitems = b.items + (size_t)nclass * P.ntiles0 * LD_CH;
+    b.tickets = (int*)((char*)a.partial + P.tmask_bytes + P.items_bytes);
+    b.partial = (float*)((char*)a.partial + P.tmask_bytes + P.items_bytes + P.ticket_bytes);
+    b.ntiles0 = P.ntiles0;
+    b.chunk_len = P.chunk_len;
+    k_dsam_plan<<<dim3(P.ntiles0, 1, nclass), 128, 0, s>>>(b, P.ntiles0, P.ntn);
+    // persistent: about one workgroup per CU (LDS-bound) over all N tiles
+    static const int pers = env_int("RGBD_DSAM_PERSIST", 256);
+    dim3 grid2(std::max(1, pers / P.ntn), P.ntn, 1);
+    const hipError_t e = P.kc == 3 ? launch_ld<3>(b, grid2, s) : P.kc == 2 ? launch_ld<2>(b, grid2, s) : launch_ld<1>(b, grid2, s);
+    if (e != hipSuccess) return (int)e;
+    RGBD_CHECK_LAUNCH();
+    return RGBD_OK;
   }
   dim3 grid(ceil_div(Mmax, BM), ceil_div(a.N, BN), nclass);
   k_conv_igemm<T><<<grid, 256, 0, s>>>(a);
@@ -1013,13 +1354,58 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   return RGBD_OK;
 }
 
-int dsam_wgrad_splits_codes(int B, int Cin, int Cout) {
-  // ~4 codes present per batch is typical; aim at ~3 live workgroups per CU
-  const long long tiles = (long long)ceil_div(9ll * Cin, WG_KK) * ceil_div(Cout, WG_O) * 4;
-  return (int)std::max<long long>(1, std::min<long long>(B, ceil_div(768, tiles)));
+// ---- bf16 dW plan: o tile (FM), unit splits obeying the per-workgroup LDS limits
+struct WgPlan {
+  int fm, splits, nunit;
+};
+int wg_fm(int Cout) { return Cout % 192 == 0 ? 6 : (Cout % 128 == 0 ? 4 : 2); }
+// largest per-workgroup code-row bytes / image count / unit count over the splits
+static bool wg_fits(int B, int h, int w, int nunit, int splits) {
+  const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo;
+  const long long U = (long long)B * nunit;
+  for (int sp = 0; sp < splits; ++sp) {
+    const long long u0 = sp * U / splits, u1 = (sp + 1) * U / splits;
+    if (u1 - u0 > WLIST_MAX) return false;
+    if (u1 <= u0) continue;
+    const long long b0 = u0 / nunit, b1 = (u1 - 1) / nunit;
+    if (b1 - b0 + 1 > WIMG_MAX) return false;
+    long long bytes = 0;
+    for (long long b = b0; b <= b1; ++b) {
+      const long long uf = std::max(u0, b * nunit), ul = std::min(u1, (b + 1) * nunit) - 1;
+      const long long pf = (uf - b * nunit) * WPX, pl = std::min<long long>(hwo, (ul - b * nunit + 1) * WPX) - 1;
+      const long long r0 = std::max<long long>(0, 2 * (pf / wo) - 1), r1 = std::min<long long>(h, 2 * (pl / wo) + 2);
+      bytes += (r1 - r0) * w;
+    }
+    if (bytes > WCODE_BYTES) return false;
+  }
+  return true;
 }
+static WgPlan wg_plan(int B, int Cin, int h, int w, int Cout) {
+  WgPlan p;
+  p.fm = wg_fm(Cout);
+  const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
+  p.nunit = (hwo + WPX - 1) / WPX;
+  const long long U = (long long)B * p.nunit;
+  // ~5 codes present per batch is typical: one workgroup per CU (LDS-limited) ~ 1.5 rounds
+  const long long tiles = (long long)ceil_div(9ll * Cin, 128) * ceil_div(Cout, 32 * p.fm) * 5;
+  int sp = (int)std::max<long long>(1, std::min<long long>(U, ceil_div(384, tiles)));
+  while (sp < U && !wg_fits(B, h, w, p.nunit, sp)) ++sp;
+  p.splits = sp;
+  return p;
+}
+
+template <int FM>
+hipError_t launch_wg(const WgArgs& a, dim3 grid, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_dsam_wgrad_mm<FM>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)WgCfg<FM>::SMEM);
+  if (attr != hipSuccess) return attr;
+  k_dsam_wgrad_mm<FM><<<grid, 256, WgCfg<FM>::SMEM, s>>>(a);
+  return hipSuccess;
+}
+
 int dsam_wgrad_splits(int B, int Cin, int Cout) {
-  const long long tiles = (long long)ceil_div(45ll * Cin, WG_KK) * ceil_div(Cout, WG_O);
+  const long long tiles = (long long)ceil_div(45ll * Cin, 64) * ceil_div(Cout, 64);
   int sp = (int)std::min<long long>(B, std::max<long long>(1, ceil_div(1024, tiles)));
   return sp < 1 ? 1 : sp;
 }
@@ -1047,21 +1433,55 @@ int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H
 long long rgbd_dsam_packed_elems(int dtype, int Cin, int Cout) {
   if (Cin <= 0 || Cout <= 0) return 0;
   if (dtype == RGBD_F32) return 45ll * Cin * Cout;
-  if (dtype == RGBD_BF16) return 144ll * Cin * Cout;
+  if (dtype == RGBD_BF16) return 144ll * Cin * Cout + 192 * 32;  // + one-tile tail pad
   return 0;
 }
 
+int rgbd_dsam_code_masks(int n, const uint8_t* const* codes_host, const long long* nbytes_host, uint32_t* masks,
+                         void* stream) {
+  RGBD_REQUIRE(n > 0 && n <= 8 && codes_host && nbytes_host && masks, RGBD_E_ARG);
+  CodeMaps cm = {};
+  long long most = 1;
+  for (int i = 0; i < n; ++i) {
+    RGBD_REQUIRE(codes_host[i] && nbytes_host[i] > 0, RGBD_E_ARG);
+    cm.p[i] = codes_host[i];
+    cm.n[i] = nbytes_host[i];
+    most = std::max(most, nbytes_host[i]);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const hipError_t me = hipMemsetAsync(masks, 0, sizeof(uint32_t) * n, s);
+  if (me != hipSuccess) return (int)me;
+  k_code_masks<<<dim3((unsigned)std::min<long long>(ceil_div(most, 256 * 8), 256), n), 256, 0, s>>>(cm, masks);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
 int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, int Cin, int Cout,
-                           void* wfwd, void* wbwd, void* stream) {
+                           const uint32_t* code_mask, void* wfwd, void* wbwd, void* stream) {
   RGBD_REQUIRE(conv_w && proj_w && (wfwd || wbwd) && Cin > 0 && Cout > 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32) {
     const int nb = (int)std::min<long long>(ceil_div(45ll * Cin * Cout, 256), 4096);
     k_pack_dsam<float><<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (float*)wfwd, (float*)wbwd);
   } else if (dtype == RGBD_BF16) {
+    RGBD_REQUIRE(wfwd, RGBD_E_ARG);  // wbwd is the transpose of wfwd
     RGBD_REQUIRE(Cin % 32 == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
-    const int nb = (int)std::min<long long>(ceil_div(9ll * Cin * Cout, 256), 4096);
-    k_pack_dsam_codes<<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (bf16_t*)wfwd, (bf16_t*)wbwd);
+    const int smem = 5 * 9 * Cin * (int)sizeof(float);
+    RGBD_REQUIRE(smem <= 163840, RGBD_E_SHAPE);
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_pack_fwd_codes,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    if (attr != hipSuccess) return (int)attr;
+    k_pack_fwd_codes<<<Cout, 256, smem, s>>>(conv_w, proj_w, Cin, Cout, code_mask, (bf16_t*)wfwd);
+    if (wbwd)
+      k_pack_bwd_codes<<<dim3(Cin / 32, Cout / 32, 144), 256, 0, s>>>((const bf16_t*)wfwd, Cin, Cout, code_mask,
+                                                                      (bf16_t*)wbwd);
+    // tail pads (read only by an over-reaching last N tile, whose outputs are dropped)
+    const hipError_t z1 = hipMemsetAsync((bf16_t*)wfwd + 144ll * Cin * Cout, 0, 192 * 32 * sizeof(bf16_t), s);
+    if (z1 != hipSuccess) return (int)z1;
+    if (wbwd) {
+      const hipError_t z2 = hipMemsetAsync((bf16_t*)wbwd + 144ll * Cin * Cout, 0, 192 * 32 * sizeof(bf16_t), s);
+      if (z2 != hipSuccess) return (int)z2;
+    }
   } else {
     return RGBD_E_DTYPE;
   }
@@ -1089,8 +1509,7 @@ static ConvArgs dx_args(int B, int Cin, int h, int w, int Cout) {
 size_t rgbd_dsam_conv_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout) {
   if (dtype != RGBD_BF16 || B <= 0 || h <= 0 || w <= 0) return 256;
   const ConvArgs f = fwd_args(B, Cin, h, w, Cout), d = dx_args(B, Cin, h, w, Cout);
-  return std::max<size_t>(256, std::max(v2_partial_bytes(f) + tile_codes_bytes(f),
-                                        v2_partial_bytes(d) + tile_codes_bytes(d)));
+  return std::max<size_t>(256, std::max(v2_partial_bytes(f), v2_partial_bytes(d)));
 }
 
 int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
@@ -1135,15 +1554,20 @@ struct WgradWs {
 static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   WgradWs o;
   size_t off = 0;
-  const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
-  const size_t part = dtype == RGBD_BF16 ? (size_t)dsam_wgrad_splits_codes(B, Cin, Cout) * 16 * Cout * 9 * Cin
-                                         : (size_t)dsam_wgrad_splits(B, Cin, Cout) * Cout * 45 * Cin;
+  size_t part, npres = 1;
+  if (dtype == RGBD_BF16) {
+    const WgPlan p = wg_plan(B, Cin, h, w, Cout);
+    part = (size_t)p.splits * 16 * Cout * 9 * Cin;
+    npres = (size_t)B * p.nunit;
+  } else {
+    part = (size_t)dsam_wgrad_splits(B, Cin, Cout) * Cout * 45 * Cin;
+  }
   o.partial = off;
   off += align256(sizeof(float) * part);
   o.csum = off;
   off += align256(sizeof(float) * (size_t)B * Cout);
   o.pres = off;
-  off += align256(sizeof(uint16_t) * (size_t)B * ((hwo + PXC - 1) / PXC));
+  off += align256(sizeof(uint16_t) * npres);
   o.gmask = off;
   off += 256;
   o.total = off;
@@ -1155,9 +1579,9 @@ size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int
   return wgrad_ws(dtype, B, Cin, h, w, Cout).total;
 }
 
-int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, const uint8_t* code,
-                         const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
-                         float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream) {
+int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
+                         const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h, int w,
+                         int Cout, float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream) {
   RGBD_REQUIRE(gout_nchw && x_nhwc && code && info && dconv_w && dproj_w && dbias && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
   RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
@@ -1166,7 +1590,7 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, c
   float* partial = (float*)((char*)ws + L.partial);
   float* csum = (float*)((char*)ws + L.csum);
   TimerScope ts("dsam_wgrad", s);
-  const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
+  const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo;
   if (dtype == RGBD_F32) {
     const int sp = dsam_wgrad_splits(B, Cin, Cout);
     dim3 grid(ceil_div(45ll * Cin, 64), ceil_div(Cout, 64), sp);
@@ -1177,21 +1601,38 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* x_nhwc, c
     k_dsam_wgrad_final<<<(int)std::min<long long>(ceil_div(total, 256), 4096), 256, 0, s>>>(
         partial, sp, Cin, Cout, dconv_w, dproj_w);
   } else if (dtype == RGBD_BF16) {
+    RGBD_REQUIRE(gout_nhwc, RGBD_E_ARG);
     RGBD_REQUIRE(Cin % 32 == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
-    const int spc = dsam_wgrad_splits_codes(B, Cin, Cout);
+    RGBD_REQUIRE((long long)hwo < (1ll << 22) && (long long)B * h * w < (1ll << 31), RGBD_E_SHAPE);
+    const WgPlan P = wg_plan(B, Cin, h, w, Cout);
+    RGBD_REQUIRE(wg_fits(B, h, w, P.nunit, P.splits), RGBD_E_SHAPE);
     uint16_t* pres = (uint16_t*)((char*)ws + L.pres);
     uint32_t* gmask = (uint32_t*)((char*)ws + L.gmask);
     const hipError_t me = hipMemsetAsync(gmask, 0, sizeof(uint32_t), s);
     if (me != hipSuccess) return (int)me;
-    const long long nthr = (long long)B * ((hwo + PXC - 1) / PXC) * 32;
+    const long long nthr = (long long)B * P.nunit * 64;
     k_code_presence<<<(int)ceil_div(nthr, 256), 256, 0, s>>>(code, B, h, w, pres, gmask);
-    dim3 g2(ceil_div(9ll * Cin, WG_KK), ceil_div(Cout, WG_O), spc * 16);
-    k_dsam_wgrad_bf16<<<g2, 256, 0, s>>>((const bf16_t*)gout_nchw, (const bf16_t*)x_nhwc, code, pres, gmask, B,
-                                         Cin, h, w, Cout, spc, partial);
+    WgArgs a;
+    a.gout = (const bf16_t*)gout_nhwc;
+    a.x = (const bf16_t*)x_nhwc;
+    a.code = code;
+    a.pres = pres;
+    a.gmask = gmask;
+    a.B = B; a.Cin = Cin; a.h = h; a.w = w; a.Cout = Cout; a.ho = ho; a.wo = wo;
+    a.nunit = P.nunit;
+    a.splits = P.splits;
+    a.inv_wo = 1.0f / (float)wo;
+    a.partial = partial;
+    dim3 g2(ceil_div(9ll * Cin, 128), ceil_div(Cout, 32 * P.fm), P.splits * 16);
+    const hipError_t e = P.fm == 6 ? launch_wg<6>(a, g2, s) : P.fm == 4 ? launch_wg<4>(a, g2, s) : launch_wg<2>(a, g2, s);
+    if (e != hipSuccess) return (int)e;
     k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
-    const long long total = 9ll * Cin * Cout;
-    k_dsam_wgrad_combine<<<(int)std::min<long long>(ceil_div(total, 256), 4096), 256, 0, s>>>(
-        partial, spc, gmask, Cin, Cout, dconv_w, dproj_w);
+    const int csmem = 5 * 9 * Cin * (int)sizeof(float);
+    static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    if (cattr != hipSuccess) return (int)cattr;
+    RGBD_REQUIRE(csmem <= 163840, RGBD_E_SHAPE);
+    k_dsam_wgrad_combine<<<Cout, 256, csmem, s>>>(partial, P.splits, gmask, Cin, Cout, dconv_w, dproj_w);
   } else {
     return RGBD_E_DTYPE;
   }

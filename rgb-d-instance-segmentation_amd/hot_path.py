@@ -23,13 +23,19 @@ DSAM_PARAMS_PER_MODULE = 9  # conv_layers.{0..3}.{weight,bias}, rgb_projection.w
 
 
 class _PackCache:
-    """Packed implicit-GEMM weights, re-packed only when a parameter changes."""
+    """Packed implicit-GEMM weights.  float32 (segment form, code independent): re-packed only
+    when a parameter changes.  bfloat16 (code-merged form): packed on every call for the region
+    codes present in this batch (``code_mask``), into fresh tensors so a pending backward keeps
+    the filters its forward used; ``want_bwd`` adds the dX operand."""
 
     def __init__(self):
         self.key = None
         self.val = None
 
-    def get(self, conv_ws, proj_w, dtype):
+    def get(self, conv_ws, proj_w, dtype, code_mask=None, want_bwd=True):
+        if dtype == torch.bfloat16:
+            return ops.dsam_pack(torch.stack([w.detach() for w in conv_ws]), proj_w.detach(), dtype,
+                                 code_mask=code_mask, want_bwd=want_bwd)
         key = (dtype, proj_w.data_ptr(), proj_w._version) + tuple((w.data_ptr(), w._version) for w in conv_ws)
         if key != self.key:
             self.val = ops.dsam_pack(torch.stack([w.detach() for w in conv_ws]), proj_w.detach(), dtype)
@@ -48,7 +54,11 @@ class HotPathFunction(torch.autograd.Function):
         codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
         if cfg.get("check_status"):
             ops.raise_on_status(info)
-        packs = [cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype) for k in range(3)]
+        training = any(ctx.needs_input_grad[7:])
+        masks = ops.dsam_code_masks(codes) if dtype == torch.bfloat16 else None
+        packs = [cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
+                                          code_mask=None if masks is None else masks[k:k + 1], want_bwd=training)
+                 for k in range(3)]
         x_nhwc = [ops.nchw_to_nhwc(colors[0])]
         cp1 = [colors[0]]
         for k in range(3):
@@ -90,7 +100,8 @@ class HotPathFunction(torch.autograd.Function):
         dcp_nhwc = ops.nchw_to_nhwc(dcp)
         grads_dsam = [None, None, None]
         for k in (2, 1, 0):
-            dconv, dproj, dbias = ops.dsam_bwd_weight(dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info)
+            dconv, dproj, dbias = ops.dsam_bwd_weight(dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
+                                                      gout_nhwc=dcp_nhwc)
             gk = []
             for i in range(4):
                 gk += [dconv[i], dbias[i]]
@@ -98,7 +109,7 @@ class HotPathFunction(torch.autograd.Function):
             grads_dsam[k] = gk
             if k > 0:
                 dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k],
-                                                  want_nhwc=(k > 1))
+                                                  want_nhwc=(k > 1 or dtype == torch.bfloat16))
         pgrads = grads_dsam[0] + grads_dsam[1] + grads_dsam[2] + grads_dggm
         return (None, None, None, None, None, None, None, *pgrads)
 

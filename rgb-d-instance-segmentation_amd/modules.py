@@ -23,9 +23,12 @@ class _DSAMFn(torch.autograd.Function):
         conv_ws, biases, proj_w = params[0:8:2], params[1:8:2], params[8]
         xc = x.detach().to(dtype)
         x_nhwc = ops.nchw_to_nhwc(xc.contiguous())
-        wfwd, wbwd = pack_cache.get(conv_ws, proj_w, dtype)
+        training = any(ctx.needs_input_grad[5:])
+        mask = ops.dsam_code_masks([code]) if dtype == torch.bfloat16 else None
+        wfwd, wbwd = pack_cache.get(conv_ws, proj_w, dtype, code_mask=mask, want_bwd=training)
         out, _ = ops.dsam_fwd(x_nhwc, code, info, wfwd, torch.stack([b.detach() for b in biases]))
         ctx.save_for_backward(x_nhwc, code, info, wbwd)
+        ctx.cin = x.shape[1]
         ctx.x_dtype = x.dtype
         return out.to(x.dtype)
 
@@ -33,10 +36,11 @@ class _DSAMFn(torch.autograd.Function):
     def backward(ctx, g):
         x_nhwc, code, info, wbwd = ctx.saved_tensors
         g = g.to(x_nhwc.dtype).contiguous()
-        dconv, dproj, dbias = ops.dsam_bwd_weight(g, x_nhwc, code, info)
+        g_nhwc = ops.nchw_to_nhwc(g)
+        dconv, dproj, dbias = ops.dsam_bwd_weight(g, x_nhwc, code, info, gout_nhwc=g_nhwc)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx, _ = ops.dsam_bwd_data(ops.nchw_to_nhwc(g), code, wbwd, None)
+            dx, _ = ops.dsam_bwd_data(g_nhwc, code, wbwd, None, cin=ctx.cin)
             dx = dx.to(ctx.x_dtype)
         grads = []
         for i in range(4):

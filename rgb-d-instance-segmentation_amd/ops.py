@@ -176,26 +176,43 @@ def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
-def dsam_pack(conv_w: torch.Tensor, proj_w: torch.Tensor, dtype: torch.dtype):
+def dsam_code_masks(codes):
+    """codes: list of uint8 region-code maps -> uint32 device tensor [len(codes)], bit k set when
+    code k occurs in map i (the codes the bf16 packed filters are needed for)."""
+    _need_cuda(*codes)
+    n = len(codes)
+    masks = torch.empty((n,), dtype=torch.int32, device=codes[0].device)
+    ptrs = (ctypes.c_void_p * n)(*[c.data_ptr() for c in codes])
+    sizes = (ctypes.c_longlong * n)(*[c.numel() for c in codes])
+    check(_lib.lib().rgbd_dsam_code_masks(n, ptrs, sizes, _p(masks), _stream(codes[0].device)),
+          "rgbd_dsam_code_masks")
+    return masks
+
+
+def dsam_pack(conv_w: torch.Tensor, proj_w: torch.Tensor, dtype: torch.dtype, code_mask: torch.Tensor = None,
+              want_bwd: bool = True):
     """conv_w float32 [4,Co,Ci,3,3], proj_w [Co,Ci,3,3] -> (wfwd, wbwd):
-    float32 segment form wfwd [Co,45*Ci], wbwd [Ci,45*Co]; bfloat16 code-merged form
-    wfwd [16,Co,9*Ci], wbwd [16,Ci,9*Co] (include/rgbd_hip.h)."""
+    float32 segment form wfwd [Co,45*Ci], wbwd [Ci,45*Co]; bfloat16 code-merged tiles, flat
+    (include/rgbd_hip.h: [16][9][Ci/32][Co][32] and [16][9][Co/32][Ci][32] + a tail pad), written
+    for the codes of ``code_mask`` (a one-element device tensor from dsam_code_masks; None = all
+    16).  ``want_bwd=False`` skips wbwd (None is returned for it)."""
     cw = conv_w.detach().float().contiguous()
     pw = proj_w.detach().float().contiguous()
-    _need_cuda(cw, pw)
+    _need_cuda(cw, pw, code_mask)
     Co, Ci = pw.shape[:2]
     if dtype == torch.bfloat16:
         if Ci % 32 or Co % 32:
             raise ValueError(f"bfloat16 DSAM needs channel counts that are multiples of 32, got {Ci}->{Co}")
-        fshape, bshape = (16, Co, 9 * Ci), (16, Ci, 9 * Co)
+        n = _lib.lib().rgbd_dsam_packed_elems(RGBD_BF16, Ci, Co)
+        fshape = bshape = (n,)
     else:
         fshape, bshape = (Co, 45 * Ci), (Ci, 45 * Co)
-    n = _lib.lib().rgbd_dsam_packed_elems(_dtype_code(torch.empty(0, dtype=dtype)), Ci, Co)
-    assert n == math.prod(fshape) == math.prod(bshape), (n, fshape, bshape)
+        n = _lib.lib().rgbd_dsam_packed_elems(RGBD_F32, Ci, Co)
+        assert n == math.prod(fshape) == math.prod(bshape), (n, fshape, bshape)
     wfwd = torch.empty(fshape, dtype=dtype, device=cw.device)
-    wbwd = torch.empty(bshape, dtype=dtype, device=cw.device)
-    check(_lib.lib().rgbd_dsam_pack_weights(_dtype_code(wfwd), _p(cw), _p(pw), Ci, Co, _p(wfwd), _p(wbwd),
-                                            _stream(cw.device)), "rgbd_dsam_pack_weights")
+    wbwd = torch.empty(bshape, dtype=dtype, device=cw.device) if want_bwd else None
+    check(_lib.lib().rgbd_dsam_pack_weights(_dtype_code(wfwd), _p(cw), _p(pw), Ci, Co, _p(code_mask), _p(wfwd),
+                                            _p(wbwd), _stream(cw.device)), "rgbd_dsam_pack_weights")
     return wfwd, wbwd
 
 
@@ -204,7 +221,7 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     """x_nhwc [B,h,w,Ci] -> (out_nchw [B,Co,ho,wo], out_nhwc or None)."""
     _need_cuda(x_nhwc, code, info, wfwd, bias4, residual)
     B, h, w, Ci = x_nhwc.shape
-    Co = wfwd.shape[-2]
+    Co = bias4.shape[-1]
     ho, wo = (h + 1) // 2, (w + 1) // 2
     if tuple(code.shape) != (B, h, w):
         raise ValueError(f"region code {tuple(code.shape)} does not match features {(B, h, w)}")
@@ -221,10 +238,19 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     return out, out_nhwc
 
 
-def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False):
+def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False, cin=None):
+    """dX of one DSAM (+ gin).  The input channel count comes from ``cin``, ``gin_nchw`` or the
+    2-D float32 wbwd (the flat bfloat16 tiles do not carry it)."""
     _need_cuda(gout_nhwc, code, wbwd, gin_nchw)
     B, ho, wo, Co = gout_nhwc.shape
-    Ci = wbwd.shape[-2]
+    if cin is not None:
+        Ci = int(cin)
+    elif gin_nchw is not None:
+        Ci = gin_nchw.shape[1]
+    elif wbwd.dim() == 2:
+        Ci = wbwd.shape[-2]
+    else:
+        raise ValueError("dsam_bwd_data needs cin (or gin_nchw) with the flat bfloat16 filter tiles")
     _, h, w = code.shape
     if gin_nchw is not None and tuple(gin_nchw.shape) != (B, Ci, h, w):
         raise ValueError("gin shape mismatch")
@@ -238,17 +264,23 @@ def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False):
     return dx, dx_nhwc
 
 
-def dsam_bwd_weight(gout_nchw, x_nhwc, code, info):
-    _need_cuda(gout_nchw, x_nhwc, code, info)
+def dsam_bwd_weight(gout_nchw, x_nhwc, code, info, gout_nhwc=None):
+    """dW/db of one DSAM.  The bfloat16 path contracts the NHWC copy of the upstream gradient
+    (``gout_nhwc``; made here when not given); bias gradients use the NCHW one."""
+    _need_cuda(gout_nchw, x_nhwc, code, info, gout_nhwc)
     B, Co, ho, wo = gout_nchw.shape
     _, h, w, Ci = x_nhwc.shape
     dev = gout_nchw.device
+    dt = _dtype_code(gout_nchw)
+    if dt == RGBD_BF16 and gout_nhwc is None:
+        gout_nhwc = nchw_to_nhwc(gout_nchw)
+    if gout_nhwc is not None and tuple(gout_nhwc.shape) != (B, ho, wo, Co):
+        raise ValueError(f"gout_nhwc {tuple(gout_nhwc.shape)} != {(B, ho, wo, Co)}")
     dconv = torch.empty((4, Co, Ci, 3, 3), dtype=torch.float32, device=dev)
     dproj = torch.empty((Co, Ci, 3, 3), dtype=torch.float32, device=dev)
     dbias = torch.empty((4, Co), dtype=torch.float32, device=dev)
-    dt = _dtype_code(gout_nchw)
     L = _lib.lib()
     ws = _workspace(dev, L.rgbd_dsam_bwd_weight_workspace_size(dt, B, Ci, h, w, Co), "dsam_wgrad")
-    check(L.rgbd_dsam_bwd_weight(dt, _p(gout_nchw), _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co,
-                                 _p(dconv), _p(dproj), _p(dbias), _p(ws), _stream(dev)), "rgbd_dsam_bwd_weight")
+    check(L.rgbd_dsam_bwd_weight(dt, _p(gout_nchw), _p(gout_nhwc), _p(x_nhwc), _p(code), _p(info), B, Ci, h, w,
+                                 Co, _p(dconv), _p(dproj), _p(dbias), _p(ws), _stream(dev)), "rgbd_dsam_bwd_weight")
     return dconv, dproj, dbias

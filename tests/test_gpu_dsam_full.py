@@ -1,0 +1,112 @@
+"""bf16 DSAM kernels (K5: code-merged forward, dX, dW) at the bench's full size, 640x480,
+B=8, against a float32 PyTorch-GPU restatement of DSAModule.forward
+(mask2former/utils/custom_model.py:682-699) on the same region codes:
+
+    y = sum_{i<4} Conv3x3s2_i(x * m_i) + sum_{i<n_masks} b_i + Proj3x3s2(x),  m_i = bit i of code
+
+The codes come from the HIP decomposition, which is pinned bit-exact elsewhere
+(test_gpu_parity.py); here they only define the masks.  Tolerance: bf16 operands with f32
+accumulation against f32 — max error <= 2e-2 of the reference's max magnitude, mean error
+<= 4e-3 of its mean magnitude (the second bound catches a dropped or doubled tile that the
+max-norm bound could hide)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import _rgbd_import  # noqa: F401
+from rgbd_amd import init as winit, ops, synthetic
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _ref_forward(x, code, n_masks, conv_w, conv_b, proj_w):
+    y = F.conv2d(x, proj_w, stride=2, padding=1)
+    for i in range(4):
+        m = ((code >> i) & 1).float()[:, None]
+        y = y + F.conv2d(x * m, conv_w[i], stride=2, padding=1)
+    bias = torch.stack([conv_b[:int(n)].sum(0) if n > 0 else torch.zeros_like(conv_b[0]) for n in n_masks])
+    return y + bias[:, :, None, None]
+
+
+def _err(a, e):
+    d = (a.float() - e).abs()
+    return float(d.max() / e.abs().max()), float(d.mean() / e.abs().mean())
+
+
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_dsam_bf16_full_size(k):
+    from rgbd_amd.modules import DSAModule
+    cin, cout = [(96, 192), (192, 384), (384, 768)][k]
+    B, H, W = 8, 480, 640
+    h, w = [(120, 160), (60, 80), (30, 40)][k]
+    m = DSAModule(cin, cout)
+    winit.init_deterministic(m, prefix=f"full.dsam{k}.")
+    m.compute_dtype = torch.bfloat16
+    m = m.to(DEV)
+    planes, _, _ = synthetic.make_batch(3, B, H, W)
+    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
+    ratio = torch.linspace(0.05, 0.45, B, device=DEV)
+    codes, info = ops.edsam_decompose(d3, ratio, [(h, w)])
+    n_masks = ops.decode_info(info)["n_masks"]
+    g = torch.Generator(device=DEV)
+    g.manual_seed(100 + k)
+    x = torch.randn((B, cin, h, w), generator=g, device=DEV).bfloat16()
+    gout = (torch.randn((B, cout, (h + 1) // 2, (w + 1) // 2), generator=g, device=DEV) * 0.1).bfloat16()
+    # HIP path, driven exactly as the fused hot path drives it
+    from rgbd_amd.modules import _DSAMFn
+    xg = x.clone().requires_grad_(True)
+    y = _DSAMFn.apply(xg, codes[0], info, torch.bfloat16, m._pack_cache, *m._params())
+    y.backward(gout)
+    # float32 reference on the same (bf16-valued) inputs
+    conv_w = torch.stack([m.conv_layers[i].weight.detach() for i in range(4)]).clone().requires_grad_(True)
+    conv_b = torch.stack([m.conv_layers[i].bias.detach() for i in range(4)]).clone().requires_grad_(True)
+    proj_w = m.rgb_projection.weight.detach().clone().requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    yr = _ref_forward(xr, codes[0].long(), n_masks, conv_w, conv_b, proj_w)
+    yr.backward(gout.float())
+    checks = {
+        "y": (y.detach(), yr.detach()),
+        "dx": (xg.grad, xr.grad),
+        "dconv_w": (torch.stack([m.conv_layers[i].weight.grad for i in range(4)]), conv_w.grad),
+        "dconv_b": (torch.stack([m.conv_layers[i].bias.grad for i in range(4)]), conv_b.grad),
+        "dproj_w": (m.rgb_projection.weight.grad, proj_w.grad),
+    }
+    for name, (a, e) in checks.items():
+        mx, mean = _err(a, e)
+        assert mx <= 2e-2 and mean <= 4e-3, f"dsam{k} {name}: max {mx:.3g} mean {mean:.3g}"
+
+
+def test_dsam_bf16_ragged_many_codes():
+    """Odd sizes (ragged tiles, 64-px units crossing rows, border taps) and a code map using
+    all 16 codes at random, B=3: the paths the full-size scenes rarely exercise."""
+    from rgbd_amd.modules import _DSAMFn, DSAModule
+    B, cin, cout, h, w = 3, 64, 96, 37, 53
+    m = DSAModule(cin, cout)
+    winit.init_deterministic(m, prefix="ragged.")
+    m.compute_dtype = torch.bfloat16
+    m = m.to(DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    code = torch.randint(0, 16, (B, h, w), generator=g, device=DEV).to(torch.uint8)
+    info = torch.zeros((B, 2116), dtype=torch.uint8, device=DEV)
+    rec = np.zeros(B, dtype=ops.DECOMP_INFO_DTYPE)
+    rec["n_masks"] = [4, 2, 0]
+    info.copy_(torch.from_numpy(rec.view(np.uint8).reshape(B, -1)))
+    x = torch.randn((B, cin, h, w), generator=g, device=DEV).bfloat16()
+    gout = torch.randn((B, cout, (h + 1) // 2, (w + 1) // 2), generator=g, device=DEV).bfloat16()
+    xg = x.clone().requires_grad_(True)
+    y = _DSAMFn.apply(xg, code, info, torch.bfloat16, m._pack_cache, *m._params())
+    y.backward(gout)
+    conv_w = torch.stack([m.conv_layers[i].weight.detach() for i in range(4)]).clone().requires_grad_(True)
+    conv_b = torch.stack([m.conv_layers[i].bias.detach() for i in range(4)]).clone().requires_grad_(True)
+    proj_w = m.rgb_projection.weight.detach().clone().requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    yr = _ref_forward(xr, code.long(), rec["n_masks"], conv_w, conv_b, proj_w)
+    yr.backward(gout.float())
+    for name, a, e in [("y", y.detach(), yr.detach()), ("dx", xg.grad, xr.grad),
+                       ("dconv_w", torch.stack([m.conv_layers[i].weight.grad for i in range(4)]), conv_w.grad),
+                       ("dproj_w", m.rgb_projection.weight.grad, proj_w.grad)]:
+        mx, mean = _err(a, e)
+        assert mx <= 2e-2 and mean <= 4e-3, f"{name}: max {mx:.3g} mean {mean:.3g}"
