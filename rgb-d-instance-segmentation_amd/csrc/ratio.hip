@@ -28,12 +28,15 @@ using namespace rgbd;
 namespace {
 
 constexpr int STEM_K = 160, STEM_C = 192, FUS_C = 128, ATT_C = 64, C5 = 256, C6 = 512;
+// bf16 chain v2 stem: k = (c*7 + dy)*8 + dx over the 7x7 window, dx = 7 a zero pad (21 groups of 8)
+constexpr int STEM_K2 = 168;
 constexpr int NBN = 6;  // BN layers: scale1, scale2, scale3, fusion, fe.1, fe.5
 constexpr float BN_EPS = 1e-5f;
 
 struct Layout {  // byte offsets into the packed blob
   size_t w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, w7, b7, w8, b8, w9, b9, w10, b10;
   size_t w5s, zero;  // bf16: conv5 weights in LDS-DMA step order; 256 zero bytes (padding source)
+  size_t w1s;        // bf16: stem weights in the chain v2 K order
   size_t total;
 };
 
@@ -67,6 +70,7 @@ inline Layout make_layout(int es) {
   L.b10 = seg(4);
   L.w5s = seg(es == 2 ? (size_t)C5 * 9 * FUS_C * 2 : 0);
   L.zero = seg(256);
+  L.w1s = seg(es == 2 ? (size_t)STEM_C * STEM_K2 * 2 : 0);
   L.total = o;
   return L;
 }
@@ -120,6 +124,17 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
   }
   for (int e = tid; e < C5; e += nth) ((float*)(blob + L.b5))[e] = w.p[13][e];
   if constexpr (sizeof(T) == 2) {
+    bf16_t* w1s = (bf16_t*)(blob + L.w1s);
+    for (int e = tid; e < STEM_C * STEM_K2; e += nth) {  // stem for chain v2: k = (c*7 + ky)*8 + kx
+      const int o = e / STEM_K2, k = e % STEM_K2, grp = k / 8, kx = k % 8, c = grp / 7, ky = grp % 7;
+      float v = 0.f;
+      if (kx < 7) {
+        const int br = o / 64, oo = o % 64, ks = 3 + 2 * br, off = 3 - ks / 2;  // 3x3 / 5x5 / 7x7
+        const int y = ky - off, x = kx - off;
+        if (y >= 0 && y < ks && x >= 0 && x < ks) v = w.p[2 * br][((oo * 3 + c) * ks + y) * ks + x];
+      }
+      w1s[e] = f32_to_bf16(v);
+    }
     // K-step order for k_rp_conv3x3_v3: [step = half*9 + tap][n][64 ch], each 128-byte row
     // holding its 16-byte chunks in the LDS swizzle order (slot q <- chunk q ^ (n & 6)), so one
     // LDS-DMA copy of a step is linear.
@@ -432,16 +447,16 @@ __device__ __forceinline__ void reduce_scatter16(float (&v)[N], int r) {
 constexpr int C2W_TH = 8, C2W_TW = 32, C2W_PH = C2W_TH + 6, C2W_PW = C2W_TW + 6;
 // LDS weight rows padded by 16 bytes: row strides of 336/400/272/144 B put the 16 rows a
 // ds_read_b128 lane group touches on distinct banks (unpadded 256-B rows are 16-way).
-constexpr int C2W_S1 = STEM_K + 8, C2W_S2 = STEM_C + 8, C2W_S3 = FUS_C + 8, C2W_S4 = ATT_C + 8;
+constexpr int C2W_S1 = STEM_K2 + 8, C2W_S2 = STEM_C + 8, C2W_S3 = FUS_C + 8, C2W_S4 = ATT_C + 8;
+constexpr int C2W_PWP = 40;  // bf16 patch row: 38 pixels + 2 zero pad (a lane reads 5 words from col & ~1)
 constexpr size_t C2W_OFF_W1 = 0;
 constexpr size_t C2W_OFF_W2 = C2W_OFF_W1 + (size_t)STEM_C * C2W_S1 * 2;
 constexpr size_t C2W_OFF_W3 = C2W_OFF_W2 + (size_t)FUS_C * C2W_S2 * 2;
 constexpr size_t C2W_OFF_W4 = C2W_OFF_W3 + (size_t)ATT_C * C2W_S3 * 2;
 constexpr size_t C2W_OFF_B = C2W_OFF_W4 + (size_t)FUS_C * C2W_S4 * 2;             // b1 b2 b3 b4 (f32)
 constexpr size_t C2W_OFF_AFF = C2W_OFF_B + (size_t)(STEM_C + FUS_C + ATT_C + FUS_C) * 4;  // aff1, aff2
-constexpr size_t C2W_OFF_PATCH = C2W_OFF_AFF + (size_t)(STEM_C + FUS_C) * 8;
-constexpr size_t C2W_OFF_KTAB = C2W_OFF_PATCH + (size_t)3 * C2W_PH * C2W_PW * 4;
-constexpr size_t C2W_SMEM = C2W_OFF_KTAB + STEM_K * 2;
+constexpr size_t C2W_OFF_PATCH = C2W_OFF_AFF + (size_t)(STEM_C + FUS_C) * 8;  // bf16 [3][14][40]
+constexpr size_t C2W_SMEM = C2W_OFF_PATCH + (size_t)3 * C2W_PH * C2W_PWP * 2 + 16;
 static_assert(C2W_SMEM <= 163840, "chain v2 LDS budget");
 
 template <int PHASE>
@@ -461,8 +476,7 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
   float* sb4 = sb3 + ATT_C;
   float2* saf1 = (float2*)(smem + C2W_OFF_AFF);
   float2* saf2 = saf1 + STEM_C;
-  float* patch = (float*)(smem + C2W_OFF_PATCH);
-  short* ktab = (short*)(smem + C2W_OFF_KTAB);
+  bf16_t* patch = (bf16_t*)(smem + C2W_OFF_PATCH);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   // ---- one-time LDS fill: weights, biases, BN affines, im2col table
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
             *reinterpret_cast<const uint4*>(blob + src + ((size_t)rr * k + 8 * q) * 2);
       }
     };
-    copy_rows(C2W_OFF_W1, L.w1, STEM_C, STEM_K, C2W_S1);
+    copy_rows(C2W_OFF_W1, L.w1s, STEM_C, STEM_K2, C2W_S1);
     copy_rows(C2W_OFF_W2, L.w2, FUS_C, STEM_C, C2W_S2);
     copy_rows(C2W_OFF_W3, L.w3, ATT_C, FUS_C, C2W_S3);
     copy_rows(C2W_OFF_W4, L.w4, FUS_C, ATT_C, C2W_S4);
@@ -489,14 +503,9 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
       for (int i = tid; i < STEM_C; i += 512) saf1[i] = aff1[i];
     if (PHASE >= 2)
       for (int i = tid; i < FUS_C; i += 512) saf2[i] = aff2[i];
-    for (int k = tid; k < STEM_K; k += 512) {
-      short v = -1;
-      if (k < 147) {
-        const int tap = k / 3, c = k % 3;
-        v = (short)((c * C2W_PH + tap / 7) * C2W_PW + tap % 7);
-      }
-      ktab[k] = v;
-    }
+    for (int i = tid; i < 3 * C2W_PH * C2W_PWP; i += 512) patch[i] = 0;  // pad columns stay zero
+    for (int i = tid; i < STEM_C * (C2W_S1 - STEM_K2); i += 512)  // W1 row pads: never garbage in an MFMA
+      ((bf16_t*)(smem + C2W_OFF_W1))[(i / (C2W_S1 - STEM_K2)) * C2W_S1 + STEM_K2 + i % (C2W_S1 - STEM_K2)] = 0;
   }
   // BN statistics (phases 0/1): per tile, each lane's (channel, {sum, sumsq}) values are
   // reduce-scattered over the 16 pixel lanes (4 butterfly rounds), so a lane keeps only
@@ -537,7 +546,7 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
 #pragma unroll
     for (int k = 0; k < PATCH_PER; ++k) {
       const int i = tid + 512 * k;
-      if (i < PATCH_N) patch[i] = pre[k];
+      if (i < PATCH_N) patch[(i / C2W_PW) * C2W_PWP + i % C2W_PW] = f32_to_bf16(pre[k]);
     }
     lds_barrier();
     fetch_patch(tile + gridDim.x);
@@ -545,31 +554,41 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
     bool pv[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) pv[u] = py < H && x0 + 16 * u + r < W;
-    // ---- stem
+    // ---- stem: K = (c, dy, dx8) groups; lane (r, g) of step s takes group q = 4s + g, i.e.
+    // the 8 bf16 patch values (c, row wave+dy, cols 16u+r .. +7): five aligned words from
+    // col & ~1 and a byte-align by 2*(col & 1).  Zero K blocks of the 3x3 / 5x5 filters
+    // embedded in the 7x7 window are skipped (channel groups t < 4: steps {0,1,2,4};
+    // t < 8: steps 0..4; t >= 8: all six).
     f32x4 a1[12][2];
 #pragma unroll
     for (int t = 0; t < 12; ++t)
 #pragma unroll
       for (int u = 0; u < 2; ++u) a1[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
+    for (int s = 0; s < 6; ++s) {
       Frag<bf16_t> bfr[2];
+      const int q = 4 * s + g;
+      const int cq = q / 7, dy = q - 7 * cq;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        float vv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int off = ktab[32 * s + 8 * g + e];
-          vv[e] = off >= 0 ? patch[off + wave * C2W_PW + 16 * u + r] : 0.f;
+        if (q < 21) {
+          const int col = 16 * u + r;
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(patch + (cq * C2W_PH + wave + dy) * C2W_PWP + (col & ~1));
+          const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3], w4 = wp[4];
+          const uint32_t sh = (col & 1) * 2;
+          bfr[u].v = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+        } else {
+          bfr[u].zero();
         }
-        bfr[u].from8(vv);
       }
 #pragma unroll
       for (int t = 0; t < 12; ++t) {
-        if (t < 4 && (s == 0 || s == 4)) continue;
-        if (t >= 4 && t < 8 && s == 4) continue;
+        if (t < 4 && (s == 3 || s == 5)) continue;
+        if (t >= 4 && t < 8 && s == 5) continue;
         Frag<bf16_t> af;
         af.v = *reinterpret_cast<const uint4*>(sW1 + (16 * t + r) * C2W_S1 + 32 * s + 8 * g);
+        if (s == 5) af.select(g == 0);  // groups 21..23 lie past the 168 packed columns
         mma(a1[t][0], af, bfr[0]);
         mma(a1[t][1], af, bfr[1]);
       }
