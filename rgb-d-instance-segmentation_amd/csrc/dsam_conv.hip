@@ -403,31 +403,28 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, 
     }
 }
 
-// bf16 dW, code-merged: the workgroup for code k accumulates
+// bf16 dW, code-merged:
 //   dW_k[o][tap][c] = sum over output px p with code(src(p, tap)) == k of G[p][o] X[src][c]
-// over a contiguous range of 64-px units (unit = 64 raster-consecutive output pixels of one
-// image), visiting only the units whose sources meet code k (presence table of
-// k_code_presence, compacted into an LDS list in the prologue).  k_dsam_wgrad_combine folds the
-// dW_k into the five filters (conv_i gets the codes with bit i, proj gets all): work ~ one dense
-// dW instead of popcount + 1 of them.
+// for every region code k present, folded by k_dsam_wgrad_combine into the five filters (conv_i
+// gets the codes with bit i, proj gets all): work ~ one dense dW instead of popcount + 1 of them.
+// A unit is 64 raster-consecutive output pixels of one image.  Load balance: one code (the
+// remainder region) typically meets every unit while the others meet a few percent, so
+// k_wg_plan builds per-code lists of live units (k_code_presence) and cuts them into items of
+// about equal length; k_wg_masks precomputes, per list entry and tap, the 64-bit mask of the
+// unit's pixels whose source meets code k; k_dsam_wgrad_mm runs persistently over
+// (item, output tile) work.
 //
-// Tile: 32*FM output channels (o) x 128 kk (kk = tap*Cin + c: four 32-wide blocks, each inside
-// one tap) per workgroup, 4 waves as 2x2 (wave tile 16*FM x 64); 64 px per step = two MFMA
-// k-blocks.  Per step the operands arrive by LDS-DMA in an S-deep ring, S-1 steps ahead:
+// Output tile: 32*FM channels (o) x 128 kk (kk = tap*Cin + c: four 32-wide blocks, each inside
+// one tap), 4 waves as 2x2 (wave tile 16*FM x 64); one unit (64 px = two MFMA k-blocks) per
+// step, operands by LDS-DMA in an S-deep ring, S-1 steps ahead:
 //   G  [64 px][32*FM o] from the NHWC upstream gradient (FM blocks of 64-byte rows),
-//   X  [64 px][4 x 32 c] im2col rows from the NHWC input.  A row whose source pixel is outside
-//      the input, has a region code other than k, or lies past the image's last output pixel
-//      still copies a valid (clamped) pixel; its 64-px x 4-block mask is published through LDS
-//      and applied to the X fragments in registers (a zero-line source for masked lanes would
-//      be an L2-channel hot spot).
-// The region codes the step needs are read from an LDS copy of the code rows the workgroup's
-// units can reach (no compiler-visible global load in the step loop).  Both MFMA operands
-// are read with ds_read_b64_tr_b16 ([px][col] -> k-major fragments); rows are XOR-swizzled by
-// row bit 3 so the 32-lane halves of a transposed read fall on disjoint banks.
-constexpr int WPX = 64;             // output pixels per unit / step
-constexpr int WCODE_BYTES = 16384;  // LDS budget for the code rows
-constexpr int WLIST_MAX = 2048;     // units per workgroup (u16 list)
-constexpr int WIMG_MAX = 32;        // images per workgroup
+//   X  [64 px][4 x 32 c] im2col rows from the NHWC input; every row copies a valid (clamped)
+//      pixel and the rows outside the input, past the image or of another code are zeroed in
+//      registers from the entry's tap masks (staged in LDS with the item's unit ids).
+// Both MFMA operands are read with ds_read_b64_tr_b16 ([px][col] -> k-major fragments); rows are
+// XOR-swizzled by row bit 3 so the 32-lane halves of a transposed read fall on disjoint banks.
+constexpr int WPX = 64;        // output pixels per unit / step
+constexpr int WITEM_MAX = 64;  // units per item (LDS staging of ids + masks)
 typedef __attribute__((ext_vector_type(4))) short v4s;
 
 template <int FM>
@@ -436,11 +433,9 @@ struct WgCfg {
   static constexpr int NBLK = FM + 4;            // 4 KB blocks per stage: FM of G, 4 of X
   static constexpr int STAGE = NBLK * WPX * 64;
   static constexpr int PER = NBLK;               // DMA pieces per wave per step
-  static constexpr int OFF_CODES = S * STAGE;
-  static constexpr int OFF_LIST = OFF_CODES + WCODE_BYTES;
-  static constexpr int OFF_TAB = OFF_LIST + 2 * WLIST_MAX;
-  static constexpr int OFF_MASK = OFF_TAB + 8 * WIMG_MAX + 64;  // [S][4 blocks][4 waves] u16
-  static constexpr size_t SMEM = (size_t)OFF_MASK + 32 * S;
+  static constexpr int OFF_UNITS = S * STAGE;    // [WITEM_MAX] int unit ids
+  static constexpr int OFF_MASKS = OFF_UNITS + WITEM_MAX * 4;  // [WITEM_MAX][9] u64 tap masks
+  static constexpr size_t SMEM = (size_t)OFF_MASKS + WITEM_MAX * 9 * 8;
   static_assert(SMEM <= 163840, "dW LDS budget");
 };
 
@@ -452,9 +447,13 @@ struct WgArgs {
   const uint8_t* code;    // [B][h][w]
   const uint16_t* pres;   // [B * nunit] bit k: code k met by the unit's sources
   const uint32_t* gmask;  // codes present in the batch
-  int B, Cin, h, w, Cout, ho, wo, nunit, splits;
+  int* list;              // [<= 16 * B * nunit] live entries: unit | code << 24, by code then unit
+  unsigned long long* masks;  // [entry][9] tap masks of the entry's unit for its code
+  int4* items;            // [<= 16 * B * nunit] (code, first entry, end entry, -)
+  int* counts;            // [0] live entries, [1] items
+  int B, Cin, h, w, Cout, ho, wo, nunit, ntile_kk, ntile_o, target;
   float inv_wo;
-  float* partial;         // [splits][16][Cout][9*Cin] f32
+  float* partial;         // [item][Cout][9*Cin] f32
 };
 
 __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict__ code, int B, int h, int w,
@@ -468,10 +467,15 @@ __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict
     const int b = (int)(u / nunit), p = (int)(u % nunit) * WPX + l;
     if (p < hwo) {
       const int oy = p / wo, ox = p % wo;
+      uint32_t cv[9];
+#pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int iy = 2 * oy - 1 + tap / 3, ix = 2 * ox - 1 + tap % 3;
-        if (iy >= 0 && iy < h && ix >= 0 && ix < w) m |= 1u << code[((long long)b * h + iy) * w + ix];
+        const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+        cv[tap] = ok ? (1u << code[((long long)b * h + (ok ? iy : 0)) * w + (ok ? ix : 0)]) : 0u;
       }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) m |= cv[tap];
     }
   }
 #pragma unroll
@@ -482,132 +486,119 @@ __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict
   }
 }
 
-// input rows of image b reachable from output units [uf, ul] of that image (3x3 s2 p1)
-__device__ __forceinline__ void wg_rows(const WgArgs& a, int b, int u0, int u1, int& r0, int& r1) {
-  const int uf = max(u0, b * a.nunit), ul = min(u1, (b + 1) * a.nunit) - 1;
-  const int pf = (uf - b * a.nunit) * WPX, pl = min(a.ho * a.wo, (ul - b * a.nunit + 1) * WPX) - 1;
-  r0 = max(0, 2 * (pf / a.wo) - 1);
-  r1 = min(a.h, 2 * (pl / a.wo) + 2);
+// Plan (one 1024-thread workgroup): per code the ordered list of live units, then items of
+// about equal length L = ceil(entries / (target / output tiles)), capped at WITEM_MAX.
+__global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
+  __shared__ int wsum[16];
+  __shared__ int cnt_s[16], off_s[17];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int U = a.B * a.nunit;
+  if (tid < 16) cnt_s[tid] = 0;
+  __syncthreads();
+  // counts per code
+  uint32_t c16[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) c16[k] = 0u;
+  for (int u = tid; u < U; u += 1024) {
+    const uint32_t m = a.pres[u];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c16[k] += (m >> k) & 1u;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    uint32_t v = c16[k];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    if (lane == 0 && v) atomicAdd(&cnt_s[k], (int)v);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int o = 0;
+    for (int k = 0; k < 16; ++k) {
+      off_s[k] = o;
+      o += cnt_s[k];
+    }
+    off_s[16] = o;
+  }
+  __syncthreads();
+  // ordered compaction per code
+  for (int k = 0; k < 16; ++k) {
+    if (cnt_s[k] == 0) continue;  // uniform
+    int base = off_s[k];
+    for (int u0 = 0; u0 < U; u0 += 1024) {
+      const int u = u0 + tid;
+      const bool live = u < U && ((a.pres[u] >> k) & 1u);
+      const unsigned long long bal = __ballot(live);
+      if (lane == 0) wsum[w] = __popcll(bal);
+      __syncthreads();
+      int before = base;
+      for (int q = 0; q < w; ++q) before += wsum[q];
+      if (live) a.list[before + __popcll(bal & ((1ull << lane) - 1ull))] = u | (k << 24);
+      int tot = 0;
+      for (int q = 0; q < 16; ++q) tot += wsum[q];
+      base += tot;
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    const int total = off_s[16];
+    const int want = max(1, a.target / max(1, a.ntile_kk * a.ntile_o));
+    int L = max(1, (total + want - 1) / want);
+    L = min(L, WITEM_MAX);
+    int ni = 0;
+    for (int k = 0; k < 16; ++k) {
+      const int c = cnt_s[k];
+      if (!c) continue;
+      const int n = (c + L - 1) / L;
+      for (int j = 0; j < n; ++j)
+        a.items[ni++] = make_int4(k, off_s[k] + (int)((long long)c * j / n), off_s[k] + (int)((long long)c * (j + 1) / n), 0);
+    }
+    a.counts[0] = total;
+    a.counts[1] = ni;
+  }
+}
+
+// Tap masks of every live entry: one wave per entry, lane = pixel of the unit.
+__global__ __launch_bounds__(256) void k_wg_masks(WgArgs a) {
+  const int e = (blockIdx.x * 256 + threadIdx.x) >> 6, l = threadIdx.x & 63;
+  if (e >= a.counts[0]) return;  // wave-uniform
+  const int v = a.list[e], u = v & 0xffffff, k = v >> 24;
+  const int hwo = a.ho * a.wo, b = u / a.nunit, p = (u % a.nunit) * WPX + l;
+  const bool pv = p < hwo;
+  const int oy = pv ? p / a.wo : 0, ox = pv ? p % a.wo : 0;
+  uint32_t cv[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int iy = 2 * oy - 1 + tap / 3, ix = 2 * ox - 1 + tap % 3;
+    const bool ok = pv && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+    cv[tap] = ok ? a.code[((long long)b * a.h + iy) * a.w + ix] : 0xffu;
+  }
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const unsigned long long m = __ballot(cv[tap] == (uint32_t)k);
+    if (l == 0) a.masks[(long long)e * 9 + tap] = m;
+  }
 }
 
 template <int FM>
 __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
   using Cfg = WgCfg<FM>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int kcode = blockIdx.z & 15, split = blockIdx.z >> 4;
-  if (!((*a.gmask >> kcode) & 1u)) return;  // code absent from the batch: combine skips it
-  uint8_t* scode = (uint8_t*)(smem + Cfg::OFF_CODES);
-  uint16_t* slist = (uint16_t*)(smem + Cfg::OFF_LIST);
-  int* img_off = (int*)(smem + Cfg::OFF_TAB);   // [WIMG_MAX] LDS offset of image b0+i's first row
-  int* img_row0 = img_off + WIMG_MAX;           // [WIMG_MAX] first input row held
-  int* wave_cnt = img_row0 + WIMG_MAX;          // [4] + total
+  int* sunits = (int*)(smem + Cfg::OFF_UNITS);
+  unsigned long long* smasks = (unsigned long long*)(smem + Cfg::OFF_MASKS);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave & 1, wn = wave >> 1;
   const int KK = 9 * a.Cin, hwo = a.ho * a.wo;
-  const int kk0 = blockIdx.x * 128, o0 = blockIdx.y * 32 * FM;
-  const int U = a.B * a.nunit;
-  const int u0 = (int)((long long)split * U / a.splits), u1 = (int)((long long)(split + 1) * U / a.splits);
-  const int b0 = u0 / a.nunit, b1 = u1 > u0 ? (u1 - 1) / a.nunit : b0;
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  uint16_t* smask = (uint16_t*)(smem + Cfg::OFF_MASK);
-  // ---- prologue 1: code rows of every image the units reach
-  if (tid == 0) {
-    int off = 0;
-    for (int b = b0; b <= b1 && u1 > u0; ++b) {
-      int r0, r1;
-      wg_rows(a, b, u0, u1, r0, r1);
-      img_off[b - b0] = off - r0 * a.w;  // LDS index of (row, col) = img_off + row*w + col
-      img_row0[b - b0] = r0;
-      off += (r1 - r0) * a.w;
-    }
-  }
-  __syncthreads();
-  for (int b = b0; b <= b1 && u1 > u0; ++b) {
-    int r0, r1;
-    wg_rows(a, b, u0, u1, r0, r1);
-    const uint8_t* src = a.code + ((long long)b * a.h + r0) * a.w;
-    uint8_t* dst = scode + img_off[b - b0] + r0 * a.w;
-    const int n = (r1 - r0) * a.w;
-    for (int i0 = 0; i0 < n; i0 += 256 * 16) {  // 16 independent loads per thread, then the stores
-      uint8_t v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = i0 + q * 256 + tid;
-        v[q] = i < n ? src[i] : 0;
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = i0 + q * 256 + tid;
-        if (i < n) dst[i] = v[q];
-      }
-    }
-  }
-  // ---- prologue 2: ordered list of the units meeting code k
-  int count = 0;
-  for (int ub = u0; ub < u1; ub += 256) {
-    const int u = ub + tid;
-    const bool live = u < u1 && ((a.pres[u] >> kcode) & 1u);
-    const unsigned long long bal = __ballot(live);
-    __syncthreads();
-    if (lane == 0) wave_cnt[wave] = __popcll(bal);
-    __syncthreads();
-    int before = count;
-    for (int w2 = 0; w2 < wave; ++w2) before += wave_cnt[w2];
-    if (live) slist[before + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(u - u0);
-    count += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
-  }
-  __syncthreads();
-  // ---- per-lane copy roles: pixel row pr of every block, 16-byte chunk q
+  const int ntile = a.ntile_kk * a.ntile_o;
+  const int nwork = a.counts[1] * ntile;
+  // per-lane copy roles: pixel row pr of every block, 16-byte chunk q
   const int pr = 16 * wave + (lane >> 2);
   const int qch = 8 * ((lane & 3) ^ wg_swz(pr));
-  int xky[4], xkx[4], xc[4];
-  bool xok[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int kk = kk0 + 32 * j;
-    xok[j] = kk < KK;
-    const int tap = xok[j] ? kk / a.Cin : 0;
-    xky[j] = tap / 3;
-    xkx[j] = tap % 3;
-    xc[j] = xok[j] ? kk % a.Cin : 0;
-  }
-  auto issue = [&](int slot, int it) {
-    const int u = u0 + (int)slist[it];
-    const int b = u / a.nunit;
-    const int p = (u - b * a.nunit) * WPX + pr;
-    const bool pv = p < hwo;
-    const int pc = pv ? p : hwo - 1;
-    const int oy = (int)(((float)pc + 0.5f) * a.inv_wo), ox = pc - oy * a.wo;
-    const uint32_t sb = lds0 + slot * Cfg::STAGE + wave * 1024;
-    const bf16_t* gsrc = a.gout + ((long long)b * hwo + pc) * a.Cout + qch;
-#pragma unroll
-    for (int ob = 0; ob < FM; ++ob) dma_lds16(gsrc + min(o0 + 32 * ob, a.Cout - 32), sb + ob * 4096);
-    const int ib = b - b0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int iy = 2 * oy - 1 + xky[j], ix = 2 * ox - 1 + xkx[j];
-      const bool inb = iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
-      const int iyc = min(max(iy, 0), a.h - 1), ixc = min(max(ix, 0), a.w - 1);
-      const bool ok = pv && xok[j] && inb && scode[img_off[ib] + iyc * a.w + ixc] == kcode;
-      dma_lds16(a.x + (((long long)b * a.h + iyc) * a.w + ixc) * a.Cin + xc[j] + qch, sb + (FM + j) * 4096);
-      // 16-bit row mask of this wave's 16 rows (lanes 4i..4i+3 share row i)
-      unsigned long long m = __ballot(ok) & 0x1111111111111111ull;
-      m = (m | (m >> 3)) & 0x0303030303030303ull;
-      m = (m | (m >> 6)) & 0x000F000F000F000Full;
-      m = (m | (m >> 12)) & 0x000000FF000000FFull;
-      m = (m | (m >> 24)) & 0xFFFFull;
-      if (lane == 0) smask[(slot * 4 + j) * 4 + wave] = (uint16_t)m;
-    }
-  };
-  f32x4 acc[FM][4];
-#pragma unroll
-  for (int mi = 0; mi < FM; ++mi)
-#pragma unroll
-    for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // transposed fragment [k = 8g + j][col = c0 + r] of a [64 px][32 col] block (64-byte rows)
   const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+  // transposed fragment [k = 8g + j][col = c0 + r] of a [64 px][32 col] block (64-byte rows)
   auto trfrag = [&](const char* blk, int kb, int c0) {
     const int col = c0 + 4 * p4, ch = col >> 3, off = (col & 7) * 2;
     const int row0 = 32 * kb + 8 * g + q4, row1 = row0 + 4;
@@ -622,83 +613,136 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
                      (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
     return f;
   };
-  const int nst = count;
-  const int npro = nst < Cfg::S - 1 ? nst : Cfg::S - 1;
-  for (int i = 0; i < npro; ++i) issue(i, i);
-  if (npro >= 3) vm_wait_barrier<2 * Cfg::PER>();
-  else if (npro == 2) vm_wait_barrier<Cfg::PER>();
-  else vm_wait_barrier<0>();
-#pragma unroll 1
-  for (int s = 0; s < nst; ++s) {
-    if (s + Cfg::S - 1 < nst) issue((s + Cfg::S - 1) % Cfg::S, s + Cfg::S - 1);
-    const int slot = s % Cfg::S;
-    const char* st = smem + slot * Cfg::STAGE;
+  for (int wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+    const int4 item = a.items[wi / ntile];
+    const int tile = wi % ntile, e0 = item.y, nst = item.z - item.y;
+    const int kk0 = (tile % a.ntile_kk) * 128, o0 = (tile / a.ntile_kk) * 32 * FM;
+    // stage the item's unit ids and tap masks
+    for (int i = tid; i < nst; i += 256) sunits[i] = a.list[e0 + i] & 0xffffff;
+    for (int i = tid; i < nst * 9; i += 256) smasks[i] = a.masks[(long long)e0 * 9 + i];
+    __syncthreads();
+    int xky[4], xkx[4], xc[4], xtap[4];
+    bool xok[4];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      Frag<bf16_t> fa[FM], fb[4];
+    for (int j = 0; j < 4; ++j) {
+      const int kk = kk0 + 32 * j;
+      xok[j] = kk < KK;
+      xtap[j] = xok[j] ? kk / a.Cin : 0;
+      xky[j] = xtap[j] / 3;
+      xkx[j] = xtap[j] % 3;
+      xc[j] = xok[j] ? kk % a.Cin : 0;
+    }
+    auto issue = [&](int slot, int it) {
+      const int u = sunits[it];
+      const int b = u / a.nunit;
+      const int p = (u - b * a.nunit) * WPX + pr;
+      const int pc = p < hwo ? p : hwo - 1;
+      const int oy = (int)(((float)pc + 0.5f) * a.inv_wo), ox = pc - oy * a.wo;
+      const uint32_t sb = lds0 + slot * Cfg::STAGE + wave * 1024;
+      const bf16_t* gsrc = a.gout + ((long long)b * hwo + pc) * a.Cout + qch;
 #pragma unroll
-      for (int mi = 0; mi < FM; ++mi) {
-        const int ol = wm * 16 * FM + 16 * mi;
-        fa[mi] = trfrag(st + (ol >> 5) * 4096, kb, ol & 31);
+      for (int ob = 0; ob < FM; ++ob) dma_lds16(gsrc + min(o0 + 32 * ob, a.Cout - 32), sb + ob * 4096);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int iyc = min(max(2 * oy - 1 + xky[j], 0), a.h - 1), ixc = min(max(2 * ox - 1 + xkx[j], 0), a.w - 1);
+        dma_lds16(a.x + (((long long)b * a.h + iyc) * a.w + ixc) * a.Cin + xc[j] + qch, sb + (FM + j) * 4096);
       }
+    };
+    f32x4 acc[FM][4];
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        const int kl = wn * 64 + 16 * nj;
-        fb[nj] = trfrag(st + (FM + (kl >> 5)) * 4096, kb, kl & 31);
-        // rows 32kb + 8g .. +7 of block kl/32: keep only the rows whose mask bit is set
-        const uint32_t bits =
-            (uint32_t)(smask[(slot * 4 + (kl >> 5)) * 4 + 2 * kb + (g >> 1)] >> (8 * (g & 1))) & 0xFFu;
-        if (bits != 0xFFu) {
-          auto hm = [&](int e) { return ((bits >> e) & 1u) ? 0xFFFFu : 0u; };
-          fb[nj].v.x &= hm(0) | (hm(1) << 16);
-          fb[nj].v.y &= hm(2) | (hm(3) << 16);
-          fb[nj].v.z &= hm(4) | (hm(5) << 16);
-          fb[nj].v.w &= hm(6) | (hm(7) << 16);
+    for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int npro = nst < Cfg::S - 1 ? nst : Cfg::S - 1;
+    for (int i = 0; i < npro; ++i) issue(i, i);
+    if (npro >= 3) vm_wait_barrier<2 * Cfg::PER>();
+    else if (npro == 2) vm_wait_barrier<Cfg::PER>();
+    else vm_wait_barrier<0>();
+#pragma unroll 1
+    for (int s = 0; s < nst; ++s) {
+      if (s + Cfg::S - 1 < nst) issue((s + Cfg::S - 1) % Cfg::S, s + Cfg::S - 1);
+      const int slot = s % Cfg::S;
+      const char* st = smem + slot * Cfg::STAGE;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        Frag<bf16_t> fa[FM], fb[4];
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi) {
+          const int ol = wm * 16 * FM + 16 * mi;
+          fa[mi] = trfrag(st + (ol >> 5) * 4096, kb, ol & 31);
+        }
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) {
+          const int kl = wn * 64 + 16 * nj, j = kl >> 5;
+          fb[nj] = trfrag(st + (FM + j) * 4096, kb, kl & 31);
+          // rows 32kb + 8g .. +7 of block j: keep the pixels whose source meets code k at tap_j
+          const uint32_t bits =
+              xok[j] ? (uint32_t)(smasks[s * 9 + xtap[j]] >> (32 * kb + 8 * g)) & 0xFFu : 0u;
+          if (bits != 0xFFu) {
+            auto hm = [&](int e) { return ((bits >> e) & 1u) ? 0xFFFFu : 0u; };
+            fb[nj].v.x &= hm(0) | (hm(1) << 16);
+            fb[nj].v.y &= hm(2) | (hm(3) << 16);
+            fb[nj].v.z &= hm(4) | (hm(5) << 16);
+            fb[nj].v.w &= hm(6) | (hm(7) << 16);
+          }
+        }
+#pragma unroll
+        for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+          for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
+      }
+      const int ahead = (nst - 1 < s + Cfg::S - 1 ? nst - 1 : s + Cfg::S - 1) - (s + 1);
+      if (ahead >= 2) vm_wait_barrier<2 * Cfg::PER>();
+      else if (ahead == 1) vm_wait_barrier<Cfg::PER>();
+      else vm_wait_barrier<0>();
+    }
+    float* dst = a.partial + ((long long)(wi / ntile) * a.Cout) * KK;
+#pragma unroll
+    for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int o = o0 + wm * 16 * FM + 16 * mi + 4 * g + reg;
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) {
+          const int c = kk0 + wn * 64 + 16 * nj + r;
+          if (o < a.Cout && c < KK) dst[(long long)o * KK + c] = acc[mi][nj][reg];
         }
       }
-#pragma unroll
-      for (int mi = 0; mi < FM; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
-    }
-    const int ahead = (nst - 1 < s + Cfg::S - 1 ? nst - 1 : s + Cfg::S - 1) - (s + 1);
-    if (ahead >= 2) vm_wait_barrier<2 * Cfg::PER>();
-    else if (ahead == 1) vm_wait_barrier<Cfg::PER>();
-    else vm_wait_barrier<0>();
+    __syncthreads();  // staged ids / masks and the ring are free for the next work unit
   }
-  float* dst = a.partial + ((long long)(split * 16 + kcode) * a.Cout) * KK;
-#pragma unroll
-  for (int mi = 0; mi < FM; ++mi)
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int o = o0 + wm * 16 * FM + 16 * mi + 4 * g + reg;
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        const int c = kk0 + wn * 64 + 16 * nj + r;
-        if (o < a.Cout && c < KK) dst[(long long)o * KK + c] = acc[mi][nj][reg];
-      }
-    }
 }
 
-// dW_k (present codes, split partials) -> the reference filters, fixed summation order.  One
-// block per output channel o: the five sums of the row are formed in (tap, c) order (coalesced
-// partial reads), parked in LDS, then written in the OIHW (c, tap) order (coalesced writes).
-__global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restrict__ partial, int splits,
-                                                            const uint32_t* __restrict__ gmask, int Cin, int Cout,
+// dW_k (per item partials) -> the reference filters, fixed summation order (items in list
+// order: codes ascending, units ascending).  One block per output channel o: the five sums of
+// the row are formed in (tap, c) order with every item's load of a thread in flight together,
+// parked in LDS, then written in the OIHW (c, tap) order.
+__global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restrict__ partial, const int4* __restrict__ items,
+                                                            const int* __restrict__ counts, int Cin, int Cout,
                                                             float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
   extern __shared__ float srow[];  // [5][9*Cin]
-  const int KK = 9 * Cin, o = blockIdx.x;
-  const uint32_t m = *gmask;
+  const int KK = 9 * Cin, o = blockIdx.x, ni = counts[1];
   for (int kk = threadIdx.x; kk < KK; kk += 256) {
     float seg[4] = {0.f, 0.f, 0.f, 0.f}, pr = 0.f;
-    for (int k = 0; k < 16; ++k) {
-      if (!((m >> k) & 1u)) continue;
-      float v = 0.f;
-      for (int sp = 0; sp < splits; ++sp) v += partial[((long long)(sp * 16 + k) * Cout + o) * KK + kk];
+    const float* src = partial + (long long)o * KK + kk;
+    int it = 0;
+    for (; it + 4 <= ni; it += 4) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = src[(long long)(it + q) * Cout * KK];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = items[it + q].x;
+        pr += v[q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) seg[i] += ((k >> i) & 1) ? v[q] : 0.f;
+      }
+    }
+    for (; it < ni; ++it) {
+      const float v = src[(long long)it * Cout * KK];
+      const int k = items[it].x;
       pr += v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if ((k >> i) & 1) seg[i] += v;
+      for (int i = 0; i < 4; ++i) seg[i] += ((k >> i) & 1) ? v : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) srow[i * KK + kk] = seg[i];
@@ -1354,48 +1398,35 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   return RGBD_OK;
 }
 
-// ---- bf16 dW plan: o tile (FM), unit splits obeying the per-workgroup LDS limits
+// ---- bf16 dW: output tile (FM); items and their partials are sized by the device plan, the
+// workspace by the worst case (every code live in every unit)
 struct WgPlan {
-  int fm, splits, nunit;
+  int fm, nunit, ntile_kk, ntile_o, max_entries;
 };
 int wg_fm(int Cout) { return Cout % 192 == 0 ? 6 : (Cout % 128 == 0 ? 4 : 2); }
-// largest per-workgroup code-row bytes / image count / unit count over the splits
-static bool wg_fits(int B, int h, int w, int nunit, int splits) {
-  const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo;
-  const long long U = (long long)B * nunit;
-  for (int sp = 0; sp < splits; ++sp) {
-    const long long u0 = sp * U / splits, u1 = (sp + 1) * U / splits;
-    if (u1 - u0 > WLIST_MAX) return false;
-    if (u1 <= u0) continue;
-    const long long b0 = u0 / nunit, b1 = (u1 - 1) / nunit;
-    if (b1 - b0 + 1 > WIMG_MAX) return false;
-    long long bytes = 0;
-    for (long long b = b0; b <= b1; ++b) {
-      const long long uf = std::max(u0, b * nunit), ul = std::min(u1, (b + 1) * nunit) - 1;
-      const long long pf = (uf - b * nunit) * WPX, pl = std::min<long long>(hwo, (ul - b * nunit + 1) * WPX) - 1;
-      const long long r0 = std::max<long long>(0, 2 * (pf / wo) - 1), r1 = std::min<long long>(h, 2 * (pl / wo) + 2);
-      bytes += (r1 - r0) * w;
-    }
-    if (bytes > WCODE_BYTES) return false;
-  }
-  return true;
-}
 static WgPlan wg_plan(int B, int Cin, int h, int w, int Cout) {
   WgPlan p;
   p.fm = wg_fm(Cout);
   const int hwo = ((h + 1) / 2) * ((w + 1) / 2);
   p.nunit = (hwo + WPX - 1) / WPX;
-  const long long U = (long long)B * p.nunit;
-  // ~5 codes present per batch is typical: one workgroup per CU (LDS-limited) ~ 1.5 rounds
-  const long long tiles = (long long)ceil_div(9ll * Cin, 128) * ceil_div(Cout, 32 * p.fm) * 5;
-  int sp = (int)std::max<long long>(1, std::min<long long>(U, ceil_div(384, tiles)));
-  while (sp < U && !wg_fits(B, h, w, p.nunit, sp)) ++sp;
-  p.splits = sp;
+  p.ntile_kk = ceil_div(9ll * Cin, 128);
+  p.ntile_o = ceil_div(Cout, 32 * p.fm);
+  p.max_entries = 16 * B * p.nunit;
   return p;
+}
+// items are at most max_entries; the plan targets ~512 work units
+static int wg_target() {
+  static const int t = getenv("RGBD_WG_TARGET") ? atoi(getenv("RGBD_WG_TARGET")) : 512;
+  return t;
+}
+// partial buffer bound: items <= entries / L + 16 with L >= entries / (target / tiles)
+static size_t wg_max_items(const WgPlan& p) {
+  const long long want = std::max(1, wg_target() / std::max(1, p.ntile_kk * p.ntile_o));
+  return (size_t)std::min<long long>(p.max_entries, want + 16 + p.max_entries / WITEM_MAX);
 }
 
 template <int FM>
-hipError_t launch_wg(const WgArgs& a, dim3 grid, hipStream_t s) {
+hipError_t launch_wg(const WgArgs& a, int grid, hipStream_t s) {
   static const hipError_t attr = hipFuncSetAttribute((const void*)k_dsam_wgrad_mm<FM>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      (int)WgCfg<FM>::SMEM);
@@ -1549,16 +1580,18 @@ int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, in
 // bf16 workspace: [splits][16 codes][Cout][9 Cin] f32 partials | [B] f32 x Cout channel sums |
 // presence table [B][chunks] u16 | global code mask u32
 struct WgradWs {
-  size_t partial, csum, pres, gmask, total;
+  size_t partial, csum, pres, gmask, list, masks, items, counts, total;
 };
 static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   WgradWs o;
   size_t off = 0;
-  size_t part, npres = 1;
+  size_t part, npres = 1, nent = 1, nitems = 1;
   if (dtype == RGBD_BF16) {
     const WgPlan p = wg_plan(B, Cin, h, w, Cout);
-    part = (size_t)p.splits * 16 * Cout * 9 * Cin;
+    nitems = wg_max_items(p);
+    part = nitems * Cout * 9 * Cin;
     npres = (size_t)B * p.nunit;
+    nent = p.max_entries;
   } else {
     part = (size_t)dsam_wgrad_splits(B, Cin, Cout) * Cout * 45 * Cin;
   }
@@ -1569,6 +1602,14 @@ static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   o.pres = off;
   off += align256(sizeof(uint16_t) * npres);
   o.gmask = off;
+  off += 256;
+  o.list = off;
+  off += align256(sizeof(int) * nent);
+  o.masks = off;
+  off += align256(sizeof(unsigned long long) * 9 * nent);
+  o.items = off;
+  off += align256(sizeof(int4) * nitems);
+  o.counts = off;
   off += 256;
   o.total = off;
   return o;
@@ -1605,7 +1646,7 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
     RGBD_REQUIRE(Cin % 32 == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
     RGBD_REQUIRE((long long)hwo < (1ll << 22) && (long long)B * h * w < (1ll << 31), RGBD_E_SHAPE);
     const WgPlan P = wg_plan(B, Cin, h, w, Cout);
-    RGBD_REQUIRE(wg_fits(B, h, w, P.nunit, P.splits), RGBD_E_SHAPE);
+    RGBD_REQUIRE((long long)B * P.nunit < (1 << 24), RGBD_E_SHAPE);
     uint16_t* pres = (uint16_t*)((char*)ws + L.pres);
     uint32_t* gmask = (uint32_t*)((char*)ws + L.gmask);
     const hipError_t me = hipMemsetAsync(gmask, 0, sizeof(uint32_t), s);
@@ -1618,13 +1659,21 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
     a.code = code;
     a.pres = pres;
     a.gmask = gmask;
+    a.list = (int*)((char*)ws + L.list);
+    a.masks = (unsigned long long*)((char*)ws + L.masks);
+    a.items = (int4*)((char*)ws + L.items);
+    a.counts = (int*)((char*)ws + L.counts);
     a.B = B; a.Cin = Cin; a.h = h; a.w = w; a.Cout = Cout; a.ho = ho; a.wo = wo;
     a.nunit = P.nunit;
-    a.splits = P.splits;
+    a.ntile_kk = P.ntile_kk;
+    a.ntile_o = P.ntile_o;
+    a.target = wg_target();
     a.inv_wo = 1.0f / (float)wo;
     a.partial = partial;
-    dim3 g2(ceil_div(9ll * Cin, 128), ceil_div(Cout, 32 * P.fm), P.splits * 16);
-    const hipError_t e = P.fm == 6 ? launch_wg<6>(a, g2, s) : P.fm == 4 ? launch_wg<4>(a, g2, s) : launch_wg<2>(a, g2, s);
+    k_wg_plan<<<1, 1024, 0, s>>>(a);
+    k_wg_masks<<<ceil_div((long long)P.max_entries, 4), 256, 0, s>>>(a);
+    const int grid = 256;  // persistent: one LDS-bound workgroup per CU
+    const hipError_t e = P.fm == 6 ? launch_wg<6>(a, grid, s) : P.fm == 4 ? launch_wg<4>(a, grid, s) : launch_wg<2>(a, grid, s);
     if (e != hipSuccess) return (int)e;
     k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
     const int csmem = 5 * 9 * Cin * (int)sizeof(float);
@@ -1632,7 +1681,7 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     if (cattr != hipSuccess) return (int)cattr;
     RGBD_REQUIRE(csmem <= 163840, RGBD_E_SHAPE);
-    k_dsam_wgrad_combine<<<Cout, 256, csmem, s>>>(partial, P.splits, gmask, Cin, Cout, dconv_w, dproj_w);
+    k_dsam_wgrad_combine<<<Cout, 256, csmem, s>>>(partial, a.items, a.counts, Cin, Cout, dconv_w, dproj_w);
   } else {
     return RGBD_E_DTYPE;
   }
