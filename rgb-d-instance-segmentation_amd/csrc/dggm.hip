@@ -6,9 +6,11 @@
 // intrinsics, so the planes are bit-exact to the numpy/OpenCV float32 result.
 //
 // K2 follows DepthGradientInjectionResidual.forward (custom_model.py:1204-1269) fused with the
-// final sum backbone_k = cp1_k + cp2_k (custom_model.py:355).  One thread owns one output
-// pixel and walks a channel chunk, so the resampled gate (3 bilinear taps x 4 + 1 nearest) is
-// computed once per pixel and the NCHW planes are streamed with coalesced accesses.
+// final sum backbone_k = cp1_k + cp2_k (custom_model.py:355).  A workgroup computes the
+// resampled gate (3 bilinear taps x 4 + 1 nearest) of a pixel tile once into LDS and streams 32
+// channel planes of that tile with vector accesses (8 pixels per lane where h*w allows).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "timing.hpp"
 
@@ -145,85 +147,235 @@ __device__ __forceinline__ Gate gate_at(const float* __restrict__ grad, const fl
   return gt;
 }
 
-constexpr int kFuseCh = 16;  // channels per thread
+// Block = a tile of 64*PX pixels of one image x 32 channels; the tile's gates are computed once
+// into LDS, each wave then owns 8 channels and each lane PX consecutive pixels: one 16-B (PX=8),
+// 8-B (PX=4) or 2-B (PX=1) access per bf16 channel plane, PX the largest of 8/4/1 dividing h*w
+// (so a lane's pixels are all valid or all past the end).  All 8 channels' loads are issued
+// before any arithmetic.
+constexpr int kBlkCh = 32;
+constexpr int kWaveCh = 8;
+constexpr int kRedStride = 36;  // floats per lane row of the bwd wave reduction
 
-template <typename T>
+template <typename T, int PX> struct PxN;
+template <int PX> struct PxN<float, PX> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[PX]) {
+    if constexpr (PX == 1) {
+      v[0] = *p;
+    } else {
+#pragma unroll
+      for (int q = 0; q < PX / 4; ++q) {
+        const float4 a = ((const float4*)p)[q];
+        v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+      }
+    }
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[PX]) {
+    if constexpr (PX == 1) {
+      *p = v[0];
+    } else {
+#pragma unroll
+      for (int q = 0; q < PX / 4; ++q) ((float4*)p)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+  }
+};
+template <int PX> struct PxN<bf16_t, PX> {
+  static __device__ __forceinline__ void load(const bf16_t* p, float (&v)[PX]) {
+    if constexpr (PX == 1) {
+      v[0] = bf16_to_f32(*p);
+    } else {
+      uint32_t w[PX / 2];
+      if constexpr (PX == 8) {
+        const uint4 u = *(const uint4*)p;
+        w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+      } else {
+        const uint2 u = *(const uint2*)p;
+        w[0] = u.x; w[1] = u.y;
+      }
+#pragma unroll
+      for (int j = 0; j < PX / 2; ++j) {
+        v[2 * j] = __uint_as_float(w[j] << 16);
+        v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      }
+    }
+  }
+  static __device__ __forceinline__ void store(bf16_t* p, const float (&v)[PX]) {
+    if constexpr (PX == 1) {
+      *p = f32_to_bf16(v[0]);
+    } else {
+      uint32_t w[PX / 2];
+#pragma unroll
+      for (int j = 0; j < PX / 2; ++j) w[j] = (uint32_t)f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+      if constexpr (PX == 8)
+        *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+      else
+        *(uint2*)p = make_uint2(w[0], w[1]);
+    }
+  }
+};
+
+__constant__ int g_dggm_dbg;  // RGBD_DGGM_DBG=1: constant gates (timing experiments only)
+__device__ __forceinline__ int dggm_dbg() { return g_dggm_dbg; }
+
+template <int PX>
+struct TileGates {
+  float g[3][PX];
+  int p;       // first pixel of this lane within the image
+  bool valid;  // the lane's PX pixels are inside the image
+};
+
+// Stage the tile's gates in LDS and return this lane's PX of them.
+// Also stages the block's 32 channels of (w0, w1, w2, bias) into swb (clamped past C).
+template <int PX>
+__device__ __forceinline__ TileGates<PX> stage_gates(float (*sg)[512], float4* swb, const float* __restrict__ grad,
+                                                     const float* __restrict__ mask, int H, int W, int h,
+                                                     int w, int p0, const float* __restrict__ wt,
+                                                     const float* __restrict__ bias, int C) {
+  constexpr int TP = 64 * PX;
+  const int hw = h * w;
+  if (threadIdx.x < kBlkCh) {
+    const int c = min((int)blockIdx.y * kBlkCh + (int)threadIdx.x, C - 1);
+    swb[threadIdx.x] = make_float4(wt[c * 3 + 0], wt[c * 3 + 1], wt[c * 3 + 2], bias[c]);
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < TP; i0 += 256) {
+    const int i = i0 + threadIdx.x;
+    const int p = p0 + i;
+    if (i < TP) {
+      Gate gt = {{0.f, 0.f, 0.f}};
+      if (p < hw) gt = (dggm_dbg() & 1) ? Gate{{0.5f, 0.25f, 0.125f}} : gate_at(grad, mask, H, W, h, w, p / w, p % w);
+      sg[0][i] = gt.g[0];
+      sg[1][i] = gt.g[1];
+      sg[2][i] = gt.g[2];
+    }
+  }
+  __syncthreads();
+  TileGates<PX> t;
+  const int lane = threadIdx.x & 63;
+  t.p = p0 + PX * lane;
+  t.valid = t.p < hw;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int j = 0; j < PX; ++j) t.g[c][j] = sg[c][PX * lane + j];
+  return t;
+}
+
+template <typename T, int PX, bool HAS1>
 __global__ __launch_bounds__(256) void k_dggm_fuse_fwd(const T* __restrict__ cp1, const T* __restrict__ color,
                                                        const float* __restrict__ grad,
                                                        const float* __restrict__ mask, long long pvs,
                                                        int H, int W, int C, int h, int w,
                                                        const float* __restrict__ wt,
                                                        const float* __restrict__ bias, T* __restrict__ out) {
-  const int b = blockIdx.z;
-  const int hw = h * w;
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= hw) return;
-  const int y = p / w, x = p % w;
-  const Gate gt = gate_at(grad + b * pvs, mask + b * pvs, H, W, h, w, y, x);
-  const int c0 = blockIdx.y * kFuseCh;
-  const int c1 = min(C, c0 + kFuseCh);
-  for (int c = c0; c < c1; ++c) {
-    const long long o = ((long long)b * C + c) * hw + p;
-    float pre = bias[c] + wt[c * 3 + 0] * gt.g[0] + wt[c * 3 + 1] * gt.g[1] + wt[c * 3 + 2] * gt.g[2];
-    const float enh = pre > 0.f ? pre : 0.f;
-    const float cp2 = Num<T>::to_f(color[o]) + enh;  // color_feat + depth_enhancement (:1255)
-    out[o] = Num<T>::from_f(cp1 ? Num<T>::to_f(cp1[o]) + cp2 : cp2);
+  __shared__ float sg[3][512];
+  __shared__ float4 swb[kBlkCh];
+  constexpr int TP = 64 * PX;
+  const int hw = h * w, tpi = (hw + TP - 1) / TP;
+  const int b = blockIdx.x / tpi, p0 = (blockIdx.x % tpi) * TP;
+  const TileGates<PX> t = stage_gates<PX>(sg, swb, grad + b * pvs, mask + b * pvs, H, W, h, w, p0, wt, bias, C);
+  const int cw = blockIdx.y * kBlkCh + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kWaveCh;
+  if (!t.valid || cw >= C) return;
+  float col[kWaveCh][PX], y[kWaveCh][PX];
+#pragma unroll
+  for (int cc = 0; cc < kWaveCh; ++cc) {
+    const long long o = ((long long)b * C + min(cw + cc, C - 1)) * hw + t.p;
+    PxN<T, PX>::load(color + o, col[cc]);
+    if constexpr (HAS1) PxN<T, PX>::load(cp1 + o, y[cc]);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the whole load batch ahead of the first use
+#pragma unroll
+  for (int cc = 0; cc < kWaveCh; ++cc) {
+    const int c = min(cw + cc, C - 1);
+    const float4 wb = swb[c - (int)blockIdx.y * kBlkCh];
+    const float w0 = wb.x, w1 = wb.y, w2 = wb.z, bc = wb.w;
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const float pre = bc + w0 * t.g[0][j] + w1 * t.g[1][j] + w2 * t.g[2][j];
+      const float cp2 = col[cc][j] + (pre > 0.f ? pre : 0.f);  // color_feat + depth_enhancement (:1255)
+      y[cc][j] = HAS1 ? y[cc][j] + cp2 : cp2;
+    }
+  }
+  if (dggm_dbg() & 4) return;
+  // stores after all arithmetic: a per-channel guard between loads and uses would let the
+  // compiler sink each load into its guarded block (one load latency per channel)
+  if (cw + kWaveCh <= C) {
+#pragma unroll
+    for (int cc = 0; cc < kWaveCh; ++cc) PxN<T, PX>::store(out + ((long long)b * C + cw + cc) * hw + t.p, y[cc]);
+  } else {
+#pragma unroll
+    for (int cc = 0; cc < kWaveCh; ++cc)
+      if (cw + cc < C) PxN<T, PX>::store(out + ((long long)b * C + cw + cc) * hw + t.p, y[cc]);
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_dggm_fuse_bwd_partial(const T* __restrict__ dout,
+template <typename T, int PX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_dggm_fuse_bwd_partial(const T* __restrict__ dout,
                                                                const float* __restrict__ grad,
                                                                const float* __restrict__ mask,
-                                                               long long pvs, int B, int H, int W,
-                                                               int C, int h, int w,
-                                                               const float* __restrict__ wt,
+                                                               long long pvs, int H, int W, int C, int h,
+                                                               int w, const float* __restrict__ wt,
                                                                const float* __restrict__ bias,
                                                                float* __restrict__ partial) {
-  // partial[tile][c][4] = sum over the tile's pixels of dout*relu'(pre) * (1, g0, g1, g2).
-  // A "tile" is the pixel range [tile*ppt, (tile+1)*ppt): each thread accumulates its pixels in
-  // registers first, then one block reduction per channel (fixed order: deterministic).
-  __shared__ float red[4][kFuseCh][4];
-  const int hw = h * w;
-  const long long P = (long long)B * hw;
-  const long long ppt = ((P + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
-  const long long q0 = (long long)blockIdx.x * ppt;
-  const int c0 = blockIdx.y * kFuseCh;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float acc[kFuseCh][4];
+  // partial[tile][c][4] = sum over the tile's pixels of dout*relu'(pre) * (1, g0, g1, g2).  Each
+  // lane sums its PX pixels for the wave's 8 channels (32 values), then the wave sums the 64
+  // lanes' values through LDS in fixed order (deterministic).
+  __shared__ float sg[3][512];
+  __shared__ float4 swb[kBlkCh];
+  __shared__ __attribute__((aligned(16))) float sred[4][64 * kRedStride];
+  constexpr int TP = 64 * PX;
+  const int hw = h * w, tpi = (hw + TP - 1) / TP;
+  const int b = blockIdx.x / tpi, p0 = (blockIdx.x % tpi) * TP;
+  const TileGates<PX> t = stage_gates<PX>(sg, swb, grad + b * pvs, mask + b * pvs, H, W, h, w, p0, wt, bias, C);
+  const int lane = threadIdx.x & 63;
+  const int cw = blockIdx.y * kBlkCh + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kWaveCh;
+  if (cw >= C) return;
+  float d[kWaveCh][PX];
+  if (t.valid && !(dggm_dbg() & 2)) {
 #pragma unroll
-  for (int cc = 0; cc < kFuseCh; ++cc)
+    for (int cc = 0; cc < kWaveCh; ++cc) PxN<T, PX>::load(dout + ((long long)b * C + min(cw + cc, C - 1)) * hw + t.p, d[cc]);
+    __builtin_amdgcn_sched_barrier(0);  // keep the whole load batch ahead of the first use
+  } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[cc][j] = 0.f;
-  for (long long q = q0 + threadIdx.x; q < q0 + ppt && q < P; q += 256) {
-    const int b = (int)(q / hw), p = (int)(q % hw);
-    const Gate gt = gate_at(grad + b * pvs, mask + b * pvs, H, W, h, w, p / w, p % w);
+    for (int cc = 0; cc < kWaveCh; ++cc)
 #pragma unroll
-    for (int cc = 0; cc < kFuseCh; ++cc) {
-      const int c = c0 + cc;
-      if (c >= C) break;
-      const float pre = bias[c] + wt[c * 3 + 0] * gt.g[0] + wt[c * 3 + 1] * gt.g[1] + wt[c * 3 + 2] * gt.g[2];
-      const float d = pre > 0.f ? Num<T>::to_f(dout[((long long)b * C + c) * hw + p]) : 0.f;
-      acc[cc][0] += d;
-      acc[cc][1] += d * gt.g[0];
-      acc[cc][2] += d * gt.g[1];
-      acc[cc][3] += d * gt.g[2];
-    }
+      for (int j = 0; j < PX; ++j) d[cc][j] = 0.f;
   }
+  float v[4 * kWaveCh];
 #pragma unroll
-  for (int cc = 0; cc < kFuseCh; ++cc)
+  for (int cc = 0; cc < kWaveCh; ++cc) {
+    const int c = min(cw + cc, C - 1);
+    const float4 wb = swb[c - (int)blockIdx.y * kBlkCh];
+    const float w0 = wb.x, w1 = wb.y, w2 = wb.z, bc = wb.w;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float s = wave_sum(acc[cc][j]);
-      if (lane == 0) red[wave][cc][j] = s;
+    for (int j = 0; j < PX; ++j) {
+      const float pre = bc + w0 * t.g[0][j] + w1 * t.g[1][j] + w2 * t.g[2][j];
+      const float dj = pre > 0.f ? d[cc][j] : 0.f;
+      s0 += dj;
+      s1 += dj * t.g[0][j];
+      s2 += dj * t.g[1][j];
+      s3 += dj * t.g[2][j];
     }
-  __syncthreads();
-  if (threadIdx.x < kFuseCh * 4) {
-    const int cc = threadIdx.x >> 2, j = threadIdx.x & 3;
-    if (c0 + cc >= C) return;
-    const float s = ((red[0][cc][j] + red[1][cc][j]) + red[2][cc][j]) + red[3][cc][j];
-    partial[((long long)blockIdx.x * C + c0 + cc) * 4 + j] = s;
+    v[4 * cc + 0] = s0;
+    v[4 * cc + 1] = s1;
+    v[4 * cc + 2] = s2;
+    v[4 * cc + 3] = s3;
   }
+  // wave reduction through LDS: row = lane (32 sums, stride 36 floats), then lane (idx, half)
+  // adds rows half*32 .. half*32+31 of column idx; independent reads, fixed order
+  float* red = sred[threadIdx.x >> 6];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    *(float4*)&red[lane * kRedStride + 4 * q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int idx = lane & 31, half = lane >> 5;
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) s += red[(half * 32 + r) * kRedStride + idx];
+  s += __shfl_xor(s, 32);
+  const int c = cw + (idx >> 2);
+  if (lane < 32 && c < C) partial[((long long)blockIdx.x * C + c) * 4 + (idx & 3)] = s;
 }
 
 __global__ __launch_bounds__(256) void k_dggm_fuse_bwd_final(const float* __restrict__ partial, int ntiles, int C,
@@ -246,6 +398,52 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_bwd_final(const float* __rest
   else
     dw[c * 3 + (j - 1)] = red[0];
 }
+
+void dggm_dbg_init() {
+  static const bool once = [] {
+    const char* e = getenv("RGBD_DGGM_DBG");
+    const int v = e ? atoi(e) : 0;
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dggm_dbg), &v, sizeof(int));
+    return true;
+  }();
+  (void)once;
+}
+
+int dggm_px(int h, int w) {
+  const long long hw = (long long)h * w;
+  return hw % 8 == 0 ? 8 : (hw % 4 == 0 ? 4 : 1);
+}
+
+template <typename T, int PX>
+void launch_fwd(const void* cp1, const void* color, const float* grad, const float* mask, long long pvs,
+                       int B, int H, int W, int C, int h, int w, const float* wt, const float* bias, void* out,
+                       hipStream_t s) {
+  dim3 grid(B * ceil_div((long long)h * w, 64 * PX), ceil_div(C, kBlkCh));
+  if (cp1)
+    k_dggm_fuse_fwd<T, PX, true><<<grid, 256, 0, s>>>((const T*)cp1, (const T*)color, grad, mask, pvs, H, W, C, h, w,
+                                                      wt, bias, (T*)out);
+  else
+    k_dggm_fuse_fwd<T, PX, false><<<grid, 256, 0, s>>>(nullptr, (const T*)color, grad, mask, pvs, H, W, C, h, w, wt,
+                                                       bias, (T*)out);
+}
+
+template <typename T, int PX>
+void launch_bwd(const void* dout, const float* grad, const float* mask, long long pvs, int B, int H, int W,
+                       int C, int h, int w, const float* wt, const float* bias, float* partial, hipStream_t s) {
+  dim3 grid(B * ceil_div((long long)h * w, 64 * PX), ceil_div(C, kBlkCh));
+  k_dggm_fuse_bwd_partial<T, PX><<<grid, 256, 0, s>>>((const T*)dout, grad, mask, pvs, H, W, C, h, w, wt, bias,
+                                                       partial);
+}
+
+#define RGBD_DGGM_DISPATCH(FN, T, PX, ...) \
+  do {                                     \
+    if ((PX) == 8)                         \
+      FN<T, 8>(__VA_ARGS__);               \
+    else if ((PX) == 4)                    \
+      FN<T, 4>(__VA_ARGS__);               \
+    else                                   \
+      FN<T, 1>(__VA_ARGS__);               \
+  } while (0)
 
 }  // namespace
 
@@ -276,23 +474,24 @@ int rgbd_dggm_fuse_fwd(int dtype, const void* cp1, const void* color, const floa
                        void* stream) {
   RGBD_REQUIRE(color && grad && mask && weight && bias && out, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0 && h > 0 && w > 0, RGBD_E_ARG);
+  RGBD_REQUIRE((long long)h * w < (1ll << 31), RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(ceil_div((long long)h * w, 256), ceil_div(C, kFuseCh), B);
   TimerScope ts("dggm_fwd", s);
+  dggm_dbg_init();
+  const int px = dggm_px(h, w);
   if (dtype == RGBD_F32)
-    k_dggm_fuse_fwd<float><<<grid, 256, 0, s>>>((const float*)cp1, (const float*)color, grad, mask,
-                                                pv_batch_stride, H, W, C, h, w, weight, bias, (float*)out);
+    RGBD_DGGM_DISPATCH(launch_fwd, float, px, cp1, color, grad, mask, pv_batch_stride, B, H, W, C, h, w, weight,
+                       bias, out, s);
   else if (dtype == RGBD_BF16)
-    k_dggm_fuse_fwd<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)cp1, (const bf16_t*)color, grad, mask,
-                                                 pv_batch_stride, H, W, C, h, w, weight, bias,
-                                                 (bf16_t*)out);
+    RGBD_DGGM_DISPATCH(launch_fwd, bf16_t, px, cp1, color, grad, mask, pv_batch_stride, B, H, W, C, h, w, weight,
+                       bias, out, s);
   else
     return RGBD_E_DTYPE;
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
 
-static int dggm_bwd_tiles(int B, int h, int w) { return std::min(ceil_div((long long)B * h * w, 256), 64); }
+static int dggm_bwd_tiles(int B, int h, int w) { return B * ceil_div((long long)h * w, 64 * dggm_px(h, w)); }
 
 size_t rgbd_dggm_fuse_bwd_workspace_size(int B, int C, int h, int w) {
   return align256(sizeof(float) * 4 * (size_t)C * dggm_bwd_tiles(B, h, w));
@@ -304,17 +503,18 @@ int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const flo
                        void* ws, void* stream) {
   RGBD_REQUIRE(dout && grad && mask && weight && bias && dweight && dbias && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0 && h > 0 && w > 0, RGBD_E_ARG);
+  RGBD_REQUIRE((long long)h * w < (1ll << 31), RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
   TimerScope ts("dggm_bwd", s);
-  const int ntiles = dggm_bwd_tiles(B, h, w);
-  dim3 grid(ntiles, ceil_div(C, kFuseCh));
+  dggm_dbg_init();
+  const int ntiles = dggm_bwd_tiles(B, h, w), px = dggm_px(h, w);
   float* partial = (float*)ws;
   if (dtype == RGBD_F32)
-    k_dggm_fuse_bwd_partial<float><<<grid, 256, 0, s>>>((const float*)dout, grad, mask, pv_batch_stride,
-                                                        B, H, W, C, h, w, weight, bias, partial);
+    RGBD_DGGM_DISPATCH(launch_bwd, float, px, dout, grad, mask, pv_batch_stride, B, H, W, C, h, w, weight, bias,
+                       partial, s);
   else if (dtype == RGBD_BF16)
-    k_dggm_fuse_bwd_partial<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)dout, grad, mask, pv_batch_stride,
-                                                         B, H, W, C, h, w, weight, bias, partial);
+    RGBD_DGGM_DISPATCH(launch_bwd, bf16_t, px, dout, grad, mask, pv_batch_stride, B, H, W, C, h, w, weight, bias,
+                       partial, s);
   else
     return RGBD_E_DTYPE;
   k_dggm_fuse_bwd_final<<<C * 4, 256, 0, s>>>(partial, ntiles, C, dweight, dbias);

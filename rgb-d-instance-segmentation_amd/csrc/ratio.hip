@@ -1156,51 +1156,126 @@ __global__ void k_rp_pool_finish(const float* __restrict__ part, int B, int H, i
   pooled[e] = s / (float)cnt;
 }
 
-__global__ __launch_bounds__(512) void k_rp_tail_conv(const float* __restrict__ pooled, int B,
+// Tail conv 256->512 (3x3 pad 1 on the 4x4 pooled map) as K-split partial sums: workgroup =
+// (32 output channels, 16 input channels); the filter slice [16 c][9 tap][32 o] and a zero-padded
+// 6x6 copy of 8 images' pooled planes sit in LDS; thread = 4 outputs x one 4-pixel row of one
+// image (4x4 register tile).  zpart[chunk][b][o][16]; the sum over the 16 chunks (fixed order)
+// happens in k_rp_tail_bn.
+constexpr int TC_O = 32, TC_C = 16, TC_IMG = 8, TC_CHUNKS = C5 / TC_C;
+
+__global__ __launch_bounds__(256) void k_rp_tail_conv(const float* __restrict__ pooled, int B,
                                                       const char* __restrict__ blob, Layout L,
-                                                      float* __restrict__ z6) {
-  // z6[b][512][16] = conv3x3 pad1 (pooled 4x4) + b6.  grid.x = 512/8 output-channel groups;
-  // thread = ((b, pos) pair, input-channel quarter); the 4 quarters are summed in fixed order.
-  __shared__ float red[4][128][8];
+                                                      float* __restrict__ zpart) {
+  __shared__ float sw[TC_C * 9 * TC_O];
+  __shared__ float sp[TC_C * TC_IMG * 36];
   const float* w6 = (const float*)(blob + L.w6);
-  const float* b6 = (const float*)(blob + L.b6);
-  const int o0 = blockIdx.x * 8;
-  const int kq = threadIdx.x >> 7, lbp = threadIdx.x & 127;
-  for (int base = 0; base < B * 16; base += 128) {
-    const int bp = base + lbp;
-    float acc[8];
+  const int o0 = blockIdx.x * TC_O, c0 = blockIdx.y * TC_C;
+  for (int i = threadIdx.x; i < TC_O * TC_C * 9; i += 256) {
+    const int ol = i / (TC_C * 9), r = i % (TC_C * 9);  // r = cl * 9 + tap: contiguous per o
+    sw[r * TC_O + ol] = w6[((long long)(o0 + ol) * C5 + c0) * 9 + r];
+  }
+  const int og = threadIdx.x >> 5, im = (threadIdx.x & 31) >> 2, py = threadIdx.x & 3;
+  for (int b0 = 0; b0 < B; b0 += TC_IMG) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < TC_C * TC_IMG * 36; i += 256) {
+      const int cl = i / (TC_IMG * 36), r = i % (TC_IMG * 36), j = r / 36, q = r % 36;
+      const int yy = q / 6 - 1, xx = q % 6 - 1, b = b0 + j;
+      float v = 0.f;
+      if (b < B && yy >= 0 && yy < 4 && xx >= 0 && xx < 4) v = pooled[((long long)b * C5 + c0 + cl) * 16 + yy * 4 + xx];
+      sp[i] = v;
+    }
+    __syncthreads();
+    float acc[4][4];
 #pragma unroll
-    for (int o = 0; o < 8; ++o) acc[o] = 0.f;
-    if (bp < B * 16) {
-      const int bb = bp / 16, pos = bp % 16, py = pos / 4, px = pos % 4;
-      for (int c = kq * 64; c < kq * 64 + 64; ++c) {
-        const float* pin = pooled + ((long long)bb * C5 + c) * 16;
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const int yy = py + ky - 1;
-          if (yy < 0 || yy >= 4) continue;
+      for (int x = 0; x < 4; ++x) acc[a][x] = 0.f;
+#pragma unroll 2
+    for (int cl = 0; cl < TC_C; ++cl) {
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int xx = px + kx - 1;
-            if (xx < 0 || xx >= 4) continue;
-            const float v = pin[yy * 4 + xx];
+      for (int ky = 0; ky < 3; ++ky) {
+        const float* row = &sp[(cl * TC_IMG + im) * 36 + (py + ky) * 6];
+        float r[6];
 #pragma unroll
-            for (int o = 0; o < 8; ++o) acc[o] += w6[(((long long)(o0 + o) * C5 + c) * 3 + ky) * 3 + kx] * v;
+        for (int x = 0; x < 6; ++x) r[x] = row[x];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float4 wv = *(const float4*)&sw[(cl * 9 + ky * 3 + kx) * TC_O + 4 * og];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            acc[0][x] += wv.x * r[x + kx];
+            acc[1][x] += wv.y * r[x + kx];
+            acc[2][x] += wv.z * r[x + kx];
+            acc[3][x] += wv.w * r[x + kx];
           }
         }
       }
     }
+    const int b = b0 + im;
+    if (b < B) {
 #pragma unroll
-    for (int o = 0; o < 8; ++o) red[kq][lbp][o] = acc[o];
-    __syncthreads();
-    if (kq == 0 && bp < B * 16) {
-      const int bb = bp / 16, pos = bp % 16;
-#pragma unroll
-      for (int o = 0; o < 8; ++o)
-        z6[((long long)bb * C6 + o0 + o) * 16 + pos] =
-            b6[o0 + o] + (((red[0][lbp][o] + red[1][lbp][o]) + red[2][lbp][o]) + red[3][lbp][o]);
+      for (int a = 0; a < 4; ++a)
+        *(float4*)&zpart[(((long long)blockIdx.y * B + b) * C6 + o0 + 4 * og + a) * 16 + py * 4] =
+            make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
     }
-    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// z6 = b6 + sum of the conv partials; BN(512) with batch statistics (train: running stats
+// updated, unbiased variance) or running statistics; ReLU; AdaptiveAvgPool2d(1).  One wave per
+// channel, lane = (b, pos) pairs strided by 64.
+__global__ __launch_bounds__(256) void k_rp_tail_bn(const float* __restrict__ zpart, int B, int training,
+                                                    float momentum, const char* __restrict__ blob, Layout L,
+                                                    BnPtrs bn, float* __restrict__ feat) {
+  const int lane = threadIdx.x & 63, c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const float bc = ((const float*)(blob + L.b6))[c];
+  const int n = B * 16;
+  auto zval = [&](int bp) {
+    const int b = bp >> 4, pos = bp & 15;
+    float z = bc;
+    for (int k = 0; k < TC_CHUNKS; ++k) z += zpart[(((long long)k * B + b) * C6 + c) * 16 + pos];
+    return z;
+  };
+  float mean, var;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int bp = lane; bp < n; bp += 64) {
+      const double v = zval(bp);
+      s += v;
+      q += v * v;
+    }
+    s = wave_sum_d(s);
+    q = wave_sum_d(q);
+    const double nn = (double)n, m = s / nn;
+    double v = q / nn - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    if (lane == 0) {
+      float* rm = bn.p[5 * 4 + 2];
+      float* rv = bn.p[5 * 4 + 3];
+      const double unb = nn > 1.0 ? v * nn / (nn - 1.0) : v;
+      rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
+      rv[c] = (1.f - momentum) * rv[c] + momentum * (float)unb;
+    }
+  } else {
+    mean = bn.p[5 * 4 + 2][c];
+    var = bn.p[5 * 4 + 3][c];
+  }
+  const float sc = bn.p[5 * 4 + 0][c] / sqrtf(var + BN_EPS), sh = bn.p[5 * 4 + 1][c] - mean * sc;
+  for (int base = 0; base < n; base += 64) {  // n is a multiple of 16: 16-lane groups are whole images
+    const int bp = base + lane;
+    float r = bp < n ? fmaxf(zval(bp) * sc + sh, 0.f) : 0.f;
+    r += __shfl_xor(r, 8);
+    r += __shfl_xor(r, 4);
+    r += __shfl_xor(r, 2);
+    r += __shfl_xor(r, 1);
+    if (bp < n && (lane & 15) == 0) feat[(long long)(bp >> 4) * C6 + c] = r / 16.f;
   }
 }
 
@@ -1212,69 +1287,52 @@ __device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned 
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
 
-// BN(512, batch or running stats) + ReLU + GAP + MLP + sigmoid; one workgroup
-__global__ __launch_bounds__(512) void k_rp_tail_mlp(const float* __restrict__ z6, int B, int training,
-                                                     float momentum, const char* __restrict__ blob, Layout L,
-                                                     BnPtrs bn, unsigned long long seed,
-                                                     float* __restrict__ ratio) {
-  __shared__ float feat[32][C6];
-  __shared__ float h1[32][128], h2[32][64], h3[32][32];
-  const int c = threadIdx.x;  // 512 threads = channels
-  {
-    float* gamma = bn.p[5 * 4 + 0];
-    float* beta = bn.p[5 * 4 + 1];
-    float* rm = bn.p[5 * 4 + 2];
-    float* rv = bn.p[5 * 4 + 3];
-    float mean, var;
-    if (training) {
-      double s = 0.0, q = 0.0;
-      for (int bb = 0; bb < B; ++bb)
-        for (int p = 0; p < 16; ++p) {
-          const double v = z6[((long long)bb * C6 + c) * 16 + p];
-          s += v;
-          q += v * v;
-        }
-      const double n = 16.0 * B, m = s / n;
-      double v = q / n - m * m;
-      if (v < 0.0) v = 0.0;
-      mean = (float)m;
-      var = (float)v;
-      const double unb = n > 1.0 ? v * n / (n - 1.0) : v;
-      rm[c] = (1.f - momentum) * rm[c] + momentum * mean;
-      rv[c] = (1.f - momentum) * rv[c] + momentum * (float)unb;
-    } else {
-      mean = rm[c];
-      var = rv[c];
-    }
-    const float sc = gamma[c] / sqrtf(var + BN_EPS), sh = beta[c] - mean * sc;
-    for (int bb = 0; bb < B; ++bb) {
-      float s = 0.f;
-      for (int p = 0; p < 16; ++p) s += fmaxf(z6[((long long)bb * C6 + c) * 16 + p] * sc + sh, 0.f);
-      feat[bb][c] = s / 16.f;  // AdaptiveAvgPool2d(1)
-    }
+// Linear 512 -> 128 + ReLU + Dropout(0.3): one workgroup per output o, thread = 2 k's for all
+// images, fixed-order block reduction per image.
+__global__ __launch_bounds__(256) void k_rp_tail_fc1(const float* __restrict__ feat, int B, int training,
+                                                     const char* __restrict__ blob, Layout L,
+                                                     unsigned long long seed, float* __restrict__ h1) {
+  __shared__ float red[4][32];
+  const int o = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const float* w7 = (const float*)(blob + L.w7);
+  const float wa = w7[o * 512 + t], wb = w7[o * 512 + t + 256];
+  for (int b = 0; b < B; ++b) {
+    float s = wa * feat[(long long)b * C6 + t] + wb * feat[(long long)b * C6 + t + 256];
+    s = wave_sum(s);
+    if (lane == 0) red[wv][b] = s;
   }
   __syncthreads();
-  const float* w7 = (const float*)(blob + L.w7);
-  const float* b7 = (const float*)(blob + L.b7);
+  if (t < B) {
+    const float* b7 = (const float*)(blob + L.b7);
+    float s = b7[o] + (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]);
+    s = fmaxf(s, 0.f);
+    const int e = t * 128 + o;
+    if (training) s = hash_uniform(seed, e) < 0.3f ? 0.f : s / 0.7f;  // Dropout(0.3)
+    h1[t * 128 + o] = s;
+  }
+}
+
+// Linear 128 -> 64 + ReLU + Dropout(0.2), Linear 64 -> 32 + ReLU, Linear 32 -> 1, sigmoid range
+// map; one workgroup, weights transposed into LDS (lanes walk output columns: conflict-free).
+__global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ h1g, int B, int training,
+                                                      const char* __restrict__ blob, Layout L,
+                                                      unsigned long long seed, float* __restrict__ ratio) {
+  __shared__ float w8t[128][64], w9t[64][32];
+  __shared__ float h1[32][128], h2[32][64], h3[32][32];
   const float* w8 = (const float*)(blob + L.w8);
   const float* b8 = (const float*)(blob + L.b8);
   const float* w9 = (const float*)(blob + L.w9);
   const float* b9 = (const float*)(blob + L.b9);
   const float* w10 = (const float*)(blob + L.w10);
   const float* b10 = (const float*)(blob + L.b10);
-  for (int e = threadIdx.x; e < B * 128; e += 512) {
-    const int bb = e / 128, o = e % 128;
-    float s = b7[o];
-    for (int k = 0; k < 512; ++k) s += w7[o * 512 + k] * feat[bb][k];
-    s = fmaxf(s, 0.f);
-    if (training) s = hash_uniform(seed, e) < 0.3f ? 0.f : s / 0.7f;  // Dropout(0.3)
-    h1[bb][o] = s;
-  }
+  for (int i = threadIdx.x; i < 64 * 128; i += 512) w8t[i % 128][i / 128] = w8[i];
+  for (int i = threadIdx.x; i < 32 * 64; i += 512) w9t[i % 64][i / 64] = w9[i];
+  for (int i = threadIdx.x; i < B * 128; i += 512) h1[i / 128][i % 128] = h1g[i];
   __syncthreads();
   for (int e = threadIdx.x; e < B * 64; e += 512) {
     const int bb = e / 64, o = e % 64;
     float s = b8[o];
-    for (int k = 0; k < 128; ++k) s += w8[o * 128 + k] * h1[bb][k];
+    for (int k = 0; k < 128; ++k) s += w8t[k][o] * h1[bb][k];
     s = fmaxf(s, 0.f);
     if (training) s = hash_uniform(seed ^ 0x5555ull, e) < 0.2f ? 0.f : s / 0.8f;  // Dropout(0.2)
     h2[bb][o] = s;
@@ -1283,7 +1341,7 @@ __global__ __launch_bounds__(512) void k_rp_tail_mlp(const float* __restrict__ z
   for (int e = threadIdx.x; e < B * 32; e += 512) {
     const int bb = e / 32, o = e % 32;
     float s = b9[o];
-    for (int k = 0; k < 64; ++k) s += w9[o * 64 + k] * h2[bb][k];
+    for (int k = 0; k < 64; ++k) s += w9t[k][o] * h2[bb][k];
     h3[bb][o] = fmaxf(s, 0.f);
   }
   __syncthreads();
@@ -1296,7 +1354,7 @@ __global__ __launch_bounds__(512) void k_rp_tail_mlp(const float* __restrict__ z
 }
 
 struct Ws {  // workspace carve
-  size_t aff1, aff2, aff5, slab, att, y, part, pooled, z6, total;
+  size_t aff1, aff2, aff5, slab, att, y, part, pooled, zpart, feat, h1, total;
 };
 
 inline int chain_grid(int B, int H, int W) {
@@ -1346,7 +1404,9 @@ inline Ws make_ws(int es, int B, int H, int W) {
   w.y = seg(es == 2 ? (size_t)conv3_tiles(B, H, W) * C3_TH * C3_TW * C5 * 2 : P * C5 * es);
   w.part = seg((size_t)B * 16 * POOL_SPLIT * C5 * sizeof(float));
   w.pooled = seg((size_t)B * C5 * 16 * sizeof(float));
-  w.z6 = seg((size_t)B * C6 * 16 * sizeof(float));
+  w.zpart = seg((size_t)TC_CHUNKS * B * C6 * 16 * sizeof(float));
+  w.feat = seg((size_t)B * C6 * sizeof(float));
+  w.h1 = seg((size_t)B * 128 * sizeof(float));
   w.total = o;
   return w;
 }
@@ -1365,7 +1425,9 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   T* y = (T*)(ws + w.y);
   float* part = (float*)(ws + w.part);
   float* pooled = (float*)(ws + w.pooled);
-  float* z6 = (float*)(ws + w.z6);
+  float* zpart = (float*)(ws + w.zpart);
+  float* feat = (float*)(ws + w.feat);
+  float* h1 = (float*)(ws + w.h1);
   const double P = (double)B * H * W;
   const bool v2 = sizeof(T) == 2;
   const int gch = v2 ? chain_grid_v2(B, H, W) : chain_grid(B, H, W);
@@ -1421,8 +1483,10 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   else
     k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
   k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
-  k_rp_tail_conv<<<C6 / 8, 512, 0, s>>>(pooled, B, blob, L, z6);
-  k_rp_tail_mlp<<<1, 512, 0, s>>>(z6, B, training, momentum, blob, L, bn, seed, ratio);
+  k_rp_tail_conv<<<dim3(C6 / TC_O, TC_CHUNKS), 256, 0, s>>>(pooled, B, blob, L, zpart);
+  k_rp_tail_bn<<<C6 / 4, 256, 0, s>>>(zpart, B, training, momentum, blob, L, bn, feat);
+  k_rp_tail_fc1<<<128, 256, 0, s>>>(feat, B, training, blob, L, seed, h1);
+  k_rp_tail_head<<<1, 512, 0, s>>>(h1, B, training, blob, L, seed, ratio);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -1460,7 +1524,7 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
                        float* ratio, void* ws, void* stream) {
   RGBD_REQUIRE(depth3 && packed && bn_host && ratio && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
-  RGBD_REQUIRE(B <= 32, RGBD_E_SHAPE);  // one workgroup runs the batch-wide tail (BN over B*16)
+  RGBD_REQUIRE(B <= 32, RGBD_E_SHAPE);  // k_rp_tail_fc1 / k_rp_tail_head hold the batch in LDS
   BnPtrs bn;
   for (int i = 0; i < RGBD_RATIO_NBN * 4; ++i) {
     RGBD_REQUIRE(bn_host[i], RGBD_E_ARG);
