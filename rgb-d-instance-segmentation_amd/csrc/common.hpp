@@ -32,6 +32,14 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 
+// Two floats -> packed bf16x2 (low = a) with one v_cvt_pk_bf16_f32 (round-to-nearest-even).
+typedef float rgbd_f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 rgbd_b2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const rgbd_f2v f = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, rgbd_b2v));
+}
+
 template <typename T> struct Num;
 template <> struct Num<float> {
   static __device__ __forceinline__ float load(const float* p) { return *p; }

@@ -20,6 +20,9 @@
 // uses batch statistics (three recompute passes of the chain for the stem / fusion BNs,
 // deterministic fixed-order reductions in double) and updates running stats like torch
 // (momentum, unbiased variance).  Dropout uses a counter-hash RNG (train mode only).
+#include <cstdlib>
+#include <type_traits>
+
 #include "mfma.hpp"
 #include "timing.hpp"
 
@@ -214,6 +217,10 @@ constexpr int CH_TW = 16, CH_TH = 4;                    // tile: 4 rows x 16 col
 constexpr int PATCH_H = CH_TH + 6, PATCH_W = CH_TW + 6;  // 7x7 halo
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// bf16 path: v_exp_f32 + v_rcp_f32 (~1 ulp each; the result is rounded to bf16)
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
 
 template <typename T>
 __device__ __forceinline__ Frag<T> load_w(const T* base, int row, int K, int s, int g) {
@@ -445,22 +452,31 @@ __device__ __forceinline__ void reduce_scatter16(float (&v)[N], int r) {
 // 0/1) are reduced across the wave's 32 pixels and kept per lane in registers, then written
 // as one slab row per wave: deterministic.
 constexpr int C2W_TH = 8, C2W_TW = 32, C2W_PH = C2W_TH + 6, C2W_PW = C2W_TW + 6;
-// LDS weight rows padded by 16 bytes: row strides of 336/400/272/144 B put the 16 rows a
-// ds_read_b128 lane group touches on distinct banks (unpadded 256-B rows are 16-way).
+// LDS weight rows padded by 16 bytes: W1's 352-B rows are conflict-free for the ds_read_b128
+// lane groups; W2/W3/W4 (400/272/144 B) are 2-way (conflict-free strides or chunk swizzles do
+// not fit the LDS budget / cost more in per-lane offsets and spills than they save, measured).
 constexpr int C2W_S1 = STEM_K2 + 8, C2W_S2 = STEM_C + 8, C2W_S3 = FUS_C + 8, C2W_S4 = ATT_C + 8;
 constexpr int C2W_PWP = 40;  // bf16 patch row: 38 pixels + 2 zero pad (a lane reads 5 words from col & ~1)
 constexpr size_t C2W_OFF_W1 = 0;
 constexpr size_t C2W_OFF_W2 = C2W_OFF_W1 + (size_t)STEM_C * C2W_S1 * 2;
 constexpr size_t C2W_OFF_W3 = C2W_OFF_W2 + (size_t)FUS_C * C2W_S2 * 2;
 constexpr size_t C2W_OFF_W4 = C2W_OFF_W3 + (size_t)ATT_C * C2W_S3 * 2;
-constexpr size_t C2W_OFF_B = C2W_OFF_W4 + (size_t)FUS_C * C2W_S4 * 2;             // b1 b2 b3 b4 (f32)
-constexpr size_t C2W_OFF_AFF = C2W_OFF_B + (size_t)(STEM_C + FUS_C + ATT_C + FUS_C) * 4;  // aff1, aff2
-constexpr size_t C2W_OFF_PATCH = C2W_OFF_AFF + (size_t)(STEM_C + FUS_C) * 8;  // bf16 [3][14][40]
-constexpr size_t C2W_SMEM = C2W_OFF_PATCH + (size_t)3 * C2W_PH * C2W_PWP * 2 + 16;
-static_assert(C2W_SMEM <= 163840, "chain v2 LDS budget");
+// Phase 0 (stem statistics) keeps only W1 resident: ~76 KB, two workgroups per CU.
+template <int PH> constexpr size_t c2w_off_b() {  // b1 b2 b3 b4 (f32)
+  return PH == 0 ? C2W_OFF_W2 : C2W_OFF_W4 + (size_t)FUS_C * C2W_S4 * 2;
+}
+template <int PH> constexpr size_t c2w_off_aff() {  // aff1, aff2
+  return c2w_off_b<PH>() + (size_t)(STEM_C + FUS_C + ATT_C + FUS_C) * 4;
+}
+template <int PH> constexpr size_t c2w_off_patch() {  // bf16 [3][14][40]
+  return c2w_off_aff<PH>() + (size_t)(STEM_C + FUS_C) * 8;
+}
+template <int PH> constexpr size_t c2w_smem() { return c2w_off_patch<PH>() + (size_t)3 * C2W_PH * C2W_PWP * 2 + 16; }
+static_assert(c2w_smem<1>() <= 163840, "chain v2 LDS budget");
+static_assert(2 * c2w_smem<0>() <= 163840, "chain v2 phase 0: two workgroups per CU");
 
 template <int PHASE>
-__global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ depth3, long long bstride, int B,
+__global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const float* __restrict__ depth3, long long bstride, int B,
                                                      int H, int W, const char* __restrict__ blob, Layout L,
                                                      const float2* __restrict__ aff1, const float2* __restrict__ aff2,
                                                      float* __restrict__ slab, bf16_t* __restrict__ att) {
@@ -469,20 +485,18 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
   const bf16_t* sW2 = (const bf16_t*)(smem + C2W_OFF_W2);
   const bf16_t* sW3 = (const bf16_t*)(smem + C2W_OFF_W3);
   const bf16_t* sW4 = (const bf16_t*)(smem + C2W_OFF_W4);
-  float* sb = (float*)(smem + C2W_OFF_B);
+  float* sb = (float*)(smem + c2w_off_b<PHASE>());
   float* sb1 = sb;
   float* sb2 = sb1 + STEM_C;
   float* sb3 = sb2 + FUS_C;
   float* sb4 = sb3 + ATT_C;
-  float2* saf1 = (float2*)(smem + C2W_OFF_AFF);
+  float2* saf1 = (float2*)(smem + c2w_off_aff<PHASE>());
   float2* saf2 = saf1 + STEM_C;
-  bf16_t* patch = (bf16_t*)(smem + C2W_OFF_PATCH);
+  bf16_t* patch = (bf16_t*)(smem + c2w_off_patch<PHASE>());
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   // ---- one-time LDS fill: weights, biases, BN affines, im2col table
   {
-    const size_t wbytes = C2W_OFF_B;  // W1..W4 are contiguous in the blob too? copy each
-    (void)wbytes;
     auto copy_rows = [&](size_t dst, size_t src, int rows, int k, int stride) {  // 16-byte pieces
       const int per = k / 8;
       for (int i = tid; i < rows * per; i += 512) {
@@ -492,9 +506,11 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
       }
     };
     copy_rows(C2W_OFF_W1, L.w1s, STEM_C, STEM_K2, C2W_S1);
-    copy_rows(C2W_OFF_W2, L.w2, FUS_C, STEM_C, C2W_S2);
-    copy_rows(C2W_OFF_W3, L.w3, ATT_C, FUS_C, C2W_S3);
-    copy_rows(C2W_OFF_W4, L.w4, FUS_C, ATT_C, C2W_S4);
+    if (PHASE >= 1) {
+      copy_rows(C2W_OFF_W2, L.w2, FUS_C, STEM_C, C2W_S2);
+      copy_rows(C2W_OFF_W3, L.w3, ATT_C, FUS_C, C2W_S3);
+      copy_rows(C2W_OFF_W4, L.w4, FUS_C, ATT_C, C2W_S4);
+    }
     for (int i = tid; i < STEM_C; i += 512) sb1[i] = ((const float*)(blob + L.b1))[i];
     for (int i = tid; i < FUS_C; i += 512) sb2[i] = ((const float*)(blob + L.b2))[i];
     for (int i = tid; i < ATT_C; i += 512) sb3[i] = ((const float*)(blob + L.b3))[i];
@@ -507,14 +523,15 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
     for (int i = tid; i < STEM_C * (C2W_S1 - STEM_K2); i += 512)  // W1 row pads: never garbage in an MFMA
       ((bf16_t*)(smem + C2W_OFF_W1))[(i / (C2W_S1 - STEM_K2)) * C2W_S1 + STEM_K2 + i % (C2W_S1 - STEM_K2)] = 0;
   }
-  // BN statistics (phases 0/1): per tile, each lane's (channel, {sum, sumsq}) values are
-  // reduce-scattered over the 16 pixel lanes (4 butterfly rounds), so a lane keeps only
-  // NV/16 running sums across tiles instead of NV.
+  // BN statistics (phases 0/1): the layer whose statistics the phase collects runs with its MFMA
+  // operands swapped, so its accumulator is [pixel][channel]: lane (r, g) owns channel 16t + r
+  // and the pixels {4g .. 4g+3} of each 16-px half.  Running sums stay per lane across tiles (no
+  // cross-lane traffic per tile) and the 4 lane groups are combined once, in fixed order, at
+  // the end.
   constexpr int NST = PHASE == 0 ? 12 : 8;  // channel tiles whose stats this phase collects
-  constexpr int NV = NST * 4 * 2, NKEEP = NV / 16;
-  float stat[NKEEP];
+  float ssum[NST], ssq[NST];
 #pragma unroll
-  for (int i = 0; i < NKEEP; ++i) stat[i] = 0.f;
+  for (int i = 0; i < NST; ++i) ssum[i] = ssq[i] = 0.f;
   const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
   const long long ntiles = (long long)B * tiles_x * tiles_y;
   const long long HW = (long long)H * W;
@@ -537,6 +554,18 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
       pre[k] = v;
     }
   };
+  // per-lane statistics of a transposed accumulator tile (pixel validity only on ragged tiles)
+  auto add_stats = [&](float& sm, float& sq, const f32x4 (&a)[2], bool full, int x0, bool row_ok) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = a[u][j];
+        if (!full) v = (row_ok && x0 + 16 * u + 4 * g + j < W) ? v : 0.f;
+        sm += v;
+        sq += v * v;
+      }
+  };
   fetch_patch(blockIdx.x);
   for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int b = (int)(tile / ((long long)tiles_x * tiles_y));
@@ -551,22 +580,15 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
     lds_barrier();
     fetch_patch(tile + gridDim.x);
     const int py = y0 + wave;
+    const bool row_ok = py < H;
+    const bool full = row_ok && x0 + C2W_TW <= W;  // wave-uniform
     bool pv[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) pv[u] = py < H && x0 + 16 * u + r < W;
-    // ---- stem: K = (c, dy, dx8) groups; lane (r, g) of step s takes group q = 4s + g, i.e.
-    // the 8 bf16 patch values (c, row wave+dy, cols 16u+r .. +7): five aligned words from
-    // col & ~1 and a byte-align by 2*(col & 1).  Zero K blocks of the 3x3 / 5x5 filters
-    // embedded in the 7x7 window are skipped (channel groups t < 4: steps {0,1,2,4};
-    // t < 8: steps 0..4; t >= 8: all six).
-    f32x4 a1[12][2];
-#pragma unroll
-    for (int t = 0; t < 12; ++t)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) a1[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      Frag<bf16_t> bfr[2];
+    for (int u = 0; u < 2; ++u) pv[u] = row_ok && x0 + 16 * u + r < W;
+    // ---- stem B operand: K = (c, dy, dx8) groups; lane (r, g) of step s takes group q = 4s + g,
+    // i.e. the 8 bf16 patch values (c, row wave+dy, cols 16u+r .. +7): five aligned words from
+    // col & ~1 and a byte-align by 2*(col & 1).
+    auto stem_b = [&](int s, Frag<bf16_t> (&bf)[2]) {
       const int q = 4 * s + g;
       const int cq = q / 7, dy = q - 7 * cq;
 #pragma unroll
@@ -576,45 +598,62 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
           const uint32_t* wp = reinterpret_cast<const uint32_t*>(patch + (cq * C2W_PH + wave + dy) * C2W_PWP + (col & ~1));
           const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3], w4 = wp[4];
           const uint32_t sh = (col & 1) * 2;
-          bfr[u].v = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+          bf[u].v = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
         } else {
-          bfr[u].zero();
+          bf[u].zero();
         }
       }
+    };
+    // Zero K blocks of the 3x3 / 5x5 filters embedded in the 7x7 window are skipped (channel
+    // groups t < 4 use steps {0,1,2,4}, t < 8 steps 0..4, t >= 8 all six); groups 21..23 of
+    // step 5 lie past the 168 packed columns.  Accumulators start at the bias.
+    auto stem_w = [&](int t, int s) {
+      Frag<bf16_t> af;
+      af.v = *reinterpret_cast<const uint4*>(sW1 + (16 * t + r) * C2W_S1 + 32 * s + 8 * g);
+      if (s == 5) af.select(g == 0);
+      return af;
+    };
+    auto stem_live = [](int t, int s) { return !((t < 4 && (s == 3 || s == 5)) || (t >= 4 && t < 8 && s == 5)); };
+    if constexpr (PHASE == 0) {
+      // statistics only: channel group outermost with the operands swapped (accumulator
+      // [pixel][channel]), all six B fragments built once, two accumulators live at a time
+      Frag<bf16_t> bfr[6][2];
+#pragma unroll
+      for (int s = 0; s < 6; ++s) stem_b(s, bfr[s]);
 #pragma unroll
       for (int t = 0; t < 12; ++t) {
-        if (t < 4 && (s == 3 || s == 5)) continue;
-        if (t >= 4 && t < 8 && s == 5) continue;
-        Frag<bf16_t> af;
-        af.v = *reinterpret_cast<const uint4*>(sW1 + (16 * t + r) * C2W_S1 + 32 * s + 8 * g);
-        if (s == 5) af.select(g == 0);  // groups 21..23 lie past the 168 packed columns
+        const float bb = sb1[16 * t + r];
+        f32x4 a1[2] = {f32x4{bb, bb, bb, bb}, f32x4{bb, bb, bb, bb}};
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+          if (!stem_live(t, s)) continue;
+          const Frag<bf16_t> af = stem_w(t, s);
+          mma(a1[0], bfr[s][0], af);
+          mma(a1[1], bfr[s][1], af);
+        }
+        add_stats(ssum[t], ssq[t], a1, full, x0, row_ok);
+      }
+      continue;
+    }
+    // phases 1, 2: K step outermost (one B fragment pair live), all 12 channel groups accumulate
+    f32x4 a1[12][2];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) {
+      const float4 bb = *reinterpret_cast<const float4*>(sb1 + 16 * t + 4 * g);
+      a1[t][0] = a1[t][1] = f32x4{bb.x, bb.y, bb.z, bb.w};
+    }
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      Frag<bf16_t> bfr[2];
+      stem_b(s, bfr);
+#pragma unroll
+      for (int t = 0; t < 12; ++t) {
+        if (!stem_live(t, s)) continue;
+        const Frag<bf16_t> af = stem_w(t, s);
         mma(a1[t][0], af, bfr[0]);
         mma(a1[t][1], af, bfr[1]);
       }
-    }
-#pragma unroll
-    for (int t = 0; t < 12; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float bb = sb1[16 * t + 4 * g + j];
-        a1[t][0][j] += bb;
-        a1[t][1][j] += bb;
-      }
-    if constexpr (PHASE == 0) {
-      float v[NV];
-#pragma unroll
-      for (int t = 0; t < 12; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v0 = pv[0] ? a1[t][0][j] : 0.f, v1 = pv[1] ? a1[t][1][j] : 0.f;
-          v[(t * 4 + j) * 2 + 0] = v0 + v1;
-          v[(t * 4 + j) * 2 + 1] = v0 * v0 + v1 * v1;
-        }
-      reduce_scatter16<NV>(v, r);
-#pragma unroll
-      for (int i = 0; i < NKEEP; ++i) stat[i] += v[i];
-      continue;
     }
     Frag<bf16_t> f1[6][2];
 #pragma unroll
@@ -630,38 +669,33 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
         }
         f1[s][u].from8(vv);
       }
-    // ---- fusion
+    // ---- fusion (phase 1: operands swapped for the statistics)
     f32x4 a2[8][2];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      a2[t][0] = a2[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (PHASE == 1) {
+        const float bb = sb2[16 * t + r];
+        a2[t][0] = a2[t][1] = f32x4{bb, bb, bb, bb};
+      } else {
+        const float4 bb = *reinterpret_cast<const float4*>(sb2 + 16 * t + 4 * g);
+        a2[t][0] = a2[t][1] = f32x4{bb.x, bb.y, bb.z, bb.w};
+      }
 #pragma unroll
       for (int s = 0; s < 6; ++s) {
         Frag<bf16_t> af;
         af.v = *reinterpret_cast<const uint4*>(sW2 + (16 * t + r) * C2W_S2 + 32 * s + 8 * g);
-        mma(a2[t][0], af, f1[s][0]);
-        mma(a2[t][1], af, f1[s][1]);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float bb = sb2[16 * t + 4 * g + j];
-        a2[t][0][j] += bb;
-        a2[t][1][j] += bb;
+        if constexpr (PHASE == 1) {
+          mma(a2[t][0], f1[s][0], af);
+          mma(a2[t][1], f1[s][1], af);
+        } else {
+          mma(a2[t][0], af, f1[s][0]);
+          mma(a2[t][1], af, f1[s][1]);
+        }
       }
     }
     if constexpr (PHASE == 1) {
-      float v[NV];
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v0 = pv[0] ? a2[t][0][j] : 0.f, v1 = pv[1] ? a2[t][1][j] : 0.f;
-          v[(t * 4 + j) * 2 + 0] = v0 + v1;
-          v[(t * 4 + j) * 2 + 1] = v0 * v0 + v1 * v1;
-        }
-      reduce_scatter16<NV>(v, r);
-#pragma unroll
-      for (int i = 0; i < NKEEP; ++i) stat[i] += v[i];
+      for (int t = 0; t < 8; ++t) add_stats(ssum[t], ssq[t], a2[t], full, x0, row_ok);
       continue;
     }
     if constexpr (PHASE == 2) {
@@ -686,19 +720,14 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
       f32x4 a3[4][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        a3[t][0] = a3[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float4 bb = *reinterpret_cast<const float4*>(sb3 + 16 * t + 4 * g);
+        a3[t][0] = a3[t][1] = f32x4{bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           Frag<bf16_t> af;
           af.v = *reinterpret_cast<const uint4*>(sW3 + (16 * t + r) * C2W_S3 + 32 * s + 8 * g);
           mma(a3[t][0], af, f2[s][0]);
           mma(a3[t][1], af, f2[s][1]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float bb = sb3[16 * t + 4 * g + j];
-          a3[t][0][j] = fmaxf(a3[t][0][j] + bb, 0.f);
-          a3[t][1][j] = fmaxf(a3[t][1][j] + bb, 0.f);
         }
       }
       Frag<bf16_t> f3[2][2];
@@ -708,12 +737,13 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
         for (int u = 0; u < 2; ++u) {
           float vv[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) vv[e] = a3[2 * s + (e >> 2)][u][e & 3];
+          for (int e = 0; e < 8; ++e) vv[e] = fmaxf(a3[2 * s + (e >> 2)][u][e & 3], 0.f);
           f3[s][u].from8(vv);
         }
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        f32x4 a4[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const float4 bb = *reinterpret_cast<const float4*>(sb4 + 16 * t + 4 * g);
+        f32x4 a4[2] = {f32x4{bb.x, bb.y, bb.z, bb.w}, f32x4{bb.x, bb.y, bb.z, bb.w}};
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           Frag<bf16_t> af;
@@ -724,32 +754,30 @@ __global__ __launch_bounds__(512) void k_rp_chain_v2(const float* __restrict__ d
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           if (!pv[u]) continue;
-          uint2 pk;
           float o[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int ch = 16 * t + 4 * g + j;
-            o[j] = a2[t][u][j] * sigmoidf_(a4[u][j] + sb4[ch]);
-          }
-          pk.x = (uint32_t)f32_to_bf16(o[0]) | ((uint32_t)f32_to_bf16(o[1]) << 16);
-          pk.y = (uint32_t)f32_to_bf16(o[2]) | ((uint32_t)f32_to_bf16(o[3]) << 16);
+          for (int j = 0; j < 4; ++j) o[j] = a2[t][u][j] * sigmoid_fast(a4[u][j]);
           *reinterpret_cast<uint2*>(att + ((long long)b * HW + (long long)py * W + x0 + 16 * u + r) * FUS_C + 16 * t +
-                                    4 * g) = pk;
+                                    4 * g) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
         }
       }
     }
   }
   if constexpr (PHASE < 2) {
-    // lane (r, g) holds original values [base, base + NKEEP) of the (t, j, q) ordering
+    // lanes r, r+16, r+32, r+48 hold channel 16t + r: combine in fixed order, one slab row per wave
     const long long row = (long long)blockIdx.x * 8 + wave;
     constexpr int NC = PHASE == 0 ? STEM_C : FUS_C;
-    const int base = ((r & 1) * (NV / 2)) + (((r >> 1) & 1) * (NV / 4)) + (((r >> 2) & 1) * (NV / 8)) +
-                     (((r >> 3) & 1) * (NV / 16));
 #pragma unroll
-    for (int i = 0; i < NKEEP; ++i) {
-      const int L = base + i, tj = L >> 1, q = L & 1;
-      const int ch = 16 * (tj >> 2) + 4 * g + (tj & 3);
-      slab[(row * NC + ch) * 2 + q] = stat[i];
+    for (int t = 0; t < NST; ++t) {
+      float a = ssum[t], q = ssq[t];
+      a += __shfl_xor(a, 16);
+      q += __shfl_xor(q, 16);
+      a += __shfl_xor(a, 32);
+      q += __shfl_xor(q, 32);
+      if (g == 0) {
+        slab[(row * NC + 16 * t + r) * 2 + 0] = a;
+        slab[(row * NC + 16 * t + r) * 2 + 1] = q;
+      }
     }
   }
 }
@@ -1361,9 +1389,10 @@ inline int chain_grid(int B, int H, int W) {
   const long long nt = (long long)B * ((W + CH_TW - 1) / CH_TW) * ((H + CH_TH - 1) / CH_TH);
   return (int)std::min<long long>(nt, 2048);
 }
-inline int chain_grid_v2(int B, int H, int W) {  // one 512-thread workgroup per CU (LDS-resident weights)
+// one 512-thread workgroup per CU (LDS-resident weights); phase 0 two
+inline int chain_grid_v2(int B, int H, int W, int phase = 1) {
   const long long nt = (long long)B * ((W + C2W_TW - 1) / C2W_TW) * ((H + C2W_TH - 1) / C2W_TH);
-  return (int)std::min<long long>(nt, 256);
+  return (int)std::min<long long>(nt, phase == 0 ? 512 : 256);
 }
 inline int conv_grid(int B, int H, int W) {
   const long long nt = (long long)B * ((W + CV_TW - 1) / CV_TW) * ((H + CV_TH - 1) / CV_TH);
@@ -1394,7 +1423,7 @@ inline Ws make_ws(int es, int B, int H, int W) {
     return r;
   };
   const size_t P = (size_t)B * H * W;
-  const int slab_rows = std::max(std::max(chain_grid(B, H, W), 8 * chain_grid_v2(B, H, W)),
+  const int slab_rows = std::max(std::max(chain_grid(B, H, W), 8 * chain_grid_v2(B, H, W, 0)),
                                  std::max(conv_grid(B, H, W), conv3_grid(B, H, W)));
   w.aff1 = seg(STEM_C * sizeof(float2));
   w.aff2 = seg(FUS_C * sizeof(float2));
@@ -1431,26 +1460,29 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   const double P = (double)B * H * W;
   const bool v2 = sizeof(T) == 2;
   const int gch = v2 ? chain_grid_v2(B, H, W) : chain_grid(B, H, W);
-  const int nslab_ch = v2 ? gch * 8 : gch;  // v2 writes one slab row per wave
+  const int gch0 = v2 ? chain_grid_v2(B, H, W, 0) : gch;
+  const int nslab_ch = v2 ? gch * 8 : gch;    // v2 writes one slab row per wave
+  const int nslab_ch0 = v2 ? gch0 * 8 : gch;  // phase 0 (stem statistics)
   if (v2) {
     static const hipError_t attr[3] = {
-        hipFuncSetAttribute((const void*)k_rp_chain_v2<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C2W_SMEM),
-        hipFuncSetAttribute((const void*)k_rp_chain_v2<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C2W_SMEM),
-        hipFuncSetAttribute((const void*)k_rp_chain_v2<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C2W_SMEM)};
+        hipFuncSetAttribute((const void*)k_rp_chain_v2<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c2w_smem<0>()),
+        hipFuncSetAttribute((const void*)k_rp_chain_v2<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c2w_smem<1>()),
+        hipFuncSetAttribute((const void*)k_rp_chain_v2<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c2w_smem<2>())};
     for (int i = 0; i < 3; ++i)
       if (attr[i] != hipSuccess) return (int)attr[i];
   }
 #define CHAIN_LAUNCH(PH, A1, A2, SL, OUT)                                                                          \
   do {                                                                                                            \
     if (v2)                                                                                                       \
-      k_rp_chain_v2<PH><<<gch, 512, C2W_SMEM, s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, (bf16_t*)(OUT)); \
+      k_rp_chain_v2<PH><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, \
+                                                                        (bf16_t*)(OUT));                          \
     else                                                                                                          \
       k_rp_chain<T, PH><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, (T*)(OUT));            \
   } while (0)
   // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
   if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
   for (int l = 0; l < 3; ++l)
-    k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
+    k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch0, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
                                  bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
   // fusion BN
   if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, nullptr);
