@@ -11,6 +11,6 @@ timeout -s KILL 60 rocprofv3 -L > "$R/gpurun_out/traffic/counters.txt" 2>&1 || t
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/traffic/p$i" -o run --output-format csv -- python3 "$R/tools/micro_dsam.py" --iters 2 > "$R/gpurun_out/traffic/p$i.log" 2>&1 || { echo "pmc pass $i ($grp) failed"; tail -5 "$R/gpurun_out/traffic/p$i.log"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/traffic/p$i" -o run --output-format csv -- python3 "$R/tools/micro_dsam.py" --iters 2 > "$R/gpurun_out/traffic/p$i.log" 2>&1 || { echo "pmc pass $i ($grp) failed"; tail -5 "$R/gpurun_out/traffic/p$i.log"; exit 1; }
 done
 echo done
