@@ -114,7 +114,7 @@ int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H
  *   wbwd [Cin][5][9][Cout]  (dX: k = (seg, tap, co), taps NOT flipped; see csrc)
  * RGBD_BF16 (code-merged form, Cin and Cout multiples of 32): for each 4-bit region code k
  * the merged filter W_k = proj + sum_{i in k} conv_i, as contiguous per-(code, tap, 32-channel
- * chunk) tiles with the 16-byte chunks of each 64-byte row XOR-swizzled by (row >> 2) & 3,
+ * chunk) tiles with the 16-byte chunks of each 64-byte row XOR-swizzled by 2*((row >> 3) & 1),
  *   wfwd [16 k][9 tap][Cin/32][Cout][32],  wbwd [16 k][9 tap][Cout/32][Cin][32],
  * each followed by a 192x32-element tail pad;
  * only the codes whose bit is set in *code_mask (a device uint32, e.g. from
@@ -142,15 +142,18 @@ int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd
                   const void* residual, void* out_nchw, void* out_nhwc, void* ws, void* stream);
 /* dX of one DSAModule, plus the upstream gradient of its input's other consumer:
  *   dx = gin + sum_i m_i * ConvT_i(gout) + ConvT_proj(gout)
- * gout_nhwc: dtype [B][ho][wo][Cout]; gin_nchw: dtype [B][Cin][h][w];
- * dx_nchw (dtype [B][Cin][h][w]) and dx_nhwc (optional) are written. */
+ * gout_nhwc: dtype [B][ho][wo][Cout].  At least one of dx_nchw (dtype [B][Cin][h][w]) and
+ * dx_nhwc (dtype [B][h][w][Cin]) is written.  The optional gin comes in the layout of the pass
+ * that adds it: gin_nchw (dtype [B][Cin][h][w]) when dx_nchw is written, gin_nhwc (RGBD_BF16
+ * only, [B][h][w][Cin]) when only dx_nhwc is (the hot path's cascade: NHWC in, NHWC out). */
 int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
-                       int w, int Cout, const void* wbwd, const void* gin_nchw, void* dx_nchw,
-                       void* dx_nhwc, void* ws, void* stream);
+                       int w, int Cout, const void* wbwd, const void* gin_nchw, const void* gin_nhwc,
+                       void* dx_nchw, void* dx_nhwc, void* ws, void* stream);
 /* dW / db of one DSAModule: dconv_w float32 [4][Cout][Cin][3][3], dproj_w float32
  * [Cout][Cin][3][3], dbias float32 [4][Cout] (all OVERWRITTEN).  gout_nchw: dtype
- * [B][Cout][ho][wo]; gout_nhwc: the same gradient as [B][ho][wo][Cout] (required for
- * RGBD_BF16, ignored for RGBD_F32); x_nhwc as in the forward. */
+ * [B][Cout][ho][wo] (required for RGBD_F32; optional for RGBD_BF16, whose bias sums then read
+ * gout_nhwc); gout_nhwc: the same gradient as [B][ho][wo][Cout] (required for RGBD_BF16,
+ * ignored for RGBD_F32); x_nhwc as in the forward. */
 size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout);
 int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
                          const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h,

@@ -39,6 +39,7 @@ struct ConvArgs {
   const float* bias4;               // DSAM conv biases [4][N] (summed over i < n_masks[b])
   const rgbd_decomp_info* info;
   const void* residual;             // NCHW [B][N][Ho][Wo] added in the epilogue (optional)
+  const void* residual_nhwc;        // bf16 only: NHWC residual, used when out_nchw is null
   void* out_nchw;                   // optional
   void* out_nhwc;                   // optional
   int ksplit;                       // unused (1)
@@ -228,9 +229,17 @@ __global__ void k_pack_dsam(const float* __restrict__ conv_w, const float* __res
 //   wfwd [16 code][9 tap][Cin/32 chunk][Cout n][32 c]   (forward: rows n = output channels)
 //   wbwd [16 code][9 tap][Cout/32 chunk][Cin n][32 o]   (dX: rows n = input channels)
 // so the tile of one (code, tap, chunk) is contiguous (one linear LDS-DMA stream), with the four
-// 16-byte chunks of each 64-byte row stored XOR-swizzled by (n >> 2) & 3 (the LDS image the
-// MFMA fragment reads want).  A one-tile tail pad keeps an over-reading last N tile in bounds.
-__device__ __forceinline__ int pk_pos(int n, int c) { return ((((c >> 3) ^ (n >> 2)) & 3) << 3) | (c & 7); }
+// 16-byte chunks of each 64-byte row stored XOR-swizzled by lds_swz(n) (the LDS image the MFMA
+// fragment reads want).  A one-tile tail pad keeps an over-reading last N tile in bounds.
+//
+// lds_swz: 16-byte chunk g of 64-byte row n sits at slot g ^ lds_swz(n).  A fragment read has
+// lane (r, g) take chunk g of row base+r (base a multiple of 16); the slot is 4*(n%4) + chunk, and
+// with the XOR by 2 on rows 8..15 of every 16 the 16 lanes of each ds_read_b128 lane group
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...; MI355X_MICROARCH.md LDS table) hit 16 distinct
+// 4-bank slots: conflict-free.  (The earlier (n >> 2) & 3 was conflict-free only for 16
+// consecutive lanes, not for the hardware groups.)
+__host__ __device__ __forceinline__ int lds_swz(int n) { return ((n >> 3) & 1) << 1; }
+__device__ __forceinline__ int pk_pos(int n, int c) { return ((((c >> 3) ^ lds_swz(n)) & 3) << 3) | (c & 7); }
 
 __global__ __launch_bounds__(256) void k_pack_fwd_codes(const float* __restrict__ conv_w, const float* __restrict__ proj_w,
                                                         int Cin, int Cout, const uint32_t* __restrict__ code_mask,
@@ -313,6 +322,36 @@ __global__ __launch_bounds__(256) void k_nchw_to_nhwc(const T* __restrict__ src,
   for (int k = ty; k < 32; k += 8) {
     const int p = p0 + k, c = c0 + tx;
     if (c < C && p < HW) dst[((long long)b * HW + p) * C + c] = tile[tx][k];
+  }
+}
+
+// bf16 NCHW -> NHWC with 16-byte global accesses (HW % 8 == 0, C % 8 == 0): a workgroup moves a
+// 64-channel x 64-pixel tile; loads take 8 pixels of one channel, stores 8 channels of one pixel,
+// the transpose happens in the LDS writes ([pixel][channel] rows padded to 72 elements).
+__global__ __launch_bounds__(256) void k_nchw_to_nhwc_v8(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                         int C, int HW) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[64][72];
+  const int b = blockIdx.z, p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = threadIdx.x + 256 * k, cl = v >> 3, pl = (v & 7) * 8;  // channel, 8-pixel group
+    const int c = c0 + cl, p = p0 + pl;
+    uint4 u = make_uint4(0u, 0u, 0u, 0u);
+    if (c < C && p < HW) u = *reinterpret_cast<const uint4*>(src + ((long long)b * C + c) * HW + p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tile[pl + 2 * e][cl] = (bf16_t)(w[e] & 0xffffu);
+      tile[pl + 2 * e + 1][cl] = (bf16_t)(w[e] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = threadIdx.x + 256 * k, pl = v >> 3, cl = (v & 7) * 8;  // pixel, 8-channel group
+    const int p = p0 + pl, c = c0 + cl;
+    if (p < HW && c < C)
+      *reinterpret_cast<uint4*>(dst + ((long long)b * HW + p) * C + c) = *reinterpret_cast<const uint4*>(&tile[pl][cl]);
   }
 }
 
@@ -788,15 +827,54 @@ __global__ __launch_bounds__(256) void k_chan_sum(const T* __restrict__ g, int H
   if (threadIdx.x == 0) out[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-__global__ void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_decomp_info* info, int B,
-                                 int Cout, float* __restrict__ dbias) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // (i, o)
+// out[(split*B + b)*C + c] = sum over pixel range `split` of g[b][p][c], NHWC bf16 g: workgroup
+// (b, 64 channels, split), thread = channel pair x one of 8 pixel strides, fixed-order combine.
+constexpr int CS_SPLIT_MAX = 16;
+inline int chan_sum_splits(int HW) { return std::max(1, std::min(CS_SPLIT_MAX, HW / 256)); }
+__global__ __launch_bounds__(256) void k_chan_sum_nhwc(const bf16_t* __restrict__ g, int HW, int C,
+                                                       float* __restrict__ out) {
+  __shared__ float2 red[8][32];
+  const int b = blockIdx.x, cp = threadIdx.x & 31, sub = threadIdx.x >> 5, sp = blockIdx.z;
+  const int c = blockIdx.y * 64 + 2 * cp;
+  const int p0 = (int)((long long)sp * HW / gridDim.z), p1 = (int)((long long)(sp + 1) * HW / gridDim.z);
+  float2 acc = make_float2(0.f, 0.f);
+  if (c < C) {
+    const bf16_t* base = g + (long long)b * HW * C + c;
+#pragma unroll 4
+    for (int p = p0 + sub; p < p1; p += 8) {
+      const uint32_t u = *reinterpret_cast<const uint32_t*>(base + (long long)p * C);
+      acc.x += __uint_as_float(u << 16);
+      acc.y += __uint_as_float(u & 0xffff0000u);
+    }
+  }
+  red[sub][cp] = acc;
+  __syncthreads();
+  if (sub == 0 && c < C) {
+    float2 t = red[0][cp];
+    for (int q = 1; q < 8; ++q) {
+      t.x += red[q][cp].x;
+      t.y += red[q][cp].y;
+    }
+    float* o = out + ((long long)sp * gridDim.x + b) * C + c;
+    o[0] = t.x;
+    if (c + 1 < C) o[1] = t.y;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_decomp_info* info,
+                                                        int B, int Cout, int nsplit, float* __restrict__ dbias) {
+  // csum [nsplit][B][Cout] channel sums (per-pixel-range partials).  One wave per (i, o): lanes
+  // over (split, b) pairs, fixed-order wave tree: deterministic.
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;  // t = (i, o)
   if (t >= 4 * Cout) return;
   const int i = t / Cout, o = t % Cout;
   float s = 0.f;
-  for (int b = 0; b < B; ++b)
-    if (i < info[b].n_masks) s += csum[b * Cout + o];  // conv_layers[i] used only if i < len(masks)
-  dbias[t] = s;
+  for (int q = lane; q < nsplit * B; q += 64) {
+    const int b = q % B;
+    if (i < info[b].n_masks) s += csum[(long long)q * Cout + o];  // conv_layers[i] used only if i < len(masks)
+  }
+  s = wave_sum(s);
+  if (lane == 0) dbias[t] = s;
 }
 
 // ----------------------------------------------------------------------- bf16: code-merged
@@ -1071,7 +1149,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     aorg = e.x;
     aval = (uint32_t)e.y;
     afall = e.y == 0 ? 0 : (a.transposed ? e.x : e.x + a.Wi + 1);
-    achk = 8 * ((lane & 3) ^ ((R >> 2) & 3));
+    achk = 8 * ((lane & 3) ^ lds_swz(R));
   }
   uint32_t cval[4], clo[4], chi[4];
 #pragma unroll
@@ -1150,13 +1228,13 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int row = wm * 64 + 16 * mi + r;
-        fa[mi].v = *reinterpret_cast<const uint4*>(sa + kc * LD_A1 + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+        fa[mi].v = *reinterpret_cast<const uint4*>(sa + kc * LD_A1 + row * 64 + 16 * (g ^ lds_swz(row)));
         fa[mi].select((keep >> mi) & 1u);
       }
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj) {
         const int row = wn * 48 + 16 * nj + r;
-        fb[nj].v = *reinterpret_cast<const uint4*>(sa + Cfg::A + kc * LD_B1 + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+        fb[nj].v = *reinterpret_cast<const uint4*>(sa + Cfg::A + kc * LD_B1 + row * 64 + 16 * (g ^ lds_swz(row)));
       }
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
@@ -1213,6 +1291,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   // ---- epilogue (same contract as k_conv_igemm), staged through LDS in two 96-column halves:
   // pass 1 runs along pixels (NCHW residual loads and stores), pass 2 along channels (NHWC);
   // every thread's loads of a pass are independent and issued together.
+  if (a.dbg & 2) return;  // RGBD_DSAM_DBG=2: no epilogue (timing experiments only)
   float* et = (float*)smem;  // [96 n][LD_EPI_LD] f32
   const bf16_t* res = (const bf16_t*)a.residual;
   bf16_t* onchw = (bf16_t*)a.out_nchw;
@@ -1231,6 +1310,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
             et[((wn & 1) * 48 + 16 * nj + r) * LD_EPI_LD + wm * 64 + 16 * mi + 4 * g + reg] = acc[mi][nj][reg];
     __syncthreads();
     const int nh = n0 + half * HN;
+    if (onchw) {
     // pass 1: items (channel, 4 consecutive tile rows = 4 consecutive pixels of one tile row);
     // forward rows are contiguous in NCHW (8-byte residual loads / stores), dX rows are not
     constexpr int NQ = HN * LD_BM / 4 / 512;  // 6 items per thread
@@ -1284,18 +1364,37 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
         }
       }
     }
-    if (onhwc) {  // pass 2: items (tile row, 8 consecutive channels) -> one 16-byte store
+    }  // pass 1
+    if (onhwc) {
+      // pass 2: items (tile row, 8 consecutive channels) -> one 16-byte store.  Consecutive lanes
+      // take consecutive tile rows of the same 8 channels, so the LDS column reads are
+      // conflict-free.  Without pass 1 (no NCHW output: the bf16 dX of the hot path) the bias
+      // and the NHWC residual are added here, in pass 1's order: res + (acc + bias), rounded once.
       __syncthreads();
+      const bool fused = !onchw;
+      const bf16_t* rnhwc = (const bf16_t*)a.residual_nhwc;
       for (int it = tid; it < LD_BM * (HN / 8); it += 512) {
-        const int ml = it / (HN / 8), nl = (it % (HN / 8)) * 8, n = nh + nl;
+        const int ml = it % LD_BM, nl = (it / LD_BM) * 8, n = nh + nl;
         const int4 ro = rowout[ml];
         if (ro.x < 0 || n >= a.N) continue;
-        uint32_t w4[4];
+        float v[8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          w4[e] = (uint32_t)f32_to_bf16(et[(nl + 2 * e) * LD_EPI_LD + ml]) |
-                  ((uint32_t)f32_to_bf16(et[(nl + 2 * e + 1) * LD_EPI_LD + ml]) << 16);
-        *reinterpret_cast<uint4*>(onhwc + (long long)ro.y * a.N + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        for (int e = 0; e < 8; ++e) v[e] = et[(nl + e) * LD_EPI_LD + ml];
+        if (fused) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bsum[ro.z * LD_BN + half * HN + nl + e];
+          if (rnhwc) {
+            const uint4 u = *reinterpret_cast<const uint4*>(rnhwc + (long long)ro.y * a.N + n);
+            const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] = __uint_as_float(uw[e] << 16) + v[2 * e];
+              v[2 * e + 1] = __uint_as_float(uw[e] & 0xffff0000u) + v[2 * e + 1];
+            }
+          }
+        }
+        *reinterpret_cast<uint4*>(onhwc + (long long)ro.y * a.N + n) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
       }
     }
   }
@@ -1450,6 +1549,12 @@ const char* rgbd_version(void) { return "rgbd_hip 0.1.0 (gfx950)"; }
 int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H, int W, void* stream) {
   RGBD_REQUIRE(src && dst && B > 0 && C > 0 && H > 0 && W > 0, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_BF16 && ((long long)H * W) % 8 == 0 && C % 8 == 0) {
+    k_nchw_to_nhwc_v8<<<dim3(ceil_div((long long)H * W, 64), ceil_div(C, 64), B), 256, 0, s>>>(
+        (const bf16_t*)src, (bf16_t*)dst, C, H * W);
+    RGBD_CHECK_LAUNCH();
+    return RGBD_OK;
+  }
   dim3 grid(ceil_div((long long)H * W, 32), ceil_div(C, 32), B);
   if (dtype == RGBD_F32)
     k_nchw_to_nhwc<float><<<grid, 256, 0, s>>>((const float*)src, (float*)dst, C, H * W);
@@ -1561,14 +1666,18 @@ int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd
 }
 
 int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
-                       int w, int Cout, const void* wbwd, const void* gin_nchw, void* dx_nchw,
-                       void* dx_nhwc, void* ws, void* stream) {
+                       int w, int Cout, const void* wbwd, const void* gin_nchw, const void* gin_nhwc,
+                       void* dx_nchw, void* dx_nhwc, void* ws, void* stream) {
   RGBD_REQUIRE(gout_nhwc && code && wbwd && (dx_nchw || dx_nhwc), RGBD_E_ARG);
+  // the residual comes in the layout of the pass that adds it: NCHW with an NCHW output, NHWC
+  // (bf16 only) without one
+  RGBD_REQUIRE(!gin_nhwc || (dtype == RGBD_BF16 && !dx_nchw && !gin_nchw), RGBD_E_ARG);
+  RGBD_REQUIRE(!gin_nchw || dx_nchw, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
   RGBD_REQUIRE(Cout % 8 == 0, RGBD_E_SHAPE);
   ConvArgs a = dx_args(B, Cin, h, w, Cout);
   a.x = gout_nhwc; a.code = code; a.w = wbwd;
-  a.residual = gin_nchw; a.out_nchw = dx_nchw; a.out_nhwc = dx_nhwc;
+  a.residual = gin_nchw; a.residual_nhwc = gin_nhwc; a.out_nchw = dx_nchw; a.out_nhwc = dx_nhwc;
   a.partial = (float*)ws;
   RGBD_REQUIRE(ws || dtype != RGBD_BF16, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
@@ -1598,7 +1707,7 @@ static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   o.partial = off;
   off += align256(sizeof(float) * part);
   o.csum = off;
-  off += align256(sizeof(float) * (size_t)B * Cout);
+  off += align256(sizeof(float) * (size_t)CS_SPLIT_MAX * B * Cout);
   o.pres = off;
   off += align256(sizeof(uint16_t) * npres);
   o.gmask = off;
@@ -1623,7 +1732,8 @@ size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int
 int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
                          const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h, int w,
                          int Cout, float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream) {
-  RGBD_REQUIRE(gout_nchw && x_nhwc && code && info && dconv_w && dproj_w && dbias && ws, RGBD_E_ARG);
+  RGBD_REQUIRE((gout_nchw || dtype == RGBD_BF16) && x_nhwc && code && info && dconv_w && dproj_w && dbias && ws,
+               RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
   RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
@@ -1675,7 +1785,11 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
     const int grid = 256;  // persistent: one LDS-bound workgroup per CU
     const hipError_t e = P.fm == 6 ? launch_wg<6>(a, grid, s) : P.fm == 4 ? launch_wg<4>(a, grid, s) : launch_wg<2>(a, grid, s);
     if (e != hipSuccess) return (int)e;
-    k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
+    if (gout_nchw)
+      k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
+    else
+      k_chan_sum_nhwc<<<dim3(B, ceil_div(Cout, 64), chan_sum_splits(hwo)), 256, 0, s>>>((const bf16_t*)gout_nhwc, hwo,
+                                                                                       Cout, csum);
     const int csmem = 5 * 9 * Cin * (int)sizeof(float);
     static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
@@ -1685,7 +1799,8 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
   } else {
     return RGBD_E_DTYPE;
   }
-  k_dsam_bias_grad<<<ceil_div(4 * Cout, 256), 256, 0, s>>>(csum, info, B, Cout, dbias);
+  const int nsplit = (dtype == RGBD_BF16 && !gout_nchw) ? chan_sum_splits(hwo) : 1;
+  k_dsam_bias_grad<<<Cout, 256, 0, s>>>(csum, info, B, Cout, nsplit, dbias);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -95,12 +95,14 @@ class HotPathFunction(torch.autograd.Function):
         for k in range(4):
             dw, db = ops.dggm_fuse_bwd(G[k], pixel_values, dggm_p[2 * k], dggm_p[2 * k + 1])
             grads_dggm += [dw.reshape(dggm_p[2 * k].shape).to(dggm_p[2 * k].dtype), db.to(dggm_p[2 * k + 1].dtype)]
-        # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}
+        # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}.  bfloat16 keeps the cascade in
+        # NHWC (dX written NHWC only, its residual G[k] converted once; bias sums from NHWC).
+        bf16 = dtype == torch.bfloat16
         dcp = G[3]
         dcp_nhwc = ops.nchw_to_nhwc(dcp)
         grads_dsam = [None, None, None]
         for k in (2, 1, 0):
-            dconv, dproj, dbias = ops.dsam_bwd_weight(dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
+            dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
                                                       gout_nhwc=dcp_nhwc)
             gk = []
             for i in range(4):
@@ -108,8 +110,11 @@ class HotPathFunction(torch.autograd.Function):
             gk.append(dproj)
             grads_dsam[k] = gk
             if k > 0:
-                dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k],
-                                                  want_nhwc=(k > 1 or dtype == torch.bfloat16))
+                if bf16:
+                    dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], None, want_nhwc=True,
+                                                      want_nchw=False, gin_nhwc=ops.nchw_to_nhwc(G[k]))
+                else:
+                    dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k], want_nhwc=(k > 1))
         pgrads = grads_dsam[0] + grads_dsam[1] + grads_dsam[2] + grads_dggm
         return (None, None, None, None, None, None, None, *pgrads)
 

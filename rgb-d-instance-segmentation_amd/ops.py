@@ -238,40 +238,56 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     return out, out_nhwc
 
 
-def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False, cin=None):
-    """dX of one DSAM (+ gin).  The input channel count comes from ``cin``, ``gin_nchw`` or the
-    2-D float32 wbwd (the flat bfloat16 tiles do not carry it)."""
-    _need_cuda(gout_nhwc, code, wbwd, gin_nchw)
+def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False, cin=None, gin_nhwc=None, want_nchw=True):
+    """dX of one DSAM (+ gin).  The input channel count comes from ``cin``, ``gin_nchw`` /
+    ``gin_nhwc`` or the 2-D float32 wbwd (the flat bfloat16 tiles do not carry it).
+    ``want_nchw=False`` (bfloat16 only) writes the NHWC result alone, with the residual given as
+    ``gin_nhwc``: the hot path's cascade, which never needs dX in NCHW."""
+    _need_cuda(gout_nhwc, code, wbwd, gin_nchw, gin_nhwc)
     B, ho, wo, Co = gout_nhwc.shape
     if cin is not None:
         Ci = int(cin)
     elif gin_nchw is not None:
         Ci = gin_nchw.shape[1]
+    elif gin_nhwc is not None:
+        Ci = gin_nhwc.shape[-1]
     elif wbwd.dim() == 2:
         Ci = wbwd.shape[-2]
     else:
-        raise ValueError("dsam_bwd_data needs cin (or gin_nchw) with the flat bfloat16 filter tiles")
+        raise ValueError("dsam_bwd_data needs cin (or gin) with the flat bfloat16 filter tiles")
     _, h, w = code.shape
     if gin_nchw is not None and tuple(gin_nchw.shape) != (B, Ci, h, w):
         raise ValueError("gin shape mismatch")
-    dx = torch.empty((B, Ci, h, w), dtype=gout_nhwc.dtype, device=gout_nhwc.device)
+    if gin_nhwc is not None and (want_nchw or tuple(gin_nhwc.shape) != (B, h, w, Ci)):
+        raise ValueError("gin_nhwc goes with want_nchw=False and shape [B, h, w, Cin]")
+    if not want_nchw and not want_nhwc:
+        raise ValueError("dsam_bwd_data: nothing to write")
+    dx = torch.empty((B, Ci, h, w), dtype=gout_nhwc.dtype, device=gout_nhwc.device) if want_nchw else None
     dx_nhwc = torch.empty((B, h, w, Ci), dtype=gout_nhwc.dtype, device=gout_nhwc.device) if want_nhwc else None
     L = _lib.lib()
     dt = _dtype_code(gout_nhwc)
     ws = _workspace(gout_nhwc.device, L.rgbd_dsam_conv_workspace_size(dt, B, Ci, h, w, Co), "dsam_conv")
-    check(L.rgbd_dsam_bwd_data(dt, _p(gout_nhwc), _p(code), B, Ci, h, w, Co, _p(wbwd), _p(gin_nchw), _p(dx),
-                               _p(dx_nhwc), _p(ws), _stream(gout_nhwc.device)), "rgbd_dsam_bwd_data")
+    check(L.rgbd_dsam_bwd_data(dt, _p(gout_nhwc), _p(code), B, Ci, h, w, Co, _p(wbwd), _p(gin_nchw), _p(gin_nhwc),
+                               _p(dx), _p(dx_nhwc), _p(ws), _stream(gout_nhwc.device)), "rgbd_dsam_bwd_data")
     return dx, dx_nhwc
 
 
 def dsam_bwd_weight(gout_nchw, x_nhwc, code, info, gout_nhwc=None):
     """dW/db of one DSAM.  The bfloat16 path contracts the NHWC copy of the upstream gradient
-    (``gout_nhwc``; made here when not given); bias gradients use the NCHW one."""
+    (``gout_nhwc``; made here when not given); bias gradients use the NCHW one when given, else
+    (bfloat16) the NHWC one."""
     _need_cuda(gout_nchw, x_nhwc, code, info, gout_nhwc)
-    B, Co, ho, wo = gout_nchw.shape
+    if gout_nchw is None:
+        if gout_nhwc is None or gout_nhwc.dtype != torch.bfloat16:
+            raise ValueError("dsam_bwd_weight: gout_nchw is required unless a bfloat16 gout_nhwc is given")
+        B, ho, wo, Co = gout_nhwc.shape
+        ref = gout_nhwc
+    else:
+        B, Co, ho, wo = gout_nchw.shape
+        ref = gout_nchw
     _, h, w, Ci = x_nhwc.shape
-    dev = gout_nchw.device
-    dt = _dtype_code(gout_nchw)
+    dev = ref.device
+    dt = _dtype_code(ref)
     if dt == RGBD_BF16 and gout_nhwc is None:
         gout_nhwc = nchw_to_nhwc(gout_nchw)
     if gout_nhwc is not None and tuple(gout_nhwc.shape) != (B, ho, wo, Co):

@@ -110,3 +110,53 @@ def test_dsam_bf16_ragged_many_codes():
                        ("dproj_w", m.rgb_projection.weight.grad, proj_w.grad)]:
         mx, mean = _err(a, e)
         assert mx <= 2e-2 and mean <= 4e-3, f"{name}: max {mx:.3g} mean {mean:.3g}"
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_dsam_bf16_dx_nhwc_only_and_nhwc_bias_sums(k):
+    """The hot path's bf16 cascade writes dX in NHWC only, with the residual gradient given in
+    NHWC (rgbd_dsam_bwd_data with dx_nchw = NULL, gin_nhwc), and takes the DSAM bias sums from the
+    NHWC upstream gradient (rgbd_dsam_bwd_weight with gout_nchw = NULL).  Same arithmetic and
+    rounding order as the NCHW path: dX bit-exact; bias sums differ only by float summation
+    order (rel 1e-5)."""
+    from rgbd_amd.modules import DSAModule
+    cin, cout = [(96, 192), (192, 384), (384, 768)][k]
+    B, H, W = 8, 480, 640
+    h, w = [(120, 160), (60, 80), (30, 40)][k]
+    m = DSAModule(cin, cout)
+    winit.init_deterministic(m, prefix=f"nhwc.dsam{k}.")
+    planes, _, _ = synthetic.make_batch(5, B, H, W)
+    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
+    codes, info = ops.edsam_decompose(d3, torch.linspace(0.05, 0.45, B, device=DEV), [(h, w)])
+    masks = ops.dsam_code_masks(codes)
+    conv_w = torch.stack([m.conv_layers[i].weight.detach() for i in range(4)]).to(DEV)
+    proj_w = m.rgb_projection.weight.detach().to(DEV)
+    _, wb = ops.dsam_pack(conv_w, proj_w, torch.bfloat16, code_mask=masks[0:1])
+    g = torch.Generator(device=DEV)
+    g.manual_seed(300 + k)
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    gy = (torch.randn((B, ho, wo, cout), generator=g, device=DEV) * 0.1).bfloat16()
+    gin = (torch.randn((B, cin, h, w), generator=g, device=DEV) * 0.1).bfloat16()
+    dx_ref, dx_ref_nhwc = ops.dsam_bwd_data(gy, codes[0], wb, gin, want_nhwc=True)
+    none, dx_nhwc = ops.dsam_bwd_data(gy, codes[0], wb, None, want_nhwc=True, want_nchw=False, cin=cin,
+                                      gin_nhwc=ops.nchw_to_nhwc(gin))
+    assert none is None
+    assert torch.equal(dx_nhwc, dx_ref_nhwc)
+    assert torch.equal(dx_nhwc, dx_ref.permute(0, 2, 3, 1))
+    x = torch.randn((B, h, w, cin), generator=g, device=DEV).bfloat16()
+    gy_nchw = gy.permute(0, 3, 1, 2).contiguous()
+    a = ops.dsam_bwd_weight(gy_nchw, x, codes[0], info, gout_nhwc=gy)
+    b = ops.dsam_bwd_weight(None, x, codes[0], info, gout_nhwc=gy)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    torch.testing.assert_close(b[2], a[2], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(2, 96, 120, 160), (3, 40, 7, 8), (2, 768, 15, 20), (1, 12, 5, 5)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_nchw_to_nhwc_exact(shape, dtype):
+    """rgbd_nchw_to_nhwc: the 16-byte bf16 path (h*w and C multiples of 8, ragged 64x64 tiles)
+    and the element-wise fallback are exact copies."""
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    x = torch.randn(shape, generator=g, device=DEV).to(dtype)
+    assert torch.equal(ops.nchw_to_nhwc(x), x.permute(0, 2, 3, 1).contiguous())

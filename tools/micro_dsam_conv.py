@@ -32,6 +32,9 @@ for k, (ci, co) in enumerate([(96, 192), (192, 384), (384, 768)]):
     fns = {f"fwd{k}": lambda: ops.dsam_fwd(x, codes[k], info, wf, b4, residual=resid, want_nhwc=(k < 2))}
     if k > 0:
         fns[f"dx{k}"] = lambda: ops.dsam_bwd_data(gy, codes[k], wb, gin, want_nhwc=True)
+        gin_nhwc = ops.nchw_to_nhwc(gin)
+        fns[f"dxh{k}"] = lambda: ops.dsam_bwd_data(gy, codes[k], wb, None, want_nhwc=True, want_nchw=False, cin=ci,
+                                                   gin_nhwc=gin_nhwc)
     for name, fn in fns.items():
         for _ in range(3):
             fn()
