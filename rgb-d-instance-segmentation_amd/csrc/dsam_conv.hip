@@ -247,6 +247,8 @@ __global__ __launch_bounds__(256) void k_pack_fwd_codes(const float* __restrict_
   extern __shared__ float srow[];  // [5][Cin*9] OIHW rows of output channel o: conv_0..3, proj
   const int o = blockIdx.x, KK = 9 * Cin, nch = Cin / 32;
   const uint32_t m = code_mask ? *code_mask : 0xffffu;
+  if (o == 0)  // tail pad (read only by an over-reaching last N tile, whose outputs are dropped)
+    for (int i = threadIdx.x; i < 192 * 32; i += 256) wfwd[144ll * Cin * Cout + i] = 0;
   for (int e = threadIdx.x; e < KK; e += 256) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) srow[i * KK + e] = conv_w[((long long)i * Cout + o) * KK + e];
@@ -281,6 +283,8 @@ __global__ __launch_bounds__(256) void k_pack_bwd_codes(const bf16_t* __restrict
   __shared__ bf16_t tile[32][34];
   const int k = blockIdx.z / 9, tap = blockIdx.z % 9;
   const uint32_t m = code_mask ? *code_mask : 0xffffu;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)  // tail pad
+    for (int i = threadIdx.x; i < 192 * 32; i += 256) wbwd[144ll * Cin * Cout + i] = 0;
   if (!((m >> k) & 1u)) return;
   const int cch = blockIdx.x, och = blockIdx.y, nci = Cin / 32, nco = Cout / 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
@@ -485,7 +489,6 @@ struct WgArgs {
   const bf16_t* x;        // NHWC [B][h][w][Cin]
   const uint8_t* code;    // [B][h][w]
   const uint16_t* pres;   // [B * nunit] bit k: code k met by the unit's sources
-  const uint32_t* gmask;  // codes present in the batch
   int* list;              // [<= 16 * B * nunit] live entries: unit | code << 24, by code then unit
   unsigned long long* masks;  // [entry][9] tap masks of the entry's unit for its code
   int4* items;            // [<= 16 * B * nunit] (code, first entry, end entry, -)
@@ -496,7 +499,7 @@ struct WgArgs {
 };
 
 __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict__ code, int B, int h, int w,
-                                                       uint16_t* __restrict__ pres, uint32_t* __restrict__ gmask) {
+                                                       uint16_t* __restrict__ pres) {
   // one wave per 64-px unit: OR of 1 << code over its 9-tap sources
   const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo, nunit = (hwo + WPX - 1) / WPX;
   const long long u = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
@@ -521,17 +524,18 @@ __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict
   for (int o = 1; o < 64; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o);
   if (l == 0 && u < (long long)B * nunit) {
     pres[u] = (uint16_t)m;
-    if (m) atomicOr(gmask, m);
   }
 }
 
 // Plan (one 1024-thread workgroup): per code the ordered list of live units, then items of
 // about equal length L = ceil(entries / (target / output tiles)), capped at WITEM_MAX.
+constexpr int WG_PRES_LDS = 8192;  // presence entries k_wg_plan keeps in LDS
 __global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
-  __shared__ int wsum[16];
   __shared__ int cnt_s[16], off_s[17];
+  __shared__ uint16_t spres[WG_PRES_LDS];  // the compaction pass re-reads presence from LDS
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int U = a.B * a.nunit;
+  const bool in_lds = U <= WG_PRES_LDS;
   if (tid < 16) cnt_s[tid] = 0;
   __syncthreads();
   // counts per code
@@ -540,6 +544,7 @@ __global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
   for (int k = 0; k < 16; ++k) c16[k] = 0u;
   for (int u = tid; u < U; u += 1024) {
     const uint32_t m = a.pres[u];
+    if (in_lds) spres[u] = (uint16_t)m;
 #pragma unroll
     for (int k = 0; k < 16; ++k) c16[k] += (m >> k) & 1u;
   }
@@ -560,40 +565,57 @@ __global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
     off_s[16] = o;
   }
   __syncthreads();
-  // ordered compaction per code
-  for (int k = 0; k < 16; ++k) {
-    if (cnt_s[k] == 0) continue;  // uniform
-    int base = off_s[k];
-    for (int u0 = 0; u0 < U; u0 += 1024) {
-      const int u = u0 + tid;
-      const bool live = u < U && ((a.pres[u] >> k) & 1u);
-      const unsigned long long bal = __ballot(live);
-      if (lane == 0) wsum[w] = __popcll(bal);
-      __syncthreads();
-      int before = base;
-      for (int q = 0; q < w; ++q) before += wsum[q];
-      if (live) a.list[before + __popcll(bal & ((1ull << lane) - 1ull))] = u | (k << 24);
-      int tot = 0;
-      for (int q = 0; q < 16; ++q) tot += wsum[q];
-      base += tot;
-      __syncthreads();
+  // ordered compaction, all 16 codes per pass: wave ballots -> per-(code, wave) counts ->
+  // exclusive offsets; units keep their order within each code
+  __shared__ int wc[16][16], wpre[16][16], cbase[16], ctot[16];
+  if (tid < 16) cbase[tid] = off_s[tid];
+  for (int u0 = 0; u0 < U; u0 += 1024) {
+    const int u = u0 + tid;
+    const uint32_t m = u < U ? (in_lds ? (uint32_t)spres[u] : (uint32_t)a.pres[u]) : 0u;
+    unsigned long long bal[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      bal[k] = __ballot((m >> k) & 1u);
+      if (lane == 0) wc[k][w] = __popcll(bal[k]);
     }
+    __syncthreads();
+    if (tid < 256) {
+      const int k = tid >> 4, q = tid & 15;
+      int pre = 0;
+      for (int i = 0; i < q; ++i) pre += wc[k][i];
+      wpre[k][q] = pre;
+      if (q == 15) ctot[k] = pre + wc[k][15];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if ((m >> k) & 1u)
+        a.list[cbase[k] + wpre[k][w] + __popcll(bal[k] & ((1ull << lane) - 1ull))] = u | (k << 24);
+    __syncthreads();
+    if (tid < 16) cbase[tid] += ctot[tid];
+    __syncthreads();
   }
+  // items: code k's c live units cut into n_k = ceil(c / L) near-equal runs, emitted in parallel
+  __shared__ int ibase[17];
+  const int total = off_s[16];
+  const int want = max(1, a.target / max(1, a.ntile_kk * a.ntile_o));
+  const int L = min(max(1, (total + want - 1) / want), WITEM_MAX);
   if (tid == 0) {
-    const int total = off_s[16];
-    const int want = max(1, a.target / max(1, a.ntile_kk * a.ntile_o));
-    int L = max(1, (total + want - 1) / want);
-    L = min(L, WITEM_MAX);
     int ni = 0;
     for (int k = 0; k < 16; ++k) {
-      const int c = cnt_s[k];
-      if (!c) continue;
-      const int n = (c + L - 1) / L;
-      for (int j = 0; j < n; ++j)
-        a.items[ni++] = make_int4(k, off_s[k] + (int)((long long)c * j / n), off_s[k] + (int)((long long)c * (j + 1) / n), 0);
+      ibase[k] = ni;
+      ni += (cnt_s[k] + L - 1) / L;
     }
+    ibase[16] = ni;
     a.counts[0] = total;
     a.counts[1] = ni;
+  }
+  __syncthreads();
+  for (int it = tid; it < ibase[16]; it += 1024) {
+    int k = 0;
+    while (it >= ibase[k + 1]) ++k;
+    const int c = cnt_s[k], n = ibase[k + 1] - ibase[k], j = it - ibase[k];
+    a.items[it] = make_int4(k, off_s[k] + (int)((long long)c * j / n), off_s[k] + (int)((long long)c * (j + 1) / n), 0);
   }
 }
 
@@ -1611,13 +1633,6 @@ int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, 
     if (wbwd)
       k_pack_bwd_codes<<<dim3(Cin / 32, Cout / 32, 144), 256, 0, s>>>((const bf16_t*)wfwd, Cin, Cout, code_mask,
                                                                       (bf16_t*)wbwd);
-    // tail pads (read only by an over-reaching last N tile, whose outputs are dropped)
-    const hipError_t z1 = hipMemsetAsync((bf16_t*)wfwd + 144ll * Cin * Cout, 0, 192 * 32 * sizeof(bf16_t), s);
-    if (z1 != hipSuccess) return (int)z1;
-    if (wbwd) {
-      const hipError_t z2 = hipMemsetAsync((bf16_t*)wbwd + 144ll * Cin * Cout, 0, 192 * 32 * sizeof(bf16_t), s);
-      if (z2 != hipSuccess) return (int)z2;
-    }
   } else {
     return RGBD_E_DTYPE;
   }
@@ -1758,17 +1773,13 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
     const WgPlan P = wg_plan(B, Cin, h, w, Cout);
     RGBD_REQUIRE((long long)B * P.nunit < (1 << 24), RGBD_E_SHAPE);
     uint16_t* pres = (uint16_t*)((char*)ws + L.pres);
-    uint32_t* gmask = (uint32_t*)((char*)ws + L.gmask);
-    const hipError_t me = hipMemsetAsync(gmask, 0, sizeof(uint32_t), s);
-    if (me != hipSuccess) return (int)me;
     const long long nthr = (long long)B * P.nunit * 64;
-    k_code_presence<<<(int)ceil_div(nthr, 256), 256, 0, s>>>(code, B, h, w, pres, gmask);
+    k_code_presence<<<(int)ceil_div(nthr, 256), 256, 0, s>>>(code, B, h, w, pres);
     WgArgs a;
     a.gout = (const bf16_t*)gout_nhwc;
     a.x = (const bf16_t*)x_nhwc;
     a.code = code;
     a.pres = pres;
-    a.gmask = gmask;
     a.list = (int*)((char*)ws + L.list);
     a.masks = (unsigned long long*)((char*)ws + L.masks);
     a.items = (int4*)((char*)ws + L.items);

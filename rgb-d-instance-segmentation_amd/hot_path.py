@@ -22,6 +22,20 @@ from . import ops
 DSAM_PARAMS_PER_MODULE = 9  # conv_layers.{0..3}.{weight,bias}, rgb_projection.weight
 
 
+def stack4(ts, view_only=False):
+    """torch.stack(ts) for same-shape tensors — as a free view when they already sit back to back
+    in one storage (DSAModule keeps its conv weights / biases that way); ``view_only``: None
+    instead of copying."""
+    t0 = ts[0]
+    n, es = t0.numel(), t0.element_size()
+    adjacent = all(t.is_contiguous() and t.dtype == t0.dtype and t.device == t0.device and t.shape == t0.shape
+                   and t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr()
+                   and t.data_ptr() == t0.data_ptr() + i * n * es for i, t in enumerate(ts))
+    if adjacent and t0.storage_offset() + len(ts) * n <= t0.untyped_storage().nbytes() // es:
+        return t0.as_strided((len(ts),) + tuple(t0.shape), (n,) + tuple(t0.stride()), t0.storage_offset())
+    return None if view_only else torch.stack(ts)
+
+
 class _PackCache:
     """Packed implicit-GEMM weights.  float32 (segment form, code independent): re-packed only
     when a parameter changes.  bfloat16 (code-merged form): packed on every call for the region
@@ -34,11 +48,11 @@ class _PackCache:
 
     def get(self, conv_ws, proj_w, dtype, code_mask=None, want_bwd=True):
         if dtype == torch.bfloat16:
-            return ops.dsam_pack(torch.stack([w.detach() for w in conv_ws]), proj_w.detach(), dtype,
+            return ops.dsam_pack(stack4([w.detach() for w in conv_ws]), proj_w.detach(), dtype,
                                  code_mask=code_mask, want_bwd=want_bwd)
         key = (dtype, proj_w.data_ptr(), proj_w._version) + tuple((w.data_ptr(), w._version) for w in conv_ws)
         if key != self.key:
-            self.val = ops.dsam_pack(torch.stack([w.detach() for w in conv_ws]), proj_w.detach(), dtype)
+            self.val = ops.dsam_pack(stack4([w.detach() for w in conv_ws]), proj_w.detach(), dtype)
             self.key = key
         return self.val
 
@@ -62,7 +76,7 @@ class HotPathFunction(torch.autograd.Function):
         x_nhwc = [ops.nchw_to_nhwc(colors[0])]
         cp1 = [colors[0]]
         for k in range(3):
-            bias4 = torch.stack([b.detach() for b in dsam_p[k][1:8:2]])
+            bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
             out, out_nhwc = ops.dsam_fwd(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual=colors[k + 1],
                                          want_nhwc=(k < 2))
             cp1.append(out)

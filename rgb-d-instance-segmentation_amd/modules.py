@@ -13,6 +13,7 @@ import torch
 from torch import nn
 
 from . import ops
+from .hot_path import stack4
 
 
 class _DSAMFn(torch.autograd.Function):
@@ -26,7 +27,7 @@ class _DSAMFn(torch.autograd.Function):
         training = any(ctx.needs_input_grad[5:])
         mask = ops.dsam_code_masks([code]) if dtype == torch.bfloat16 else None
         wfwd, wbwd = pack_cache.get(conv_ws, proj_w, dtype, code_mask=mask, want_bwd=training)
-        out, _ = ops.dsam_fwd(x_nhwc, code, info, wfwd, torch.stack([b.detach() for b in biases]))
+        out, _ = ops.dsam_fwd(x_nhwc, code, info, wfwd, stack4([b.detach() for b in biases]))
         ctx.save_for_backward(x_nhwc, code, info, wbwd)
         ctx.cin = x.shape[1]
         ctx.x_dtype = x.dtype
@@ -73,6 +74,28 @@ class DSAModule(nn.Module):
         self.compute_dtype = torch.float32
         from .hot_path import _PackCache
         self._pack_cache = _PackCache()
+        self._group_storage()
+
+    def _group_storage(self):
+        """Keep the four conv_layers weights (and the four biases) in one storage each, in order,
+        so the packer and the fused forward read them as the [4, ...] arrays they take
+        (hot_path.stack4 then returns a view instead of copying 2 x 4 tensors every step).
+        Parameter identity is kept (only .data moves), so optimizers and state_dicts are
+        unaffected; re-applied after every .to() / .cuda() (Module._apply)."""
+        from .hot_path import stack4
+        with torch.no_grad():
+            for attr in ("weight", "bias"):
+                ps = [getattr(self.conv_layers[i], attr) for i in range(4)]
+                if stack4([p.data for p in ps], view_only=True) is not None:
+                    continue
+                flat = torch.stack([p.data for p in ps])
+                for i, p in enumerate(ps):
+                    p.data = flat[i]
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._group_storage()
+        return out
 
     def _params(self):
         p = []

@@ -63,8 +63,9 @@ def assemble_pixel_values(depth_u8: torch.Tensor, rgb_u8: torch.Tensor = None, o
     B, H, W = depth_u8.shape
     if rgb_u8 is not None and (rgb_u8.dtype != torch.uint8 or tuple(rgb_u8.shape) != (B, H, W, 3)):
         raise ValueError("rgb_u8 must be uint8 [B,H,W,3]")
-    if out is None:
-        out = torch.zeros((B, 10, H, W), dtype=torch.float32, device=depth_u8.device)
+    if out is None:  # every plane is written when RGB is given; planes 0:3 stay zero otherwise
+        alloc = torch.empty if rgb_u8 is not None else torch.zeros
+        out = alloc((B, 10, H, W), dtype=torch.float32, device=depth_u8.device)
     L = _lib.lib()
     ws = _workspace(depth_u8.device, L.rgbd_assemble_workspace_size(B), "assemble")
     check(L.rgbd_assemble_pixel_values(_p(rgb_u8), _p(depth_u8), B, H, W, _p(out), _p(ws),

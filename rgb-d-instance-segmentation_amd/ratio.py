@@ -83,8 +83,7 @@ def ratio_predictor_forward(module, depth_image: torch.Tensor) -> torch.Tensor:
     check(L.rgbd_ratio_forward(code, int(training), ctypes.c_float(momentum), ctypes.c_void_p(d.data_ptr()),
                                d.stride(0), B, H, W, _p(blob), bn_arr, ctypes.c_ulonglong(seed), _p(ratio), _p(ws),
                                _stream(d.device)), "rgbd_ratio_forward")
-    if training:
+    if training:  # one multi-tensor launch for the six BatchNorm counters
         with torch.no_grad():
-            for bn in bns:
-                bn.num_batches_tracked.add_(1)
+            torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
     return ratio.reshape(B, 1)
