@@ -40,6 +40,7 @@ struct Layout {  // byte offsets into the packed blob
   size_t w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, w7, b7, w8, b8, w9, b9, w10, b10;
   size_t w5s, zero;  // bf16: conv5 weights in LDS-DMA step order; 256 zero bytes (padding source)
   size_t w1s;        // bf16: stem weights in the chain v2 K order
+  size_t w1f, w2f;   // bf16 blobs: f32 stem (w1s order) and fusion (chain order) weights, the BN-fold sources
   size_t total;
 };
 
@@ -74,6 +75,8 @@ inline Layout make_layout(int es) {
   L.w5s = seg(es == 2 ? (size_t)C5 * 9 * FUS_C * 2 : 0);
   L.zero = seg(256);
   L.w1s = seg(es == 2 ? (size_t)STEM_C * STEM_K2 * 2 : 0);
+  L.w1f = seg(es == 2 ? (size_t)STEM_C * STEM_K2 * 4 : 0);
+  L.w2f = seg(es == 2 ? (size_t)FUS_C * STEM_C * 4 : 0);
   L.total = o;
   return L;
 }
@@ -137,6 +140,11 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
         if (y >= 0 && y < ks && x >= 0 && x < ks) v = w.p[2 * br][((oo * 3 + c) * ks + y) * ks + x];
       }
       w1s[e] = f32_to_bf16(v);
+      ((float*)(blob + L.w1f))[e] = v;
+    }
+    for (int e = tid; e < FUS_C * STEM_C; e += nth) {  // f32 fusion weights in the chain order
+      const int o = e / STEM_C, kk = e % STEM_C, s = kk / 32, g = (kk % 32) / 8, ee = kk % 8;
+      ((float*)(blob + L.w2f))[e] = w.p[6][o * STEM_C + 32 * s + chain_perm(g, ee)];
     }
     // K-step order for k_rp_conv3x3_v3: [step = half*9 + tap][n][64 ch], each 128-byte row
     // holding its 16-byte chunks in the LDS swizzle order (slot q <- chunk q ^ (n & 6)), so one
@@ -217,7 +225,9 @@ constexpr int CH_TW = 16, CH_TH = 4;                    // tile: 4 rows x 16 col
 constexpr int PATCH_H = CH_TH + 6, PATCH_W = CH_TW + 6;  // 7x7 halo
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
-// bf16 path: v_exp_f32 + v_rcp_f32 (~1 ulp each; the result is rounded to bf16)
+// bf16 path: v_exp_f32 + v_rcp_f32 (~1 ulp each; the result is rounded to bf16).  The bf16 chain
+// also writes its BN affines and statistics with explicit fmaf (the file builds with
+// -ffp-contract=off for the bit-exact paths, which would split them into v_mul + v_add).
 __device__ __forceinline__ float sigmoid_fast(float x) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
 }
@@ -445,6 +455,27 @@ __device__ __forceinline__ void reduce_scatter16(float (&v)[N], int r) {
   }
 }
 
+// ------------------------------------------------------------------ BN folding (bf16 chain)
+// Once the statistics of a BN layer are known, fold its affine (sc, sh) into the producing
+// layer: W' = bf16(sc * W_f32) row-wise, b' = sc * b + sh, so the chain applies only the ReLU.
+// fold: [W1' 192 x 168 bf16][W2' 128 x 192 bf16][b1' 192 f32][b2' 128 f32].  which = 1 | 2.
+constexpr size_t FOLD_W1 = 0, FOLD_W2 = FOLD_W1 + (size_t)STEM_C * STEM_K2 * 2;
+constexpr size_t FOLD_B1 = FOLD_W2 + (size_t)FUS_C * STEM_C * 2, FOLD_B2 = FOLD_B1 + STEM_C * 4;
+constexpr size_t FOLD_BYTES = FOLD_B2 + FUS_C * 4;
+__global__ __launch_bounds__(256) void k_rp_fold(const char* __restrict__ blob, Layout L,
+                                                 const float2* __restrict__ aff, int which, char* __restrict__ fold) {
+  const int c = blockIdx.x;
+  const int K = which == 1 ? STEM_K2 : STEM_C;
+  const float* w = (const float*)(blob + (which == 1 ? L.w1f : L.w2f)) + (size_t)c * K;
+  bf16_t* wo = (bf16_t*)(fold + (which == 1 ? FOLD_W1 : FOLD_W2)) + (size_t)c * K;
+  const float2 a = aff[c];
+  for (int k = threadIdx.x; k < K; k += 256) wo[k] = f32_to_bf16(w[k] * a.x);
+  if (threadIdx.x == 0) {
+    const float b = ((const float*)(blob + (which == 1 ? L.b1 : L.b2)))[c];
+    ((float*)(fold + (which == 1 ? FOLD_B1 : FOLD_B2)))[c] = __builtin_fmaf(b, a.x, a.y);
+  }
+}
+
 // ------------------------------------------------------------------ chain v2 (bf16)
 // 512 threads = 8 waves; persistent; ALL chain weights (143 KB bf16) live in LDS for the
 // workgroup's lifetime; a wave owns 32 pixels (one row of a 8x32 tile, two 16-px MFMA
@@ -479,7 +510,9 @@ template <int PHASE>
 __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const float* __restrict__ depth3, long long bstride, int B,
                                                      int H, int W, const char* __restrict__ blob, Layout L,
                                                      const float2* __restrict__ aff1, const float2* __restrict__ aff2,
-                                                     float* __restrict__ slab, bf16_t* __restrict__ att) {
+                                                     const char* __restrict__ fold, float* __restrict__ slab,
+                                                     bf16_t* __restrict__ att) {
+  // phases 1/2 take W1 (and in phase 2 W2) with their BN folded in (k_rp_fold): ReLU only
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bf16_t* sW1 = (const bf16_t*)(smem + C2W_OFF_W1);
   const bf16_t* sW2 = (const bf16_t*)(smem + C2W_OFF_W2);
@@ -490,8 +523,6 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
   float* sb2 = sb1 + STEM_C;
   float* sb3 = sb2 + FUS_C;
   float* sb4 = sb3 + ATT_C;
-  float2* saf1 = (float2*)(smem + c2w_off_aff<PHASE>());
-  float2* saf2 = saf1 + STEM_C;
   bf16_t* patch = (bf16_t*)(smem + c2w_off_patch<PHASE>());
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -505,20 +536,32 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
             *reinterpret_cast<const uint4*>(blob + src + ((size_t)rr * k + 8 * q) * 2);
       }
     };
-    copy_rows(C2W_OFF_W1, L.w1s, STEM_C, STEM_K2, C2W_S1);
+    auto copy_rows_p = [&](size_t dst, const char* base, int rows, int k, int stride) {
+      const int per = k / 8;
+      for (int i = tid; i < rows * per; i += 512) {
+        const int rr = i / per, q = i % per;
+        *reinterpret_cast<uint4*>(smem + dst + ((size_t)rr * stride + 8 * q) * 2) =
+            *reinterpret_cast<const uint4*>(base + ((size_t)rr * k + 8 * q) * 2);
+      }
+    };
+    if (PHASE == 0)
+      copy_rows(C2W_OFF_W1, L.w1s, STEM_C, STEM_K2, C2W_S1);
+    else
+      copy_rows_p(C2W_OFF_W1, fold + FOLD_W1, STEM_C, STEM_K2, C2W_S1);
     if (PHASE >= 1) {
-      copy_rows(C2W_OFF_W2, L.w2, FUS_C, STEM_C, C2W_S2);
+      if (PHASE == 2)
+        copy_rows_p(C2W_OFF_W2, fold + FOLD_W2, FUS_C, STEM_C, C2W_S2);
+      else
+        copy_rows(C2W_OFF_W2, L.w2, FUS_C, STEM_C, C2W_S2);
       copy_rows(C2W_OFF_W3, L.w3, ATT_C, FUS_C, C2W_S3);
       copy_rows(C2W_OFF_W4, L.w4, FUS_C, ATT_C, C2W_S4);
     }
-    for (int i = tid; i < STEM_C; i += 512) sb1[i] = ((const float*)(blob + L.b1))[i];
-    for (int i = tid; i < FUS_C; i += 512) sb2[i] = ((const float*)(blob + L.b2))[i];
+    for (int i = tid; i < STEM_C; i += 512)
+      sb1[i] = PHASE == 0 ? ((const float*)(blob + L.b1))[i] : ((const float*)(fold + FOLD_B1))[i];
+    for (int i = tid; i < FUS_C; i += 512)
+      sb2[i] = PHASE == 2 ? ((const float*)(fold + FOLD_B2))[i] : ((const float*)(blob + L.b2))[i];
     for (int i = tid; i < ATT_C; i += 512) sb3[i] = ((const float*)(blob + L.b3))[i];
     for (int i = tid; i < FUS_C; i += 512) sb4[i] = ((const float*)(blob + L.b4))[i];
-    if (PHASE >= 1)
-      for (int i = tid; i < STEM_C; i += 512) saf1[i] = aff1[i];
-    if (PHASE >= 2)
-      for (int i = tid; i < FUS_C; i += 512) saf2[i] = aff2[i];
     for (int i = tid; i < 3 * C2W_PH * C2W_PWP; i += 512) patch[i] = 0;  // pad columns stay zero
     for (int i = tid; i < STEM_C * (C2W_S1 - STEM_K2); i += 512)  // W1 row pads: never garbage in an MFMA
       ((bf16_t*)(smem + C2W_OFF_W1))[(i / (C2W_S1 - STEM_K2)) * C2W_S1 + STEM_K2 + i % (C2W_S1 - STEM_K2)] = 0;
@@ -563,7 +606,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
         float v = a[u][j];
         if (!full) v = (row_ok && x0 + 16 * u + 4 * g + j < W) ? v : 0.f;
         sm += v;
-        sq += v * v;
+        sq = __builtin_fmaf(v, v, sq);
       }
   };
   fetch_patch(blockIdx.x);
@@ -662,11 +705,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
       for (int u = 0; u < 2; ++u) {
         float vv[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int t = 2 * s + (e >> 2), j = e & 3;
-          const float2 af = saf1[16 * t + 4 * g + j];
-          vv[e] = fmaxf(a1[t][u][j] * af.x + af.y, 0.f);
-        }
+        for (int e = 0; e < 8; ++e) vv[e] = fmaxf(a1[2 * s + (e >> 2)][u][e & 3], 0.f);  // BN1 folded into W1
         f1[s][u].from8(vv);
       }
     // ---- fusion (phase 1: operands swapped for the statistics)
@@ -700,12 +739,11 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
     }
     if constexpr (PHASE == 2) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
+      for (int t = 0; t < 8; ++t)  // BN2 folded into W2
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float2 af = saf2[16 * t + 4 * g + j];
-          a2[t][0][j] = fmaxf(a2[t][0][j] * af.x + af.y, 0.f);
-          a2[t][1][j] = fmaxf(a2[t][1][j] * af.x + af.y, 0.f);
+          a2[t][0][j] = fmaxf(a2[t][0][j], 0.f);
+          a2[t][1][j] = fmaxf(a2[t][1][j], 0.f);
         }
       Frag<bf16_t> f2[4][2];
 #pragma unroll
@@ -1382,7 +1420,7 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
 }
 
 struct Ws {  // workspace carve
-  size_t aff1, aff2, aff5, slab, att, y, part, pooled, zpart, feat, h1, total;
+  size_t aff1, aff2, aff5, slab, att, y, part, pooled, zpart, feat, h1, fold, total;
 };
 
 inline int chain_grid(int B, int H, int W) {
@@ -1436,6 +1474,7 @@ inline Ws make_ws(int es, int B, int H, int W) {
   w.zpart = seg((size_t)TC_CHUNKS * B * C6 * 16 * sizeof(float));
   w.feat = seg((size_t)B * C6 * sizeof(float));
   w.h1 = seg((size_t)B * 128 * sizeof(float));
+  w.fold = seg(es == 2 ? FOLD_BYTES : 0);
   w.total = o;
   return w;
 }
@@ -1457,6 +1496,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   float* zpart = (float*)(ws + w.zpart);
   float* feat = (float*)(ws + w.feat);
   float* h1 = (float*)(ws + w.h1);
+  char* fold = ws + w.fold;
   const double P = (double)B * H * W;
   const bool v2 = sizeof(T) == 2;
   const int gch = v2 ? chain_grid_v2(B, H, W) : chain_grid(B, H, W);
@@ -1474,8 +1514,8 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
 #define CHAIN_LAUNCH(PH, A1, A2, SL, OUT)                                                                          \
   do {                                                                                                            \
     if (v2)                                                                                                       \
-      k_rp_chain_v2<PH><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, \
-                                                                        (bf16_t*)(OUT));                          \
+      k_rp_chain_v2<PH><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, \
+                                                                        fold, SL, (bf16_t*)(OUT));                \
     else                                                                                                          \
       k_rp_chain<T, PH><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, (T*)(OUT));            \
   } while (0)
@@ -1484,10 +1524,12 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   for (int l = 0; l < 3; ++l)
     k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch0, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
                                  bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
+  if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
   // fusion BN
   if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, nullptr);
   k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, nslab_ch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
                                 bn.p[15], aff2);
+  if (v2) k_rp_fold<<<FUS_C, 256, 0, s>>>(blob, L, aff2, 2, fold);  // BN2 -> W2', b2'
   // gated attention features
   {
     TimerScope ts("rp_chain", s);
