@@ -115,9 +115,11 @@ def build(args, dev):
 def make_step(ctx, world, inference=False):
     from rgbd_amd import ops
     from rgbd_amd.hot_path import hot_path
-    from rgbd_amd.distributed import GradBucket
+    from rgbd_amd.distributed import OverlappedGradReducer, hot_path_grad_groups
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
-    bucket = GradBucket(params) if world > 1 else None
+    # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
+    reducer = OverlappedGradReducer(hot_path_grad_groups(ctx["dsams"], ctx["dg"])) if world > 1 else None
+    hook = None if reducer is None else reducer.ready
     opt = None if inference else torch.optim.AdamW(params, lr=1e-5, fused=True)
 
     def step():
@@ -127,10 +129,10 @@ def make_step(ctx, world, inference=False):
                 ratio = ctx["rp"](pv[:, 3:6])
                 return hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"])
         ratio = ctx["rp"](pv[:, 3:6])
-        feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"])
+        feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], grad_hook=hook)
         torch.autograd.backward(feats, ctx["gouts"])
-        if bucket is not None:  # DDP gradient exchange of the hot-path parameters (RCCL over xGMI)
-            bucket.allreduce_mean()
+        if reducer is not None:  # DDP gradient exchange of the hot-path parameters (RCCL over xGMI)
+            reducer.finish()
         opt.step()
         opt.zero_grad(set_to_none=True)
         return feats

@@ -112,6 +112,7 @@ class HotPathFunction(torch.autograd.Function):
         # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}.  bfloat16 keeps the cascade in
         # NHWC (dX written NHWC only, its residual G[k] converted once; bias sums from NHWC).
         bf16 = dtype == torch.bfloat16
+        hook = ctx.cfg.get("grad_hook")
         dcp = G[3]
         dcp_nhwc = ops.nchw_to_nhwc(dcp)
         grads_dsam = [None, None, None]
@@ -123,6 +124,8 @@ class HotPathFunction(torch.autograd.Function):
                 gk += [dconv[i], dbias[i]]
             gk.append(dproj)
             grads_dsam[k] = gk
+            if hook is not None:  # DDP: this module's all-reduce runs under the rest of the cascade
+                hook(2 - k, gk if k > 0 else gk + grads_dggm)
             if k > 0:
                 if bf16:
                     dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], None, want_nhwc=True,
@@ -133,9 +136,13 @@ class HotPathFunction(torch.autograd.Function):
         return (None, None, None, None, None, None, None, *pgrads)
 
 
-def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch.float32, check_status=False):
+def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch.float32, check_status=False,
+             grad_hook=None):
     """Run the fused hot path.  ``dsam_modules``: the three DSAModule instances;
-    ``dggm_module``: the DepthGradientInjectionResidual instance."""
+    ``dggm_module``: the DepthGradientInjectionResidual instance.  ``grad_hook(i, grads)``, if
+    given, is called during backward as each parameter group's gradients are enqueued, in the
+    order of ``distributed.hot_path_grad_groups`` (dsam2, dsam1, dsam0 + DGGM) — the data-parallel
+    reducer uses it to overlap the gradient all-reduce with the rest of the backward."""
     params = []
     for m in dsam_modules:
         for i in range(4):
@@ -144,7 +151,7 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
     for i in range(4):
         conv = dggm_module.depth_enhancement_layers[i][0]
         params += [conv.weight, conv.bias]
-    cfg = {"dtype": dtype, "check_status": check_status,
+    cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook,
            "pack_cache": [m._pack_cache for m in dsam_modules]}
     pv = pixel_values.detach().float().contiguous()
     return list(HotPathFunction.apply(pv, ratio, cfg, *colors, *params))

@@ -1,7 +1,9 @@
-"""world_size-2 gloo test of the data-parallel exchange (CPU, no GPU needed)."""
+"""world_size-2 tests of the data-parallel exchange: gloo on CPU tensors, and (gpu) two ranks on one
+MI355X running the fused hot path with the overlapped reducer."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -50,3 +52,129 @@ def test_grad_allreduce_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _worker_overlapped(rank, world, port, q):
+    """OverlappedGradReducer on CPU tensors: groups handed over in cascade order, None = zero."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import _rgbd_import  # noqa: F401
+    from rgbd_amd.distributed import OverlappedGradReducer, hot_path_grad_groups
+    from rgbd_amd.modules import DSAModule, DepthGradientInjectionResidual
+    torch.manual_seed(0)
+    dsams = [DSAModule(4, 8), DSAModule(8, 16), DSAModule(16, 32)]
+    dg = DepthGradientInjectionResidual([4, 8, 16, 32], 3)
+    groups = hot_path_grad_groups(dsams, dg)
+    assert [len(g) for g in groups] == [9, 9, 17]
+    red = OverlappedGradReducer(groups)
+    ok = True
+    for step in range(2):  # buffers are reused across steps
+        exp = []
+        for gi, g in enumerate(groups):
+            grads = []
+            for i, p in enumerate(g):
+                t = torch.randn(p.shape, generator=torch.Generator().manual_seed(1000 * step + 100 * gi + i))
+                grads.append(None if (rank == 0 and i == 1) else t * (rank + 1))
+                exp.append(t * (1.0 if i == 1 else 1.5))  # mean over ranks of t*(r+1), rank 0 missing i==1
+                if p.grad is None or step == 0:
+                    p.grad = torch.zeros_like(p)
+            red.ready(gi, grads)
+        red.finish()
+        got = [p.grad for g in groups for p in g]
+        ok &= all(torch.allclose(a, b, rtol=1e-6, atol=1e-7) for a, b in zip(got, exp))
+    try:
+        red.finish()  # nothing handed over: must fail loudly
+        ok = False
+    except RuntimeError:
+        pass
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_overlapped_reducer_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overlapped, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
+def _worker_gpu_hot_path(rank, world, port, q):
+    """Both ranks on cuda:0 over gloo: the overlapped reducer fed by the fused backward's hook
+    yields exactly the mean of the two ranks' standalone gradients."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path[:0] = [root, os.path.join(root, "tests", "golden")]
+        import _rgbd_import  # noqa: F401
+        import golden_inputs as gi
+        from rgbd_amd import init as winit
+        from rgbd_amd.distributed import OverlappedGradReducer, hot_path_grad_groups
+        from rgbd_amd.hot_path import hot_path
+        from rgbd_amd.modules import DSAModule, DepthGradientInjectionResidual
+        dev = torch.device("cuda:0")
+        H, W, B = 64, 96, 2
+        sizes = gi.swin_sizes(H, W)
+        pre = "model.pixel_level_module."
+        dsams = []
+        for k, (ci, co) in enumerate([(96, 192), (192, 384), (384, 768)]):
+            m = DSAModule(ci, co)
+            winit.init_deterministic(m, prefix=f"{pre}dsam{k}.")
+            dsams.append(m.to(dev))
+        dg = DepthGradientInjectionResidual([96, 192, 384, 768], 3)
+        winit.init_deterministic(dg, prefix=f"{pre}depth_gradient_injection.")
+        dg = dg.to(dev)
+        params = [p for m in dsams + [dg] for p in m.parameters()]
+
+        def inputs(r):
+            pv = torch.from_numpy(gi.pixel_values(40 + r, B, H, W)).to(dev)
+            ratios = torch.tensor([[0.12 + 0.1 * r], [0.3]], device=dev)
+            colors = [torch.from_numpy(gi.feature(f"ddp.c{k}.{r}", (B, c, *sizes[k]))).to(dev)
+                      for k, c in enumerate([96, 192, 384, 768])]
+            return pv, ratios, colors
+
+        def grads(r, hook=None):
+            for p in params:
+                p.grad = None
+            pv, ratios, colors = inputs(r)
+            outs = hot_path(pv, ratios, colors, dsams, dg, grad_hook=hook)
+            torch.autograd.backward(outs, [torch.full_like(o, 1e-2 * (k + 1)) * (1 + r) for k, o in enumerate(outs)])
+            return [p.grad.clone() for p in params]
+
+        ref = [(a + b) / 2 for a, b in zip(grads(0), grads(1))]
+        red = OverlappedGradReducer(hot_path_grad_groups(dsams, dg))
+        grads(rank, hook=red.ready)
+        red.finish()
+        torch.cuda.synchronize()
+        err = max(float(((p.grad - e).abs().max() / (e.abs().max() + 1e-12))) for p, e in zip(params, ref))
+        q.put((rank, err))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.gpu
+def test_gpu_hot_path_ddp_overlap_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_gpu_hot_path, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert isinstance(res[r], float), res[r]
+        assert res[r] < 1e-6, res
