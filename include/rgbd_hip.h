@@ -183,6 +183,22 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        float* ratio, void* ws, void* stream);
 
+/* ---------------------------------------------------------------- f1 mask predictor
+ * Replaces the dense work of Mask2FormerMaskPredictor.forward (transformers 5.15
+ * modeling_mask2former.py:2040-2056; called 10x per forward from :1896 and :1929).
+ * rgbd_mask_logits: einsum("bqc,bchw->bqhw") (:2046) as an MFMA GEMM.
+ *   emb: dtype [B][Q][C] (the mask embeddings, mask_embedder output), pix: dtype NCHW
+ *   [B][C][H][W] (pixel decoder mask features), logits: dtype [B][Q][H][W] (OVERWRITTEN).
+ *   C % 32 == 0; emb / pix / logits 16-byte aligned.  f32: exact-f32 MFMA products, f32 sums. */
+int rgbd_mask_logits(int dtype, const void* emb, const void* pix, int B, int Q, int C, int H, int W,
+                     void* logits, void* stream);
+/* rgbd_mask_attention: the attention mask of :2048-2054 from those logits —
+ *   bilinear resample to th x tw (align_corners=False, torch's source-index rule), rounded to
+ *   dtype, sigmoid rounded to dtype, < 0.5 — written as bytes 0/1 (torch.bool) to
+ *   attn [B*heads][Q][th*tw] (head-major repeat, :2052-2053). */
+int rgbd_mask_attention(int dtype, const void* logits, int B, int Q, int H, int W, int th, int tw,
+                        int heads, uint8_t* attn, void* stream);
+
 /* ---------------------------------------------------------------- kernel timing (bench only)
  * When enabled, launch functions bracket their main kernel with hipEvents recorded on the
  * launch stream; rgbd_timing_read synchronises those events and returns the summed

@@ -46,6 +46,8 @@ SIGNATURES = {
     "rgbd_dsam_bwd_data": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_weight_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rgbd_dsam_bwd_weight": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "rgbd_mask_logits": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "rgbd_mask_attention": (_I, [_I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rgbd_timing_enable": (_I, [_I]),
     "rgbd_timing_read": (ctypes.c_double, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "rgbd_ratio_packed_size": (_SZ, [_I]),

@@ -17,6 +17,7 @@ from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation,
 from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
                                                                   Mask2FormerPixelLevelModuleOutput)
 
+from . import mask_predictor
 from .hot_path import hot_path
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
@@ -98,6 +99,9 @@ class CustomMask2FormerModel(Mask2FormerModel):
     def __init__(self, config, version):
         super().__init__(config)
         self.pixel_level_module = CustomMask2FormerPixelLevelModule(config, version=version)
+        # f1: mask einsum + attention-mask binarisation of the masked-attention decoder on the
+        # HIP kernels (class swap: parameters and state_dict keys unchanged)
+        mask_predictor.install(self.transformer_module)
 
 
 class CustomMask2FormerForUniversalSegmentation(Mask2FormerForUniversalSegmentation):

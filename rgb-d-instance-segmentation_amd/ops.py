@@ -301,3 +301,36 @@ def dsam_bwd_weight(gout_nchw, x_nhwc, code, info, gout_nhwc=None):
     check(L.rgbd_dsam_bwd_weight(dt, _p(gout_nchw), _p(gout_nhwc), _p(x_nhwc), _p(code), _p(info), B, Ci, h, w,
                                  Co, _p(dconv), _p(dproj), _p(dbias), _p(ws), _stream(dev)), "rgbd_dsam_bwd_weight")
     return dconv, dproj, dbias
+
+
+# ------------------------------------------------------------------ f1 mask predictor
+def mask_logits(emb: torch.Tensor, pix: torch.Tensor) -> torch.Tensor:
+    """einsum("bqc,bchw->bqhw", emb, pix) (modeling_mask2former.py:2046) on the MFMA kernel.
+    emb [B,Q,C], pix [B,C,H,W], same dtype (float32 or bfloat16) -> [B,Q,H,W] of that dtype."""
+    emb = emb.contiguous()
+    pix = pix.contiguous()
+    _need_cuda(emb, pix)
+    if emb.dim() != 3 or pix.dim() != 4 or emb.shape[0] != pix.shape[0] or emb.shape[2] != pix.shape[1]:
+        raise ValueError(f"mask_logits: emb {tuple(emb.shape)} and pix {tuple(pix.shape)} do not contract")
+    if emb.dtype != pix.dtype:
+        raise TypeError(f"mask_logits: emb {emb.dtype} != pix {pix.dtype}")
+    B, Q, C = emb.shape
+    H, W = pix.shape[2:]
+    out = torch.empty((B, Q, H, W), dtype=pix.dtype, device=pix.device)
+    check(_lib.lib().rgbd_mask_logits(_dtype_code(pix), _p(emb), _p(pix), B, Q, C, H, W, _p(out),
+                                      _stream(pix.device)), "rgbd_mask_logits")
+    return out
+
+
+def mask_attention(logits: torch.Tensor, size, heads: int) -> torch.Tensor:
+    """The binarised attention mask of modeling_mask2former.py:2048-2054: bilinear resample of
+    ``logits`` [B,Q,H,W] to ``size`` (align_corners=False), sigmoid, < 0.5, repeated over
+    ``heads`` -> bool [B*heads, Q, th*tw]."""
+    logits = logits.contiguous()
+    _need_cuda(logits)
+    B, Q, H, W = logits.shape
+    th, tw = (int(size), int(size)) if isinstance(size, int) else (int(size[0]), int(size[1]))
+    attn = torch.empty((B * heads, Q, th * tw), dtype=torch.bool, device=logits.device)
+    check(_lib.lib().rgbd_mask_attention(_dtype_code(logits), _p(logits), B, Q, H, W, th, tw, int(heads),
+                                         _p(attn), _stream(logits.device)), "rgbd_mask_attention")
+    return attn

@@ -40,3 +40,17 @@ def test_ops_refuse_cpu_tensors():
     from rgbd_amd import ops
     with pytest.raises(RuntimeError, match="GPU only"):
         ops.nchw_to_nhwc(torch.zeros(1, 8, 4, 4))
+
+
+def test_mask_predictor_install_keeps_state_dict():
+    """f1 drop-in: the decoder's Mask2FormerMaskPredictor becomes HipMaskPredictor by a class
+    swap — same parameters, same state_dict keys (no GPU needed)."""
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerMaskPredictor
+    from rgbd_amd import mask_predictor
+    m = Mask2FormerMaskPredictor(hidden_size=32, num_heads=4, mask_feature_size=32)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    assert mask_predictor.install(m) == 1
+    assert type(m) is mask_predictor.HipMaskPredictor
+    after = m.state_dict()
+    assert list(after) == list(before) and all(bool((after[k] == before[k]).all()) for k in before)
+    assert mask_predictor.install(m) == 0

@@ -10,7 +10,7 @@ import torch
 
 import golden_inputs as gi
 from oracle import ratio as ratio_o
-from rgbd_amd import init as winit
+from rgbd_amd import init as winit, mask_predictor
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -140,9 +140,30 @@ def test_full_model_mask_logits_fp32(golden):
         h2.remove()
     # the same model on the CPU, fed with the GPU hot-path features
     mc = _full_model().cpu().eval()
+    assert mask_predictor.uninstall(mc) == 1  # the reference HF predictor is the CPU checker
     mc.model.pixel_level_module.hot_path_features = lambda pv_, colors, ratios=None: caps["bb"]
-    with torch.no_grad():
-        out = mc(pixel_values=pv_cpu)
+    calls = []
+    h3 = mc.model.transformer_module.decoder.mask_predictor.register_forward_hook(
+        lambda mod, inp, out: calls.append((inp, out)))
+    try:
+        with torch.no_grad():
+            out = mc(pixel_values=pv_cpu)
+    finally:
+        h3.remove()
+    # f1 pinned on the reference's own calls: each of the 10 mask-predictor calls of the CPU run,
+    # replayed through the HIP predictor on the GPU with the same inputs
+    hip_pred = m.model.transformer_module.decoder.mask_predictor
+    assert isinstance(hip_pred, mask_predictor.HipMaskPredictor) and len(calls) == 10
+    worst = 0.0
+    for (outputs, pix_emb, size), (mask_ref, attn_ref) in calls:
+        with torch.no_grad():
+            mask_h, attn_h = hip_pred(outputs.to(DEV), pix_emb.to(DEV), size)
+        worst = max(worst, float((mask_h.cpu() - mask_ref).abs().max()))
+        val = torch.nn.functional.interpolate(mask_ref, size=size, mode="bilinear", align_corners=False).flatten(2)
+        near = (val.abs() < 1e-4).unsqueeze(1).expand(-1, hip_pred.num_heads, -1, -1).flatten(0, 1)
+        assert not bool(((attn_h.cpu() != attn_ref) & ~near).any())
+    print(f"f1 mask predictor (HIP vs reference CPU calls): max-abs-err {worst:.3g}")
+    assert worst <= 1e-4
     err = float(np.abs(out.masks_queries_logits.numpy() - g5["mask_logits"]).max())
     gpu = float(np.abs(out_gpu.masks_queries_logits.cpu().numpy() - g5["mask_logits"]).max())
     print(f"mask-logit max-abs-err (fp32): hot path {err:.3g}; everything on the GPU {gpu:.3g}")
