@@ -72,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-sample", type=int, default=1, help="images in the bounded CPU sample")
     ap.add_argument("--inference", type=int, default=1, help="also report forward-only img/s")
+    ap.add_argument("--c5-stream", type=int, default=1,
+                    help="also report the C5 RealSense 1280x720 B=1 streaming inference rate (rank 0, N=1)")
     return ap.parse_args(argv)
 
 
@@ -159,6 +161,39 @@ def timed(step, steps, warmup, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt
+
+
+def c5_stream(ctx, frames=100):
+    """BASELINE configs[4]: RealSense 1280x720 RGB-D stream inference, one frame per step, the
+    hot path in eval mode replayed from a HIP graph (rgbd_amd/stream.py).  Reports the graph
+    rate with the frame resident, the graph rate including the pinned-host -> HBM copy of the
+    raw u8 frame (RGB + depth, 3.7 MB), and the same path launched eagerly from Python."""
+    from rgbd_amd import synthetic
+    from rgbd_amd.stream import StreamingHotPath
+    H, W = 720, 1280
+    sp = StreamingHotPath(ctx["rp"], ctx["dsams"], ctx["dg"], H, W, B=1, dtype=ctx["dtype"])
+    sc = synthetic.make_scene(synthetic.scene_seed(5, 0), H, W)
+    d_host = torch.from_numpy(sc["depth_u8"][None]).pin_memory()
+    c_host = torch.from_numpy(sc["rgb_u8"][None]).contiguous().pin_memory()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    colors = [torch.randn(c.shape, generator=g, device="cuda").to(c.dtype) for c in sp.colors]
+    sp(d_host, c_host, colors)  # captures
+
+    def rate(fn):
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            fn()
+        torch.cuda.synchronize()
+        return round(frames / (time.perf_counter() - t0), 1)
+    graph = rate(lambda: sp())
+    graph_h2d = rate(lambda: sp(d_host, c_host))
+    with torch.no_grad():
+        eager = rate(lambda: sp._run())
+    return {"shape": f"{W}x{H}", "batch": 1, "dtype": "bf16" if ctx["dtype"] == torch.bfloat16 else "f32",
+            "graph_img_s": graph, "graph_with_h2d_img_s": graph_h2d, "eager_img_s": eager, "frames": frames}
 
 
 def cpu_baseline(ctx, args):
@@ -258,6 +293,8 @@ def main():
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, args)
+    if rank == 0 and world == 1 and args.c5_stream:
+        out["c5_stream"] = c5_stream(ctx)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

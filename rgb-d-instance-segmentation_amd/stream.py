@@ -1,0 +1,73 @@
+"""C5 (BASELINE configs[4]): RealSense-style streaming inference of the hot path, one frame (or
+a small fixed batch) at a time, replayed from a HIP graph.
+
+At 1280x720, B=1 the kernels of one frame take about 1 ms, and issuing the ~40 launches of the
+path from Python (ctypes + torch allocator) costs a comparable amount of host time.  The whole
+inference path — u8 frames -> 10-channel pixel_values + DGGM planes (K1) -> ratio predictor
+eval (K4) -> decomposition (K3) -> DSAM x3 cascade (K5) -> DGGM + final sum (K2) — is captured
+once per shape into a graph (torch.cuda.CUDAGraph over hipGraph) and replayed per frame from
+static device buffers, so the per-frame host cost is one graph launch.
+
+Reference path per frame: CustomMask2FormerPixelLevelModule.forward (custom_model.py:324-355)
+in eval mode, with the dataloader's 10-channel assembly (dataloader.py:386-425) moved on-device.
+The Swin colour features are inputs (``colors``), as in the module (they come from the encoder,
+outside the hot path).
+"""
+import torch
+
+from . import ops
+from .hot_path import hot_path
+
+
+class StreamingHotPath:
+    def __init__(self, ratio_predictor, dsams, dggm, H, W, B=1, dtype=torch.bfloat16, device="cuda",
+                 color_channels=(96, 192, 384, 768)):
+        self.rp, self.dsams, self.dg = ratio_predictor, list(dsams), dggm
+        self.dtype = dtype
+        for m in [self.rp, self.dg] + self.dsams:
+            m.compute_dtype = dtype
+            m.eval()
+        dev = torch.device(device)
+        self.depth_u8 = torch.zeros((B, H, W), dtype=torch.uint8, device=dev)
+        self.rgb_u8 = torch.zeros((B, H, W, 3), dtype=torch.uint8, device=dev)
+        h, w = -(-H // 4), -(-W // 4)
+        self.colors = []
+        for c in color_channels:
+            self.colors.append(torch.zeros((B, c, h, w), dtype=dtype, device=dev))
+            h, w = -(-h // 2), -(-w // 2)
+        self.graph = None
+        self.outs = None
+
+    def _run(self):
+        pv = ops.assemble_pixel_values(self.depth_u8, self.rgb_u8)
+        ratio = self.rp(pv[:, 3:6])
+        return hot_path(pv, ratio, self.colors, self.dsams, self.dg, dtype=self.dtype), ratio
+
+    def capture(self):
+        """Warm up (packs weights, sizes workspaces) on a side stream, then capture the path."""
+        with torch.no_grad():
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._run()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.outs = self._run()
+        return self
+
+    def __call__(self, depth_u8=None, rgb_u8=None, colors=None):
+        """Copy the frame (if given) into the static buffers and replay.  Returns the 4 backbone
+        features and the ratio, as static tensors overwritten by the next call."""
+        if self.graph is None:
+            self.capture()
+        if depth_u8 is not None:
+            self.depth_u8.copy_(depth_u8, non_blocking=True)
+        if rgb_u8 is not None:
+            self.rgb_u8.copy_(rgb_u8, non_blocking=True)
+        if colors is not None:
+            for dst, src in zip(self.colors, colors):
+                dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.outs

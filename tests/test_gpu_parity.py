@@ -262,3 +262,86 @@ def test_hot_path_fused_vs_oracle(dtype):
         scale = max(float(np.abs(e).max()), 1e-6)
         err = np.abs(a - e).max() / scale
         assert err < (2e-4 if dtype == torch.float32 else BF16_REL), f"{n}: rel err {err}"
+
+
+# ------------------------------------------------------------------ C5: RealSense 1280x720
+def test_c5_assemble_and_decompose_1280x720():
+    """BASELINE config C5 (RealSense 1280x720): 10-channel assembly incl. the DGGM Sobel planes
+    bit-exact, and the decomposition (histogram, modes, region codes at the three DSAM input
+    resolutions 180x320 / 90x160 / 45x80) bit-exact against the oracle, two frames in one batch."""
+    ops = _ops()
+    H, W, B = 720, 1280, 2
+    scenes = [synthetic.make_scene(synthetic.scene_seed(5, i), H, W) for i in range(B)]
+    depth = torch.from_numpy(np.stack([s["depth_u8"] for s in scenes])).to(DEV)
+    rgb = torch.from_numpy(np.stack([s["rgb_u8"] for s in scenes])).contiguous().to(DEV)
+    pv = ops.assemble_pixel_values(depth, rgb).cpu().numpy()
+    for b, s in enumerate(scenes):
+        exp = np.concatenate([synthetic.rgbd_planes(s), dggm_pre.dggm_planes(s["depth_u8"])])
+        np.testing.assert_array_equal(bits(pv[b]), bits(exp))
+    ratios = np.array([0.1, 0.33], dtype=np.float32)
+    sizes = gi.pool_sizes(H, W)
+    assert sizes[0] == (180, 320) and sizes[2] == (45, 80)
+    codes, info = ops.edsam_decompose(torch.from_numpy(pv).to(DEV), torch.from_numpy(ratios).to(DEV), sizes)
+    rec = ops.decode_info(info)
+    for b in range(B):
+        dec = edsam.decompose(pv[b, 3:6], float(ratios[b]))
+        np.testing.assert_array_equal(rec[b]["hist"], dec["hist"])
+        assert rec[b]["n_modes"] == dec["n_modes"]
+        for s, (oh, ow) in enumerate(sizes):
+            np.testing.assert_array_equal(codes[s][b].cpu().numpy(), edsam.pooled_codes(dec["code"], oh, ow))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c5_hot_path_forward_1280x720(dtype):
+    """C5 streaming inference shape (B=1, 1280x720; Swin maps 180x320 ... 23x40, so the last DSAM
+    sees an odd 45x80 -> 23x40 reduction): fused forward vs the oracle."""
+    from rgbd_amd.hot_path import hot_path
+    H, W, B = 720, 1280, 1
+    pv = torch.from_numpy(gi.pixel_values(9, B, H, W))
+    ratios = torch.tensor([[0.15]], dtype=torch.float32)
+    sizes = gi.swin_sizes(H, W)
+    assert sizes[3] == (23, 40)
+    colors = [torch.from_numpy(gi.feature(f"c5.c{k}", (B, c, *sizes[k])))
+              for k, c in enumerate([96, 192, 384, 768])]
+    dsams, dg = _hot_modules(dtype)
+    with torch.no_grad():
+        outs = hot_path(pv.to(DEV), ratios.to(DEV), [c.to(DEV) for c in colors], dsams, dg, dtype=dtype,
+                        check_status=True)
+    sd = {}
+    for k, m in enumerate(dsams):
+        sd.update({f"dsam{k}.{kk}": v.detach().cpu() for kk, v in m.state_dict().items()})
+    sd.update({f"depth_gradient_injection.{kk}": v.detach().cpu() for kk, v in dg.state_dict().items()})
+    with torch.no_grad():
+        ref, _, _ = hot_o.hot_path_forward(colors, pv, sd, ratios=ratios)
+    for k in range(4):
+        a, e = outs[k].float().cpu().numpy(), ref[k].numpy()
+        if dtype == torch.float32:
+            np.testing.assert_allclose(a, e, rtol=1e-4, atol=1e-3, err_msg=f"feature {k}")
+        else:
+            assert np.abs(a - e).max() / np.abs(e).max() < BF16_REL, f"feature {k}"
+
+
+def test_streaming_graph_replay_matches_eager():
+    """stream.StreamingHotPath: the graph replay gives the eager path's features for a frame, and
+    a new frame copied into the static buffers gives that frame's features (no stale state)."""
+    from rgbd_amd.modules import EnhancedDepthImageRatioPredictor
+    from rgbd_amd.stream import StreamingHotPath
+    H, W = 96, 128
+    rp = EnhancedDepthImageRatioPredictor(3)
+    winit.init_deterministic(rp, prefix="model.pixel_level_module.ratio_predictor.")
+    dsams, dg = _hot_modules(torch.bfloat16)
+    sp = StreamingHotPath(rp.to(DEV), dsams, dg, H, W, B=1, dtype=torch.bfloat16)
+    frames = [synthetic.make_scene(synthetic.scene_seed(6, i), H, W) for i in range(2)]
+    g = torch.Generator(device=DEV).manual_seed(2)
+    colors = [torch.randn(c.shape, generator=g, device=DEV).to(c.dtype) for c in sp.colors]
+    for f in frames:
+        d = torch.from_numpy(f["depth_u8"][None]).to(DEV)
+        c = torch.from_numpy(f["rgb_u8"][None]).contiguous().to(DEV)
+        feats, ratio = sp(d, c, colors)
+        feats = [t.clone() for t in feats]
+        ratio = ratio.clone()
+        with torch.no_grad():
+            ref_feats, ref_ratio = sp._run()
+        assert torch.equal(ratio, ref_ratio)
+        for a, e in zip(feats, ref_feats):
+            assert torch.equal(a, e)
