@@ -107,6 +107,120 @@ __global__ __launch_bounds__(256) void k_prep_pass2(int H, int W, float* __restr
   }
 }
 
+// Quad variants (W % 4 == 0, every NYUv2 / RealSense width): a thread owns 4 x-consecutive
+// pixels — one 4-byte depth load per stencil row plus the two reflected edge bytes, three 4-byte
+// RGB loads, and one 16-byte store per output plane — instead of 9 byte loads and 8 scalar
+// stores per pixel.  Same arithmetic, same order per pixel, so the planes stay bit-exact.
+__device__ __forceinline__ void row6(const uint8_t* __restrict__ row, int x0, int W, int (&v)[6]) {
+  const uint32_t c = *reinterpret_cast<const uint32_t*>(row + x0);
+  v[0] = row[reflect101(x0 - 1, W)];
+  v[1] = c & 0xff;
+  v[2] = (c >> 8) & 0xff;
+  v[3] = (c >> 16) & 0xff;
+  v[4] = c >> 24;
+  v[5] = row[reflect101(x0 + 4, W)];
+}
+
+__global__ __launch_bounds__(256) void k_prep_pass1_q(const uint8_t* __restrict__ rgb,
+                                                      const uint8_t* __restrict__ depth, int H, int W,
+                                                      float* __restrict__ pv, float2* __restrict__ part) {
+  const int b = blockIdx.y;
+  const long long HW = (long long)H * W;
+  const int WQ = W >> 2;
+  const uint8_t* d = depth + b * HW;
+  float* out = pv + b * 10 * HW;
+  float vmax = 0.f, vmin = __uint_as_float(0x7f800000u);
+  const int nq = (int)(HW >> 2);
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += 256 * gridDim.x) {
+    const int y = q / WQ, x0 = (q - y * WQ) * 4;
+    const long long p = (long long)y * W + x0;
+    int up[6], mid[6], dn[6];
+    row6(d + (long long)reflect101(y - 1, H) * W, x0, W, up);
+    row6(d + (long long)y * W, x0, W, mid);
+    row6(d + (long long)reflect101(y + 1, H) * W, x0, W, dn);
+    if (rgb) {
+      const uint32_t* px = reinterpret_cast<const uint32_t*>(rgb + (b * HW + p) * 3);
+      const uint32_t w0 = px[0], w1 = px[1], w2 = px[2];
+      const uint8_t c[12] = {(uint8_t)w0, (uint8_t)(w0 >> 8), (uint8_t)(w0 >> 16), (uint8_t)(w0 >> 24),
+                             (uint8_t)w1, (uint8_t)(w1 >> 8), (uint8_t)(w1 >> 16), (uint8_t)(w1 >> 24),
+                             (uint8_t)w2, (uint8_t)(w2 >> 8), (uint8_t)(w2 >> 16), (uint8_t)(w2 >> 24)};
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+        *reinterpret_cast<float4*>(out + ch * HW + p) =
+            make_float4(norm_u8(c[ch], ch), norm_u8(c[3 + ch], ch), norm_u8(c[6 + ch], ch), norm_u8(c[9 + ch], ch));
+    }
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+      *reinterpret_cast<float4*>(out + (3 + ch) * HW + p) =
+          make_float4(norm_u8(mid[1], ch), norm_u8(mid[2], ch), norm_u8(mid[3], ch), norm_u8(mid[4], ch));
+    float mag[4], msk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int l = i, c = i + 1, r = i + 2;
+      const int gx = (up[r] - up[l]) + 2 * (mid[r] - mid[l]) + (dn[r] - dn[l]);
+      const int gy = (dn[l] - up[l]) + 2 * (dn[c] - up[c]) + (dn[r] - up[r]);
+      float m = sqrt_rn((float)(gx * gx + gy * gy));  // exact integer argument (< 2^24)
+      if (mid[c] == 0) m = 0.f;                         // invalid depth (:1265, :1278)
+      mag[i] = m;
+      msk[i] = m > 0.f ? 1.f : 0.f;                     // valid-gradient mask (:1282)
+      vmax = fmaxf(vmax, m);
+      if (m > 0.f) vmin = fminf(vmin, m);
+    }
+    *reinterpret_cast<float4*>(out + 6 * HW + p) = make_float4(mag[0], mag[1], mag[2], mag[3]);  // scratch
+    *reinterpret_cast<float4*>(out + 9 * HW + p) = make_float4(msk[0], msk[1], msk[2], msk[3]);
+  }
+  vmax = -wave_min(-vmax);
+  vmin = wave_min(vmin);
+  __shared__ float rmax[4], rmin[4];
+  if ((threadIdx.x & 63) == 0) {
+    rmax[threadIdx.x >> 6] = vmax;
+    rmin[threadIdx.x >> 6] = vmin;
+  }
+  __syncthreads();
+  // one (min, max) partial per block, reduced by pass 2 (no same-address atomics: 256 blocks of
+  // one image serialising on one L2 line cost ~25 us)
+  if (threadIdx.x == 0)
+    part[(long long)b * gridDim.x + blockIdx.x] =
+        make_float2(fminf(fminf(rmin[0], rmin[1]), fminf(rmin[2], rmin[3])),
+                    fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3])));
+}
+
+__global__ __launch_bounds__(256) void k_prep_pass2_q(int H, int W, float* __restrict__ pv,
+                                                      const float2* __restrict__ part, int nparts) {
+  const int b = blockIdx.y;
+  const long long HW = (long long)H * W;
+  float* out = pv + b * 10 * HW;
+  float lmn = __uint_as_float(0x7f800000u), lmx = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) {
+    const float2 v = part[(long long)b * nparts + i];
+    lmn = fminf(lmn, v.x);
+    lmx = fmaxf(lmx, v.y);
+  }
+  lmn = wave_min(lmn);
+  lmx = -wave_min(-lmx);
+  __shared__ float smn[4], smx[4];
+  if ((threadIdx.x & 63) == 0) {
+    smn[threadIdx.x >> 6] = lmn;
+    smx[threadIdx.x >> 6] = lmx;
+  }
+  __syncthreads();
+  const float mn = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+  const float mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+  const uint32_t mnb = __float_as_uint(mn);
+  const bool scale = (mnb != 0x7f800000u) && (mx > mn);  // :1285-1293
+  const float den = __fsub_rn(mx, mn);
+  for (long long p = (blockIdx.x * 256ll + threadIdx.x) * 4; p < HW; p += 1024ll * gridDim.x) {
+    const float4 m = *reinterpret_cast<const float4*>(out + 6 * HW + p);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (scale)
+      v = make_float4(div_rn(__fsub_rn(m.x, mn), den), div_rn(__fsub_rn(m.y, mn), den),
+                      div_rn(__fsub_rn(m.z, mn), den), div_rn(__fsub_rn(m.w, mn), den));
+    *reinterpret_cast<float4*>(out + 6 * HW + p) = v;
+    *reinterpret_cast<float4*>(out + 7 * HW + p) = v;
+    *reinterpret_cast<float4*>(out + 8 * HW + p) = v;
+  }
+}
+
 // ------------------------------------------------------------------ K2 fusion
 struct Gate {
   float g[3];
@@ -449,7 +563,11 @@ void launch_bwd(const void* dout, const float* grad, const float* mask, long lon
 
 extern "C" {
 
-size_t rgbd_assemble_workspace_size(int B) { return align256(sizeof(PrepWs) * (size_t)(B > 0 ? B : 1)); }
+constexpr int kPrepMaxParts = 1024;  // pass-1 blocks per image (quad path)
+size_t rgbd_assemble_workspace_size(int B) {
+  const size_t nb = (size_t)(B > 0 ? B : 1);
+  return align256(sizeof(PrepWs) * nb) + align256(sizeof(float2) * kPrepMaxParts * nb);
+}
 
 int rgbd_assemble_pixel_values(const uint8_t* rgb_u8, const uint8_t* depth_u8, int B, int H, int W,
                                float* pv, void* ws, void* stream) {
@@ -458,12 +576,21 @@ int rgbd_assemble_pixel_values(const uint8_t* rgb_u8, const uint8_t* depth_u8, i
   hipStream_t s = (hipStream_t)stream;
   PrepWs* w = (PrepWs*)ws;
   TimerScope ts("assemble", s);
-  k_prep_init<<<ceil_div(B, 64), 64, 0, s>>>(w, B);
   const long long HW = (long long)H * W;
   RGBD_REQUIRE(HW < (1ll << 31), RGBD_E_SHAPE);
-  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 128), B);
-  k_prep_pass1<<<grid, 256, 0, s>>>(rgb_u8, depth_u8, H, W, pv, w);
-  k_prep_pass2<<<grid, 256, 0, s>>>(H, W, pv, w);
+  if (W % 4 == 0 && ((uintptr_t)pv & 15) == 0 && ((uintptr_t)depth_u8 & 3) == 0 && ((uintptr_t)rgb_u8 & 3) == 0) {
+    const int nparts = (int)std::min<long long>(std::min<long long>(ceil_div(HW / 4, 256), std::max(2048 / B, 16)),
+                                                kPrepMaxParts);
+    float2* part = (float2*)((char*)ws + align256(sizeof(PrepWs) * (size_t)B));
+    dim3 grid((unsigned)nparts, B);
+    k_prep_pass1_q<<<grid, 256, 0, s>>>(rgb_u8, depth_u8, H, W, pv, part);
+    k_prep_pass2_q<<<grid, 256, 0, s>>>(H, W, pv, part, nparts);
+  } else {
+    k_prep_init<<<ceil_div(B, 64), 64, 0, s>>>(w, B);
+    dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 128), B);
+    k_prep_pass1<<<grid, 256, 0, s>>>(rgb_u8, depth_u8, H, W, pv, w);
+    k_prep_pass2<<<grid, 256, 0, s>>>(H, W, pv, w);
+  }
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

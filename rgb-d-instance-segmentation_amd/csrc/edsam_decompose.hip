@@ -26,6 +26,7 @@ namespace {
 struct DecWs {
   uint32_t min_key, max_key;
 };
+constexpr int kDecParts = 128;  // blocks per image of the min/max and histogram passes
 
 __device__ __forceinline__ float grey_at(const float* __restrict__ d, long long HW, long long p, int nch) {
   if (nch == 1) return d[p];  // already grey (DSAModule called with a 1-channel depth map)
@@ -76,8 +77,10 @@ __global__ void k_init(DecWs* ws, rgbd_decomp_info* info, int B) {
   for (int i = threadIdx.x; i < RGBD_NBINS; i += blockDim.x) info[b].hist[i] = 0;
 }
 
+// One (min, max) key pair per block into part[b][blockIdx.x]; k_hist reduces them (the 96
+// blocks x 8 images of same-line atomics this replaced serialised for ~20 us).
 __global__ __launch_bounds__(256) void k_grey_minmax(const float* __restrict__ depth3, long long bstride,
-                                                     long long HW, int nch, DecWs* ws) {
+                                                     long long HW, int nch, uint2* __restrict__ part) {
   const int b = blockIdx.y;
   const float* d = depth3 + b * bstride;
   uint32_t kmin = 0xffffffffu, kmax = 0u;
@@ -99,17 +102,43 @@ __global__ __launch_bounds__(256) void k_grey_minmax(const float* __restrict__ d
     rmax[threadIdx.x >> 6] = kmax;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // one atomic pair per block (same-address atomics serialise)
-    atomicMin(&ws[b].min_key, min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3])));
-    atomicMax(&ws[b].max_key, max(max(rmax[0], rmax[1]), max(rmax[2], rmax[3])));
+  if (threadIdx.x == 0)
+    part[(long long)b * gridDim.x + blockIdx.x] =
+        make_uint2(min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3])), max(max(rmax[0], rmax[1]), max(rmax[2], rmax[3])));
+}
+
+// Block-level reduction of an image's min/max partials (every k_hist block needs the range).
+__device__ __forceinline__ DecWs reduce_parts(const uint2* __restrict__ part, int nparts) {
+  uint32_t kmin = 0xffffffffu, kmax = 0u;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    const uint2 v = part[i];
+    kmin = min(kmin, v.x);
+    kmax = max(kmax, v.y);
   }
+  for (int o = 32; o > 0; o >>= 1) {
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+  }
+  __shared__ uint32_t rmin[4], rmax[4];
+  if ((threadIdx.x & 63) == 0) {
+    rmin[threadIdx.x >> 6] = kmin;
+    rmax[threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  DecWs w;
+  w.min_key = min(min(rmin[0], rmin[1]), min(rmin[2], rmin[3]));
+  w.max_key = max(max(rmax[0], rmax[1]), max(rmax[2], rmax[3]));
+  return w;
 }
 
 __global__ __launch_bounds__(256) void k_hist(const float* __restrict__ depth3, long long bstride,
-                                              long long HW, int nch, const DecWs* ws, rgbd_decomp_info* info) {
+                                              long long HW, int nch, const uint2* __restrict__ part, DecWs* ws,
+                                              rgbd_decomp_info* info) {
   __shared__ uint32_t h[RGBD_NBINS];
   const int b = blockIdx.y;
-  const Range r = make_range(ws[b]);
+  const DecWs mm = reduce_parts(part + (long long)b * gridDim.x, gridDim.x);
+  if (blockIdx.x == 0 && threadIdx.x == 0) ws[b] = mm;  // for k_peaks / k_codes_pool
+  const Range r = make_range(mm);
   if (r.status != 0) return;  // uniform per block
   for (int i = threadIdx.x; i < RGBD_NBINS; i += 256) h[i] = 0;
   __syncthreads();
@@ -313,7 +342,10 @@ __global__ __launch_bounds__(256) void k_codes_or_pool(const uint8_t* __restrict
 
 extern "C" {
 
-size_t rgbd_edsam_decompose_workspace_size(int B) { return align256(sizeof(DecWs) * (size_t)(B > 0 ? B : 1)); }
+size_t rgbd_edsam_decompose_workspace_size(int B) {
+  const size_t nb = (size_t)(B > 0 ? B : 1);
+  return align256(sizeof(DecWs) * nb) + align256(sizeof(uint2) * kDecParts * nb);
+}
 
 int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
                          const float* ratio, int n_scales, const int* out_h_host,
@@ -333,9 +365,10 @@ int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_
   const long long HW = (long long)H * W;
   TimerScope ts("decompose", st);
   k_init<<<B, 256, 0, st>>>(w, info, B);
-  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), 96), B);
-  k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w);
-  k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, w, info);
+  dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), kDecParts), B);
+  uint2* part = (uint2*)((char*)ws + align256(sizeof(DecWs) * (size_t)B));
+  k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part);
+  k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, w, info);
   k_peaks<<<B, 512, 0, st>>>(w, ratio, info);
   for (int s = 0; s < n_scales; ++s) {
     const int oh = out_h_host[s], ow = out_w_host[s];
