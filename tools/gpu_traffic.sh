@@ -13,4 +13,10 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "SQ_V
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/traffic/p$i" -o run --output-format csv -- python3 "$R/tools/micro_dsam.py" --iters 2 > "$R/gpurun_out/traffic/p$i.log" 2>&1 || { echo "pmc pass $i ($grp) failed"; tail -5 "$R/gpurun_out/traffic/p$i.log"; exit 1; }
 done
+# f1 mask-predictor kernels at the C2 shape
+j=0
+for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+  j=$((j+1))
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/traffic/m$j" -o run --output-format csv -- python3 "$R/tools/micro_mask.py" --iters 2 --no-torch > "$R/gpurun_out/traffic/m$j.log" 2>&1 || { echo "mask pmc pass $j ($grp) failed"; tail -5 "$R/gpurun_out/traffic/m$j.log"; exit 1; }
+done
 echo done

@@ -27,6 +27,14 @@ def timeit(fn, iters=50, warm=5):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--no-torch", action="store_true", help="skip the torch reference timings (PMC passes)")
+    args = ap.parse_args()
+    global timeit
+    _t = timeit
+    timeit = lambda fn: _t(fn, iters=args.iters, warm=min(5, args.iters))  # noqa: E731
     B, Q, C, H, W = 8, 100, 256, 120, 160
     P = H * W
     for dt in (torch.bfloat16, torch.float32):
@@ -34,7 +42,7 @@ def main():
         emb = torch.randn((B, Q, C), device="cuda").to(dt)
         pix = torch.randn((B, C, H, W), device="cuda").to(dt)
         t_hip = timeit(lambda: ops.mask_logits(emb, pix))
-        t_ref = timeit(lambda: torch.einsum("bqc,bchw->bqhw", emb, pix))
+        t_ref = 0.0 if args.no_torch else timeit(lambda: torch.einsum("bqc,bchw->bqhw", emb, pix))
         nbytes = B * P * (C + Q) * es + B * Q * C * es
         print(json.dumps({"kernel": "k_mask_logits", "dtype": str(dt), "us": round(t_hip, 2),
                           "GB/s": round(nbytes / t_hip / 1e3, 1), "frac_hbm": round(nbytes / t_hip / 1e3 / 8000, 3),
@@ -42,7 +50,7 @@ def main():
         logits = torch.randn((B, Q, H, W), device="cuda").to(dt)
         for size in [(60, 80), (30, 40), (15, 20)]:
             t_hip = timeit(lambda: ops.mask_attention(logits, size, 8))
-            t_ref = timeit(lambda: (F.interpolate(logits, size=size, mode="bilinear", align_corners=False)
+            t_ref = 0.0 if args.no_torch else timeit(lambda: (F.interpolate(logits, size=size, mode="bilinear", align_corners=False)
                                     .sigmoid().flatten(2).unsqueeze(1).repeat(1, 8, 1, 1).flatten(0, 1) < 0.5).bool())
             print(json.dumps({"kernel": "k_mask_attention", "dtype": str(dt), "target": size, "us": round(t_hip, 2),
                               "torch_us": round(t_ref, 2)}))

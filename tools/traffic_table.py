@@ -10,7 +10,7 @@ import collections, csv, glob, json, os, sys
 
 root, out = sys.argv[1], sys.argv[2]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for path in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
+for path in sorted(glob.glob(os.path.join(root, "[pm]*", "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(path)):
         n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         agg[(n, r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
