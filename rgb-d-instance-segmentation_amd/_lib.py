@@ -5,11 +5,13 @@ There is no fallback: if the library is missing or fails to load, every op raise
 one the library binds to — one HIP runtime per process.
 """
 import ctypes
+import os
 from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "librgbd_hip.so"
+# RGBD_HIP_LIB overrides the in-tree library (A/B timing of two builds on one box)
+LIB_PATH = Path(os.environ.get("RGBD_HIP_LIB", Path(__file__).resolve().parent / "librgbd_hip.so"))
 
 RGBD_F32 = 0
 RGBD_BF16 = 1
