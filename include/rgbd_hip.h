@@ -183,6 +183,19 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        float* ratio, void* ws, void* stream);
 
+/* ---------------------------------------------------------------- f3 matcher assignment
+ * Replaces scipy.optimize.linear_sum_assignment(cost_matrix.cpu()) in
+ * Mask2FormerHungarianMatcher.forward (transformers 5.15 modeling_mask2former.py:474): a batch of
+ * n cost matrices (float32, row-major, at cost + meta[4k+0], meta[4k+1] rows x meta[4k+2] cols;
+ * meta is a DEVICE int64 [n][4]) solved with scipy 1.15's shortest-augmenting-path algorithm in
+ * float64, one wavefront per matrix, same optimum as scipy including ties.  Outputs (int64,
+ * min(rows, cols) each, at rows_out / cols_out + meta[4k+3]) are scipy's (row_ind, col_ind);
+ * status[k] = 0 ok, 1 infeasible, 2 NaN / -inf entries (scipy's ValueErrors).
+ * max(max_rows, max_cols) <= 2048. */
+size_t rgbd_lsa_lds_bytes(int max_rows, int max_cols);
+int rgbd_lsa_batch(int n, const float* cost, const long long* meta, int max_rows, int max_cols,
+                   int64_t* rows_out, int64_t* cols_out, int* status, void* stream);
+
 /* ---------------------------------------------------------------- f1 mask predictor
  * Replaces the dense work of Mask2FormerMaskPredictor.forward (transformers 5.15
  * modeling_mask2former.py:2040-2056; called 10x per forward from :1896 and :1929).

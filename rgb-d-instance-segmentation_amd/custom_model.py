@@ -17,7 +17,7 @@ from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation,
 from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
                                                                   Mask2FormerPixelLevelModuleOutput)
 
-from . import mask_predictor
+from . import mask_predictor, matcher
 from .hot_path import hot_path
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
@@ -112,6 +112,8 @@ class CustomMask2FormerForUniversalSegmentation(Mask2FormerForUniversalSegmentat
         super().__init__(config)
         set_seed(42)                                                    # Q17: after HF init
         self.model = CustomMask2FormerModel(config, version=version)
+        # f3: the loss's Hungarian matcher solves its assignments on the GPU (no host round trip)
+        matcher.install(self.criterion)
 
     def set_compute_dtype(self, dtype):
         self.model.pixel_level_module.set_compute_dtype(dtype)

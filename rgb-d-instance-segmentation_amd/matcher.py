@@ -1,0 +1,66 @@
+"""f3: the Mask2Former Hungarian matcher without the host round trip.
+
+Reference: ``Mask2FormerHungarianMatcher.forward`` (transformers 5.15 modeling_mask2former.py:
+412-483), used by ``Mask2FormerLoss`` (:762) for the final and every auxiliary decoder output.
+Per image it builds the (queries x targets) cost — class probability, point-sampled sigmoid-CE and
+dice — and calls ``scipy.optimize.linear_sum_assignment(cost_matrix.cpu())``: one device->host
+sync and one CPU solve per image per output.
+
+``HipHungarianMatcher`` keeps the cost construction op for op (same torch calls in the same
+order, so the same ``torch.rand`` draws and bit-identical cost matrices) and solves all images'
+matrices in one ``rgbd_lsa_batch`` launch (csrc/lsap.hip: scipy's algorithm in float64, same
+optimum including ties).  The matched indices stay on the GPU as int64 tensors, which the loss
+indexes with directly.  ``install(model)`` swaps the class of every HF matcher in place.
+"""
+import torch
+from torch import nn
+from transformers.models.mask2former.modeling_mask2former import (Mask2FormerHungarianMatcher,
+                                                                  pair_wise_dice_loss,
+                                                                  pair_wise_sigmoid_cross_entropy_loss,
+                                                                  sample_point)
+
+from . import ops
+
+
+def matching_cost(matcher, masks_queries_logits, class_queries_logits, mask_labels, class_labels, i):
+    """Cost matrix of image i, as the reference builds it (modeling_mask2former.py:445-470)."""
+    probs = class_queries_logits[i].softmax(-1)
+    pred = masks_queries_logits[i]
+    c_class = -probs[:, class_labels[i]]
+    tgt = mask_labels[i].to(pred)[:, None]
+    pred = pred[:, None]
+    pts = torch.rand(1, matcher.num_points, 2, device=pred.device)
+    tgt = sample_point(tgt, pts.repeat(tgt.shape[0], 1, 1), align_corners=False).squeeze(1)
+    pred = sample_point(pred, pts.repeat(pred.shape[0], 1, 1), align_corners=False).squeeze(1)
+    c_mask = pair_wise_sigmoid_cross_entropy_loss(pred, tgt)
+    c_dice = pair_wise_dice_loss(pred, tgt)
+    cost = matcher.cost_mask * c_mask + matcher.cost_class * c_class + matcher.cost_dice * c_dice
+    cost = torch.minimum(cost, torch.tensor(1e10))
+    cost = torch.maximum(cost, torch.tensor(-1e10))
+    return torch.nan_to_num(cost, 0)
+
+
+class HipHungarianMatcher(Mask2FormerHungarianMatcher):
+    @torch.no_grad()
+    def forward(self, masks_queries_logits, class_queries_logits, mask_labels, class_labels):
+        costs = [matching_cost(self, masks_queries_logits, class_queries_logits, mask_labels, class_labels, i)
+                 for i in range(masks_queries_logits.shape[0])]
+        return ops.linear_sum_assignment_batch(costs)
+
+
+def install(model: nn.Module) -> int:
+    n = 0
+    for m in model.modules():
+        if type(m) is Mask2FormerHungarianMatcher:
+            m.__class__ = HipHungarianMatcher
+            n += 1
+    return n
+
+
+def uninstall(model: nn.Module) -> int:
+    n = 0
+    for m in model.modules():
+        if type(m) is HipHungarianMatcher:
+            m.__class__ = Mask2FormerHungarianMatcher
+            n += 1
+    return n

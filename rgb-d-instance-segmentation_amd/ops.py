@@ -334,3 +334,47 @@ def mask_attention(logits: torch.Tensor, size, heads: int) -> torch.Tensor:
     check(_lib.lib().rgbd_mask_attention(_dtype_code(logits), _p(logits), B, Q, H, W, th, tw, int(heads),
                                          _p(attn), _stream(logits.device)), "rgbd_mask_attention")
     return attn
+
+
+# ------------------------------------------------------------------ f3 matcher assignment
+def linear_sum_assignment_batch(costs, validate=False):
+    """scipy.optimize.linear_sum_assignment for a list of 2-D float32 CUDA cost matrices in one
+    launch (rgbd_lsa_batch).  Returns [(row_ind, col_ind)] as int64 CUDA tensors, scipy's order.
+    Nothing synchronises unless ``validate`` (then a status read-back raises scipy's ValueErrors)."""
+    if not costs:
+        return []
+    dev = costs[0].device
+    flat, meta, coff, ooff, mr, mc = [], [], 0, 0, 0, 0
+    for c in costs:
+        if c.dim() != 2:
+            raise ValueError("cost matrix must be 2-D")
+        c = c.detach().float().contiguous()
+        _need_cuda(c)
+        r, k = c.shape
+        meta += [coff, r, k, ooff]
+        flat.append(c.reshape(-1))
+        coff += r * k
+        ooff += min(r, k)
+        mr, mc = max(mr, r), max(mc, k)
+    if max(mr, mc) > 2048:
+        raise ValueError("rgbd_lsa_batch: matrices up to 2048 on a side")
+    cost = torch.cat(flat) if coff > 0 else torch.zeros(1, dtype=torch.float32, device=dev)
+    meta_t = torch.tensor(meta, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    rows = torch.empty(max(ooff, 1), dtype=torch.int64, device=dev)
+    cols = torch.empty(max(ooff, 1), dtype=torch.int64, device=dev)
+    status = torch.empty(len(costs), dtype=torch.int32, device=dev)
+    check(_lib.lib().rgbd_lsa_batch(len(costs), _p(cost), _p(meta_t), mr, mc, _p(rows), _p(cols), _p(status),
+                                    _stream(dev)), "rgbd_lsa_batch")
+    if validate:
+        st = status.cpu().tolist()
+        for s in st:
+            if s == 1:
+                raise ValueError("cost matrix is infeasible")
+            if s == 2:
+                raise ValueError("matrix contains invalid numeric entries")
+    out, o = [], 0
+    for i in range(len(costs)):
+        n = int(min(meta[4 * i + 1], meta[4 * i + 2]))
+        out.append((rows[o:o + n], cols[o:o + n]))
+        o += n
+    return out

@@ -19,8 +19,9 @@ def _model():
     m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
     missing = winit.init_deterministic(m)
     assert not missing.unexpected_keys
-    from rgbd_amd import mask_predictor
-    mask_predictor.uninstall(m)  # CPU oracle run: the reference HF mask predictor
+    from rgbd_amd import mask_predictor, matcher
+    mask_predictor.uninstall(m)  # CPU oracle run: the reference HF mask predictor and matcher
+    matcher.uninstall(m)
     return m
 
 
