@@ -183,6 +183,21 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        float* ratio, void* ws, void* stream);
 
+/* ---------------------------------------------------------------- f2 deformable attention
+ * Replaces multi_scale_deformable_attention (transformers 5.15 modeling_mask2former.py:798-837),
+ * the core of each pixel-decoder encoder layer (:1011).  value: dtype [B][S][NH][D] with
+ * S = sum of the L level sizes; shapes_host: host int [L][2] = (H, W) per level (L <= 4);
+ * loc: float32 [B][Q][NH][L][P][2] sampling locations in [0, 1] (x, y); attw: float32
+ * [B][Q][NH][L][P] softmaxed weights; out: dtype [B][Q][NH*D].  D in {16, 32, 64}.
+ * Bilinear, zero padding, align_corners=False (grid_sample's rule). */
+int rgbd_msda_fwd(int dtype, const void* value, int B, int L, const int* shapes_host, int NH, int D, int Q,
+                  int P, const float* loc, const float* attw, void* out, void* stream);
+/* Backward: gvalue float32 [B][S][NH][D] (zeroed here, then accumulated with atomics), gloc
+ * float32 like loc, gattw float32 like attw (both OVERWRITTEN); gout dtype like out. */
+int rgbd_msda_bwd(int dtype, const void* value, int B, int L, const int* shapes_host, int NH, int D, int Q,
+                  int P, const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
+                  float* gattw, void* stream);
+
 /* ---------------------------------------------------------------- f3 matcher assignment
  * Replaces scipy.optimize.linear_sum_assignment(cost_matrix.cpu()) in
  * Mask2FormerHungarianMatcher.forward (transformers 5.15 modeling_mask2former.py:474): a batch of

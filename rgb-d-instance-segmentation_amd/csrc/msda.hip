@@ -1,0 +1,223 @@
+// f2: the pixel decoder's multi-scale deformable attention core on gfx950.
+//
+// Reference: multi_scale_deformable_attention (transformers 5.15 modeling_mask2former.py:798-837),
+// called by Mask2FormerPixelDecoderEncoderMultiscaleDeformableAttention.forward (:1011) in each of
+// the 6 pixel-decoder encoder layers.  The reference splits the value per level, runs one
+// grid_sample per level over a [B*heads, D, H, W] re-layout of it (a transposed copy of the value
+// per level), stacks the samples [B*heads, D, Q, L*P], multiplies by the attention weights and sums.
+//
+// Here one launch does all levels and points: a group of D lanes (D = head dim, 32 for the
+// reference config) owns one (image, query, head); lane c keeps channel c.  Per (level, point) the
+// group computes the bilinear source position once (grid = 2*loc - 1, ix = ((grid + 1) * W - 1) / 2,
+// grid_sample's align_corners=False rule with zero padding), reads the four taps as D contiguous
+// channels of the [B][S][heads][D] value (one 128-byte line per tap in f32), and accumulates
+// weight * sample in registers — no per-level copy, no [.., Q, L*P] intermediate.
+// Backward: per (level, point) the group reduces go . sample (attention-weight gradient) and
+// go . d sample / d(ix, iy) (sampling-location gradient) over its lanes with shuffles, and scatters
+// weight * tap weight * go into the value gradient with float atomics (as grid_sample's backward
+// does).  Bound: gather / L2 latency (the value of a level is at most a few MB per image).
+#include "common.hpp"
+
+namespace rgbd {
+namespace {
+
+constexpr int MSDA_MAX_L = 4;
+
+struct MsdaLevels {
+  int L;
+  int H[MSDA_MAX_L], W[MSDA_MAX_L], start[MSDA_MAX_L];
+};
+
+struct Tap {
+  int idx[4];     // spatial index within the level, -1 when outside (zero padding)
+  float w[4];     // bilinear weights (x0y0, x1y0, x0y1, x1y1)
+  float lx, ly;   // fractional parts (for the location gradient)
+};
+
+__device__ __forceinline__ Tap msda_tap(float locx, float locy, int H, int W) {
+  // grid_sample(align_corners=False): grid = 2*loc - 1 (computed by the reference in the tensor
+  // op), unnormalised with ((grid + 1) * size - 1) / 2
+  const float gx = 2.f * locx - 1.f, gy = 2.f * locy - 1.f;
+  // clamped into [-2, size + 1]: beyond that all four taps are padding either way, and the
+  // float -> int conversion stays defined
+  const float ix = fminf(fmaxf(((gx + 1.f) * (float)W - 1.f) / 2.f, -2.f), (float)W + 1.f);
+  const float iy = fminf(fmaxf(((gy + 1.f) * (float)H - 1.f) / 2.f, -2.f), (float)H + 1.f);
+  const float fx = floorf(ix), fy = floorf(iy);
+  const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+  Tap t;
+  t.lx = ix - fx;
+  t.ly = iy - fy;
+  const float wx0 = 1.f - t.lx, wy0 = 1.f - t.ly;
+  t.w[0] = wx0 * wy0;
+  t.w[1] = t.lx * wy0;
+  t.w[2] = wx0 * t.ly;
+  t.w[3] = t.lx * t.ly;
+  const bool vx0 = x0 >= 0 && x0 < W, vx1 = x1 >= 0 && x1 < W, vy0 = y0 >= 0 && y0 < H, vy1 = y1 >= 0 && y1 < H;
+  t.idx[0] = vx0 && vy0 ? y0 * W + x0 : -1;
+  t.idx[1] = vx1 && vy0 ? y0 * W + x1 : -1;
+  t.idx[2] = vx0 && vy1 ? y1 * W + x0 : -1;
+  t.idx[3] = vx1 && vy1 ? y1 * W + x1 : -1;
+  return t;
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_msda_fwd(const T* __restrict__ value, MsdaLevels lv, int S, int Q, int NH,
+                                                  int P, const float* __restrict__ loc, const float* __restrict__ attw,
+                                                  long long nqh, T* __restrict__ out) {
+  const int c = threadIdx.x % D;
+  const long long qh = (long long)blockIdx.x * (256 / D) + threadIdx.x / D;
+  if (qh >= nqh) return;
+  const int h = (int)(qh % NH);
+  const long long bq = qh / NH;
+  const long long b = bq / Q;
+  const float* lq = loc + qh * lv.L * P * 2;
+  const float* wq = attw + qh * lv.L * P;
+  const T* vb = value + b * S * NH * D + (long long)h * D + c;
+  float acc = 0.f;
+  for (int l = 0; l < lv.L; ++l) {
+    const int H = lv.H[l], W = lv.W[l];
+    const T* vl = vb + (long long)lv.start[l] * NH * D;
+    for (int p = 0; p < P; ++p) {
+      const int k = l * P + p;
+      const Tap t = msda_tap(lq[2 * k], lq[2 * k + 1], H, W);
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (t.idx[e] >= 0) s += t.w[e] * Num<T>::to_f(vl[(long long)t.idx[e] * NH * D]);
+      acc += wq[k] * s;
+    }
+  }
+  out[qh * D + c] = Num<T>::from_f(acc);
+}
+
+template <int D>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = D / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void k_msda_bwd(const T* __restrict__ value, MsdaLevels lv, int S, int Q, int NH,
+                                                  int P, const float* __restrict__ loc, const float* __restrict__ attw,
+                                                  const T* __restrict__ gout, long long nqh, float* __restrict__ gvalue,
+                                                  float* __restrict__ gloc, float* __restrict__ gattw) {
+  const int c = threadIdx.x % D;
+  const long long qh = (long long)blockIdx.x * (256 / D) + threadIdx.x / D;
+  // every lane of a group takes part in the shuffles: out-of-range groups run with zero weight
+  const bool live = qh < nqh;
+  const long long q0 = live ? qh : 0;
+  const int h = (int)(q0 % NH);
+  const long long b = (q0 / NH) / Q;
+  const float* lq = loc + q0 * lv.L * P * 2;
+  const float* wq = attw + q0 * lv.L * P;
+  const long long voff = b * S * NH * D + (long long)h * D + c;
+  const T* vb = value + voff;
+  float* gvb = gvalue + voff;
+  const float go = live ? Num<T>::to_f(gout[q0 * D + c]) : 0.f;
+  for (int l = 0; l < lv.L; ++l) {
+    const int H = lv.H[l], W = lv.W[l];
+    const long long lo = (long long)lv.start[l] * NH * D;
+    for (int p = 0; p < P; ++p) {
+      const int k = l * P + p;
+      const Tap t = msda_tap(lq[2 * k], lq[2 * k + 1], H, W);
+      const float a = wq[k];
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = t.idx[e] >= 0 ? Num<T>::to_f(vb[lo + (long long)t.idx[e] * NH * D]) : 0.f;
+      const float s = t.w[0] * v[0] + t.w[1] * v[1] + t.w[2] * v[2] + t.w[3] * v[3];
+      // d sample / d ix, d iy (zero-padded taps are zeros)
+      const float dsx = (1.f - t.ly) * (v[1] - v[0]) + t.ly * (v[3] - v[2]);
+      const float dsy = (1.f - t.lx) * (v[2] - v[0]) + t.lx * (v[3] - v[1]);
+      const float gw = group_sum<D>(go * s);
+      const float gx = group_sum<D>(go * dsx);
+      const float gy = group_sum<D>(go * dsy);
+      if (live) {
+        if (c == 0) {
+          gattw[q0 * lv.L * P + k] = gw;
+          // ix = loc * W - 1/2 through grid = 2 loc - 1: d ix / d loc = W
+          gloc[(q0 * lv.L * P + k) * 2] = a * gx * (float)W;
+          gloc[(q0 * lv.L * P + k) * 2 + 1] = a * gy * (float)H;
+        }
+        const float ga = a * go;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (t.idx[e] >= 0) atomicAdd(gvb + lo + (long long)t.idx[e] * NH * D, ga * t.w[e]);
+      }
+    }
+  }
+}
+
+int msda_levels(int L, const int* shapes_host, MsdaLevels& lv, int& S) {
+  if (L < 1 || L > MSDA_MAX_L || !shapes_host) return RGBD_E_SHAPE;
+  lv.L = L;
+  S = 0;
+  for (int l = 0; l < L; ++l) {
+    lv.H[l] = shapes_host[2 * l];
+    lv.W[l] = shapes_host[2 * l + 1];
+    if (lv.H[l] <= 0 || lv.W[l] <= 0) return RGBD_E_SHAPE;
+    lv.start[l] = S;
+    S += lv.H[l] * lv.W[l];
+  }
+  return RGBD_OK;
+}
+
+}  // namespace
+}  // namespace rgbd
+
+using namespace rgbd;
+
+extern "C" int rgbd_msda_fwd(int dtype, const void* value, int B, int L, const int* shapes_host, int NH, int D,
+                             int Q, int P, const float* loc, const float* attw, void* out, void* stream) {
+  RGBD_REQUIRE(value && loc && attw && out && B > 0 && NH > 0 && Q > 0 && P > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(D == 16 || D == 32 || D == 64, RGBD_E_SHAPE);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  MsdaLevels lv;
+  int S = 0;
+  const int rc = msda_levels(L, shapes_host, lv, S);
+  if (rc) return rc;
+  const long long nqh = (long long)B * Q * NH;
+  const dim3 grid((unsigned)ceil_div(nqh, 256 / D));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_F32) {
+    if (D == 32) k_msda_fwd<float, 32><<<grid, 256, 0, s>>>((const float*)value, lv, S, Q, NH, P, loc, attw, nqh, (float*)out);
+    else if (D == 64) k_msda_fwd<float, 64><<<grid, 256, 0, s>>>((const float*)value, lv, S, Q, NH, P, loc, attw, nqh, (float*)out);
+    else k_msda_fwd<float, 16><<<grid, 256, 0, s>>>((const float*)value, lv, S, Q, NH, P, loc, attw, nqh, (float*)out);
+  } else {
+    if (D == 32) k_msda_fwd<bf16_t, 32><<<grid, 256, 0, s>>>((const bf16_t*)value, lv, S, Q, NH, P, loc, attw, nqh, (bf16_t*)out);
+    else if (D == 64) k_msda_fwd<bf16_t, 64><<<grid, 256, 0, s>>>((const bf16_t*)value, lv, S, Q, NH, P, loc, attw, nqh, (bf16_t*)out);
+    else k_msda_fwd<bf16_t, 16><<<grid, 256, 0, s>>>((const bf16_t*)value, lv, S, Q, NH, P, loc, attw, nqh, (bf16_t*)out);
+  }
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+extern "C" int rgbd_msda_bwd(int dtype, const void* value, int B, int L, const int* shapes_host, int NH, int D,
+                             int Q, int P, const float* loc, const float* attw, const void* gout, float* gvalue,
+                             float* gloc, float* gattw, void* stream) {
+  RGBD_REQUIRE(value && loc && attw && gout && gvalue && gloc && gattw && B > 0 && NH > 0 && Q > 0 && P > 0,
+               RGBD_E_ARG);
+  RGBD_REQUIRE(D == 16 || D == 32 || D == 64, RGBD_E_SHAPE);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  MsdaLevels lv;
+  int S = 0;
+  const int rc = msda_levels(L, shapes_host, lv, S);
+  if (rc) return rc;
+  const long long nqh = (long long)B * Q * NH;
+  hipStream_t s = (hipStream_t)stream;
+  // the value gradient is accumulated with atomics: zero it first (stream-ordered)
+  const hipError_t e = hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * NH * D, s);
+  if (e != hipSuccess) return (int)e;
+  const dim3 grid((unsigned)ceil_div(nqh, 256 / D));
+  if (dtype == RGBD_F32) {
+    if (D == 32) k_msda_bwd<float, 32><<<grid, 256, 0, s>>>((const float*)value, lv, S, Q, NH, P, loc, attw, (const float*)gout, nqh, gvalue, gloc, gattw);
+    else if (D == 64) k_msda_bwd<float, 64><<<grid, 256, 0, s>>>((const float*)value, lv, S, Q, NH, P, loc, attw, (const float*)gout, nqh, gvalue, gloc, gattw);
+    else k_msda_bwd<float, 16><<<grid, 256, 0, s>>>((const float*)value, lv, S, Q, NH, P, loc, attw, (const float*)gout, nqh, gvalue, gloc, gattw);
+  } else {
+    if (D == 32) k_msda_bwd<bf16_t, 32><<<grid, 256, 0, s>>>((const bf16_t*)value, lv, S, Q, NH, P, loc, attw, (const bf16_t*)gout, nqh, gvalue, gloc, gattw);
+    else if (D == 64) k_msda_bwd<bf16_t, 64><<<grid, 256, 0, s>>>((const bf16_t*)value, lv, S, Q, NH, P, loc, attw, (const bf16_t*)gout, nqh, gvalue, gloc, gattw);
+    else k_msda_bwd<bf16_t, 16><<<grid, 256, 0, s>>>((const bf16_t*)value, lv, S, Q, NH, P, loc, attw, (const bf16_t*)gout, nqh, gvalue, gloc, gattw);
+  }
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}

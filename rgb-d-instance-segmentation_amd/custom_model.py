@@ -17,7 +17,7 @@ from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation,
 from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
                                                                   Mask2FormerPixelLevelModuleOutput)
 
-from . import mask_predictor, matcher
+from . import deform_attn, mask_predictor, matcher
 from .hot_path import hot_path
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
@@ -102,6 +102,8 @@ class CustomMask2FormerModel(Mask2FormerModel):
         # f1: mask einsum + attention-mask binarisation of the masked-attention decoder on the
         # HIP kernels (class swap: parameters and state_dict keys unchanged)
         mask_predictor.install(self.transformer_module)
+        # f2: the pixel decoder's deformable-attention core on the fused HIP gather kernels
+        deform_attn.install(self.pixel_level_module.decoder)
 
 
 class CustomMask2FormerForUniversalSegmentation(Mask2FormerForUniversalSegmentation):

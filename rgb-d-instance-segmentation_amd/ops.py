@@ -378,3 +378,45 @@ def linear_sum_assignment_batch(costs, validate=False):
         out.append((rows[o:o + n], cols[o:o + n]))
         o += n
     return out
+
+
+# ------------------------------------------------------------------ f2 deformable attention
+def _msda_args(value, shapes, loc, attw):
+    _need_cuda(value, loc, attw)
+    B, S, NH, D = value.shape
+    _, Q, nh2, L, P, two = loc.shape
+    if nh2 != NH or two != 2 or tuple(attw.shape) != (B, Q, NH, L, P) or len(shapes) != L:
+        raise ValueError(f"msda: value {tuple(value.shape)}, loc {tuple(loc.shape)}, attw {tuple(attw.shape)}, "
+                         f"{len(shapes)} levels do not match")
+    if sum(int(h) * int(w) for h, w in shapes) != S:
+        raise ValueError("msda: spatial shapes do not add up to the value length")
+    arr = (ctypes.c_int * (2 * L))(*[int(x) for hw in shapes for x in hw])
+    return B, S, NH, D, Q, L, P, arr
+
+
+def msda_forward(value, shapes, loc, attw):
+    """multi_scale_deformable_attention(value, shapes, loc, attw) (modeling_mask2former.py:798) on
+    the HIP kernel.  value [B,S,NH,D] f32/bf16; loc [B,Q,NH,L,P,2] and attw [B,Q,NH,L,P] float32."""
+    value = value.contiguous()
+    loc = loc.float().contiguous()
+    attw = attw.float().contiguous()
+    B, S, NH, D, Q, L, P, arr = _msda_args(value, shapes, loc, attw)
+    out = torch.empty((B, Q, NH * D), dtype=value.dtype, device=value.device)
+    check(_lib.lib().rgbd_msda_fwd(_dtype_code(value), _p(value), B, L, arr, NH, D, Q, P, _p(loc), _p(attw),
+                                   _p(out), _stream(value.device)), "rgbd_msda_fwd")
+    return out
+
+
+def msda_backward(value, shapes, loc, attw, gout):
+    """-> (grad_value float32 [B,S,NH,D], grad_loc, grad_attw)."""
+    value = value.contiguous()
+    loc = loc.float().contiguous()
+    attw = attw.float().contiguous()
+    gout = gout.to(value.dtype).contiguous()
+    B, S, NH, D, Q, L, P, arr = _msda_args(value, shapes, loc, attw)
+    gv = torch.empty((B, S, NH, D), dtype=torch.float32, device=value.device)
+    gl = torch.empty_like(loc)
+    ga = torch.empty_like(attw)
+    check(_lib.lib().rgbd_msda_bwd(_dtype_code(value), _p(value), B, L, arr, NH, D, Q, P, _p(loc), _p(attw),
+                                   _p(gout), _p(gv), _p(gl), _p(ga), _stream(value.device)), "rgbd_msda_bwd")
+    return gv, gl, ga

@@ -10,7 +10,7 @@ import torch
 
 import golden_inputs as gi
 from oracle import ratio as ratio_o
-from rgbd_amd import init as winit, mask_predictor
+from rgbd_amd import deform_attn, init as winit, mask_predictor
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -119,7 +119,9 @@ def test_full_model_mask_logits_fp32(golden):
       changes (measured: backbone features 5e-6 relative, full-GPU mask logits 2.3e-3).  The
       hot-path parity is therefore measured by running the reference-identical HF stages on the
       CPU from the backbone features the HIP hot path produced on the GPU.
-    The fully-on-GPU end-to-end error is asserted at 1e-2."""
+    With the pixel decoder's deformable attention, the mask predictor and the matcher on the HIP
+    kernels the fully-on-GPU end-to-end error is asserted at 1e-3 too (measured 4.6e-6; the HF
+    grid_sample path gave 2.3e-3 through one flipped attention-mask bit)."""
     g5 = golden("g5_model")
     m = _full_model().eval()
     pv_cpu = torch.from_numpy(gi.pixel_values(1, 1, 240, 320))
@@ -140,7 +142,8 @@ def test_full_model_mask_logits_fp32(golden):
         h2.remove()
     # the same model on the CPU, fed with the GPU hot-path features
     mc = _full_model().cpu().eval()
-    assert mask_predictor.uninstall(mc) == 1  # the reference HF predictor is the CPU checker
+    assert mask_predictor.uninstall(mc) == 1  # the reference HF modules are the CPU checker
+    assert deform_attn.uninstall(mc) == 6
     mc.model.pixel_level_module.hot_path_features = lambda pv_, colors, ratios=None: caps["bb"]
     calls = []
     h3 = mc.model.transformer_module.decoder.mask_predictor.register_forward_hook(
@@ -168,7 +171,7 @@ def test_full_model_mask_logits_fp32(golden):
     gpu = float(np.abs(out_gpu.masks_queries_logits.cpu().numpy() - g5["mask_logits"]).max())
     print(f"mask-logit max-abs-err (fp32): hot path {err:.3g}; everything on the GPU {gpu:.3g}")
     assert err <= 1e-3
-    assert gpu <= 1e-2
+    assert gpu <= 1e-3
     np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-3)
 
 

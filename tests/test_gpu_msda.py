@@ -1,0 +1,87 @@
+"""f2: fused multi-scale deformable attention (csrc/msda.hip) vs the reference's pure-torch
+multi_scale_deformable_attention (transformers 5.15 modeling_mask2former.py:798-837, grid_sample
+per level) on the same inputs, forward and all three gradients, fp32 (and bf16 value)."""
+import pytest
+import torch
+from transformers.models.mask2former.modeling_mask2former import (
+    Mask2FormerPixelDecoderEncoderMultiscaleDeformableAttention, multi_scale_deformable_attention as hf_msda)
+
+from rgbd_amd import deform_attn, ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CASES = [
+    # shapes of the C1 pixel decoder (320x240 input: /8, /16, /32), 8 heads x 32, 4 points
+    (2, [(30, 40), (15, 20), (8, 10)], 8, 32, 4, 1525),
+    # ragged levels, 64-wide heads, queries != value length
+    (1, [(7, 9), (4, 5), (2, 3)], 4, 64, 3, 50),
+    (1, [(16, 12)], 2, 16, 2, 33),
+]
+
+
+def _inputs(B, shapes, NH, D, P, Q, dtype=torch.float32, seed=0, spread=1.4):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    S = sum(h * w for h, w in shapes)
+    L = len(shapes)
+    value = torch.randn((B, S, NH, D), generator=g, device=DEV).to(dtype)
+    # locations partly outside [0, 1] to exercise the zero padding
+    loc = torch.rand((B, Q, NH, L, P, 2), generator=g, device=DEV) * spread - (spread - 1) / 2
+    attw = torch.rand((B, Q, NH, L, P), generator=g, device=DEV)
+    attw = attw / attw.sum(dim=(-1, -2), keepdim=True)
+    return value, loc, attw
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_msda_forward_backward_f32(case):
+    B, shapes, NH, D, P, Q = case
+    value, loc, attw = _inputs(B, shapes, NH, D, P, Q)
+    vr, lr, ar = (t.clone().requires_grad_(True) for t in (value, loc, attw))
+    vh, lh, ah = (t.clone().requires_grad_(True) for t in (value, loc, attw))
+    out_r = hf_msda(vr, shapes, lr, ar)
+    out_h = deform_attn.multi_scale_deformable_attention(vh, shapes, lh, ah)
+    assert out_h.shape == out_r.shape
+    assert float((out_h - out_r).abs().max()) < 2e-5
+    go = torch.randn(out_r.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(9))
+    (out_r * go).sum().backward()
+    (out_h * go).sum().backward()
+    for a, b, name in ((vh.grad, vr.grad, "value"), (lh.grad, lr.grad, "loc"), (ah.grad, ar.grad, "attw")):
+        scale = float(b.abs().max()) + 1e-12
+        err = float((a - b).abs().max()) / scale
+        assert err < 1e-4, (name, err)
+
+
+def test_msda_bf16_value():
+    B, shapes, NH, D, P, Q = CASES[0]
+    value, loc, attw = _inputs(B, shapes, NH, D, P, Q, dtype=torch.bfloat16, seed=3)
+    out = ops.msda_forward(value, shapes, loc, attw)
+    ref = hf_msda(value.float(), shapes, loc, attw)
+    assert out.dtype == torch.bfloat16
+    assert float((out.float() - ref).abs().max()) <= 2.0 ** -7 * float(ref.abs().max()) + 1e-3
+
+
+def test_hip_msda_module_matches_hf():
+    torch.manual_seed(0)
+    ref = Mask2FormerPixelDecoderEncoderMultiscaleDeformableAttention(256, 8, 3, 4).to(DEV)
+    hip = Mask2FormerPixelDecoderEncoderMultiscaleDeformableAttention(256, 8, 3, 4).to(DEV)
+    hip.load_state_dict(ref.state_dict())
+    assert deform_attn.install(hip) == 1
+    shapes = [(30, 40), (15, 20), (8, 10)]
+    S = sum(h * w for h, w in shapes)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    hs = torch.randn((2, S, 256), generator=g, device=DEV)
+    pos = torch.randn((2, S, 256), generator=g, device=DEV) * 0.1
+    refp = torch.rand((2, S, 3, 2), generator=g, device=DEV)
+    starts = torch.tensor([0, 1200, 1500], device=DEV)
+    outs = []
+    for m in (ref, hip):
+        x = hs.clone().requires_grad_(True)
+        o, w = m(x, encoder_hidden_states=x, position_embeddings=pos, reference_points=refp,
+                 spatial_shapes_list=shapes, level_start_index=starts)
+        o.square().mean().backward()
+        outs.append((o.detach(), w.detach(), x.grad, {n: p.grad.clone() for n, p in m.named_parameters()}))
+    (o_r, w_r, gx_r, gp_r), (o_h, w_h, gx_h, gp_h) = outs
+    assert float((o_h - o_r).abs().max()) < 1e-4
+    assert torch.equal(w_h, w_r)
+    assert float((gx_h - gx_r).abs().max()) / float(gx_r.abs().max()) < 1e-4
+    for n in gp_r:
+        assert float((gp_h[n] - gp_r[n]).abs().max()) / (float(gp_r[n].abs().max()) + 1e-12) < 1e-4, n

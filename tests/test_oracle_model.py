@@ -19,9 +19,10 @@ def _model():
     m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
     missing = winit.init_deterministic(m)
     assert not missing.unexpected_keys
-    from rgbd_amd import mask_predictor, matcher
-    mask_predictor.uninstall(m)  # CPU oracle run: the reference HF mask predictor and matcher
+    from rgbd_amd import deform_attn, mask_predictor, matcher
+    mask_predictor.uninstall(m)  # CPU oracle run: the reference HF modules
     matcher.uninstall(m)
+    deform_attn.uninstall(m)
     return m
 
 
