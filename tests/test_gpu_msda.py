@@ -16,6 +16,8 @@ CASES = [
     # ragged levels, 64-wide heads, queries != value length
     (1, [(7, 9), (4, 5), (2, 3)], 4, 64, 3, 50),
     (1, [(16, 12)], 2, 16, 2, 33),
+    # queries = value pixels (the encoder case)
+    (2, [(30, 40), (15, 20), (8, 10)], 8, 32, 4, 1580),
 ]
 
 

@@ -32,7 +32,16 @@ def main():
     S = sum(h * w for h, w in shapes)
     g = torch.Generator(device=dev).manual_seed(0)
     value = torch.randn((B, S, NH, D), generator=g, device=dev).requires_grad_(True)
-    loc = torch.rand((B, S, NH, 3, P, 2), generator=g, device=dev).requires_grad_(True)
+    # encoder-like locations: each query (a value pixel) samples its own neighbourhood on every
+    # level (reference point = its centre, offsets ~ N(0, 2 px) of the sampled level)
+    refs = []
+    for H, W in shapes:
+        ys, xs = torch.meshgrid(torch.arange(H, device=dev), torch.arange(W, device=dev), indexing="ij")
+        refs.append(torch.stack([(xs.reshape(-1) + 0.5) / W, (ys.reshape(-1) + 0.5) / H], -1))
+    ref = torch.cat(refs)
+    norm = torch.tensor([[w, h] for h, w in shapes], device=dev, dtype=torch.float32)
+    off = torch.randn((B, S, NH, 3, P, 2), generator=g, device=dev) * 2.0
+    loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).requires_grad_(True)
     attw = torch.softmax(torch.randn((B, S, NH, 3 * P), generator=g, device=dev), -1).view(B, S, NH, 3, P)
     attw.requires_grad_(True)
     go = torch.randn((B, S, NH * D), generator=g, device=dev)
