@@ -104,6 +104,22 @@ int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const flo
                        const float* weight, const float* bias, float* dweight, float* dbias,
                        void* ws, void* stream);
 
+/* All backbone scales in one launch (the fused hot path calls these): n <= 4 scales given as
+ * host arrays of device pointers and sizes; same arithmetic per element as the single-scale
+ * forms (bitwise identical results).  cp1_host may be NULL (no residual); workspace for the
+ * backward from rgbd_dggm_fuse_bwd_multi_workspace_size. */
+int rgbd_dggm_fuse_fwd_multi(int dtype, int n, const void* const* cp1_host, const void* const* color_host,
+                             void* const* out_host, const float* const* weight_host, const float* const* bias_host,
+                             const int* C_host, const int* h_host, const int* w_host, const float* grad,
+                             const float* mask, long long pv_batch_stride, int B, int H, int W, void* stream);
+size_t rgbd_dggm_fuse_bwd_multi_workspace_size(int n, const int* C_host, const int* h_host, const int* w_host,
+                                               int B);
+int rgbd_dggm_fuse_bwd_multi(int dtype, int n, const void* const* dout_host, const float* const* weight_host,
+                             const float* const* bias_host, float* const* dweight_host, float* const* dbias_host,
+                             const int* C_host, const int* h_host, const int* w_host, const float* grad,
+                             const float* mask, long long pv_batch_stride, int B, int H, int W, void* ws,
+                             void* stream);
+
 /* ---------------------------------------------------------------- layout helpers */
 int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H, int W,
                       void* stream);

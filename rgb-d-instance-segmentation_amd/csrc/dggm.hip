@@ -343,11 +343,11 @@ template <int PX>
 __device__ __forceinline__ TileGates<PX> stage_gates(float (*sg)[512], float4* swb, const float* __restrict__ grad,
                                                      const float* __restrict__ mask, int H, int W, int h,
                                                      int w, int p0, const float* __restrict__ wt,
-                                                     const float* __restrict__ bias, int C) {
+                                                     const float* __restrict__ bias, int C, int by) {
   constexpr int TP = 64 * PX;
   const int hw = h * w;
   if (threadIdx.x < kBlkCh) {
-    const int c = min((int)blockIdx.y * kBlkCh + (int)threadIdx.x, C - 1);
+    const int c = min(by * kBlkCh + (int)threadIdx.x, C - 1);
     swb[threadIdx.x] = make_float4(wt[c * 3 + 0], wt[c * 3 + 1], wt[c * 3 + 2], bias[c]);
   }
 #pragma unroll
@@ -374,20 +374,20 @@ __device__ __forceinline__ TileGates<PX> stage_gates(float (*sg)[512], float4* s
   return t;
 }
 
+// One (pixel tile bx, 32-channel block by) of the fused forward; the kernels below map block
+// indices onto it (one scale per launch, or all scales in one launch).
 template <typename T, int PX, bool HAS1>
-__global__ __launch_bounds__(256) void k_dggm_fuse_fwd(const T* __restrict__ cp1, const T* __restrict__ color,
-                                                       const float* __restrict__ grad,
-                                                       const float* __restrict__ mask, long long pvs,
-                                                       int H, int W, int C, int h, int w,
-                                                       const float* __restrict__ wt,
-                                                       const float* __restrict__ bias, T* __restrict__ out) {
-  __shared__ float sg[3][512];
-  __shared__ float4 swb[kBlkCh];
+__device__ __forceinline__ void dggm_fwd_block(float (*sg)[512], float4* swb, int bx, int by,
+                                               const T* __restrict__ cp1, const T* __restrict__ color,
+                                               const float* __restrict__ grad, const float* __restrict__ mask,
+                                               long long pvs, int H, int W, int C, int h, int w,
+                                               const float* __restrict__ wt, const float* __restrict__ bias,
+                                               T* __restrict__ out) {
   constexpr int TP = 64 * PX;
   const int hw = h * w, tpi = (hw + TP - 1) / TP;
-  const int b = blockIdx.x / tpi, p0 = (blockIdx.x % tpi) * TP;
-  const TileGates<PX> t = stage_gates<PX>(sg, swb, grad + b * pvs, mask + b * pvs, H, W, h, w, p0, wt, bias, C);
-  const int cw = blockIdx.y * kBlkCh + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kWaveCh;
+  const int b = bx / tpi, p0 = (bx % tpi) * TP;
+  const TileGates<PX> t = stage_gates<PX>(sg, swb, grad + b * pvs, mask + b * pvs, H, W, h, w, p0, wt, bias, C, by);
+  const int cw = by * kBlkCh + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kWaveCh;
   if (!t.valid || cw >= C) return;
   float col[kWaveCh][PX], y[kWaveCh][PX];
 #pragma unroll
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_fwd(const T* __restrict__ cp1
 #pragma unroll
   for (int cc = 0; cc < kWaveCh; ++cc) {
     const int c = min(cw + cc, C - 1);
-    const float4 wb = swb[c - (int)blockIdx.y * kBlkCh];
+    const float4 wb = swb[c - by * kBlkCh];
     const float w0 = wb.x, w1 = wb.y, w2 = wb.z, bc = wb.w;
 #pragma unroll
     for (int j = 0; j < PX; ++j) {
@@ -422,26 +422,34 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_fwd(const T* __restrict__ cp1
   }
 }
 
-template <typename T, int PX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_dggm_fuse_bwd_partial(const T* __restrict__ dout,
-                                                               const float* __restrict__ grad,
-                                                               const float* __restrict__ mask,
-                                                               long long pvs, int H, int W, int C, int h,
-                                                               int w, const float* __restrict__ wt,
-                                                               const float* __restrict__ bias,
-                                                               float* __restrict__ partial) {
-  // partial[tile][c][4] = sum over the tile's pixels of dout*relu'(pre) * (1, g0, g1, g2).  Each
-  // lane sums its PX pixels for the wave's 8 channels (32 values), then the wave sums the 64
-  // lanes' values through LDS in fixed order (deterministic).
+template <typename T, int PX, bool HAS1>
+__global__ __launch_bounds__(256) void k_dggm_fuse_fwd(const T* __restrict__ cp1, const T* __restrict__ color,
+                                                       const float* __restrict__ grad,
+                                                       const float* __restrict__ mask, long long pvs,
+                                                       int H, int W, int C, int h, int w,
+                                                       const float* __restrict__ wt,
+                                                       const float* __restrict__ bias, T* __restrict__ out) {
   __shared__ float sg[3][512];
   __shared__ float4 swb[kBlkCh];
-  __shared__ __attribute__((aligned(16))) float sred[4][64 * kRedStride];
+  dggm_fwd_block<T, PX, HAS1>(sg, swb, blockIdx.x, blockIdx.y, cp1, color, grad, mask, pvs, H, W, C, h, w, wt, bias,
+                              out);
+}
+
+// partial[tile][c][4] = sum over the tile's pixels of dout*relu'(pre) * (1, g0, g1, g2).  Each
+// lane sums its PX pixels for the wave's 8 channels (32 values), then the wave sums the 64
+// lanes' values through LDS in fixed order (deterministic).
+template <typename T, int PX>
+__device__ __forceinline__ void dggm_bwd_block(float (*sg)[512], float4* swb, float (*sred)[64 * kRedStride], int bx,
+                                               int by, const T* __restrict__ dout, const float* __restrict__ grad,
+                                               const float* __restrict__ mask, long long pvs, int H, int W, int C,
+                                               int h, int w, const float* __restrict__ wt,
+                                               const float* __restrict__ bias, float* __restrict__ partial) {
   constexpr int TP = 64 * PX;
   const int hw = h * w, tpi = (hw + TP - 1) / TP;
-  const int b = blockIdx.x / tpi, p0 = (blockIdx.x % tpi) * TP;
-  const TileGates<PX> t = stage_gates<PX>(sg, swb, grad + b * pvs, mask + b * pvs, H, W, h, w, p0, wt, bias, C);
+  const int b = bx / tpi, p0 = (bx % tpi) * TP;
+  const TileGates<PX> t = stage_gates<PX>(sg, swb, grad + b * pvs, mask + b * pvs, H, W, h, w, p0, wt, bias, C, by);
   const int lane = threadIdx.x & 63;
-  const int cw = blockIdx.y * kBlkCh + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kWaveCh;
+  const int cw = by * kBlkCh + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kWaveCh;
   if (cw >= C) return;
   float d[kWaveCh][PX];
   if (t.valid && !(dggm_dbg() & 2)) {
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
   for (int cc = 0; cc < kWaveCh; ++cc) {
     const int c = min(cw + cc, C - 1);
-    const float4 wb = swb[c - (int)blockIdx.y * kBlkCh];
+    const float4 wb = swb[c - by * kBlkCh];
     const float w0 = wb.x, w1 = wb.y, w2 = wb.z, bc = wb.w;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
@@ -489,7 +497,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   for (int r = 0; r < 32; ++r) s += red[(half * 32 + r) * kRedStride + idx];
   s += __shfl_xor(s, 32);
   const int c = cw + (idx >> 2);
-  if (lane < 32 && c < C) partial[((long long)blockIdx.x * C + c) * 4 + (idx & 3)] = s;
+  if (lane < 32 && c < C) partial[((long long)bx * C + c) * 4 + (idx & 3)] = s;
+}
+
+template <typename T, int PX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_dggm_fuse_bwd_partial(const T* __restrict__ dout,
+                                                               const float* __restrict__ grad,
+                                                               const float* __restrict__ mask,
+                                                               long long pvs, int H, int W, int C, int h,
+                                                               int w, const float* __restrict__ wt,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ partial) {
+  __shared__ float sg[3][512];
+  __shared__ float4 swb[kBlkCh];
+  __shared__ __attribute__((aligned(16))) float sred[4][64 * kRedStride];
+  dggm_bwd_block<T, PX>(sg, swb, sred, blockIdx.x, blockIdx.y, dout, grad, mask, pvs, H, W, C, h, w, wt, bias,
+                        partial);
 }
 
 __global__ __launch_bounds__(256) void k_dggm_fuse_bwd_final(const float* __restrict__ partial, int ntiles, int C,
@@ -511,6 +534,112 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_bwd_final(const float* __rest
     db[c] = red[0];
   else
     dw[c * 3 + (j - 1)] = red[0];
+}
+
+// ---- all scales in one launch (the four backbone scales of one step): a flat block index is
+// mapped onto (scale, pixel tile, channel block); the vector width PX is per scale, uniform per
+// block.  Cuts three launch/drain tails per direction on the small scales.
+constexpr int DGGM_MAX_SCALES = 4;
+struct DggmScaleArgs {
+  const void* cp1;
+  const void* color;  // fwd input / bwd: dout
+  void* out;
+  const float* wt;
+  const float* bias;
+  float* partial;     // bwd
+  float* dw;          // bwd outputs
+  float* db;
+  int C, h, w, px, nbx, blk0, tiles;
+};
+struct DggmMulti {
+  DggmScaleArgs s[DGGM_MAX_SCALES];
+  int n, total;
+};
+
+__device__ __forceinline__ int dggm_scale_of(const DggmMulti& m, int blk) {
+  int k = 0;
+#pragma unroll
+  for (int i = 1; i < DGGM_MAX_SCALES; ++i)
+    if (i < m.n && blk >= m.s[i].blk0) k = i;
+  return k;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_dggm_fuse_fwd_multi(DggmMulti m, const float* __restrict__ grad,
+                                                             const float* __restrict__ mask, long long pvs, int H,
+                                                             int W) {
+  __shared__ float sg[3][512];
+  __shared__ float4 swb[kBlkCh];
+  const int k = dggm_scale_of(m, blockIdx.x);
+  const DggmScaleArgs& d = m.s[k];
+  const int local = blockIdx.x - d.blk0, bx = local % d.nbx, by = local / d.nbx;
+  const T* cp1 = (const T*)d.cp1;
+  if (cp1) {
+    if (d.px == 8)
+      dggm_fwd_block<T, 8, true>(sg, swb, bx, by, cp1, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w, d.wt,
+                                 d.bias, (T*)d.out);
+    else if (d.px == 4)
+      dggm_fwd_block<T, 4, true>(sg, swb, bx, by, cp1, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w, d.wt,
+                                 d.bias, (T*)d.out);
+    else
+      dggm_fwd_block<T, 1, true>(sg, swb, bx, by, cp1, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w, d.wt,
+                                 d.bias, (T*)d.out);
+  } else {
+    if (d.px == 8)
+      dggm_fwd_block<T, 8, false>(sg, swb, bx, by, nullptr, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w,
+                                  d.wt, d.bias, (T*)d.out);
+    else if (d.px == 4)
+      dggm_fwd_block<T, 4, false>(sg, swb, bx, by, nullptr, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w,
+                                  d.wt, d.bias, (T*)d.out);
+    else
+      dggm_fwd_block<T, 1, false>(sg, swb, bx, by, nullptr, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w,
+                                  d.wt, d.bias, (T*)d.out);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_dggm_fuse_bwd_multi(
+    DggmMulti m, const float* __restrict__ grad, const float* __restrict__ mask, long long pvs, int H, int W) {
+  __shared__ float sg[3][512];
+  __shared__ float4 swb[kBlkCh];
+  __shared__ __attribute__((aligned(16))) float sred[4][64 * kRedStride];
+  const int k = dggm_scale_of(m, blockIdx.x);
+  const DggmScaleArgs& d = m.s[k];
+  const int local = blockIdx.x - d.blk0, bx = local % d.nbx, by = local / d.nbx;
+  if (d.px == 8)
+    dggm_bwd_block<T, 8>(sg, swb, sred, bx, by, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w, d.wt, d.bias,
+                         d.partial);
+  else if (d.px == 4)
+    dggm_bwd_block<T, 4>(sg, swb, sred, bx, by, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w, d.wt, d.bias,
+                         d.partial);
+  else
+    dggm_bwd_block<T, 1>(sg, swb, sred, bx, by, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w, d.wt, d.bias,
+                         d.partial);
+}
+
+// the tile sums of every scale reduced in one launch: block = (scale, c, j), same fixed tree
+__global__ __launch_bounds__(256) void k_dggm_fuse_bwd_final_multi(DggmMulti m) {
+  __shared__ float red[256];
+  int k = 0, t = blockIdx.x;
+  while (k + 1 < m.n && t >= 4 * m.s[k].C) {
+    t -= 4 * m.s[k].C;
+    ++k;
+  }
+  const DggmScaleArgs& d = m.s[k];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < d.tiles; i += 256) s += d.partial[(long long)i * d.C * 4 + t];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x) return;
+  const int c = t >> 2, j = t & 3;
+  if (j == 0)
+    d.db[c] = red[0];
+  else
+    d.dw[c * 3 + (j - 1)] = red[0];
 }
 
 void dggm_dbg_init() {
@@ -645,6 +774,107 @@ int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const flo
   else
     return RGBD_E_DTYPE;
   k_dggm_fuse_bwd_final<<<C * 4, 256, 0, s>>>(partial, ntiles, C, dweight, dbias);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+
+// Multi-scale forms: scales given as host arrays (n <= 4), one launch (fwd) / two launches (bwd).
+static int dggm_multi_setup(int n, const int* C, const int* h, const int* w, int B, DggmMulti& m) {
+  RGBD_REQUIRE(n >= 1 && n <= DGGM_MAX_SCALES && C && h && w, RGBD_E_ARG);
+  m.n = n;
+  int blk = 0;
+  for (int k = 0; k < n; ++k) {
+    RGBD_REQUIRE(C[k] > 0 && h[k] > 0 && w[k] > 0 && (long long)h[k] * w[k] < (1ll << 31), RGBD_E_ARG);
+    DggmScaleArgs& d = m.s[k];
+    d.C = C[k];
+    d.h = h[k];
+    d.w = w[k];
+    d.px = dggm_px(h[k], w[k]);
+    d.nbx = B * ceil_div((long long)h[k] * w[k], 64 * d.px);
+    d.tiles = d.nbx;
+    d.blk0 = blk;
+    blk += d.nbx * ceil_div(C[k], kBlkCh);
+  }
+  m.total = blk;
+  return RGBD_OK;
+}
+
+size_t rgbd_dggm_fuse_bwd_multi_workspace_size(int n, const int* C_host, const int* h_host, const int* w_host,
+                                               int B) {
+  size_t tot = 0;
+  for (int k = 0; k < n; ++k) tot += rgbd_dggm_fuse_bwd_workspace_size(B, C_host[k], h_host[k], w_host[k]);
+  return tot;
+}
+
+int rgbd_dggm_fuse_fwd_multi(int dtype, int n, const void* const* cp1_host, const void* const* color_host,
+                             void* const* out_host, const float* const* weight_host, const float* const* bias_host,
+                             const int* C_host, const int* h_host, const int* w_host, const float* grad,
+                             const float* mask, long long pv_batch_stride, int B, int H, int W, void* stream) {
+  RGBD_REQUIRE(grad && mask && color_host && out_host && weight_host && bias_host && B > 0 && H > 0 && W > 0,
+               RGBD_E_ARG);
+  DggmMulti m;
+  const int rc = dggm_multi_setup(n, C_host, h_host, w_host, B, m);
+  if (rc) return rc;
+  for (int k = 0; k < n; ++k) {
+    RGBD_REQUIRE(color_host[k] && out_host[k] && weight_host[k] && bias_host[k], RGBD_E_ARG);
+    m.s[k].cp1 = cp1_host ? cp1_host[k] : nullptr;
+    m.s[k].color = color_host[k];
+    m.s[k].out = out_host[k];
+    m.s[k].wt = weight_host[k];
+    m.s[k].bias = bias_host[k];
+    m.s[k].partial = nullptr;
+    m.s[k].dw = m.s[k].db = nullptr;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TimerScope ts("dggm_fwd", s);
+  dggm_dbg_init();
+  if (dtype == RGBD_F32)
+    k_dggm_fuse_fwd_multi<float><<<m.total, 256, 0, s>>>(m, grad, mask, pv_batch_stride, H, W);
+  else if (dtype == RGBD_BF16)
+    k_dggm_fuse_fwd_multi<bf16_t><<<m.total, 256, 0, s>>>(m, grad, mask, pv_batch_stride, H, W);
+  else
+    return RGBD_E_DTYPE;
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_dggm_fuse_bwd_multi(int dtype, int n, const void* const* dout_host, const float* const* weight_host,
+                             const float* const* bias_host, float* const* dweight_host, float* const* dbias_host,
+                             const int* C_host, const int* h_host, const int* w_host, const float* grad,
+                             const float* mask, long long pv_batch_stride, int B, int H, int W, void* ws,
+                             void* stream) {
+  RGBD_REQUIRE(grad && mask && dout_host && weight_host && bias_host && dweight_host && dbias_host && ws && B > 0 &&
+                   H > 0 && W > 0,
+               RGBD_E_ARG);
+  DggmMulti m;
+  const int rc = dggm_multi_setup(n, C_host, h_host, w_host, B, m);
+  if (rc) return rc;
+  char* p = (char*)ws;
+  int nfin = 0;
+  for (int k = 0; k < n; ++k) {
+    RGBD_REQUIRE(dout_host[k] && weight_host[k] && bias_host[k] && dweight_host[k] && dbias_host[k], RGBD_E_ARG);
+    m.s[k].cp1 = nullptr;
+    m.s[k].color = dout_host[k];
+    m.s[k].out = nullptr;
+    m.s[k].wt = weight_host[k];
+    m.s[k].bias = bias_host[k];
+    m.s[k].partial = (float*)p;
+    m.s[k].dw = dweight_host[k];
+    m.s[k].db = dbias_host[k];
+    p += rgbd_dggm_fuse_bwd_workspace_size(B, C_host[k], h_host[k], w_host[k]);
+    nfin += 4 * C_host[k];
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TimerScope ts("dggm_bwd", s);
+  dggm_dbg_init();
+  if (dtype == RGBD_F32)
+    k_dggm_fuse_bwd_multi<float><<<m.total, 256, 0, s>>>(m, grad, mask, pv_batch_stride, H, W);
+  else if (dtype == RGBD_BF16)
+    k_dggm_fuse_bwd_multi<bf16_t><<<m.total, 256, 0, s>>>(m, grad, mask, pv_batch_stride, H, W);
+  else
+    return RGBD_E_DTYPE;
+  k_dggm_fuse_bwd_final_multi<<<nfin, 256, 0, s>>>(m);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

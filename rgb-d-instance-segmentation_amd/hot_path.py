@@ -11,7 +11,7 @@ Here:
     dsam_k over the whole batch in one masked implicit-GEMM launch whose epilogue adds the
       residual colour map (cp1[k+1] = colour[k+1] + dsam_k) and writes the NHWC copy the next
       DSAM reads (K5),
-    DGGM gate + final sum in one elementwise pass per scale (K2).
+    DGGM gate + final sum in one elementwise pass over all four scales (K2, one launch).
 Backward produces exactly the gradients the reference graph has: DSAM / DGGM parameters,
 nothing for the colour maps (detached) or the ratio (left the graph via .item()).
 """
@@ -82,8 +82,8 @@ class HotPathFunction(torch.autograd.Function):
             cp1.append(out)
             if k < 2:
                 x_nhwc.append(out_nhwc)
-        outs = [ops.dggm_fuse_fwd(cp1[k], colors[k], pixel_values, dggm_p[2 * k], dggm_p[2 * k + 1])
-                for k in range(4)]
+        # DGGM gate + final sum of all four scales in one launch
+        outs = ops.dggm_fuse_fwd_multi(cp1, colors, pixel_values, dggm_p[0::2], dggm_p[1::2])
         ctx.cfg = cfg
         ctx.codes = codes
         ctx.info = info
@@ -106,8 +106,7 @@ class HotPathFunction(torch.autograd.Function):
                                    if shape is None else "missing gradient for scale 0")
             G.append(g.to(dtype).contiguous())
         grads_dggm = []
-        for k in range(4):
-            dw, db = ops.dggm_fuse_bwd(G[k], pixel_values, dggm_p[2 * k], dggm_p[2 * k + 1])
+        for k, (dw, db) in enumerate(ops.dggm_fuse_bwd_multi(G, pixel_values, dggm_p[0::2], dggm_p[1::2])):
             grads_dggm += [dw.reshape(dggm_p[2 * k].shape).to(dggm_p[2 * k].dtype), db.to(dggm_p[2 * k + 1].dtype)]
         # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}.  bfloat16 keeps the cascade in
         # NHWC (dX written NHWC only, its residual G[k] converted once; bias sums from NHWC).

@@ -167,6 +167,62 @@ def dggm_fuse_bwd(dout, pixel_values, weight, bias):
     return dw, db
 
 
+def _ptrs(ts):
+    return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+
+def _ints(xs):
+    return (ctypes.c_int * len(xs))(*[int(x) for x in xs])
+
+
+def dggm_fuse_fwd_multi(cp1s, colors, pixel_values, weights, biases):
+    """dggm_fuse_fwd for every scale in one launch (rgbd_dggm_fuse_fwd_multi); cp1s may be None."""
+    _need_cuda(*colors, pixel_values)
+    n = len(colors)
+    B, _, H, W = pixel_values.shape
+    if cp1s is not None:
+        _need_cuda(*cp1s)
+        for a, c in zip(cp1s, colors):
+            if a.shape != c.shape or a.dtype != c.dtype:
+                raise ValueError("cp1/color mismatch")
+    for c, w, b in zip(colors, weights, biases):
+        if c.dtype != colors[0].dtype or c.shape[0] != B:
+            raise ValueError("colour maps must share dtype and batch")
+        if w.shape[0] != c.shape[1] or b.shape[0] != c.shape[1]:
+            raise AssertionError(f"Expected {c.shape[1]} channels in the DGGM projection")
+    outs = [torch.empty_like(c) for c in colors]
+    wts = [w.reshape(w.shape[0], 3).float().contiguous() for w in weights]
+    bss = [b.float().contiguous() for b in biases]
+    grad, mask = _grad_mask(pixel_values)
+    check(_lib.lib().rgbd_dggm_fuse_fwd_multi(
+        _dtype_code(colors[0]), n, None if cp1s is None else _ptrs(cp1s), _ptrs(colors), _ptrs(outs), _ptrs(wts),
+        _ptrs(bss), _ints([c.shape[1] for c in colors]), _ints([c.shape[2] for c in colors]),
+        _ints([c.shape[3] for c in colors]), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(mask.data_ptr()),
+        pixel_values.stride(0), B, H, W, _stream(pixel_values.device)), "rgbd_dggm_fuse_fwd_multi")
+    return outs
+
+
+def dggm_fuse_bwd_multi(douts, pixel_values, weights, biases):
+    """dggm_fuse_bwd for every scale: one partial launch + one final launch.  -> [(dw, db)]."""
+    _need_cuda(*douts, pixel_values)
+    n = len(douts)
+    B, _, H, W = pixel_values.shape
+    Cs, hs, ws_ = [d.shape[1] for d in douts], [d.shape[2] for d in douts], [d.shape[3] for d in douts]
+    wts = [w.reshape(w.shape[0], 3).float().contiguous() for w in weights]
+    bss = [b.float().contiguous() for b in biases]
+    dws = [torch.empty((c, 3), dtype=torch.float32, device=pixel_values.device) for c in Cs]
+    dbs = [torch.empty((c,), dtype=torch.float32, device=pixel_values.device) for c in Cs]
+    L = _lib.lib()
+    ci, hi, wi = _ints(Cs), _ints(hs), _ints(ws_)
+    ws = _workspace(pixel_values.device, L.rgbd_dggm_fuse_bwd_multi_workspace_size(n, ci, hi, wi, B), "dggm_bwd_multi")
+    grad, mask = _grad_mask(pixel_values)
+    check(L.rgbd_dggm_fuse_bwd_multi(_dtype_code(douts[0]), n, _ptrs(douts), _ptrs(wts), _ptrs(bss), _ptrs(dws),
+                                     _ptrs(dbs), ci, hi, wi, ctypes.c_void_p(grad.data_ptr()),
+                                     ctypes.c_void_p(mask.data_ptr()), pixel_values.stride(0), B, H, W, _p(ws),
+                                     _stream(pixel_values.device)), "rgbd_dggm_fuse_bwd_multi")
+    return list(zip(dws, dbs))
+
+
 # ------------------------------------------------------------------ layout / packing
 def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     _need_cuda(x)

@@ -345,3 +345,28 @@ def test_streaming_graph_replay_matches_eager():
         assert torch.equal(ratio, ref_ratio)
         for a, e in zip(feats, ref_feats):
             assert torch.equal(a, e)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_dggm_multi_scale_equals_per_scale(dtype):
+    """rgbd_dggm_fuse_{fwd,bwd}_multi (all scales in one launch, as the fused hot path calls them)
+    give bitwise the per-scale entry points' outputs and gradients, incl. PX = 8 / 4 / 1 scales."""
+    ops = _ops()
+    B, H, W = 2, 97, 130
+    pv = torch.from_numpy(gi.pixel_values(12, B, H, W)).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    shapes = [(96, 25, 33), (192, 13, 17), (384, 7, 9), (768, 4, 4)]   # h*w % 8 / % 4 / odd
+    colors = [torch.randn((B, c, h, w), generator=g, device=DEV).to(dtype) for c, h, w in shapes]
+    cp1s = [torch.randn((B, c, h, w), generator=g, device=DEV).to(dtype) for c, h, w in shapes]
+    wts = [torch.randn((c, 3, 1, 1), generator=g, device=DEV) for c, _, _ in shapes]
+    bss = [torch.randn((c,), generator=g, device=DEV) for c, _, _ in shapes]
+    for cps in (cp1s, None):
+        multi = ops.dggm_fuse_fwd_multi(cps, colors, pv, wts, bss)
+        for k in range(4):
+            one = ops.dggm_fuse_fwd(None if cps is None else cps[k], colors[k], pv, wts[k], bss[k])
+            assert torch.equal(multi[k], one), k
+    douts = [torch.randn(c.shape, generator=g, device=DEV).to(dtype) for c in colors]
+    multi = ops.dggm_fuse_bwd_multi(douts, pv, wts, bss)
+    for k in range(4):
+        dw, db = ops.dggm_fuse_bwd(douts[k], pv, wts[k], bss[k])
+        assert torch.equal(multi[k][0], dw) and torch.equal(multi[k][1], db), k
