@@ -735,6 +735,15 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
     if constexpr (PHASE == 1) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) add_stats(ssum[t], ssq[t], a2[t], full, x0, row_ok);
+      if (att) {  // raw fusion output for k_rp_gate: [tile][wave][t][u][lane][4 px], 512 B per store
+        bf16_t* ft = att + ((tile * 8 + wave) * 16) * 256;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            *reinterpret_cast<uint2*>(ft + ((t * 2 + u) * 64 + lane) * 4) =
+                make_uint2(pack_bf16x2(a2[t][u][0], a2[t][u][1]), pack_bf16x2(a2[t][u][2], a2[t][u][3]));
+      }
       continue;
     }
     if constexpr (PHASE == 2) {
@@ -815,6 +824,155 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
       if (g == 0) {
         slab[(row * NC + 16 * t + r) * 2 + 0] = a;
         slab[(row * NC + 16 * t + r) * 2 + 1] = q;
+      }
+    }
+  }
+}
+
+// ---- train mode, bf16: the chain's last stage from phase 1's stored fusion output.
+// Phase 1 has to run the stem + fusion for the BN2 statistics anyway; storing its raw fusion
+// output (fragment-native, 256 B/px) lets this kernel skip the stem + fusion recompute that
+// phase 2 would do (111 k FLOP/px): per 8x32-px tile a wave owns one pixel row, reads its 8 KB,
+// applies BN2 + ReLU, transposes through a wave-private LDS image [32 px][128 ch], and runs the
+// attention 1x1s (128->64->128, LDS-resident weights) and the sigmoid gate; HBM-bound
+// (512 B/px).  The eval path (no statistics pass) keeps phase 2.
+constexpr int GT_S = FUS_C + 8;  // image row: 128 channels + 8 pad (272 B, conflict-free b64 reads)
+constexpr size_t GT_OFF_W3 = 0;
+constexpr size_t GT_OFF_W4 = GT_OFF_W3 + (size_t)ATT_C * C2W_S3 * 2;
+constexpr size_t GT_OFF_B = GT_OFF_W4 + (size_t)FUS_C * C2W_S4 * 2;  // b3[64], b4[128], aff2[128]
+constexpr size_t GT_OFF_IMG = GT_OFF_B + (size_t)(ATT_C + FUS_C + 2 * FUS_C) * 4;
+constexpr size_t GT_SMEM = GT_OFF_IMG + (size_t)8 * C2W_TW * GT_S * 2;
+static_assert(GT_SMEM <= 163840, "gate LDS budget");
+
+__global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus, int B, int H, int W,
+                                                 const char* __restrict__ blob, Layout L,
+                                                 const float2* __restrict__ aff2, bf16_t* __restrict__ att) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bf16_t* sW3 = (const bf16_t*)(smem + GT_OFF_W3);
+  const bf16_t* sW4 = (const bf16_t*)(smem + GT_OFF_W4);
+  float* sb3 = (float*)(smem + GT_OFF_B);
+  float* sb4 = sb3 + ATT_C;
+  float2* saff = (float2*)(sb4 + FUS_C);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  bf16_t* img = (bf16_t*)(smem + GT_OFF_IMG) + (size_t)wave * C2W_TW * GT_S;
+  {
+    auto copy_rows = [&](size_t dst, size_t src, int rows, int k, int stride) {
+      const int per = k / 8;
+      for (int i = tid; i < rows * per; i += 512) {
+        const int rr = i / per, q = i % per;
+        *reinterpret_cast<uint4*>(smem + dst + ((size_t)rr * stride + 8 * q) * 2) =
+            *reinterpret_cast<const uint4*>(blob + src + ((size_t)rr * k + 8 * q) * 2);
+      }
+    };
+    copy_rows(GT_OFF_W3, L.w3, ATT_C, FUS_C, C2W_S3);
+    copy_rows(GT_OFF_W4, L.w4, FUS_C, ATT_C, C2W_S4);
+    for (int i = tid; i < ATT_C; i += 512) sb3[i] = ((const float*)(blob + L.b3))[i];
+    for (int i = tid; i < FUS_C; i += 512) {
+      sb4[i] = ((const float*)(blob + L.b4))[i];
+      saff[i] = aff2[i];
+    }
+  }
+  __syncthreads();
+  const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
+  const long long ntiles = (long long)B * tiles_x * tiles_y;
+  const long long HW = (long long)H * W;
+  // this wave's raw fusion output of a tile: lane (r, g) has channel 16t + r, pixels 16u + 4g + j;
+  // the next tile's 8 KB are loaded while the current one computes
+  uint2 nxt[8][2];
+  auto fetch = [&](long long tl) {
+    if (tl >= ntiles) return;
+    const bf16_t* ft = fus + ((tl * 8 + wave) * 16) * 256;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) nxt[t][u] = *reinterpret_cast<const uint2*>(ft + ((t * 2 + u) * 64 + lane) * 4);
+  };
+  fetch(blockIdx.x);
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
+    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
+    const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
+    const int py = y0 + wave;
+    uint2 raw[8][2];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) raw[t][u] = nxt[t][u];
+    fetch(tile + gridDim.x);
+    if (py >= H) continue;  // wave-uniform; nothing below synchronises across waves
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous tile's image reads are done
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int c = 16 * t + r;
+      const float2 a = saff[c];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t w01 = raw[t][u].x, w23 = raw[t][u].y;
+        const float v[4] = {__uint_as_float(w01 << 16), __uint_as_float(w01 & 0xffff0000u),
+                            __uint_as_float(w23 << 16), __uint_as_float(w23 & 0xffff0000u)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          img[(16 * u + 4 * g + j) * GT_S + c] = f32_to_bf16(fmaxf(__builtin_fmaf(v[j], a.x, a.y), 0.f));  // BN2 + ReLU
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- W3 B operand in the chain's K order: element e of chunk s = channel 32s + 16(e>>2) + 4g + (e&3)
+    Frag<bf16_t> f2[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16_t* row = img + (16 * u + r) * GT_S + 32 * s + 4 * g;
+        const uint2 lo = *reinterpret_cast<const uint2*>(row), hi = *reinterpret_cast<const uint2*>(row + 16);
+        f2[s][u].v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    f32x4 a3[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 bb = *reinterpret_cast<const float4*>(sb3 + 16 * t + 4 * g);
+      a3[t][0] = a3[t][1] = f32x4{bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        Frag<bf16_t> af;
+        af.v = *reinterpret_cast<const uint4*>(sW3 + (16 * t + r) * C2W_S3 + 32 * s + 8 * g);
+        mma(a3[t][0], af, f2[s][0]);
+        mma(a3[t][1], af, f2[s][1]);
+      }
+    }
+    Frag<bf16_t> f3[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float vv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vv[e] = fmaxf(a3[2 * s + (e >> 2)][u][e & 3], 0.f);
+        f3[s][u].from8(vv);
+      }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float4 bb = *reinterpret_cast<const float4*>(sb4 + 16 * t + 4 * g);
+      f32x4 a4[2] = {f32x4{bb.x, bb.y, bb.z, bb.w}, f32x4{bb.x, bb.y, bb.z, bb.w}};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        Frag<bf16_t> af;
+        af.v = *reinterpret_cast<const uint4*>(sW4 + (16 * t + r) * C2W_S4 + 32 * s + 8 * g);
+        mma(a4[0], af, f3[s][0]);
+        mma(a4[1], af, f3[s][1]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (x0 + 16 * u + r >= W) continue;
+        const uint2 act = *reinterpret_cast<const uint2*>(img + (16 * u + r) * GT_S + 16 * t + 4 * g);
+        const float av[4] = {__uint_as_float(act.x << 16), __uint_as_float(act.x & 0xffff0000u),
+                             __uint_as_float(act.y << 16), __uint_as_float(act.y & 0xffff0000u)};
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = av[j] * sigmoid_fast(a4[u][j]);
+        *reinterpret_cast<uint2*>(att + ((long long)b * HW + (long long)py * W + x0 + 16 * u + r) * FUS_C + 16 * t +
+                                  4 * g) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
       }
     }
   }
@@ -1549,15 +1707,26 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
     k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch0, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
                                  bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
-  // fusion BN
-  if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, nullptr);
+  // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
+  // buffer, which is dead until conv5) for k_rp_gate
+  const bool gate = v2 && training;
+  bf16_t* fus = (bf16_t*)y;
+  if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, gate ? (void*)fus : nullptr);
   k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, nslab_ch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
                                 bn.p[15], aff2);
-  if (v2) k_rp_fold<<<FUS_C, 256, 0, s>>>(blob, L, aff2, 2, fold);  // BN2 -> W2', b2'
+  if (v2 && !gate) k_rp_fold<<<FUS_C, 256, 0, s>>>(blob, L, aff2, 2, fold);  // BN2 -> W2', b2'
   // gated attention features
   {
     TimerScope ts("rp_chain", s);
-    CHAIN_LAUNCH(2, aff1, aff2, nullptr, att);
+    if (gate) {
+      static const hipError_t gattr =
+          hipFuncSetAttribute((const void*)k_rp_gate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GT_SMEM);
+      if (gattr != hipSuccess) return (int)gattr;
+      const int gg = (int)std::min<long long>(conv3_tiles(B, H, W), device_cus());
+      k_rp_gate<<<gg, 512, GT_SMEM, s>>>(fus, B, H, W, blob, L, aff2, (bf16_t*)att);
+    } else {
+      CHAIN_LAUNCH(2, aff1, aff2, nullptr, att);
+    }
   }
   // conv5 + its BN statistics
   int gcv;
