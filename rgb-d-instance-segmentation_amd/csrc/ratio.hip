@@ -964,16 +964,28 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        if (x0 + 16 * u + r >= W) continue;
-        const uint2 act = *reinterpret_cast<const uint2*>(img + (16 * u + r) * GT_S + 16 * t + 4 * g);
+        // the gated value replaces the activation it came from (same lane, same 8 bytes)
+        uint2* cell = reinterpret_cast<uint2*>(img + (16 * u + r) * GT_S + 16 * t + 4 * g);
+        const uint2 act = *cell;
         const float av[4] = {__uint_as_float(act.x << 16), __uint_as_float(act.x & 0xffff0000u),
                              __uint_as_float(act.y << 16), __uint_as_float(act.y & 0xffff0000u)};
         float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = av[j] * sigmoid_fast(a4[u][j]);
-        *reinterpret_cast<uint2*>(att + ((long long)b * HW + (long long)py * W + x0 + 16 * u + r) * FUS_C + 16 * t +
-                                  4 * g) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+        *cell = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
       }
+    }
+    // NHWC store of the wave's 32 pixels from the image: 16 lanes per 256-byte pixel row, four
+    // consecutive pixels (1 KB contiguous) per store instruction
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bf16_t* orow = att + ((long long)b * HW + (long long)py * W + x0) * FUS_C;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int pr = 4 * k + (lane >> 4), q = lane & 15;
+      if (x0 + pr < W)
+        *reinterpret_cast<uint4*>(orow + (long long)pr * FUS_C + 8 * q) =
+            *reinterpret_cast<const uint4*>(img + pr * GT_S + 8 * q);
     }
   }
 }
