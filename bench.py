@@ -4,27 +4,38 @@ One step = one training pass of the v0.4.0 pixel-level hot path (SURVEY §8 rows
 a batch of synthetic NYUv2-shaped frames (640x480, 8 images per GPU, bf16 MFMA):
   u8 RGB + u8 depth (resident in HBM)
   -> 10-channel pixel_values incl. DGGM Sobel planes         (K1, rgbd_assemble_pixel_values)
+  -> (N > 1) rank 0's ratio-predictor BatchNorm buffers broadcast (DDP broadcast_buffers)
   -> ratio predictor, train-mode BatchNorm + dropout          (K4, rgbd_ratio_forward)
   -> depth decomposition once per image                       (K3, rgbd_edsam_decompose)
   -> DSAM x3 masked implicit GEMMs (cascade) + DGGM + sum     (K5, K2)
   -> backward from a fixed synthetic upstream gradient of the 4 backbone features:
      DSAM dW/db/dX cascade + DGGM dW/db                        (K5, K2)
-  -> (N > 1) RCCL all-reduce of the hot-path parameter gradients (DDP semantics)
+  -> (N > 1) RCCL all-reduce (mean) of the hot-path parameter gradients, overlapped with the
+     backward cascade (DDP semantics of the reference's Trainer, finetuning.py:98-113)
   -> AdamW step on the hot-path parameters (HF Trainer's optimizer; lr 1e-5 constant,
      mask2former/config.json), so every step re-packs the changed DSAM filters.
 The Swin encoder / pixel decoder / transformer decoder are outside the hot path (SURVEY §8(f)
 "next"); their colour-feature inputs are synthetic tensors of the Swin-T shapes.
 
+Launch: ``python bench.py --gpus N`` spawns N rank processes itself (before any GPU call) when
+no launcher set WORLD_SIZE; under ``torch.distributed.run`` each rank reads RANK / LOCAL_RANK /
+WORLD_SIZE from the environment.  8 images per rank (scaling "weak").
+
 Prints ONE JSON line (rank 0).  ``value`` = images processed by all ranks / max-over-ranks
 time.  ``roofline`` is for the dominant kernel (the ratio predictor's 3x3 128->256 conv,
-k_rp_conv3x3), timed with HIP events on its launch stream inside the timed region.
+k_rp_conv3x3), timed with HIP events on its launch stream inside the timed region;
+``kernels`` carries the same for K5 and the whole step's t_ideal / t_measured.
 ``cpu_baseline`` = the oracle (PyTorch-CPU fp32 restatement of the reference, tests-only
-code) on a bounded sample of the same workload on this host's cores.
+code) on bounded samples of the same workloads on this host's cores (BASELINE.md plan).
+``parity`` = the fp32 mask-logit max-abs-err of the full drop-in model at 640x480 against the
+reference's committed fixture (tests/golden/g7_model640.npz), measured outside the timed region.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -42,14 +53,22 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip 
 HBM_PEAK_GBS = 8000.0
 CONV5_FLOP_PER_PX = 2 * 128 * 9 * 256  # 3x3 128->256 (custom_model.py:1413)
 CONV5_KERNEL = "k_rp_conv3x3_v3"
+DSAM_CH = [(96, 192), (192, 384), (384, 768)]
+# SURVEY §8(d), per input pixel of the batch (P = B*H*W): reference-algorithmic work
+K4_FLOP_PER_PX = 703_616          # ratio predictor forward
+K5_FWD_FLOP_PER_PX = 77_760       # 3 DSAMs x (4 masked 3x3 s2 convs + projection)
+K5_BWD_FLOP_PER_PX = 129_600      # dX (dsam1, dsam2) + dW (all) of the same convs
+K1_BYTES_PER_PX = 6.0
+K2_BYTES_PER_PX = 71.5
+K3_BYTES_PER_PX = 12.04
+ADAMW_BYTES_PER_PARAM = 28        # fused AdamW: read p, g, m, v; write p, m, v (f32)
 
 
 def pmc_traffic(kernel, default_shape):
     """HBM bytes per launch of ``kernel`` from the newest committed PMC table
-    (profiles/*/pmc_traffic.json, written by tools/gpu_traffic.sh + tools/traffic_table.py over
-    this bench's default step: FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE).
-    rocprofv3 cannot run inside this process, so the counters come from their own passes; the
-    value is null for a non-default shape or when no table holds this kernel."""
+    (profiles/*/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 correction, plus
+    WRITE_SIZE, one pass each, over this bench's default step).  rocprofv3 cannot run inside
+    this process, so the counters come from their own passes; null for a non-default shape."""
     if not default_shape:
         return None
     best = None
@@ -69,15 +88,68 @@ def parse(argv=None):
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse several ranks on one GPU)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
-    ap.add_argument("--cpu-sample", type=int, default=1, help="images in the bounded CPU sample")
     ap.add_argument("--inference", type=int, default=1, help="also report forward-only img/s")
     ap.add_argument("--c5-stream", type=int, default=1,
                     help="also report the C5 RealSense 1280x720 B=1 streaming inference rate (rank 0, N=1)")
+    ap.add_argument("--parity", type=int, default=1,
+                    help="report the fp32 mask-logit max-abs-err vs the committed 640x480 fixture (rank 0)")
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
-def build(args, dev):
+# ------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """One child process per rank, started before this process touches the GPU, with the
+    environment torch.distributed.run would give it.  Returns the first non-zero exit code (the
+    other ranks are then terminated) or 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + list(argv), env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def launcher_selftest():
+    """CPU plumbing check of spawn_ranks (tests/test_bench_launcher.py): gloo on CPU tensors."""
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"world": dist.get_world_size(), "rank_sum": float(t.item()),
+                          "local_rank": int(os.environ["LOCAL_RANK"])}), flush=True)
+    dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ workload
+def build(args, dev, rank=0):
     from rgbd_amd import init as winit, synthetic
     from rgbd_amd.modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -85,7 +157,7 @@ def build(args, dev):
     rp = EnhancedDepthImageRatioPredictor(3)
     winit.init_deterministic(rp, prefix=pre + "ratio_predictor.")
     dsams = []
-    for k, (ci, co) in enumerate([(96, 192), (192, 384), (384, 768)]):
+    for k, (ci, co) in enumerate(DSAM_CH):
         m = DSAModule(ci, co)
         winit.init_deterministic(m, prefix=f"{pre}dsam{k}.")
         dsams.append(m)
@@ -95,7 +167,6 @@ def build(args, dev):
         m.compute_dtype = dtype
         m.to(dev).train()
     B, H, W = args.batch, args.height, args.width
-    rank = int(os.environ.get("RANK", "0"))
     scenes = [synthetic.make_scene(synthetic.scene_seed(3, rank * B + i), H, W) for i in range(B)]
     depth_u8 = torch.from_numpy(np.stack([s["depth_u8"] for s in scenes])).to(dev)
     rgb_u8 = torch.from_numpy(np.stack([s["rgb_u8"] for s in scenes])).contiguous().to(dev)
@@ -114,29 +185,52 @@ def build(args, dev):
                 gouts=gouts, scenes=scenes, sizes=sizes)
 
 
-def make_step(ctx, world, inference=False):
+def make_parts(ctx, world):
+    """(forward_backward, optimizer_step, reducer, broadcaster) of one training step.
+    forward_backward() leaves the (all-reduced, for N > 1) gradients in p.grad."""
     from rgbd_amd import ops
+    from rgbd_amd.distributed import BufferBroadcaster, OverlappedGradReducer, hot_path_grad_groups
     from rgbd_amd.hot_path import hot_path
-    from rgbd_amd.distributed import OverlappedGradReducer, hot_path_grad_groups
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
     # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
     reducer = OverlappedGradReducer(hot_path_grad_groups(ctx["dsams"], ctx["dg"])) if world > 1 else None
+    bcast = BufferBroadcaster([ctx["rp"]]) if world > 1 else None
     hook = None if reducer is None else reducer.ready
-    opt = None if inference else torch.optim.AdamW(params, lr=1e-5, fused=True)
+    opt = torch.optim.AdamW(params, lr=1e-5, fused=True)
 
-    def step():
+    def forward_backward():
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
-        if inference:
-            with torch.no_grad():
-                ratio = ctx["rp"](pv[:, 3:6])
-                return hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"])
+        if bcast is not None:  # DDP broadcast_buffers: every forward starts from rank 0's BN stats
+            bcast.sync()
         ratio = ctx["rp"](pv[:, 3:6])
         feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], grad_hook=hook)
         torch.autograd.backward(feats, ctx["gouts"])
         if reducer is not None:  # DDP gradient exchange of the hot-path parameters (RCCL over xGMI)
             reducer.finish()
+        return feats
+
+    def optimizer_step():
         opt.step()
         opt.zero_grad(set_to_none=True)
+
+    return forward_backward, optimizer_step, reducer, bcast
+
+
+def make_step(ctx, world, inference=False):
+    from rgbd_amd import ops
+    from rgbd_amd.hot_path import hot_path
+    if inference:
+        def istep():
+            pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
+            with torch.no_grad():
+                ratio = ctx["rp"](pv[:, 3:6])
+                return hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"])
+        return istep
+    fb, ostep, _, _ = make_parts(ctx, world)
+
+    def step():
+        feats = fb()
+        ostep()
         return feats
     return step
 
@@ -157,12 +251,14 @@ def timed(step, steps, warmup, world):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt
 
 
+# ------------------------------------------------------------------ side measurements
 def c5_stream(ctx, frames=100):
     """BASELINE configs[4]: RealSense 1280x720 RGB-D stream inference, one frame per step, the
     hot path in eval mode replayed from a HIP graph (rgbd_amd/stream.py).  Reports the graph
@@ -192,75 +288,210 @@ def c5_stream(ctx, frames=100):
     graph_h2d = rate(lambda: sp(d_host, c_host))
     with torch.no_grad():
         eager = rate(lambda: sp._run())
+    for m in [ctx["rp"], ctx["dg"]] + ctx["dsams"]:
+        m.train()
     return {"shape": f"{W}x{H}", "batch": 1, "dtype": "bf16" if ctx["dtype"] == torch.bfloat16 else "f32",
             "graph_img_s": graph, "graph_with_h2d_img_s": graph_h2d, "eager_img_s": eager, "frames": frames}
 
 
+def cpu_threads():
+    """Threads for the CPU baseline: every core of this process's affinity set, capped by the
+    host's per-job CPU share when the environment states one (OMP_NUM_THREADS; 16 per GPU on
+    the GPU box) — both numbers are reported."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return aff, (min(aff, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else aff)
+
+
 def cpu_baseline(ctx, args):
-    """Oracle (PyTorch-CPU fp32 restatement, tests-only code) on a bounded sample: the same
-    training hot path (ratio predictor train mode + decomposition + DSAM x3 + DGGM, forward and
-    backward) for ``--cpu-sample`` images at the same resolution."""
+    """BASELINE.md's CPU plan on the oracle (PyTorch-CPU fp32 + numpy restatement of the
+    reference, tests-only code): 1 warm-up + 3 timed iterations each of
+      (value) the hot-path training step, fwd+bwd (ratio predictor train mode, decomposition,
+              DSAM x3, DGGM), 640x480, B=2 — the GPU workload on a bounded sample;
+      (hot_path_eval_b8) hot path only, eval, 640x480, B=8 (BASELINE run 1);
+      (c5_eval_b1) hot path only, eval, 1280x720, B=1 (BASELINE run 2)."""
     from oracle import dggm_pre, hot_path as hot_o
     from rgbd_amd import synthetic
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(threads, 16))
+    aff, threads = cpu_threads()
     torch.set_num_threads(threads)
-    n = args.cpu_sample
-    H, W = args.height, args.width
-    pv = []
-    for s in ctx["scenes"][:n]:
-        pv.append(np.concatenate([synthetic.rgbd_planes(s), dggm_pre.dggm_planes(s["depth_u8"])]))
+
     sd = {}
-    pre = ""
     for k, m in enumerate(ctx["dsams"]):
         sd.update({f"dsam{k}.{kk}": v.detach().float().cpu().clone().requires_grad_(v.is_floating_point())
                    for kk, v in m.state_dict().items()})
     sd.update({f"depth_gradient_injection.{kk}": v.detach().float().cpu().clone().requires_grad_(True)
                for kk, v in ctx["dg"].state_dict().items()})
-    sd.update({f"ratio_predictor.{kk}": v.detach().cpu().clone() for kk, v in ctx["rp"].state_dict().items()})
-    colors = [c[:n].float().cpu() for c in ctx["colors"]]
-    gouts = [g[:n].float().cpu() for g in ctx["gouts"]]
-    pvt = torch.from_numpy(np.stack(pv))
-    t0 = time.perf_counter()
-    feats, _, _ = hot_o.hot_path_forward(colors, pvt, sd, prefix=pre, training=True)
-    torch.autograd.backward(feats, gouts)
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"{n} image(s) {W}x{H}, full hot-path train step (fwd+bwd), oracle fp32 on {threads} thread(s)"}
+    rp_sd = {f"ratio_predictor.{kk}": v.detach().cpu().clone() for kk, v in ctx["rp"].state_dict().items()}
+    sd.update(rp_sd)
+
+    def inputs(scenes, H, W):
+        pv = torch.from_numpy(np.stack([np.concatenate([synthetic.rgbd_planes(s), dggm_pre.dggm_planes(s["depth_u8"])])
+                                        for s in scenes]))
+        sizes, h, w = [], -(-H // 4), -(-W // 4)
+        for _ in range(4):
+            sizes.append((h, w))
+            h, w = -(-h // 2), -(-w // 2)
+        g = torch.Generator().manual_seed(7)
+        colors = [torch.randn((len(scenes), c, *sizes[k]), generator=g) for k, c in enumerate([96, 192, 384, 768])]
+        return pv, colors
+
+    def run(fn, n_img):
+        fn()  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(3):
+            fn()
+        dt = (time.perf_counter() - t0) / 3
+        return round(n_img / dt, 4), round(dt, 3)
+
+    H, W = args.height, args.width
+    pv2, col2 = inputs(ctx["scenes"][:2], H, W)
+    gouts = [g[:2].float().cpu() for g in ctx["gouts"]]
+
+    def train_step():
+        for v in sd.values():
+            v.grad = None
+        feats, _, _ = hot_o.hot_path_forward(col2, pv2, sd, training=True)
+        torch.autograd.backward(feats, gouts)
+    train, train_s = run(train_step, 2)
+
+    scenes8 = [synthetic.make_scene(synthetic.scene_seed(3, i), H, W) for i in range(8)]
+    pv8, col8 = inputs(scenes8, H, W)
+
+    def eval8():
+        with torch.no_grad():
+            hot_o.hot_path_forward(col8, pv8, sd, training=False)
+    ev8, ev8_s = run(eval8, 8)
+
+    c5 = synthetic.make_scene(synthetic.scene_seed(5, 0), 720, 1280)
+    pv5, col5 = inputs([c5], 720, 1280)
+
+    def eval_c5():
+        with torch.no_grad():
+            hot_o.hot_path_forward(col5, pv5, sd, training=False)
+    c5r, c5_s = run(eval_c5, 1)
+    return {"value": train, "unit": "img/s", "cores": threads, "affinity_cores": aff, "kind": "port",
+            "sample": f"2 images {W}x{H}, hot-path train step fwd+bwd (ratio predictor train mode, decomposition, "
+                      f"DSAM x3, DGGM), oracle fp32 on {threads} thread(s); 1 warm-up + 3 timed iterations "
+                      f"({train_s} s each)",
+            "runs": {"hot_path_eval_b8_640x480_img_s": ev8, "hot_path_eval_b8_s_per_iter": ev8_s,
+                     "c5_eval_b1_1280x720_img_s": c5r, "c5_eval_s_per_iter": c5_s}}
 
 
+def parity_fp32(dev):
+    """BASELINE.json's second metric: the full drop-in model (HF Swin / pixel decoder /
+    transformer decoder around the HIP hot path, f1/f2 kernels installed) in float32 at 640x480,
+    B=1, eval, deterministic weights, against the reference CPU run committed as
+    tests/golden/g7_model640.npz (made by tests/golden/make_golden.py).  The 10-channel input is
+    assembled on the GPU by K1 from the scene's u8 planes; its sha256 must equal the one the
+    fixture was generated from."""
+    import hashlib
+    from rgbd_amd import init as winit, ops, synthetic
+    from rgbd_amd.config import standard_config
+    from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
+    g7 = np.load(REPO / "tests" / "golden" / "g7_model640.npz", allow_pickle=False)
+    sc = synthetic.make_scene(synthetic.scene_seed(7, 0), 480, 640)
+    pv = ops.assemble_pixel_values(torch.from_numpy(sc["depth_u8"][None]).to(dev),
+                                   torch.from_numpy(sc["rgb_u8"][None]).contiguous().to(dev))
+    sha_ok = hashlib.sha256(pv.cpu().numpy().tobytes()).hexdigest() == str(g7["input_sha"])
+    torch.manual_seed(0)
+    m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
+    winit.init_deterministic(m)
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        out = m(pixel_values=pv)
+        ratio = m.model.pixel_level_module.ratio_predictor(pv[:, 3:6])
+    ml = out.masks_queries_logits.float().cpu().numpy().ravel()
+    err = float(np.abs(ml[g7["mask_idx"]] - g7["mask_val"]).max())
+    cls = float(np.abs(out.class_queries_logits.float().cpu().numpy() - g7["class_logits"]).max())
+    rrel = float(np.abs(ratio.cpu().numpy() - g7["ratio"]).max() / np.abs(g7["ratio"]).max())
+    del m
+    torch.cuda.empty_cache()
+    return {"mask_logit_max_abs_err": err, "tolerance": 1e-3, "class_logit_max_abs_err": cls,
+            "ratio_rel_err": rrel, "input_sha_match": sha_ok, "dtype": "f32", "shape": "640x480",
+            "fixture": "tests/golden/g7_model640.npz", "sampled_logits": int(g7["mask_idx"].size)}
+
+
+def kernel_fractions(L, ctx, B, H, W, step_ms, world):
+    """K5 achieved rates (reference-algorithmic and executed FLOPs) and the whole step's
+    t_ideal / t_measured from the HIP-event timings of the timed steps."""
+    cnt = ctypes.c_int(0)
+    ms = {}
+    for name in ("rp_conv3x3", "rp_chain", "dsam_fwd", "dsam_dx", "dsam_wgrad", "decompose", "dggm_fwd",
+                 "dggm_bwd", "assemble"):
+        tot = L.rgbd_timing_read(name.encode(), ctypes.byref(cnt))
+        ms[name] = (tot, cnt.value)
+    P = B * H * W
+    ho = [(-(-H // 4) + 1) // 2, (-(-H // 8) + 1) // 2, (-(-H // 16) + 1) // 2]
+    wo = [(-(-W // 4) + 1) // 2, (-(-W // 8) + 1) // 2, (-(-W // 16) + 1) // 2]
+    conv = [2 * 9 * ci * co * B * ho[k] * wo[k] for k, (ci, co) in enumerate(DSAM_CH)]  # one 3x3 s2 conv
+    n_steps = max(ms["dsam_wgrad"][1] // 3, 1)
+    k5_ms = (ms["dsam_fwd"][0] + ms["dsam_dx"][0] + ms["dsam_wgrad"][0]) / n_steps
+    k5_exec = 3 * sum(conv) - conv[0]           # merged filter: fwd x3 + dX (dsam1, dsam2) + dW x3
+    k5_alg = (K5_FWD_FLOP_PER_PX + K5_BWD_FLOP_PER_PX) * P
+    per = {k: round(v[0] / max(v[1], 1), 4) for k, v in ms.items()}
+    n_params = sum(p.numel() for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters())
+    t_ideal = (K4_FLOP_PER_PX * P / (MFMA_BF16_PEAK_TFLOPS * 1e12)
+               + (K5_FWD_FLOP_PER_PX + K5_BWD_FLOP_PER_PX) * P / (MFMA_BF16_PEAK_TFLOPS * 1e12)
+               + (K1_BYTES_PER_PX + K2_BYTES_PER_PX + K3_BYTES_PER_PX) * P / (HBM_PEAK_GBS * 1e9)
+               + ADAMW_BYTES_PER_PARAM * n_params / (HBM_PEAK_GBS * 1e9)) * 1e3
+    return per, {
+        "k5_dsam": {"ms_per_step": round(k5_ms, 4),
+                    "algorithmic_tflop_s": round(k5_alg / (k5_ms * 1e-3) / 1e12, 1),
+                    "executed_tflop_s": round(k5_exec / (k5_ms * 1e-3) / 1e12, 1),
+                    "frac_algorithmic": round(k5_alg / (k5_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                    "frac_executed": round(k5_exec / (k5_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                    "note": "algorithmic = reference FLOPs (4 masked convs + projection per DSAM); executed = one "
+                            "code-merged filter per output pixel and tap"},
+        "whole_step": {"t_ideal_ms": round(t_ideal, 4), "t_measured_ms": round(step_ms, 4),
+                       "frac": round(t_ideal / step_ms, 4),
+                       "note": "t_ideal = K4+K5 FLOPs at bf16 MFMA peak + K1/K2/K3/AdamW bytes at HBM peak "
+                               "(SURVEY §8(d)); per rank" + ("" if world == 1 else ", collectives excluded")},
+    }
+
+
+# ------------------------------------------------------------------ main
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.launcher_selftest:
+        return launcher_selftest()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     from rgbd_amd import _lib
+    from rgbd_amd.distributed import broadcast_parameters
     L = _lib.lib()
-    ctx = build(args, dev)
+    ctx = build(args, dev, rank)
+    if world > 1:  # DDP construction: rank 0's parameters and buffers everywhere
+        broadcast_parameters([ctx["rp"], ctx["dg"]] + ctx["dsams"])
     step = make_step(ctx, world)
-    # timed region, kernel timing on for the dominant kernel
+    # timed region, kernel timing on
     L.rgbd_timing_enable(1)
     dt = timed(step, args.steps, args.warmup, world)
+    B = args.batch
+    step_ms = dt / args.steps * 1e3
+    per, fracs = kernel_fractions(L, ctx, B, args.height, args.width, step_ms, world)
     cnt = ctypes.c_int(0)
     conv_ms = L.rgbd_timing_read(b"rp_conv3x3", ctypes.byref(cnt))
     conv_launches = cnt.value
-    others = {}
-    for name in ("rp_chain", "dsam_fwd", "dsam_dx", "dsam_wgrad", "decompose", "dggm_fwd", "dggm_bwd", "assemble"):
-        ms = L.rgbd_timing_read(name.encode(), ctypes.byref(cnt))
-        others[name] = round(ms / max(cnt.value, 1), 4)
     L.rgbd_timing_enable(0)
-    B = args.batch
-    imgs = B * world * args.steps
-    value = imgs / dt
+    value = B * world * args.steps / dt
     inf = None
     if args.inference:
         istep = make_step(ctx, world, inference=True)
         idt = timed(istep, args.steps, args.warmup, world)
         inf = round(B * world * args.steps / idt, 2)
+        for m in [ctx["rp"], ctx["dg"]] + ctx["dsams"]:
+            m.train()
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     flop = CONV5_FLOP_PER_PX * B * args.height * args.width
     achieved = flop / (conv_avg_ms * 1e-3) / 1e12
@@ -272,7 +503,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "ms_per_step": round(step_ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -282,22 +513,30 @@ def main():
                                f"DGGM, fwd+bwd + AdamW), {args.width}x{args.height}, batch {B}/GPU",
                    "global_batch": B * world, "height": args.height, "width": args.width,
                    "parallelism": f"dp{world}"},
+        "distributed": {"world_size": dist.get_world_size() if world > 1 else 1,
+                        "backend": (dist.get_backend() if world > 1 else None),
+                        "collectives_per_step": ("3 async all-reduce (grad buckets dsam2, dsam1, dsam0+DGGM) + "
+                                                 "2 broadcasts (ratio-predictor BN buffers)") if world > 1 else None},
         "inference_img_s": inf,
-        "kernel_ms": dict(rp_conv3x3=round(conv_avg_ms, 4), **others),
+        "kernel_ms": per,
         "roofline": {"bound": "mfma", "kernel": "k_rp_conv3x3 (3x3 128->256, custom_model.py:1413)",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
                      "traffic": None if traffic is None else round(traffic[0]),
                      "traffic_unit": "bytes/launch", "traffic_source": None if traffic is None else traffic[1],
                      "algorithmic_bytes": (128 + 256) * 2 * B * args.height * args.width},
+        "kernels": fracs,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(ctx, args)
+    if rank == 0 and args.parity:
+        out["parity"] = parity_fp32(dev)
     if rank == 0 and world == 1 and args.c5_stream:
         out["c5_stream"] = c5_stream(ctx)
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(ctx, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

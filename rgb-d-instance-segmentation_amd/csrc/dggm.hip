@@ -18,8 +18,13 @@ using namespace rgbd;
 
 namespace {
 
-__constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
-__constant__ float kStd[3] = {0.229f, 0.224f, 0.225f};
+// image_mean / image_std of the reference's processor config
+// (mask2former/checkpoints/standard/preprocessor_config.json), rounded to float32 as
+// transformers' normalize does (np.array(mean, dtype=image.dtype)).  The config's std[1],
+// 0.2239999920129776, is one float32 ulp below 0.224f.
+__constant__ float kMean[3] = {0.48500001430511475f, 0.4560000002384186f, 0.4059999883174896f};
+__constant__ float kStd[3] = {0.2290000021457672f, 0.2239999920129776f, 0.22499999403953552f};
+constexpr double kRescale = 0.00392156862745098;  // rescale_factor of the same config
 
 struct PrepWs {
   uint32_t min_bits;  // min over mag > 0 (non-negative floats order as their bits)
@@ -42,8 +47,10 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 }
 
 __device__ __forceinline__ float norm_u8(uint8_t v, int c) {
-  // numpy: (x.astype(f32) * f32(1/255) - mean_c) / std_c, one rounding per op
-  float x = __fmul_rn((float)v, 0.003921568859368563f);
+  // Mask2FormerImageProcessor (dataloader.py:405-410): transformers image_transforms.rescale
+  // multiplies in float64 and rounds once to float32; normalize is (x - mean_c) / std_c in
+  // float32, one rounding per op.
+  const float x = (float)__dmul_rn((double)v, kRescale);
   return div_rn(__fsub_rn(x, kMean[c]), kStd[c]);
 }
 

@@ -68,12 +68,14 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
                 m.compute_dtype = dtype
         return self
 
-    def hot_path_features(self, pixel_values: Tensor, color_feature_map, ratios=None):
-        """custom_model.py:325-355 on the HIP kernels: returns the 4 backbone features."""
+    def hot_path_features(self, pixel_values: Tensor, color_feature_map, ratios=None, status_sink=None):
+        """custom_model.py:325-355 on the HIP kernels: returns the 4 backbone features.
+        ``status_sink``: see hot_path.hot_path (None = raise the reference's ValueError at once)."""
         if ratios is None:
             ratios = self.ratio_predictor(pixel_values[:, 3:6])       # :336 (no grad, Q2)
         feats = hot_path(pixel_values, ratios, list(color_feature_map), [self.dsam0, self.dsam1, self.dsam2],
-                         self.depth_gradient_injection, dtype=self.compute_dtype)
+                         self.depth_gradient_injection, dtype=self.compute_dtype,
+                         check_status=status_sink is None, status_sink=status_sink)
         dt = color_feature_map[0].dtype
         return [f.to(dt) for f in feats]
 
@@ -83,8 +85,16 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
         else:
             rgb = pixel_values[:, 0:3, :, :]
             color_feature_map = self.encoder(rgb).feature_maps          # :330 (Swin, HF)
-            backbone_features = self.hot_path_features(pixel_values, color_feature_map)
+            statuses = []
+            backbone_features = self.hot_path_features(pixel_values, color_feature_map, status_sink=statuses)
         decoder_output = self.decoder(backbone_features, output_hidden_states=output_hidden_states)
+        if self.version != "0.0.0":
+            # The reference raises numpy's ValueError for a non-finite or too-narrow depth range
+            # (custom_model.py:715-717).  The decomposition status was copied to the host behind
+            # the decomposition; waiting for it here lets the DSAM / DGGM / pixel-decoder kernels
+            # already enqueued keep the GPU busy.
+            for st in statuses:
+                st.check()
         return Mask2FormerPixelLevelModuleOutput(
             encoder_last_hidden_state=backbone_features[-1],
             encoder_hidden_states=tuple(backbone_features) if output_hidden_states else None,

@@ -76,12 +76,20 @@ class OverlappedGradReducer:
         dev = self.groups[0][0].device
         self.flats = [torch.empty(sum(p.numel() for p in g), dtype=torch.float32, device=dev) for g in self.groups]
         self.works = [None] * len(self.groups)
+        self.prev = [None] * len(self.groups)
 
     def ready(self, idx, grads):
-        """Gradients of group ``idx`` (same order as its parameters; None counts as zero)."""
+        """Gradients of group ``idx`` (same order as its parameters; None counts as zero).
+
+        Called from inside the backward, before autograd accumulates ``grads`` into ``p.grad``.
+        A ``p.grad`` that already holds a value (gradient accumulation over several backwards)
+        is snapshotted here, so ``finish()`` leaves ``previous + mean(this backward)`` in it, as
+        DDP's reducer does; with ``p.grad`` None (``zero_grad(set_to_none=True)``) no copy is
+        made.  Do not also wrap these parameters in torch DDP: they would be reduced twice."""
         g = self.groups[idx]
         if len(grads) != len(g):
             raise ValueError(f"group {idx}: {len(grads)} gradients for {len(g)} parameters")
+        self.prev[idx] = [None if p.grad is None else p.grad.detach().clone() for p in g]
         flat = self.flats[idx]
         parts = [(t if t is not None else torch.zeros_like(p)).reshape(-1).float() for t, p in zip(grads, g)]
         torch.cat(parts, out=flat)
@@ -100,14 +108,59 @@ class OverlappedGradReducer:
             flat.div_(world)
             views, dsts = [], []
             off = 0
-            for p in g:
+            for p, prev in zip(g, self.prev[idx]):
                 k = p.numel()
                 v = flat[off:off + k].view_as(p)
                 off += k
+                if prev is not None:
+                    v = v + prev
                 if p.grad is None:
                     p.grad = v.clone()
                 else:
                     views.append(v)
                     dsts.append(p.grad)
+            self.prev[idx] = None
             if dsts:
                 torch._foreach_copy_(dsts, views)
+
+
+class BufferBroadcaster:
+    """DDP's ``broadcast_buffers=True`` for the modules outside torch DDP: at the start of every
+    forward, rank 0's buffers overwrite every other rank's (torch DDP ``_sync_buffers`` before
+    each forward).  Under the reference's Trainer that applies to the ratio predictor's BatchNorm
+    running statistics (SURVEY §2 "(2) DDP broadcast of buffers"): each rank updates them from
+    its own batch statistics (no SyncBN), and the next forward starts from rank 0's.  Buffers
+    are flattened per dtype (float32 statistics, int64 counters), so a step costs one broadcast
+    per dtype."""
+
+    def __init__(self, modules, group=None):
+        self.pg = group
+        bufs = [b for m in modules for b in m.buffers()]
+        self.by_dtype = {}
+        for b in bufs:
+            self.by_dtype.setdefault(b.dtype, []).append(b)
+        self.flats = {dt: torch.empty(sum(b.numel() for b in bs), dtype=dt, device=bs[0].device)
+                      for dt, bs in self.by_dtype.items()}
+
+    def sync(self, src=0):
+        if dist.get_world_size(self.pg) == 1:
+            return
+        for dt, bs in self.by_dtype.items():
+            flat = self.flats[dt]
+            torch.cat([b.reshape(-1) for b in bs], out=flat)
+            dist.broadcast(flat, src=src, group=self.pg)
+            views, off = [], 0
+            for b in bs:
+                views.append(flat[off:off + b.numel()].view_as(b))
+                off += b.numel()
+            torch._foreach_copy_(bs, views)
+
+
+def broadcast_parameters(modules, group=None, src=0):
+    """DDP's construction-time broadcast of rank 0's parameters and buffers."""
+    if dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for m in modules:
+            for t in list(m.parameters()) + list(m.buffers()):
+                dist.broadcast(t.data, src=src, group=group)

@@ -68,6 +68,8 @@ class HotPathFunction(torch.autograd.Function):
         codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
         if cfg.get("check_status"):
             ops.raise_on_status(info)
+        if cfg.get("status_sink") is not None:
+            cfg["status_sink"].append(ops.DeferredStatus(info))
         training = any(ctx.needs_input_grad[7:])
         masks = ops.dsam_code_masks(codes) if dtype == torch.bfloat16 else None
         packs = [cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
@@ -136,9 +138,12 @@ class HotPathFunction(torch.autograd.Function):
 
 
 def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch.float32, check_status=False,
-             grad_hook=None):
+             grad_hook=None, status_sink=None):
     """Run the fused hot path.  ``dsam_modules``: the three DSAModule instances;
-    ``dggm_module``: the DepthGradientInjectionResidual instance.  ``grad_hook(i, grads)``, if
+    ``dggm_module``: the DepthGradientInjectionResidual instance.  ``check_status`` raises the
+    reference's ValueError for a degenerate depth histogram right away (synchronising);
+    ``status_sink`` (a list) instead receives an ``ops.DeferredStatus`` to check later.
+    ``grad_hook(i, grads)``, if
     given, is called during backward as each parameter group's gradients are enqueued, in the
     order of ``distributed.hot_path_grad_groups`` (dsam2, dsam1, dsam0 + DGGM) — the data-parallel
     reducer uses it to overlap the gradient all-reduce with the rest of the backward."""
@@ -150,7 +155,7 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
     for i in range(4):
         conv = dggm_module.depth_enhancement_layers[i][0]
         params += [conv.weight, conv.bias]
-    cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook,
+    cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook, "status_sink": status_sink,
            "pack_cache": [m._pack_cache for m in dsam_modules]}
     pv = pixel_values.detach().float().contiguous()
     return list(HotPathFunction.apply(pv, ratio, cfg, *colors, *params))

@@ -16,6 +16,10 @@ from . import _lib
 from ._lib import RGBD_BF16, RGBD_F32, DECOMP_INFO_DTYPE, check
 
 _ws_cache = {}
+# Workspaces replaced by a larger one stay alive for the life of the process: a HIP graph
+# captured earlier (stream.StreamingHotPath) keeps the raw pointer of the buffer it was
+# captured with, so that buffer must never return to the caching allocator.
+_ws_retired = []
 
 
 def _dtype_code(t: torch.Tensor) -> int:
@@ -43,9 +47,14 @@ def _need_cuda(*ts):
 
 
 def _workspace(dev, nbytes: int, tag: str):
-    key = (dev, tag)
+    """Scratch buffer for one entry point, one per (device, tag, stream): launches on two
+    streams never share one, and launches on one stream are ordered.  Never freed (see
+    ``_ws_retired``)."""
+    key = (dev, tag, torch.cuda.current_stream(dev).cuda_stream)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None:
+            _ws_retired.append(buf)
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
         _ws_cache[key] = buf
     return buf
@@ -108,15 +117,36 @@ def decode_info(info: torch.Tensor) -> np.ndarray:
     return info.cpu().numpy().view(DECOMP_INFO_DTYPE).reshape(-1)
 
 
-def raise_on_status(info: torch.Tensor):
-    """Mirror the reference's ValueError for degenerate histograms (numpy raises inside
-    DSAModule._calculate_depth_histogram, custom_model.py:717).  Synchronises."""
-    rec = decode_info(info)
-    for b, s in enumerate(rec["status"]):
+def _raise_statuses(statuses):
+    for b, s in enumerate(statuses):
         if s == 1:
             raise ValueError(f"image {b}: supplied range of depth is not finite (np.histogram)")
         if s == 2:
             raise ValueError(f"image {b}: Too many bins for data range. Cannot create 512 finite-sized bins.")
+
+
+def raise_on_status(info: torch.Tensor):
+    """Mirror the reference's ValueError for degenerate histograms (numpy raises inside
+    DSAModule._calculate_depth_histogram, custom_model.py:715-717).  Synchronises."""
+    _raise_statuses(decode_info(info)["status"])
+
+
+class DeferredStatus:
+    """The per-image decomposition status, copied to pinned host memory behind the
+    decomposition on its stream.  ``check()`` waits only for that copy (the kernels enqueued
+    after it keep running) and raises the reference's ValueError; the drop-in module calls it
+    at the end of its forward, after the pixel decoder has been enqueued."""
+
+    def __init__(self, info: torch.Tensor):
+        st = info.view(torch.int32)[:, 0]  # rgbd_decomp_info.status, the record's first word
+        self.host = torch.empty(st.shape, dtype=torch.int32, pin_memory=True)
+        self.host.copy_(st, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(info.device))
+
+    def check(self):
+        self.event.synchronize()
+        _raise_statuses(self.host.tolist())
 
 
 # ------------------------------------------------------------------ K2 DGGM fusion
@@ -393,12 +423,14 @@ def mask_attention(logits: torch.Tensor, size, heads: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ f3 matcher assignment
-def linear_sum_assignment_batch(costs, validate=False):
+def linear_sum_assignment_batch(costs, validate=False, return_status=False):
     """scipy.optimize.linear_sum_assignment for a list of 2-D float32 CUDA cost matrices in one
-    launch (rgbd_lsa_batch).  Returns [(row_ind, col_ind)] as int64 CUDA tensors, scipy's order.
-    Nothing synchronises unless ``validate`` (then a status read-back raises scipy's ValueErrors)."""
+    launch (rgbd_lsa_batch).  Returns [(row_ind, col_ind)] as int64 CUDA tensors, scipy's order
+    (with ``return_status`` also the int32 device tensor of per-matrix statuses: 0 ok,
+    1 infeasible, 2 invalid entries — scipy's two ValueErrors).  Nothing synchronises unless
+    ``validate`` (then a status read-back raises scipy's ValueErrors)."""
     if not costs:
-        return []
+        return ([], None) if return_status else []
     dev = costs[0].device
     flat, meta, coff, ooff, mr, mc = [], [], 0, 0, 0, 0
     for c in costs:
@@ -416,9 +448,11 @@ def linear_sum_assignment_batch(costs, validate=False):
         raise ValueError("rgbd_lsa_batch: matrices up to 2048 on a side")
     cost = torch.cat(flat) if coff > 0 else torch.zeros(1, dtype=torch.float32, device=dev)
     meta_t = torch.tensor(meta, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
-    rows = torch.empty(max(ooff, 1), dtype=torch.int64, device=dev)
-    cols = torch.empty(max(ooff, 1), dtype=torch.int64, device=dev)
-    status = torch.empty(len(costs), dtype=torch.int32, device=dev)
+    # zero-initialised: a matrix the kernel rejects (status != 0) leaves valid indices behind,
+    # never uninitialised ones
+    rows = torch.zeros(max(ooff, 1), dtype=torch.int64, device=dev)
+    cols = torch.zeros(max(ooff, 1), dtype=torch.int64, device=dev)
+    status = torch.zeros(len(costs), dtype=torch.int32, device=dev)
     check(_lib.lib().rgbd_lsa_batch(len(costs), _p(cost), _p(meta_t), mr, mc, _p(rows), _p(cols), _p(status),
                                     _stream(dev)), "rgbd_lsa_batch")
     if validate:
@@ -433,7 +467,7 @@ def linear_sum_assignment_batch(costs, validate=False):
         n = int(min(meta[4 * i + 1], meta[4 * i + 2]))
         out.append((rows[o:o + n], cols[o:o + n]))
         o += n
-    return out
+    return (out, status) if return_status else out
 
 
 # ------------------------------------------------------------------ f2 deformable attention

@@ -15,8 +15,12 @@ The 10-channel ``pixel_values`` layout is the one ``map_10channel_case2`` builds
 """
 import numpy as np
 
-IMAGENET_MEAN = np.array([0.485, 0.456, 0.406], dtype=np.float32)
-IMAGENET_STD = np.array([0.229, 0.224, 0.225], dtype=np.float32)
+# image_mean / image_std / rescale_factor of the reference's processor config
+# (mask2former/checkpoints/standard/preprocessor_config.json), float32 as transformers'
+# normalize casts them; the config's std[1] is one float32 ulp below float32(0.224).
+IMAGENET_MEAN = np.array([0.48500001430511475, 0.4560000002384186, 0.4059999883174896], dtype=np.float32)
+IMAGENET_STD = np.array([0.2290000021457672, 0.2239999920129776, 0.22499999403953552], dtype=np.float32)
+RESCALE_FACTOR = 0.00392156862745098
 
 
 def scene_seed(config_id: int, index: int) -> int:
@@ -63,8 +67,10 @@ def make_scene(seed: int, h: int, w: int, hole_frac: float = 0.03):
 
 
 def normalize_u8(x_u8_chw: np.ndarray) -> np.ndarray:
-    """(x/255 - mean_c)/std_c in float32, per channel (C=3, CHW)."""
-    x = x_u8_chw.astype(np.float32) * np.float32(1.0 / 255.0)
+    """Channels as Mask2FormerImageProcessor leaves them (reference dataloader.py:405-410):
+    transformers image_transforms.rescale (float64 multiply, one rounding to float32), then
+    normalize ((x - mean_c) / std_c in float32), per channel (C=3, CHW)."""
+    x = (x_u8_chw.astype(np.float64) * RESCALE_FACTOR).astype(np.float32)
     return (x - IMAGENET_MEAN[:, None, None]) / IMAGENET_STD[:, None, None]
 
 

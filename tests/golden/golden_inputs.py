@@ -52,6 +52,18 @@ def labels(config_id, B, H, W):
     return ([s["masks"].astype(F32) for s in scenes], [s["classes"] for s in scenes])
 
 
+def instance_map(scene):
+    """The instance channel of the reference's annotation PNG for a synthetic scene
+    (dataloader.py:391-403): uint8 [H,W], 0 = background, rectangle i -> id 7*i + 3, plus the
+    instance -> semantic id table built from the (instance, semantic) pairs."""
+    inst = np.zeros(scene["masks"].shape[1:], np.uint8)
+    table = {0: 0}
+    for i, m in enumerate(scene["masks"]):
+        inst[m > 0] = 7 * i + 3
+        table[7 * i + 3] = int(scene["classes"][i])
+    return inst, table
+
+
 def label_kwargs():
     id2label = {i: f"label_{i}" for i in range(48)}
     return dict(id2label=id2label, label2id={v: k for k, v in id2label.items()})

@@ -208,7 +208,70 @@ def main():
             raise AssertionError(f"unexpected grad on {n} (Q1/Q2)")
     g6["names"] = np.array(names)
     np.savez_compressed(OUT / "g6_grads.npz", **g6)
+
+    # ------------------------------------------------------------------ G7 (C2 shape)
+    pv7 = golden_inputs.pixel_values(7, 1, 480, 640)
+    caps.clear()
+    with torch.no_grad():
+        out = model(pixel_values=torch.from_numpy(pv7))
+    g7 = {"input_sha": np.array(sha(pv7)), "ratio": caps["ratio"].numpy(),
+          "class_logits": out.class_queries_logits.numpy()}
+    ml = out.masks_queries_logits.numpy().ravel()
+    idx = golden_inputs.sample_index("g7.mask", ml.size, 1 << 16)
+    g7.update(mask_idx=idx, mask_val=ml[idx], mask_sum=np.array(ml.astype(np.float64).sum()),
+              mask_abs=np.array(np.abs(ml.astype(np.float64)).sum()), mask_shape=np.array(out.masks_queries_logits.shape))
+    for k in range(4):
+        t = caps["bb"][k].numpy().ravel()
+        idx = golden_inputs.sample_index(f"g7.bb{k}", t.size, 8192)
+        g7[f"bb{k}_idx"] = idx
+        g7[f"bb{k}_val"] = t[idx]
+        g7[f"bb{k}_sum"] = np.array(t.astype(np.float64).sum())
+    np.savez_compressed(OUT / "g7_model640.npz", **g7)
+
+    processor_fixture()
     print("golden fixtures written to", OUT)
+
+
+def reference_processor(h, w):
+    """The image processor finetuning.py:72-80 builds from the reference's checkpoint directory
+    (do_resize, size = image_height x image_width, do_reduce_labels False, ignore_index 0 as in
+    mask2former/config.json).  transformers 5.15's AutoImageProcessor needs torchvision, which is
+    absent; the numpy ("PIL") backend is the processor transformers 4.47 — the version the
+    reference's checkpoints were written with — instantiates by default."""
+    from transformers.models.mask2former.image_processing_pil_mask2former import Mask2FormerImageProcessorPil
+    cfg = json.loads(Path(f"{REF}/mask2former/checkpoints/standard/preprocessor_config.json").read_text())
+    for k in ("image_processor_type", "_max_size", "reduce_labels", "num_labels"):
+        cfg.pop(k, None)
+    cfg.update(do_resize=True, size={"height": h, "width": w}, do_reduce_labels=False, ignore_index=0)
+    return Mask2FormerImageProcessorPil(**cfg)
+
+
+def processor_fixture():
+    """G0 (a11): channels 0:6 of pixel_values and the label tensors exactly as
+    map_10channel_case2 gets them from the processor (dataloader.py:405-423)."""
+    g0 = {}
+    # every u8 value in every channel (8 copies each, a different permutation per channel)
+    base = np.tile(np.arange(256, dtype=np.uint8), 8).reshape(32, 64)
+    rng = np.random.default_rng(11)
+    lut_img = np.stack([base, rng.permutation(base.ravel()).reshape(32, 64), base[::-1, ::-1]], axis=-1)
+    g0["lut_rgb_u8"] = lut_img
+    g0["lut_out"] = reference_processor(32, 64)(images=[lut_img], return_tensors="np")["pixel_values"][0]
+    for tag, (H, W) in {"small": (64, 96), "c2": (480, 640)}.items():
+        sc = synthetic.make_scene(synthetic.scene_seed(70, 0), H, W)
+        inst, inst2sem = golden_inputs.instance_map(sc)
+        depth_rgb = np.stack([sc["depth_u8"]] * 3, axis=-1)  # PIL convert('L') -> convert('RGB')
+        mi = reference_processor(H, W)(images=[sc["rgb_u8"], depth_rgb], segmentation_maps=[inst, inst],
+                                        instance_id_to_semantic_id=inst2sem, return_tensors="np")
+        pv6 = mi["pixel_values"].reshape(-1, H, W)                     # dataloader.py:417-418
+        masks, classes = np.asarray(mi["mask_labels"][0]), np.asarray(mi["class_labels"][0])
+        g0[f"{tag}_pv6_sha"] = np.array(sha(pv6.astype(np.float32)))
+        g0[f"{tag}_masks_sha"] = np.array(sha(masks.astype(np.float32)))
+        g0[f"{tag}_masks_shape"] = np.array(masks.shape)
+        g0[f"{tag}_classes"] = classes.astype(np.int64)
+        if tag == "small":
+            g0["small_pv6"] = pv6.astype(np.float32)
+            g0["small_masks"] = masks.astype(np.float32)
+    np.savez_compressed(OUT / "g0_processor.npz", **g0)
 
 
 def build_model(cm):

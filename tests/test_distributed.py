@@ -71,16 +71,20 @@ def _worker_overlapped(rank, world, port, q):
     assert [len(g) for g in groups] == [9, 9, 17]
     red = OverlappedGradReducer(groups)
     ok = True
-    for step in range(2):  # buffers are reused across steps
+    for step in range(3):  # buffers are reused across steps
+        # step 0: p.grad None (zero_grad(set_to_none=True)) -> overwritten with the mean;
+        # step 1: p.grad holds step 0's mean (gradient accumulation) -> previous + mean;
+        # step 2: p.grad reset to None again
         exp = []
         for gi, g in enumerate(groups):
             grads = []
             for i, p in enumerate(g):
+                if step != 1:
+                    p.grad = None
+                prev = torch.zeros_like(p) if p.grad is None else p.grad.clone()
                 t = torch.randn(p.shape, generator=torch.Generator().manual_seed(1000 * step + 100 * gi + i))
                 grads.append(None if (rank == 0 and i == 1) else t * (rank + 1))
-                exp.append(t * (1.0 if i == 1 else 1.5))  # mean over ranks of t*(r+1), rank 0 missing i==1
-                if p.grad is None or step == 0:
-                    p.grad = torch.zeros_like(p)
+                exp.append(prev + t * (1.0 if i == 1 else 1.5))  # mean over ranks of t*(r+1), rank 0 missing i==1
             red.ready(gi, grads)
         red.finish()
         got = [p.grad for g in groups for p in g]

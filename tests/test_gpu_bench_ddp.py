@@ -1,0 +1,108 @@
+"""Row (e) on the GPU: bench.py's data-parallel step at world size 2 (both ranks on the one
+MI355X of the test box, gloo — RCCL refuses two ranks on one device).
+
+* the launcher: ``bench.py --gpus 2`` spawns two ranks and reports n_gpus 2 / global batch 16;
+* DDP semantics of the step (the reference's Trainer, finetuning.py:98-113): after the
+  overlapped reducer, every rank holds the mean of the two ranks' standalone gradients, and
+  every forward starts from rank 0's ratio-predictor BatchNorm buffers (broadcast_buffers)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parents[1]
+
+
+def test_bench_launcher_world2_json():
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "2",
+                        "--warmup", "1", "--cpu-baseline", "0", "--c5-stream", "0", "--inference", "0", "--parity", "0",
+                        "--height", "96", "--width", "128"],
+                       capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 16
+    assert out["distributed"]["world_size"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["value"] > 0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        sys.path.insert(0, str(REPO))
+        import bench
+        dev = torch.device("cuda:0")
+        args = bench.parse(["--height", "96", "--width", "128", "--batch", "3"])
+        # standalone gradients of both shards (ratio predictor in eval: a deterministic ratio)
+        ref = []
+        for r in range(world):
+            ctx = bench.build(args, dev, rank=r)
+            ctx["rp"].eval()
+            fb, _, _, _ = bench.make_parts(ctx, 1)
+            fb()
+            ref.append([p.grad.clone() for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()])
+        mean = [(a + b) / 2 for a, b in zip(*ref)]
+        # the DDP step of this rank
+        ctx = bench.build(args, dev, rank=rank)
+        ctx["rp"].eval()
+        fb, _, _, _ = bench.make_parts(ctx, world)
+        fb()
+        got = [p.grad for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
+        grad_err = max(float(((a - e).abs().max() / (e.abs().max() + 1e-12))) for a, e in zip(got, mean))
+        # buffer broadcast in train mode: rank 1 starts from different BN statistics; the forward
+        # must see rank 0's
+        ctx = bench.build(args, dev, rank=rank)
+        bns = [b for b in ctx["rp"].buffers()]
+        with torch.no_grad():
+            for b in bns:
+                if b.is_floating_point():
+                    b.add_(0.5 * rank)
+        seen = {}
+        ctx["rp"].register_forward_pre_hook(lambda m, a: seen.__setitem__("bufs", [b.clone() for b in m.buffers()]))
+        fb, _, _, _ = bench.make_parts(ctx, world)
+        fb()
+        flat = torch.cat([b.double().reshape(-1) for b in seen["bufs"]]).cpu()
+        other = flat.clone()
+        dist.broadcast(other, src=0)
+        buf_err = float((flat - other).abs().max())
+        torch.cuda.synchronize()
+        q.put((rank, (grad_err, buf_err)))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+def test_ddp_step_gradients_and_buffers_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=200) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert isinstance(res[r], tuple), res[r]
+        grad_err, buf_err = res[r]
+        assert grad_err < 1e-5, res
+        assert buf_err == 0.0, res

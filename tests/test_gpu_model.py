@@ -144,7 +144,7 @@ def test_full_model_mask_logits_fp32(golden):
     mc = _full_model().cpu().eval()
     assert mask_predictor.uninstall(mc) == 1  # the reference HF modules are the CPU checker
     assert deform_attn.uninstall(mc) == 6
-    mc.model.pixel_level_module.hot_path_features = lambda pv_, colors, ratios=None: caps["bb"]
+    mc.model.pixel_level_module.hot_path_features = lambda pv_, colors, ratios=None, **kw: caps["bb"]
     calls = []
     h3 = mc.model.transformer_module.decoder.mask_predictor.register_forward_hook(
         lambda mod, inp, out: calls.append((inp, out)))

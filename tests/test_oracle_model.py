@@ -31,7 +31,7 @@ def _oracle_hot(plm, captured):
     named = dict(plm.named_parameters())
     sd.update(named)  # parameters as leaves so grads flow (G6)
 
-    def hot(pixel_values, color_feature_map, ratios=None):
+    def hot(pixel_values, color_feature_map, ratios=None, **kw):
         feats, r, _ = hot_o.hot_path_forward(list(color_feature_map), pixel_values, sd, training=False)
         captured["ratio"] = r
         return feats
@@ -59,6 +59,24 @@ def test_oracle_full_model_matches_g5(golden):
     np.testing.assert_allclose(cap["ratio"].numpy(), g5["ratio"], rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-4, rtol=1e-4)
     np.testing.assert_allclose(out.masks_queries_logits.numpy(), g5["mask_logits"], atol=1e-3, rtol=1e-4)
+
+
+def test_oracle_full_model_matches_g7_640x480(golden):
+    """The oracle composition at the C2 shape (640x480) against the reference run G7."""
+    g7 = golden("g7_model640")
+    m = _model().eval()
+    cap = {}
+    m.model.pixel_level_module.hot_path_features = _oracle_hot(m.model.pixel_level_module, cap)
+    pv = gi.pixel_values(7, 1, 480, 640)
+    import hashlib
+    assert hashlib.sha256(pv.tobytes()).hexdigest() == str(g7["input_sha"])
+    with torch.no_grad():
+        out = m(pixel_values=torch.from_numpy(pv))
+    np.testing.assert_allclose(cap["ratio"].numpy(), g7["ratio"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(out.class_queries_logits.numpy(), g7["class_logits"], atol=1e-4, rtol=1e-4)
+    ml = out.masks_queries_logits.numpy().ravel()
+    assert tuple(out.masks_queries_logits.shape) == tuple(g7["mask_shape"])
+    assert np.abs(ml[g7["mask_idx"]] - g7["mask_val"]).max() <= 1e-3
 
 
 def test_oracle_grads_match_g6(golden):
