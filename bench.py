@@ -235,10 +235,12 @@ def make_step(ctx, world, inference=False):
     return step
 
 
-def timed(step, steps, warmup, world):
+def timed(step, steps, warmup, world, on_start=None):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    if on_start is not None:
+        on_start()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -434,7 +436,7 @@ def kernel_fractions(L, ctx, B, H, W, step_ms, world):
                + (K5_FWD_FLOP_PER_PX + K5_BWD_FLOP_PER_PX) * P / (MFMA_BF16_PEAK_TFLOPS * 1e12)
                + (K1_BYTES_PER_PX + K2_BYTES_PER_PX + K3_BYTES_PER_PX) * P / (HBM_PEAK_GBS * 1e9)
                + ADAMW_BYTES_PER_PARAM * n_params / (HBM_PEAK_GBS * 1e9)) * 1e3
-    return per, {
+    return ms, per, {
         "k5_dsam": {"ms_per_step": round(k5_ms, 4),
                     "algorithmic_tflop_s": round(k5_alg / (k5_ms * 1e-3) / 1e12, 1),
                     "executed_tflop_s": round(k5_exec / (k5_ms * 1e-3) / 1e12, 1),
@@ -474,15 +476,12 @@ def main():
     if world > 1:  # DDP construction: rank 0's parameters and buffers everywhere
         broadcast_parameters([ctx["rp"], ctx["dg"]] + ctx["dsams"])
     step = make_step(ctx, world)
-    # timed region, kernel timing on
-    L.rgbd_timing_enable(1)
-    dt = timed(step, args.steps, args.warmup, world)
+    # timed region; per-kernel HIP-event timing over the timed steps only
+    dt = timed(step, args.steps, args.warmup, world, on_start=lambda: L.rgbd_timing_enable(1))
     B = args.batch
     step_ms = dt / args.steps * 1e3
-    per, fracs = kernel_fractions(L, ctx, B, args.height, args.width, step_ms, world)
-    cnt = ctypes.c_int(0)
-    conv_ms = L.rgbd_timing_read(b"rp_conv3x3", ctypes.byref(cnt))
-    conv_launches = cnt.value
+    raw, per, fracs = kernel_fractions(L, ctx, B, args.height, args.width, step_ms, world)
+    conv_ms, conv_launches = raw["rp_conv3x3"]
     L.rgbd_timing_enable(0)
     value = B * world * args.steps / dt
     inf = None

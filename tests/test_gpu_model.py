@@ -134,12 +134,16 @@ def test_full_model_mask_logits_fp32(golden):
     caps = {}
     h1 = plm.ratio_predictor.register_forward_hook(lambda mod, inp, out: ref_ratio.clone())
     h2 = plm.decoder.register_forward_pre_hook(lambda mod, a: caps.__setitem__("bb", [t.detach().cpu() for t in a[0]]))
+    gpu_calls = []
+    h4 = m.model.transformer_module.decoder.mask_predictor.register_forward_hook(
+        lambda mod, inp, out: gpu_calls.append(out[1].cpu()))
     try:
         with torch.no_grad():
             out_gpu = m(pixel_values=pv)
     finally:
         h1.remove()
         h2.remove()
+        h4.remove()
     # the same model on the CPU, fed with the GPU hot-path features
     mc = _full_model().cpu().eval()
     assert mask_predictor.uninstall(mc) == 1  # the reference HF modules are the CPU checker
@@ -169,9 +173,24 @@ def test_full_model_mask_logits_fp32(golden):
     assert worst <= 1e-4
     err = float(np.abs(out.masks_queries_logits.numpy() - g5["mask_logits"]).max())
     gpu = float(np.abs(out_gpu.masks_queries_logits.cpu().numpy() - g5["mask_logits"]).max())
-    print(f"mask-logit max-abs-err (fp32): hot path {err:.3g}; everything on the GPU {gpu:.3g}")
+    # Everything on the GPU: the HF decoder layers (GPU vs CPU GEMMs, 1e-6 apart) feed the
+    # sigmoid(mask) < 0.5 attention binarisation between layers; an attention bit whose logit
+    # sits within float noise of 0 may flip, which moves later logits by ~1e-3.  Such flips are
+    # counted against the CPU run's own interpolated logits: every flipped bit must lie within
+    # 1e-3 of the threshold, and only then is the end-to-end bound relaxed to 1e-2.
+    assert len(gpu_calls) == len(calls)
+    flips, explained = 0, True
+    for attn_g, ((_, _, size), (mask_ref, attn_ref)) in zip(gpu_calls, calls):
+        val = torch.nn.functional.interpolate(mask_ref, size=size, mode="bilinear", align_corners=False).flatten(2)
+        val = val.unsqueeze(1).expand(-1, hip_pred.num_heads, -1, -1).flatten(0, 1)
+        d = attn_g != attn_ref
+        flips += int(d.sum())
+        explained &= bool((val[d].abs() < 1e-3).all())
+    print(f"mask-logit max-abs-err (fp32): hot path {err:.3g}; everything on the GPU {gpu:.3g} "
+          f"({flips} near-threshold attention-mask flips)")
     assert err <= 1e-3
-    assert gpu <= 1e-3
+    assert explained, "an attention-mask bit flipped away from the threshold"
+    assert gpu <= (1e-3 if flips == 0 else 1e-2)
     np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-3)
 
 
