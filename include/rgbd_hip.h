@@ -67,6 +67,19 @@ size_t rgbd_assemble_workspace_size(int B);
 int rgbd_assemble_pixel_values(const uint8_t* rgb_u8, const uint8_t* depth_u8, int B, int H, int W,
                                float* pv, void* ws, void* stream);
 
+/* ---------------------------------------------------------------- a11 labels
+ * Replaces the label half of map_10channel_case2 (dataloader.py:391-423): the processor's
+ * convert_segmentation_map_to_binary_masks (transformers image_processing_pil_mask2former.py:81-115)
+ * on the annotation's instance channel.
+ * rgbd_instance_presence: instance_map uint8 [B][H][W] (16-byte aligned; H*W % 16 == 0 when
+ *   B > 1) -> presence uint32 [B][8] (zeroed here), bit id of image b = id occurs in the map.
+ * rgbd_instance_masks: for j < n, masks[j] (float32 [H][W], 16-byte aligned, H*W % 16 == 0) =
+ *   (instance_map[image_of[j]] == ids[j]) as 1.0 / 0.0; ids / image_of int32 [n] on the device.
+ * The host orders ids ascending per image and drops ignore_index, like np.unique. */
+int rgbd_instance_presence(const uint8_t* instance_map, int B, int H, int W, uint32_t* presence, void* stream);
+int rgbd_instance_masks(const uint8_t* instance_map, int H, int W, const int* ids, const int* image_of, int n,
+                        float* masks, void* stream);
+
 /* ---------------------------------------------------------------- K3 E-DSAM decomposition
  * Replaces, per image and ONCE for all three DSAMs, DSAModule.forward lines 661-687:
  * to_grayscale (custom_model.py:466-480) -> nanmin/nanmax -> np.histogram(512) ->

@@ -179,3 +179,34 @@ def test_degenerate_depth_raises_value_error(case):
     with torch.no_grad(), pytest.raises(ValueError):
         m(pixel_values=pv)
     torch.cuda.synchronize()
+
+
+def test_instance_labels_match_image_processor(golden):
+    """a11 labels on the device (rgbd_amd.data.instance_labels) against the processor's own
+    mask_labels / class_labels (g0_processor.npz), plus a batch with an all-background map."""
+    from oracle import labels as labels_o
+    from rgbd_amd import data
+    g0 = golden("g0_processor")
+    for tag, (H, W) in {"small": (64, 96), "c2": (480, 640)}.items():
+        sc = synthetic.make_scene(synthetic.scene_seed(70, 0), H, W)
+        inst, table = gi.instance_map(sc)
+        masks, classes = data.instance_labels(torch.from_numpy(inst[None]).to(DEV), [table])
+        m = masks[0].cpu().numpy()
+        assert tuple(m.shape) == tuple(g0[f"{tag}_masks_shape"])
+        assert hashlib.sha256(np.ascontiguousarray(m).tobytes()).hexdigest() == str(g0[f"{tag}_masks_sha"]), tag
+        np.testing.assert_array_equal(classes[0].cpu().numpy(), g0[f"{tag}_classes"])
+    scenes = [synthetic.make_scene(synthetic.scene_seed(71, i), 48, 80) for i in range(3)]
+    maps, tables = zip(*[gi.instance_map(s) for s in scenes])
+    maps = np.stack(maps)
+    maps[1] = 0                                            # background only -> no instance
+    out = data.map_10channel(torch.from_numpy(np.stack([s["rgb_u8"] for s in scenes])).to(DEV),
+                             torch.from_numpy(np.stack([s["depth_u8"] for s in scenes])).to(DEV),
+                             torch.from_numpy(maps).to(DEV), list(tables))
+    for b in range(3):
+        em, ec = labels_o.instance_labels(maps[b], tables[b], ignore_index=0)
+        np.testing.assert_array_equal(out["mask_labels"][b].cpu().numpy(), em)
+        np.testing.assert_array_equal(out["class_labels"][b].cpu().numpy(), ec)
+    assert out["mask_labels"][1].shape[0] == 0
+    batch = data.collate_fn_v2([{k: (v[b] if k == "pixel_values" else v[b]) for k, v in out.items()}
+                                for b in range(3)])
+    assert tuple(batch["pixel_values"].shape) == (3, 10, 48, 80) and len(batch["mask_labels"]) == 3
