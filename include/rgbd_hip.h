@@ -125,6 +125,13 @@ int rgbd_dggm_fuse_fwd_multi(int dtype, int n, const void* const* cp1_host, cons
                              void* const* out_host, const float* const* weight_host, const float* const* bias_host,
                              const int* C_host, const int* h_host, const int* w_host, const float* grad,
                              const float* mask, long long pv_batch_stride, int B, int H, int W, void* stream);
+/* rgbd_dggm_fuse_fwd_multi with per-scale cp1 layout: bit k of cp1_nhwc_mask set = scale k's cp1
+ * is NHWC dtype [B][h][w][C] (C % 8 == 0; the DSAM cascade's layout), else NCHW. */
+int rgbd_dggm_fuse_fwd_multi_mixed(int dtype, int n, const void* const* cp1_host, int cp1_nhwc_mask,
+                                   const void* const* color_host, void* const* out_host,
+                                   const float* const* weight_host, const float* const* bias_host, const int* C_host,
+                                   const int* h_host, const int* w_host, const float* grad, const float* mask,
+                                   long long pv_batch_stride, int B, int H, int W, void* stream);
 size_t rgbd_dggm_fuse_bwd_multi_workspace_size(int n, const int* C_host, const int* h_host, const int* w_host,
                                                int B);
 int rgbd_dggm_fuse_bwd_multi(int dtype, int n, const void* const* dout_host, const float* const* weight_host,
@@ -169,6 +176,12 @@ size_t rgbd_dsam_conv_workspace_size(int dtype, int B, int Cin, int h, int w, in
 int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
                   int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
                   const void* residual, void* out_nchw, void* out_nhwc, void* ws, void* stream);
+/* The same forward with everything in NHWC (RGBD_BF16 only; the hot path's cascade): residual_nhwc
+ * (may be NULL) and out_nhwc dtype [B][ho][wo][Cout]; no NCHW output.  Same arithmetic and
+ * rounding as rgbd_dsam_fwd (res + (acc + bias), one rounding). */
+int rgbd_dsam_fwd_nhwc(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                       int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
+                       const void* residual_nhwc, void* out_nhwc, void* ws, void* stream);
 /* dX of one DSAModule, plus the upstream gradient of its input's other consumer:
  *   dx = gin + sum_i m_i * ConvT_i(gout) + ConvT_proj(gout)
  * gout_nhwc: dtype [B][ho][wo][Cout].  At least one of dx_nchw (dtype [B][Cin][h][w]) and

@@ -42,6 +42,8 @@ SIGNATURES = {
     "rgbd_dggm_fuse_bwd_workspace_size": (_SZ, [_I, _I, _I, _I]),
     "rgbd_dggm_fuse_bwd": (_I, [_I, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_dggm_fuse_fwd_multi": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _P]),
+    "rgbd_dggm_fuse_fwd_multi_mixed": (_I, [_I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LL, _I, _I, _I,
+                                            _P]),
     "rgbd_dggm_fuse_bwd_multi_workspace_size": (_SZ, [_I, _P, _P, _P, _I]),
     "rgbd_dggm_fuse_bwd_multi": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _LL, _I, _I, _I, _P, _P]),
     "rgbd_nchw_to_nhwc": (_I, [_I, _P, _P, _I, _I, _I, _I, _P]),
@@ -50,6 +52,7 @@ SIGNATURES = {
     "rgbd_dsam_code_masks": (_I, [_I, _P, _P, _P, _P]),
     "rgbd_dsam_conv_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rgbd_dsam_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "rgbd_dsam_fwd_nhwc": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_data": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_weight_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rgbd_dsam_bwd_weight": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),

@@ -383,7 +383,25 @@ __device__ __forceinline__ TileGates<PX> stage_gates(float (*sg)[512], float4* s
 
 // One (pixel tile bx, 32-channel block by) of the fused forward; the kernels below map block
 // indices onto it (one scale per launch, or all scales in one launch).
-template <typename T, int PX, bool HAS1>
+// One pixel's 8 channels [c0, c0+8) of an NHWC map -> v[cc][j] (cc < 8); C % 8 == 0.
+template <typename T, int PX>
+__device__ __forceinline__ void load_nhwc8(const T* p, float (&v)[kWaveCh][PX], int j) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[2 * q][j] = __uint_as_float(w[q] << 16);
+      v[2 * q + 1][j] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  } else {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    v[0][j] = a.x; v[1][j] = a.y; v[2][j] = a.z; v[3][j] = a.w;
+    v[4][j] = b.x; v[5][j] = b.y; v[6][j] = b.z; v[7][j] = b.w;
+  }
+}
+
+template <typename T, int PX, bool HAS1, bool CP1_NHWC = false>
 __device__ __forceinline__ void dggm_fwd_block(float (*sg)[512], float4* swb, int bx, int by,
                                                const T* __restrict__ cp1, const T* __restrict__ color,
                                                const float* __restrict__ grad, const float* __restrict__ mask,
@@ -401,8 +419,11 @@ __device__ __forceinline__ void dggm_fwd_block(float (*sg)[512], float4* swb, in
   for (int cc = 0; cc < kWaveCh; ++cc) {
     const long long o = ((long long)b * C + min(cw + cc, C - 1)) * hw + t.p;
     PxN<T, PX>::load(color + o, col[cc]);
-    if constexpr (HAS1) PxN<T, PX>::load(cp1 + o, y[cc]);
+    if constexpr (HAS1 && !CP1_NHWC) PxN<T, PX>::load(cp1 + o, y[cc]);
   }
+  if constexpr (HAS1 && CP1_NHWC)  // cp1 NHWC (the DSAM cascade's layout): 8 channels per pixel load
+#pragma unroll
+    for (int j = 0; j < PX; ++j) load_nhwc8<T, PX>(cp1 + ((long long)b * hw + t.p + j) * C + cw, y, j);
   __builtin_amdgcn_sched_barrier(0);  // keep the whole load batch ahead of the first use
 #pragma unroll
   for (int cc = 0; cc < kWaveCh; ++cc) {
@@ -557,6 +578,7 @@ struct DggmScaleArgs {
   float* dw;          // bwd outputs
   float* db;
   int C, h, w, px, nbx, blk0, tiles;
+  int cp1_nhwc;       // fwd: cp1 is NHWC [B][h][w][C] (C % 8 == 0)
 };
 struct DggmMulti {
   DggmScaleArgs s[DGGM_MAX_SCALES];
@@ -581,7 +603,17 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_fwd_multi(DggmMulti m, const 
   const DggmScaleArgs& d = m.s[k];
   const int local = blockIdx.x - d.blk0, bx = local % d.nbx, by = local / d.nbx;
   const T* cp1 = (const T*)d.cp1;
-  if (cp1) {
+  if (cp1 && d.cp1_nhwc) {
+    if (d.px == 8)
+      dggm_fwd_block<T, 8, true, true>(sg, swb, bx, by, cp1, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w,
+                                       d.wt, d.bias, (T*)d.out);
+    else if (d.px == 4)
+      dggm_fwd_block<T, 4, true, true>(sg, swb, bx, by, cp1, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w,
+                                       d.wt, d.bias, (T*)d.out);
+    else
+      dggm_fwd_block<T, 1, true, true>(sg, swb, bx, by, cp1, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w,
+                                       d.wt, d.bias, (T*)d.out);
+  } else if (cp1) {
     if (d.px == 8)
       dggm_fwd_block<T, 8, true>(sg, swb, bx, by, cp1, (const T*)d.color, grad, mask, pvs, H, W, d.C, d.h, d.w, d.wt,
                                  d.bias, (T*)d.out);
@@ -818,6 +850,15 @@ int rgbd_dggm_fuse_fwd_multi(int dtype, int n, const void* const* cp1_host, cons
                              void* const* out_host, const float* const* weight_host, const float* const* bias_host,
                              const int* C_host, const int* h_host, const int* w_host, const float* grad,
                              const float* mask, long long pv_batch_stride, int B, int H, int W, void* stream) {
+  return rgbd_dggm_fuse_fwd_multi_mixed(dtype, n, cp1_host, 0, color_host, out_host, weight_host, bias_host, C_host,
+                                        h_host, w_host, grad, mask, pv_batch_stride, B, H, W, stream);
+}
+
+int rgbd_dggm_fuse_fwd_multi_mixed(int dtype, int n, const void* const* cp1_host, int cp1_nhwc_mask,
+                                   const void* const* color_host, void* const* out_host,
+                                   const float* const* weight_host, const float* const* bias_host, const int* C_host,
+                                   const int* h_host, const int* w_host, const float* grad, const float* mask,
+                                   long long pv_batch_stride, int B, int H, int W, void* stream) {
   RGBD_REQUIRE(grad && mask && color_host && out_host && weight_host && bias_host && B > 0 && H > 0 && W > 0,
                RGBD_E_ARG);
   DggmMulti m;
@@ -826,6 +867,8 @@ int rgbd_dggm_fuse_fwd_multi(int dtype, int n, const void* const* cp1_host, cons
   for (int k = 0; k < n; ++k) {
     RGBD_REQUIRE(color_host[k] && out_host[k] && weight_host[k] && bias_host[k], RGBD_E_ARG);
     m.s[k].cp1 = cp1_host ? cp1_host[k] : nullptr;
+    m.s[k].cp1_nhwc = (cp1_nhwc_mask >> k) & 1;
+    RGBD_REQUIRE(!m.s[k].cp1_nhwc || (C_host[k] % 8 == 0 && m.s[k].cp1), RGBD_E_SHAPE);
     m.s[k].color = color_host[k];
     m.s[k].out = out_host[k];
     m.s[k].wt = weight_host[k];

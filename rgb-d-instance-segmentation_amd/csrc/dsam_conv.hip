@@ -51,6 +51,7 @@ struct ConvArgs {
   int ntiles0;                      // bf16: tiles of the largest class
   int chunk_len;                    // bf16: steps per workgroup chunk of a tile
   float* partial;                   // bf16: partial tiles of multi-chunk tiles (reduced by their last chunk)
+  const bf16_t* zero;               // bf16: LD_ZERO_BYTES of zeros (zeroed by k_dsam_plan)
 };
 
 constexpr int BM = 64, BN = 64;
@@ -921,18 +922,21 @@ __global__ __launch_bounds__(256) void k_dsam_bias_grad(const float* __restrict_
 // and the tile's steps are cut into nc = ceil(steps / chunk_len) equal chunks, one workgroup
 // each; the last chunk of a multi-chunk tile to finish sums the f32 partials in chunk order.
 constexpr int LD_BM = 128, LD_BN = 192, LD_CH = 8;  // tile rows, tile columns, max chunks per tile
+constexpr int LD_MAXSTEP = 2048;    // steps of one tile (9 taps x 16 codes x chunk groups)
+constexpr int LD_ZERO_BYTES = 512;  // zeroed global row the DMA reads for masked-out A rows
 constexpr int LD_A1 = LD_BM * 64;   // 8 KB per chunk
 constexpr int LD_B1 = LD_BN * 64;   // 12 KB per chunk
 template <int KC>
 struct LdCfg {
-  static constexpr int S = KC == 3 ? 2 : 3;
+  static constexpr int S = KC == 3 ? 2 : (KC == 2 ? 3 : 6);  // ring depth the LDS admits
   static constexpr int A = KC * LD_A1;
   static constexpr int STAGE = KC * (LD_A1 + LD_B1);
   static constexpr int ROWTAB = S * STAGE;                // [128] int4 row table
   static constexpr int ROWOUT = ROWTAB + LD_BM * 16;      // [128] int4 NCHW base, NHWC pixel, n_masks
   static constexpr int TMASK = ROWOUT + LD_BM * 16;       // [9] u32 code set per tap, [9][16] u8 code list
   static constexpr int BSUM = TMASK + 64 + 160;           // [5][192] f32 bias prefix sums
-  static constexpr size_t SMEM = BSUM + 5 * LD_BN * 4;
+  static constexpr int STEPTAB = BSUM + 5 * LD_BN * 4;    // [LD_MAXSTEP] int: tap | cg << 4 | code << 12
+  static constexpr size_t SMEM = STEPTAB + LD_MAXSTEP * 4;
   static_assert(SMEM <= 163840, "LDS budget");
 };
 constexpr int LD_EPI_LD = LD_BM + 4;  // epilogue LDS tile [96 n][132] f32 (two halves)
@@ -1058,6 +1062,8 @@ __global__ __launch_bounds__(128) void k_dsam_plan(ConvArgs a, int ntiles0, int 
     }
   __syncthreads();
   if (tid < 16) a.tmasks[((long long)cls * ntiles0 + tile) * 16 + tid] = tid < 9 ? (uint16_t)tm_s[tid] : 0;
+  if (cls == 0 && tile == 0 && tid < LD_ZERO_BYTES / 16)
+    reinterpret_cast<uint4*>(const_cast<bf16_t*>(a.zero))[tid] = make_uint4(0u, 0u, 0u, 0u);
   for (int q = tid; q < ntn; q += 128) a.tickets[((long long)cls * ntiles0 + tile) * ntn + q] = 0;
 }
 
@@ -1139,13 +1145,17 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
       for (int sb = 0; sb < k; ++sb) s += a.bias4[sb * a.N + n];
     bsum[e] = s;
   }
-  if (tid < 9) {
+  if (tid < 9) {  // per tap: its code list, and its run of the step table (chunk group major)
     uint32_t msk = tmask[tid];
     int n = 0;
     while (msk) {
       tcl[tid * 16 + n++] = (uint8_t)(__ffs(msk) - 1);
       msk &= msk - 1u;
     }
+    int* steptab = (int*)(smem + Cfg::STEPTAB);
+    int e = tb[tid];
+    for (int cg = 0; cg < ncg; ++cg)
+      for (int ci = 0; ci < n; ++ci) steptab[e++] = tid | (cg << 4) | ((int)tcl[tid * 16 + ci] << 12);
   }
   if (tid < LD_BM) {
     int b, i, j, org;
@@ -1162,44 +1172,36 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     rowout[tid] = make_int4(obase, opix, nmk, 0);
   }
   __syncthreads();
-  // DMA role: A rows 16*wave + lane/4 of every chunk, slot lane%4
+  // DMA role: A rows 16*wave + lane/4 of every chunk, slot lane%4.  A row that is outside the
+  // input at the step's tap, or whose source code is not the step's code, is read from the zero
+  // row instead: it contributes exactly zero, with no masking of fragments in registers.
   const int R = 16 * wave + (lane >> 2);
-  int aorg, afall, achk;
-  uint32_t aval;
+  int aorg, achk;
+  uint32_t aval, alo, ahi;
   {
     const int4 e = rowtab[R];
     aorg = e.x;
     aval = (uint32_t)e.y;
-    afall = e.y == 0 ? 0 : (a.transposed ? e.x : e.x + a.Wi + 1);
+    alo = (uint32_t)e.z;
+    ahi = (uint32_t)e.w;
     achk = 8 * ((lane & 3) ^ lds_swz(R));
   }
-  uint32_t cval[4], clo[4], chi[4];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int4 e = rowtab[wm * 64 + 16 * mi + r];
-    cval[mi] = (uint32_t)e.y;
-    clo[mi] = (uint32_t)e.z;
-    chi[mi] = (uint32_t)e.w;
-  }
+  const int* steptab = (const int*)(smem + Cfg::STEPTAB);
+  const bf16_t* zrow = a.zero + achk;
   const int s0 = (int)((long long)chunk * total / nc), s1 = (int)((long long)(chunk + 1) * total / nc);
   const int nst = (a.dbg & 1) ? 0 : s1 - s0;
-  int st_t[S], st_code[S];
   auto issue = [&](int slot, int s) {  // step s (absolute)
-    int t = 0;
-#pragma unroll
-    for (int q = 1; q < 9; ++q) t += s >= tb[q] ? 1 : 0;
-    t = __builtin_amdgcn_readfirstlane(t);
-    const int cnt = __popc(tmask[t]);
-    const int rel = s - tb[t], cg = rel / cnt, ci = rel - cg * cnt;
-    const int code = __builtin_amdgcn_readfirstlane((int)tcl[t * 16 + ci]);
+    const int e = __builtin_amdgcn_readfirstlane(steptab[s]);
+    const int t = e & 15, cg = (e >> 4) & 255, code = e >> 12;
     int ky, kx, dy, dx;
     ld_tap(a, G, t, ky, kx, dy, dx);
     const int delta = dy * a.Wi + dx, tap = ky * 3 + kx;
     const uint32_t sb = lds0 + slot * Cfg::STAGE;
-    const int pix = ((aval >> t) & 1u) ? aorg + delta : afall;
-    const bf16_t* asrc = xp + (long long)pix * a.C + cg * 32 * KC + achk;
+    const uint32_t rc = (t < 8 ? alo >> (4 * t) : ahi) & 15u;
+    const bool live = ((aval >> t) & 1u) && rc == (uint32_t)code;
+    const bf16_t* asrc = live ? xp + (long long)(aorg + delta) * a.C + cg * 32 * KC + achk : zrow;
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) dma_lds16(asrc + kc * 32, sb + kc * LD_A1 + wave * 1024);
+    for (int kc = 0; kc < KC; ++kc) dma_lds16(live ? asrc + kc * 32 : zrow, sb + kc * LD_A1 + wave * 1024);
     const long long tstride = (long long)a.N * 32;  // one (code, tap, chunk) tile, elements
     const bf16_t* bsrc = wp + ((long long)(code * 9 + tap) * (a.C / 32) + cg * KC) * tstride + (long long)n0 * 32 + lane * 8;
 #pragma unroll
@@ -1209,12 +1211,6 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
       dma_lds16(tbk + wave * 512, db + wave * 1024);
       if (wave < 4) dma_lds16(tbk + (wave + 8) * 512, db + (wave + 8) * 1024);
     }
-#pragma unroll
-    for (int q = 0; q < S; ++q)
-      if (q == slot) {
-        st_t[q] = t;
-        st_code[q] = code;
-      }
   };
   const int cnt = KC * (wave < 4 ? 3 : 2);  // DMA instructions of this wave per step
   f32x4 acc[4][3];
@@ -1224,50 +1220,39 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int npro = nst < S - 1 ? nst : S - 1;
   for (int i = 0; i < npro; ++i) issue(i, s0 + i);
-  if (npro >= 2) vm_wait_barrier_dyn(cnt);
+  if (npro >= 2) vm_wait_barrier_dyn((npro - 1) * cnt);  // step 0 landed, later ones may fly
   else vm_wait_barrier<0>();
 #pragma unroll 1
   for (int s = 0; s < nst; ++s) {
     if (s + S - 1 < nst) issue((s + S - 1) % S, s0 + s + S - 1);
-    const int slot = s % S;
-    int t = 0, code = 0;
-#pragma unroll
-    for (int q = 0; q < S; ++q)
-      if (q == slot) {
-        t = st_t[q];
-        code = st_code[q];
-      }
-    uint32_t keep = 0u;  // bit mi: row mi's code at tap t is the step's code
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const uint32_t c = (t < 8 ? clo[mi] >> (4 * t) : chi[mi]) & 15u;
-      keep |= (((cval[mi] >> t) & 1u) && c == (uint32_t)code) ? 1u << mi : 0u;
-    }
-    const char* sa = smem + slot * Cfg::STAGE;
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      Frag<bf16_t> fa[4], fb[3];
+    const char* sa = smem + (s % S) * Cfg::STAGE;
+    // fragments of chunk kc+1 are read while chunk kc's 12 MFMAs run
+    Frag<bf16_t> fa[2][4], fb[2][3];
+    auto rd = [&](int kc, int q) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int row = wm * 64 + 16 * mi + r;
-        fa[mi].v = *reinterpret_cast<const uint4*>(sa + kc * LD_A1 + row * 64 + 16 * (g ^ lds_swz(row)));
-        fa[mi].select((keep >> mi) & 1u);
+        fa[q][mi].v = *reinterpret_cast<const uint4*>(sa + kc * LD_A1 + row * 64 + 16 * (g ^ lds_swz(row)));
       }
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj) {
         const int row = wn * 48 + 16 * nj + r;
-        fb[nj].v = *reinterpret_cast<const uint4*>(sa + Cfg::A + kc * LD_B1 + row * 64 + 16 * (g ^ lds_swz(row)));
+        fb[q][nj].v = *reinterpret_cast<const uint4*>(sa + Cfg::A + kc * LD_B1 + row * 64 + 16 * (g ^ lds_swz(row)));
       }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      if (kc + 1 < KC) rd(kc + 1, (kc + 1) & 1);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int nj = 0; nj < 3; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
+        for (int nj = 0; nj < 3; ++nj) mma(acc[mi][nj], fa[kc & 1][mi], fb[kc & 1][nj]);
     }
     // own DMA of step s+1 landed (only later steps' may stay in flight), LDS reads done, barrier
     const int ahead = (nst - 1 < s + S - 1 ? nst - 1 : s + S - 1) - (s + 1);
     if (ahead <= 0) vm_wait_barrier<0>();
-    else if (ahead == 1) vm_wait_barrier_dyn(cnt);
-    else vm_wait_barrier_dyn(2 * cnt);
+    else vm_wait_barrier_dyn(ahead * cnt);
   }
   if (nc > 1) {
     // Multi-chunk tile: publish this chunk's fragment-native partial ([wave][mi][nj][lane][4] f32),
@@ -1314,6 +1299,58 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   // pass 1 runs along pixels (NCHW residual loads and stores), pass 2 along channels (NHWC);
   // every thread's loads of a pass are independent and issued together.
   if (a.dbg & 2) return;  // RGBD_DSAM_DBG=2: no epilogue (timing experiments only)
+  if (!a.out_nchw) {
+    // NHWC-only epilogue (the hot path's forward cascade and dX): one pass.  The accumulators go
+    // to an LDS image [128 rows][196] f32 (rows = tile pixels; the 4-float pad makes the 4 rows
+    // a wave writes per register land on disjoint banks), then each thread owns 6 (row, 8-channel)
+    // items: all six 16-byte NHWC residual loads in flight together, two 16-byte LDS reads, the
+    // bias sum of the row's image, res + (acc + bias) rounded once, one 16-byte store.
+    constexpr int LDE = LD_BN + 4;
+    constexpr int NCH = LD_BN / 8;
+    constexpr int NIT = LD_BM * NCH / 512;
+    static_assert(LD_BM * LDE * 4 <= Cfg::ROWTAB, "epilogue image must not overlap the row tables");
+    float* et = (float*)smem;
+    __syncthreads();  // ring reads done
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 3; ++nj)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+          et[(wm * 64 + 16 * mi + 4 * g + reg) * LDE + wn * 48 + 16 * nj + r] = acc[mi][nj][reg];
+    __syncthreads();
+    const bf16_t* rnhwc = (const bf16_t*)a.residual_nhwc;
+    bf16_t* onhwc = (bf16_t*)a.out_nhwc;
+    uint4 rv[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int it = tid + 512 * i, ml = it / NCH, n = n0 + 8 * (it % NCH);
+      const int4 ro = rowout[ml];
+      rv[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (rnhwc && ro.x >= 0 && n < a.N) rv[i] = *reinterpret_cast<const uint4*>(rnhwc + (long long)ro.y * a.N + n);
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int it = tid + 512 * i, ml = it / NCH, nl = 8 * (it % NCH), n = n0 + nl;
+      const int4 ro = rowout[ml];
+      if (ro.x < 0 || n >= a.N) continue;
+      const float4 e0 = *reinterpret_cast<const float4*>(et + ml * LDE + nl);
+      const float4 e1 = *reinterpret_cast<const float4*>(et + ml * LDE + nl + 4);
+      float v[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      const uint32_t uw[4] = {rv[i].x, rv[i].y, rv[i].z, rv[i].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bsum[ro.z * LD_BN + nl + e];
+      if (rnhwc)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] = __uint_as_float(uw[e] << 16) + v[2 * e];
+          v[2 * e + 1] = __uint_as_float(uw[e] & 0xffff0000u) + v[2 * e + 1];
+        }
+      *reinterpret_cast<uint4*>(onhwc + (long long)ro.y * a.N + n) =
+          make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
+    return;
+  }
   float* et = (float*)smem;  // [96 n][LD_EPI_LD] f32
   const bf16_t* res = (const bf16_t*)a.residual;
   bf16_t* onchw = (bf16_t*)a.out_nchw;
@@ -1464,7 +1501,7 @@ LdPlan ld_plan(const ConvArgs& a) {
   p.chunk_len = std::max(1, (ntap * (a.C / (32 * p.kc)) * pct + 99) / 100);
   p.tmask_bytes = align256((size_t)nclass * p.ntiles0 * 16 * sizeof(uint16_t));
   p.items_bytes = align256(((size_t)nclass * p.ntiles0 * LD_CH + 1) * sizeof(int));
-  p.ticket_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * sizeof(int));
+  p.ticket_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * sizeof(int)) + LD_ZERO_BYTES;
   p.partial_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * LD_CH * LD_BN * LD_BM * sizeof(float));
   return p;
 }
@@ -1502,6 +1539,8 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
     b.nitems = b.items + (size_t)nclass * P.ntiles0 * LD_CH;
     b.tickets = (int*)((char*)a.partial + P.tmask_bytes + P.items_bytes);
     b.partial = (float*)((char*)a.partial + P.tmask_bytes + P.items_bytes + P.ticket_bytes);
+    b.zero = (const bf16_t*)((char*)b.partial - LD_ZERO_BYTES);  // the ticket region's tail
+    RGBD_REQUIRE(9 * 16 * (a.C / (32 * P.kc)) <= LD_MAXSTEP, RGBD_E_SHAPE);
     b.ntiles0 = P.ntiles0;
     b.chunk_len = P.chunk_len;
     k_dsam_plan<<<dim3(P.ntiles0, 1, nclass), 128, 0, s>>>(b, P.ntiles0, P.ntn);
@@ -1678,6 +1717,19 @@ int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd
   if (dtype == RGBD_F32) return launch_conv<float>(a, s);
   if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);
   return RGBD_E_DTYPE;
+}
+
+int rgbd_dsam_fwd_nhwc(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                       int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
+                       const void* residual_nhwc, void* out_nhwc, void* ws, void* stream) {
+  RGBD_REQUIRE(dtype == RGBD_BF16, RGBD_E_DTYPE);
+  RGBD_REQUIRE(x_nhwc && code && info && wfwd && bias && out_nhwc && ws, RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
+  ConvArgs a = fwd_args(B, Cin, h, w, Cout);
+  a.x = x_nhwc; a.code = code; a.w = wfwd;
+  a.bias4 = bias; a.info = info; a.residual_nhwc = residual_nhwc; a.out_nhwc = out_nhwc;
+  a.partial = (float*)ws;
+  return launch_conv<bf16_t>(a, (hipStream_t)stream);
 }
 
 int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,

@@ -77,15 +77,28 @@ class HotPathFunction(torch.autograd.Function):
                  for k in range(3)]
         x_nhwc = [ops.nchw_to_nhwc(colors[0])]
         cp1 = [colors[0]]
-        for k in range(3):
-            bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
-            out, out_nhwc = ops.dsam_fwd(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual=colors[k + 1],
-                                         want_nhwc=(k < 2))
-            cp1.append(out)
-            if k < 2:
-                x_nhwc.append(out_nhwc)
+        if dtype == torch.bfloat16:
+            # bf16 cascade entirely in NHWC: each DSAM adds its residual colour map in NHWC and writes
+            # cp1[k+1] once, in the layout the next DSAM reads and the DGGM pass accepts
+            res_nhwc = [ops.nchw_to_nhwc(c) for c in colors[1:]]
+            for k in range(3):
+                bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
+                out_nhwc = ops.dsam_fwd_nhwc(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual_nhwc=res_nhwc[k])
+                cp1.append(out_nhwc)
+                if k < 2:
+                    x_nhwc.append(out_nhwc)
+            cp1_nhwc = (1, 2, 3)
+        else:
+            for k in range(3):
+                bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
+                out, out_nhwc = ops.dsam_fwd(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual=colors[k + 1],
+                                             want_nhwc=(k < 2))
+                cp1.append(out)
+                if k < 2:
+                    x_nhwc.append(out_nhwc)
+            cp1_nhwc = ()
         # DGGM gate + final sum of all four scales in one launch
-        outs = ops.dggm_fuse_fwd_multi(cp1, colors, pixel_values, dggm_p[0::2], dggm_p[1::2])
+        outs = ops.dggm_fuse_fwd_multi(cp1, colors, pixel_values, dggm_p[0::2], dggm_p[1::2], cp1_nhwc=cp1_nhwc)
         ctx.cfg = cfg
         ctx.codes = codes
         ctx.info = info

@@ -205,16 +205,21 @@ def _ints(xs):
     return (ctypes.c_int * len(xs))(*[int(x) for x in xs])
 
 
-def dggm_fuse_fwd_multi(cp1s, colors, pixel_values, weights, biases):
-    """dggm_fuse_fwd for every scale in one launch (rgbd_dggm_fuse_fwd_multi); cp1s may be None."""
+def dggm_fuse_fwd_multi(cp1s, colors, pixel_values, weights, biases, cp1_nhwc=()):
+    """dggm_fuse_fwd for every scale in one launch (rgbd_dggm_fuse_fwd_multi[_mixed]); cp1s may be
+    None; scales listed in ``cp1_nhwc`` take their cp1 as NHWC [B,h,w,C] (the DSAM cascade's
+    output layout) instead of NCHW."""
     _need_cuda(*colors, pixel_values)
     n = len(colors)
     B, _, H, W = pixel_values.shape
+    cp1_mask = 0
     if cp1s is not None:
         _need_cuda(*cp1s)
-        for a, c in zip(cp1s, colors):
-            if a.shape != c.shape or a.dtype != c.dtype:
+        for k, (a, c) in enumerate(zip(cp1s, colors)):
+            exp = (c.shape[0], c.shape[2], c.shape[3], c.shape[1]) if k in cp1_nhwc else tuple(c.shape)
+            if tuple(a.shape) != exp or a.dtype != c.dtype:
                 raise ValueError("cp1/color mismatch")
+            cp1_mask |= (1 << k) if k in cp1_nhwc else 0
     for c, w, b in zip(colors, weights, biases):
         if c.dtype != colors[0].dtype or c.shape[0] != B:
             raise ValueError("colour maps must share dtype and batch")
@@ -223,12 +228,12 @@ def dggm_fuse_fwd_multi(cp1s, colors, pixel_values, weights, biases):
     outs = [torch.empty_like(c) for c in colors]
     wts = [w.reshape(w.shape[0], 3).float().contiguous() for w in weights]
     bss = [b.float().contiguous() for b in biases]
-    grad, mask = _grad_mask(pixel_values)
-    check(_lib.lib().rgbd_dggm_fuse_fwd_multi(
-        _dtype_code(colors[0]), n, None if cp1s is None else _ptrs(cp1s), _ptrs(colors), _ptrs(outs), _ptrs(wts),
-        _ptrs(bss), _ints([c.shape[1] for c in colors]), _ints([c.shape[2] for c in colors]),
-        _ints([c.shape[3] for c in colors]), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(mask.data_ptr()),
-        pixel_values.stride(0), B, H, W, _stream(pixel_values.device)), "rgbd_dggm_fuse_fwd_multi")
+    grad, gmask = _grad_mask(pixel_values)
+    check(_lib.lib().rgbd_dggm_fuse_fwd_multi_mixed(
+        _dtype_code(colors[0]), n, None if cp1s is None else _ptrs(cp1s), cp1_mask, _ptrs(colors), _ptrs(outs),
+        _ptrs(wts), _ptrs(bss), _ints([c.shape[1] for c in colors]), _ints([c.shape[2] for c in colors]),
+        _ints([c.shape[3] for c in colors]), ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(gmask.data_ptr()),
+        pixel_values.stride(0), B, H, W, _stream(pixel_values.device)), "rgbd_dggm_fuse_fwd_multi_mixed")
     return outs
 
 
@@ -323,6 +328,28 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     check(L.rgbd_dsam_fwd(dt, _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co, _p(wfwd), _p(b4), _p(residual),
                           _p(out), _p(out_nhwc), _p(ws), _stream(x_nhwc.device)), "rgbd_dsam_fwd")
     return out, out_nhwc
+
+
+def dsam_fwd_nhwc(x_nhwc, code, info, wfwd, bias4, residual_nhwc=None):
+    """bfloat16 forward with NHWC residual and NHWC output only -> out_nhwc [B,ho,wo,Co]
+    (rgbd_dsam_fwd_nhwc; the hot path's cascade)."""
+    _need_cuda(x_nhwc, code, info, wfwd, bias4, residual_nhwc)
+    if x_nhwc.dtype != torch.bfloat16:
+        raise TypeError("dsam_fwd_nhwc is the bfloat16 path")
+    B, h, w, Ci = x_nhwc.shape
+    Co = bias4.shape[-1]
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    if tuple(code.shape) != (B, h, w):
+        raise ValueError(f"region code {tuple(code.shape)} does not match features {(B, h, w)}")
+    if residual_nhwc is not None and tuple(residual_nhwc.shape) != (B, ho, wo, Co):
+        raise ValueError(f"residual {tuple(residual_nhwc.shape)} != {(B, ho, wo, Co)}")
+    out = torch.empty((B, ho, wo, Co), dtype=x_nhwc.dtype, device=x_nhwc.device)
+    b4 = bias4.detach().float().contiguous()
+    L = _lib.lib()
+    ws = _workspace(x_nhwc.device, L.rgbd_dsam_conv_workspace_size(RGBD_BF16, B, Ci, h, w, Co), "dsam_conv")
+    check(L.rgbd_dsam_fwd_nhwc(RGBD_BF16, _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co, _p(wfwd), _p(b4),
+                               _p(residual_nhwc), _p(out), _p(ws), _stream(x_nhwc.device)), "rgbd_dsam_fwd_nhwc")
+    return out
 
 
 def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False, cin=None, gin_nhwc=None, want_nchw=True):

@@ -160,3 +160,51 @@ def test_nchw_to_nhwc_exact(shape, dtype):
     g.manual_seed(11)
     x = torch.randn(shape, generator=g, device=DEV).to(dtype)
     assert torch.equal(ops.nchw_to_nhwc(x), x.permute(0, 2, 3, 1).contiguous())
+
+
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_dsam_fwd_nhwc_equals_nchw_path(k):
+    """rgbd_dsam_fwd_nhwc (NHWC residual in, NHWC out only: the hot path's bf16 cascade) gives
+    bitwise the NHWC output of rgbd_dsam_fwd with the same residual in NCHW."""
+    from rgbd_amd.modules import DSAModule
+    cin, cout = [(96, 192), (192, 384), (384, 768)][k]
+    B, H, W = 8, 480, 640
+    h, w = [(120, 160), (60, 80), (30, 40)][k]
+    m = DSAModule(cin, cout)
+    winit.init_deterministic(m, prefix=f"nhwcfwd.dsam{k}.")
+    planes, _, _ = synthetic.make_batch(4, B, H, W)
+    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
+    codes, info = ops.edsam_decompose(d3, torch.linspace(0.05, 0.45, B, device=DEV), [(h, w)])
+    masks = ops.dsam_code_masks(codes)
+    conv_w = torch.stack([m.conv_layers[i].weight.detach() for i in range(4)]).to(DEV)
+    proj_w = m.rgb_projection.weight.detach().to(DEV)
+    bias4 = torch.stack([m.conv_layers[i].bias.detach() for i in range(4)]).to(DEV)
+    wf, _ = ops.dsam_pack(conv_w, proj_w, torch.bfloat16, code_mask=masks[0:1], want_bwd=False)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(500 + k)
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    x = torch.randn((B, h, w, cin), generator=g, device=DEV).bfloat16()
+    res = torch.randn((B, cout, ho, wo), generator=g, device=DEV).bfloat16()
+    _, ref_nhwc = ops.dsam_fwd(x, codes[0], info, wf, bias4, residual=res, want_nhwc=True)
+    got = ops.dsam_fwd_nhwc(x, codes[0], info, wf, bias4, residual_nhwc=ops.nchw_to_nhwc(res))
+    assert torch.equal(got, ref_nhwc)
+    no_res = ops.dsam_fwd_nhwc(x, codes[0], info, wf, bias4)
+    _, ref2 = ops.dsam_fwd(x, codes[0], info, wf, bias4, want_nhwc=True)
+    assert torch.equal(no_res, ref2)
+
+
+@pytest.mark.parametrize("shape", [(2, 96, 120, 160), (3, 192, 13, 17), (2, 384, 7, 9)])
+def test_dggm_cp1_nhwc_equals_nchw(shape):
+    """rgbd_dggm_fuse_fwd_multi_mixed with cp1 in NHWC gives bitwise the NCHW-cp1 result."""
+    import golden_inputs as gi
+    B, C, h, w = shape
+    H, W = 4 * h, 4 * w
+    pv = torch.from_numpy(gi.pixel_values(13, B, H, W)).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    color = torch.randn((B, C, h, w), generator=g, device=DEV).bfloat16()
+    cp1 = torch.randn((B, C, h, w), generator=g, device=DEV).bfloat16()
+    wt = torch.randn((C, 3, 1, 1), generator=g, device=DEV)
+    bs = torch.randn((C,), generator=g, device=DEV)
+    ref = ops.dggm_fuse_fwd_multi([cp1], [color], pv, [wt], [bs])[0]
+    got = ops.dggm_fuse_fwd_multi([ops.nchw_to_nhwc(cp1)], [color], pv, [wt], [bs], cp1_nhwc=(0,))[0]
+    assert torch.equal(got, ref)

@@ -27,9 +27,12 @@ for k, (ci, co) in enumerate([(96, 192), (192, 384), (384, 768)]):
     x = torch.randn((B, h, w, ci), generator=g, device=dev).bfloat16()
     b4 = torch.zeros((4, co), device=dev)
     resid = torch.randn((B, co, (h + 1) // 2, (w + 1) // 2), generator=g, device=dev).bfloat16()
+    resid_nhwc = ops.nchw_to_nhwc(resid)
     gy = torch.randn((B, (h + 1) // 2, (w + 1) // 2, co), generator=g, device=dev).bfloat16()
     gin = torch.randn((B, ci, h, w), generator=g, device=dev).bfloat16()
-    fns = {f"fwd{k}": lambda: ops.dsam_fwd(x, codes[k], info, wf, b4, residual=resid, want_nhwc=(k < 2))}
+    fns = {f"fwd{k}": lambda: ops.dsam_fwd(x, codes[k], info, wf, b4, residual=resid, want_nhwc=(k < 2)),
+           f"fwdh{k}": lambda: ops.dsam_fwd_nhwc(x, codes[k], info, wf, b4, residual_nhwc=resid_nhwc),
+           f"dw{k}": lambda: ops.dsam_bwd_weight(None, x, codes[k], info, gout_nhwc=gy)}
     if k > 0:
         fns[f"dx{k}"] = lambda: ops.dsam_bwd_data(gy, codes[k], wb, gin, want_nhwc=True)
         gin_nhwc = ops.nchw_to_nhwc(gin)
