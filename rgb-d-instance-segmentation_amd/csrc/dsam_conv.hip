@@ -467,6 +467,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, 
 //      registers from the entry's tap masks (staged in LDS with the item's unit ids).
 // Both MFMA operands are read with ds_read_b64_tr_b16 ([px][col] -> k-major fragments); rows are
 // XOR-swizzled by row bit 3 so the 32-lane halves of a transposed read fall on disjoint banks.
+constexpr int LD_ZERO_BYTES = 512;  // zeroed global row the DMA reads for masked-out operand rows
 constexpr int WPX = 64;        // output pixels per unit / step
 constexpr int WITEM_MAX = 64;  // units per item (LDS staging of ids + masks)
 typedef __attribute__((ext_vector_type(4))) short v4s;
@@ -496,6 +497,7 @@ struct WgArgs {
   int* counts;            // [0] live entries, [1] items
   int B, Cin, h, w, Cout, ho, wo, nunit, ntile_kk, ntile_o, target;
   float inv_wo;
+  const bf16_t* zero;     // LD_ZERO_BYTES of zeros (rows the im2col gather masks out)
   float* partial;         // [item][Cout][9*Cin] f32
 };
 
@@ -533,6 +535,8 @@ __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict
 constexpr int WG_PRES_LDS = 8192;  // presence entries k_wg_plan keeps in LDS
 __global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
   __shared__ int cnt_s[16], off_s[17];
+  if (threadIdx.x < LD_ZERO_BYTES / 16)
+    reinterpret_cast<uint4*>(const_cast<bf16_t*>(a.zero))[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
   __shared__ uint16_t spres[WG_PRES_LDS];  // the compaction pass re-reads presence from LDS
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int U = a.B * a.nunit;
@@ -659,20 +663,25 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
   // per-lane copy roles: pixel row pr of every block, 16-byte chunk q
   const int pr = 16 * wave + (lane >> 2);
   const int qch = 8 * ((lane & 3) ^ wg_swz(pr));
+  // transposed fragment [k = 8g + j][col = c0 + r] of a [64 px][32 col] block (64-byte rows): the
+  // XOR swizzle term depends on row bit 3 = g & 1 only, so every read of a lane is its base
+  // address plus a compile-time offset
   const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-  // transposed fragment [k = 8g + j][col = c0 + r] of a [64 px][32 col] block (64-byte rows)
-  auto trfrag = [&](const char* blk, int kb, int c0) {
-    const int col = c0 + 4 * p4, ch = col >> 3, off = (col & 7) * 2;
-    const int row0 = 32 * kb + 8 * g + q4, row1 = row0 + 4;
-    v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) v4s*)(blk + row0 * 64 + 16 * (ch ^ wg_swz(row0)) + off));
-    v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) v4s*)(blk + row1 * 64 + 16 * (ch ^ wg_swz(row1)) + off));
+  const int trow = 8 * g + q4;
+  const int tbase0 = trow * 64 + 16 * ((p4 >> 1) ^ wg_swz(trow)) + (4 * p4 & 7) * 2;        // c0 = 0
+  const int tbase16 = trow * 64 + 16 * ((2 | (p4 >> 1)) ^ wg_swz(trow)) + (4 * p4 & 7) * 2;  // c0 = 16
+  typedef __attribute__((address_space(3))) char lds_char;
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  lds_char* const lsm = (lds_char*)smem;  // one generic -> LDS conversion, not one per read
+  lds_char* b0 = lsm;   // this step's slot + the lane's base, per c0
+  lds_char* b16 = lsm;
+  auto trfrag = [&](int blk, int kb, int c0) {  // blk: block byte offset in the slot; c0 in {0, 16}
+    lds_char* p = (c0 ? b16 : b0) + blk + kb * 32 * 64;
+    const v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p);
+    const v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p + 4 * 64));
     Frag<bf16_t> f;
-    f.v = make_uint4((uint32_t)(uint16_t)t0.x | ((uint32_t)(uint16_t)t0.y << 16),
-                     (uint32_t)(uint16_t)t0.z | ((uint32_t)(uint16_t)t0.w << 16),
-                     (uint32_t)(uint16_t)t1.x | ((uint32_t)(uint16_t)t1.y << 16),
-                     (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
+    const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
+    f.v = make_uint4(u0.x, u0.y, u1.x, u1.y);
     return f;
   };
   for (int wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
@@ -683,19 +692,23 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
     for (int i = tid; i < nst; i += 256) sunits[i] = a.list[e0 + i] & 0xffffff;
     for (int i = tid; i < nst * 9; i += 256) smasks[i] = a.masks[(long long)e0 * 9 + i];
     __syncthreads();
-    int xky[4], xkx[4], xc[4], xtap[4];
-    bool xok[4];
+    // X block j: (tap, channel offset) uniform; source offset dy*w + dx from the row's origin
+    int xtap[4], xoff[4], xc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int kk = kk0 + 32 * j;
-      xok[j] = kk < KK;
-      xtap[j] = xok[j] ? kk / a.Cin : 0;
-      xky[j] = xtap[j] / 3;
-      xkx[j] = xtap[j] % 3;
-      xc[j] = xok[j] ? kk % a.Cin : 0;
+      const bool ok = kk < KK;
+      xtap[j] = ok ? kk / a.Cin : -1;
+      const int tp = ok ? xtap[j] : 0;
+      xoff[j] = (tp / 3) * a.w + tp % 3;
+      xc[j] = ok ? kk % a.Cin : 0;
     }
+    const bf16_t* zrow = a.zero + qch;
+    // One step = one unit: G rows (its 64 output pixels) and X rows (their im2col sources).  A
+    // row of X whose source is outside the input, past the image, or of another code than the
+    // item's reads the zero row: it contributes exactly zero, no masking in registers.
     auto issue = [&](int slot, int it) {
-      const int u = sunits[it];
+      const int u = __builtin_amdgcn_readfirstlane(sunits[it]);
       const int b = u / a.nunit;
       const int p = (u - b * a.nunit) * WPX + pr;
       const int pc = p < hwo ? p : hwo - 1;
@@ -704,10 +717,13 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
       const bf16_t* gsrc = a.gout + ((long long)b * hwo + pc) * a.Cout + qch;
 #pragma unroll
       for (int ob = 0; ob < FM; ++ob) dma_lds16(gsrc + min(o0 + 32 * ob, a.Cout - 32), sb + ob * 4096);
+      const int org = (b * a.h + 2 * oy - 1) * a.w + 2 * ox - 1;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int iyc = min(max(2 * oy - 1 + xky[j], 0), a.h - 1), ixc = min(max(2 * ox - 1 + xkx[j], 0), a.w - 1);
-        dma_lds16(a.x + (((long long)b * a.h + iyc) * a.w + ixc) * a.Cin + xc[j] + qch, sb + (FM + j) * 4096);
+        const unsigned long long m = xtap[j] >= 0 ? smasks[it * 9 + xtap[j]] : 0ull;
+        const bool live = (m >> pr) & 1ull;
+        const bf16_t* src = live ? a.x + (long long)(org + xoff[j]) * a.Cin + xc[j] + qch : zrow;
+        dma_lds16(src, sb + (FM + j) * 4096);
       }
     };
     f32x4 acc[FM][4];
@@ -723,30 +739,22 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
 #pragma unroll 1
     for (int s = 0; s < nst; ++s) {
       if (s + Cfg::S - 1 < nst) issue((s + Cfg::S - 1) % Cfg::S, s + Cfg::S - 1);
-      const int slot = s % Cfg::S;
-      const char* st = smem + slot * Cfg::STAGE;
+      int st = (s % Cfg::S) * Cfg::STAGE;
+      asm volatile("" : "+s"(st));  // no strength reduction of the slot offset into per-read registers
+      b0 = lsm + st + tbase0;
+      b16 = lsm + st + tbase16;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         Frag<bf16_t> fa[FM], fb[4];
 #pragma unroll
         for (int mi = 0; mi < FM; ++mi) {
           const int ol = wm * 16 * FM + 16 * mi;
-          fa[mi] = trfrag(st + (ol >> 5) * 4096, kb, ol & 31);
+          fa[mi] = trfrag((ol >> 5) * 4096, kb, ol & 31);
         }
 #pragma unroll
         for (int nj = 0; nj < 4; ++nj) {
-          const int kl = wn * 64 + 16 * nj, j = kl >> 5;
-          fb[nj] = trfrag(st + (FM + j) * 4096, kb, kl & 31);
-          // rows 32kb + 8g .. +7 of block j: keep the pixels whose source meets code k at tap_j
-          const uint32_t bits =
-              xok[j] ? (uint32_t)(smasks[s * 9 + xtap[j]] >> (32 * kb + 8 * g)) & 0xFFu : 0u;
-          if (bits != 0xFFu) {
-            auto hm = [&](int e) { return ((bits >> e) & 1u) ? 0xFFFFu : 0u; };
-            fb[nj].v.x &= hm(0) | (hm(1) << 16);
-            fb[nj].v.y &= hm(2) | (hm(3) << 16);
-            fb[nj].v.z &= hm(4) | (hm(5) << 16);
-            fb[nj].v.w &= hm(6) | (hm(7) << 16);
-          }
+          const int kl = wn * 64 + 16 * nj;
+          fb[nj] = trfrag((FM + (kl >> 5)) * 4096, kb, kl & 31);
         }
 #pragma unroll
         for (int mi = 0; mi < FM; ++mi)
@@ -782,33 +790,38 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restr
                                                             const int* __restrict__ counts, int Cin, int Cout,
                                                             float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
   extern __shared__ float srow[];  // [5][9*Cin]
+  __shared__ int scode[1024];      // item -> code, staged once
   const int KK = 9 * Cin, o = blockIdx.x, ni = counts[1];
-  for (int kk = threadIdx.x; kk < KK; kk += 256) {
-    float seg[4] = {0.f, 0.f, 0.f, 0.f}, pr = 0.f;
-    const float* src = partial + (long long)o * KK + kk;
+  for (int it = threadIdx.x; it < ni && it < 1024; it += 256) scode[it] = items[it].x;
+  __syncthreads();
+  // 4 consecutive kk per thread (16-byte loads), 8 items' loads in flight per iteration
+  for (int k4 = 4 * threadIdx.x; k4 < KK; k4 += 1024) {
+    float4 seg[4], pr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) seg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    pr = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* src = partial + (long long)o * KK + k4;
+    const long long istr = (long long)Cout * KK;
     int it = 0;
-    for (; it + 4 <= ni; it += 4) {
-      float v[4];
+    auto acc = [&](const float4 v, int k) {
+      pr.x += v.x; pr.y += v.y; pr.z += v.z; pr.w += v.w;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = src[(long long)(it + q) * Cout * KK];
+      for (int i = 0; i < 4; ++i)
+        if ((k >> i) & 1) {
+          seg[i].x += v.x; seg[i].y += v.y; seg[i].z += v.z; seg[i].w += v.w;
+        }
+    };
+    for (; it + 8 <= ni; it += 8) {
+      float4 v[8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int k = items[it + q].x;
-        pr += v[q];
+      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(src + (it + q) * istr);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) seg[i] += ((k >> i) & 1) ? v[q] : 0.f;
-      }
+      for (int q = 0; q < 8; ++q) acc(v[q], it + q < 1024 ? scode[it + q] : items[it + q].x);
     }
-    for (; it < ni; ++it) {
-      const float v = src[(long long)it * Cout * KK];
-      const int k = items[it].x;
-      pr += v;
+    for (; it < ni; ++it) acc(*reinterpret_cast<const float4*>(src + it * istr), it < 1024 ? scode[it] : items[it].x);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) seg[i] += ((k >> i) & 1) ? v : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) srow[i * KK + kk] = seg[i];
-    srow[4 * KK + kk] = pr;
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(srow + i * KK + k4) = seg[i];
+    *reinterpret_cast<float4*>(srow + 4 * KK + k4) = pr;
   }
   __syncthreads();
   for (int e = threadIdx.x; e < KK; e += 256) {  // e = c*9 + tap (OIHW order)
@@ -923,7 +936,6 @@ __global__ __launch_bounds__(256) void k_dsam_bias_grad(const float* __restrict_
 // each; the last chunk of a multi-chunk tile to finish sums the f32 partials in chunk order.
 constexpr int LD_BM = 128, LD_BN = 192, LD_CH = 8;  // tile rows, tile columns, max chunks per tile
 constexpr int LD_MAXSTEP = 2048;    // steps of one tile (9 taps x 16 codes x chunk groups)
-constexpr int LD_ZERO_BYTES = 512;  // zeroed global row the DMA reads for masked-out A rows
 constexpr int LD_A1 = LD_BM * 64;   // 8 KB per chunk
 constexpr int LD_B1 = LD_BN * 64;   // 12 KB per chunk
 template <int KC>
@@ -1756,7 +1768,7 @@ int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, in
 // bf16 workspace: [splits][16 codes][Cout][9 Cin] f32 partials | [B] f32 x Cout channel sums |
 // presence table [B][chunks] u16 | global code mask u32
 struct WgradWs {
-  size_t partial, csum, pres, gmask, list, masks, items, counts, total;
+  size_t partial, csum, pres, gmask, list, masks, items, counts, zero, total;
 };
 static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   WgradWs o;
@@ -1787,6 +1799,8 @@ static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   off += align256(sizeof(int4) * nitems);
   o.counts = off;
   off += 256;
+  o.zero = off;
+  off += LD_ZERO_BYTES;
   o.total = off;
   return o;
 }
@@ -1842,6 +1856,7 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
     a.ntile_o = P.ntile_o;
     a.target = wg_target();
     a.inv_wo = 1.0f / (float)wo;
+    a.zero = (const bf16_t*)((char*)ws + L.zero);
     a.partial = partial;
     k_wg_plan<<<1, 1024, 0, s>>>(a);
     k_wg_masks<<<ceil_div((long long)P.max_entries, 4), 256, 0, s>>>(a);
@@ -1854,10 +1869,11 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
       k_chan_sum_nhwc<<<dim3(B, ceil_div(Cout, 64), chan_sum_splits(hwo)), 256, 0, s>>>((const bf16_t*)gout_nhwc, hwo,
                                                                                        Cout, csum);
     const int csmem = 5 * 9 * Cin * (int)sizeof(float);
+    constexpr int kCombineDyn = 163840 - 1024 * 4;  // the kernel's static item -> code table
     static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
     if (cattr != hipSuccess) return (int)cattr;
-    RGBD_REQUIRE(csmem <= 163840, RGBD_E_SHAPE);
+    RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
     k_dsam_wgrad_combine<<<Cout, 256, csmem, s>>>(partial, a.items, a.counts, Cin, Cout, dconv_w, dproj_w);
   } else {
     return RGBD_E_DTYPE;
