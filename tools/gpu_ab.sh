@@ -3,8 +3,8 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 for i in 1 2; do
-  timeout -k 10 200 python bench.py --cpu-baseline 0 --c5-stream 0 --inference 0 > gpurun_out/ab_new$i.json 2>/dev/null || exit 1
-  RGBD_HIP_LIB="$GRAFT_REPO_ROOT/$1" timeout -k 10 200 python bench.py --cpu-baseline 0 --c5-stream 0 --inference 0 > gpurun_out/ab_old$i.json 2>/dev/null || exit 1
+  timeout -k 10 200 python bench.py --cpu-baseline 0 --c5-stream 0 --inference 0 --parity 0 > gpurun_out/ab_new$i.json 2>/dev/null || exit 1
+  RGBD_HIP_LIB="$GRAFT_REPO_ROOT/$1" timeout -k 10 200 python bench.py --cpu-baseline 0 --c5-stream 0 --inference 0 --parity 0 > gpurun_out/ab_old$i.json 2>/dev/null || exit 1
 done
 python3 - <<'PY'
 import json
