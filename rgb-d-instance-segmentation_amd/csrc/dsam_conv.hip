@@ -242,58 +242,94 @@ __global__ void k_pack_dsam(const float* __restrict__ conv_w, const float* __res
 __host__ __device__ __forceinline__ int lds_swz(int n) { return ((n >> 3) & 1) << 1; }
 __device__ __forceinline__ int pk_pos(int n, int c) { return ((((c >> 3) ^ lds_swz(n)) & 3) << 3) | (c & 7); }
 
-__global__ __launch_bounds__(256) void k_pack_fwd_codes(const float* __restrict__ conv_w, const float* __restrict__ proj_w,
-                                                        int Cin, int Cout, const uint32_t* __restrict__ code_mask,
-                                                        bf16_t* __restrict__ wfwd) {
-  extern __shared__ float srow[];  // [5][Cin*9] OIHW rows of output channel o: conv_0..3, proj
-  const int o = blockIdx.x, KK = 9 * Cin, nch = Cin / 32;
-  const uint32_t m = code_mask ? *code_mask : 0xffffu;
-  if (o == 0)  // tail pad (read only by an over-reaching last N tile, whose outputs are dropped)
-    for (int i = threadIdx.x; i < 192 * 32; i += 256) wfwd[144ll * Cin * Cout + i] = 0;
-  for (int e = threadIdx.x; e < KK; e += 256) {
+// Both packings from one pass over the f32 weights.  Workgroup = a block of PK_OB output x PK_CB
+// input channels: its 5 x PK_OB rows of (32 c x 9 taps) f32 (conv_0..3, proj; 1152 contiguous
+// bytes each in OIHW) are staged in LDS by 16-byte loads, all in flight together.  A unit is 8
+// consecutive channels of one (row, tap): wfwd units (o, tap, 8 c) and wbwd units (c, tap, 8 o);
+// each reads its 5 x 8 segment values once and writes one 16-byte chunk per present code.  Rows
+// are padded to 289 floats so the unit reads of a wave fall on distinct banks.
+constexpr int PK_OB = 16, PK_CB = 32, PK_LD = PK_CB * 9 + 1;
+constexpr size_t PK_SMEM = 5 * PK_OB * PK_LD * sizeof(float);
+__global__ __launch_bounds__(256) void k_pack_codes(const float* __restrict__ conv_w, const float* __restrict__ proj_w,
+                                                    int Cin, int Cout, const uint32_t* __restrict__ code_mask,
+                                                    bf16_t* __restrict__ wfwd, bf16_t* __restrict__ wbwd) {
+  extern __shared__ float sw[];  // [5 seg][PK_OB o][PK_LD]: element (o, c, tap) at c * 9 + tap
+  const int c0 = blockIdx.x * PK_CB, o0 = blockIdx.y * PK_OB, tid = threadIdx.x;
+  const int nci = Cin / 32, nco = Cout / 32;
+  if (blockIdx.x == 0 && blockIdx.y == 0)  // tail pads (read only by an over-reaching last N tile)
+    for (int i = tid; i < 192 * 32; i += 256) {
+      wfwd[144ll * Cin * Cout + i] = 0;
+      if (wbwd) wbwd[144ll * Cin * Cout + i] = 0;
+    }
+  constexpr int NQ = 5 * PK_OB * (PK_CB * 9 / 4);  // float4 pieces of the block
+  constexpr int PER = (NQ + 255) / 256;
+  float4 v[PER];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) srow[i * KK + e] = conv_w[((long long)i * Cout + o) * KK + e];
-    srow[4 * KK + e] = proj_w[(long long)o * KK + e];
-  }
-  __syncthreads();
-  for (int k = 0; k < 16; ++k) {
-    if (!((m >> k) & 1u)) continue;
-    for (int e2 = threadIdx.x; e2 < KK / 2; e2 += 256) {  // element pair (tap, c), (tap, c+1)
-      const int e = 2 * e2, tap = e / Cin, c = e % Cin;
-      float v[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int src = (c + h) * 9 + tap;
-        float s = srow[4 * KK + src];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if ((k >> i) & 1) s += srow[i * KK + src];
-        v[h] = s;
-      }
-      const long long tile = ((long long)(k * 9 + tap) * nch + (c >> 5)) * Cout + o;
-      *reinterpret_cast<uint32_t*>(wfwd + tile * 32 + pk_pos(o, c & 31)) =
-          (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + 256 * j;
+    if (i < NQ) {
+      const int row = i / (PK_CB * 9 / 4), q = i - row * (PK_CB * 9 / 4), seg = row / PK_OB, o = o0 + row % PK_OB;
+      const float* src = seg < 4 ? conv_w + (((long long)seg * Cout + o) * Cin + c0) * 9 : proj_w + ((long long)o * Cin + c0) * 9;
+      v[j] = reinterpret_cast<const float4*>(src)[q];
     }
   }
-}
-
-// wbwd from wfwd: per (code, tap, 32x32 (o, c) block) an LDS transpose
-__global__ __launch_bounds__(256) void k_pack_bwd_codes(const bf16_t* __restrict__ wfwd, int Cin, int Cout,
-                                                        const uint32_t* __restrict__ code_mask,
-                                                        bf16_t* __restrict__ wbwd) {
-  __shared__ bf16_t tile[32][34];
-  const int k = blockIdx.z / 9, tap = blockIdx.z % 9;
-  const uint32_t m = code_mask ? *code_mask : 0xffffu;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)  // tail pad
-    for (int i = threadIdx.x; i < 192 * 32; i += 256) wbwd[144ll * Cin * Cout + i] = 0;
-  if (!((m >> k) & 1u)) return;
-  const int cch = blockIdx.x, och = blockIdx.y, nci = Cin / 32, nco = Cout / 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  const bf16_t* src = wfwd + (((long long)(k * 9 + tap) * nci + cch) * Cout + och * 32) * 32;
-  for (int i = ty; i < 32; i += 8) tile[i][tx] = src[i * 32 + pk_pos(och * 32 + i, tx)];  // [o][c]
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + 256 * j;
+    if (i < NQ) {
+      const int row = i / (PK_CB * 9 / 4), q = i - row * (PK_CB * 9 / 4);
+      float* d = sw + row * PK_LD + 4 * q;
+      d[0] = v[j].x;
+      d[1] = v[j].y;
+      d[2] = v[j].z;
+      d[3] = v[j].w;
+    }
+  }
   __syncthreads();
-  bf16_t* dst = wbwd + (((long long)(k * 9 + tap) * nco + och) * Cin + cch * 32) * 32;
-  for (int i = ty; i < 32; i += 8) dst[i * 32 + pk_pos(cch * 32 + i, tx)] = tile[tx][i];  // [c][o]
+  const uint32_t m = code_mask ? *code_mask : 0xffffu;
+  // units 0..575: wfwd (tap, o, 8-c chunk q); 576..1151: wbwd (tap, c, 8-o chunk q)
+  const int nunits = wbwd ? 2 * 9 * PK_OB * 4 : 9 * PK_OB * 4;
+  for (int u = tid; u < nunits; u += 256) {
+    const bool bwd = u >= 9 * PK_OB * 4;
+    const int w = bwd ? u - 9 * PK_OB * 4 : u;
+    const int tap = w / (PK_OB * 4);
+    int base, step;  // LDS offset of value e: base + e * step (+ seg * PK_OB * PK_LD)
+    long long dst0;  // element offset of the unit's 16-byte chunk for code 0
+    long long kstride;
+    if (!bwd) {
+      const int ol = (w >> 2) & (PK_OB - 1), q = w & 3, n = o0 + ol;
+      base = ol * PK_LD + 8 * q * 9 + tap;
+      step = 9;
+      dst0 = (((long long)tap * nci + blockIdx.x) * Cout + n) * 32 + 8 * ((q ^ lds_swz(n)) & 3);
+      kstride = 9ll * nci * Cout * 32;
+    } else {
+      const int cl = (w >> 1) & (PK_CB - 1), q = w & 1, n = c0 + cl, qo = (o0 & 31) / 8 + q;
+      base = 8 * q * PK_LD + cl * 9 + tap;
+      step = PK_LD;
+      dst0 = (((long long)tap * nco + (o0 >> 5)) * Cin + n) * 32 + 8 * ((qo ^ lds_swz(n)) & 3);
+      kstride = 9ll * nco * Cin * 32;
+    }
+    float s[5][8];
+#pragma unroll
+    for (int sg = 0; sg < 5; ++sg)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[sg][e] = sw[sg * PK_OB * PK_LD + base + e * step];
+    bf16_t* out = bwd ? wbwd : wfwd;
+    for (int k = 0; k < 16; ++k) {
+      if (!((m >> k) & 1u)) continue;
+      float r[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = s[4][e];  // proj, then conv_0..conv_3 of the code's bits, in f32, rounded once
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if ((k >> i) & 1) t += s[i][e];
+        r[e] = t;
+      }
+      *reinterpret_cast<uint4*>(out + dst0 + k * kstride) =
+          make_uint4(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]), pack_bf16x2(r[4], r[5]), pack_bf16x2(r[6], r[7]));
+    }
+  }
 }
 
 // OR of (1 << code) over each code map (codes present per DSAM input resolution).
@@ -1674,16 +1710,12 @@ int rgbd_dsam_pack_weights(int dtype, const float* conv_w, const float* proj_w, 
     k_pack_dsam<float><<<nb, 256, 0, s>>>(conv_w, proj_w, Cin, Cout, (float*)wfwd, (float*)wbwd);
   } else if (dtype == RGBD_BF16) {
     RGBD_REQUIRE(wfwd, RGBD_E_ARG);  // wbwd is the transpose of wfwd
-    RGBD_REQUIRE(Cin % 32 == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
-    const int smem = 5 * 9 * Cin * (int)sizeof(float);
-    RGBD_REQUIRE(smem <= 163840, RGBD_E_SHAPE);
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_pack_fwd_codes,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    RGBD_REQUIRE(Cin % PK_CB == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_pack_codes,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)PK_SMEM);
     if (attr != hipSuccess) return (int)attr;
-    k_pack_fwd_codes<<<Cout, 256, smem, s>>>(conv_w, proj_w, Cin, Cout, code_mask, (bf16_t*)wfwd);
-    if (wbwd)
-      k_pack_bwd_codes<<<dim3(Cin / 32, Cout / 32, 144), 256, 0, s>>>((const bf16_t*)wfwd, Cin, Cout, code_mask,
-                                                                      (bf16_t*)wbwd);
+    k_pack_codes<<<dim3(Cin / PK_CB, Cout / PK_OB), 256, PK_SMEM, s>>>(conv_w, proj_w, Cin, Cout, code_mask,
+                                                                       (bf16_t*)wfwd, (bf16_t*)wbwd);
   } else {
     return RGBD_E_DTYPE;
   }

@@ -73,7 +73,8 @@ class HotPathFunction(torch.autograd.Function):
         training = any(ctx.needs_input_grad[7:])
         masks = ops.dsam_code_masks(codes) if dtype == torch.bfloat16 else None
         packs = [cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
-                                          code_mask=None if masks is None else masks[k:k + 1], want_bwd=training)
+                                          code_mask=None if masks is None else masks[k:k + 1],
+                                          want_bwd=training and k > 0)  # dsam0's input takes no gradient
                  for k in range(3)]
         x_nhwc = [ops.nchw_to_nhwc(colors[0])]
         cp1 = [colors[0]]

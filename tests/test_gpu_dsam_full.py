@@ -208,3 +208,59 @@ def test_dggm_cp1_nhwc_equals_nchw(shape):
     ref = ops.dggm_fuse_fwd_multi([cp1], [color], pv, [wt], [bs])[0]
     got = ops.dggm_fuse_fwd_multi([ops.nchw_to_nhwc(cp1)], [color], pv, [wt], [bs], cp1_nhwc=(0,))[0]
     assert torch.equal(got, ref)
+
+
+def _pack_reference(conv_w, proj_w, codes_present):
+    """numpy restatement of the bf16 code-merged packing (dsam_conv.hip, k_pack_codes):
+    W_k = proj + sum_{i in k} conv_i in f32 (proj first, conv_0..3 ascending), rounded once to bf16,
+    laid out as wfwd [k][tap][Cin/32][Cout][32 c] / wbwd [k][tap][Cout/32][Cin][32 o] with the
+    16-byte chunk g of row n at slot g ^ (((n >> 3) & 1) << 1)."""
+    conv = conv_w.cpu().numpy().astype(np.float32)
+    proj = proj_w.cpu().numpy().astype(np.float32)
+    _, Co, Ci = conv.shape[:3]
+    nci, nco = Ci // 32, Co // 32
+    wf = {}
+    wb = {}
+    n_o = np.arange(Co)
+    n_c = np.arange(Ci)
+
+    def slot(n, j):  # position of element j (0..31) of row n
+        return ((((j >> 3) ^ (((n >> 3) & 1) << 1)) & 3) << 3) | (j & 7)
+    for k in codes_present:
+        t = proj.copy()
+        for i in range(4):
+            if (k >> i) & 1:
+                t = (t + conv[i]).astype(np.float32)
+        bf = torch.from_numpy(t).to(torch.bfloat16).view(torch.int16).numpy().reshape(Co, Ci, 9)
+        f = np.zeros((9, nci, Co, 32), np.int16)
+        b = np.zeros((9, nco, Ci, 32), np.int16)
+        for tap in range(9):
+            for cc in range(nci):
+                blk = bf[:, cc * 32:(cc + 1) * 32, tap]  # [o][32 c]
+                f[tap, cc][n_o[:, None], slot(n_o[:, None], np.arange(32)[None, :])] = blk
+            for oc in range(nco):
+                blk = bf[oc * 32:(oc + 1) * 32, :, tap].T  # [c][32 o]
+                b[tap, oc][n_c[:, None], slot(n_c[:, None], np.arange(32)[None, :])] = blk
+        wf[k], wb[k] = f, b
+    return wf, wb
+
+
+@pytest.mark.parametrize("cin,cout,mask", [(64, 96, 0b1000000000010011), (96, 192, 0xffff), (32, 32, 0b10)])
+def test_pack_codes_layout_bit_exact(cin, cout, mask):
+    """The bf16 code-merged filters (fwd and dX operands) equal, bit for bit, the numpy
+    restatement of the packing for every code present; the one-tile tail pads are zero."""
+    g = torch.Generator(device=DEV)
+    g.manual_seed(cin + cout)
+    conv_w = torch.randn((4, cout, cin, 3, 3), generator=g, device=DEV) * 0.05
+    proj_w = torch.randn((cout, cin, 3, 3), generator=g, device=DEV) * 0.05
+    cm = torch.tensor([mask], dtype=torch.int32, device=DEV)
+    wf, wb = ops.dsam_pack(conv_w, proj_w, torch.bfloat16, code_mask=cm)
+    present = [k for k in range(16) if (mask >> k) & 1]
+    ref_f, ref_b = _pack_reference(conv_w, proj_w, present)
+    slab = 9 * cin * cout
+    wf16 = wf.view(torch.int16).cpu().numpy().reshape(-1)
+    wb16 = wb.view(torch.int16).cpu().numpy().reshape(-1)
+    for k in present:
+        assert np.array_equal(wf16[k * slab:(k + 1) * slab], ref_f[k].reshape(-1)), f"wfwd code {k}"
+        assert np.array_equal(wb16[k * slab:(k + 1) * slab], ref_b[k].reshape(-1)), f"wbwd code {k}"
+    assert not wf16[16 * slab:16 * slab + 192 * 32].any() and not wb16[16 * slab:16 * slab + 192 * 32].any()

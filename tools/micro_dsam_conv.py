@@ -30,7 +30,8 @@ for k, (ci, co) in enumerate([(96, 192), (192, 384), (384, 768)]):
     resid_nhwc = ops.nchw_to_nhwc(resid)
     gy = torch.randn((B, (h + 1) // 2, (w + 1) // 2, co), generator=g, device=dev).bfloat16()
     gin = torch.randn((B, ci, h, w), generator=g, device=dev).bfloat16()
-    fns = {f"fwd{k}": lambda: ops.dsam_fwd(x, codes[k], info, wf, b4, residual=resid, want_nhwc=(k < 2)),
+    fns = {f"pack{k}": lambda: ops.dsam_pack(cw, pw, torch.bfloat16, code_mask=masks[k:k + 1], want_bwd=k > 0),
+           f"fwd{k}": lambda: ops.dsam_fwd(x, codes[k], info, wf, b4, residual=resid, want_nhwc=(k < 2)),
            f"fwdh{k}": lambda: ops.dsam_fwd_nhwc(x, codes[k], info, wf, b4, residual_nhwc=resid_nhwc),
            f"dw{k}": lambda: ops.dsam_bwd_weight(None, x, codes[k], info, gout_nhwc=gy)}
     if k > 0:
