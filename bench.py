@@ -97,6 +97,9 @@ def parse(argv=None):
                     help="also report the C5 RealSense 1280x720 B=1 streaming inference rate (rank 0, N=1)")
     ap.add_argument("--parity", type=int, default=1,
                     help="report the fp32 mask-logit max-abs-err vs the committed 640x480 fixture (rank 0)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="N=1: time the step replayed from a HIP graph (rgbd_amd/train_graph.py); the eager "
+                         "rate and the per-kernel HIP-event timings come from an eager pass beside it")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -185,9 +188,10 @@ def build(args, dev, rank=0):
                 gouts=gouts, scenes=scenes, sizes=sizes)
 
 
-def make_parts(ctx, world):
+def make_parts(ctx, world, capturable=False):
     """(forward_backward, optimizer_step, reducer, broadcaster) of one training step.
-    forward_backward() leaves the (all-reduced, for N > 1) gradients in p.grad."""
+    forward_backward() leaves the (all-reduced, for N > 1) gradients in p.grad;
+    optimizer_step.opt is the AdamW instance (``capturable`` for graph capture)."""
     from rgbd_amd import ops
     from rgbd_amd.distributed import BufferBroadcaster, OverlappedGradReducer, hot_path_grad_groups
     from rgbd_amd.hot_path import hot_path
@@ -196,7 +200,7 @@ def make_parts(ctx, world):
     reducer = OverlappedGradReducer(hot_path_grad_groups(ctx["dsams"], ctx["dg"])) if world > 1 else None
     bcast = BufferBroadcaster([ctx["rp"]]) if world > 1 else None
     hook = None if reducer is None else reducer.ready
-    opt = torch.optim.AdamW(params, lr=1e-5, fused=True)
+    opt = torch.optim.AdamW(params, lr=1e-5, fused=True, capturable=capturable)
 
     def forward_backward():
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
@@ -212,11 +216,12 @@ def make_parts(ctx, world):
     def optimizer_step():
         opt.step()
         opt.zero_grad(set_to_none=True)
+    optimizer_step.opt = opt
 
     return forward_backward, optimizer_step, reducer, bcast
 
 
-def make_step(ctx, world, inference=False):
+def make_step(ctx, world, inference=False, graph=False):
     from rgbd_amd import ops
     from rgbd_amd.hot_path import hot_path
     if inference:
@@ -226,6 +231,16 @@ def make_step(ctx, world, inference=False):
                 ratio = ctx["rp"](pv[:, 3:6])
                 return hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"])
         return istep
+    if graph:  # single process: the whole step replayed from a HIP graph, captured on first use
+        from rgbd_amd.train_graph import CapturedTrainStep
+        fb, ostep, _, _ = make_parts(ctx, world, capturable=True)
+        held = {}
+
+        def gstep():
+            if "g" not in held:
+                held["g"] = CapturedTrainStep(fb, ostep.opt)
+            return held["g"]()
+        return gstep
     fb, ostep, _, _ = make_parts(ctx, world)
 
     def step():
@@ -413,15 +428,20 @@ def parity_fp32(dev):
             "fixture": "tests/golden/g7_model640.npz", "sampled_logits": int(g7["mask_idx"].size)}
 
 
-def kernel_fractions(L, ctx, B, H, W, step_ms, world):
-    """K5 achieved rates (reference-algorithmic and executed FLOPs) and the whole step's
-    t_ideal / t_measured (SURVEY §8(d)) from the HIP-event timings of the timed steps."""
+def read_timings(L):
+    """{scope: (total ms, launches)} of the HIP-event timers since rgbd_timing_enable(1)."""
     cnt = ctypes.c_int(0)
     ms = {}
     for name in ("rp_conv3x3", "rp_chain", "dsam_fwd", "dsam_dx", "dsam_wgrad", "decompose", "dggm_fwd",
                  "dggm_bwd", "assemble"):
         tot = L.rgbd_timing_read(name.encode(), ctypes.byref(cnt))
         ms[name] = (tot, cnt.value)
+    return ms
+
+
+def kernel_fractions(ms, ctx, B, H, W, step_ms, world):
+    """K5 achieved rates (reference-algorithmic and executed FLOPs) and the whole step's
+    t_ideal / t_measured (SURVEY §8(d)) from the HIP-event timings of the timed steps."""
     P = B * H * W
     ho = [(-(-H // 4) + 1) // 2, (-(-H // 8) + 1) // 2, (-(-H // 16) + 1) // 2]
     wo = [(-(-W // 4) + 1) // 2, (-(-W // 8) + 1) // 2, (-(-W // 16) + 1) // 2]
@@ -476,13 +496,16 @@ def main():
     if world > 1:  # DDP construction: rank 0's parameters and buffers everywhere
         broadcast_parameters([ctx["rp"], ctx["dg"]] + ctx["dsams"])
     step = make_step(ctx, world)
-    # timed region; per-kernel HIP-event timing over the timed steps only
-    dt = timed(step, args.steps, args.warmup, world, on_start=lambda: L.rgbd_timing_enable(1))
+    # eager pass: per-kernel HIP-event timing over its timed steps only
+    dt_eager = timed(step, args.steps, args.warmup, world, on_start=lambda: L.rgbd_timing_enable(1))
+    timings = read_timings(L)
+    L.rgbd_timing_enable(0)
+    use_graph = bool(args.graph) and world == 1
+    dt = timed(make_step(ctx, world, graph=True), args.steps, args.warmup, world) if use_graph else dt_eager
     B = args.batch
     step_ms = dt / args.steps * 1e3
-    raw, per, fracs = kernel_fractions(L, ctx, B, args.height, args.width, step_ms, world)
+    raw, per, fracs = kernel_fractions(timings, ctx, B, args.height, args.width, step_ms, world)
     conv_ms, conv_launches = raw["rp_conv3x3"]
-    L.rgbd_timing_enable(0)
     value = B * world * args.steps / dt
     inf = None
     if args.inference:
@@ -516,6 +539,8 @@ def main():
                         "backend": (dist.get_backend() if world > 1 else None),
                         "collectives_per_step": ("3 async all-reduce (grad buckets dsam2, dsam1, dsam0+DGGM) + "
                                                  "2 broadcasts (ratio-predictor BN buffers)") if world > 1 else None},
+        "graph": use_graph,
+        "eager_img_s": round(B * world * args.steps / dt_eager, 2),
         "inference_img_s": inf,
         "kernel_ms": per,
         "roofline": {"bound": "mfma", "kernel": "k_rp_conv3x3 (3x3 128->256, custom_model.py:1413)",

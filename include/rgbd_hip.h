@@ -215,7 +215,9 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
  *     scale1_conv.1, scale2_conv.1, scale3_conv.1, feature_fusion.1, feature_extractor.1,
  *     feature_extractor.5.  training=1 uses batch statistics and updates the running stats
  *     in place (torch semantics, `momentum`), and applies dropout with a counter hash of
- *     `seed`; training=0 uses the running stats.  B <= 32. */
+ *     `seed` + *seed_counter; the forward then increments *seed_counter on the device (a
+ *     u64 the caller owns; NULL = `seed` alone), so a captured graph's replays draw fresh
+ *     masks.  training=0 uses the running stats.  B <= 32. */
 #define RGBD_RATIO_NW 24
 #define RGBD_RATIO_NBN 6
 size_t rgbd_ratio_packed_size(int dtype);
@@ -223,7 +225,7 @@ int rgbd_ratio_pack(int dtype, const float* const* weights_host, void* packed, v
 size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W);
 int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
-                       float* ratio, void* ws, void* stream);
+                       unsigned long long* seed_counter, float* ratio, void* ws, void* stream);
 
 /* ---------------------------------------------------------------- f2 deformable attention
  * Replaces multi_scale_deformable_attention (transformers 5.15 modeling_mask2former.py:798-837),

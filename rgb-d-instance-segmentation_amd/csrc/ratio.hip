@@ -1554,8 +1554,10 @@ __device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned 
 // images, fixed-order block reduction per image.
 __global__ __launch_bounds__(256) void k_rp_tail_fc1(const float* __restrict__ feat, int B, int training,
                                                      const char* __restrict__ blob, Layout L,
-                                                     unsigned long long seed, float* __restrict__ h1) {
+                                                     unsigned long long seed, const unsigned long long* seed_ctr,
+                                                     float* __restrict__ h1) {
   __shared__ float red[4][32];
+  if (seed_ctr) seed += *seed_ctr;
   const int o = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const float* w7 = (const float*)(blob + L.w7);
   const float wa = w7[o * 512 + t], wb = w7[o * 512 + t + 256];
@@ -1579,8 +1581,11 @@ __global__ __launch_bounds__(256) void k_rp_tail_fc1(const float* __restrict__ f
 // map; one workgroup, weights transposed into LDS (lanes walk output columns: conflict-free).
 __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ h1g, int B, int training,
                                                       const char* __restrict__ blob, Layout L,
-                                                      unsigned long long seed, float* __restrict__ ratio) {
+                                                      unsigned long long seed, unsigned long long* seed_ctr,
+                                                      float* __restrict__ ratio) {
   __shared__ float w8t[128][64], w9t[64][32];
+  const unsigned long long ctr = seed_ctr ? *seed_ctr : 0ull;
+  seed += ctr;
   __shared__ float h1[32][128], h2[32][64], h3[32][32];
   const float* w8 = (const float*)(blob + L.w8);
   const float* b8 = (const float*)(blob + L.b8);
@@ -1608,6 +1613,9 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
     h3[bb][o] = fmaxf(s, 0.f);
   }
   __syncthreads();
+  // every read of the counter (k_rp_tail_fc1, this kernel's prologue) precedes this store: the
+  // next forward (or graph replay) draws fresh dropout masks
+  if (training && seed_ctr && threadIdx.x == 0) *seed_ctr = ctr + 1ull;
   if (threadIdx.x < B) {
     const int bb = threadIdx.x;
     float s = b10[0];
@@ -1678,8 +1686,8 @@ inline Ws make_ws(int es, int B, int H, int W) {
 
 template <typename T>
 int ratio_forward(int training, float momentum, const float* depth3, long long bstride, int B, int H, int W,
-                  const char* blob, const BnPtrs& bn, unsigned long long seed, float* ratio, char* ws,
-                  hipStream_t s) {
+                  const char* blob, const BnPtrs& bn, unsigned long long seed, unsigned long long* seed_ctr,
+                  float* ratio, char* ws, hipStream_t s) {
   const Layout L = make_layout(sizeof(T));
   const Ws w = make_ws(sizeof(T), B, H, W);
   float2* aff1 = (float2*)(ws + w.aff1);
@@ -1767,8 +1775,8 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
   k_rp_tail_conv<<<dim3(C6 / TC_O, TC_CHUNKS), 256, 0, s>>>(pooled, B, blob, L, zpart);
   k_rp_tail_bn<<<C6 / 4, 256, 0, s>>>(zpart, B, training, momentum, blob, L, bn, feat);
-  k_rp_tail_fc1<<<128, 256, 0, s>>>(feat, B, training, blob, L, seed, h1);
-  k_rp_tail_head<<<1, 512, 0, s>>>(h1, B, training, blob, L, seed, ratio);
+  k_rp_tail_fc1<<<128, 256, 0, s>>>(feat, B, training, blob, L, seed, seed_ctr, h1);
+  k_rp_tail_head<<<1, 512, 0, s>>>(h1, B, training, blob, L, seed, seed_ctr, ratio);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -1803,7 +1811,7 @@ size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W) {
 
 int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
-                       float* ratio, void* ws, void* stream) {
+                       unsigned long long* seed_counter, float* ratio, void* ws, void* stream) {
   RGBD_REQUIRE(depth3 && packed && bn_host && ratio && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
   RGBD_REQUIRE(B <= 32, RGBD_E_SHAPE);  // k_rp_tail_fc1 / k_rp_tail_head hold the batch in LDS
@@ -1815,10 +1823,10 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32)
     return ratio_forward<float>(training, momentum, depth3, batch_stride, B, H, W, (const char*)packed, bn, seed,
-                                ratio, (char*)ws, s);
+                                seed_counter, ratio, (char*)ws, s);
   if (dtype == RGBD_BF16)
     return ratio_forward<bf16_t>(training, momentum, depth3, batch_stride, B, H, W, (const char*)packed, bn, seed,
-                                 ratio, (char*)ws, s);
+                                 seed_counter, ratio, (char*)ws, s);
   return RGBD_E_DTYPE;
 }
 

@@ -79,10 +79,14 @@ def ratio_predictor_forward(module, depth_image: torch.Tensor) -> torch.Tensor:
     L = _lib.lib()
     code = _dtype_code(torch.empty(0, dtype=dtype))
     ws = _workspace(d.device, L.rgbd_ratio_workspace_size(code, B, H, W), "ratio")
-    seed = (torch.initial_seed() * 1000003 + next(_seed_counter)) & 0xFFFFFFFFFFFF
+    # dropout stream: a per-module base seed and a device counter the forward advances itself
+    ctr = getattr(module, "_rgbd_dropout_ctr", None)
+    if ctr is None or ctr.device != d.device:
+        ctr = module._rgbd_dropout_ctr = torch.zeros((1,), dtype=torch.int64, device=d.device)
+        module._rgbd_dropout_seed = (torch.initial_seed() * 1000003 + next(_seed_counter) * 0x10000) & 0xFFFFFFFFFFFF
     check(L.rgbd_ratio_forward(code, int(training), ctypes.c_float(momentum), ctypes.c_void_p(d.data_ptr()),
-                               d.stride(0), B, H, W, _p(blob), bn_arr, ctypes.c_ulonglong(seed), _p(ratio), _p(ws),
-                               _stream(d.device)), "rgbd_ratio_forward")
+                               d.stride(0), B, H, W, _p(blob), bn_arr, ctypes.c_ulonglong(module._rgbd_dropout_seed),
+                               _p(ctr), _p(ratio), _p(ws), _stream(d.device)), "rgbd_ratio_forward")
     if training:  # one multi-tensor launch for the six BatchNorm counters
         with torch.no_grad():
             torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)

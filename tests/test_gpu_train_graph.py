@@ -1,0 +1,63 @@
+"""The hot-path training step replayed from a HIP graph (rgbd_amd/train_graph.py, bench.py's
+N=1 timed step) computes exactly what the eager step computes: after the same number of steps
+from the same weights, every trained parameter and every ratio-predictor BatchNorm buffer is
+bitwise equal, and the dropout counter has advanced once per step in both."""
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+import _rgbd_import  # noqa: E402,F401
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _ctx(bench, args):
+    ctx = bench.build(args, DEV)
+    rp = ctx["rp"]
+    rp._rgbd_dropout_ctr = torch.zeros((1,), dtype=torch.int64, device=DEV)
+    rp._rgbd_dropout_seed = 0x5EED1234  # the same dropout stream in both arms
+    return ctx
+
+
+def _state(ctx):
+    out = [p.detach().clone() for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
+    out += [b.detach().clone() for b in ctx["rp"].buffers()]
+    return out
+
+
+def test_captured_step_equals_eager_steps():
+    import bench
+    from rgbd_amd.train_graph import CapturedTrainStep
+    args = bench.parse(["--height", "96", "--width", "128", "--batch", "3"])
+    a, b = _ctx(bench, args), _ctx(bench, args)
+    fa, oa, _, _ = bench.make_parts(a, 1, capturable=True)
+    for _ in range(4):
+        fa()
+        oa()
+    fb, ob, _, _ = bench.make_parts(b, 1, capturable=True)
+    step = CapturedTrainStep(fb, ob.opt, warmup=2)  # 2 eager steps, then capture
+    for _ in range(2):
+        outs = step()
+    torch.cuda.synchronize()
+    assert int(a["rp"]._rgbd_dropout_ctr.item()) == 4 == int(b["rp"]._rgbd_dropout_ctr.item())
+    sa, sb = _state(a), _state(b)
+    assert len(sa) == len(sb)
+    for i, (x, y) in enumerate(zip(sa, sb)):
+        assert torch.equal(x, y), f"state tensor {i} differs after 4 steps"
+    assert len(outs) == 4 and all(torch.isfinite(o.float()).all() for o in outs)
+
+
+def test_captured_step_needs_capturable_optimizer():
+    import bench
+    from rgbd_amd.train_graph import CapturedTrainStep
+    args = bench.parse(["--height", "64", "--width", "96", "--batch", "2"])
+    ctx = _ctx(bench, args)
+    fb, ob, _, _ = bench.make_parts(ctx, 1)
+    with pytest.raises(ValueError, match="capturable"):
+        CapturedTrainStep(fb, ob.opt)
