@@ -23,6 +23,19 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
 typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+// Buffer descriptor over [base, base + bytes) built from wave-uniform values (readfirstlane of the
+// pointer halves, so no waterfall loop around each access), for write-through hand-offs: 16-byte
+// buffer stores / loads with aux WT_SC1 carry sc1 (they bypass this CU's L1 and write through the
+// XCD's L2), the form MI355X_MICROARCH.md's visibility table (row 1) admits without fences.
+constexpr int WT_SC1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base, int bytes) {
+  const uintptr_t p = (uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
 
 typedef uint16_t bf16_t;  // raw bfloat16 storage (same bits as torch.bfloat16)
 

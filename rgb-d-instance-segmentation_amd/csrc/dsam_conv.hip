@@ -240,7 +240,6 @@ __global__ void k_pack_dsam(const float* __restrict__ conv_w, const float* __res
 // 4-bank slots: conflict-free.  (The earlier (n >> 2) & 3 was conflict-free only for 16
 // consecutive lanes, not for the hardware groups.)
 __host__ __device__ __forceinline__ int lds_swz(int n) { return ((n >> 3) & 1) << 1; }
-__device__ __forceinline__ int pk_pos(int n, int c) { return ((((c >> 3) ^ lds_swz(n)) & 3) << 3) | (c & 7); }
 
 // Both packings from one pass over the f32 weights.  Workgroup = a block of PK_OB output x PK_CB
 // input channels: its 5 x PK_OB rows of (32 c x 9 taps) f32 (conv_0..3, proj; 1152 contiguous
@@ -1305,43 +1304,48 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   if (nc > 1) {
     // Multi-chunk tile: publish this chunk's fragment-native partial ([wave][mi][nj][lane][4] f32),
     // take a ticket; the chunk that draws nc-1 sums all partials in chunk order (deterministic)
-    // and runs the epilogue.  Agent-scope release / acquire per cdna_hip_programming.md
-    // (in-launch split-K reduction, Guideline 16): correct for any placement of the chunks.
+    // and runs the epilogue.  The hand-off is write-through: every partial byte is stored and
+    // loaded sc1 (16 B per lane, through one wave-uniform buffer descriptor), every storing wave
+    // drains, one lane per workgroup adds to the tile's ticket after the barrier, and only the
+    // workgroup whose add returned nc-1 loads (MI355X_MICROARCH.md, visibility table row 1;
+    // cdna_hip_programming.md Guideline 16).  No agent-scope release (an XCD-wide L2 write-back)
+    // or acquire is needed, and the result is correct for any placement of the chunks.
     const long long tslab = (((long long)cls * a.ntiles0 + tile) * ntn + ntile) * LD_CH;
-    float* slab = a.partial + (tslab + chunk) * (LD_BN * LD_BM);
+    const __amdgpu_buffer_rsrc_t prs = wt_rsrc(a.partial + tslab * (LD_BN * LD_BM), LD_CH * LD_BN * LD_BM * 4);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj)
-        *reinterpret_cast<f32x4*>(slab + (((wave * 4 + mi) * 3 + nj) * 64 + lane) * 4) = acc[mi][nj];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][nj]), prs,
+                                               (chunk * (LD_BN * LD_BM) + (((wave * 4 + mi) * 3 + nj) * 64 + lane) * 4) * 4,
+                                               0, WT_SC1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* last_s = (int*)(smem + Cfg::TMASK);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int old = __hip_atomic_fetch_add(a.tickets + tslab / LD_CH, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *last_s = old == nc - 1;
     }
     __syncthreads();
     if (!*last_s) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    const float* base = a.partial + tslab * (LD_BN * LD_BM);
+    // every partial of the tile in flight at once, then summed in chunk order
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nc; ++c)
+    for (int c = 0; c < nc; ++c) {
+      u32x4 pv[4][3];
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 3; ++nj)
-          acc[mi][nj] += *reinterpret_cast<const f32x4*>(base + (long long)c * (LD_BN * LD_BM) +
-                                                         (((wave * 4 + mi) * 3 + nj) * 64 + lane) * 4);
+          pv[mi][nj] = __builtin_amdgcn_raw_buffer_load_b128(
+              prs, (c * (LD_BN * LD_BM) + (((wave * 4 + mi) * 3 + nj) * 64 + lane) * 4) * 4, 0, WT_SC1);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 3; ++nj) acc[mi][nj] += __builtin_bit_cast(f32x4, pv[mi][nj]);
+    }
   }
   // ---- epilogue (same contract as k_conv_igemm), staged through LDS in two 96-column halves:
   // pass 1 runs along pixels (NCHW residual loads and stores), pass 2 along channels (NHWC);

@@ -1,5 +1,6 @@
 """Micro benchmark of the bf16 DSAM conv entry points at the bench's shapes (B=8, 640x480):
-forward of dsam0/1/2 and dX of dsam1/2, each timed with CUDA events over --iters calls."""
+packing, forward of dsam0/1/2, dW, and dX of dsam1/2, each timed with CUDA events over a graph of
+--iters calls."""
 import argparse, os, sys
 _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [_R]
@@ -40,14 +41,24 @@ for k, (ci, co) in enumerate([(96, 192), (192, 384), (384, 768)]):
         fns[f"dxh{k}"] = lambda: ops.dsam_bwd_data(gy, codes[k], wb, None, want_nhwc=True, want_nchw=False, cin=ci,
                                                    gin_nhwc=gin_nhwc)
     for name, fn in fns.items():
-        for _ in range(3):
-            fn()
+        # captured into a graph (iters calls) so host launch cost does not set the rate
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                fn()
+        torch.cuda.current_stream().wait_stream(s)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            for _ in range(a.iters):
+                fn()
+        gr.replay()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record()
-        for _ in range(a.iters):
-            fn()
+        gr.replay()
         e1.record()
         torch.cuda.synchronize()
         res.append(f"{name} {e0.elapsed_time(e1) / a.iters * 1e3:.1f}us")
+        del gr
 print(f"DBG={os.environ.get('RGBD_DSAM_DBG', '0')}: " + "  ".join(res))
