@@ -534,6 +534,7 @@ struct WgArgs {
   float inv_wo;
   const bf16_t* zero;     // LD_ZERO_BYTES of zeros (rows the im2col gather masks out)
   float* partial;         // [item][Cout][9*Cin] f32
+  int dbg;                // RGBD_WG_DBG (timing experiments only): 1 = no steps, 2 = no partial stores
 };
 
 __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict__ code, int B, int h, int w,
@@ -721,7 +722,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
   };
   for (int wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
     const int4 item = a.items[wi / ntile];
-    const int tile = wi % ntile, e0 = item.y, nst = item.z - item.y;
+    const int tile = wi % ntile, e0 = item.y, nst = (a.dbg & 1) ? 0 : item.z - item.y;
     const int kk0 = (tile % a.ntile_kk) * 128, o0 = (tile / a.ntile_kk) * 32 * FM;
     // stage the item's unit ids and tap masks
     for (int i = tid; i < nst; i += 256) sunits[i] = a.list[e0 + i] & 0xffffff;
@@ -802,6 +803,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
       else vm_wait_barrier<0>();
     }
     float* dst = a.partial + ((long long)(wi / ntile) * a.Cout) * KK;
+    if (!(a.dbg & 2))
 #pragma unroll
     for (int mi = 0; mi < FM; ++mi)
 #pragma unroll
@@ -1626,9 +1628,10 @@ static WgPlan wg_plan(int B, int Cin, int h, int w, int Cout) {
   p.max_entries = 16 * B * p.nunit;
   return p;
 }
-// items are at most max_entries; the plan targets ~512 work units
+// items are at most max_entries; the plan targets ~256 work units (one per CU: every unit writes an
+// f32 partial tile the combine re-reads, so more units cost more than the balance they buy)
 static int wg_target() {
-  static const int t = getenv("RGBD_WG_TARGET") ? atoi(getenv("RGBD_WG_TARGET")) : 512;
+  static const int t = getenv("RGBD_WG_TARGET") ? atoi(getenv("RGBD_WG_TARGET")) : 256;
   return t;
 }
 // partial buffer bound: items <= entries / L + 16 with L >= entries / (target / tiles)
@@ -1894,6 +1897,8 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
     a.inv_wo = 1.0f / (float)wo;
     a.zero = (const bf16_t*)((char*)ws + L.zero);
     a.partial = partial;
+    static const int wdbg = env_int("RGBD_WG_DBG", 0);
+    a.dbg = wdbg;
     k_wg_plan<<<1, 1024, 0, s>>>(a);
     k_wg_masks<<<ceil_div((long long)P.max_entries, 4), 256, 0, s>>>(a);
     const int grid = 256;  // persistent: one LDS-bound workgroup per CU
