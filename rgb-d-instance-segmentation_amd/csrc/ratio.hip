@@ -1292,6 +1292,28 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
     }
     // ---- epilogue: bias, bf16, fragment-native y store, statistics of the stored values
     bf16_t* yt = y + (((tile * 8 + wave) * 4) * 8) * 256;  // [mi][nj][lane][4]
+    if (t.y0 + C3_TH <= H && t.x0 + C3_TW <= W) {
+      // interior tile (every tile at 640x480): no bounds selects; two packed conversions per
+      // 4 values, the statistics from the rounded values' bits (same values, same order)
+#pragma unroll
+      for (int nj = 0; nj < 8; ++nj) {
+        const float bias = sbias[wn * 128 + 16 * nj + r];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const f32x4 v = acc[mi][nj];
+          const uint32_t p0 = pack_bf16x2(v[0] + bias, v[1] + bias), p1 = pack_bf16x2(v[2] + bias, v[3] + bias);
+          *reinterpret_cast<uint2*>(yt + ((mi * 8 + nj) * 64 + lane) * 4) = make_uint2(p0, p1);
+          const float q[4] = {__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u), __uint_as_float(p1 << 16),
+                              __uint_as_float(p1 & 0xffff0000u)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ssum[nj] += q[j];
+            ssq[nj] += q[j] * q[j];
+          }
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const bool row_ok = t.y0 + 2 * wm + (mi >> 1) < H;
