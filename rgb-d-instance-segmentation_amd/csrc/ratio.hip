@@ -1148,8 +1148,8 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y
 // runs its 64 MFMAs, waits for its own DMA except the A piece just issued, barrier.
 // Epilogue straight from the accumulators: y is written in a fragment-native layout
 // [tile][wave][mi][nj][lane][4 px] (512 contiguous bytes per store instruction; read back by
-// k_rp_bn_relu_pool_frag) and the BN statistics of the stored bf16 values accumulate in
-// registers across tiles.
+// k_rp_bn_relu_pool_frag) and the BN statistics of the float32 conv outputs (as the fp32
+// reference takes them) accumulate in registers across tiles.
 constexpr int C3_TH = 8, C3_TW = 32;
 constexpr int C3_PW = C3_TW + 2, C3_NPIX = (C3_TH + 2) * C3_PW;  // 340 halo pixels
 constexpr int C3_APIX = 344, C3_APIECES = C3_APIX / 8;            // whole 1 KiB DMA pieces
@@ -1293,24 +1293,24 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
     // ---- epilogue: bias, bf16, fragment-native y store, statistics of the stored values
     bf16_t* yt = y + (((tile * 8 + wave) * 4) * 8) * 256;  // [mi][nj][lane][4]
     if (t.y0 + C3_TH <= H && t.x0 + C3_TW <= W) {
-      // interior tile (every tile at 640x480): no bounds selects; two packed conversions per
-      // 4 values, the statistics from the rounded values' bits (same values, same order)
+      // interior tile (every tile at 640x480): no bounds selects; per 4 values one packed bias
+      // add pair, two packed conversions, and the (sum, sum of squares) of the float32 conv
+      // outputs as one packed FMA each
 #pragma unroll
       for (int nj = 0; nj < 8; ++nj) {
         const float bias = sbias[wn * 128 + 16 * nj + r];
+        f32x2 st = {ssum[nj], ssq[nj]};
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
           const f32x4 v = acc[mi][nj];
-          const uint32_t p0 = pack_bf16x2(v[0] + bias, v[1] + bias), p1 = pack_bf16x2(v[2] + bias, v[3] + bias);
-          *reinterpret_cast<uint2*>(yt + ((mi * 8 + nj) * 64 + lane) * 4) = make_uint2(p0, p1);
-          const float q[4] = {__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u), __uint_as_float(p1 << 16),
-                              __uint_as_float(p1 & 0xffff0000u)};
+          const float a[4] = {v[0] + bias, v[1] + bias, v[2] + bias, v[3] + bias};
+          *reinterpret_cast<uint2*>(yt + ((mi * 8 + nj) * 64 + lane) * 4) =
+              make_uint2(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            ssum[nj] += q[j];
-            ssq[nj] += q[j] * q[j];
-          }
+          for (int j = 0; j < 4; ++j) st = __builtin_elementwise_fma(f32x2{a[j], a[j]}, f32x2{1.f, a[j]}, st);
         }
+        ssum[nj] = st.x;
+        ssq[nj] = st.y;
       }
       continue;
     }
@@ -1324,12 +1324,11 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
         uint32_t hv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const bf16_t tv = f32_to_bf16(acc[mi][nj][j] + bias);
-          hv[j] = (uint32_t)tv;
+          const float av = acc[mi][nj][j] + bias;
+          hv[j] = (uint32_t)f32_to_bf16(av);
           if (row_ok && xb + j < W) {
-            const float vr = bf16_to_f32(tv);
-            ssum[nj] += vr;
-            ssq[nj] += vr * vr;
+            ssum[nj] += av;
+            ssq[nj] = __builtin_fmaf(av, av, ssq[nj]);
           }
         }
         *reinterpret_cast<uint2*>(yt + ((mi * 8 + nj) * 64 + lane) * 4) =
