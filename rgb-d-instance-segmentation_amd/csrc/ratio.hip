@@ -1147,7 +1147,7 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y
 // one piece of A (this tile's half 1 during steps 0-5, the next tile's half 0 during 9-14),
 // runs its 64 MFMAs, waits for its own DMA except the A piece just issued, barrier.
 // Epilogue straight from the accumulators: y is written in a fragment-native layout
-// [tile][wave][mi][nj][lane][4 px] (512 contiguous bytes per store instruction; read back by
+// [tile][wave][mi][nj/2][lane][2 ch x 4 px] (1 KiB contiguous per store instruction; read back by
 // k_rp_bn_relu_pool_frag) and the BN statistics of the float32 conv outputs (as the fp32
 // reference takes them) accumulate in registers across tiles.
 constexpr int C3_TH = 8, C3_TW = 32;
@@ -1290,49 +1290,58 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    // ---- epilogue: bias, bf16, fragment-native y store, statistics of the stored values
-    bf16_t* yt = y + (((tile * 8 + wave) * 4) * 8) * 256;  // [mi][nj][lane][4]
-    if (t.y0 + C3_TH <= H && t.x0 + C3_TW <= W) {
-      // interior tile (every tile at 640x480): no bounds selects; per 4 values one packed bias
-      // add pair, two packed conversions, and the (sum, sum of squares) of the float32 conv
-      // outputs as one packed FMA each
+    // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
+    // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
+    bf16_t* yt = y + (((tile * 8 + wave) * 4) * 4) * 512;  // [mi][nj/2][lane][8]
+    const bool interior = t.y0 + C3_TH <= H && t.x0 + C3_TW <= W;
 #pragma unroll
-      for (int nj = 0; nj < 8; ++nj) {
-        const float bias = sbias[wn * 128 + 16 * nj + r];
-        f32x2 st = {ssum[nj], ssq[nj]};
+    for (int np = 0; np < 4; ++np) {
+      const float b0 = sbias[wn * 128 + 32 * np + r], b1 = sbias[wn * 128 + 32 * np + 16 + r];
+      if (interior) {
+        // every tile at 640x480: no bounds selects; per 4 values one packed bias add pair, two
+        // packed conversions, and (sum, sum of squares) as one packed FMA each
+        f32x2 s0 = {ssum[2 * np], ssq[2 * np]}, s1 = {ssum[2 * np + 1], ssq[2 * np + 1]};
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
-          const f32x4 v = acc[mi][nj];
-          const float a[4] = {v[0] + bias, v[1] + bias, v[2] + bias, v[3] + bias};
-          *reinterpret_cast<uint2*>(yt + ((mi * 8 + nj) * 64 + lane) * 4) =
-              make_uint2(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]));
+          const f32x4 v = acc[mi][2 * np], w = acc[mi][2 * np + 1];
+          const float a[4] = {v[0] + b0, v[1] + b0, v[2] + b0, v[3] + b0};
+          const float c[4] = {w[0] + b1, w[1] + b1, w[2] + b1, w[3] + b1};
+          *reinterpret_cast<uint4*>(yt + ((mi * 4 + np) * 64 + lane) * 8) =
+              make_uint4(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(c[0], c[1]),
+                         pack_bf16x2(c[2], c[3]));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) st = __builtin_elementwise_fma(f32x2{a[j], a[j]}, f32x2{1.f, a[j]}, st);
-        }
-        ssum[nj] = st.x;
-        ssq[nj] = st.y;
-      }
-      continue;
-    }
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const bool row_ok = t.y0 + 2 * wm + (mi >> 1) < H;
-      const int xb = t.x0 + (mi & 1) * 16 + 4 * g;
-#pragma unroll
-      for (int nj = 0; nj < 8; ++nj) {
-        const float bias = sbias[wn * 128 + 16 * nj + r];
-        uint32_t hv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float av = acc[mi][nj][j] + bias;
-          hv[j] = (uint32_t)f32_to_bf16(av);
-          if (row_ok && xb + j < W) {
-            ssum[nj] += av;
-            ssq[nj] = __builtin_fmaf(av, av, ssq[nj]);
+          for (int j = 0; j < 4; ++j) {
+            s0 = __builtin_elementwise_fma(f32x2{a[j], a[j]}, f32x2{1.f, a[j]}, s0);
+            s1 = __builtin_elementwise_fma(f32x2{c[j], c[j]}, f32x2{1.f, c[j]}, s1);
           }
         }
-        *reinterpret_cast<uint2*>(yt + ((mi * 8 + nj) * 64 + lane) * 4) =
-            make_uint2(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16));
+        ssum[2 * np] = s0.x;
+        ssq[2 * np] = s0.y;
+        ssum[2 * np + 1] = s1.x;
+        ssq[2 * np + 1] = s1.y;
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const bool row_ok = t.y0 + 2 * wm + (mi >> 1) < H;
+          const int xb = t.x0 + (mi & 1) * 16 + 4 * g;
+          uint32_t hv[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int nj = 2 * np + h;
+            const float bias = h ? b1 : b0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float av = acc[mi][nj][j] + bias;
+              hv[4 * h + j] = (uint32_t)f32_to_bf16(av);
+              if (row_ok && xb + j < W) {
+                ssum[nj] += av;
+                ssq[nj] = __builtin_fmaf(av, av, ssq[nj]);
+              }
+            }
+          }
+          *reinterpret_cast<uint4*>(yt + ((mi * 4 + np) * 64 + lane) * 8) =
+              make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16));
+        }
       }
     }
   }
@@ -1359,8 +1368,9 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 }
 
 // BN + ReLU + AdaptiveAvgPool(4) partial sums over the fragment-native y of k_rp_conv3x3_v3.
-// grid: (16 regions * POOL_SPLIT, B); 256 threads = 128 channel pairs x 2 quad lanes; a quad is
-// 4 x-consecutive pixels (never straddles a 32-px tile); one 16-byte load = 2 channels x 4 px.
+// grid: (16 regions * POOL_SPLIT, B); 256 threads = 128 channel pairs (c, c + 16) x 2 quad lanes;
+// a quad is 4 x-consecutive pixels (never straddles a 32-px tile); one 16-byte load (one lane of
+// the conv's store) = 2 channels x 4 px.
 __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __restrict__ y, int H, int W,
                                                               const float2* __restrict__ aff,
                                                               float* __restrict__ part) {
@@ -1368,13 +1378,13 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __re
   const int b = blockIdx.y, reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
   const int i = reg / 4, j = reg % 4;
   const int cp = threadIdx.x & 127, ql = threadIdx.x >> 7;
-  const int n0 = 2 * cp, wn = n0 >> 7, nj = (n0 & 127) >> 4, r = n0 & 15;
+  const int wn = cp >> 6, np = (cp >> 4) & 3, r = cp & 15, n0 = wn * 128 + 32 * np + r, n1 = n0 + 16;
   const int ya = (i * H) / 4, yb = ((i + 1) * H + 3) / 4, xa = (j * W) / 4, xb = ((j + 1) * W + 3) / 4;
   const int rows = yb - ya;
   const int r0 = ya + (rows * sp) / POOL_SPLIT, r1 = ya + (rows * (sp + 1)) / POOL_SPLIT;
   const int qa = xa >> 2, nq = ((xb + 3) >> 2) - qa;
   const int tiles_x = (W + C3_TW - 1) / C3_TW, tiles_y = (H + C3_TH - 1) / C3_TH;
-  const float2 a0 = aff[n0], a1 = aff[n0 + 1];
+  const float2 a0 = aff[n0], a1 = aff[n1];
   float s0 = 0.f, s1 = 0.f;
   // The thread walks its quads (row yy, quad k of the row, k += 2) with counters instead of
   // divisions and keeps PU independent 16-byte loads in flight per batch (addresses clamped to a
@@ -1398,7 +1408,7 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __re
       const long long tile = ((long long)b * tiles_y + ry / C3_TH) * tiles_x + xq / C3_TW;
       const int ly = ry % C3_TH, lx = xq % C3_TW;
       const int wave = wn * 4 + (ly >> 1), mi = (ly & 1) * 2 + (lx >> 4), g = (lx & 15) >> 2;
-      v[u] = *reinterpret_cast<const uint4*>(y + ((((tile * 8 + wave) * 4 + mi) * 8 + nj) * 64 + g * 16 + r) * 4);
+      v[u] = *reinterpret_cast<const uint4*>(y + ((((tile * 8 + wave) * 4 + mi) * 4 + np) * 64 + g * 16 + r) * 8);
       k += 2;
       while (k >= nq) {
         k -= nq;
@@ -1421,7 +1431,7 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __re
     }
   }
   red[ql][n0] = s0;
-  red[ql][n0 + 1] = s1;
+  red[ql][n1] = s1;
   __syncthreads();
   const int c = threadIdx.x;
   part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = red[0][c] + red[1][c];
