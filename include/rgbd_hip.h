@@ -271,6 +271,23 @@ int rgbd_mask_logits(int dtype, const void* emb, const void* pix, int B, int Q, 
 int rgbd_mask_attention(int dtype, const void* logits, int B, int Q, int H, int W, int th, int tw,
                         int heads, uint8_t* attn, void* stream);
 
+/* ---------------------------------------------------------------- f4 instance post-processing
+ * Replaces Mask2FormerImageProcessor.post_process_instance_segmentation (transformers 5.15
+ * image_processing_mask2former.py:627-744; called by the reference's process_prediction,
+ * mask2former/predictor.py:697-700) with return_coco_annotation / return_binary_maps False.
+ *   class_logits float32 [B][Q][C1] (C1 = classes + no-object), mask_logits float32 [B][Q][h][w];
+ *   target_h_host / target_w_host: per-image output sizes (the reference's target_sizes; pass
+ *   384 x 384 for "no resize"); seg_host: B device pointers to float32 [Ht][Wt] maps (written:
+ *   segment id per pixel, -1 = none); topk_idx int32 [B][Q]: flat (query * C + class) indices in
+ *   the order CPU torch.topk(sorted=False) returns them (libstdc++ nth_element, restated);
+ *   pred_scores float32 [B][Q] (class prob x mask score); seg_id int32 [B][Q]: the segment id of
+ *   each top-k entry, -1 when dropped (empty mask at the target size or score < threshold).
+ *   Q * (C1 - 1) <= 20480 (the selection runs in LDS).  ws: rgbd_pp_instance_workspace_size. */
+size_t rgbd_pp_instance_workspace_size(int B, int Q);
+int rgbd_pp_instance(const float* class_logits, const float* mask_logits, int B, int Q, int C1, int h, int w,
+                     const int* target_h_host, const int* target_w_host, double threshold, float* const* seg_host,
+                     int* topk_idx, float* pred_scores, int* seg_id, void* ws, void* stream);
+
 /* ---------------------------------------------------------------- kernel timing (bench only)
  * When enabled, launch functions bracket their main kernel with hipEvents recorded on the
  * launch stream; rgbd_timing_read synchronises those events and returns the summed

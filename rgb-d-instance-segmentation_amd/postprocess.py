@@ -1,0 +1,98 @@
+"""f4: instance post-processing on the device.
+
+The reference turns its predictions into instance maps with the Hugging Face image processor on
+the CPU (mask2former/predictor.py:697-700, process_prediction ->
+Mask2FormerImageProcessor.post_process_instance_segmentation, transformers 5.15
+image_processing_mask2former.py:627-744): per image a 100-query top-k over the class
+probabilities, 100 bilinear 384x384 mask upsamplings, sigmoid mask scores, a nearest resize to
+the original size and an ordered paint of the kept masks.  ``post_process_instance_segmentation``
+does the same on the GPU (csrc/postprocess.hip, rgbd_pp_instance) with the reference's
+arguments and return format; ``install`` swaps it into an image processor instance, so
+``process_prediction`` runs unchanged.
+
+Parity (tests/test_gpu_postprocess.py, against the HF processor on the CPU): the top-k indices
+come out in CPU torch.topk(sorted=False)'s order (libstdc++ nth_element, restated and pinned in
+oracle/postprocess.py), so segment ids, labels and the painted map are identical; pred scores
+agree to float32 summation order (rtol 1e-5).  A pixel whose interpolated logit lies within a
+few ulp of 0 could binarise differently (the CPU kernel's rounding is not reproduced bit for
+bit); the fixtures check none does.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check
+from .ops import _need_cuda, _p, _stream, _workspace
+
+CHUNK = 64  # images per launch (bounds the device copy of the mask logits)
+
+
+def _run(cls, masks, sizes, threshold):
+    B, Q, C1 = cls.shape
+    h, w = masks.shape[-2:]
+    dev = cls.device
+    segs = [torch.empty(s, dtype=torch.float32, device=dev) for s in sizes]
+    topk = torch.empty((B, Q), dtype=torch.int32, device=dev)
+    ps = torch.empty((B, Q), dtype=torch.float32, device=dev)
+    sid = torch.empty((B, Q), dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    ws = _workspace(dev, L.rgbd_pp_instance_workspace_size(B, Q), "postprocess")
+    th = (ctypes.c_int * B)(*[s[0] for s in sizes])
+    tw = (ctypes.c_int * B)(*[s[1] for s in sizes])
+    sp = (ctypes.c_void_p * B)(*[t.data_ptr() for t in segs])
+    check(L.rgbd_pp_instance(_p(cls), _p(masks), B, Q, C1, h, w, th, tw, ctypes.c_double(threshold), sp, _p(topk),
+                             _p(ps), _p(sid), _p(ws), _stream(dev)), "rgbd_pp_instance")
+    return segs, topk, ps, sid
+
+
+def post_process_instance_segmentation(outputs, threshold: float = 0.5, mask_threshold: float = 0.5,
+                                       overlap_mask_area_threshold: float = 0.8, target_sizes=None,
+                                       return_coco_annotation: bool = False, return_binary_maps: bool = False,
+                                       device=None, keep_on_device: bool = False):
+    """Same arguments and results as the HF method (mask_threshold and
+    overlap_mask_area_threshold are accepted and unused there too).  Inputs may be CPU tensors
+    (the reference passes the predictions as numpy-backed CPU tensors); they are moved to
+    ``device`` (default: the current GPU).  Segmentation maps come back as CPU float32 tensors
+    like the reference's, or stay on the GPU with ``keep_on_device``."""
+    if return_coco_annotation and return_binary_maps:
+        raise ValueError("return_coco_annotation and return_binary_maps can not be both set to True.")
+    if return_binary_maps:
+        raise NotImplementedError("return_binary_maps: not used by the reference; not built on the device")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    cls_all = outputs.class_queries_logits
+    masks_all = outputs.masks_queries_logits
+    B = cls_all.shape[0]
+    if target_sizes is not None and len(target_sizes) != B:
+        raise ValueError("Make sure that you pass in as many target sizes as the batch dimension of the logits")
+    results = []
+    for b0 in range(0, B, CHUNK):
+        b1 = min(B, b0 + CHUNK)
+        cls = cls_all[b0:b1].to(device=dev, dtype=torch.float32).contiguous()
+        masks = masks_all[b0:b1].to(device=dev, dtype=torch.float32).contiguous()
+        _need_cuda(cls, masks)
+        sizes = [(384, 384)] * (b1 - b0) if target_sizes is None else \
+            [(int(t[0]), int(t[1])) for t in target_sizes[b0:b1]]
+        segs, topk, ps, sid = _run(cls, masks, sizes, float(threshold))
+        C = cls.shape[-1] - 1
+        topk_h, ps_h, sid_h = topk.cpu().tolist(), ps.cpu().tolist(), sid.cpu().tolist()
+        for i in range(b1 - b0):
+            segments = [{"id": sid_h[i][j], "label_id": topk_h[i][j] % C, "was_fused": False,
+                         "score": round(ps_h[i][j], 6)}
+                        for j in range(len(sid_h[i])) if sid_h[i][j] >= 0]
+            seg = segs[i] if keep_on_device else segs[i].cpu()
+            if return_coco_annotation:
+                from transformers.models.mask2former.image_processing_pil_mask2former import convert_segmentation_to_rle
+                seg = convert_segmentation_to_rle(seg)
+            results.append({"segmentation": seg, "segments_info": segments})
+    return results
+
+
+def install(image_processor, device=None):
+    """Route ``image_processor.post_process_instance_segmentation`` (an HF Mask2Former image
+    processor instance, as the reference's predictor builds it) through the device path."""
+    def method(outputs, *args, **kwargs):
+        kwargs.setdefault("device", device)
+        return post_process_instance_segmentation(outputs, *args, **kwargs)
+    image_processor.post_process_instance_segmentation = method
+    return image_processor
