@@ -1437,6 +1437,68 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __re
   part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = red[0][c] + red[1][c];
 }
 
+// The same pool over whole 8x32-px conv tiles, when every tile lies inside one pool region and no
+// regions overlap (H % 32 == 0, W % 128 == 0: 640x480).  A tile's 128 KiB of y is one contiguous
+// stream; thread t reads 16-byte chunk t + 256k (k = wave x mi of the conv tile), so a wave load
+// is 1 KiB contiguous and the thread keeps fixed channels: (np, r) of the chunk lane, both wn
+// halves -> 4 channel sums; the 4 pixel-quad lanes of a channel fold by shuffles at the end.
+// Split sp of region reg takes the region's tiles sp, sp + POOL_SPLIT, ... (raster order).
+__global__ __launch_bounds__(256) void k_rp_bn_relu_pool_tiles(const bf16_t* __restrict__ y, int H, int W,
+                                                               const float2* __restrict__ aff,
+                                                               float* __restrict__ part) {
+  __shared__ float red[C5];
+  const int b = blockIdx.y, reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
+  const int i = reg / 4, j = reg % 4;
+  const int tiles_x = W / C3_TW, tiles_y = H / C3_TH;
+  const int rty = tiles_y / 4, rtx = tiles_x / 4;  // region size in tiles
+  const int t = threadIdx.x, lane = t & 63, np = t >> 6, r = lane & 15;
+  float2 af[2][2];
+#pragma unroll
+  for (int wn = 0; wn < 2; ++wn)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) af[wn][h] = aff[wn * 128 + 32 * np + 16 * h + r];
+  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  for (int q = sp; q < rty * rtx; q += POOL_SPLIT) {
+    const int ty = i * rty + q / rtx, tx = j * rtx + q % rtx;
+    const long long tile = ((long long)b * tiles_y + ty) * tiles_x + tx;
+    const uint4* src = reinterpret_cast<const uint4*>(y + tile * (8 * 4 * 4 * 512)) + t;
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 16) {
+      uint4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 256 * (k0 + u)));
+        v[u] = make_uint4(x.x, x.y, x.z, x.w);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int wn = (k0 + u) >> 4;  // k = wv * 4 + mi, wv = wn * 4 + row pair
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float lo = __uint_as_float(w[2 * h + e] << 16), hi = __uint_as_float(w[2 * h + e] & 0xffff0000u);
+            acc[wn][h] += fmaxf(lo * af[wn][h].x + af[wn][h].y, 0.f);
+            acc[wn][h] += fmaxf(hi * af[wn][h].x + af[wn][h].y, 0.f);
+          }
+      }
+    }
+  }
+  // the 4 pixel-quad lanes (g) of each (np, r) -> one sum per channel, fixed order
+#pragma unroll
+  for (int wn = 0; wn < 2; ++wn)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v = acc[wn][h];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) red[wn * 128 + 32 * np + 16 * h + r] = v;
+    }
+  __syncthreads();
+  part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + t] = red[t];
+}
+
 // ------------------------------------------------------------------ tail: conv 256->512 on 4x4
 __global__ void k_rp_pool_finish(const float* __restrict__ part, int B, int H, int W, float* __restrict__ pooled) {
   // pooled[b][256][16] = mean over the region = sum of the split partials / count
@@ -1800,7 +1862,10 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
                                 bn.p[19], aff5);
   if constexpr (sizeof(T) == 2)
-    k_rp_bn_relu_pool_frag<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
+    if (H % (4 * C3_TH) == 0 && W % (4 * C3_TW) == 0)
+      k_rp_bn_relu_pool_tiles<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
+    else
+      k_rp_bn_relu_pool_frag<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
   else
     k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
   k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);

@@ -347,6 +347,34 @@ def test_streaming_graph_replay_matches_eager():
             assert torch.equal(a, e)
 
 
+def test_graph_survives_a_larger_later_capture():
+    """ADVICE r1 (workspaces and captured graphs): a graph keeps pointing at the workspaces it was
+    captured with.  Capturing a second, larger path on the same capture stream grows those
+    workspaces; the replaced buffers must stay alive (ops._ws_retired), so replaying the first
+    graph afterwards still reproduces its own earlier output bit for bit."""
+    from rgbd_amd.modules import EnhancedDepthImageRatioPredictor
+    from rgbd_amd.stream import StreamingHotPath
+    rp = EnhancedDepthImageRatioPredictor(3)
+    winit.init_deterministic(rp, prefix="model.pixel_level_module.ratio_predictor.")
+    rp = rp.to(DEV)
+    dsams, dg = _hot_modules(torch.bfloat16)
+    small = StreamingHotPath(rp, dsams, dg, 64, 96, B=1, dtype=torch.bfloat16)
+    f = synthetic.make_scene(synthetic.scene_seed(8, 0), 64, 96)
+    d = torch.from_numpy(f["depth_u8"][None]).to(DEV)
+    c = torch.from_numpy(f["rgb_u8"][None]).contiguous().to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    colors = [torch.randn(t.shape, generator=g, device=DEV).to(t.dtype) for t in small.colors]
+    first = [t.clone() for t in small(d, c, colors)[0]]
+    big = StreamingHotPath(rp, dsams, dg, 192, 256, B=2, dtype=torch.bfloat16).capture()
+    fb = synthetic.make_scene(synthetic.scene_seed(8, 1), 192, 256)
+    big(torch.from_numpy(np.stack([fb["depth_u8"]] * 2)).to(DEV),
+        torch.from_numpy(np.stack([fb["rgb_u8"]] * 2)).contiguous().to(DEV))
+    torch.cuda.synchronize()
+    again = small(d, c, colors)[0]
+    for a, e in zip(again, first):
+        assert torch.equal(a, e)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_dggm_multi_scale_equals_per_scale(dtype):
     """rgbd_dggm_fuse_{fwd,bwd}_multi (all scales in one launch, as the fused hot path calls them)
