@@ -886,7 +886,11 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
 #pragma unroll
     for (int t = 0; t < 8; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) nxt[t][u] = *reinterpret_cast<const uint2*>(ft + ((t * 2 + u) * 64 + lane) * 4);
+      for (int u = 0; u < 2; ++u) {  // read once: non-temporal
+        const unsigned long long q =
+            __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ft + ((t * 2 + u) * 64 + lane) * 4));
+        nxt[t][u] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+      }
   };
   fetch(blockIdx.x);
   for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
