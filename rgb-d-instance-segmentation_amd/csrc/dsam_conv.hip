@@ -825,7 +825,9 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
 // parked in LDS, then written in the OIHW (c, tap) order.
 __global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restrict__ partial, const int4* __restrict__ items,
                                                             const int* __restrict__ counts, int Cin, int Cout,
-                                                            float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
+                                                            float* __restrict__ dconv_w, float* __restrict__ dproj_w,
+                                                            const float* __restrict__ csum, const rgbd_decomp_info* info,
+                                                            int B, int nsplit, float* __restrict__ dbias) {
   extern __shared__ float srow[];  // [5][9*Cin]
   __shared__ int scode[1024];      // item -> code, staged once
   const int KK = 9 * Cin, o = blockIdx.x, ni = counts[1];
@@ -866,6 +868,18 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restr
 #pragma unroll
     for (int i = 0; i < 4; ++i) dconv_w[((long long)i * Cout + o) * KK + e] = srow[i * KK + kk];
     dproj_w[(long long)o * KK + e] = srow[4 * KK + kk];
+  }
+  // the biases' gradients of o (csum [nsplit][B][Cout]; conv_layers[i] only where i < len(masks)),
+  // wave i in k_dsam_bias_grad's fixed order
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (dbias && wv < 4) {
+    float sb = 0.f;
+    for (int q = lane; q < nsplit * B; q += 64) {
+      const int b = q % B;
+      if (wv < info[b].n_masks) sb += csum[(long long)q * Cout + o];
+    }
+    sb = wave_sum(sb);
+    if (lane == 0) dbias[wv * Cout + o] = sb;
   }
 }
 
@@ -1915,7 +1929,11 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
     if (cattr != hipSuccess) return (int)cattr;
     RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
-    k_dsam_wgrad_combine<<<Cout, 256, csmem, s>>>(partial, a.items, a.counts, Cin, Cout, dconv_w, dproj_w);
+    const int nsplit_bf = gout_nchw ? 1 : chan_sum_splits(hwo);
+    k_dsam_wgrad_combine<<<Cout, 256, csmem, s>>>(partial, a.items, a.counts, Cin, Cout, dconv_w, dproj_w, csum, info,
+                                                  B, nsplit_bf, dbias);
+    RGBD_CHECK_LAUNCH();
+    return RGBD_OK;  // the combine also wrote the bias gradients
   } else {
     return RGBD_E_DTYPE;
   }
