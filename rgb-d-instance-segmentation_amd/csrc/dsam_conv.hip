@@ -48,6 +48,7 @@ struct ConvArgs {
   int* items;                       // bf16: work list of k_dsam_lds (k_dsam_items)
   int* nitems;
   int* tickets;                     // bf16: per (class, tile, N tile) chunk counter, zeroed by k_dsam_plan
+  int* work;                        // bf16: per N tile next-item counter of k_dsam_lds, zeroed by k_dsam_plan
   int ntiles0;                      // bf16: tiles of the largest class
   int chunk_len;                    // bf16: steps per workgroup chunk of a tile
   float* partial;                   // bf16: partial tiles of multi-chunk tiles (reduced by their last chunk)
@@ -1128,6 +1129,7 @@ __global__ __launch_bounds__(128) void k_dsam_plan(ConvArgs a, int ntiles0, int 
   if (cls == 0 && tile == 0 && tid < LD_ZERO_BYTES / 16)
     reinterpret_cast<uint4*>(const_cast<bf16_t*>(a.zero))[tid] = make_uint4(0u, 0u, 0u, 0u);
   for (int q = tid; q < ntn; q += 128) a.tickets[((long long)cls * ntiles0 + tile) * ntn + q] = 0;
+  if (cls == 0 && tile == 0 && tid < ntn) a.work[tid] = 0;
 }
 
 // Work list: per (class, tile) the chunk count, compacted into items (cls | chunk << 2 |
@@ -1527,14 +1529,24 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   }
 }
 
-// Persistent: grid (workgroups, N tiles); each workgroup walks the item list.
+// Persistent: grid (workgroups, N tiles); each workgroup takes the next item of its N tile's list
+// from a counter (items differ up to ~5x in steps: dynamic assignment balances the tail; the
+// multi-chunk reductions stay in chunk order, so results do not depend on who ran what).
 template <int KC>
 __global__ __launch_bounds__(512, 1) void k_dsam_lds(ConvArgs a) {
+  using Cfg = LdCfg<KC>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  int* next_s = (int*)(smem + Cfg::TMASK + 216);  // free bytes behind the per-tap code lists
   const int nitems = *a.nitems;
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+  for (;;) {
+    if (threadIdx.x == 0)
+      *next_s = __hip_atomic_fetch_add(a.work + blockIdx.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int it = *next_s;
+    if (it >= nitems) break;  // workgroup-uniform
     const int v = a.items[it];
     ld_item<KC>(a, v & 3, v >> 5, (v >> 2) & 7, blockIdx.y, gridDim.y);
-    __syncthreads();  // LDS of this item no longer read
+    __syncthreads();  // LDS of this item no longer read, next_s read by every thread
   }
 }
 
@@ -1569,7 +1581,7 @@ LdPlan ld_plan(const ConvArgs& a) {
   p.chunk_len = std::max(1, (ntap * (a.C / (32 * p.kc)) * pct + 99) / 100);
   p.tmask_bytes = align256((size_t)nclass * p.ntiles0 * 16 * sizeof(uint16_t));
   p.items_bytes = align256(((size_t)nclass * p.ntiles0 * LD_CH + 1) * sizeof(int));
-  p.ticket_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * sizeof(int)) + LD_ZERO_BYTES;
+  p.ticket_bytes = align256((size_t)(nclass * p.ntiles0 * p.ntn + 64) * sizeof(int)) + LD_ZERO_BYTES;  // + work counters
   p.partial_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * LD_CH * LD_BN * LD_BM * sizeof(float));
   return p;
 }
@@ -1606,6 +1618,8 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
     b.items = (int*)((char*)a.partial + P.tmask_bytes);
     b.nitems = b.items + (size_t)nclass * P.ntiles0 * LD_CH;
     b.tickets = (int*)((char*)a.partial + P.tmask_bytes + P.items_bytes);
+    b.work = b.tickets + (size_t)nclass * P.ntiles0 * P.ntn;
+    RGBD_REQUIRE(P.ntn <= 64, RGBD_E_SHAPE);
     b.partial = (float*)((char*)a.partial + P.tmask_bytes + P.items_bytes + P.ticket_bytes);
     b.zero = (const bf16_t*)((char*)b.partial - LD_ZERO_BYTES);  // the ticket region's tail
     RGBD_REQUIRE(9 * 16 * (a.C / (32 * P.kc)) <= LD_MAXSTEP, RGBD_E_SHAPE);
