@@ -651,6 +651,7 @@ __global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
     ibase[16] = ni;
     a.counts[0] = total;
     a.counts[1] = ni;
+    a.counts[2] = 0;  // k_dsam_wgrad_mm's next-work counter
   }
   __syncthreads();
   for (int it = tid; it < ibase[16]; it += 1024) {
@@ -721,7 +722,15 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
     f.v = make_uint4(u0.x, u0.y, u1.x, u1.y);
     return f;
   };
-  for (int wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+  int* next_s = (int*)(smem + Cfg::OFF_UNITS) + WITEM_MAX - 1;  // unit ids are staged after the read
+  for (;;) {
+    // dynamic assignment of (item, tile) work: items differ in live units per code
+    __syncthreads();
+    if (tid == 0) *next_s = __hip_atomic_fetch_add(a.counts + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int wi = *next_s;
+    __syncthreads();  // every thread has it before the unit ids overwrite the slot
+    if (wi >= nwork) break;
     const int4 item = a.items[wi / ntile];
     const int tile = wi % ntile, e0 = item.y, nst = (a.dbg & 1) ? 0 : item.z - item.y;
     const int kk0 = (tile % a.ntile_kk) * 128, o0 = (tile / a.ntile_kk) * 32 * FM;
