@@ -1665,15 +1665,19 @@ static WgPlan wg_plan(int B, int Cin, int h, int w, int Cout) {
   p.max_entries = 16 * B * p.nunit;
   return p;
 }
-// items are at most max_entries; the plan targets ~256 work units (one per CU: every unit writes an
-// f32 partial tile the combine re-reads, so more units cost more than the balance they buy)
-static int wg_target() {
-  static const int t = getenv("RGBD_WG_TARGET") ? atoi(getenv("RGBD_WG_TARGET")) : 256;
-  return t;
+// items are at most max_entries; the plan targets about one work unit per CU (every unit writes an
+// f32 partial tile the combine re-reads, so more units cost more than the balance they buy): 256,
+// 384 for layers with many output tiles (dsam2's 108: units of ~3 items balance better under the
+// dynamic assignment), 192 for layers with few (dsam0's 7) — measured per layer at 640x480
+static int wg_target(const WgPlan& p) {
+  static const int t = getenv("RGBD_WG_TARGET") ? atoi(getenv("RGBD_WG_TARGET")) : 0;
+  if (t > 0) return t;
+  const int tiles = p.ntile_kk * p.ntile_o;
+  return tiles >= 64 ? 384 : (tiles <= 8 ? 192 : 256);
 }
 // partial buffer bound: items <= entries / L + 16 with L >= entries / (target / tiles)
 static size_t wg_max_items(const WgPlan& p) {
-  const long long want = std::max(1, wg_target() / std::max(1, p.ntile_kk * p.ntile_o));
+  const long long want = std::max(1, wg_target(p) / std::max(1, p.ntile_kk * p.ntile_o));
   return (size_t)std::min<long long>(p.max_entries, want + 16 + p.max_entries / WITEM_MAX);
 }
 
@@ -1930,7 +1934,7 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
     a.nunit = P.nunit;
     a.ntile_kk = P.ntile_kk;
     a.ntile_o = P.ntile_o;
-    a.target = wg_target();
+    a.target = wg_target(P);
     a.inv_wo = 1.0f / (float)wo;
     a.zero = (const bf16_t*)((char*)ws + L.zero);
     a.partial = partial;
