@@ -1142,7 +1142,9 @@ __global__ __launch_bounds__(128) void k_dsam_plan(ConvArgs a, int ntiles0, int 
 }
 
 // Work list: per (class, tile) the chunk count, compacted into items (cls | chunk << 2 |
-// tile << 5) in (class, tile, chunk) order by one workgroup; a[*nitems] = count.
+// tile << 5) in (class, tile, chunk) order by one workgroup; a[*nitems] = count.  dX lists the
+// parity classes by decreasing live-tap count (3: 4 taps, 1 and 2: 2, 0: 1), so the longest
+// items are taken first under the dynamic assignment.
 __global__ __launch_bounds__(1024) void k_dsam_items(ConvArgs a, int ntiles0, int ncg) {
   __shared__ int wsum[16];
   __shared__ int base_s;
@@ -1154,9 +1156,11 @@ __global__ __launch_bounds__(1024) void k_dsam_items(ConvArgs a, int ntiles0, in
     const int e = e0 + tid;
     int nc = 0;
     if (e < total) {
-      const int cls = e / ntiles0, tile = e - cls * ntiles0;
+      const int ce = e / ntiles0, tile = e - ce * ntiles0;
+      const int cls = a.transposed ? (0x0213 >> (4 * ce)) & 15 : ce;  // class order 3, 1, 2, 0
       const LdGeom G = ld_geom(a, cls);
-      if (tile < G.ntiles) nc = ld_nchunks(ld_steps(a.tmasks + (long long)e * 16, G.ntap, ncg), a.chunk_len);
+      if (tile < G.ntiles)
+        nc = ld_nchunks(ld_steps(a.tmasks + ((long long)cls * ntiles0 + tile) * 16, G.ntap, ncg), a.chunk_len);
     }
     // block exclusive scan of nc
     int x = nc;
@@ -1171,7 +1175,8 @@ __global__ __launch_bounds__(1024) void k_dsam_items(ConvArgs a, int ntiles0, in
     for (int q = 0; q < w; ++q) before += wsum[q];
     const int off = before + x - nc;
     if (e < total) {
-      const int cls = e / ntiles0, tile = e - cls * ntiles0;
+      const int ce = e / ntiles0, tile = e - ce * ntiles0;
+      const int cls = a.transposed ? (0x0213 >> (4 * ce)) & 15 : ce;  // class order 3, 1, 2, 0
       for (int c = 0; c < nc; ++c) a.items[off + c] = cls | (c << 2) | (tile << 5);
     }
     __syncthreads();
