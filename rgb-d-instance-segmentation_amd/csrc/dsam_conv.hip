@@ -43,7 +43,7 @@ struct ConvArgs {
   void* out_nchw;                   // optional
   void* out_nhwc;                   // optional
   int ksplit;                       // unused (1)
-  int dbg;                          // diagnostics (RGBD_DSAM_DBG): 1 skip steps
+  int dbg;                          // diagnostics (RGBD_DSAM_DBG): 1 skip steps, 2 epilogue, 4 hand-off
   uint16_t* tmasks;                 // bf16: [class][tile][16] per-tap code sets (k_dsam_plan)
   int* items;                       // bf16: work list of k_dsam_lds (k_dsam_items)
   int* nitems;
@@ -1194,7 +1194,6 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   int4* rowtab = (int4*)(smem + Cfg::ROWTAB);
   int4* rowout = (int4*)(smem + Cfg::ROWOUT);
-  uint8_t* tcl = (uint8_t*)(smem + Cfg::TMASK + 64);  // [9][16]
   float* bsum = (float*)(smem + Cfg::BSUM);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1224,17 +1223,23 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
       for (int sb = 0; sb < k; ++sb) s += a.bias4[sb * a.N + n];
     bsum[e] = s;
   }
-  if (tid < 9) {  // per tap: its code list, and its run of the step table (chunk group major)
-    uint32_t msk = tmask[tid];
-    int n = 0;
+  // step table, tap major, then chunk group, then code (ascending): one thread per (tap, chunk
+  // group) writes its run from registers (no LDS round trips)
+  for (int q = tid; q < G.ntap * ncg; q += 512) {
+    const int t = q / ncg, cg = q - t * ncg;
+    uint32_t msk = 0u;
+    int e = 0;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      if (u == t) msk = tmask[u];
+      if (u < t) e += __popc(tmask[u]) * ncg;
+    }
+    e += cg * __popc(msk);
+    int* steptab = (int*)(smem + Cfg::STEPTAB);
     while (msk) {
-      tcl[tid * 16 + n++] = (uint8_t)(__ffs(msk) - 1);
+      steptab[e++] = t | (cg << 4) | ((__ffs(msk) - 1) << 12);
       msk &= msk - 1u;
     }
-    int* steptab = (int*)(smem + Cfg::STEPTAB);
-    int e = tb[tid];
-    for (int cg = 0; cg < ncg; ++cg)
-      for (int ci = 0; ci < n; ++ci) steptab[e++] = tid | (cg << 4) | ((int)tcl[tid * 16 + ci] << 12);
   }
   if (tid < LD_BM) {
     int b, i, j, org;
@@ -1333,7 +1338,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     if (ahead <= 0) vm_wait_barrier<0>();
     else vm_wait_barrier_dyn(ahead * cnt);
   }
-  if (nc > 1) {
+  if (nc > 1 && !(a.dbg & 4)) {  // RGBD_DSAM_DBG bit 4: no hand-off (timing experiments only)
     // Multi-chunk tile: publish this chunk's fragment-native partial ([wave][mi][nj][lane][4] f32),
     // take a ticket; the chunk that draws nc-1 sums all partials in chunk order (deterministic)
     // and runs the epilogue.  The hand-off is write-through: every partial byte is stored and

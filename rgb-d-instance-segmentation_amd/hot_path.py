@@ -15,11 +15,62 @@ Here:
 Backward produces exactly the gradients the reference graph has: DSAM / DGGM parameters,
 nothing for the colour maps (detached) or the ratio (left the graph via .item()).
 """
+import os
+
 import torch
 
 from . import ops
 
 DSAM_PARAMS_PER_MODULE = 9  # conv_layers.{0..3}.{weight,bias}, rgb_projection.weight
+_SIDE_STREAMS = {}
+_OVERLAP = os.environ.get("RGBD_OVERLAP", "1") != "0"  # side-stream backward (A/B switch)
+
+
+def side_stream(dev):
+    """The per-device stream the bf16 backward runs its off-critical-path launches on."""
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+class _Side:
+    """Fork/join of launches onto the side stream (works eagerly and under graph capture: the side
+    stream joins the capture through the fork's event).  Inputs are recorded on the side stream
+    so the allocator does not hand their memory to the main stream while side work reads it;
+    outputs are recorded on the main stream at the join."""
+
+    def __init__(self, dev, enabled):
+        self.on = enabled
+        if enabled:
+            self.main = torch.cuda.current_stream(dev)
+            self.side = side_stream(dev)
+        self.outs = []
+
+    def run(self, fn, *inputs):
+        if not self.on:
+            return fn()
+        self.side.wait_stream(self.main)
+        for t in inputs:
+            t.record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            out = fn()
+        self.outs.append(out)
+        return out
+
+    def join(self):
+        if not self.on:
+            return
+        self.main.wait_stream(self.side)
+
+        def rec(o):
+            if isinstance(o, torch.Tensor):
+                o.record_stream(self.main)
+            elif isinstance(o, (list, tuple)):
+                for x in o:
+                    rec(x)
+        rec(self.outs)
+        self.outs = []
 
 
 def stack4(ts, view_only=False):
@@ -65,24 +116,36 @@ class HotPathFunction(torch.autograd.Function):
         dsam_p = [params[9 * k:9 * k + 9] for k in range(3)]
         dggm_p = params[27:35]
         sizes = [tuple(c.shape[2:]) for c in colors[:3]]
+        bf16 = dtype == torch.bfloat16
+        # bf16 on the GPU: the colour-map layout changes run beside the decomposition and the
+        # dsam1 / dsam2 packing beside dsam0 (side stream; joined before their consumers)
+        side = _Side(pixel_values.device, bf16 and pixel_values.is_cuda and cfg.get("overlap", True))
+        if bf16:
+            nhwc = side.run(lambda: [ops.nchw_to_nhwc(c) for c in colors], *colors)
         codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
         if cfg.get("check_status"):
             ops.raise_on_status(info)
         if cfg.get("status_sink") is not None:
             cfg["status_sink"].append(ops.DeferredStatus(info))
         training = any(ctx.needs_input_grad[7:])
-        masks = ops.dsam_code_masks(codes) if dtype == torch.bfloat16 else None
-        packs = [cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
-                                          code_mask=None if masks is None else masks[k:k + 1],
-                                          want_bwd=training and k > 0)  # dsam0's input takes no gradient
-                 for k in range(3)]
-        x_nhwc = [ops.nchw_to_nhwc(colors[0])]
+        masks = ops.dsam_code_masks(codes) if bf16 else None
+
+        def pack(k):
+            return cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
+                                            code_mask=None if masks is None else masks[k:k + 1],
+                                            want_bwd=training and k > 0)  # dsam0's input takes no gradient
         cp1 = [colors[0]]
-        if dtype == torch.bfloat16:
+        if bf16:
+            packs = [pack(0)]
+            side.join()  # the NHWC colour maps
+            packs += side.run(lambda: [pack(1), pack(2)], masks)
+            x_nhwc = [nhwc[0]]
+            res_nhwc = nhwc[1:]
             # bf16 cascade entirely in NHWC: each DSAM adds its residual colour map in NHWC and writes
             # cp1[k+1] once, in the layout the next DSAM reads and the DGGM pass accepts
-            res_nhwc = [ops.nchw_to_nhwc(c) for c in colors[1:]]
             for k in range(3):
+                if k == 1:
+                    side.join()  # the dsam1 / dsam2 packs
                 bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
                 out_nhwc = ops.dsam_fwd_nhwc(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual_nhwc=res_nhwc[k])
                 cp1.append(out_nhwc)
@@ -90,6 +153,8 @@ class HotPathFunction(torch.autograd.Function):
                     x_nhwc.append(out_nhwc)
             cp1_nhwc = (1, 2, 3)
         else:
+            packs = [pack(k) for k in range(3)]
+            x_nhwc = [ops.nchw_to_nhwc(colors[0])]
             for k in range(3):
                 bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
                 out, out_nhwc = ops.dsam_fwd(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual=colors[k + 1],
@@ -121,26 +186,40 @@ class HotPathFunction(torch.autograd.Function):
                 raise RuntimeError("hot-path backward needs gradients for all four backbone features"
                                    if shape is None else "missing gradient for scale 0")
             G.append(g.to(dtype).contiguous())
-        grads_dggm = []
-        for k, (dw, db) in enumerate(ops.dggm_fuse_bwd_multi(G, pixel_values, dggm_p[0::2], dggm_p[1::2])):
-            grads_dggm += [dw.reshape(dggm_p[2 * k].shape).to(dggm_p[2 * k].dtype), db.to(dggm_p[2 * k + 1].dtype)]
+        bf16 = dtype == torch.bfloat16
+        # bf16 on the GPU: the critical path is dX2 -> dX1 -> dW0 (main stream); the DGGM backward
+        # and the dW of dsam2 / dsam1 run beside it on the side stream (their persistent kernels
+        # take CUs as the other stream's work drains; every kernel assigns its work dynamically)
+        side = _Side(G[0].device, bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True))
+
+        def dggm_bwd():
+            out = []
+            for k, (dw, db) in enumerate(ops.dggm_fuse_bwd_multi(G, pixel_values, dggm_p[0::2], dggm_p[1::2])):
+                out += [dw.reshape(dggm_p[2 * k].shape).to(dggm_p[2 * k].dtype), db.to(dggm_p[2 * k + 1].dtype)]
+            return out
+        grads_dggm = side.run(dggm_bwd, *G, pixel_values)
         # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}.  bfloat16 keeps the cascade in
         # NHWC (dX written NHWC only, its residual G[k] converted once; bias sums from NHWC).
-        bf16 = dtype == torch.bfloat16
         hook = ctx.cfg.get("grad_hook")
         dcp = G[3]
         dcp_nhwc = ops.nchw_to_nhwc(dcp)
         grads_dsam = [None, None, None]
         for k in (2, 1, 0):
-            dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
-                                                      gout_nhwc=dcp_nhwc)
-            gk = []
-            for i in range(4):
-                gk += [dconv[i], dbias[i]]
-            gk.append(dproj)
-            grads_dsam[k] = gk
-            if hook is not None:  # DDP: this module's all-reduce runs under the rest of the cascade
-                hook(2 - k, gk if k > 0 else gk + grads_dggm)
+            def dsam_dw(k=k, dcp=dcp, dcp_nhwc=dcp_nhwc):
+                dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k],
+                                                          ctx.info, gout_nhwc=dcp_nhwc)
+                gk = []
+                for i in range(4):
+                    gk += [dconv[i], dbias[i]]
+                gk.append(dproj)
+                if hook is not None:  # DDP: this module's all-reduce runs under the rest of the cascade
+                    hook(2 - k, gk if k > 0 else gk + grads_dggm)
+                return gk
+            if k > 0:
+                grads_dsam[k] = side.run(dsam_dw, dcp_nhwc, ctx.x_nhwc[k], ctx.codes[k], ctx.info)
+            else:  # the last launch of the backward: on the main stream, after the join
+                side.join()
+                grads_dsam[k] = dsam_dw()
             if k > 0:
                 if bf16:
                     dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], None, want_nhwc=True,
@@ -170,6 +249,6 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
         conv = dggm_module.depth_enhancement_layers[i][0]
         params += [conv.weight, conv.bias]
     cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook, "status_sink": status_sink,
-           "pack_cache": [m._pack_cache for m in dsam_modules]}
+           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": _OVERLAP}
     pv = pixel_values.detach().float().contiguous()
     return list(HotPathFunction.apply(pv, ratio, cfg, *colors, *params))
