@@ -1151,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y
 // one piece of A (this tile's half 1 during steps 0-5, the next tile's half 0 during 9-14),
 // runs its 64 MFMAs, waits for its own DMA except the A piece just issued, barrier.
 // Epilogue straight from the accumulators: y is written in a fragment-native layout
-// [tile][wave][mi][nj/2][lane][2 ch x 4 px] (1 KiB contiguous per store instruction; read back by
+// [tile][wave][mi][nj/2][lane][2 ch x 4 px] (1 KiB contiguous per non-temporal store instruction; read back by
 // k_rp_bn_relu_pool_frag) and the BN statistics of the float32 conv outputs (as the fp32
 // reference takes them) accumulate in registers across tiles.
 constexpr int C3_TH = 8, C3_TW = 32;
@@ -1190,7 +1190,7 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
 
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
-                                                       bf16_t* __restrict__ y, float* __restrict__ slab) {
+                                                       bf16_t* __restrict__ y, float* __restrict__ slab, int dbg) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1222,9 +1222,11 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
     for (int k = 0; k < 4; ++k) glds16(src + 1024 * k, dst + 1024 * k);
   };
 
-  float ssum[8], ssq[8];
+  // BN statistics per channel as (even, odd) pixel pairs: packed adds / FMAs, one instruction
+  // per value for the sum and the sum of squares together
+  f32x2 ssum[8], ssq[8];
 #pragma unroll
-  for (int nj = 0; nj < 8; ++nj) ssum[nj] = ssq[nj] = 0.f;
+  for (int nj = 0; nj < 8; ++nj) ssum[nj] = ssq[nj] = f32x2{0.f, 0.f};
 
   // static priority for the second-dispatched half of the workgroup (the arbitration loser of
   // every step with two waves per SIMD; MI355X_MICROARCH "two waves per SIMD", item 4)
@@ -1251,7 +1253,8 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 
 #pragma unroll 1
     for (int st = 0; st < C3_STEPS; ++st) {
-      if (st + 1 < C3_STEPS)
+      if (dbg & 1) {  // RGBD_C5_DBG bit 1: no weight DMA in the loop (timing experiments only)
+      } else if (st + 1 < C3_STEPS)
         issue_b(st + 1);
       else if (has_next)
         issue_b(0);
@@ -1289,11 +1292,14 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
       }
       // own DMA landed (except the A piece just issued), own LDS reads done, then the barrier
-      if (a_issued)
+      if (dbg & 2)  // RGBD_C5_DBG bit 2: no DMA wait (timing experiments only)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (a_issued)
         asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    if (dbg & 4) continue;  // RGBD_C5_DBG bit 4: no epilogue
     // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
     // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
     bf16_t* yt = y + (((tile * 8 + wave) * 4) * 4) * 512;  // [mi][nj/2][lane][8]
@@ -1302,27 +1308,22 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
     for (int np = 0; np < 4; ++np) {
       const float b0 = sbias[wn * 128 + 32 * np + r], b1 = sbias[wn * 128 + 32 * np + 16 + r];
       if (interior) {
-        // every tile at 640x480: no bounds selects; per 4 values one packed bias add pair, two
-        // packed conversions, and (sum, sum of squares) as one packed FMA each
-        f32x2 s0 = {ssum[2 * np], ssq[2 * np]}, s1 = {ssum[2 * np + 1], ssq[2 * np + 1]};
+        // every tile at 640x480: no bounds selects; per pixel pair one packed bias add, one packed
+        // conversion, one packed add (sum) and one packed FMA (sum of squares)
+        const f32x2 bb0 = {b0, b0}, bb1 = {b1, b1};
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
           const f32x4 v = acc[mi][2 * np], w = acc[mi][2 * np + 1];
-          const float a[4] = {v[0] + b0, v[1] + b0, v[2] + b0, v[3] + b0};
-          const float c[4] = {w[0] + b1, w[1] + b1, w[2] + b1, w[3] + b1};
-          *reinterpret_cast<uint4*>(yt + ((mi * 4 + np) * 64 + lane) * 8) =
-              make_uint4(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(c[0], c[1]),
-                         pack_bf16x2(c[2], c[3]));
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s0 = __builtin_elementwise_fma(f32x2{a[j], a[j]}, f32x2{1.f, a[j]}, s0);
-            s1 = __builtin_elementwise_fma(f32x2{c[j], c[j]}, f32x2{1.f, c[j]}, s1);
-          }
+          const f32x2 a0 = f32x2{v[0], v[1]} + bb0, a1 = f32x2{v[2], v[3]} + bb0;
+          const f32x2 c0 = f32x2{w[0], w[1]} + bb1, c1 = f32x2{w[2], w[3]} + bb1;
+          const u32x4 pk = {pack_bf16x2(a0.x, a0.y), pack_bf16x2(a1.x, a1.y), pack_bf16x2(c0.x, c0.y),
+                            pack_bf16x2(c1.x, c1.y)};
+          __builtin_nontemporal_store(pk, reinterpret_cast<u32x4*>(yt + ((mi * 4 + np) * 64 + lane) * 8));
+          ssum[2 * np] += a0 + a1;
+          ssq[2 * np] = __builtin_elementwise_fma(a0, a0, __builtin_elementwise_fma(a1, a1, ssq[2 * np]));
+          ssum[2 * np + 1] += c0 + c1;
+          ssq[2 * np + 1] = __builtin_elementwise_fma(c0, c0, __builtin_elementwise_fma(c1, c1, ssq[2 * np + 1]));
         }
-        ssum[2 * np] = s0.x;
-        ssq[2 * np] = s0.y;
-        ssum[2 * np + 1] = s1.x;
-        ssq[2 * np + 1] = s1.y;
       } else {
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
@@ -1338,8 +1339,8 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
               const float av = acc[mi][nj][j] + bias;
               hv[4 * h + j] = (uint32_t)f32_to_bf16(av);
               if (row_ok && xb + j < W) {
-                ssum[nj] += av;
-                ssq[nj] = __builtin_fmaf(av, av, ssq[nj]);
+                ssum[nj].x += av;
+                ssq[nj].x = __builtin_fmaf(av, av, ssq[nj].x);
               }
             }
           }
@@ -1355,7 +1356,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   float* red = (float*)smem;  // [4 wm][256 n][2]
 #pragma unroll
   for (int nj = 0; nj < 8; ++nj) {
-    float a = ssum[nj], q = ssq[nj];
+    float a = ssum[nj].x + ssum[nj].y, q = ssq[nj].x + ssq[nj].y;
     a += __shfl_xor(a, 16);
     a += __shfl_xor(a, 32);
     q += __shfl_xor(q, 16);
@@ -1857,7 +1858,8 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
           (const void*)k_rp_conv3x3_v3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       if (attr != hipSuccess) return (int)attr;
       gcv = conv3_grid(B, H, W);
-      k_rp_conv3x3_v3<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+      static const int c5dbg = getenv("RGBD_C5_DBG") ? atoi(getenv("RGBD_C5_DBG")) : 0;
+      k_rp_conv3x3_v3<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab, c5dbg);
     } else {
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
