@@ -202,6 +202,38 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
                          int w, int Cout, float* dconv_w, float* dproj_w, float* dbias, void* ws,
                          void* stream);
 
+/* Planning ahead (RGBD_BF16).  What a bf16 leg sets up before its GEMM (per-tile code sets and
+ * the work list of a forward / dX leg; per-code live units, items and tap masks of a dW leg)
+ * depends only on the region codes, so a caller may plan every leg of a step at once, right
+ * after rgbd_edsam_decompose (two launches for all forward / dX legs), and run the legs later
+ * with the _planned entry points: same arguments as the plain ones plus the leg's plan buffer,
+ * and ws then needs only rgbd_dsam_run_workspace_size bytes (split-K / dW partials, which legs
+ * run one after another on one stream may share).  Results are bitwise those of the plain
+ * entry points.  A plan buffer serves one run of one leg (the run uses up its work counters):
+ * plan again before running the leg again, and leave the buffer untouched until the leg ran. */
+enum { RGBD_LEG_FWD = 0, RGBD_LEG_DX = 1, RGBD_LEG_DW = 2 };
+typedef struct rgbd_dsam_leg {
+  int kind;                /* RGBD_LEG_* */
+  const uint8_t* code;     /* the DSAM's region codes [B][h][w] (device) */
+  int B, Cin, h, w, Cout;  /* the DSAModule's shape; h x w = its input resolution */
+  void* plan;              /* rgbd_dsam_plan_size bytes (device), OVERWRITTEN */
+} rgbd_dsam_leg;
+size_t rgbd_dsam_plan_size(int kind, int B, int Cin, int h, int w, int Cout);
+size_t rgbd_dsam_run_workspace_size(int kind, int B, int Cin, int h, int w, int Cout);
+int rgbd_dsam_plan(int n, const rgbd_dsam_leg* legs, void* stream);  /* legs: host array */
+int rgbd_dsam_fwd_nhwc_planned(int dtype, const void* x_nhwc, const uint8_t* code,
+                               const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
+                               const void* wfwd, const float* bias, const void* residual_nhwc,
+                               void* out_nhwc, const void* plan, void* ws, void* stream);
+int rgbd_dsam_bwd_data_planned(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin,
+                               int h, int w, int Cout, const void* wbwd, const void* gin_nchw,
+                               const void* gin_nhwc, void* dx_nchw, void* dx_nhwc, const void* plan,
+                               void* ws, void* stream);
+int rgbd_dsam_bwd_weight_planned(int dtype, const void* gout_nchw, const void* gout_nhwc,
+                                 const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                                 int B, int Cin, int h, int w, int Cout, float* dconv_w, float* dproj_w,
+                                 float* dbias, const void* plan, void* ws, void* stream);
+
 /* ---------------------------------------------------------------- K4 ratio predictor
  * EnhancedDepthImageRatioPredictor.forward (custom_model.py:1444-1487) for the batch:
  * depth3 (float32 planes as for the decomposition) -> ratio float32 [B] in [0.01, 0.5],

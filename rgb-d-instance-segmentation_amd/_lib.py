@@ -58,6 +58,12 @@ SIGNATURES = {
     "rgbd_dsam_bwd_data": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_weight_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rgbd_dsam_bwd_weight": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "rgbd_dsam_plan_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
+    "rgbd_dsam_run_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
+    "rgbd_dsam_plan": (_I, [_I, _P, _P]),
+    "rgbd_dsam_fwd_nhwc_planned": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "rgbd_dsam_bwd_data_planned": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rgbd_dsam_bwd_weight_planned": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_msda_fwd": (_I, [_I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rgbd_msda_bwd": (_I, [_I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "rgbd_lsa_lds_bytes": (_SZ, [_I, _I]),

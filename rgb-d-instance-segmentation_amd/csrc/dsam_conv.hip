@@ -43,7 +43,7 @@ struct ConvArgs {
   void* out_nchw;                   // optional
   void* out_nhwc;                   // optional
   int ksplit;                       // unused (1)
-  int dbg;                          // diagnostics (RGBD_DSAM_DBG): 1 skip steps, 2 epilogue, 4 hand-off
+  int dbg;                          // diagnostics (RGBD_DSAM_DBG): 1 skip steps, 2 epilogue, 4 hand-off, 8 loop DMA
   uint16_t* tmasks;                 // bf16: [class][tile][16] per-tap code sets (k_dsam_plan)
   int* items;                       // bf16: work list of k_dsam_lds (k_dsam_items)
   int* nitems;
@@ -51,6 +51,9 @@ struct ConvArgs {
   int* work;                        // bf16: per N tile next-item counter of k_dsam_lds, zeroed by k_dsam_plan
   int ntiles0;                      // bf16: tiles of the largest class
   int chunk_len;                    // bf16: steps per workgroup chunk of a tile
+  int ncg;                          // bf16: K chunk groups per tap (C / (32 * KC))
+  int linear;                       // bf16: tile rows = 128 consecutive pixels of the (class) grid
+                                    // over the batch instead of 8 x 16 blocks (small grids)
   float* partial;                   // bf16: partial tiles of multi-chunk tiles (reduced by their last chunk)
   const bf16_t* zero;               // bf16: LD_ZERO_BYTES of zeros (zeroed by k_dsam_plan)
 };
@@ -1033,7 +1036,7 @@ __device__ __forceinline__ LdGeom ld_geom(const ConvArgs& a, int cls) {
   G.ntap = G.nyl * G.nxl;
   G.tiles_x = (G.Wc + 15) >> 4;
   G.tiles_y = (G.Hc + 7) >> 3;
-  G.ntiles = a.B * G.tiles_x * G.tiles_y;
+  G.ntiles = a.linear ? (int)(((long long)a.B * G.Hc * G.Wc + LD_BM - 1) / LD_BM) : a.B * G.tiles_x * G.tiles_y;
   return G;
 }
 // live tap t of the class -> kernel tap (ky, kx) and source offset (dy, dx) from the row origin
@@ -1054,9 +1057,19 @@ __device__ __forceinline__ void ld_tap(const ConvArgs& a, const LdGeom& G, int t
 // the row exists; org = origin pixel of its taps, rv = in-bounds taps, lo/hi = 4-bit code per tap.
 __device__ __forceinline__ bool ld_row(const ConvArgs& a, const LdGeom& G, int tile, int ml, int& b, int& i,
                                        int& j, int& org, uint32_t& rv, uint32_t& lo, uint32_t& hi) {
-  b = tile / (G.tiles_x * G.tiles_y);
-  const int trem = tile - b * G.tiles_x * G.tiles_y;
-  const int iq = (trem / G.tiles_x) * 8 + (ml >> 4), jq = (trem % G.tiles_x) * 16 + (ml & 15);
+  int iq, jq;
+  if (a.linear) {  // row ml = pixel tile * 128 + ml of the batch's (class) grid
+    const int hw = G.Hc * G.Wc, m = tile * LD_BM + ml;
+    b = m / hw;
+    const int rem = m - b * hw;
+    iq = rem / G.Wc;
+    jq = rem - iq * G.Wc;
+  } else {
+    b = tile / (G.tiles_x * G.tiles_y);
+    const int trem = tile - b * G.tiles_x * G.tiles_y;
+    iq = (trem / G.tiles_x) * 8 + (ml >> 4);
+    jq = (trem % G.tiles_x) * 16 + (ml & 15);
+  }
   const bool mv = b < a.B && iq < G.Hc && jq < G.Wc;
   b = mv ? b : 0;
   i = mv ? iq : 0;
@@ -1106,9 +1119,9 @@ __device__ __forceinline__ int ld_nchunks(int steps, int len) {
 
 // Plan: per (class, tile) the set of region codes the tile's rows meet at each live tap,
 // tmasks[(cls * ntiles0 + tile) * 16 + t] (u16).  One 128-thread workgroup per tile.
-__global__ __launch_bounds__(128) void k_dsam_plan(ConvArgs a, int ntiles0, int ntn) {
+__device__ __forceinline__ void plan_tile(const ConvArgs& a, int cls, int tile, int ntn) {
   __shared__ uint32_t tm_s[9];
-  const int cls = blockIdx.z, tile = blockIdx.x, tid = threadIdx.x;
+  const int ntiles0 = a.ntiles0, tid = threadIdx.x;
   const LdGeom G = ld_geom(a, cls);
   if (tile >= G.ntiles) return;
   if (tid < 9) tm_s[tid] = 0u;
@@ -1141,13 +1154,30 @@ __global__ __launch_bounds__(128) void k_dsam_plan(ConvArgs a, int ntiles0, int 
   if (cls == 0 && tile == 0 && tid < ntn) a.work[tid] = 0;
 }
 
+// Several conv legs planned by one launch (the forward cascade's three DSAMs and the two dX
+// legs, right after the decomposition): blockIdx.z runs over (leg, class), blockIdx.x over tiles.
+constexpr int PLAN_MAXLEG = 8;
+struct PlanLegs {
+  ConvArgs a[PLAN_MAXLEG];
+  int zb[PLAN_MAXLEG + 1];  // first z of each leg
+  int ntn[PLAN_MAXLEG];
+  int n;
+};
+__global__ __launch_bounds__(128) void k_dsam_plan(const PlanLegs L) {
+  const int z = blockIdx.z;
+  int leg = 0;
+  while (leg + 1 < L.n && z >= L.zb[leg + 1]) ++leg;
+  plan_tile(L.a[leg], z - L.zb[leg], blockIdx.x, L.ntn[leg]);
+}
+
 // Work list: per (class, tile) the chunk count, compacted into items (cls | chunk << 2 |
 // tile << 5) in (class, tile, chunk) order by one workgroup; a[*nitems] = count.  dX lists the
 // parity classes by decreasing live-tap count (3: 4 taps, 1 and 2: 2, 0: 1), so the longest
 // items are taken first under the dynamic assignment.
-__global__ __launch_bounds__(1024) void k_dsam_items(ConvArgs a, int ntiles0, int ncg) {
+__device__ __forceinline__ void items_body(const ConvArgs& a) {
   __shared__ int wsum[16];
   __shared__ int base_s;
+  const int ntiles0 = a.ntiles0, ncg = a.ncg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nclass = a.transposed ? 4 : 1, total = nclass * ntiles0;
   if (tid == 0) base_s = 0;
@@ -1185,6 +1215,7 @@ __global__ __launch_bounds__(1024) void k_dsam_items(ConvArgs a, int ntiles0, in
   }
   if (tid == 0) *a.nitems = base_s;
 }
+__global__ __launch_bounds__(1024) void k_dsam_items(const PlanLegs L) { items_body(L.a[blockIdx.x]); }
 
 // One (tile, chunk) item of k_dsam_lds for N tile ntile (of ntn).
 template <int KC>
@@ -1308,7 +1339,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   else vm_wait_barrier<0>();
 #pragma unroll 1
   for (int s = 0; s < nst; ++s) {
-    if (s + S - 1 < nst) issue((s + S - 1) % S, s0 + s + S - 1);
+    if (s + S - 1 < nst && !(a.dbg & 8)) issue((s + S - 1) % S, s0 + s + S - 1);  // bit 8: no DMA in the loop
     const char* sa = smem + (s % S) * Cfg::STAGE;
     // fragments of chunk kc+1 are read while chunk kc's 12 MFMAs run
     Frag<bf16_t> fa[2][4], fb[2][3];
@@ -1583,15 +1614,24 @@ int ld_kc(int C) {
   return C % 96 == 0 ? 3 : (C % 64 == 0 ? 2 : 1);
 }
 // k_dsam_lds tiling of a conv: tiles of the largest parity class, N tiles
+// Linear tiles when 8 x 16 blocks would leave more than 15 % of the rows dead (the small grids:
+// dsam1 / dsam2 outputs, their dX parity classes); RGBD_DSAM_LINEAR=0/1 forces (A/B)
+int ld_linear(int Hc, int Wc) {
+  static const int force = env_int("RGBD_DSAM_LINEAR", -1);
+  if (force >= 0) return force;
+  const long long blk = (long long)((Hc + 7) / 8 * 8) * ((Wc + 15) / 16 * 16);
+  return (long long)Hc * Wc * 100 < 85 * blk;
+}
 struct LdPlan {
-  int ntiles0, ntn, kc, chunk_len;
+  int ntiles0, ntn, kc, chunk_len, linear;
   size_t tmask_bytes, items_bytes, ticket_bytes, partial_bytes;
 };
 LdPlan ld_plan(const ConvArgs& a) {
   LdPlan p;
   const int Hc0 = a.transposed ? (a.Ho + 1) / 2 : a.Ho, Wc0 = a.transposed ? (a.Wo + 1) / 2 : a.Wo;
   const int nclass = a.transposed ? 4 : 1;
-  p.ntiles0 = a.B * ((Hc0 + 7) / 8) * ((Wc0 + 15) / 16);
+  p.linear = ld_linear(Hc0, Wc0);
+  p.ntiles0 = p.linear ? (int)(((long long)a.B * Hc0 * Wc0 + LD_BM - 1) / LD_BM) : a.B * ((Hc0 + 7) / 8) * ((Wc0 + 15) / 16);
   p.ntn = ceil_div(a.N, LD_BN);
   p.kc = ld_kc(a.C);
   // chunk length in steps: pct % of a dense tile (one code per tap); tuning override
@@ -1604,9 +1644,51 @@ LdPlan ld_plan(const ConvArgs& a) {
   p.partial_bytes = align256((size_t)nclass * p.ntiles0 * p.ntn * LD_CH * LD_BN * LD_BM * sizeof(float));
   return p;
 }
+size_t ld_plan_bytes(const LdPlan& p) { return p.tmask_bytes + p.items_bytes + p.ticket_bytes; }
 size_t v2_partial_bytes(const ConvArgs& a) {
   const LdPlan p = ld_plan(a);
-  return p.tmask_bytes + p.items_bytes + p.ticket_bytes + p.partial_bytes;
+  return ld_plan_bytes(p) + p.partial_bytes;
+}
+// The bf16 launch arguments of a conv leg over its plan buffer [code sets | work list | tickets,
+// counters, zero row] (ld_plan_bytes) and its partial-tile buffer (P.partial_bytes).
+ConvArgs conv_carve(const ConvArgs& a, const LdPlan& P, char* plan, float* partial) {
+  ConvArgs b = a;
+  const int nclass = a.transposed ? 4 : 1;
+  static const int dbg = env_int("RGBD_DSAM_DBG", 0);
+  b.dbg = dbg;
+  b.tmasks = (uint16_t*)plan;
+  b.items = (int*)(plan + P.tmask_bytes);
+  b.nitems = b.items + (size_t)nclass * P.ntiles0 * LD_CH;
+  b.tickets = (int*)(plan + P.tmask_bytes + P.items_bytes);
+  b.work = b.tickets + (size_t)nclass * P.ntiles0 * P.ntn;
+  b.zero = (const bf16_t*)(plan + ld_plan_bytes(P) - LD_ZERO_BYTES);  // the ticket region's tail
+  b.partial = partial;
+  b.ntiles0 = P.ntiles0;
+  b.chunk_len = P.chunk_len;
+  b.ncg = a.C / (32 * P.kc);
+  b.linear = P.linear;
+  return b;
+}
+bool conv_shape_ok(const ConvArgs& a, const LdPlan& P) {
+  return a.C % 32 == 0 && a.N % 32 == 0 && (long long)a.B * a.Hi * a.Wi < (1ll << 31) && conv_mmax(a) < (1ll << 31) &&
+         P.ntn <= 64 && 9 * 16 * (a.C / (32 * P.kc)) <= LD_MAXSTEP;
+}
+// plan + work list of n conv legs (two launches)
+hipError_t plan_convs(int n, const ConvArgs* legs, hipStream_t s) {
+  PlanLegs L = {};
+  L.n = n;
+  int z = 0, mt = 1;
+  for (int i = 0; i < n; ++i) {
+    L.a[i] = legs[i];
+    L.zb[i] = z;
+    L.ntn[i] = ceil_div(legs[i].N, LD_BN);
+    z += legs[i].transposed ? 4 : 1;
+    mt = std::max(mt, legs[i].ntiles0);
+  }
+  L.zb[n] = z;
+  k_dsam_plan<<<dim3(mt, 1, z), 128, 0, s>>>(L);
+  k_dsam_items<<<n, 1024, 0, s>>>(L);
+  return hipGetLastError();
 }
 
 template <int KC>
@@ -1615,36 +1697,27 @@ hipError_t launch_ld(const ConvArgs& b, dim3 grid, hipStream_t s) {
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      (int)LdCfg<KC>::SMEM);
   if (attr != hipSuccess) return attr;
-  k_dsam_items<<<1, 1024, 0, s>>>(b, b.ntiles0, b.C / (32 * KC));
   k_dsam_lds<KC><<<grid, 512, LdCfg<KC>::SMEM, s>>>(b);
   return hipSuccess;
 }
 
 template <typename T>
-int launch_conv(const ConvArgs& a, hipStream_t s) {
+int launch_conv(const ConvArgs& a, hipStream_t s, const void* planned = nullptr) {
   TimerScope ts(a.transposed ? "dsam_dx" : "dsam_fwd", s);
   int nclass = a.transposed ? 4 : 1;
   const long long Mmax = conv_mmax(a);
   if constexpr (sizeof(T) == 2) {
-    RGBD_REQUIRE(a.C % 32 == 0 && a.N % 32 == 0, RGBD_E_SHAPE);  // code-merged bf16 path only
-    RGBD_REQUIRE((long long)a.B * a.Hi * a.Wi < (1ll << 31) && Mmax < (1ll << 31), RGBD_E_SHAPE);
-    ConvArgs b = a;
-    static const int dbg = env_int("RGBD_DSAM_DBG", 0);
-    b.dbg = dbg;
+    // code-merged bf16 path: the plan (unless the caller planned this leg ahead with
+    // rgbd_dsam_plan) into the head of the workspace, then the persistent kernel
     const LdPlan P = ld_plan(a);
-    // workspace: [per-tile code sets | partial tiles of multi-chunk tiles]
-    b.tmasks = (uint16_t*)a.partial;
-    b.items = (int*)((char*)a.partial + P.tmask_bytes);
-    b.nitems = b.items + (size_t)nclass * P.ntiles0 * LD_CH;
-    b.tickets = (int*)((char*)a.partial + P.tmask_bytes + P.items_bytes);
-    b.work = b.tickets + (size_t)nclass * P.ntiles0 * P.ntn;
-    RGBD_REQUIRE(P.ntn <= 64, RGBD_E_SHAPE);
-    b.partial = (float*)((char*)a.partial + P.tmask_bytes + P.items_bytes + P.ticket_bytes);
-    b.zero = (const bf16_t*)((char*)b.partial - LD_ZERO_BYTES);  // the ticket region's tail
-    RGBD_REQUIRE(9 * 16 * (a.C / (32 * P.kc)) <= LD_MAXSTEP, RGBD_E_SHAPE);
-    b.ntiles0 = P.ntiles0;
-    b.chunk_len = P.chunk_len;
-    k_dsam_plan<<<dim3(P.ntiles0, 1, nclass), 128, 0, s>>>(b, P.ntiles0, P.ntn);
+    RGBD_REQUIRE(conv_shape_ok(a, P), RGBD_E_SHAPE);
+    char* plan = planned ? (char*)planned : (char*)a.partial;
+    float* partial = planned ? a.partial : (float*)((char*)a.partial + ld_plan_bytes(P));
+    const ConvArgs b = conv_carve(a, P, plan, partial);
+    if (!planned) {
+      const hipError_t pe = plan_convs(1, &b, s);
+      if (pe != hipSuccess) return (int)pe;
+    }
     // persistent: about one workgroup per CU (LDS-bound) over all N tiles
     static const int pers = env_int("RGBD_DSAM_PERSIST", 256);
     dim3 grid2(std::max(1, pers / P.ntn), P.ntn, 1);
@@ -1821,9 +1894,9 @@ int rgbd_dsam_fwd(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd
   return RGBD_E_DTYPE;
 }
 
-int rgbd_dsam_fwd_nhwc(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
-                       int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
-                       const void* residual_nhwc, void* out_nhwc, void* ws, void* stream) {
+static int fwd_nhwc(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info, int B,
+                    int Cin, int h, int w, int Cout, const void* wfwd, const float* bias, const void* residual_nhwc,
+                    void* out_nhwc, const void* planned, void* ws, void* stream) {
   RGBD_REQUIRE(dtype == RGBD_BF16, RGBD_E_DTYPE);
   RGBD_REQUIRE(x_nhwc && code && info && wfwd && bias && out_nhwc && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
@@ -1831,12 +1904,26 @@ int rgbd_dsam_fwd_nhwc(int dtype, const void* x_nhwc, const uint8_t* code, const
   a.x = x_nhwc; a.code = code; a.w = wfwd;
   a.bias4 = bias; a.info = info; a.residual_nhwc = residual_nhwc; a.out_nhwc = out_nhwc;
   a.partial = (float*)ws;
-  return launch_conv<bf16_t>(a, (hipStream_t)stream);
+  return launch_conv<bf16_t>(a, (hipStream_t)stream, planned);
+}
+int rgbd_dsam_fwd_nhwc(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                       int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
+                       const void* residual_nhwc, void* out_nhwc, void* ws, void* stream) {
+  return fwd_nhwc(dtype, x_nhwc, code, info, B, Cin, h, w, Cout, wfwd, bias, residual_nhwc, out_nhwc, nullptr, ws,
+                  stream);
+}
+int rgbd_dsam_fwd_nhwc_planned(int dtype, const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
+                               int B, int Cin, int h, int w, int Cout, const void* wfwd, const float* bias,
+                               const void* residual_nhwc, void* out_nhwc, const void* plan, void* ws, void* stream) {
+  RGBD_REQUIRE(plan, RGBD_E_ARG);
+  return fwd_nhwc(dtype, x_nhwc, code, info, B, Cin, h, w, Cout, wfwd, bias, residual_nhwc, out_nhwc, plan, ws,
+                  stream);
 }
 
-int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
-                       int w, int Cout, const void* wbwd, const void* gin_nchw, const void* gin_nhwc,
-                       void* dx_nchw, void* dx_nhwc, void* ws, void* stream) {
+static int bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h, int w, int Cout,
+                    const void* wbwd, const void* gin_nchw, const void* gin_nhwc, void* dx_nchw, void* dx_nhwc,
+                    const void* planned, void* ws, void* stream) {
+  RGBD_REQUIRE(!planned || dtype == RGBD_BF16, RGBD_E_DTYPE);
   RGBD_REQUIRE(gout_nhwc && code && wbwd && (dx_nchw || dx_nhwc), RGBD_E_ARG);
   // the residual comes in the layout of the pass that adds it: NCHW with an NCHW output, NHWC
   // (bf16 only) without one
@@ -1851,14 +1938,28 @@ int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, in
   RGBD_REQUIRE(ws || dtype != RGBD_BF16, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32) return launch_conv<float>(a, s);
-  if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s);
+  if (dtype == RGBD_BF16) return launch_conv<bf16_t>(a, s, planned);
   return RGBD_E_DTYPE;
 }
+int rgbd_dsam_bwd_data(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
+                       int w, int Cout, const void* wbwd, const void* gin_nchw, const void* gin_nhwc,
+                       void* dx_nchw, void* dx_nhwc, void* ws, void* stream) {
+  return bwd_data(dtype, gout_nhwc, code, B, Cin, h, w, Cout, wbwd, gin_nchw, gin_nhwc, dx_nchw, dx_nhwc, nullptr, ws,
+                  stream);
+}
+int rgbd_dsam_bwd_data_planned(int dtype, const void* gout_nhwc, const uint8_t* code, int B, int Cin, int h,
+                               int w, int Cout, const void* wbwd, const void* gin_nchw, const void* gin_nhwc,
+                               void* dx_nchw, void* dx_nhwc, const void* plan, void* ws, void* stream) {
+  RGBD_REQUIRE(plan, RGBD_E_ARG);
+  return bwd_data(dtype, gout_nhwc, code, B, Cin, h, w, Cout, wbwd, gin_nchw, gin_nhwc, dx_nchw, dx_nhwc, plan, ws,
+                  stream);
+}
 
-// bf16 workspace: [splits][16 codes][Cout][9 Cin] f32 partials | [B] f32 x Cout channel sums |
-// presence table [B][chunks] u16 | global code mask u32
+// bf16 workspace: the plan part [presence table [B][units] u16 | live entry list | their tap
+// masks | items | counters | zero row] (plan_total bytes; rgbd_dsam_plan can fill it ahead),
+// then [items][Cout][9 Cin] f32 partials | channel sums
 struct WgradWs {
-  size_t partial, csum, pres, gmask, list, masks, items, counts, zero, total;
+  size_t pres, gmask, list, masks, items, counts, zero, plan_total, partial, csum, total;
 };
 static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   WgradWs o;
@@ -1873,10 +1974,6 @@ static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   } else {
     part = (size_t)dsam_wgrad_splits(B, Cin, Cout) * Cout * 45 * Cin;
   }
-  o.partial = off;
-  off += align256(sizeof(float) * part);
-  o.csum = off;
-  off += align256(sizeof(float) * (size_t)CS_SPLIT_MAX * B * Cout);
   o.pres = off;
   off += align256(sizeof(uint16_t) * npres);
   o.gmask = off;
@@ -1891,8 +1988,51 @@ static WgradWs wgrad_ws(int dtype, int B, int Cin, int h, int w, int Cout) {
   off += 256;
   o.zero = off;
   off += LD_ZERO_BYTES;
+  o.plan_total = off;
+  o.partial = off;
+  off += align256(sizeof(float) * part);
+  o.csum = off;
+  off += align256(sizeof(float) * (size_t)CS_SPLIT_MAX * B * Cout);
   o.total = off;
   return o;
+}
+
+// dW launch arguments over a plan part (wgrad_ws offsets below plan_total) and the partials
+static WgArgs wg_args(const WgradWs& L, const WgPlan& P, char* plan, float* partial, const void* gout_nhwc,
+                      const void* x_nhwc, const uint8_t* code, int B, int Cin, int h, int w, int Cout) {
+  WgArgs a;
+  a.gout = (const bf16_t*)gout_nhwc;
+  a.x = (const bf16_t*)x_nhwc;
+  a.code = code;
+  a.pres = (uint16_t*)(plan + L.pres);
+  a.list = (int*)(plan + L.list);
+  a.masks = (unsigned long long*)(plan + L.masks);
+  a.items = (int4*)(plan + L.items);
+  a.counts = (int*)(plan + L.counts);
+  a.B = B; a.Cin = Cin; a.h = h; a.w = w; a.Cout = Cout;
+  a.ho = (h + 1) / 2; a.wo = (w + 1) / 2;
+  a.nunit = P.nunit;
+  a.ntile_kk = P.ntile_kk;
+  a.ntile_o = P.ntile_o;
+  a.target = wg_target(P);
+  a.inv_wo = 1.0f / (float)a.wo;
+  a.zero = (const bf16_t*)(plan + L.zero);
+  a.partial = partial;
+  static const int wdbg = env_int("RGBD_WG_DBG", 0);
+  a.dbg = wdbg;
+  return a;
+}
+static bool wg_shape_ok(int B, int Cin, int h, int w, int Cout, const WgPlan& P) {
+  const long long hwo = (long long)((h + 1) / 2) * ((w + 1) / 2);
+  return Cin % 32 == 0 && Cout % 32 == 0 && hwo < (1ll << 22) && (long long)B * h * w < (1ll << 31) &&
+         (long long)B * P.nunit < (1 << 24);
+}
+// the code-dependent part of a dW leg: unit presence, the per-code live lists and items, tap masks
+static void wg_plan_launch(const WgArgs& a, const WgPlan& P, hipStream_t s) {
+  const long long nthr = (long long)a.B * P.nunit * 64;
+  k_code_presence<<<(int)ceil_div(nthr, 256), 256, 0, s>>>(a.code, a.B, a.h, a.w, const_cast<uint16_t*>(a.pres));
+  k_wg_plan<<<1, 1024, 0, s>>>(a);
+  k_wg_masks<<<ceil_div((long long)P.max_entries, 4), 256, 0, s>>>(a);
 }
 
 size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout) {
@@ -1900,17 +2040,19 @@ size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int
   return wgrad_ws(dtype, B, Cin, h, w, Cout).total;
 }
 
-int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
-                         const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h, int w,
-                         int Cout, float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream) {
+static int bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
+                      const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
+                      float* dconv_w, float* dproj_w, float* dbias, const void* planned, void* ws, void* stream) {
   RGBD_REQUIRE((gout_nchw || dtype == RGBD_BF16) && x_nhwc && code && info && dconv_w && dproj_w && dbias && ws,
                RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && h > 0 && w > 0 && Cout > 0 && Cin > 0, RGBD_E_ARG);
   RGBD_REQUIRE(Cin % 8 == 0, RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
   const WgradWs L = wgrad_ws(dtype, B, Cin, h, w, Cout);
-  float* partial = (float*)((char*)ws + L.partial);
-  float* csum = (float*)((char*)ws + L.csum);
+  // planned ahead: ws holds only [partials | channel sums]
+  const size_t run0 = planned ? L.plan_total : 0;
+  float* partial = (float*)((char*)ws + L.partial - run0);
+  float* csum = (float*)((char*)ws + L.csum - run0);
   TimerScope ts("dsam_wgrad", s);
   const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo;
   if (dtype == RGBD_F32) {
@@ -1924,34 +2066,11 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
         partial, sp, Cin, Cout, dconv_w, dproj_w);
   } else if (dtype == RGBD_BF16) {
     RGBD_REQUIRE(gout_nhwc, RGBD_E_ARG);
-    RGBD_REQUIRE(Cin % 32 == 0 && Cout % 32 == 0, RGBD_E_SHAPE);
-    RGBD_REQUIRE((long long)hwo < (1ll << 22) && (long long)B * h * w < (1ll << 31), RGBD_E_SHAPE);
     const WgPlan P = wg_plan(B, Cin, h, w, Cout);
-    RGBD_REQUIRE((long long)B * P.nunit < (1 << 24), RGBD_E_SHAPE);
-    uint16_t* pres = (uint16_t*)((char*)ws + L.pres);
-    const long long nthr = (long long)B * P.nunit * 64;
-    k_code_presence<<<(int)ceil_div(nthr, 256), 256, 0, s>>>(code, B, h, w, pres);
-    WgArgs a;
-    a.gout = (const bf16_t*)gout_nhwc;
-    a.x = (const bf16_t*)x_nhwc;
-    a.code = code;
-    a.pres = pres;
-    a.list = (int*)((char*)ws + L.list);
-    a.masks = (unsigned long long*)((char*)ws + L.masks);
-    a.items = (int4*)((char*)ws + L.items);
-    a.counts = (int*)((char*)ws + L.counts);
-    a.B = B; a.Cin = Cin; a.h = h; a.w = w; a.Cout = Cout; a.ho = ho; a.wo = wo;
-    a.nunit = P.nunit;
-    a.ntile_kk = P.ntile_kk;
-    a.ntile_o = P.ntile_o;
-    a.target = wg_target(P);
-    a.inv_wo = 1.0f / (float)wo;
-    a.zero = (const bf16_t*)((char*)ws + L.zero);
-    a.partial = partial;
-    static const int wdbg = env_int("RGBD_WG_DBG", 0);
-    a.dbg = wdbg;
-    k_wg_plan<<<1, 1024, 0, s>>>(a);
-    k_wg_masks<<<ceil_div((long long)P.max_entries, 4), 256, 0, s>>>(a);
+    RGBD_REQUIRE(wg_shape_ok(B, Cin, h, w, Cout, P), RGBD_E_SHAPE);
+    char* plan = planned ? (char*)planned : (char*)ws;
+    const WgArgs a = wg_args(L, P, plan, partial, gout_nhwc, x_nhwc, code, B, Cin, h, w, Cout);
+    if (!planned) wg_plan_launch(a, P, s);
     const int grid = 256;  // persistent: one LDS-bound workgroup per CU
     const hipError_t e = P.fm == 6 ? launch_wg<6>(a, grid, s) : P.fm == 4 ? launch_wg<4>(a, grid, s) : launch_wg<2>(a, grid, s);
     if (e != hipSuccess) return (int)e;
@@ -1976,6 +2095,77 @@ int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc
   }
   const int nsplit = (dtype == RGBD_BF16 && !gout_nchw) ? chan_sum_splits(hwo) : 1;
   k_dsam_bias_grad<<<Cout, 256, 0, s>>>(csum, info, B, Cout, nsplit, dbias);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_dsam_bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
+                         const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h, int w,
+                         int Cout, float* dconv_w, float* dproj_w, float* dbias, void* ws, void* stream) {
+  return bwd_weight(dtype, gout_nchw, gout_nhwc, x_nhwc, code, info, B, Cin, h, w, Cout, dconv_w, dproj_w, dbias,
+                    nullptr, ws, stream);
+}
+int rgbd_dsam_bwd_weight_planned(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
+                                 const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h, int w,
+                                 int Cout, float* dconv_w, float* dproj_w, float* dbias, const void* plan, void* ws,
+                                 void* stream) {
+  RGBD_REQUIRE(plan && dtype == RGBD_BF16, RGBD_E_ARG);
+  return bwd_weight(dtype, gout_nchw, gout_nhwc, x_nhwc, code, info, B, Cin, h, w, Cout, dconv_w, dproj_w, dbias,
+                    plan, ws, stream);
+}
+
+// ---- planning ahead (bf16): the code-dependent set-up of a leg depends only on the region codes,
+// so the hot path plans every leg of the step once, right after the decomposition
+static ConvArgs leg_conv_args(const rgbd_dsam_leg& g) {
+  ConvArgs a = g.kind == RGBD_LEG_FWD ? fwd_args(g.B, g.Cin, g.h, g.w, g.Cout) : dx_args(g.B, g.Cin, g.h, g.w, g.Cout);
+  a.code = g.code;
+  return a;
+}
+static bool leg_ok(const rgbd_dsam_leg& g) {
+  return (g.kind == RGBD_LEG_FWD || g.kind == RGBD_LEG_DX || g.kind == RGBD_LEG_DW) && g.B > 0 && g.h > 0 &&
+         g.w > 0 && g.Cin > 0 && g.Cout > 0;
+}
+size_t rgbd_dsam_plan_size(int kind, int B, int Cin, int h, int w, int Cout) {
+  const rgbd_dsam_leg g = {kind, nullptr, B, Cin, h, w, Cout, nullptr};
+  if (!leg_ok(g)) return 0;
+  if (kind == RGBD_LEG_DW) return wgrad_ws(RGBD_BF16, B, Cin, h, w, Cout).plan_total;
+  return ld_plan_bytes(ld_plan(leg_conv_args(g)));
+}
+size_t rgbd_dsam_run_workspace_size(int kind, int B, int Cin, int h, int w, int Cout) {
+  const rgbd_dsam_leg g = {kind, nullptr, B, Cin, h, w, Cout, nullptr};
+  if (!leg_ok(g)) return 0;
+  if (kind == RGBD_LEG_DW) {
+    const WgradWs L = wgrad_ws(RGBD_BF16, B, Cin, h, w, Cout);
+    return L.total - L.plan_total;
+  }
+  return std::max<size_t>(256, ld_plan(leg_conv_args(g)).partial_bytes);
+}
+int rgbd_dsam_plan(int n, const rgbd_dsam_leg* legs, void* stream) {
+  RGBD_REQUIRE(n > 0 && legs, RGBD_E_ARG);
+  hipStream_t s = (hipStream_t)stream;
+  ConvArgs conv[PLAN_MAXLEG];
+  int nconv = 0;
+  for (int i = 0; i < n; ++i) {
+    const rgbd_dsam_leg& g = legs[i];
+    RGBD_REQUIRE(leg_ok(g) && g.code && g.plan, RGBD_E_ARG);
+    if (g.kind == RGBD_LEG_DW) {
+      const WgPlan P = wg_plan(g.B, g.Cin, g.h, g.w, g.Cout);
+      RGBD_REQUIRE(wg_shape_ok(g.B, g.Cin, g.h, g.w, g.Cout, P), RGBD_E_SHAPE);
+      const WgradWs L = wgrad_ws(RGBD_BF16, g.B, g.Cin, g.h, g.w, g.Cout);
+      wg_plan_launch(wg_args(L, P, (char*)g.plan, nullptr, nullptr, nullptr, g.code, g.B, g.Cin, g.h, g.w, g.Cout), P,
+                     s);
+      continue;
+    }
+    RGBD_REQUIRE(nconv < PLAN_MAXLEG, RGBD_E_ARG);
+    const ConvArgs a = leg_conv_args(g);
+    const LdPlan P = ld_plan(a);
+    RGBD_REQUIRE(conv_shape_ok(a, P), RGBD_E_SHAPE);
+    conv[nconv++] = conv_carve(a, P, (char*)g.plan, nullptr);
+  }
+  if (nconv) {
+    const hipError_t e = plan_convs(nconv, conv, s);
+    if (e != hipSuccess) return (int)e;
+  }
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

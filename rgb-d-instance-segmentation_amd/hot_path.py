@@ -129,6 +129,15 @@ class HotPathFunction(torch.autograd.Function):
             cfg["status_sink"].append(ops.DeferredStatus(info))
         training = any(ctx.needs_input_grad[7:])
         masks = ops.dsam_code_masks(codes) if bf16 else None
+        chans = [(colors[k].shape[1], colors[k + 1].shape[1]) for k in range(3)]
+        conv_plans = dw_plans = None
+        if bf16:
+            # every leg's code-dependent set-up planned once, right after the decomposition: the
+            # forward and dX legs by two launches here, the dW legs on the side stream below
+            legs = [(ops.LEG_FWD, codes[k], *chans[k]) for k in range(3)]
+            if training:
+                legs += [(ops.LEG_DX, codes[k], *chans[k]) for k in (1, 2)]
+            conv_plans = ops.dsam_plan(legs)
 
         def pack(k):
             return cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
@@ -146,8 +155,12 @@ class HotPathFunction(torch.autograd.Function):
             for k in range(3):
                 if k == 1:
                     side.join()  # the dsam1 / dsam2 packs
+                    if training:  # dW plans beside the rest of the forward
+                        dw_plans = side.run(lambda: ops.dsam_plan([(ops.LEG_DW, codes[j], *chans[j]) for j in range(3)]),
+                                            *codes)
                 bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
-                out_nhwc = ops.dsam_fwd_nhwc(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual_nhwc=res_nhwc[k])
+                out_nhwc = ops.dsam_fwd_nhwc(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual_nhwc=res_nhwc[k],
+                                             plan=conv_plans[k])
                 cp1.append(out_nhwc)
                 if k < 2:
                     x_nhwc.append(out_nhwc)
@@ -165,7 +178,10 @@ class HotPathFunction(torch.autograd.Function):
             cp1_nhwc = ()
         # DGGM gate + final sum of all four scales in one launch
         outs = ops.dggm_fuse_fwd_multi(cp1, colors, pixel_values, dggm_p[0::2], dggm_p[1::2], cp1_nhwc=cp1_nhwc)
+        side.join()  # the dW plans
         ctx.cfg = cfg
+        ctx.dx_plans = {1: conv_plans[3], 2: conv_plans[4]} if conv_plans and training else {}
+        ctx.dw_plans = dw_plans
         ctx.codes = codes
         ctx.info = info
         ctx.x_nhwc = x_nhwc
@@ -207,7 +223,8 @@ class HotPathFunction(torch.autograd.Function):
         for k in (2, 1, 0):
             def dsam_dw(k=k, dcp=dcp, dcp_nhwc=dcp_nhwc):
                 dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k],
-                                                          ctx.info, gout_nhwc=dcp_nhwc)
+                                                          ctx.info, gout_nhwc=dcp_nhwc,
+                                                          plan=ctx.dw_plans[k] if ctx.dw_plans else None)
                 gk = []
                 for i in range(4):
                     gk += [dconv[i], dbias[i]]
@@ -223,7 +240,8 @@ class HotPathFunction(torch.autograd.Function):
             if k > 0:
                 if bf16:
                     dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], None, want_nhwc=True,
-                                                      want_nchw=False, gin_nhwc=ops.nchw_to_nhwc(G[k]))
+                                                      want_nchw=False, gin_nhwc=ops.nchw_to_nhwc(G[k]),
+                                                      plan=ctx.dx_plans.get(k))
                 else:
                     dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k], want_nhwc=(k > 1))
         pgrads = grads_dsam[0] + grads_dsam[1] + grads_dsam[2] + grads_dggm

@@ -309,6 +309,36 @@ def dsam_pack(conv_w: torch.Tensor, proj_w: torch.Tensor, dtype: torch.dtype, co
 
 
 # ------------------------------------------------------------------ K5 DSAM convs
+LEG_FWD, LEG_DX, LEG_DW = 0, 1, 2  # include/rgbd_hip.h RGBD_LEG_*
+
+
+class _Leg(ctypes.Structure):  # rgbd_dsam_leg
+    _fields_ = [("kind", ctypes.c_int), ("code", ctypes.c_void_p), ("B", ctypes.c_int), ("Cin", ctypes.c_int),
+                ("h", ctypes.c_int), ("w", ctypes.c_int), ("Cout", ctypes.c_int), ("plan", ctypes.c_void_p)]
+
+
+def dsam_plan(legs):
+    """Plan bfloat16 DSAM legs ahead (rgbd_dsam_plan): ``legs`` is a list of (kind, code [B,h,w]
+    uint8, Cin, Cout) with kind one of LEG_FWD / LEG_DX / LEG_DW; returns one plan buffer per
+    leg, to be passed as ``plan=`` to dsam_fwd_nhwc / dsam_bwd_data / dsam_bwd_weight.  All
+    forward / dX legs are planned by two launches together on the current stream."""
+    codes = [c for _, c, _, _ in legs]
+    _need_cuda(*codes)
+    L = _lib.lib()
+    arr = (_Leg * len(legs))()
+    plans = []
+    for i, (kind, code, ci, co) in enumerate(legs):
+        B, h, w = code.shape
+        nb = L.rgbd_dsam_plan_size(kind, B, ci, h, w, co)
+        if nb == 0:
+            raise ValueError(f"dsam_plan: bad leg {kind} {tuple(code.shape)} {ci}->{co}")
+        p = torch.empty((nb,), dtype=torch.uint8, device=code.device)
+        plans.append(p)
+        arr[i] = _Leg(kind, code.data_ptr(), B, ci, h, w, co, p.data_ptr())
+    check(L.rgbd_dsam_plan(len(legs), arr, _stream(codes[0].device)), "rgbd_dsam_plan")
+    return plans
+
+
 def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     """x_nhwc [B,h,w,Ci] -> (out_nchw [B,Co,ho,wo], out_nhwc or None)."""
     _need_cuda(x_nhwc, code, info, wfwd, bias4, residual)
@@ -330,10 +360,10 @@ def dsam_fwd(x_nhwc, code, info, wfwd, bias4, residual=None, want_nhwc=False):
     return out, out_nhwc
 
 
-def dsam_fwd_nhwc(x_nhwc, code, info, wfwd, bias4, residual_nhwc=None):
+def dsam_fwd_nhwc(x_nhwc, code, info, wfwd, bias4, residual_nhwc=None, plan=None):
     """bfloat16 forward with NHWC residual and NHWC output only -> out_nhwc [B,ho,wo,Co]
-    (rgbd_dsam_fwd_nhwc; the hot path's cascade)."""
-    _need_cuda(x_nhwc, code, info, wfwd, bias4, residual_nhwc)
+    (rgbd_dsam_fwd_nhwc; the hot path's cascade).  ``plan``: this leg's buffer from dsam_plan."""
+    _need_cuda(x_nhwc, code, info, wfwd, bias4, residual_nhwc, plan)
     if x_nhwc.dtype != torch.bfloat16:
         raise TypeError("dsam_fwd_nhwc is the bfloat16 path")
     B, h, w, Ci = x_nhwc.shape
@@ -346,18 +376,25 @@ def dsam_fwd_nhwc(x_nhwc, code, info, wfwd, bias4, residual_nhwc=None):
     out = torch.empty((B, ho, wo, Co), dtype=x_nhwc.dtype, device=x_nhwc.device)
     b4 = bias4.detach().float().contiguous()
     L = _lib.lib()
+    if plan is not None:
+        ws = _workspace(x_nhwc.device, L.rgbd_dsam_run_workspace_size(LEG_FWD, B, Ci, h, w, Co), "dsam_conv")
+        check(L.rgbd_dsam_fwd_nhwc_planned(RGBD_BF16, _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co, _p(wfwd),
+                                           _p(b4), _p(residual_nhwc), _p(out), _p(plan), _p(ws),
+                                           _stream(x_nhwc.device)), "rgbd_dsam_fwd_nhwc_planned")
+        return out
     ws = _workspace(x_nhwc.device, L.rgbd_dsam_conv_workspace_size(RGBD_BF16, B, Ci, h, w, Co), "dsam_conv")
     check(L.rgbd_dsam_fwd_nhwc(RGBD_BF16, _p(x_nhwc), _p(code), _p(info), B, Ci, h, w, Co, _p(wfwd), _p(b4),
                                _p(residual_nhwc), _p(out), _p(ws), _stream(x_nhwc.device)), "rgbd_dsam_fwd_nhwc")
     return out
 
 
-def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False, cin=None, gin_nhwc=None, want_nchw=True):
+def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False, cin=None, gin_nhwc=None, want_nchw=True,
+                  plan=None):
     """dX of one DSAM (+ gin).  The input channel count comes from ``cin``, ``gin_nchw`` /
     ``gin_nhwc`` or the 2-D float32 wbwd (the flat bfloat16 tiles do not carry it).
     ``want_nchw=False`` (bfloat16 only) writes the NHWC result alone, with the residual given as
     ``gin_nhwc``: the hot path's cascade, which never needs dX in NCHW."""
-    _need_cuda(gout_nhwc, code, wbwd, gin_nchw, gin_nhwc)
+    _need_cuda(gout_nhwc, code, wbwd, gin_nchw, gin_nhwc, plan)
     B, ho, wo, Co = gout_nhwc.shape
     if cin is not None:
         Ci = int(cin)
@@ -380,17 +417,23 @@ def dsam_bwd_data(gout_nhwc, code, wbwd, gin_nchw, want_nhwc=False, cin=None, gi
     dx_nhwc = torch.empty((B, h, w, Ci), dtype=gout_nhwc.dtype, device=gout_nhwc.device) if want_nhwc else None
     L = _lib.lib()
     dt = _dtype_code(gout_nhwc)
+    if plan is not None:
+        ws = _workspace(gout_nhwc.device, L.rgbd_dsam_run_workspace_size(LEG_DX, B, Ci, h, w, Co), "dsam_conv")
+        check(L.rgbd_dsam_bwd_data_planned(dt, _p(gout_nhwc), _p(code), B, Ci, h, w, Co, _p(wbwd), _p(gin_nchw),
+                                           _p(gin_nhwc), _p(dx), _p(dx_nhwc), _p(plan), _p(ws),
+                                           _stream(gout_nhwc.device)), "rgbd_dsam_bwd_data_planned")
+        return dx, dx_nhwc
     ws = _workspace(gout_nhwc.device, L.rgbd_dsam_conv_workspace_size(dt, B, Ci, h, w, Co), "dsam_conv")
     check(L.rgbd_dsam_bwd_data(dt, _p(gout_nhwc), _p(code), B, Ci, h, w, Co, _p(wbwd), _p(gin_nchw), _p(gin_nhwc),
                                _p(dx), _p(dx_nhwc), _p(ws), _stream(gout_nhwc.device)), "rgbd_dsam_bwd_data")
     return dx, dx_nhwc
 
 
-def dsam_bwd_weight(gout_nchw, x_nhwc, code, info, gout_nhwc=None):
+def dsam_bwd_weight(gout_nchw, x_nhwc, code, info, gout_nhwc=None, plan=None):
     """dW/db of one DSAM.  The bfloat16 path contracts the NHWC copy of the upstream gradient
     (``gout_nhwc``; made here when not given); bias gradients use the NCHW one when given, else
-    (bfloat16) the NHWC one."""
-    _need_cuda(gout_nchw, x_nhwc, code, info, gout_nhwc)
+    (bfloat16) the NHWC one.  ``plan``: this leg's buffer from dsam_plan (bfloat16)."""
+    _need_cuda(gout_nchw, x_nhwc, code, info, gout_nhwc, plan)
     if gout_nchw is None:
         if gout_nhwc is None or gout_nhwc.dtype != torch.bfloat16:
             raise ValueError("dsam_bwd_weight: gout_nchw is required unless a bfloat16 gout_nhwc is given")
@@ -410,6 +453,14 @@ def dsam_bwd_weight(gout_nchw, x_nhwc, code, info, gout_nhwc=None):
     dproj = torch.empty((Co, Ci, 3, 3), dtype=torch.float32, device=dev)
     dbias = torch.empty((4, Co), dtype=torch.float32, device=dev)
     L = _lib.lib()
+    if plan is not None:
+        if dt != RGBD_BF16:
+            raise ValueError("dsam_bwd_weight: a plan goes with the bfloat16 path")
+        ws = _workspace(dev, L.rgbd_dsam_run_workspace_size(LEG_DW, B, Ci, h, w, Co), "dsam_wgrad")
+        check(L.rgbd_dsam_bwd_weight_planned(dt, _p(gout_nchw), _p(gout_nhwc), _p(x_nhwc), _p(code), _p(info), B, Ci,
+                                             h, w, Co, _p(dconv), _p(dproj), _p(dbias), _p(plan), _p(ws),
+                                             _stream(dev)), "rgbd_dsam_bwd_weight_planned")
+        return dconv, dproj, dbias
     ws = _workspace(dev, L.rgbd_dsam_bwd_weight_workspace_size(dt, B, Ci, h, w, Co), "dsam_wgrad")
     check(L.rgbd_dsam_bwd_weight(dt, _p(gout_nchw), _p(gout_nhwc), _p(x_nhwc), _p(code), _p(info), B, Ci, h, w,
                                  Co, _p(dconv), _p(dproj), _p(dbias), _p(ws), _stream(dev)), "rgbd_dsam_bwd_weight")

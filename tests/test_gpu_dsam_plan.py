@@ -1,0 +1,68 @@
+"""Planning ahead (include/rgbd_hip.h rgbd_dsam_plan): every bf16 DSAM leg run with a plan made
+earlier — all forward / dX legs of the three DSAMs planned by one call, the dW legs by another —
+gives bitwise the outputs of the plain entry points, which plan inside the call.  Shapes: the
+bench's 640x480 B=8 pyramid and a ragged one (97x131 input, odd feature sizes), region codes
+from the HIP decomposition.  Reference path: custom_model.py:682-699 (DSAModule.forward); the
+parity of the plain entry points themselves is test_gpu_dsam_full.py / test_gpu_parity.py."""
+import pytest
+import torch
+
+import _rgbd_import  # noqa: F401
+from rgbd_amd import ops, synthetic
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+CH = [(96, 192), (192, 384), (384, 768)]
+
+
+def _sizes(H, W):
+    s = [((H + 3) // 4, (W + 3) // 4)]
+    for _ in range(2):
+        s.append(((s[-1][0] + 1) // 2, (s[-1][1] + 1) // 2))
+    return s
+
+
+@pytest.mark.parametrize("H,W,B", [(480, 640, 8), (97, 131, 3)])
+def test_planned_legs_bitwise(H, W, B):
+    planes, _, _ = synthetic.make_batch(7, B, H, W)
+    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
+    sizes = _sizes(H, W)
+    codes, info = ops.edsam_decompose(d3, torch.linspace(0.05, 0.45, B, device=DEV), sizes)
+    masks = ops.dsam_code_masks(codes)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    legs = [(ops.LEG_FWD, codes[k], *CH[k]) for k in range(3)] + [(ops.LEG_DX, codes[k], *CH[k]) for k in (1, 2)]
+    conv_plans = ops.dsam_plan(legs)
+    dw_plans = ops.dsam_plan([(ops.LEG_DW, codes[k], *CH[k]) for k in range(3)])
+    for k in range(3):
+        ci, co = CH[k]
+        h, w = sizes[k]
+        ho, wo = (h + 1) // 2, (w + 1) // 2
+        cw = torch.randn((4, co, ci, 3, 3), generator=g, device=DEV) * 0.03
+        pw = torch.randn((co, ci, 3, 3), generator=g, device=DEV) * 0.03
+        b4 = torch.randn((4, co), generator=g, device=DEV) * 0.1
+        wf, wb = ops.dsam_pack(cw, pw, torch.bfloat16, code_mask=masks[k:k + 1])
+        x = torch.randn((B, h, w, ci), generator=g, device=DEV).bfloat16()
+        res = torch.randn((B, ho, wo, co), generator=g, device=DEV).bfloat16()
+        gy = (torch.randn((B, ho, wo, co), generator=g, device=DEV) * 0.1).bfloat16()
+        gin = torch.randn((B, h, w, ci), generator=g, device=DEV).bfloat16()
+        y0 = ops.dsam_fwd_nhwc(x, codes[k], info, wf, b4, residual_nhwc=res)
+        y1 = ops.dsam_fwd_nhwc(x, codes[k], info, wf, b4, residual_nhwc=res, plan=conv_plans[k])
+        assert torch.equal(y0, y1), f"forward {k}"
+        w0 = ops.dsam_bwd_weight(None, x, codes[k], info, gout_nhwc=gy)
+        w1 = ops.dsam_bwd_weight(None, x, codes[k], info, gout_nhwc=gy, plan=dw_plans[k])
+        for a, b, name in zip(w0, w1, ("dconv", "dproj", "dbias")):
+            assert torch.equal(a, b), f"dW {k} {name}"
+        if k > 0:
+            _, d0 = ops.dsam_bwd_data(gy, codes[k], wb, None, want_nhwc=True, want_nchw=False, gin_nhwc=gin)
+            _, d1 = ops.dsam_bwd_data(gy, codes[k], wb, None, want_nhwc=True, want_nchw=False, gin_nhwc=gin,
+                                      plan=conv_plans[3 + (k - 1)])
+            assert torch.equal(d0, d1), f"dX {k}"
+
+
+def test_plan_rejects_bad_legs():
+    code = torch.zeros((2, 30, 40), dtype=torch.uint8, device=DEV)
+    with pytest.raises(ValueError):
+        ops.dsam_plan([(7, code, 96, 192)])
+    with pytest.raises(ops._lib.RgbdHipError):  # channel counts the bf16 path does not tile
+        ops.dsam_plan([(ops.LEG_FWD, code, 40, 192)])
