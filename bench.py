@@ -188,19 +188,31 @@ def build(args, dev, rank=0):
                 gouts=gouts, scenes=scenes, sizes=sizes)
 
 
-def make_parts(ctx, world, capturable=False):
+def make_parts(ctx, world, capturable=False, overlap_opt=False):
     """(forward_backward, optimizer_step, reducer, broadcaster) of one training step.
     forward_backward() leaves the (all-reduced, for N > 1) gradients in p.grad;
-    optimizer_step.opt is the AdamW instance (``capturable`` for graph capture)."""
+    optimizer_step.opt is the AdamW instance (``capturable`` for graph capture).
+    ``overlap_opt``: the AdamW steps run inside the backward instead, one per parameter group as
+    its gradients are enqueued (distributed.InBackwardOptimizer; bitwise the same update);
+    forward_backward() then trains and optimizer_step() only clears the gradients
+    (optimizer_step.opt None, optimizer_step.opts the per-group optimizers)."""
     from rgbd_amd import ops
-    from rgbd_amd.distributed import BufferBroadcaster, OverlappedGradReducer, hot_path_grad_groups
+    from rgbd_amd.distributed import (BufferBroadcaster, InBackwardOptimizer, OverlappedGradReducer,
+                                      hot_path_grad_groups)
     from rgbd_amd.hot_path import hot_path
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
+    groups = hot_path_grad_groups(ctx["dsams"], ctx["dg"])
     # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
-    reducer = OverlappedGradReducer(hot_path_grad_groups(ctx["dsams"], ctx["dg"])) if world > 1 else None
+    reducer = OverlappedGradReducer(groups) if world > 1 else None
     bcast = BufferBroadcaster([ctx["rp"]]) if world > 1 else None
     hook = None if reducer is None else reducer.ready
-    opt = torch.optim.AdamW(params, lr=1e-5, fused=True, capturable=capturable)
+    if overlap_opt:
+        parts = {"1": ((0,), (1, 2)), "2": ((0,), (1,), (2,)), "3": ((0, 1, 2),)}[os.environ.get("RGBD_OPT_PARTS", "1")]
+        inb = InBackwardOptimizer(groups, lambda g: torch.optim.AdamW(g, lr=1e-5, fused=True, capturable=capturable),
+                                  reducer, steps=parts)
+        hook, opt = inb.hook, None
+    else:
+        opt = torch.optim.AdamW(params, lr=1e-5, fused=True, capturable=capturable)
 
     def forward_backward():
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
@@ -209,14 +221,18 @@ def make_parts(ctx, world, capturable=False):
         ratio = ctx["rp"](pv[:, 3:6])
         feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], grad_hook=hook)
         torch.autograd.backward(feats, ctx["gouts"])
-        if reducer is not None:  # DDP gradient exchange of the hot-path parameters (RCCL over xGMI)
+        if reducer is not None and not overlap_opt:  # DDP gradient exchange (RCCL over xGMI)
             reducer.finish()
         return feats
 
     def optimizer_step():
+        if overlap_opt:
+            inb.zero_grad(set_to_none=True)
+            return
         opt.step()
         opt.zero_grad(set_to_none=True)
     optimizer_step.opt = opt
+    optimizer_step.opts = inb.opts if overlap_opt else [opt]
 
     return forward_backward, optimizer_step, reducer, bcast
 
@@ -233,15 +249,15 @@ def make_step(ctx, world, inference=False, graph=False):
         return istep
     if graph:  # single process: the whole step replayed from a HIP graph, captured on first use
         from rgbd_amd.train_graph import CapturedTrainStep
-        fb, ostep, _, _ = make_parts(ctx, world, capturable=True)
+        fb, ostep, _, _ = make_parts(ctx, world, capturable=True, overlap_opt=True)
         held = {}
 
         def gstep():
             if "g" not in held:
-                held["g"] = CapturedTrainStep(fb, ostep.opt)
+                held["g"] = CapturedTrainStep(fb, ostep.opt, opts=ostep.opts, clear=ostep)
             return held["g"]()
         return gstep
-    fb, ostep, _, _ = make_parts(ctx, world)
+    fb, ostep, _, _ = make_parts(ctx, world, overlap_opt=True)
 
     def step():
         feats = fb()

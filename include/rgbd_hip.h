@@ -255,6 +255,10 @@ int rgbd_dsam_bwd_weight_planned(int dtype, const void* gout_nchw, const void* g
 size_t rgbd_ratio_packed_size(int dtype);
 int rgbd_ratio_pack(int dtype, const float* const* weights_host, void* packed, void* stream);
 size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W);
+/* Byte offset in the workspace of the gated attention features x * sigmoid(attention(x))
+ * (the input of feature_extractor, custom_model.py:1468-1471) as rgbd_ratio_forward leaves
+ * them: dtype NHWC [B][H][W][128], valid until the workspace is reused (diagnostics / tests). */
+size_t rgbd_ratio_features_offset(int dtype, int B, int H, int W);
 int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        unsigned long long* seed_counter, float* ratio, void* ws, void* stream);

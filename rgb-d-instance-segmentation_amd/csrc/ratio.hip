@@ -1830,7 +1830,10 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate
-  const bool gate = v2 && training;
+  // RGBD_RATIO_PHASE2=1 (read per call): train mode through phase 2 instead of the gate kernel
+  // (a test compares the two paths' gated features)
+  const char* ph2 = getenv("RGBD_RATIO_PHASE2");
+  const bool gate = v2 && training && !(ph2 && atoi(ph2) != 0);
   bf16_t* fus = (bf16_t*)y;
   if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, gate ? (void*)fus : nullptr);
   k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, nslab_ch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
@@ -1905,6 +1908,10 @@ int rgbd_ratio_pack(int dtype, const float* const* weights_host, void* packed, v
     return RGBD_E_DTYPE;
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
+}
+
+size_t rgbd_ratio_features_offset(int dtype, int B, int H, int W) {
+  return make_ws(dtype == RGBD_BF16 ? 2 : 4, B > 0 ? B : 1, H > 0 ? H : 1, W > 0 ? W : 1).att;
 }
 
 size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W) {

@@ -24,13 +24,14 @@ from . import ops
 DSAM_PARAMS_PER_MODULE = 9  # conv_layers.{0..3}.{weight,bias}, rgb_projection.weight
 _SIDE_STREAMS = {}
 _OVERLAP = os.environ.get("RGBD_OVERLAP", "1") != "0"  # side-stream backward (A/B switch)
+_DW1_STREAM = int(os.environ.get("RGBD_DW1_STREAM", "0"))  # side stream of dsam1's dW (A/B switch)
 
 
-def side_stream(dev):
-    """The per-device stream the bf16 backward runs its off-critical-path launches on."""
-    s = _SIDE_STREAMS.get(dev.index)
+def side_stream(dev, idx=0):
+    """Per-device side streams (``idx`` 0, 1) the bf16 path runs its off-critical-path launches on."""
+    s = _SIDE_STREAMS.get((dev.index, idx))
     if s is None:
-        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+        s = _SIDE_STREAMS[(dev.index, idx)] = torch.cuda.Stream(device=dev)
     return s
 
 
@@ -40,11 +41,11 @@ class _Side:
     so the allocator does not hand their memory to the main stream while side work reads it;
     outputs are recorded on the main stream at the join."""
 
-    def __init__(self, dev, enabled):
+    def __init__(self, dev, enabled, idx=0):
         self.on = enabled
         if enabled:
             self.main = torch.cuda.current_stream(dev)
-            self.side = side_stream(dev)
+            self.side = side_stream(dev, idx)
         self.outs = []
 
     def run(self, fn, *inputs):
@@ -117,9 +118,11 @@ class HotPathFunction(torch.autograd.Function):
         dggm_p = params[27:35]
         sizes = [tuple(c.shape[2:]) for c in colors[:3]]
         bf16 = dtype == torch.bfloat16
-        # bf16 on the GPU: the colour-map layout changes run beside the decomposition and the
-        # dsam1 / dsam2 packing beside dsam0 (side stream; joined before their consumers)
-        side = _Side(pixel_values.device, bf16 and pixel_values.is_cuda and cfg.get("overlap", True))
+        # bf16 on the GPU: the colour-map layout changes run beside the decomposition, the dsam1 /
+        # dsam2 packing beside dsam0 (one side stream each; joined before their consumers)
+        on = bf16 and pixel_values.is_cuda and cfg.get("overlap", True)
+        side = _Side(pixel_values.device, on)
+        side1 = _Side(pixel_values.device, on, idx=1)
         if bf16:
             nhwc = side.run(lambda: [ops.nchw_to_nhwc(c) for c in colors], *colors)
         codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
@@ -147,14 +150,16 @@ class HotPathFunction(torch.autograd.Function):
         if bf16:
             packs = [pack(0)]
             side.join()  # the NHWC colour maps
-            packs += side.run(lambda: [pack(1), pack(2)], masks)
+            packs += [side.run(lambda: pack(1), masks), side1.run(lambda: pack(2), masks)]
             x_nhwc = [nhwc[0]]
             res_nhwc = nhwc[1:]
             # bf16 cascade entirely in NHWC: each DSAM adds its residual colour map in NHWC and writes
             # cp1[k+1] once, in the layout the next DSAM reads and the DGGM pass accepts
             for k in range(3):
+                if k == 2:
+                    side1.join()  # the dsam2 pack
                 if k == 1:
-                    side.join()  # the dsam1 / dsam2 packs
+                    side.join()  # the dsam1 pack
                     if training:  # dW plans beside the rest of the forward
                         dw_plans = side.run(lambda: ops.dsam_plan([(ops.LEG_DW, codes[j], *chans[j]) for j in range(3)]),
                                             *codes)
@@ -203,17 +208,21 @@ class HotPathFunction(torch.autograd.Function):
                                    if shape is None else "missing gradient for scale 0")
             G.append(g.to(dtype).contiguous())
         bf16 = dtype == torch.bfloat16
-        # bf16 on the GPU: the critical path is dX2 -> dX1 -> dW0 (main stream); the DGGM backward
-        # and the dW of dsam2 / dsam1 run beside it on the side stream (their persistent kernels
-        # take CUs as the other stream's work drains; every kernel assigns its work dynamically)
-        side = _Side(G[0].device, bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True))
+        # bf16 on the GPU: the critical path is dX2 -> dX1 -> dW0 (main stream); the dW of dsam2
+        # (side stream 0, from the start) and the DGGM backward then the dW of dsam1 (side stream
+        # 1, once dX2 is done) run beside it, each on its own stream so dW1 need not wait for dW2
+        # (the latency-bound persistent kernels take CUs as the other streams' work drains; every
+        # kernel assigns its work dynamically)
+        on = bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True)
+        side = _Side(G[0].device, on)
+        side1 = _Side(G[0].device, on, idx=1)
 
         def dggm_bwd():
             out = []
             for k, (dw, db) in enumerate(ops.dggm_fuse_bwd_multi(G, pixel_values, dggm_p[0::2], dggm_p[1::2])):
                 out += [dw.reshape(dggm_p[2 * k].shape).to(dggm_p[2 * k].dtype), db.to(dggm_p[2 * k + 1].dtype)]
             return out
-        grads_dggm = side.run(dggm_bwd, *G, pixel_values)
+        grads_dggm = side1.run(dggm_bwd, *G, pixel_values)
         # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}.  bfloat16 keeps the cascade in
         # NHWC (dX written NHWC only, its residual G[k] converted once; bias sums from NHWC).
         hook = ctx.cfg.get("grad_hook")
@@ -225,6 +234,9 @@ class HotPathFunction(torch.autograd.Function):
                 dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k],
                                                           ctx.info, gout_nhwc=dcp_nhwc,
                                                           plan=ctx.dw_plans[k] if ctx.dw_plans else None)
+                if k == 0:  # dW0 needs nothing from the side streams; the hook and the caller do
+                    side.join()
+                    side1.join()
                 gk = []
                 for i in range(4):
                     gk += [dconv[i], dbias[i]]
@@ -233,9 +245,9 @@ class HotPathFunction(torch.autograd.Function):
                     hook(2 - k, gk if k > 0 else gk + grads_dggm)
                 return gk
             if k > 0:
-                grads_dsam[k] = side.run(dsam_dw, dcp_nhwc, ctx.x_nhwc[k], ctx.codes[k], ctx.info)
-            else:  # the last launch of the backward: on the main stream, after the join
-                side.join()
+                grads_dsam[k] = (side1 if k == 1 and _DW1_STREAM else side).run(dsam_dw, dcp_nhwc, ctx.x_nhwc[k],
+                                                                               ctx.codes[k], ctx.info)
+            else:  # the last launches of the backward: on the main stream, joins after them
                 grads_dsam[k] = dsam_dw()
             if k > 0:
                 if bf16:

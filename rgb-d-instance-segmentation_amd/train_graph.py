@@ -29,23 +29,32 @@ class CapturedTrainStep:
     the step is captured.  Calling the object replays it and returns ``fb``'s outputs, static
     tensors overwritten by the next replay."""
 
-    def __init__(self, fb, opt, warmup=2):
-        for g in opt.param_groups:
-            if not g.get("capturable", False):
-                raise ValueError("CapturedTrainStep needs a capturable optimizer (capturable=True)")
+    def __init__(self, fb, opt, warmup=2, opts=None, clear=None):
+        """``opt`` None: ``fb`` steps the optimizers itself (distributed.InBackwardOptimizer),
+        ``opts`` lists them (checked for capturable) and ``clear()`` clears the gradients."""
+        opts = [opt] if opt is not None else list(opts or ())
+        if not opts:
+            raise ValueError("CapturedTrainStep needs the optimizer(s) the step uses")
+        for o in opts:
+            for g in o.param_groups:
+                if not g.get("capturable", False):
+                    raise ValueError("CapturedTrainStep needs a capturable optimizer (capturable=True)")
         self.fb, self.opt = fb, opt
+        clear = clear or (lambda: [o.zero_grad(set_to_none=True) for o in opts])
         self.stream = torch.cuda.Stream()
         self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):
             for _ in range(max(warmup, 1)):
                 self.fb()
-                self.opt.step()
-                self.opt.zero_grad(set_to_none=True)
+                if opt is not None:
+                    self.opt.step()
+                clear()
         torch.cuda.current_stream().wait_stream(self.stream)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=self.stream):
             self.outs = self.fb()
-            self.opt.step()
+            if opt is not None:
+                self.opt.step()
 
     def __call__(self):
         self.graph.replay()

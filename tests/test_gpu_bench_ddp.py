@@ -4,7 +4,9 @@ MI355X of the test box, gloo — RCCL refuses two ranks on one device).
 * the launcher: ``bench.py --gpus 2`` spawns two ranks and reports n_gpus 2 / global batch 16;
 * DDP semantics of the step (the reference's Trainer, finetuning.py:98-113): after the
   overlapped reducer, every rank holds the mean of the two ranks' standalone gradients, and
-  every forward starts from rank 0's ratio-predictor BatchNorm buffers (broadcast_buffers)."""
+  every forward starts from rank 0's ratio-predictor BatchNorm buffers (broadcast_buffers);
+* the timed step's AdamW steps inside the backward give bitwise the parameters of DDP + one
+  optimizer step after the backward."""
 import json
 import os
 import socket
@@ -83,8 +85,20 @@ def _worker(rank, world, port, q):
         other = flat.clone()
         dist.broadcast(other, src=0)
         buf_err = float((flat - other).abs().max())
+        # the AdamW steps inside the backward (bench.py's timed step): each group waits for its
+        # all-reduce on its stream and steps on the mean -> the parameters of DDP + one step
+        outs = []
+        for overlap in (False, True):
+            ctx = bench.build(args, dev, rank=rank)
+            ctx["rp"].eval()
+            fb, ostep, _, _ = bench.make_parts(ctx, world, overlap_opt=overlap)
+            for _ in range(2):
+                fb()
+                ostep()
+            outs.append([p.detach().clone() for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()])
+        opt_err = max(float((a - e).abs().max()) for a, e in zip(outs[1], outs[0]))
         torch.cuda.synchronize()
-        q.put((rank, (grad_err, buf_err)))
+        q.put((rank, (grad_err, buf_err, opt_err)))
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent
         import traceback
@@ -103,6 +117,7 @@ def test_ddp_step_gradients_and_buffers_world2():
         p.join(timeout=60)
     for r in (0, 1):
         assert isinstance(res[r], tuple), res[r]
-        grad_err, buf_err = res[r]
+        grad_err, buf_err, opt_err = res[r]
         assert grad_err < 1e-5, res
         assert buf_err == 0.0, res
+        assert opt_err == 0.0, res

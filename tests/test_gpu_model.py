@@ -106,6 +106,43 @@ def test_bf16_train_mode_batchnorm_stats(H, W):
             assert rel <= 5e-2, (k, rel)
 
 
+@pytest.mark.parametrize("H,W", [(64, 96), (90, 125), (240, 320)])
+@pytest.mark.parametrize("path", ["gate", "phase2"])
+def test_bf16_train_mode_gated_features(H, W, path, monkeypatch):
+    """The train-mode gated features (fused * attention(fused), custom_model.py:1469-1470, the
+    conv5 input) read from the ratio workspace, against the PyTorch-CPU fp32 module tree in
+    train mode, for both bf16 routes: k_rp_gate over phase 1's stored raw fusion output (the
+    default) and phase 2's stem + fusion recompute (RGBD_RATIO_PHASE2=1).  Aligned (64x96,
+    240x320) and ragged (90x125) shapes.  Tolerance on the features themselves: bf16 operands
+    and a bf16-stored fusion output against f32 — max |diff| <= 3e-2 of max |ref|, mean |diff|
+    <= 1e-2 of mean |ref| (a fragment-order slip moves whole channel/pixel blocks and fails
+    both by orders of magnitude)."""
+    from rgbd_amd import _lib, ops
+    monkeypatch.setenv("RGBD_RATIO_PHASE2", "1" if path == "phase2" else "0")
+    B = 2
+    pv = gi.pixel_values(12, B, H, W)
+    m_cpu = _ratio_module().train()
+    m = copy.deepcopy(m_cpu)
+    m.compute_dtype = torch.bfloat16
+    m = m.to(DEV).train()
+    x = torch.from_numpy(pv).to(DEV)[:, 3:6]
+    m(x)
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    ws = ops._workspace(x.device, L.rgbd_ratio_workspace_size(1, B, H, W), "ratio")
+    off = L.rgbd_ratio_features_offset(1, B, H, W)
+    att = ws[off:off + B * H * W * 128 * 2].view(torch.bfloat16).reshape(B, H, W, 128)
+    got = att.permute(0, 3, 1, 2).float().cpu()
+    ref = {}
+    m_cpu.feature_extractor.register_forward_pre_hook(lambda mod, a: ref.__setitem__("x", a[0].detach().clone()))
+    with torch.no_grad():
+        ratio_o.ratio_forward_modules(m_cpu, torch.from_numpy(pv[:, 3:6]))
+    e = ref["x"]
+    d = (got - e).abs()
+    assert float(d.max()) <= 3e-2 * float(e.abs().max()), (path, float(d.max()), float(e.abs().max()))
+    assert float(d.mean()) <= 1e-2 * float(e.abs().mean()), (path, float(d.mean()), float(e.abs().mean()))
+
+
 def test_full_model_mask_logits_fp32(golden):
     """North-star parity: mask-logit max-abs-err vs the reference CPU path <= 1e-3 (fp32 mode).
 

@@ -53,6 +53,28 @@ def test_captured_step_equals_eager_steps():
     assert len(outs) == 4 and all(torch.isfinite(o.float()).all() for o in outs)
 
 
+def test_captured_in_backward_optimizer_equals_eager_steps():
+    """bench.py's timed N=1 step: the AdamW steps issued inside the backward, one per parameter
+    group (distributed.InBackwardOptimizer), replayed from a graph, against plain eager steps
+    with one optimizer.step() after each backward: bitwise the same parameters and buffers."""
+    import bench
+    from rgbd_amd.train_graph import CapturedTrainStep
+    args = bench.parse(["--height", "96", "--width", "128", "--batch", "3"])
+    a, b = _ctx(bench, args), _ctx(bench, args)
+    fa, oa, _, _ = bench.make_parts(a, 1, capturable=True)
+    for _ in range(4):
+        fa()
+        oa()
+    fb, ob, _, _ = bench.make_parts(b, 1, capturable=True, overlap_opt=True)
+    assert ob.opt is None and len(ob.opts) >= 1
+    step = CapturedTrainStep(fb, None, warmup=2, opts=ob.opts, clear=ob)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    for i, (x, y) in enumerate(zip(_state(a), _state(b))):
+        assert torch.equal(x, y), f"state tensor {i} differs after 4 steps"
+
+
 def test_captured_step_needs_capturable_optimizer():
     import bench
     from rgbd_amd.train_graph import CapturedTrainStep
