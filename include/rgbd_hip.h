@@ -96,6 +96,13 @@ int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_
                          const float* ratio, int n_scales, const int* out_h_host,
                          const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
                          void* ws, void* stream);
+/* The same decomposition, also writing code_masks[s] (device uint32 [n_scales], OVERWRITTEN):
+ * bit k set when region code k occurs in codes[s] — the codes the bf16 DSAM filters are packed
+ * for (rgbd_dsam_pack_weights' code_mask), without a pass of its own over the code planes. */
+int rgbd_edsam_decompose_masks(const float* depth3, long long batch_stride, int depth_channels, int B, int H,
+                               int W, const float* ratio, int n_scales, const int* out_h_host,
+                               const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
+                               uint32_t* code_masks, void* ws, void* stream);
 
 /* ---------------------------------------------------------------- K2 DGGM gated fusion
  * Replaces DepthGradientInjectionResidual.forward (custom_model.py:1204-1269) for one

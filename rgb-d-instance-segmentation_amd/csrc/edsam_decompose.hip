@@ -67,21 +67,17 @@ __device__ __forceinline__ float edge_at(const Range& r, int i) {
   return i == RGBD_NBINS ? r.last : __fadd_rn(__fmul_rn((float)i, r.step), r.first);
 }
 
-__global__ void k_init(DecWs* ws, rgbd_decomp_info* info, int B) {
-  const int b = blockIdx.x;
-  if (b >= B) return;
-  if (threadIdx.x == 0) {
-    ws[b].min_key = 0xffffffffu;
-    ws[b].max_key = 0u;
-  }
-  for (int i = threadIdx.x; i < RGBD_NBINS; i += blockDim.x) info[b].hist[i] = 0;
-}
-
 // One (min, max) key pair per block into part[b][blockIdx.x]; k_hist reduces them (the 96
 // blocks x 8 images of same-line atomics this replaced serialised for ~20 us).
 __global__ __launch_bounds__(256) void k_grey_minmax(const float* __restrict__ depth3, long long bstride,
-                                                     long long HW, int nch, uint2* __restrict__ part) {
+                                                     long long HW, int nch, uint2* __restrict__ part,
+                                                     rgbd_decomp_info* __restrict__ info, uint32_t* __restrict__ cmask,
+                                                     int ncmask) {
   const int b = blockIdx.y;
+  if (blockIdx.x == 0) {  // k_hist adds into the histogram; the code-presence masks are OR-ed into
+    for (int i = threadIdx.x; i < RGBD_NBINS; i += 256) info[b].hist[i] = 0;
+    if (b == 0 && cmask && threadIdx.x < ncmask) cmask[threadIdx.x] = 0u;
+  }
   const float* d = depth3 + b * bstride;
   uint32_t kmin = 0xffffffffu, kmax = 0u;
   for (long long p = blockIdx.x * 256ll + threadIdx.x; p < HW; p += 256ll * gridDim.x) {
@@ -324,6 +320,73 @@ __global__ __launch_bounds__(256) void k_codes_pool(const float* __restrict__ de
   code[(long long)b * oh * ow + q] = (uint8_t)c;
 }
 
+// The three-level code pyramid of the Swin input resolutions in one pass, for the common case
+// where each level halves the previous one and the first pools whole f0y x f0x pixel blocks:
+// a 256-thread block owns 16 x 16 level-0 cells (whole level-1 / level-2 cells: tile origins are
+// multiples of 4 cells and level 0 has exactly 4x the level-2 cells), computes each level-0 code
+// from its pixels, OR-pools 2 x 2 cells twice through LDS (exactly adaptive_max_pool2d of the
+// full-resolution masks, bins nesting), and ORs 1 << code into the per-level presence masks.
+__global__ __launch_bounds__(256) void k_codes_pyramid(const float* __restrict__ depth3, long long bstride, int H, int W,
+                                                       int nch, int oh0, int ow0, const rgbd_decomp_info* info,
+                                                       uint8_t* __restrict__ c0, uint8_t* __restrict__ c1,
+                                                       uint8_t* __restrict__ c2, uint32_t* __restrict__ cmask) {
+  __shared__ uint8_t s0[16][17], s1[8][9];
+  __shared__ uint32_t smask[3];
+  const int b = blockIdx.z, tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int i = blockIdx.y * 16 + ty, j = blockIdx.x * 16 + tx;
+  const int n = info[b].n_modes;
+  float lo[RGBD_MAX_MODES], hi[RGBD_MAX_MODES];
+  for (int t = 0; t < RGBD_MAX_MODES; ++t) {
+    lo[t] = info[b].lo[t];
+    hi[t] = info[b].hi[t];
+  }
+  if (threadIdx.x < 3) smask[threadIdx.x] = 0u;
+  const int fy = H / oh0, fx = W / ow0;
+  const long long HW = (long long)H * W;
+  const float* d = depth3 + b * bstride;
+  uint32_t c = 0u;
+  const bool in0 = i < oh0 && j < ow0;
+  if (in0 && n > 0)
+    for (int y = i * fy; y < (i + 1) * fy; ++y)
+      for (int x = j * fx; x < (j + 1) * fx; ++x) c |= pixel_code(grey_at(d, HW, (long long)y * W + x, nch), n, lo, hi);
+  s0[ty][tx] = (uint8_t)c;
+  __syncthreads();
+  if (in0) {
+    c0[((long long)b * oh0 + i) * ow0 + j] = (uint8_t)c;
+    atomicOr(&smask[0], 1u << c);
+  }
+  const int oh1 = oh0 / 2, ow1 = ow0 / 2, oh2 = oh1 / 2, ow2 = ow1 / 2;
+  if (ty < 8 && tx < 8) {
+    const uint32_t v = s0[2 * ty][2 * tx] | s0[2 * ty][2 * tx + 1] | s0[2 * ty + 1][2 * tx] | s0[2 * ty + 1][2 * tx + 1];
+    s1[ty][tx] = (uint8_t)v;
+    const int i1 = blockIdx.y * 8 + ty, j1 = blockIdx.x * 8 + tx;
+    if (i1 < oh1 && j1 < ow1) {
+      c1[((long long)b * oh1 + i1) * ow1 + j1] = (uint8_t)v;
+      atomicOr(&smask[1], 1u << v);
+    }
+  }
+  __syncthreads();
+  if (ty < 4 && tx < 4) {
+    const uint32_t v = s1[2 * ty][2 * tx] | s1[2 * ty][2 * tx + 1] | s1[2 * ty + 1][2 * tx] | s1[2 * ty + 1][2 * tx + 1];
+    const int i2 = blockIdx.y * 4 + ty, j2 = blockIdx.x * 4 + tx;
+    if (i2 < oh2 && j2 < ow2) {
+      c2[((long long)b * oh2 + i2) * ow2 + j2] = (uint8_t)v;
+      atomicOr(&smask[2], 1u << v);
+    }
+  }
+  __syncthreads();
+  if (cmask && threadIdx.x < 3 && smask[threadIdx.x]) atomicOr(cmask + threadIdx.x, smask[threadIdx.x]);
+}
+
+// Presence masks of code planes the pyramid kernel did not build (the general path).
+__global__ __launch_bounds__(256) void k_codes_presence(const uint8_t* __restrict__ code, long long n,
+                                                        uint32_t* __restrict__ cmask) {
+  uint32_t m = 0u;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) m |= 1u << (code[i] & 15);
+  for (int o = 1; o < 64; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+  if ((threadIdx.x & 63) == 0 && m) atomicOr(cmask, m);
+}
+
 // OR-pool a finer code plane into a coarser one when the adaptive bins nest exactly
 // (H_in % H_out == 0, W_in % W_out == 0): identical to pooling the full-resolution masks.
 __global__ __launch_bounds__(256) void k_codes_or_pool(const uint8_t* __restrict__ fine, int fh, int fw,
@@ -347,10 +410,10 @@ size_t rgbd_edsam_decompose_workspace_size(int B) {
   return align256(sizeof(DecWs) * nb) + align256(sizeof(uint2) * kDecParts * nb);
 }
 
-int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
-                         const float* ratio, int n_scales, const int* out_h_host,
-                         const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
-                         void* ws, void* stream) {
+static int decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
+                     const float* ratio, int n_scales, const int* out_h_host, const int* out_w_host,
+                     uint8_t* const* codes_host, rgbd_decomp_info* info, uint32_t* code_masks, void* ws,
+                     void* stream) {
   RGBD_REQUIRE(depth3 && ratio && info && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && n_scales >= 0 && n_scales <= 8, RGBD_E_ARG);
   RGBD_REQUIRE(depth_channels == 1 || depth_channels == 3, RGBD_E_SHAPE);
@@ -364,12 +427,23 @@ int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_
   DecWs* w = (DecWs*)ws;
   const long long HW = (long long)H * W;
   TimerScope ts("decompose", st);
-  k_init<<<B, 256, 0, st>>>(w, info, B);
   dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), kDecParts), B);
   uint2* part = (uint2*)((char*)ws + align256(sizeof(DecWs) * (size_t)B));
-  k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part);
+  k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, info, code_masks, n_scales);
   k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, w, info);
   k_peaks<<<B, 512, 0, st>>>(w, ratio, info);
+  // the Swin pyramid (each level half the previous, level 0 whole pixel blocks): one launch
+  const bool pyramid = n_scales == 3 && H % out_h_host[0] == 0 && W % out_w_host[0] == 0 &&
+                       out_h_host[0] % 4 == 0 && out_w_host[0] % 4 == 0 && out_h_host[1] * 2 == out_h_host[0] &&
+                       out_w_host[1] * 2 == out_w_host[0] && out_h_host[2] * 2 == out_h_host[1] &&
+                       out_w_host[2] * 2 == out_w_host[1];
+  if (pyramid) {
+    dim3 g3(ceil_div(out_w_host[0], 16), ceil_div(out_h_host[0], 16), B);
+    k_codes_pyramid<<<g3, 256, 0, st>>>(depth3, batch_stride, H, W, nch, out_h_host[0], out_w_host[0], info,
+                                        codes_host[0], codes_host[1], codes_host[2], code_masks);
+    RGBD_CHECK_LAUNCH();
+    return RGBD_OK;
+  }
   for (int s = 0; s < n_scales; ++s) {
     const int oh = out_h_host[s], ow = out_w_host[s];
     dim3 g2(ceil_div((long long)oh * ow, 256), B);
@@ -383,9 +457,31 @@ int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_
       k_codes_or_pool<<<g2, 256, 0, st>>>(codes_host[src], out_h_host[src], out_w_host[src], oh, ow, codes_host[s]);
     else
       k_codes_pool<<<g2, 256, 0, st>>>(depth3, batch_stride, H, W, nch, oh, ow, info, codes_host[s]);
+    if (code_masks) {
+      const long long nb = (long long)B * oh * ow;
+      k_codes_presence<<<(unsigned)std::min<long long>(ceil_div(nb, 256 * 8), 256), 256, 0, st>>>(codes_host[s], nb,
+                                                                                              code_masks + s);
+    }
   }
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
+}
+
+int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
+                         const float* ratio, int n_scales, const int* out_h_host,
+                         const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
+                         void* ws, void* stream) {
+  return decompose(depth3, batch_stride, depth_channels, B, H, W, ratio, n_scales, out_h_host, out_w_host, codes_host,
+                   info, nullptr, ws, stream);
+}
+
+int rgbd_edsam_decompose_masks(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
+                               const float* ratio, int n_scales, const int* out_h_host, const int* out_w_host,
+                               uint8_t* const* codes_host, rgbd_decomp_info* info, uint32_t* code_masks, void* ws,
+                               void* stream) {
+  RGBD_REQUIRE(code_masks, RGBD_E_ARG);
+  return decompose(depth3, batch_stride, depth_channels, B, H, W, ratio, n_scales, out_h_host, out_w_host, codes_host,
+                   info, code_masks, ws, stream);
 }
 
 }  // extern "C"

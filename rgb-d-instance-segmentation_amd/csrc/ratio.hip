@@ -178,13 +178,11 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
 // (sum, sum of squares), reduced in fixed order in double; running stats updated like torch.
 // one 256-thread block per channel; thread i sums slab rows i, i+256, ... in double, then a
 // fixed-shape tree reduction: deterministic for a given nslab.
-__global__ __launch_bounds__(256) void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off,
-                                                   int C, double count, int training, float momentum,
-                                                   const float* gamma, const float* beta, float* run_mean,
-                                                   float* run_var, float2* __restrict__ affine) {
+__device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, int nslab, int row, int c_off, int c,
+                                               double count, int training, float momentum, const float* gamma,
+                                               const float* beta, float* run_mean, float* run_var,
+                                               float2* __restrict__ affine) {
   __shared__ double red[2][256];
-  const int c = blockIdx.x;
-  if (c >= C) return;
   double s = 0.0, q = 0.0;
   if (training)
     for (int i = threadIdx.x; i < nslab; i += 256) {
@@ -218,6 +216,21 @@ __global__ __launch_bounds__(256) void k_bn_affine(const float* __restrict__ sla
   }
   const float sc = gamma[c] / sqrtf(var + BN_EPS);
   affine[c] = make_float2(sc, beta[c] - mean * sc);
+}
+__global__ __launch_bounds__(256) void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off,
+                                                   int C, double count, int training, float momentum,
+                                                   const float* gamma, const float* beta, float* run_mean,
+                                                   float* run_var, float2* __restrict__ affine) {
+  if ((int)blockIdx.x >= C) return;
+  bn_affine_body(slab, nslab, row, c_off, blockIdx.x, count, training, momentum, gamma, beta, run_mean, run_var, affine);
+}
+// the three stem BNs (scale1/2/3, 64 channels each, concatenated :1463) in one launch
+__global__ __launch_bounds__(256) void k_bn_affine_stem(const float* __restrict__ slab, int nslab, double count,
+                                                        int training, float momentum, BnPtrs bn,
+                                                        float2* __restrict__ affine) {
+  const int l = blockIdx.x / 64, c = blockIdx.x % 64;
+  bn_affine_body(slab, nslab, STEM_C, 64 * l, c, count, training, momentum, bn.p[4 * l], bn.p[4 * l + 1],
+                 bn.p[4 * l + 2], bn.p[4 * l + 3], affine + 64 * l);
 }
 
 // ------------------------------------------------------------------ chain (stem, fusion, attention)
@@ -1824,9 +1837,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   } while (0)
   // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
   if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
-  for (int l = 0; l < 3; ++l)
-    k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch0, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
-                                 bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
+  k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate

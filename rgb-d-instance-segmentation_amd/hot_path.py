@@ -125,13 +125,16 @@ class HotPathFunction(torch.autograd.Function):
         side1 = _Side(pixel_values.device, on, idx=1)
         if bf16:
             nhwc = side.run(lambda: [ops.nchw_to_nhwc(c) for c in colors], *colors)
-        codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
+        if bf16:  # the code-presence masks the bf16 filter packing needs come out of the decomposition
+            codes, info, masks = ops.edsam_decompose(pixel_values, ratio.detach(), sizes, code_masks=True)
+        else:
+            codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
+            masks = None
         if cfg.get("check_status"):
             ops.raise_on_status(info)
         if cfg.get("status_sink") is not None:
             cfg["status_sink"].append(ops.DeferredStatus(info))
         training = any(ctx.needs_input_grad[7:])
-        masks = ops.dsam_code_masks(codes) if bf16 else None
         chans = [(colors[k].shape[1], colors[k + 1].shape[1]) for k in range(3)]
         conv_plans = dw_plans = None
         if bf16:

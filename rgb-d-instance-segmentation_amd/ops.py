@@ -83,12 +83,14 @@ def assemble_pixel_values(depth_u8: torch.Tensor, rgb_u8: torch.Tensor = None, o
 
 
 # ------------------------------------------------------------------ K3 decomposition
-def edsam_decompose(pixel_values: torch.Tensor, ratio: torch.Tensor, sizes):
+def edsam_decompose(pixel_values: torch.Tensor, ratio: torch.Tensor, sizes, code_masks=False):
     """Depth decomposition of every image, once for all DSAMs.
 
     pixel_values: float32 [B,C>=6,H,W] (depth planes = channels 3:6, custom_model.py:326), a
     [B,3,H,W] depth tensor, or a [B,1,H,W] already-grey map; ratio: float32 [B] or [B,1] on device; sizes: list of (h, w).
-    Returns (codes list of uint8 [B,h,w], info uint8 [B, 2116] device tensor)."""
+    Returns (codes list of uint8 [B,h,w], info uint8 [B, 2116] device tensor); with
+    ``code_masks`` also the int32 device tensor [len(sizes)] of dsam_code_masks(codes), made by
+    the decomposition itself (rgbd_edsam_decompose_masks)."""
     _need_cuda(pixel_values, ratio)
     if pixel_values.dtype != torch.float32:
         raise TypeError("the decomposition consumes float32 depth (SURVEY §7 (i))")
@@ -107,6 +109,12 @@ def edsam_decompose(pixel_values: torch.Tensor, ratio: torch.Tensor, sizes):
     cp = (ctypes.c_void_p * max(n, 1))(*[c.data_ptr() for c in codes])
     L = _lib.lib()
     ws = _workspace(dev, L.rgbd_edsam_decompose_workspace_size(B), "decompose")
+    if code_masks:
+        masks = torch.empty((max(n, 1),), dtype=torch.int32, device=dev)
+        check(L.rgbd_edsam_decompose_masks(ctypes.c_void_p(depth3.data_ptr()), depth3.stride(0), nch, B, H, W, _p(r),
+                                           n, oh, ow, cp, _p(info), _p(masks), _p(ws), _stream(dev)),
+              "rgbd_edsam_decompose_masks")
+        return codes, info, masks[:n]
     check(L.rgbd_edsam_decompose(ctypes.c_void_p(depth3.data_ptr()), depth3.stride(0), nch, B, H, W, _p(r), n,
                                  oh, ow, cp, _p(info), _p(ws), _stream(dev)), "rgbd_edsam_decompose")
     return codes, info

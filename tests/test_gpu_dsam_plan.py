@@ -66,3 +66,20 @@ def test_plan_rejects_bad_legs():
         ops.dsam_plan([(7, code, 96, 192)])
     with pytest.raises(ops._lib.RgbdHipError):  # channel counts the bf16 path does not tile
         ops.dsam_plan([(ops.LEG_FWD, code, 40, 192)])
+
+
+@pytest.mark.parametrize("H,W,B", [(480, 640, 8), (720, 1280, 1), (97, 131, 3), (64, 96, 2)])
+def test_decompose_code_masks(H, W, B):
+    """rgbd_edsam_decompose_masks: the same codes and info as the plain decomposition, and per
+    scale the presence mask dsam_code_masks computes from the code planes (the Swin pyramid
+    shapes take the one-launch pyramid kernel, the others the general path)."""
+    planes, _, _ = synthetic.make_batch(9, B, H, W)
+    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
+    sizes = _sizes(H, W)
+    r = torch.linspace(0.05, 0.45, B, device=DEV)
+    c0, i0 = ops.edsam_decompose(d3, r, sizes)
+    c1, i1, m1 = ops.edsam_decompose(d3, r, sizes, code_masks=True)
+    assert torch.equal(i0, i1)
+    for a, b in zip(c0, c1):
+        assert torch.equal(a, b)
+    assert torch.equal(m1, ops.dsam_code_masks(c0))
