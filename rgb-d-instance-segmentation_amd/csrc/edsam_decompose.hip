@@ -16,6 +16,7 @@
 //                      over the adaptive_max_pool2d bins of each DSAM input resolution (:687)
 // Every float op that feeds a discrete decision uses an explicitly rounded intrinsic, so the
 // result is bit-exact to the numpy 2.2 / scipy 1.15 reference.
+#include <cstdlib>
 #include "common.hpp"
 #include "timing.hpp"
 
@@ -433,7 +434,8 @@ static int decompose(const float* depth3, long long batch_stride, int depth_chan
   k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, w, info);
   k_peaks<<<B, 512, 0, st>>>(w, ratio, info);
   // the Swin pyramid (each level half the previous, level 0 whole pixel blocks): one launch
-  const bool pyramid = n_scales == 3 && H % out_h_host[0] == 0 && W % out_w_host[0] == 0 &&
+  const char* pe = getenv("RGBD_DECOMP_PYRAMID");  // A/B switch (read per call)
+  const bool pyramid = !(pe && atoi(pe) == 0) && n_scales == 3 && H % out_h_host[0] == 0 && W % out_w_host[0] == 0 &&
                        out_h_host[0] % 4 == 0 && out_w_host[0] % 4 == 0 && out_h_host[1] * 2 == out_h_host[0] &&
                        out_w_host[1] * 2 == out_w_host[0] && out_h_host[2] * 2 == out_h_host[1] &&
                        out_w_host[2] * 2 == out_w_host[1];

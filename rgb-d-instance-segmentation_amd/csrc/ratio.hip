@@ -1837,7 +1837,13 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   } while (0)
   // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
   if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
-  k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
+  const char* bse = getenv("RGBD_BN_STEM_MERGED");  // A/B switch (read per call)
+  if (!(bse && atoi(bse) == 0))
+    k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
+  else
+    for (int l = 0; l < 3; ++l)
+      k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch0, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
+                                   bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate

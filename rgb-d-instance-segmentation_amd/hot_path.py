@@ -15,6 +15,7 @@ Here:
 Backward produces exactly the gradients the reference graph has: DSAM / DGGM parameters,
 nothing for the colour maps (detached) or the ratio (left the graph via .item()).
 """
+import ctypes
 import os
 
 import torch
@@ -23,35 +24,59 @@ from . import ops
 
 DSAM_PARAMS_PER_MODULE = 9  # conv_layers.{0..3}.{weight,bias}, rgb_projection.weight
 _SIDE_STREAMS = {}
-_OVERLAP = os.environ.get("RGBD_OVERLAP", "1") != "0"  # side-stream backward (A/B switch)
-_DW1_STREAM = int(os.environ.get("RGBD_DW1_STREAM", "0"))  # side stream of dsam1's dW (A/B switch)
+_HIP = None
+_OVERLAP = os.environ.get("RGBD_OVERLAP", "1") != "0"  # side-stream launches (A/B switch)
+_PLAN_AHEAD = os.environ.get("RGBD_PLAN_AHEAD", "1") != "0"  # DSAM legs planned ahead (A/B switch)
 
 
-def side_stream(dev, idx=0):
-    """Per-device side streams (``idx`` 0, 1) the bf16 path runs its off-critical-path launches on."""
-    s = _SIDE_STREAMS.get((dev.index, idx))
+def _hip_stream(dev):
+    """A stream of its own (hipStreamCreateWithFlags, non-blocking) wrapped for torch.  torch's
+    Stream() hands out one of a fixed pool of 32 streams round-robin, so after enough stream
+    creations in a process a "new" capture stream can be the very stream used as a side branch,
+    which corrupts a captured graph; these streams are never in that pool."""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    with torch.cuda.device(dev):
+        h = ctypes.c_void_p()
+        rc = _HIP.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1))  # hipStreamNonBlocking
+        if rc != 0:
+            raise RuntimeError(f"hipStreamCreateWithFlags failed ({rc})")
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
+def side_stream(dev):
+    """The per-device side stream the bf16 path runs its off-critical-path launches on (a
+    process-lifetime stream of its own, never one of torch's pooled streams)."""
+    s = _SIDE_STREAMS.get(dev.index)
     if s is None:
-        s = _SIDE_STREAMS[(dev.index, idx)] = torch.cuda.Stream(device=dev)
+        s = _SIDE_STREAMS[dev.index] = _hip_stream(dev)
     return s
 
 
 class _Side:
     """Fork/join of launches onto the side stream (works eagerly and under graph capture: the side
-    stream joins the capture through the fork's event).  Inputs are recorded on the side stream
+    stream joins the capture through the fork's event).  One side stream, and never two forks
+    back to back from the same point of the main stream: captured graphs with either (a second
+    side stream forked beside the first, or the same one forked twice) made hipGraphLaunch
+    segfault on ROCm 7.2 once the process had captured and replayed other graphs (measured; see
+    DESIGN.md §5.1).  Inputs are recorded on the side stream
     so the allocator does not hand their memory to the main stream while side work reads it;
     outputs are recorded on the main stream at the join."""
 
-    def __init__(self, dev, enabled, idx=0):
+    def __init__(self, dev, enabled):
         self.on = enabled
         if enabled:
             self.main = torch.cuda.current_stream(dev)
-            self.side = side_stream(dev, idx)
+            self.side = side_stream(dev)
         self.outs = []
+        self.forked = False  # launches on the side stream since the last join
 
     def run(self, fn, *inputs):
         if not self.on:
             return fn()
         self.side.wait_stream(self.main)
+        self.forked = True
         for t in inputs:
             t.record_stream(self.side)
         with torch.cuda.stream(self.side):
@@ -60,8 +85,11 @@ class _Side:
         return out
 
     def join(self):
-        if not self.on:
+        # a join without a fork since the last one is a no-op: under graph capture, waiting on a
+        # side stream that is not part of the capture would tie the graph to outside work
+        if not self.on or not self.forked:
             return
+        self.forked = False
         self.main.wait_stream(self.side)
 
         def rec(o):
@@ -119,10 +147,9 @@ class HotPathFunction(torch.autograd.Function):
         sizes = [tuple(c.shape[2:]) for c in colors[:3]]
         bf16 = dtype == torch.bfloat16
         # bf16 on the GPU: the colour-map layout changes run beside the decomposition, the dsam1 /
-        # dsam2 packing beside dsam0 (one side stream each; joined before their consumers)
-        on = bf16 and pixel_values.is_cuda and cfg.get("overlap", True)
-        side = _Side(pixel_values.device, on)
-        side1 = _Side(pixel_values.device, on, idx=1)
+        # dsam2 packing beside dsam0 and the dW plans beside dsam1 / dsam2 (side stream; joined
+        # before their consumers)
+        side = _Side(pixel_values.device, bf16 and pixel_values.is_cuda and cfg.get("overlap", True))
         if bf16:
             nhwc = side.run(lambda: [ops.nchw_to_nhwc(c) for c in colors], *colors)
         if bf16:  # the code-presence masks the bf16 filter packing needs come out of the decomposition
@@ -143,7 +170,7 @@ class HotPathFunction(torch.autograd.Function):
             legs = [(ops.LEG_FWD, codes[k], *chans[k]) for k in range(3)]
             if training:
                 legs += [(ops.LEG_DX, codes[k], *chans[k]) for k in (1, 2)]
-            conv_plans = ops.dsam_plan(legs)
+            conv_plans = ops.dsam_plan(legs) if _PLAN_AHEAD else [None] * len(legs)
 
         def pack(k):
             return cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
@@ -153,17 +180,15 @@ class HotPathFunction(torch.autograd.Function):
         if bf16:
             packs = [pack(0)]
             side.join()  # the NHWC colour maps
-            packs += [side.run(lambda: pack(1), masks), side1.run(lambda: pack(2), masks)]
+            packs += side.run(lambda: [pack(1), pack(2)], masks)
             x_nhwc = [nhwc[0]]
             res_nhwc = nhwc[1:]
             # bf16 cascade entirely in NHWC: each DSAM adds its residual colour map in NHWC and writes
             # cp1[k+1] once, in the layout the next DSAM reads and the DGGM pass accepts
             for k in range(3):
-                if k == 2:
-                    side1.join()  # the dsam2 pack
                 if k == 1:
-                    side.join()  # the dsam1 pack
-                    if training:  # dW plans beside the rest of the forward
+                    side.join()  # the dsam1 / dsam2 packs
+                    if training and _PLAN_AHEAD:  # dW plans beside the rest of the forward
                         dw_plans = side.run(lambda: ops.dsam_plan([(ops.LEG_DW, codes[j], *chans[j]) for j in range(3)]),
                                             *codes)
                 bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
@@ -211,21 +236,17 @@ class HotPathFunction(torch.autograd.Function):
                                    if shape is None else "missing gradient for scale 0")
             G.append(g.to(dtype).contiguous())
         bf16 = dtype == torch.bfloat16
-        # bf16 on the GPU: the critical path is dX2 -> dX1 -> dW0 (main stream); the dW of dsam2
-        # (side stream 0, from the start) and the DGGM backward then the dW of dsam1 (side stream
-        # 1, once dX2 is done) run beside it, each on its own stream so dW1 need not wait for dW2
-        # (the latency-bound persistent kernels take CUs as the other streams' work drains; every
-        # kernel assigns its work dynamically)
-        on = bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True)
-        side = _Side(G[0].device, on)
-        side1 = _Side(G[0].device, on, idx=1)
+        # bf16 on the GPU: the critical path is dX2 -> dX1 -> dW0 (main stream); the DGGM backward
+        # and the dW of dsam2 / dsam1 run beside it on the side stream (their persistent kernels
+        # take CUs as the other stream's work drains; every kernel assigns its work dynamically)
+        side = _Side(G[0].device, bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True))
 
         def dggm_bwd():
             out = []
             for k, (dw, db) in enumerate(ops.dggm_fuse_bwd_multi(G, pixel_values, dggm_p[0::2], dggm_p[1::2])):
                 out += [dw.reshape(dggm_p[2 * k].shape).to(dggm_p[2 * k].dtype), db.to(dggm_p[2 * k + 1].dtype)]
             return out
-        grads_dggm = side1.run(dggm_bwd, *G, pixel_values)
+        grads_dggm = side.run(dggm_bwd, *G, pixel_values)
         # DSAM cascade backward: d cp1[k+1] = G[k+1] + dX_{k+1}.  bfloat16 keeps the cascade in
         # NHWC (dX written NHWC only, its residual G[k] converted once; bias sums from NHWC).
         hook = ctx.cfg.get("grad_hook")
@@ -237,9 +258,8 @@ class HotPathFunction(torch.autograd.Function):
                 dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k],
                                                           ctx.info, gout_nhwc=dcp_nhwc,
                                                           plan=ctx.dw_plans[k] if ctx.dw_plans else None)
-                if k == 0:  # dW0 needs nothing from the side streams; the hook and the caller do
+                if k == 0:  # dW0 needs nothing from the side stream; the hook and the caller do
                     side.join()
-                    side1.join()
                 gk = []
                 for i in range(4):
                     gk += [dconv[i], dbias[i]]
@@ -248,9 +268,8 @@ class HotPathFunction(torch.autograd.Function):
                     hook(2 - k, gk if k > 0 else gk + grads_dggm)
                 return gk
             if k > 0:
-                grads_dsam[k] = (side1 if k == 1 and _DW1_STREAM else side).run(dsam_dw, dcp_nhwc, ctx.x_nhwc[k],
-                                                                               ctx.codes[k], ctx.info)
-            else:  # the last launches of the backward: on the main stream, joins after them
+                grads_dsam[k] = side.run(dsam_dw, dcp_nhwc, ctx.x_nhwc[k], ctx.codes[k], ctx.info)
+            else:  # the last launches of the backward: on the main stream, the join after them
                 grads_dsam[k] = dsam_dw()
             if k > 0:
                 if bf16:
