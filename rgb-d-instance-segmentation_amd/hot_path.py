@@ -27,6 +27,7 @@ _SIDE_STREAMS = {}
 _HIP = None
 _OVERLAP = os.environ.get("RGBD_OVERLAP", "1") != "0"  # side-stream launches (A/B switch)
 _PLAN_AHEAD = os.environ.get("RGBD_PLAN_AHEAD", "1") != "0"  # DSAM legs planned ahead (A/B switch)
+_DW1_MAIN = os.environ.get("RGBD_DW1_MAIN", "0") != "0"  # dsam1's dW on the main stream (A/B switch)
 
 
 def _hip_stream(dev):
@@ -236,9 +237,9 @@ class HotPathFunction(torch.autograd.Function):
                                    if shape is None else "missing gradient for scale 0")
             G.append(g.to(dtype).contiguous())
         bf16 = dtype == torch.bfloat16
-        # bf16 on the GPU: the critical path is dX2 -> dX1 -> dW0 (main stream); the DGGM backward
-        # and the dW of dsam2 / dsam1 run beside it on the side stream (their persistent kernels
-        # take CUs as the other stream's work drains; every kernel assigns its work dynamically)
+        # bf16 on the GPU: the main stream runs dX2 -> dX1 -> dW1 -> dW0; the DGGM backward and the
+        # dW of dsam2 run beside it on the side stream (their persistent kernels take CUs as the
+        # other stream's work drains; every kernel assigns its work dynamically)
         side = _Side(G[0].device, bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True))
 
         def dggm_bwd():
@@ -253,31 +254,38 @@ class HotPathFunction(torch.autograd.Function):
         dcp = G[3]
         dcp_nhwc = ops.nchw_to_nhwc(dcp)
         grads_dsam = [None, None, None]
-        for k in (2, 1, 0):
-            def dsam_dw(k=k, dcp=dcp, dcp_nhwc=dcp_nhwc):
-                dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k],
-                                                          ctx.info, gout_nhwc=dcp_nhwc,
-                                                          plan=ctx.dw_plans[k] if ctx.dw_plans else None)
-                if k == 0:  # dW0 needs nothing from the side stream; the hook and the caller do
-                    side.join()
-                gk = []
-                for i in range(4):
-                    gk += [dconv[i], dbias[i]]
-                gk.append(dproj)
-                if hook is not None:  # DDP: this module's all-reduce runs under the rest of the cascade
-                    hook(2 - k, gk if k > 0 else gk + grads_dggm)
-                return gk
-            if k > 0:
-                grads_dsam[k] = side.run(dsam_dw, dcp_nhwc, ctx.x_nhwc[k], ctx.codes[k], ctx.info)
-            else:  # the last launches of the backward: on the main stream, the join after them
-                grads_dsam[k] = dsam_dw()
-            if k > 0:
-                if bf16:
-                    dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], None, want_nhwc=True,
-                                                      want_nchw=False, gin_nhwc=ops.nchw_to_nhwc(G[k]),
-                                                      plan=ctx.dx_plans.get(k))
-                else:
-                    dcp, dcp_nhwc = ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k], want_nhwc=(k > 1))
+        def dsam_dw(k, dcp, dcp_nhwc):
+            dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
+                                                      gout_nhwc=dcp_nhwc,
+                                                      plan=ctx.dw_plans[k] if ctx.dw_plans else None)
+            if k == 0:  # dW0 needs nothing from the side stream; the hook and the caller do
+                side.join()
+            gk = []
+            for i in range(4):
+                gk += [dconv[i], dbias[i]]
+            gk.append(dproj)
+            if hook is not None:  # DDP: this module's all-reduce runs under the rest of the cascade
+                hook(2 - k, gk if k > 0 else gk + grads_dggm)
+            return gk
+
+        def dsam_dx(k, dcp, dcp_nhwc):
+            if bf16:
+                return ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], None, want_nhwc=True,
+                                         want_nchw=False, gin_nhwc=ops.nchw_to_nhwc(G[k]), plan=ctx.dx_plans.get(k))
+            return ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k], want_nhwc=(k > 1))
+        # dW2 beside the cascade; dX2, dX1, then dW1 and dW0 on the main stream (the side stream
+        # already carries the DGGM backward, dW2 and, with in-backward optimizer steps, the
+        # dsam2 update)
+        grads_dsam = [None, None, None]
+        grads_dsam[2] = side.run(lambda: dsam_dw(2, dcp, dcp_nhwc), dcp_nhwc, ctx.x_nhwc[2], ctx.codes[2], ctx.info)
+        dcp1, dcp1_nhwc = dsam_dx(2, dcp, dcp_nhwc)
+        dcp0, dcp0_nhwc = dsam_dx(1, dcp1, dcp1_nhwc)
+        if _DW1_MAIN:
+            grads_dsam[1] = dsam_dw(1, dcp1, dcp1_nhwc)
+        else:
+            grads_dsam[1] = side.run(lambda: dsam_dw(1, dcp1, dcp1_nhwc), dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1],
+                                     ctx.info)
+        grads_dsam[0] = dsam_dw(0, dcp0, dcp0_nhwc)  # the last launches of the backward, the join after them
         pgrads = grads_dsam[0] + grads_dsam[1] + grads_dsam[2] + grads_dggm
         return (None, None, None, None, None, None, None, *pgrads)
 
