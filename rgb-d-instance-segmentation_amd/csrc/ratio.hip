@@ -748,14 +748,13 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
     if constexpr (PHASE == 1) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) add_stats(ssum[t], ssq[t], a2[t], full, x0, row_ok);
-      if (att) {  // raw fusion output for k_rp_gate: [tile][wave][t][u][lane][4 px], 512 B per store
+      if (att) {  // raw fusion output for k_rp_gate: [tile][wave][t][lane][u][4 px], 1 KiB per store
         bf16_t* ft = att + ((tile * 8 + wave) * 16) * 256;
 #pragma unroll
         for (int t = 0; t < 8; ++t)
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            *reinterpret_cast<uint2*>(ft + ((t * 2 + u) * 64 + lane) * 4) =
-                make_uint2(pack_bf16x2(a2[t][u][0], a2[t][u][1]), pack_bf16x2(a2[t][u][2], a2[t][u][3]));
+          *reinterpret_cast<uint4*>(ft + (t * 64 + lane) * 8) =
+              make_uint4(pack_bf16x2(a2[t][0][0], a2[t][0][1]), pack_bf16x2(a2[t][0][2], a2[t][0][3]),
+                         pack_bf16x2(a2[t][1][0], a2[t][1][1]), pack_bf16x2(a2[t][1][2], a2[t][1][3]));
       }
       continue;
     }
@@ -890,20 +889,19 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
   const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
   const long long ntiles = (long long)B * tiles_x * tiles_y;
   const long long HW = (long long)H * W;
-  // this wave's raw fusion output of a tile: lane (r, g) has channel 16t + r, pixels 16u + 4g + j;
+  // this wave's raw fusion output of a tile ([t][lane][u][4 px]): lane (r, g) has channel 16t + r,
+  // pixels 16u + 4g + j;
   // the next tile's 8 KB are loaded while the current one computes
   uint2 nxt[8][2];
   auto fetch = [&](long long tl) {
     if (tl >= ntiles) return;
     const bf16_t* ft = fus + ((tl * 8 + wave) * 16) * 256;
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {  // read once: non-temporal
-        const unsigned long long q =
-            __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ft + ((t * 2 + u) * 64 + lane) * 4));
-        nxt[t][u] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
-      }
+    for (int t = 0; t < 8; ++t) {  // read once: non-temporal, 16 B per lane (1 KiB per wave load)
+      const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ft + (t * 64 + lane) * 8));
+      nxt[t][0] = make_uint2(q[0], q[1]);
+      nxt[t][1] = make_uint2(q[2], q[3]);
+    }
   };
   fetch(blockIdx.x);
   for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
