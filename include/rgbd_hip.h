@@ -270,6 +270,33 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        unsigned long long* seed_counter, float* ratio, void* ws, void* stream);
 
+/* ---------------------------------------------------------------- f3 point-sampled mask terms
+ * The mask terms of the Mask2Former matcher and loss (transformers 5.15 modeling_mask2former.py,
+ * the library the reference trains through): sample_point (:245-275), the matcher's pair-wise
+ * sigmoid-CE and dice costs (:328-375, :445-470) and loss_masks' sigmoid-CE / dice over the
+ * matched pairs (:278-325, :580-630).  All float32.
+ * rgbd_point_sample: out[m][p] = grid_sample(maps[m] ([h][w]), 2*coords - 1, bilinear,
+ *   align_corners=False, zeros) at coords[m / maps_per_coord][p] = (x, y) in [0, 1]^2 (one point
+ *   set per group of maps_per_coord consecutive maps);
+ *   rgbd_point_sample_bwd ADDS the transposed scatter of gout into gmaps (f32 atomics).
+ * rgbd_match_cost: image b's cost [Q][T_b] at cost + coff[b] = w_mask * CE + w_class *
+ *   class_cost + w_dice * DICE over pred [B][Q][P] and the targets' sampled labels at tgt +
+ *   toff[b]*P (toff int [B+1], coff int64 [B], device), clamped to +-1e10, NaN -> 0.
+ * rgbd_point_losses: per row n of logits / labels [N][P]: ce[n] = mean BCEWithLogits, dice[n] =
+ *   1 - (2 sum sig*y + 1) / (sum sig + sum y + 1), sums[n] = (sum sig*y, sum sig, sum y);
+ *   rgbd_point_losses_bwd: glogits [N][P] from the per-row upstream gradients g_ce, g_dice [N]. */
+int rgbd_point_sample(const float* maps, int nmaps, int h, int w, const float* coords, int maps_per_coord, int P,
+                      float* out, void* stream);
+int rgbd_point_sample_bwd(const float* gout, int nmaps, int h, int w, const float* coords, int maps_per_coord,
+                          int P, float* gmaps, void* stream);
+int rgbd_match_cost(const float* pred, int B, int Q, int P, const float* tgt, const int* toff,
+                    const float* class_cost, const long long* coff, float w_mask, float w_class, float w_dice,
+                    float* cost, void* stream);
+int rgbd_point_losses(const float* logits, const float* labels, int N, int P, float* ce, float* dice,
+                      float* sums, void* stream);
+int rgbd_point_losses_bwd(const float* logits, const float* labels, int N, int P, const float* sums,
+                          const float* g_ce, const float* g_dice, float* glogits, void* stream);
+
 /* ---------------------------------------------------------------- f2 deformable attention
  * Replaces multi_scale_deformable_attention (transformers 5.15 modeling_mask2former.py:798-837),
  * the core of each pixel-decoder encoder layer (:1011).  value: dtype [B][S][NH][D] with

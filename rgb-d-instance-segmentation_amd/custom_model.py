@@ -17,7 +17,7 @@ from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation,
 from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
                                                                   Mask2FormerPixelLevelModuleOutput)
 
-from . import deform_attn, mask_predictor, matcher
+from . import deform_attn, mask_predictor, point_loss
 from .hot_path import hot_path
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
@@ -124,8 +124,9 @@ class CustomMask2FormerForUniversalSegmentation(Mask2FormerForUniversalSegmentat
         super().__init__(config)
         set_seed(42)                                                    # Q17: after HF init
         self.model = CustomMask2FormerModel(config, version=version)
-        # f3: the loss's Hungarian matcher solves its assignments on the GPU (no host round trip)
-        matcher.install(self.criterion)
+        # f3: the loss's point-sampled mask terms and its matcher's costs on the HIP kernels, the
+        # Hungarian assignments solved on the GPU (no host round trip)
+        point_loss.install(self.criterion)
 
     def set_compute_dtype(self, dtype):
         self.model.pixel_level_module.set_compute_dtype(dtype)

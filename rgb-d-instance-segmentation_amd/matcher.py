@@ -6,9 +6,10 @@ Per image it builds the (queries x targets) cost — class probability, point-sa
 dice — and calls ``scipy.optimize.linear_sum_assignment(cost_matrix.cpu())``: one device->host
 sync and one CPU solve per image per output.
 
-``HipHungarianMatcher`` keeps the cost construction op for op (same torch calls in the same
-order, so the same ``torch.rand`` draws and bit-identical cost matrices) and solves all images'
-matrices in one ``rgbd_lsa_batch`` launch (csrc/lsap.hip: scipy's algorithm in float64, same
+``HipHungarianMatcher`` draws the same ``torch.rand`` points in the same order, builds every
+image's cost on the GPU kernels of point_loss.py (sampling, pair-wise CE / dice, clamping in one
+launch for all images; ``matching_cost`` keeps the reference's torch form as the checker) and
+solves all images' matrices in one ``rgbd_lsa_batch`` launch (csrc/lsap.hip: scipy's algorithm in float64, same
 optimum including ties).  The matched indices stay on the GPU as int64 tensors, which the loss
 indexes with directly.  ``install(model)`` swaps the class of every HF matcher in place.
 """
@@ -43,8 +44,10 @@ def matching_cost(matcher, masks_queries_logits, class_queries_logits, mask_labe
 class HipHungarianMatcher(Mask2FormerHungarianMatcher):
     @torch.no_grad()
     def forward(self, masks_queries_logits, class_queries_logits, mask_labels, class_labels):
-        costs = [matching_cost(self, masks_queries_logits, class_queries_logits, mask_labels, class_labels, i)
-                 for i in range(masks_queries_logits.shape[0])]
+        # point sampling + pair-wise CE / dice of all images on the GPU kernels (point_loss.py),
+        # the same torch.rand draws as the reference; matching_cost above is the torch form
+        from .point_loss import match_costs
+        costs = match_costs(self, masks_queries_logits.float(), class_queries_logits, mask_labels, class_labels)
         return ops.linear_sum_assignment_batch(costs)
 
 

@@ -1,0 +1,178 @@
+"""f3: the point-sampled mask terms of the Mask2Former matcher and loss on the GPU.
+
+Reference (the library the reference trains through, transformers 5.15 modeling_mask2former.py):
+``Mask2FormerHungarianMatcher.forward`` (:412-483) builds, per image, a point-sampled sigmoid-CE
+and dice cost against every target (:445-470); ``Mask2FormerLoss.loss_masks`` (:580-630) samples
+12 544 points per matched pair by uncertainty (:671-724) and averages sigmoid-CE and dice over
+them.  Here the sampling (``rgbd_point_sample`` / ``_bwd``), the cost reduction
+(``rgbd_match_cost``, all images in one launch) and the loss reductions with their backward
+(``rgbd_point_losses`` / ``_bwd``) are HIP kernels (csrc/point_loss.hip).  The random point
+coordinates (``torch.rand``), the uncertainty ``torch.topk`` and the index gathers stay torch
+calls in the reference's order, so the RNG stream and the selected points are the reference's.
+
+``install(model)`` swaps the HF loss (and its matcher) for ``HipMask2FormerLoss`` /
+``matcher.HipHungarianMatcher`` in place; ``uninstall`` restores them.
+"""
+import torch
+from torch import nn
+from transformers.models.mask2former.modeling_mask2former import Mask2FormerHungarianMatcher, Mask2FormerLoss
+
+from . import _lib
+from ._lib import check
+from .ops import _need_cuda, _p, _stream
+
+
+def point_sample(maps: torch.Tensor, coords: torch.Tensor) -> torch.Tensor:
+    """maps float32 [N, h, w]; coords [G, P, 2] in [0, 1] (x, y), one point set per N / G
+    consecutive maps -> [N, P]: ``sample_point(maps[:, None], coords, align_corners=False)``
+    (modeling_mask2former.py:245-275).  Differentiable in ``maps``."""
+    return _PointSample.apply(maps, coords)
+
+
+def _sample(maps, coords):
+    maps = maps.detach().float().contiguous()
+    coords = coords.detach().float().contiguous()
+    _need_cuda(maps, coords)
+    N, h, w = maps.shape
+    G, P, _ = coords.shape
+    if N % max(G, 1) or (N and G == 0):
+        raise ValueError(f"point_sample: {N} maps for {G} point sets")
+    out = torch.empty((N, P), dtype=torch.float32, device=maps.device)
+    if N:
+        check(_lib.lib().rgbd_point_sample(_p(maps), N, h, w, _p(coords), N // G, P, _p(out), _stream(maps.device)),
+              "rgbd_point_sample")
+    return out
+
+
+class _PointSample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, maps, coords):
+        ctx.save_for_backward(coords)
+        ctx.shape = tuple(maps.shape)
+        return _sample(maps, coords)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (coords,) = ctx.saved_tensors
+        N, h, w = ctx.shape
+        g = gout.float().contiguous()
+        gmaps = torch.zeros((N, h, w), dtype=torch.float32, device=g.device)
+        if N:
+            c = coords.float().contiguous()
+            check(_lib.lib().rgbd_point_sample_bwd(_p(g), N, h, w, _p(c), N // c.shape[0], c.shape[1], _p(gmaps),
+                                                   _stream(g.device)), "rgbd_point_sample_bwd")
+        return gmaps, None
+
+
+class _PointLosses(torch.autograd.Function):
+    """(logits [N, P], labels [N, P]) -> per-row (mean BCEWithLogits, dice)
+    (sigmoid_cross_entropy_loss / dice_loss before their sums, :278-325)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        x = logits.detach().float().contiguous()
+        y = labels.detach().float().contiguous()
+        _need_cuda(x, y)
+        N, P = x.shape
+        ce = torch.empty((N,), dtype=torch.float32, device=x.device)
+        dice = torch.empty_like(ce)
+        sums = torch.empty((N, 3), dtype=torch.float32, device=x.device)
+        check(_lib.lib().rgbd_point_losses(_p(x), _p(y), N, P, _p(ce), _p(dice), _p(sums), _stream(x.device)),
+              "rgbd_point_losses")
+        ctx.save_for_backward(x, y, sums)
+        return ce, dice
+
+    @staticmethod
+    def backward(ctx, g_ce, g_dice):
+        x, y, sums = ctx.saved_tensors
+        N, P = x.shape
+        g_ce = torch.zeros((N,), device=x.device) if g_ce is None else g_ce.float().contiguous()
+        g_dice = torch.zeros((N,), device=x.device) if g_dice is None else g_dice.float().contiguous()
+        gx = torch.empty_like(x)
+        check(_lib.lib().rgbd_point_losses_bwd(_p(x), _p(y), N, P, _p(sums), _p(g_ce), _p(g_dice), _p(gx),
+                                               _stream(x.device)), "rgbd_point_losses_bwd")
+        return gx, None
+
+
+def match_costs(matcher, masks_queries_logits, class_queries_logits, mask_labels, class_labels):
+    """The matcher's cost matrices of every image ([Q, T_b] each), as
+    Mask2FormerHungarianMatcher.forward builds them (:445-470): one ``torch.rand(1, P, 2)`` per
+    image in image order, then the point sampling and the pair-wise CE / dice reduction on the
+    GPU (all images' costs in one launch)."""
+    B, Q, h, w = masks_queries_logits.shape
+    P = matcher.num_points
+    dev = masks_queries_logits.device
+    pts, tgts, ccls, toff, coff = [], [], [], [0], [0]
+    for i in range(B):
+        probs = class_queries_logits[i].softmax(-1)
+        ccls.append((-probs[:, class_labels[i]]).float().reshape(-1))
+        pts.append(torch.rand(1, P, 2, device=dev))
+        tm = mask_labels[i].to(masks_queries_logits)
+        tgts.append(_sample(tm.reshape(-1, *tm.shape[-2:]), pts[-1]) if tm.shape[0] else
+                    torch.empty((0, P), device=dev))
+        toff.append(toff[-1] + tm.shape[0])
+        coff.append(coff[-1] + Q * tm.shape[0])
+    pred = _sample(masks_queries_logits.reshape(B * Q, h, w), torch.cat(pts))
+    tgt = torch.cat(tgts) if toff[-1] else torch.zeros((1, P), device=dev)
+    cls = torch.cat(ccls) if coff[-1] else torch.zeros((1,), device=dev)
+    cost = torch.empty((max(coff[-1], 1),), dtype=torch.float32, device=dev)
+    toff_t = torch.tensor(toff, dtype=torch.int32).to(dev, non_blocking=True)
+    coff_t = torch.tensor(coff[:-1], dtype=torch.int64).to(dev, non_blocking=True)
+    check(_lib.lib().rgbd_match_cost(_p(pred), B, Q, P, _p(tgt), _p(toff_t), _p(cls), _p(coff_t),
+                                     float(matcher.cost_mask), float(matcher.cost_class), float(matcher.cost_dice),
+                                     _p(cost), _stream(dev)), "rgbd_match_cost")
+    return [cost[coff[i]:coff[i + 1]].view(Q, toff[i + 1] - toff[i]) for i in range(B)]
+
+
+class HipMask2FormerLoss(Mask2FormerLoss):
+    """Mask2FormerLoss with loss_masks' sampling and reductions on the GPU kernels."""
+
+    def loss_masks(self, masks_queries_logits, mask_labels, indices, num_masks):
+        src_idx = self._get_predictions_permutation_indices(indices)
+        tgt_idx = self._get_targets_permutation_indices(indices)
+        pred_masks = masks_queries_logits[src_idx]  # [N, h, w]
+        target_masks, _ = self._pad_images_to_max_in_batch(mask_labels)
+        target_masks = target_masks[tgt_idx]
+        N = pred_masks.shape[0]
+        P = self.num_points
+        with torch.no_grad():
+            # sample_points_using_uncertainty (:671-724), same torch.rand / topk calls and order
+            n_over = int(P * self.oversample_ratio)
+            coords = torch.rand(N, n_over, 2, device=pred_masks.device)
+            unc = -(torch.abs(_sample(pred_masks, coords)))
+            k = int(self.importance_sample_ratio * P)
+            idx = torch.topk(unc, k=k, dim=1)[1]
+            shift = n_over * torch.arange(N, dtype=torch.long, device=pred_masks.device)
+            idx += shift[:, None]
+            coords = coords.view(-1, 2)[idx.view(-1), :].view(N, k, 2)
+            if P - k > 0:
+                coords = torch.cat([coords, torch.rand(N, P - k, 2, device=pred_masks.device)], dim=1)
+            labels = _sample(target_masks.to(pred_masks).reshape(N, *target_masks.shape[-2:]), coords)
+        logits = point_sample(pred_masks, coords)
+        ce, dice = _PointLosses.apply(logits, labels)
+        return {"loss_mask": ce.sum() / num_masks, "loss_dice": dice.sum() / num_masks}
+
+
+def install(model: nn.Module) -> int:
+    """Swap every HF Mask2FormerLoss (and its matcher) in ``model`` for the HIP versions."""
+    from .matcher import HipHungarianMatcher
+    n = 0
+    for m in model.modules():
+        if type(m) is Mask2FormerLoss:
+            m.__class__ = HipMask2FormerLoss
+            n += 1
+        if type(m) is Mask2FormerHungarianMatcher:
+            m.__class__ = HipHungarianMatcher
+    return n
+
+
+def uninstall(model: nn.Module) -> int:
+    from .matcher import HipHungarianMatcher
+    n = 0
+    for m in model.modules():
+        if type(m) is HipMask2FormerLoss:
+            m.__class__ = Mask2FormerLoss
+            n += 1
+        if type(m) is HipHungarianMatcher:
+            m.__class__ = Mask2FormerHungarianMatcher
+    return n

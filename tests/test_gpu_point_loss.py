@@ -1,0 +1,97 @@
+"""f3: the point-sampled mask terms on the GPU kernels (csrc/point_loss.hip, rgbd_amd/point_loss.py)
+against the library code the reference trains through (transformers 5.15
+modeling_mask2former.py): sample_point (:245-275) and its autograd, the matcher's cost matrices
+(:445-470, restated op for op in matcher.matching_cost) and Mask2FormerLoss.loss_masks
+(:580-630) with its gradient.  Same torch RNG state on both sides, so the same random points.
+Tolerances: float32 reductions in a different order — 1e-5 relative on sampled values, 1e-5 relative on
+costs and losses, 1e-4 relative on gradients."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from rgbd_amd import matcher, point_loss
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, e):
+    return float((a - e).abs().max() / (e.abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("N,G,h,w,P", [(6, 1, 30, 40, 1000), (5, 5, 17, 23, 777), (8, 2, 120, 160, 12544)])
+def test_point_sample_matches_grid_sample(N, G, h, w, P):
+    g = torch.Generator(device=DEV).manual_seed(N * 7 + P)
+    maps = torch.randn((N, h, w), generator=g, device=DEV)
+    coords = torch.rand((G, P, 2), generator=g, device=DEV)
+    coords[0, :4] = torch.tensor([[0.0, 0.0], [1.0, 1.0], [0.0, 1.0], [0.999999, 0.5]], device=DEV)  # edges
+    ref_c = coords.repeat_interleave(N // G, dim=0)
+    mref = maps.clone().requires_grad_(True)
+    ref = F.grid_sample(mref[:, None], 2.0 * ref_c[:, :, None] - 1.0, align_corners=False)[:, 0, :, 0]
+    mh = maps.clone().requires_grad_(True)
+    got = point_loss.point_sample(mh, coords)
+    assert float((got - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+    go = torch.randn(ref.shape, generator=g, device=DEV)
+    ref.backward(go)
+    got.backward(go)
+    assert _rel(mh.grad, mref.grad) <= 1e-5
+
+
+def _case(seed, B=3, Q=100, L=49, H=60, W=80, counts=(5, 0, 23)):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    masks = torch.randn((B, Q, H, W), generator=g, device=DEV)
+    classes = torch.randn((B, Q, L), generator=g, device=DEV)
+    mask_labels, class_labels = [], []
+    for n in counts:
+        mask_labels.append((torch.rand((n, H * 4, W * 4), generator=g, device=DEV) > 0.7).float())
+        class_labels.append(torch.randint(0, L - 1, (n,), generator=g, device=DEV))
+    return masks, classes, mask_labels, class_labels
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_match_costs_match_reference(seed):
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerHungarianMatcher
+    m = Mask2FormerHungarianMatcher(cost_class=2.0, cost_mask=5.0, cost_dice=5.0, num_points=12544)
+    masks, classes, ml, cl = _case(seed)
+    torch.manual_seed(21 + seed)
+    ref = [matcher.matching_cost(m, masks, classes, ml, cl, i) for i in range(masks.shape[0])]
+    torch.manual_seed(21 + seed)
+    got = point_loss.match_costs(m, masks, classes, ml, cl)
+    for r, h in zip(ref, got):
+        assert r.shape == h.shape
+        if r.numel():
+            assert _rel(h, r) <= 1e-5, _rel(h, r)
+
+
+def test_loss_masks_and_grad_match_reference():
+    from transformers import Mask2FormerConfig
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerLoss
+    cfg = Mask2FormerConfig(num_labels=48)
+    ref_loss = Mask2FormerLoss(cfg, weight_dict={"loss_cross_entropy": 2.0, "loss_mask": 5.0, "loss_dice": 5.0})
+    hip_loss = Mask2FormerLoss(cfg, weight_dict={"loss_cross_entropy": 2.0, "loss_mask": 5.0, "loss_dice": 5.0})
+    hip_loss.__class__ = point_loss.HipMask2FormerLoss
+    masks, classes, ml, cl = _case(3, B=2, counts=(7, 12))
+    indices = [(torch.arange(n, device=DEV) * 3, torch.arange(n, device=DEV).flip(0)) for n in (7, 12)]
+    mr = masks.clone().requires_grad_(True)
+    mh = masks.clone().requires_grad_(True)
+    torch.manual_seed(5)
+    r = ref_loss.loss_masks(mr, ml, indices, num_masks=19.0)
+    torch.manual_seed(5)
+    h = hip_loss.loss_masks(mh, ml, indices, num_masks=19.0)
+    for k in ("loss_mask", "loss_dice"):
+        assert abs(float(h[k]) - float(r[k])) <= 1e-5 * abs(float(r[k])) + 1e-7, (k, float(h[k]), float(r[k]))
+    (r["loss_mask"] * 5 + r["loss_dice"] * 5).backward()
+    (h["loss_mask"] * 5 + h["loss_dice"] * 5).backward()
+    assert _rel(mh.grad, mr.grad) <= 1e-4, _rel(mh.grad, mr.grad)
+
+
+def test_install_swaps_loss_and_matcher():
+    from transformers import Mask2FormerConfig
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerLoss
+    cfg = Mask2FormerConfig(num_labels=48)
+    holder = torch.nn.Module()
+    holder.criterion = Mask2FormerLoss(cfg, weight_dict={"loss_cross_entropy": 2.0, "loss_mask": 5.0, "loss_dice": 5.0})
+    assert point_loss.install(holder) == 1
+    assert isinstance(holder.criterion, point_loss.HipMask2FormerLoss)
+    assert isinstance(holder.criterion.matcher, matcher.HipHungarianMatcher)
+    assert point_loss.uninstall(holder) == 1 and type(holder.criterion) is Mask2FormerLoss
