@@ -341,6 +341,26 @@ int rgbd_mask_logits(int dtype, const void* emb, const void* pix, int B, int Q, 
 int rgbd_mask_attention(int dtype, const void* logits, int B, int Q, int H, int W, int th, int tw,
                         int heads, uint8_t* attn, void* stream);
 
+/* ---------------------------------------------------------------- f1 masked cross-attention
+ * The attention core of nn.MultiheadAttention's math path as the masked-attention decoder layers
+ * call it (transformers 5.15 modeling_mask2former.py:1640-1647 with the mask of :2048-2055), all
+ * float32: per bh (= batch * heads + head), S = (q * scale) k^T, masked entries -inf,
+ * P = softmax(S), out = P v.  Sequence-major, as the module's projections lay them out:
+ * q [Q][BH][head_dim], k / v [L][BH][head_dim], out [Q][BH][head_dim], lse [Q][BH] (log-sum-exp
+ * of the masked scaled scores, saved for the backward); mask bool bytes [BH][Q][L] (1 = not
+ * allowed).  head_dim == 32.  A fully masked row gives NaN, as torch's softmax does.
+ * ws: rgbd_masked_attn_fwd_workspace_size(BH, Q, L) bytes (per-key-split partials).
+ * rgbd_masked_attn_bwd: dq, dk, dv (OVERWRITTEN) from dout; deterministic (no atomics);
+ *   ws: rgbd_masked_attn_bwd_workspace_size(BH, Q, L) bytes.
+ * q, k, v, out, dout, dk, dv 16-byte aligned. */
+size_t rgbd_masked_attn_fwd_workspace_size(int BH, int Q, int L);
+int rgbd_masked_attn_fwd(const float* q, const float* k, const float* v, const uint8_t* mask, int BH, int Q, int L,
+                         int head_dim, float scale, float* out, float* lse, void* ws, void* stream);
+size_t rgbd_masked_attn_bwd_workspace_size(int BH, int Q, int L);
+int rgbd_masked_attn_bwd(const float* q, const float* k, const float* v, const uint8_t* mask, const float* out,
+                         const float* lse, const float* dout, int BH, int Q, int L, int head_dim, float scale,
+                         float* dq, float* dk, float* dv, void* ws, void* stream);
+
 /* ---------------------------------------------------------------- f4 instance post-processing
  * Replaces Mask2FormerImageProcessor.post_process_instance_segmentation (transformers 5.15
  * image_processing_mask2former.py:627-744; called by the reference's process_prediction,

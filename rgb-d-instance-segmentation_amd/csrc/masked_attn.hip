@@ -1,0 +1,383 @@
+// f1: the masked cross-attention core of the Mask2Former decoder layers (gfx950, float32).
+//
+// Reference (third-party, in the model the reference trains, custom_model.py:37-53):
+// transformers 5.15 Mask2FormerMaskedAttentionDecoderLayer.forward_post (modeling_mask2former.py
+// :1640-1647) calls nn.MultiheadAttention with the mask predictor's boolean attention mask
+// (:2048-2055); torch's math path computes, per (batch*head) bh,
+//     S = (q * head_dim^-1/2) k^T + where(mask, -inf, 0),  P = softmax(S),  O = P v
+// (L = the level's pixels).  The in / out projections stay the module's GEMMs (library, genuine
+// dense contractions); this file is the non-GEMM part.  Layout is sequence-major, as the
+// projections produce it (no head transposes): q / o [Q][BH][32], k / v [L][BH][32], the
+// per-row lse / delta [Q][BH]; the mask is the predictor's [BH][Q][L] bytes.
+//
+// Shapes here are few queries (100) against many keys (300 .. 19 200 per level), so the work is
+// split over KEY ranges (flash-decoding style) to fill 256 CUs:
+//   forward   one thread per query, a workgroup per (bh, key split): the K / V rows are the same
+//             for every lane, so they are scalar loads (SGPR operands of the FMAs); scores in
+//             chunks of 16 keys (mask bits from one 16-byte load) with one online-softmax rescale
+//             per chunk; partial (max, sum, o[32]) per split, merged by k_attn_merge, which also
+//             writes the row log-sum-exp the backward reuses.
+//   dK / dV   one thread per key, a workgroup per (bh, 256 keys): q_scaled / dO rows per query are
+//             scalar loads; p = exp(s - lse), ds = p (dO.v - delta); dv += p dO, dk += ds q_scaled.
+//   dQ        like the forward (thread per query, key splits), partial dq per split summed in split
+//             order by k_attn_dq_sum — no atomics anywhere, the backward is deterministic.
+#include <cmath>
+
+#include "common.hpp"
+
+using namespace rgbd;
+
+namespace {
+
+constexpr int HD = 32;      // head dim (hidden 256 / 8 heads)
+constexpr int QW = 128;     // queries per forward / dQ workgroup (one per thread)
+constexpr int KS = 64;      // key-split granularity
+constexpr int KC = 16;      // keys per online-softmax chunk
+constexpr int KVW = 256;    // keys per dK / dV workgroup (one per thread)
+
+struct AttnArgs {
+  const float* q;        // [Q][BH][HD] (unscaled)
+  const float* k;        // [L][BH][HD]
+  const float* v;        // [L][BH][HD]
+  const uint8_t* mask;   // [BH][Q][L] bool, true = not allowed
+  float* o;              // [Q][BH][HD]
+  float* lse;            // [Q][BH] log-sum-exp of the scaled, masked scores
+  float* part_o;         // [nsplit][Q][BH][HD]
+  float* part_ml;        // [nsplit][Q][BH][2] = (max, sum)
+  int BH, Q, L;
+  int nsplit, span;      // key range of split s: [s*span, min(L, (s+1)*span)), span % KS == 0
+  float scale;
+  bool vec_mask;         // mask rows 16-byte aligned (L % 16 == 0)
+};
+
+// Rows of K / V (forward, dQ) and of q_scaled / dO (dK / dV) are the same for every lane of a
+// wave: they are read through the constant address space, so they arrive as scalar loads into
+// SGPRs and feed the FMAs as scalar operands — no LDS staging, no broadcast traffic.
+typedef const float __attribute__((address_space(4))) cfloat;
+
+__device__ __forceinline__ const cfloat* uniform_row(const float* base, long long row, int BH, int bh) {
+  return (const cfloat*)(base + (row * BH + bh) * HD);
+}
+
+// Packed fp32 (v_pk_fma_f32): a 32-wide row is 16 float pairs; dot products keep two partial
+// sums (even / odd dims) added at the end.
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int HP = HD / 2;
+
+__device__ __forceinline__ f2 pair(const cfloat* row, int c) { return f2{row[2 * c], row[2 * c + 1]}; }
+
+__device__ __forceinline__ float dot_row(const f2 (&x)[HP], const cfloat* row) {
+  f2 acc = {0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < HP; ++c) acc = __builtin_elementwise_fma(x[c], pair(row, c), acc);
+  return acc.x + acc.y;
+}
+
+__device__ __forceinline__ void axpy_row(f2 (&acc)[HP], float a, const cfloat* row) {
+  const f2 a2 = {a, a};
+#pragma unroll
+  for (int c = 0; c < HP; ++c) acc[c] = __builtin_elementwise_fma(a2, pair(row, c), acc[c]);
+}
+
+__device__ __forceinline__ void load_row(f2 (&x)[HP], const float* row, bool ok, float mul) {
+#pragma unroll
+  for (int c = 0; c < HP; ++c) {
+    const float2 t = ok ? *reinterpret_cast<const float2*>(row + 2 * c) : make_float2(0.f, 0.f);
+    x[c] = f2{t.x * mul, t.y * mul};
+  }
+}
+
+__device__ __forceinline__ void store_row(float* row, const f2 (&x)[HP]) {
+#pragma unroll
+  for (int c = 0; c < HD / 4; ++c)
+    *reinterpret_cast<float4*>(row + 4 * c) = make_float4(x[2 * c].x, x[2 * c].y, x[2 * c + 1].x, x[2 * c + 1].y);
+}
+
+// bit j = key c0 + j masked (or past ke), from the lane's own mask row: one 16-byte load when
+// the row is 16-byte aligned (vec), else byte loads.
+__device__ __forceinline__ uint32_t mask_bits16(const uint8_t* mrow, int c0, int ke, bool vec) {
+  uint32_t bits = 0;
+  if (vec && c0 + KC <= ke) {
+    const uint4 w = *reinterpret_cast<const uint4*>(mrow + c0);
+    const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) bits |= ((x[i] >> (8 * b)) & 1u) << (4 * i + b);
+  } else {
+    for (int j = 0; j < KC; ++j)
+      if (c0 + j >= ke || mrow[c0 + j]) bits |= 1u << j;
+  }
+  return bits;
+}
+
+// grid (nsplit, BH, ceil(Q / QW)), QW threads
+__global__ __launch_bounds__(QW) void k_attn_fwd(AttnArgs a) {
+  const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
+  const int qrow = blockIdx.z * QW + tid;
+  const bool qv = qrow < a.Q;
+  f2 qr[HP], o[HP];
+  load_row(qr, a.q + ((long long)qrow * a.BH + bh) * HD, qv, a.scale);  // q * scale, as torch forms it
+#pragma unroll
+  for (int c = 0; c < HP; ++c) o[c] = f2{0.f, 0.f};
+  const int kb = split * a.span, ke = min(a.L, kb + a.span);
+  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  float m = -INFINITY, l = 0.f;
+  uint32_t next_bits = kb < ke ? mask_bits16(mrow, kb, ke, a.vec_mask) : 0u;
+  for (int c0 = kb; c0 < ke; c0 += KC) {
+    const uint32_t bits = next_bits;  // mask bits one chunk ahead, so the load latency overlaps a chunk
+    if (c0 + KC < ke) next_bits = mask_bits16(mrow, c0 + KC, ke, a.vec_mask);
+    float s[KC];
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      s[j] = -INFINITY;
+      if (c0 + j < ke) {
+        const float acc = dot_row(qr, uniform_row(a.k, c0 + j, a.BH, bh));
+        if (!((bits >> j) & 1u)) s[j] = acc;
+      }
+      cmax = fmaxf(cmax, s[j]);
+    }
+    if (cmax != -INFINITY) {  // else the whole chunk is masked for this query
+      const float mn = fmaxf(m, cmax);
+      const float alpha = expf(m - mn);  // m == -inf -> 0 (l, o are 0 then)
+      l *= alpha;
+#pragma unroll
+      for (int c = 0; c < HP; ++c) o[c] *= alpha;
+      m = mn;
+    }
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      if (c0 + j >= ke) break;
+      const float p = s[j] == -INFINITY ? 0.f : expf(s[j] - m);  // masked: exactly 0, as torch's softmax
+      l += p;
+      axpy_row(o, p, uniform_row(a.v, c0 + j, a.BH, bh));
+    }
+  }
+  if (!qv) return;
+  const long long row = ((long long)split * a.Q + qrow) * a.BH + bh;
+  store_row(a.part_o + row * HD, o);
+  *reinterpret_cast<float2*>(a.part_ml + row * 2) = make_float2(m, l);
+}
+
+// One 32-lane group per (q, bh) row: merge the splits' partials; o = sum_s e_s o_s / sum_s e_s l_s.
+__global__ __launch_bounds__(256) void k_attn_merge(AttnArgs a) {
+  const long long rows = (long long)a.Q * a.BH;
+  const long long r = blockIdx.x * 8ll + (threadIdx.x >> 5);
+  const int d = threadIdx.x & 31;
+  if (r >= rows) return;
+  float M = -INFINITY;
+  for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[(s * rows + r) * 2]);
+  float Ls = 0.f, acc = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < a.nsplit; ++s) {
+      const float ms = a.part_ml[(s * rows + r) * 2];
+      if (ms == -INFINITY) continue;
+      const float e = expf(ms - M);
+      Ls = __builtin_fmaf(e, a.part_ml[(s * rows + r) * 2 + 1], Ls);
+      acc = __builtin_fmaf(e, a.part_o[(s * rows + r) * HD + d], acc);
+    }
+  }
+  // a fully masked row: 0 / 0 = NaN, as torch's softmax gives
+  a.o[r * HD + d] = M == -INFINITY ? __builtin_nanf("") : acc / Ls;
+  if (d == 0) a.lse[r] = M == -INFINITY ? INFINITY : M + logf(Ls);
+}
+
+struct AttnBwdArgs {
+  const float* q;
+  const float* k;
+  const float* v;
+  const uint8_t* mask;
+  const float* lse;     // [Q][BH]
+  const float* delta;   // [Q][BH] = rowsum(dO * O)
+  const float* dout;    // [Q][BH][HD]
+  const float* qs;      // [Q][BH][HD] = q * scale (k_attn_delta)
+  float* dq;            // [Q][BH][HD]
+  float* dk;            // [L][BH][HD]
+  float* dv;            // [L][BH][HD]
+  float* part_dq;       // [nsplit][Q][BH][HD]
+  int BH, Q, L;
+  int nsplit, span;
+  float scale;
+  bool vec_mask;
+};
+
+// One 32-lane group per (q, bh) row: delta = sum_d dO * O, and q_scaled = q * scale (fp32, as
+// torch forms it) for the dK / dV kernel's scalar reads.
+__global__ __launch_bounds__(256) void k_attn_delta(AttnBwdArgs a, const float* __restrict__ o, float* delta,
+                                                    float* qs) {
+  const long long rows = (long long)a.Q * a.BH;
+  const long long r = blockIdx.x * 8ll + (threadIdx.x >> 5);
+  const int d = threadIdx.x & 31;
+  float v = 0.f;
+  if (r < rows) {
+    v = o[r * HD + d] * a.dout[r * HD + d];
+    qs[r * HD + d] = a.q[r * HD + d] * a.scale;
+  }
+  for (int s = 16; s > 0; s >>= 1) v += __shfl_xor(v, s, 32);
+  if (r < rows && d == 0) delta[r] = v;
+}
+
+// grid (ceil(L / KVW), BH), KVW threads: thread = key; q_scaled / dO rows of each query are
+// wave-uniform scalar reads.
+__global__ __launch_bounds__(KVW) void k_attn_bwd_kv(AttnBwdArgs a) {
+  const int bh = blockIdx.y, tid = threadIdx.x;
+  const int key = blockIdx.x * KVW + tid;
+  const bool kv = key < a.L;
+  f2 kr[HP], vr[HP], dk[HP], dv[HP];
+  load_row(kr, a.k + ((long long)key * a.BH + bh) * HD, kv, 1.f);
+  load_row(vr, a.v + ((long long)key * a.BH + bh) * HD, kv, 1.f);
+#pragma unroll
+  for (int c = 0; c < HP; ++c) dk[c] = dv[c] = f2{0.f, 0.f};
+  const cfloat* lse = (const cfloat*)a.lse;
+  const cfloat* del = (const cfloat*)a.delta;
+  const uint8_t* mcol = a.mask + (long long)bh * a.Q * a.L + (kv ? key : 0);
+  for (int q0 = 0; q0 < a.Q; q0 += 16) {
+    // the next 16 queries' mask bytes for this key, all loads in flight at once
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (q0 + j < a.Q && (!kv || mcol[(long long)(q0 + j) * a.L])) bits |= 1u << j;
+    const int qn = min(16, a.Q - q0);
+#pragma unroll 2
+    for (int j = 0; j < qn; ++j) {
+      const int qi = q0 + j;
+      const cfloat* qr = uniform_row(a.qs, qi, a.BH, bh);
+      const cfloat* dor = uniform_row(a.dout, qi, a.BH, bh);
+      const float s = dot_row(kr, qr);
+      const float dp = dot_row(vr, dor);
+      const float p = ((bits >> j) & 1u) ? 0.f : expf(s - lse[(long long)qi * a.BH + bh]);
+      const float ds = p * (dp - del[(long long)qi * a.BH + bh]);
+      axpy_row(dv, p, dor);
+      axpy_row(dk, ds, qr);  // dK = dS^T (q * scale)
+    }
+  }
+  if (!kv) return;
+  store_row(a.dk + ((long long)key * a.BH + bh) * HD, dk);
+  store_row(a.dv + ((long long)key * a.BH + bh) * HD, dv);
+}
+
+// grid (nsplit, BH, ceil(Q / QW)), QW threads: thread = query; partial sum_k ds k over the split.
+__global__ __launch_bounds__(QW) void k_attn_bwd_q(AttnBwdArgs a) {
+  const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
+  const int qrow = blockIdx.z * QW + tid;
+  const bool qv = qrow < a.Q;
+  f2 qr[HP], dor[HP], g[HP];
+  load_row(qr, a.q + ((long long)qrow * a.BH + bh) * HD, qv, a.scale);
+  load_row(dor, a.dout + ((long long)qrow * a.BH + bh) * HD, qv, 1.f);
+#pragma unroll
+  for (int c = 0; c < HP; ++c) g[c] = f2{0.f, 0.f};
+  const float lse = qv ? a.lse[(long long)qrow * a.BH + bh] : 0.f;
+  const float del = qv ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
+  const int kb = split * a.span, ke = min(a.L, kb + a.span);
+  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  uint32_t next_bits = kb < ke ? mask_bits16(mrow, kb, ke, a.vec_mask) : 0u;
+  for (int c0 = kb; c0 < ke; c0 += KC) {
+    const uint32_t bits = next_bits;  // mask bits one chunk ahead, so the load latency overlaps a chunk
+    if (c0 + KC < ke) next_bits = mask_bits16(mrow, c0 + KC, ke, a.vec_mask);
+#pragma unroll 4
+    for (int j = 0; j < KC; ++j) {
+      if (c0 + j >= ke) break;
+      const cfloat* kr = uniform_row(a.k, c0 + j, a.BH, bh);
+      const float s = dot_row(qr, kr);
+      const float dp = dot_row(dor, uniform_row(a.v, c0 + j, a.BH, bh));
+      const float ds = ((bits >> j) & 1u) ? 0.f : expf(s - lse) * (dp - del);
+      axpy_row(g, ds, kr);
+    }
+  }
+  if (!qv) return;
+  store_row(a.part_dq + (((long long)split * a.Q + qrow) * a.BH + bh) * HD, g);
+}
+
+// dq = scale * sum over splits (split order, deterministic)
+__global__ __launch_bounds__(256) void k_attn_dq_sum(AttnBwdArgs a) {
+  const long long n = (long long)a.Q * a.BH * HD;
+  const long long i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  float acc = 0.f;
+  for (int s = 0; s < a.nsplit; ++s) acc += a.part_dq[s * n + i];
+  a.dq[i] = acc * a.scale;
+}
+
+// Key splits: enough workgroups to fill the chip (>= ~2048 across the grid), >= KS keys each.
+void split_keys(int BH, int Q, int L, int* nsplit, int* span) {
+  const long long base = (long long)BH * ((Q + QW - 1) / QW);
+  const int max_split = (L + KS - 1) / KS;
+  int ns = (int)std::min<long long>(max_split, std::max<long long>(1, (2048 + base - 1) / base));
+  int sp = (L + ns - 1) / ns;
+  sp = (sp + KS - 1) / KS * KS;
+  *span = sp;
+  *nsplit = (L + sp - 1) / sp;
+}
+
+bool attn_shape_ok(const void* q, const void* k, const void* v, int BH, int Q, int L, int head_dim) {
+  return head_dim == HD && BH > 0 && Q > 0 && L > 0 && ((uintptr_t)q % 16) == 0 && ((uintptr_t)k % 16) == 0 &&
+         ((uintptr_t)v % 16) == 0;
+}
+
+size_t attn_align(size_t x) { return (x + 255) / 256 * 256; }
+
+bool mask_vec(const uint8_t* mask, int L) { return (L % 16) == 0 && ((uintptr_t)mask % 16) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+size_t rgbd_masked_attn_fwd_workspace_size(int BH, int Q, int L) {
+  if (BH <= 0 || Q <= 0 || L <= 0) return 256;
+  int ns, sp;
+  split_keys(BH, Q, L, &ns, &sp);
+  const size_t rows = (size_t)ns * Q * BH;
+  return attn_align(rows * HD * sizeof(float)) + attn_align(rows * 2 * sizeof(float));
+}
+
+int rgbd_masked_attn_fwd(const float* q, const float* k, const float* v, const uint8_t* mask, int BH, int Q, int L,
+                         int head_dim, float scale, float* out, float* lse, void* ws, void* stream) {
+  RGBD_REQUIRE(q && k && v && mask && out && lse && ws && BH > 0 && Q > 0 && L > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(attn_shape_ok(q, k, v, BH, Q, L, head_dim) && ((uintptr_t)out % 16) == 0, RGBD_E_SHAPE);
+  hipStream_t s = (hipStream_t)stream;
+  AttnArgs a = {q, k, v, mask, out, lse, nullptr, nullptr, BH, Q, L, 0, 0, scale, mask_vec(mask, L)};
+  split_keys(BH, Q, L, &a.nsplit, &a.span);
+  const size_t rows = (size_t)a.nsplit * Q * BH;
+  a.part_o = (float*)ws;
+  a.part_ml = (float*)((char*)ws + attn_align(rows * HD * sizeof(float)));
+  k_attn_fwd<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
+  const long long orows = (long long)Q * BH;
+  k_attn_merge<<<(unsigned)((orows + 7) / 8), 256, 0, s>>>(a);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+size_t rgbd_masked_attn_bwd_workspace_size(int BH, int Q, int L) {
+  if (BH <= 0 || Q <= 0 || L <= 0) return 256;
+  int ns, sp;
+  split_keys(BH, Q, L, &ns, &sp);
+  return attn_align((size_t)Q * BH * sizeof(float)) + attn_align((size_t)Q * BH * HD * sizeof(float)) +
+         attn_align((size_t)ns * Q * BH * HD * sizeof(float));
+}
+
+int rgbd_masked_attn_bwd(const float* q, const float* k, const float* v, const uint8_t* mask, const float* out,
+                         const float* lse, const float* dout, int BH, int Q, int L, int head_dim, float scale,
+                         float* dq, float* dk, float* dv, void* ws, void* stream) {
+  RGBD_REQUIRE(q && k && v && mask && out && lse && dout && dq && dk && dv && ws && BH > 0 && Q > 0 && L > 0,
+               RGBD_E_ARG);
+  RGBD_REQUIRE(attn_shape_ok(q, k, v, BH, Q, L, head_dim) && ((uintptr_t)dout % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
+                   ((uintptr_t)dk % 16) == 0 && ((uintptr_t)dv % 16) == 0,
+               RGBD_E_SHAPE);
+  hipStream_t s = (hipStream_t)stream;
+  const long long rows = (long long)BH * Q;
+  float* delta = (float*)ws;
+  float* qs = (float*)((char*)ws + attn_align((size_t)rows * sizeof(float)));
+  AttnBwdArgs a = {q, k, v, mask, lse, delta, dout, qs, dq, dk, dv, nullptr, BH, Q, L, 0, 0, scale,
+                   mask_vec(mask, L)};
+  split_keys(BH, Q, L, &a.nsplit, &a.span);
+  a.part_dq = (float*)((char*)qs + attn_align((size_t)rows * HD * sizeof(float)));
+  k_attn_delta<<<(unsigned)((rows + 7) / 8), 256, 0, s>>>(a, out, delta, qs);
+  k_attn_bwd_kv<<<dim3((L + KVW - 1) / KVW, BH), KVW, 0, s>>>(a);
+  k_attn_bwd_q<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
+  k_attn_dq_sum<<<(unsigned)((rows * HD + 255) / 256), 256, 0, s>>>(a);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+}  // extern "C"

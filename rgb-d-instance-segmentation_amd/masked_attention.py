@@ -1,0 +1,128 @@
+"""f1: the masked cross-attention of the Mask2Former decoder layers on HIP kernels.
+
+Reference: each ``Mask2FormerMaskedAttentionDecoderLayer`` (transformers 5.15
+modeling_mask2former.py:1627-1654) calls ``nn.MultiheadAttention`` with the boolean mask the
+mask predictor produced (:2048-2055) — 9 calls per forward over the three pixel-decoder levels.
+torch's math path (need_weights=True, F.multi_head_attention_forward) does, per batch*head bh:
+    q, k, v = linear(query / key / value, in_proj chunks)            library GEMMs
+    S = (q * head_dim^-1/2) k^T + where(mask, -inf, 0); P = softmax(S); O = P v
+    out = linear(O, out_proj)                                         library GEMM
+``HipMultiheadAttention`` keeps the projections as the module's GEMMs and runs the masked
+softmax-attention core (scores, mask, softmax, P.V and the backward) as the HIP kernels
+``rgbd_masked_attn_fwd`` / ``_bwd`` (csrc/masked_attn.hip), on the projections' own
+sequence-major layout (no head transposes, no [BH, Q, L] score tensor in HBM).
+
+Differences from the torch module, by design: the attention weights (the second output) are not
+materialised — ``None`` is returned unless ``need_weights_output`` is set on the module, in which
+case the call goes through torch's path.  Inputs the kernels do not cover (non-float32, a key
+padding mask, a float mask, dropout in training, head_dim != 32, batch_first) also go through
+torch's path unchanged.  ``install(model)`` swaps the class of the decoder layers'
+``cross_attn`` modules in place (same parameters, same state_dict keys).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib
+from ._lib import check
+from .ops import _need_cuda, _p, _stream
+
+
+class MaskedAttentionFunction(torch.autograd.Function):
+    """q [Q, BH, 32], k / v [L, BH, 32] float32 (contiguous), mask bool [BH, Q, L] -> o [Q, BH, 32]."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, mask, scale):
+        _need_cuda(q, k, v, mask)
+        Q, BH, hd = q.shape
+        L = k.shape[0]
+        out = torch.empty_like(q)
+        lse = torch.empty((Q, BH), dtype=torch.float32, device=q.device)
+        L_ = _lib.lib()
+        ws = torch.empty((L_.rgbd_masked_attn_fwd_workspace_size(BH, Q, L),), dtype=torch.uint8, device=q.device)
+        check(L_.rgbd_masked_attn_fwd(_p(q), _p(k), _p(v), _p(mask), BH, Q, L, hd, float(scale), _p(out), _p(lse),
+                                      _p(ws), _stream(q.device)), "rgbd_masked_attn_fwd")
+        ctx.save_for_backward(q, k, v, mask, out, lse)
+        ctx.scale = float(scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        q, k, v, mask, out, lse = ctx.saved_tensors
+        Q, BH, hd = q.shape
+        L = k.shape[0]
+        g = gout.float().contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        L_ = _lib.lib()
+        ws = torch.empty((L_.rgbd_masked_attn_bwd_workspace_size(BH, Q, L),), dtype=torch.uint8, device=q.device)
+        check(L_.rgbd_masked_attn_bwd(_p(q), _p(k), _p(v), _p(mask), _p(out), _p(lse), _p(g), BH, Q, L, hd,
+                                      ctx.scale, _p(dq), _p(dk), _p(dv), _p(ws), _stream(q.device)),
+              "rgbd_masked_attn_bwd")
+        return dq, dk, dv, None, None
+
+
+def masked_attention(q, k, v, mask, scale):
+    return MaskedAttentionFunction.apply(q.contiguous(), k.contiguous(), v.contiguous(), mask.contiguous(), scale)
+
+
+class HipMultiheadAttention(nn.MultiheadAttention):
+    need_weights_output = False
+
+    def _hip_ok(self, query, key, value, key_padding_mask, attn_mask, is_causal):
+        E = self.embed_dim
+        return (query.is_cuda and query.dtype == key.dtype == value.dtype == torch.float32
+                and not self.batch_first and self._qkv_same_embed_dim and self.in_proj_bias is not None
+                and self.bias_k is None and not self.add_zero_attn and key_padding_mask is None
+                and not is_causal and E // self.num_heads == 32 and (self.dropout == 0.0 or not self.training)
+                and attn_mask is not None and attn_mask.dtype == torch.bool and attn_mask.dim() == 3
+                and query.dim() == 3 and key.shape == value.shape
+                and tuple(attn_mask.shape) == (query.shape[1] * self.num_heads, query.shape[0], key.shape[0])
+                and not torch.is_autocast_enabled("cuda"))
+
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=True, attn_mask=None,
+                average_attn_weights=True, is_causal=False):
+        if self.need_weights_output or not self._hip_ok(query, key, value, key_padding_mask, attn_mask, is_causal):
+            return super().forward(query, key, value, key_padding_mask=key_padding_mask, need_weights=need_weights,
+                                   attn_mask=attn_mask, average_attn_weights=average_attn_weights,
+                                   is_causal=is_causal)
+        Q, B, E = query.shape
+        L = key.shape[0]
+        H = self.num_heads
+        w_q, w_k, w_v = self.in_proj_weight.chunk(3)
+        b_q, b_k, b_v = self.in_proj_bias.chunk(3)
+        q = F.linear(query, w_q, b_q).view(Q, B * H, E // H)
+        k = F.linear(key, w_k, b_k).view(L, B * H, E // H)
+        v = F.linear(value, w_v, b_v).view(L, B * H, E // H)
+        scale = math.sqrt(1.0 / float(E // H))  # torch's q scaling
+        o = masked_attention(q, k, v, attn_mask, scale)
+        out = F.linear(o.view(Q * B, E), self.out_proj.weight, self.out_proj.bias).view(Q, B, E)
+        return out, None
+
+
+def install_module(m: nn.Module) -> bool:
+    """Swap one nn.MultiheadAttention for the HIP one in place (same parameters)."""
+    if type(m) is not nn.MultiheadAttention:
+        return False
+    m.__class__ = HipMultiheadAttention
+    return True
+
+
+def install(model: nn.Module) -> int:
+    """Swap the decoder layers' cross-attention modules for the HIP one; returns the count."""
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerMaskedAttentionDecoderLayer
+    n = 0
+    for m in model.modules():
+        if isinstance(m, Mask2FormerMaskedAttentionDecoderLayer):
+            n += install_module(m.cross_attn)
+    return n
+
+
+def uninstall(model: nn.Module) -> int:
+    n = 0
+    for m in model.modules():
+        if type(m) is HipMultiheadAttention:
+            m.__class__ = nn.MultiheadAttention
+            n += 1
+    return n
