@@ -17,7 +17,7 @@ from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation,
 from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
                                                                   Mask2FormerPixelLevelModuleOutput)
 
-from . import deform_attn, mask_predictor, point_loss
+from . import deform_attn, mask_predictor, masked_attention, point_loss
 from .hot_path import hot_path
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
@@ -112,6 +112,9 @@ class CustomMask2FormerModel(Mask2FormerModel):
         # f1: mask einsum + attention-mask binarisation of the masked-attention decoder on the
         # HIP kernels (class swap: parameters and state_dict keys unchanged)
         mask_predictor.install(self.transformer_module)
+        # f1: the decoder layers' masked cross-attention core (scores, mask, softmax, P.V and its
+        # backward) on the HIP kernels; torch's module path for inputs the kernels do not cover
+        masked_attention.install(self.transformer_module)
         # f2: the pixel decoder's deformable-attention core on the fused HIP gather kernels
         deform_attn.install(self.pixel_level_module.decoder)
 

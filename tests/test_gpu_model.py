@@ -10,7 +10,7 @@ import torch
 
 import golden_inputs as gi
 from oracle import ratio as ratio_o
-from rgbd_amd import deform_attn, init as winit, mask_predictor
+from rgbd_amd import deform_attn, init as winit, mask_predictor, masked_attention
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -185,6 +185,7 @@ def test_full_model_mask_logits_fp32(golden):
     mc = _full_model().cpu().eval()
     assert mask_predictor.uninstall(mc) == 1  # the reference HF modules are the CPU checker
     assert deform_attn.uninstall(mc) == 6
+    assert masked_attention.uninstall(mc) == 9
     mc.model.pixel_level_module.hot_path_features = lambda pv_, colors, ratios=None, **kw: caps["bb"]
     calls = []
     h3 = mc.model.transformer_module.decoder.mask_predictor.register_forward_hook(

@@ -19,8 +19,9 @@ def _model():
     m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
     missing = winit.init_deterministic(m)
     assert not missing.unexpected_keys
-    from rgbd_amd import deform_attn, mask_predictor, point_loss
+    from rgbd_amd import deform_attn, mask_predictor, masked_attention, point_loss
     mask_predictor.uninstall(m)  # CPU oracle run: the reference HF modules
+    masked_attention.uninstall(m)
     point_loss.uninstall(m)  # the HF loss and its matcher
     deform_attn.uninstall(m)
     return m

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--amp", type=int, default=1)
     ap.add_argument("--arms", default="hip,hf")
     args = ap.parse_args()
-    from rgbd_amd import deform_attn, init as winit, mask_predictor, point_loss, ops, synthetic
+    from rgbd_amd import deform_attn, init as winit, mask_predictor, masked_attention, point_loss, ops, synthetic
     from rgbd_amd.config import standard_config
     from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
     dev = torch.device("cuda")
@@ -45,6 +45,7 @@ def main():
         m.set_compute_dtype(torch.bfloat16).to(dev).train()
         if arm == "hf":
             mask_predictor.uninstall(m)
+            masked_attention.uninstall(m)
             deform_attn.uninstall(m)
             point_loss.uninstall(m)
         opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, fused=True)
