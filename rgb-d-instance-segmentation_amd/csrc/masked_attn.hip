@@ -22,6 +22,7 @@
 //   dQ        like the forward (thread per query, key splits), partial dq per split summed in split
 //             order by k_attn_dq_sum — no atomics anywhere, the backward is deterministic.
 #include <cmath>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -257,6 +258,87 @@ __global__ __launch_bounds__(KVW) void k_attn_bwd_kv(AttnBwdArgs a) {
   store_row(a.dv + ((long long)key * a.BH + bh) * HD, dv);
 }
 
+// dK / dV on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact f32): a wave owns 16 keys, a workgroup 64;
+// per block of 16 queries
+//   S = q_scaled . K^T, dP = dO . V^T                 (16q x 16k, 8 + 8 MFMAs over the 32 dims)
+//   P = exp(S - lse), dS = P (dP - delta)              (in the accumulator layout: lane l holds
+//                                                       query (l>>4)*4+i, key l&15)
+//   dV^T += dO^T . P, dK^T += q_scaled^T . dS          (32d x 16k, 8 + 8 MFMAs; P / dS feed the B
+//                                                       operand straight from the accumulators:
+//                                                       chunk i contracts queries (l>>4)*4+i)
+// The K / V tiles stay in registers for the whole loop; q_scaled and dO are staged 64 queries at
+// a time in LDS (rows padded to 33 floats).
+typedef float f4v __attribute__((ext_vector_type(4)));
+constexpr int QB = 64;
+
+__global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs a) {
+  __shared__ float sq[QB][HD + 1];
+  __shared__ float sdo[QB][HD + 1];
+  __shared__ float slse[QB], sdel[QB];
+  const int bh = blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int lc = l & 15, lg = l >> 4;
+  const int key0 = blockIdx.x * 64 + w * 16, keyl = key0 + lc;
+  const bool kv = keyl < a.L;
+  float kb[8], vb[8];  // B operands: K^T / V^T [d = 4c + lg][key lc]
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    kb[c] = kv ? a.k[((long long)keyl * a.BH + bh) * HD + 4 * c + lg] : 0.f;
+    vb[c] = kv ? a.v[((long long)keyl * a.BH + bh) * HD + 4 * c + lg] : 0.f;
+  }
+  f4v dv[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+  f4v dk[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+  const uint8_t* mcol = a.mask + (long long)bh * a.Q * a.L + (kv ? keyl : 0);
+  for (int qb0 = 0; qb0 < a.Q; qb0 += QB) {
+    __syncthreads();
+    for (int i = tid; i < QB * HD; i += 256) {
+      const int r = i / HD, d = i % HD, qrow = qb0 + r;
+      const bool ok = qrow < a.Q;
+      sq[r][d] = ok ? a.qs[((long long)qrow * a.BH + bh) * HD + d] : 0.f;
+      sdo[r][d] = ok ? a.dout[((long long)qrow * a.BH + bh) * HD + d] : 0.f;
+    }
+    if (tid < QB) {
+      const int qrow = qb0 + tid;
+      slse[tid] = qrow < a.Q ? a.lse[(long long)qrow * a.BH + bh] : 0.f;
+      sdel[tid] = qrow < a.Q ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
+    }
+    __syncthreads();
+    const int qn = min(QB, a.Q - qb0);
+    for (int r0 = 0; r0 < qn; r0 += 16) {
+      f4v S = {0.f, 0.f, 0.f, 0.f}, DP = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        S = __builtin_amdgcn_mfma_f32_16x16x4f32(sq[r0 + lc][4 * c + lg], kb[c], S, 0, 0, 0);
+        DP = __builtin_amdgcn_mfma_f32_16x16x4f32(sdo[r0 + lc][4 * c + lg], vb[c], DP, 0, 0, 0);
+      }
+      float p[4], ds[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = r0 + lg * 4 + i, qq = qb0 + rr;
+        const bool masked = !kv || qq >= a.Q || mcol[(long long)(qq < a.Q ? qq : 0) * a.L];
+        p[i] = masked ? 0.f : expf(S[i] - slse[rr]);
+        ds[i] = p[i] * (DP[i] - sdel[rr]);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = r0 + lg * 4 + i;
+          dv[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(sdo[rr][h * 16 + lc], p[i], dv[h], 0, 0, 0);
+          dk[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(sq[rr][h * 16 + lc], ds[i], dk[h], 0, 0, 0);
+        }
+    }
+  }
+  if (!kv) return;
+  // accumulators: row = d = h*16 + lg*4 + j, col = key lc
+  float* dkr = a.dk + ((long long)keyl * a.BH + bh) * HD;
+  float* dvr = a.dv + ((long long)keyl * a.BH + bh) * HD;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    *reinterpret_cast<float4*>(dkr + h * 16 + lg * 4) = make_float4(dk[h][0], dk[h][1], dk[h][2], dk[h][3]);
+    *reinterpret_cast<float4*>(dvr + h * 16 + lg * 4) = make_float4(dv[h][0], dv[h][1], dv[h][2], dv[h][3]);
+  }
+}
+
 // grid (nsplit, BH, ceil(Q / QW)), QW threads: thread = query; partial sum_k ds k over the split.
 __global__ __launch_bounds__(QW) void k_attn_bwd_q(AttnBwdArgs a) {
   const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
@@ -373,7 +455,11 @@ int rgbd_masked_attn_bwd(const float* q, const float* k, const float* v, const u
   split_keys(BH, Q, L, &a.nsplit, &a.span);
   a.part_dq = (float*)((char*)qs + attn_align((size_t)rows * HD * sizeof(float)));
   k_attn_delta<<<(unsigned)((rows + 7) / 8), 256, 0, s>>>(a, out, delta, qs);
-  k_attn_bwd_kv<<<dim3((L + KVW - 1) / KVW, BH), KVW, 0, s>>>(a);
+  static const char* kv_env = getenv("RGBD_ATTN_KV");  // "valu": the thread-per-key kernel
+  if (kv_env && kv_env[0] == 'v')
+    k_attn_bwd_kv<<<dim3((L + KVW - 1) / KVW, BH), KVW, 0, s>>>(a);
+  else
+    k_attn_bwd_kv_mfma<<<dim3((L + 63) / 64, BH), 256, 0, s>>>(a);
   k_attn_bwd_q<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
   k_attn_dq_sum<<<(unsigned)((rows * HD + 255) / 256), 256, 0, s>>>(a);
   RGBD_CHECK_LAUNCH();
