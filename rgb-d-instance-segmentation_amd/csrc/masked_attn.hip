@@ -161,6 +161,96 @@ __global__ __launch_bounds__(QW) void k_attn_fwd(AttnArgs a) {
   *reinterpret_cast<float2*>(a.part_ml + row * 2) = make_float2(m, l);
 }
 
+// Forward on fp32 MFMA: a wave owns 16 queries (a workgroup 64), keys of the split staged 64 at a
+// time in LDS; per 16-key block
+//   S^T = K . q_scaled^T                     (16k x 16q, 8 MFMAs; q_scaled^T is the register-held
+//                                             B operand; lane l holds key (l>>4)*4+i, query l&15)
+//   online softmax per query column          (max / sum over i, then across the 4 lane groups)
+//   O^T += V^T . P^T                         (32d x 16q, 8 MFMAs; P^T feeds the B operand from the
+//                                             accumulators, chunk i contracts keys (l>>4)*4+i)
+// Every accumulator of a lane belongs to its query column, so the rescale is a per-lane multiply.
+typedef float f4m __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs a) {
+  __shared__ float sk[64][HD + 1];
+  __shared__ float sv[64][HD + 1];
+  const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int lc = l & 15, lg = l >> 4;
+  const int qrow = blockIdx.z * 64 + w * 16 + lc;
+  const bool qv = qrow < a.Q;
+  float qb[8];  // B operand: q_scaled^T [d = 4c + lg][query lc]
+#pragma unroll
+  for (int c = 0; c < 8; ++c) qb[c] = qv ? a.q[((long long)qrow * a.BH + bh) * HD + 4 * c + lg] * a.scale : 0.f;
+  f4m o[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
+  float m = -INFINITY, lsum = 0.f;
+  const int kb = split * a.span, ke = min(a.L, kb + a.span);
+  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  for (int k0 = kb; k0 < ke; k0 += 64) {
+    __syncthreads();
+    for (int i = tid; i < 64 * HD; i += 256) {
+      const int r = i / HD, d = i % HD, key = k0 + r;
+      const bool ok = key < ke;
+      sk[r][d] = ok ? a.k[((long long)key * a.BH + bh) * HD + d] : 0.f;
+      sv[r][d] = ok ? a.v[((long long)key * a.BH + bh) * HD + d] : 0.f;
+    }
+    __syncthreads();
+    const int kn = min(64, ke - k0);
+    for (int r0 = 0; r0 < kn; r0 += 16) {
+      f4m S = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) S = __builtin_amdgcn_mfma_f32_16x16x4f32(sk[r0 + lc][4 * c + lg], qb[c], S, 0, 0, 0);
+      // this lane's 4 keys: k0 + r0 + lg*4 + i, query qrow
+      const int kbase = k0 + r0 + lg * 4;
+      uint32_t mb = 0;
+      if (a.vec_mask && kbase + 4 <= ke) {
+        mb = *reinterpret_cast<const uint32_t*>(mrow + kbase);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mb |= (kbase + i < ke ? (uint32_t)mrow[kbase + i] : 1u) << (8 * i);
+      }
+      float sc[4];
+      float bmax = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool masked = !qv || kbase + i >= ke || ((mb >> (8 * i)) & 0xffu);
+        sc[i] = masked ? -INFINITY : S[i];
+        bmax = fmaxf(bmax, sc[i]);
+      }
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 16));
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+      const float mn = fmaxf(m, bmax);
+      float p[4], bsum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p[i] = sc[i] == -INFINITY ? 0.f : expf(sc[i] - mn);
+        bsum += p[i];
+      }
+      bsum += __shfl_xor(bsum, 16);
+      bsum += __shfl_xor(bsum, 32);
+      if (mn != -INFINITY) {
+        const float alpha = expf(m - mn);  // m == -inf -> 0 (o, lsum are 0 then)
+        lsum = lsum * alpha + bsum;
+        o[0] *= alpha;
+        o[1] *= alpha;
+        m = mn;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          o[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(sv[r0 + lg * 4 + i][h * 16 + lc], p[i], o[h], 0, 0, 0);
+    }
+  }
+  if (!qv) return;
+  // accumulators: row = d = h*16 + lg*4 + j, col = query lc
+  const long long row = ((long long)split * a.Q + qrow) * a.BH + bh;
+  float* po = a.part_o + row * HD;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    *reinterpret_cast<float4*>(po + h * 16 + lg * 4) = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
+  if (lg == 0) *reinterpret_cast<float2*>(a.part_ml + row * 2) = make_float2(m, lsum);
+}
+
 // One 32-lane group per (q, bh) row: merge the splits' partials; o = sum_s e_s o_s / sum_s e_s l_s.
 __global__ __launch_bounds__(256) void k_attn_merge(AttnArgs a) {
   const long long rows = (long long)a.Q * a.BH;
@@ -371,6 +461,72 @@ __global__ __launch_bounds__(QW) void k_attn_bwd_q(AttnBwdArgs a) {
   store_row(a.part_dq + (((long long)split * a.Q + qrow) * a.BH + bh) * HD, g);
 }
 
+// dQ on fp32 MFMA, the forward's tiling: per 16-key block S^T = K . q_scaled^T and
+// dP^T = V . dO^T (8 + 8 MFMAs), dS^T = exp(S^T - lse) (dP^T - delta) in the accumulator layout,
+// then dq^T += K^T . dS^T (8 MFMAs, dS^T as the B operand); partial per key split.
+__global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs a) {
+  __shared__ float sk[64][HD + 1];
+  __shared__ float sv[64][HD + 1];
+  const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int lc = l & 15, lg = l >> 4;
+  const int qrow = blockIdx.z * 64 + w * 16 + lc;
+  const bool qv = qrow < a.Q;
+  float qb[8], db[8];  // B operands: q_scaled^T, dO^T [d = 4c + lg][query lc]
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    qb[c] = qv ? a.q[((long long)qrow * a.BH + bh) * HD + 4 * c + lg] * a.scale : 0.f;
+    db[c] = qv ? a.dout[((long long)qrow * a.BH + bh) * HD + 4 * c + lg] : 0.f;
+  }
+  const float lse = qv ? a.lse[(long long)qrow * a.BH + bh] : 0.f;
+  const float del = qv ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
+  f4m g[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
+  const int kb = split * a.span, ke = min(a.L, kb + a.span);
+  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  for (int k0 = kb; k0 < ke; k0 += 64) {
+    __syncthreads();
+    for (int i = tid; i < 64 * HD; i += 256) {
+      const int r = i / HD, d = i % HD, key = k0 + r;
+      const bool ok = key < ke;
+      sk[r][d] = ok ? a.k[((long long)key * a.BH + bh) * HD + d] : 0.f;
+      sv[r][d] = ok ? a.v[((long long)key * a.BH + bh) * HD + d] : 0.f;
+    }
+    __syncthreads();
+    const int kn = min(64, ke - k0);
+    for (int r0 = 0; r0 < kn; r0 += 16) {
+      f4m S = {0.f, 0.f, 0.f, 0.f}, DP = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        S = __builtin_amdgcn_mfma_f32_16x16x4f32(sk[r0 + lc][4 * c + lg], qb[c], S, 0, 0, 0);
+        DP = __builtin_amdgcn_mfma_f32_16x16x4f32(sv[r0 + lc][4 * c + lg], db[c], DP, 0, 0, 0);
+      }
+      const int kbase = k0 + r0 + lg * 4;
+      uint32_t mb = 0;
+      if (a.vec_mask && kbase + 4 <= ke) {
+        mb = *reinterpret_cast<const uint32_t*>(mrow + kbase);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mb |= (kbase + i < ke ? (uint32_t)mrow[kbase + i] : 1u) << (8 * i);
+      }
+      float ds[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool masked = !qv || kbase + i >= ke || ((mb >> (8 * i)) & 0xffu);
+        ds[i] = masked ? 0.f : expf(S[i] - lse) * (DP[i] - del);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          g[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(sk[r0 + lg * 4 + i][h * 16 + lc], ds[i], g[h], 0, 0, 0);
+    }
+  }
+  if (!qv) return;
+  float* pg = a.part_dq + (((long long)split * a.Q + qrow) * a.BH + bh) * HD;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    *reinterpret_cast<float4*>(pg + h * 16 + lg * 4) = make_float4(g[h][0], g[h][1], g[h][2], g[h][3]);
+}
+
 // dq = scale * sum over splits (split order, deterministic)
 __global__ __launch_bounds__(256) void k_attn_dq_sum(AttnBwdArgs a) {
   const long long n = (long long)a.Q * a.BH * HD;
@@ -423,7 +579,11 @@ int rgbd_masked_attn_fwd(const float* q, const float* k, const float* v, const u
   const size_t rows = (size_t)a.nsplit * Q * BH;
   a.part_o = (float*)ws;
   a.part_ml = (float*)((char*)ws + attn_align(rows * HD * sizeof(float)));
-  k_attn_fwd<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
+  static const char* fwd_env = getenv("RGBD_ATTN_FWD");  // "valu": the thread-per-query kernel
+  if (fwd_env && fwd_env[0] == 'v')
+    k_attn_fwd<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
+  else
+    k_attn_fwd_mfma<<<dim3(a.nsplit, BH, (Q + 63) / 64), 256, 0, s>>>(a);
   const long long orows = (long long)Q * BH;
   k_attn_merge<<<(unsigned)((orows + 7) / 8), 256, 0, s>>>(a);
   RGBD_CHECK_LAUNCH();
@@ -460,7 +620,10 @@ int rgbd_masked_attn_bwd(const float* q, const float* k, const float* v, const u
     k_attn_bwd_kv<<<dim3((L + KVW - 1) / KVW, BH), KVW, 0, s>>>(a);
   else
     k_attn_bwd_kv_mfma<<<dim3((L + 63) / 64, BH), 256, 0, s>>>(a);
-  k_attn_bwd_q<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
+  if (kv_env && kv_env[0] == 'v')
+    k_attn_bwd_q<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
+  else
+    k_attn_bwd_q_mfma<<<dim3(a.nsplit, BH, (Q + 63) / 64), 256, 0, s>>>(a);
   k_attn_dq_sum<<<(unsigned)((rows * HD + 255) / 256), 256, 0, s>>>(a);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
