@@ -10,17 +10,18 @@
 // projections produce it (no head transposes): q / o [Q][BH][32], k / v [L][BH][32], the
 // per-row lse / delta [Q][BH]; the mask is the predictor's [BH][Q][L] bytes.
 //
-// Shapes here are few queries (100) against many keys (300 .. 19 200 per level), so the work is
-// split over KEY ranges (flash-decoding style) to fill 256 CUs:
-//   forward   one thread per query, a workgroup per (bh, key split): the K / V rows are the same
-//             for every lane, so they are scalar loads (SGPR operands of the FMAs); scores in
-//             chunks of 16 keys (mask bits from one 16-byte load) with one online-softmax rescale
-//             per chunk; partial (max, sum, o[32]) per split, merged by k_attn_merge, which also
-//             writes the row log-sum-exp the backward reuses.
-//   dK / dV   one thread per key, a workgroup per (bh, 256 keys): q_scaled / dO rows per query are
-//             scalar loads; p = exp(s - lse), ds = p (dO.v - delta); dv += p dO, dk += ds q_scaled.
-//   dQ        like the forward (thread per query, key splits), partial dq per split summed in split
-//             order by k_attn_dq_sum — no atomics anywhere, the backward is deterministic.
+// Shapes here are few queries (100) against many keys (300 .. 19 200 per level), so the forward
+// and dQ split the work over KEY ranges (flash-decoding style) to fill 256 CUs; partials are merged
+// in split order (no atomics anywhere: the backward is deterministic).  Default kernels run on fp32
+// MFMA (v_mfma_f32_16x16x4_f32, exact f32 products and sums):
+//   k_attn_fwd_mfma     wave = 16 queries; S^T = K q_scaled^T, online softmax per query column,
+//                       O^T += V^T P^T with P^T taken straight from the accumulators; partial
+//                       (max, sum, o) per split -> k_attn_merge (also writes the row log-sum-exp)
+//   k_attn_bwd_kv_mfma  wave = 16 keys over all queries; S, dP, then dV^T += dO^T P, dK^T +=
+//                       q_scaled^T dS, K / V tiles held in registers
+//   k_attn_bwd_q_mfma   the forward's tiling: dq^T += K^T dS^T, partial per split -> k_attn_dq_sum
+// The earlier packed-fp32 VALU kernels (thread per query / per key, K / V rows as scalar loads)
+// stay selectable with RGBD_ATTN_FWD=valu / RGBD_ATTN_KV=valu (A/B and diagnosis).
 #include <cmath>
 #include <cstdlib>
 
