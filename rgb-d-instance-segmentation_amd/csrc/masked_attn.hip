@@ -162,6 +162,34 @@ __global__ __launch_bounds__(QW) void k_attn_fwd(AttnArgs a) {
   *reinterpret_cast<float2*>(a.part_ml + row * 2) = make_float2(m, l);
 }
 
+// K / V tile staging for the MFMA forward and dQ: 64 keys x 32 dims of each, two float4 per
+// thread per matrix, loaded one tile ahead into registers so the global loads overlap the
+// current tile's MFMAs.
+struct KVTile {
+  float4 k[2], v[2];
+};
+
+__device__ __forceinline__ void kv_load(KVTile& t, const float* K, const float* V, int k0, int ke, int BH, int bh,
+                                        int tid) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = tid + 256 * j, row = idx >> 3, c = idx & 7, key = k0 + row;
+    const bool ok = key < ke;
+    const long long off = ((long long)key * BH + bh) * HD + 4 * c;
+    t.k[j] = ok ? *reinterpret_cast<const float4*>(K + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    t.v[j] = ok ? *reinterpret_cast<const float4*>(V + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void kv_store(float (*sk)[HD + 1], float (*sv)[HD + 1], const KVTile& t, int tid) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = tid + 256 * j, row = idx >> 3, c = idx & 7;
+    sk[row][4 * c] = t.k[j].x; sk[row][4 * c + 1] = t.k[j].y; sk[row][4 * c + 2] = t.k[j].z; sk[row][4 * c + 3] = t.k[j].w;
+    sv[row][4 * c] = t.v[j].x; sv[row][4 * c + 1] = t.v[j].y; sv[row][4 * c + 2] = t.v[j].z; sv[row][4 * c + 3] = t.v[j].w;
+  }
+}
+
 // Forward on fp32 MFMA: a wave owns 16 queries (a workgroup 64), keys of the split staged 64 at a
 // time in LDS; per 16-key block
 //   S^T = K . q_scaled^T                     (16k x 16q, 8 MFMAs; q_scaled^T is the register-held
@@ -186,15 +214,13 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs a) {
   float m = -INFINITY, lsum = 0.f;
   const int kb = split * a.span, ke = min(a.L, kb + a.span);
   const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  KVTile nxt;
+  if (kb < ke) kv_load(nxt, a.k, a.v, kb, ke, a.BH, bh, tid);
   for (int k0 = kb; k0 < ke; k0 += 64) {
     __syncthreads();
-    for (int i = tid; i < 64 * HD; i += 256) {
-      const int r = i / HD, d = i % HD, key = k0 + r;
-      const bool ok = key < ke;
-      sk[r][d] = ok ? a.k[((long long)key * a.BH + bh) * HD + d] : 0.f;
-      sv[r][d] = ok ? a.v[((long long)key * a.BH + bh) * HD + d] : 0.f;
-    }
+    kv_store(sk, sv, nxt, tid);
     __syncthreads();
+    if (k0 + 64 < ke) kv_load(nxt, a.k, a.v, k0 + 64, ke, a.BH, bh, tid);
     const int kn = min(64, ke - k0);
     for (int r0 = 0; r0 < kn; r0 += 16) {
       f4m S = {0.f, 0.f, 0.f, 0.f};
@@ -483,15 +509,13 @@ __global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs a) {
   f4m g[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
   const int kb = split * a.span, ke = min(a.L, kb + a.span);
   const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  KVTile nxt;
+  if (kb < ke) kv_load(nxt, a.k, a.v, kb, ke, a.BH, bh, tid);
   for (int k0 = kb; k0 < ke; k0 += 64) {
     __syncthreads();
-    for (int i = tid; i < 64 * HD; i += 256) {
-      const int r = i / HD, d = i % HD, key = k0 + r;
-      const bool ok = key < ke;
-      sk[r][d] = ok ? a.k[((long long)key * a.BH + bh) * HD + d] : 0.f;
-      sv[r][d] = ok ? a.v[((long long)key * a.BH + bh) * HD + d] : 0.f;
-    }
+    kv_store(sk, sv, nxt, tid);
     __syncthreads();
+    if (k0 + 64 < ke) kv_load(nxt, a.k, a.v, k0 + 64, ke, a.BH, bh, tid);
     const int kn = min(64, ke - k0);
     for (int r0 = 0; r0 < kn; r0 += 16) {
       f4m S = {0.f, 0.f, 0.f, 0.f}, DP = {0.f, 0.f, 0.f, 0.f};
