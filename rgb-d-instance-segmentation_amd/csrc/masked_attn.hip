@@ -562,11 +562,16 @@ __global__ __launch_bounds__(256) void k_attn_dq_sum(AttnBwdArgs a) {
   a.dq[i] = acc * a.scale;
 }
 
-// Key splits: enough workgroups to fill the chip (>= ~2048 across the grid), >= KS keys each.
+// Key splits: ~1024 x (Q / 128) workgroups (swept 512..4096 at B=8, L=4800: fewer splits make the
+// merge cheaper, more leave the MFMA kernels no faster), >= KS keys each.
 void split_keys(int BH, int Q, int L, int* nsplit, int* span) {
   const long long base = (long long)BH * ((Q + QW - 1) / QW);
   const int max_split = (L + KS - 1) / KS;
-  int ns = (int)std::min<long long>(max_split, std::max<long long>(1, (2048 + base - 1) / base));
+  static const long long target = [] {  // workgroups to aim for (RGBD_ATTN_WG_TARGET, tuning)
+    const char* e = getenv("RGBD_ATTN_WG_TARGET");
+    return e ? std::max(1LL, atoll(e)) : 1024LL;
+  }();
+  int ns = (int)std::min<long long>(max_split, std::max<long long>(1, (target + base - 1) / base));
   int sp = (L + ns - 1) / ns;
   sp = (sp + KS - 1) / KS * KS;
   *span = sp;
