@@ -377,6 +377,12 @@ size_t rgbd_pp_instance_workspace_size(int B, int Q);
 int rgbd_pp_instance(const float* class_logits, const float* mask_logits, int B, int Q, int C1, int h, int w,
                      const int* target_h_host, const int* target_w_host, double threshold, float* const* seg_host,
                      int* topk_idx, float* pred_scores, int* seg_id, void* ws, void* stream);
+/* return_binary_maps=True of the same call (image_processing_mask2former.py:731-733, used by the
+ * reference's Evaluator, model_essential_part.py:87-92): after rgbd_pp_instance on the same ws and
+ * stream, writes image b's kept masks at its target size, stacked in segment-id order, as float32
+ * 0/1 into out [n_kept][Ht][Wt] (n_kept = the number of seg_id[b][:] >= 0). */
+int rgbd_pp_binary_maps(const void* ws, int B, int Q, int b, int Ht, int Wt, const int* seg_id, float* out,
+                        void* stream);
 
 /* ---------------------------------------------------------------- kernel timing (bench only)
  * When enabled, launch functions bracket their main kernel with hipEvents recorded on the

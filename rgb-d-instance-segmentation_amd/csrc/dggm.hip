@@ -334,8 +334,6 @@ template <int PX> struct PxN<bf16_t, PX> {
   }
 };
 
-__constant__ int g_dggm_dbg;  // RGBD_DGGM_DBG=1: constant gates (timing experiments only)
-__device__ __forceinline__ int dggm_dbg() { return g_dggm_dbg; }
 
 template <int PX>
 struct TileGates {
@@ -363,7 +361,7 @@ __device__ __forceinline__ TileGates<PX> stage_gates(float (*sg)[512], float4* s
     const int p = p0 + i;
     if (i < TP) {
       Gate gt = {{0.f, 0.f, 0.f}};
-      if (p < hw) gt = (dggm_dbg() & 1) ? Gate{{0.5f, 0.25f, 0.125f}} : gate_at(grad, mask, H, W, h, w, p / w, p % w);
+      if (p < hw) gt = gate_at(grad, mask, H, W, h, w, p / w, p % w);
       sg[0][i] = gt.g[0];
       sg[1][i] = gt.g[1];
       sg[2][i] = gt.g[2];
@@ -437,7 +435,6 @@ __device__ __forceinline__ void dggm_fwd_block(float (*sg)[512], float4* swb, in
       y[cc][j] = HAS1 ? y[cc][j] + cp2 : cp2;
     }
   }
-  if (dggm_dbg() & 4) return;
   // stores after all arithmetic: a per-channel guard between loads and uses would let the
   // compiler sink each load into its guarded block (one load latency per channel)
   if (cw + kWaveCh <= C) {
@@ -480,7 +477,7 @@ __device__ __forceinline__ void dggm_bwd_block(float (*sg)[512], float4* swb, fl
   const int cw = by * kBlkCh + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kWaveCh;
   if (cw >= C) return;
   float d[kWaveCh][PX];
-  if (t.valid && !(dggm_dbg() & 2)) {
+  if (t.valid) {
 #pragma unroll
     for (int cc = 0; cc < kWaveCh; ++cc) PxN<T, PX>::load(dout + ((long long)b * C + min(cw + cc, C - 1)) * hw + t.p, d[cc]);
     __builtin_amdgcn_sched_barrier(0);  // keep the whole load batch ahead of the first use
@@ -681,15 +678,6 @@ __global__ __launch_bounds__(256) void k_dggm_fuse_bwd_final_multi(DggmMulti m) 
     d.dw[c * 3 + (j - 1)] = red[0];
 }
 
-void dggm_dbg_init() {
-  static const bool once = [] {
-    const char* e = getenv("RGBD_DGGM_DBG");
-    const int v = e ? atoi(e) : 0;
-    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dggm_dbg), &v, sizeof(int));
-    return true;
-  }();
-  (void)once;
-}
 
 int dggm_px(int h, int w) {
   const long long hw = (long long)h * w;
@@ -772,7 +760,6 @@ int rgbd_dggm_fuse_fwd(int dtype, const void* cp1, const void* color, const floa
   RGBD_REQUIRE((long long)h * w < (1ll << 31), RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
   TimerScope ts("dggm_fwd", s);
-  dggm_dbg_init();
   const int px = dggm_px(h, w);
   if (dtype == RGBD_F32)
     RGBD_DGGM_DISPATCH(launch_fwd, float, px, cp1, color, grad, mask, pv_batch_stride, B, H, W, C, h, w, weight,
@@ -801,7 +788,6 @@ int rgbd_dggm_fuse_bwd(int dtype, const void* dout, const float* grad, const flo
   RGBD_REQUIRE((long long)h * w < (1ll << 31), RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
   TimerScope ts("dggm_bwd", s);
-  dggm_dbg_init();
   const int ntiles = dggm_bwd_tiles(B, h, w), px = dggm_px(h, w);
   float* partial = (float*)ws;
   if (dtype == RGBD_F32)
@@ -878,7 +864,6 @@ int rgbd_dggm_fuse_fwd_multi_mixed(int dtype, int n, const void* const* cp1_host
   }
   hipStream_t s = (hipStream_t)stream;
   TimerScope ts("dggm_fwd", s);
-  dggm_dbg_init();
   if (dtype == RGBD_F32)
     k_dggm_fuse_fwd_multi<float><<<m.total, 256, 0, s>>>(m, grad, mask, pv_batch_stride, H, W);
   else if (dtype == RGBD_BF16)
@@ -917,7 +902,6 @@ int rgbd_dggm_fuse_bwd_multi(int dtype, int n, const void* const* dout_host, con
   }
   hipStream_t s = (hipStream_t)stream;
   TimerScope ts("dggm_bwd", s);
-  dggm_dbg_init();
   if (dtype == RGBD_F32)
     k_dggm_fuse_bwd_multi<float><<<m.total, 256, 0, s>>>(m, grad, mask, pv_batch_stride, H, W);
   else if (dtype == RGBD_BF16)

@@ -218,9 +218,11 @@ extern "C" {
 
 int rgbd_point_sample(const float* maps, int nmaps, int h, int w, const float* coords, int maps_per_coord, int P,
                       float* out, void* stream) {
-  RGBD_REQUIRE(maps && coords && out && nmaps >= 0 && h > 0 && w > 0 && P >= 0 && maps_per_coord > 0, RGBD_E_ARG);
+  // nothing to sample (empty tensors carry null data pointers): checked before the pointers
+  RGBD_REQUIRE(nmaps >= 0 && h > 0 && w > 0 && P >= 0 && maps_per_coord > 0, RGBD_E_ARG);
   const long long n = (long long)nmaps * P;
   if (n == 0) return RGBD_OK;
+  RGBD_REQUIRE(maps && coords && out, RGBD_E_ARG);
   k_point_sample<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(maps, nmaps, h, w, coords,
                                                                                maps_per_coord, P, out);
   RGBD_CHECK_LAUNCH();
@@ -229,9 +231,10 @@ int rgbd_point_sample(const float* maps, int nmaps, int h, int w, const float* c
 
 int rgbd_point_sample_bwd(const float* gout, int nmaps, int h, int w, const float* coords, int maps_per_coord, int P,
                           float* gmaps, void* stream) {
-  RGBD_REQUIRE(gout && coords && gmaps && nmaps >= 0 && h > 0 && w > 0 && P >= 0 && maps_per_coord > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(nmaps >= 0 && h > 0 && w > 0 && P >= 0 && maps_per_coord > 0, RGBD_E_ARG);
   const long long n = (long long)nmaps * P;
   if (n == 0) return RGBD_OK;
+  RGBD_REQUIRE(gout && coords && gmaps, RGBD_E_ARG);
   k_point_sample_bwd<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(gout, nmaps, h, w, coords,
                                                                                    maps_per_coord, P, gmaps);
   RGBD_CHECK_LAUNCH();
@@ -250,8 +253,10 @@ int rgbd_match_cost(const float* pred, int B, int Q, int P, const float* tgt, co
 
 int rgbd_point_losses(const float* logits, const float* labels, int N, int P, float* ce, float* dice, float* sums,
                       void* stream) {
-  RGBD_REQUIRE(logits && labels && ce && dice && sums && N >= 0 && P > 0, RGBD_E_ARG);
+  // N == 0 (a batch without target instances): empty tensors, null pointers, nothing to do
+  RGBD_REQUIRE(N >= 0 && P > 0, RGBD_E_ARG);
   if (N == 0) return RGBD_OK;
+  RGBD_REQUIRE(logits && labels && ce && dice && sums, RGBD_E_ARG);
   k_point_losses<<<N, 256, 0, (hipStream_t)stream>>>(logits, labels, P, ce, dice, sums);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
@@ -259,9 +264,10 @@ int rgbd_point_losses(const float* logits, const float* labels, int N, int P, fl
 
 int rgbd_point_losses_bwd(const float* logits, const float* labels, int N, int P, const float* sums,
                           const float* g_ce, const float* g_dice, float* glogits, void* stream) {
-  RGBD_REQUIRE(logits && labels && sums && g_ce && g_dice && glogits && N >= 0 && P > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(N >= 0 && P > 0, RGBD_E_ARG);
   const long long n = (long long)N * P;
   if (n == 0) return RGBD_OK;
+  RGBD_REQUIRE(logits && labels && sums && g_ce && g_dice && glogits, RGBD_E_ARG);
   k_point_losses_bwd<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(logits, labels, N, P, sums, g_ce,
                                                                                    g_dice, glogits);
   RGBD_CHECK_LAUNCH();

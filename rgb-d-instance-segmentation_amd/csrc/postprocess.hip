@@ -327,6 +327,23 @@ __global__ __launch_bounds__(256) void k_pp_paint(const unsigned long long* __re
   }
 }
 
+// return_binary_maps: the kept entries' resized masks stacked in segment-id order (the
+// reference's torch.stack(instance_maps), float 0/1 at the target size); grid (pixel blocks, Q)
+__global__ __launch_bounds__(256) void k_pp_binary(const unsigned long long* __restrict__ bits,
+                                                   const int* __restrict__ seg_id, int Q, int b, int Ht, int Wt,
+                                                   float* __restrict__ out) {
+  const int j = blockIdx.y;
+  const int id = seg_id[(long long)b * Q + j];
+  if (id < 0) return;  // block-uniform
+  const unsigned long long* bm = bits + ((long long)b * Q + j) * PP_WORDS;
+  const long long np = (long long)Ht * Wt;
+  float* o = out + (long long)id * np;
+  for (long long p = blockIdx.x * 256ll + threadIdx.x; p < np; p += 256ll * gridDim.x) {
+    const int ty = (int)(p / Wt), tx = (int)(p - (long long)ty * Wt);
+    o[p] = bit_at(bm, nearest_index(ty, PP_S, Ht), nearest_index(tx, PP_S, Wt)) ? 1.f : 0.f;
+  }
+}
+
 struct PPWs {
   size_t topv, bits, keep, cnt, total;
 };
@@ -379,6 +396,17 @@ int rgbd_pp_instance(const float* class_logits, const float* mask_logits, int B,
     const int grid = (int)std::min<long long>(std::max<long long>(1, ((long long)Ht * Wt + 255) / 256), 1024);
     k_pp_paint<<<grid, 256, (size_t)Q * 4, s>>>(bits, keep, Q, b, Ht, Wt, seg_id, seg_host[b]);
   }
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_pp_binary_maps(const void* ws, int B, int Q, int b, int Ht, int Wt, const int* seg_id, float* out,
+                        void* stream) {
+  RGBD_REQUIRE(ws && seg_id && out && B > 0 && Q > 0 && b >= 0 && b < B && Ht > 0 && Wt > 0, RGBD_E_ARG);
+  const PPWs L = pp_ws(B, Q);
+  const unsigned long long* bits = (const unsigned long long*)((const char*)ws + L.bits);
+  const int gx = (int)std::min<long long>(std::max<long long>(1, ((long long)Ht * Wt + 255) / 256), 256);
+  k_pp_binary<<<dim3(gx, Q), 256, 0, (hipStream_t)stream>>>(bits, seg_id, Q, b, Ht, Wt, out);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -1201,7 +1201,7 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
 
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
-                                                       bf16_t* __restrict__ y, float* __restrict__ slab, int dbg) {
+                                                       bf16_t* __restrict__ y, float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1264,8 +1264,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 
 #pragma unroll 1
     for (int st = 0; st < C3_STEPS; ++st) {
-      if (dbg & 1) {  // RGBD_C5_DBG bit 1: no weight DMA in the loop (timing experiments only)
-      } else if (st + 1 < C3_STEPS)
+      if (st + 1 < C3_STEPS)
         issue_b(st + 1);
       else if (has_next)
         issue_b(0);
@@ -1303,14 +1302,11 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
       }
       // own DMA landed (except the A piece just issued), own LDS reads done, then the barrier
-      if (dbg & 2)  // RGBD_C5_DBG bit 2: no DMA wait (timing experiments only)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (a_issued)
+      if (a_issued)
         asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    if (dbg & 4) continue;  // RGBD_C5_DBG bit 4: no epilogue
     // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
     // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
     bf16_t* yt = y + (((tile * 8 + wave) * 4) * 4) * 512;  // [mi][nj/2][lane][8]
@@ -1835,13 +1831,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   } while (0)
   // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
   if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
-  const char* bse = getenv("RGBD_BN_STEM_MERGED");  // A/B switch (read per call)
-  if (!(bse && atoi(bse) == 0))
-    k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
-  else
-    for (int l = 0; l < 3; ++l)
-      k_bn_affine<<<64, 256, 0, s>>>(slab, nslab_ch0, STEM_C, 64 * l, 64, P, training, momentum, bn.p[4 * l],
-                                   bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], aff1 + 64 * l);
+  k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate
@@ -1876,8 +1866,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
           (const void*)k_rp_conv3x3_v3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       if (attr != hipSuccess) return (int)attr;
       gcv = conv3_grid(B, H, W);
-      static const int c5dbg = getenv("RGBD_C5_DBG") ? atoi(getenv("RGBD_C5_DBG")) : 0;
-      k_rp_conv3x3_v3<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab, c5dbg);
+      k_rp_conv3x3_v3<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
     } else {
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);

@@ -16,7 +16,6 @@ Backward produces exactly the gradients the reference graph has: DSAM / DGGM par
 nothing for the colour maps (detached) or the ratio (left the graph via .item()).
 """
 import ctypes
-import os
 
 import torch
 
@@ -25,9 +24,6 @@ from . import ops
 DSAM_PARAMS_PER_MODULE = 9  # conv_layers.{0..3}.{weight,bias}, rgb_projection.weight
 _SIDE_STREAMS = {}
 _HIP = None
-_OVERLAP = os.environ.get("RGBD_OVERLAP", "1") != "0"  # side-stream launches (A/B switch)
-_PLAN_AHEAD = os.environ.get("RGBD_PLAN_AHEAD", "1") != "0"  # DSAM legs planned ahead (A/B switch)
-_DW1_MAIN = os.environ.get("RGBD_DW1_MAIN", "0") != "0"  # dsam1's dW on the main stream (A/B switch)
 
 
 def _hip_stream(dev):
@@ -171,7 +167,7 @@ class HotPathFunction(torch.autograd.Function):
             legs = [(ops.LEG_FWD, codes[k], *chans[k]) for k in range(3)]
             if training:
                 legs += [(ops.LEG_DX, codes[k], *chans[k]) for k in (1, 2)]
-            conv_plans = ops.dsam_plan(legs) if _PLAN_AHEAD else [None] * len(legs)
+            conv_plans = ops.dsam_plan(legs)
 
         def pack(k):
             return cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
@@ -189,7 +185,7 @@ class HotPathFunction(torch.autograd.Function):
             for k in range(3):
                 if k == 1:
                     side.join()  # the dsam1 / dsam2 packs
-                    if training and _PLAN_AHEAD:  # dW plans beside the rest of the forward
+                    if training:  # dW plans beside the rest of the forward
                         dw_plans = side.run(lambda: ops.dsam_plan([(ops.LEG_DW, codes[j], *chans[j]) for j in range(3)]),
                                             *codes)
                 bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
@@ -280,11 +276,8 @@ class HotPathFunction(torch.autograd.Function):
         grads_dsam[2] = side.run(lambda: dsam_dw(2, dcp, dcp_nhwc), dcp_nhwc, ctx.x_nhwc[2], ctx.codes[2], ctx.info)
         dcp1, dcp1_nhwc = dsam_dx(2, dcp, dcp_nhwc)
         dcp0, dcp0_nhwc = dsam_dx(1, dcp1, dcp1_nhwc)
-        if _DW1_MAIN:
-            grads_dsam[1] = dsam_dw(1, dcp1, dcp1_nhwc)
-        else:
-            grads_dsam[1] = side.run(lambda: dsam_dw(1, dcp1, dcp1_nhwc), dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1],
-                                     ctx.info)
+        grads_dsam[1] = side.run(lambda: dsam_dw(1, dcp1, dcp1_nhwc), dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1],
+                                 ctx.info)
         grads_dsam[0] = dsam_dw(0, dcp0, dcp0_nhwc)  # the last launches of the backward, the join after them
         pgrads = grads_dsam[0] + grads_dsam[1] + grads_dsam[2] + grads_dggm
         return (None, None, None, None, None, None, None, *pgrads)
@@ -309,6 +302,6 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
         conv = dggm_module.depth_enhancement_layers[i][0]
         params += [conv.weight, conv.bias]
     cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook, "status_sink": status_sink,
-           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": _OVERLAP}
+           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": True}
     pv = pixel_values.detach().float().contiguous()
     return list(HotPathFunction.apply(pv, ratio, cfg, *colors, *params))

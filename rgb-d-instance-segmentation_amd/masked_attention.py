@@ -13,11 +13,20 @@ softmax-attention core (scores, mask, softmax, P.V and the backward) as the HIP 
 sequence-major layout (no head transposes, no [BH, Q, L] score tensor in HBM).
 
 Differences from the torch module, by design: the attention weights (the second output) are not
-materialised — ``None`` is returned unless ``need_weights_output`` is set on the module, in which
-case the call goes through torch's path.  Inputs the kernels do not cover (non-float32, a key
-padding mask, a float mask, dropout in training, head_dim != 32, batch_first) also go through
-torch's path unchanged.  ``install(model)`` swaps the class of the decoder layers'
-``cross_attn`` modules in place (same parameters, same state_dict keys).
+materialised — HF's decoder layer calls the module with the default ``need_weights=True`` whether
+or not anyone reads the weights, so the module takes torch's path (weights returned) only when
+they are consumed: ``need_weights_output`` set on the module, or the decoder layer called with
+``output_attentions=True`` (``install`` registers a forward pre-hook on each decoder layer that
+tells its ``cross_attn`` so).  Inputs the kernels do not cover (a key padding mask, a float
+mask, dropout in training, head_dim != 32, batch_first) also go through torch's path unchanged.
+``install(model)`` swaps the class of the decoder layers' ``cross_attn`` modules in place (same
+parameters, same state_dict keys).
+
+A query row whose every key is masked: torch's softmax gives NaN for the row and its backward
+spreads NaN into dq, dk and dv of that batch-head; the kernels return the NaN row in the forward
+but no gradient from it (its log-sum-exp is +inf, so its probabilities are 0 in the backward).
+HF's decoder un-masks such rows before the call (modeling_mask2former.py:2054-2055), so the model
+never reaches this case.
 """
 import math
 
@@ -69,6 +78,7 @@ def masked_attention(q, k, v, mask, scale):
 
 class HipMultiheadAttention(nn.MultiheadAttention):
     need_weights_output = False
+    _weights_consumed = False  # set per call by the decoder layer's pre-hook (install)
 
     def _hip_ok(self, query, key, value, key_padding_mask, attn_mask, is_causal):
         E = self.embed_dim
@@ -83,7 +93,8 @@ class HipMultiheadAttention(nn.MultiheadAttention):
 
     def forward(self, query, key, value, key_padding_mask=None, need_weights=True, attn_mask=None,
                 average_attn_weights=True, is_causal=False):
-        if self.need_weights_output or not self._hip_ok(query, key, value, key_padding_mask, attn_mask, is_causal):
+        wants = need_weights and (self.need_weights_output or self._weights_consumed)
+        if wants or not self._hip_ok(query, key, value, key_padding_mask, attn_mask, is_causal):
             return super().forward(query, key, value, key_padding_mask=key_padding_mask, need_weights=need_weights,
                                    attn_mask=attn_mask, average_attn_weights=average_attn_weights,
                                    is_causal=is_causal)
@@ -109,13 +120,24 @@ def install_module(m: nn.Module) -> bool:
     return True
 
 
+def _layer_pre_hook(layer, args, kwargs):
+    """Tell the layer's cross-attention whether this call's attention weights are returned."""
+    ca = layer.cross_attn
+    if isinstance(ca, HipMultiheadAttention):
+        ca._weights_consumed = bool(kwargs.get("output_attentions", False))
+    return None
+
+
 def install(model: nn.Module) -> int:
     """Swap the decoder layers' cross-attention modules for the HIP one; returns the count."""
     from transformers.models.mask2former.modeling_mask2former import Mask2FormerMaskedAttentionDecoderLayer
     n = 0
     for m in model.modules():
         if isinstance(m, Mask2FormerMaskedAttentionDecoderLayer):
-            n += install_module(m.cross_attn)
+            if install_module(m.cross_attn):
+                n += 1
+                if getattr(m, "_rgbd_attn_hook", None) is None:
+                    m._rgbd_attn_hook = m.register_forward_pre_hook(_layer_pre_hook, with_kwargs=True)
     return n
 
 
@@ -124,5 +146,10 @@ def uninstall(model: nn.Module) -> int:
     for m in model.modules():
         if type(m) is HipMultiheadAttention:
             m.__class__ = nn.MultiheadAttention
+            m.__dict__.pop("_weights_consumed", None)
             n += 1
+        hook = getattr(m, "_rgbd_attn_hook", None)
+        if hook is not None:
+            hook.remove()
+            m._rgbd_attn_hook = None
     return n

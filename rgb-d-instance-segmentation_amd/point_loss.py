@@ -135,6 +135,11 @@ class HipMask2FormerLoss(Mask2FormerLoss):
         target_masks = target_masks[tgt_idx]
         N = pred_masks.shape[0]
         P = self.num_points
+        if N == 0:
+            # no target instance in the whole batch: HF's sums over zero rows give 0 for both
+            # terms (and zero gradients); keep them attached to the graph like the reference's
+            zero = masks_queries_logits.sum() * 0.0
+            return {"loss_mask": zero, "loss_dice": zero.clone()}
         with torch.no_grad():
             # sample_points_using_uncertainty (:671-724), same torch.rand / topk calls and order
             n_over = int(P * self.oversample_ratio)

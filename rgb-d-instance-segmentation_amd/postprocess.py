@@ -43,7 +43,15 @@ def _run(cls, masks, sizes, threshold):
     sp = (ctypes.c_void_p * B)(*[t.data_ptr() for t in segs])
     check(L.rgbd_pp_instance(_p(cls), _p(masks), B, Q, C1, h, w, th, tw, ctypes.c_double(threshold), sp, _p(topk),
                              _p(ps), _p(sid), _p(ws), _stream(dev)), "rgbd_pp_instance")
-    return segs, topk, ps, sid
+    return segs, topk, ps, sid, ws
+
+
+def _binary_maps(ws, B, Q, b, size, sid, n_kept, dev):
+    """The kept masks of image b at its target size, stacked in segment-id order (float 0/1)."""
+    out = torch.empty((n_kept, *size), dtype=torch.float32, device=dev)
+    check(_lib.lib().rgbd_pp_binary_maps(_p(ws), B, Q, b, size[0], size[1], _p(sid), _p(out), _stream(dev)),
+          "rgbd_pp_binary_maps")
+    return out
 
 
 def post_process_instance_segmentation(outputs, threshold: float = 0.5, mask_threshold: float = 0.5,
@@ -57,8 +65,6 @@ def post_process_instance_segmentation(outputs, threshold: float = 0.5, mask_thr
     like the reference's, or stay on the GPU with ``keep_on_device``."""
     if return_coco_annotation and return_binary_maps:
         raise ValueError("return_coco_annotation and return_binary_maps can not be both set to True.")
-    if return_binary_maps:
-        raise NotImplementedError("return_binary_maps: not used by the reference; not built on the device")
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     cls_all = outputs.class_queries_logits
     masks_all = outputs.masks_queries_logits
@@ -73,14 +79,17 @@ def post_process_instance_segmentation(outputs, threshold: float = 0.5, mask_thr
         _need_cuda(cls, masks)
         sizes = [(384, 384)] * (b1 - b0) if target_sizes is None else \
             [(int(t[0]), int(t[1])) for t in target_sizes[b0:b1]]
-        segs, topk, ps, sid = _run(cls, masks, sizes, float(threshold))
+        segs, topk, ps, sid, ws = _run(cls, masks, sizes, float(threshold))
         C = cls.shape[-1] - 1
         topk_h, ps_h, sid_h = topk.cpu().tolist(), ps.cpu().tolist(), sid.cpu().tolist()
         for i in range(b1 - b0):
             segments = [{"id": sid_h[i][j], "label_id": topk_h[i][j] % C, "was_fused": False,
                          "score": round(ps_h[i][j], 6)}
                         for j in range(len(sid_h[i])) if sid_h[i][j] >= 0]
-            seg = segs[i] if keep_on_device else segs[i].cpu()
+            seg = segs[i]
+            if return_binary_maps and segments:  # the reference keeps the -1 map when nothing is kept
+                seg = _binary_maps(ws, b1 - b0, cls.shape[1], i, sizes[i], sid, len(segments), dev)
+            seg = seg if keep_on_device else seg.cpu()
             if return_coco_annotation:
                 from transformers.models.mask2former.image_processing_pil_mask2former import convert_segmentation_to_rle
                 seg = convert_segmentation_to_rle(seg)
@@ -88,11 +97,27 @@ def post_process_instance_segmentation(outputs, threshold: float = 0.5, mask_thr
     return results
 
 
+def _device_covers(outputs) -> bool:
+    """Inputs the device path takes: a class-logit table the top-k selection fits in LDS."""
+    cls = outputs.class_queries_logits
+    return cls.dim() == 3 and cls.shape[1] * (cls.shape[2] - 1) * 8 <= 163840 and cls.shape[2] >= 2
+
+
 def install(image_processor, device=None):
     """Route ``image_processor.post_process_instance_segmentation`` (an HF Mask2Former image
-    processor instance, as the reference's predictor builds it) through the device path."""
+    processor instance, as the reference's predictor builds it, and as its Evaluator calls it
+    with ``return_binary_maps=True``, model_essential_part.py:87-92) through the device path.
+    The original bound method is kept (``image_processor._hf_post_process_instance_segmentation``)
+    and taken for inputs the device path does not cover (a class table too large for the LDS
+    top-k), so an installed processor never fails where the reference's would not."""
+    original = getattr(image_processor, "_hf_post_process_instance_segmentation",
+                       image_processor.post_process_instance_segmentation)
+
     def method(outputs, *args, **kwargs):
+        if not _device_covers(outputs):
+            return original(outputs, *args, **kwargs)
         kwargs.setdefault("device", device)
         return post_process_instance_segmentation(outputs, *args, **kwargs)
+    image_processor._hf_post_process_instance_segmentation = original
     image_processor.post_process_instance_segmentation = method
     return image_processor

@@ -22,11 +22,15 @@ pytestmark = pytest.mark.gpu
 REPO = Path(__file__).resolve().parents[1]
 
 
-def test_bench_launcher_world2_json():
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("H,W", [(96, 128), (480, 640)], ids=["96x128", "C3_640x480"])
+def test_bench_launcher_world2_json(H, W):
+    """bench.py --gpus 2 end to end (its own launcher, 8 images per rank), incl. BASELINE's C3
+    shape; gloo, both ranks on the test box's one GPU."""
     r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "2",
                         "--warmup", "1", "--cpu-baseline", "0", "--c5-stream", "0", "--inference", "0", "--parity", "0",
-                        "--height", "96", "--width", "128"],
-                       capture_output=True, text=True, timeout=240, cwd=REPO)
+                        "--height", str(H), "--width", str(W)],
+                       capture_output=True, text=True, timeout=280, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -44,7 +48,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, shape):
     try:
         import torch.distributed as dist
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -52,7 +56,8 @@ def _worker(rank, world, port, q):
         sys.path.insert(0, str(REPO))
         import bench
         dev = torch.device("cuda:0")
-        args = bench.parse(["--height", "96", "--width", "128", "--batch", "3"])
+        H, W, B = shape
+        args = bench.parse(["--height", str(H), "--width", str(W), "--batch", str(B)])
         # standalone gradients of both shards (ratio predictor in eval: a deterministic ratio)
         ref = []
         for r in range(world):
@@ -105,14 +110,18 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-def test_ddp_step_gradients_and_buffers_world2():
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("shape", [(96, 128, 3), (480, 640, 8)], ids=["96x128_b3", "C3_640x480_b8"])
+def test_ddp_step_gradients_and_buffers_world2(shape):
+    """Small shape, and BASELINE configs[2] (C3) at its workload: 640x480, 8 images per rank, bf16,
+    world size 2 (global batch 16) — gloo with both ranks on the one GPU of the test box."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shape)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=200) for _ in procs)
+    res = dict(q.get(timeout=360) for _ in procs)
     for p in procs:
         p.join(timeout=60)
     for r in (0, 1):

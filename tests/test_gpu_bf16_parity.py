@@ -1,0 +1,119 @@
+"""bf16 parity at BASELINE's headline configurations, with the ratio predictor NOT injected.
+
+BASELINE.json names bf16 at 640x480 (configs[1], C2: inference, B=8) and 1280x720 (configs[4],
+C5: the RealSense stream, B=1).  In bf16 the whole chain runs as it does in the bench: K1
+assembles pixel_values from the u8 frames, K4 predicts the ratio in bf16 (eval mode), and K3
+decomposes the depth at THAT ratio.  The reference computes everything in float32
+(custom_model.py:336-351), so the only way bf16 can change a discrete decision is through the
+ratio: the window bounds c -/+ c*r/2 (custom_model.py:766-772) move with r, and pixels whose
+grey depth lies between the two bounds change region.  These tests measure exactly that:
+
+* the bf16 ratio against the fp32 oracle's (oracle/ratio.py, the reference's float32 module
+  math), per image;
+* everything of the decomposition that does not depend on the ratio (histogram, modes,
+  centres) bit-exact against the oracle;
+* the DSAM region codes the GPU computes at its bf16 ratio, bit-exact against the oracle at
+  the same ratio (the kernel path is exact);
+* the region-code cells (at the three DSAM input resolutions) that differ from the oracle's
+  decomposition at the fp32 ratio — the decisions bf16 flips — counted and bounded.
+
+Stated bf16 tolerances (measured values are printed):
+    |ratio_bf16 - ratio_fp32| <= 2e-3 (absolute; the ratio lies in [0.01, 0.5])
+    flipped region-code cells <= 0.5 % per scale and image
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_inputs as gi
+from oracle import edsam, ratio as ratio_o
+from rgbd_amd import init as winit, synthetic
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+PRE = "model.pixel_level_module.ratio_predictor."
+RATIO_ATOL = 2e-3
+FLIP_FRAC = 5e-3
+
+
+def _ratio_module():
+    from rgbd_amd.modules import EnhancedDepthImageRatioPredictor
+    m = EnhancedDepthImageRatioPredictor(3)
+    winit.init_deterministic(m, prefix=PRE)
+    return m.eval()
+
+
+def _check_config(cfg_id, B, H, W):
+    from rgbd_amd import ops
+    scenes = [synthetic.make_scene(synthetic.scene_seed(cfg_id, i), H, W) for i in range(B)]
+    depth = torch.from_numpy(np.stack([s["depth_u8"] for s in scenes])).to(DEV)
+    rgb = torch.from_numpy(np.stack([s["rgb_u8"] for s in scenes])).contiguous().to(DEV)
+    pv = ops.assemble_pixel_values(depth, rgb)
+    m = _ratio_module()
+    p32 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m.compute_dtype = torch.bfloat16
+    m = m.to(DEV)
+    with torch.no_grad():
+        r_bf16 = m(pv[:, 3:6]).float()
+    sizes = gi.pool_sizes(H, W)
+    codes, info = ops.edsam_decompose(pv, r_bf16, sizes)
+    rec = ops.decode_info(info)
+    pv_h = pv.cpu()
+    with torch.no_grad():
+        r_fp32 = ratio_o.ratio_forward(pv_h[:, 3:6], p32, training=False).numpy().reshape(-1)
+    r_bf16 = r_bf16.cpu().numpy().reshape(-1)
+    report = []
+    for b in range(B):
+        d3 = pv_h[b, 3:6].numpy()
+        ref = edsam.decompose(d3, float(r_fp32[b]))       # the reference's decisions (fp32 ratio)
+        at_bf16 = edsam.decompose(d3, float(r_bf16[b]))   # the oracle at the GPU's own ratio
+        # ratio-independent parts: bit-exact
+        np.testing.assert_array_equal(rec[b]["hist"], ref["hist"])
+        assert rec[b]["n_modes"] == ref["n_modes"] and rec[b]["n_masks"] == ref["n_masks"]
+        np.testing.assert_array_equal(rec[b]["center"][:ref["n_modes"]], np.asarray(ref["centers"], np.float32))
+        flips = []
+        for s, (oh, ow) in enumerate(sizes):
+            got = codes[s][b].cpu().numpy()
+            # the kernels are exact: at the bf16 ratio they reproduce the oracle at that ratio
+            np.testing.assert_array_equal(got, edsam.pooled_codes(at_bf16["code"], oh, ow))
+            flips.append(float((got != edsam.pooled_codes(ref["code"], oh, ow)).mean()))
+        report.append((float(r_bf16[b]), float(r_fp32[b]), flips))
+    for b, (rb, rf, flips) in enumerate(report):
+        print(f"cfg{cfg_id} {W}x{H} image {b}: ratio bf16 {rb:.6f} fp32 {rf:.6f} (|d| {abs(rb - rf):.2e}); "
+              f"flipped region-code cells per scale {[f'{f:.2e}' for f in flips]}")
+    worst_r = max(abs(rb - rf) for rb, rf, _ in report)
+    worst_f = max(max(f) for _, _, f in report)
+    print(f"cfg{cfg_id}: worst |ratio_bf16 - ratio_fp32| = {worst_r:.3g} (bound {RATIO_ATOL}); "
+          f"worst flipped fraction = {worst_f:.3g} (bound {FLIP_FRAC})")
+    assert worst_r <= RATIO_ATOL
+    assert worst_f <= FLIP_FRAC
+
+
+@pytest.mark.timeout(240)
+def test_bf16_eval_decisions_c2_640x480_b8():
+    """BASELINE configs[1] (C2): 640x480, B=8, bf16 inference."""
+    _check_config(2, 8, 480, 640)
+
+
+@pytest.mark.timeout(240)
+def test_bf16_eval_decisions_c5_1280x720():
+    """BASELINE configs[4] (C5): 1280x720 RealSense frame, B=1 (the ragged conv5 path: 720 rows
+    are not a multiple of the 32-row pool tiles) — plus a second frame in the same batch."""
+    _check_config(5, 2, 720, 1280)
+
+
+@pytest.mark.timeout(240)
+def test_bf16_full_model_mask_logits_vs_g7_640x480():
+    """BASELINE.json's mask-logit metric at 640x480 with the hot path in bf16 (as benched; the
+    ratio from the bf16 ratio predictor): max |mask logit - reference| against the reference's
+    float32 CPU run (G7), bounded relative to the logit scale (bench.BF16_LOGIT_REL_TOL); the
+    float32 run of the same model stays within BASELINE's 1e-3."""
+    import bench
+    f32 = bench.parity(torch.device(DEV))
+    b16 = bench.parity(torch.device(DEV), torch.bfloat16)
+    print(f"G7 640x480 mask logits: f32 max-abs-err {f32['mask_logit_max_abs_err']:.3g}; bf16 max-abs-err "
+          f"{b16['mask_logit_max_abs_err']:.3g} (rel {b16['mask_logit_max_rel_err']:.3g}), bf16 ratio rel err "
+          f"{b16['ratio_rel_err']:.3g}")
+    assert f32["input_sha_match"] and b16["input_sha_match"]
+    assert f32["mask_logit_max_abs_err"] <= 1e-3
+    assert b16["mask_logit_max_rel_err"] <= bench.BF16_LOGIT_REL_TOL

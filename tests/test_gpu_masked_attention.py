@@ -97,6 +97,14 @@ def test_fully_masked_row_is_nan_like_torch():
     assert bool(out_r[2, 0].isnan().all()) and bool(out_h[2, 0].isnan().all())
     ok = ~out_r.isnan()
     assert float((out_h[ok] - out_r[ok]).abs().max()) <= 1e-5 * (1 + float(out_r[ok].abs().max()))
+    # backward (documented divergence, masked_attention.py docstring): torch spreads NaN into the
+    # whole batch-head; the kernels give that row no gradient and keep every other one finite
+    qh = [t.clone().requires_grad_() for t in (query, key, value)]
+    out_h, _ = hip(*qh, attn_mask=mask)
+    g = torch.ones_like(out_h)
+    g[2] = 0.0  # the NaN query row carries no upstream gradient
+    torch.nan_to_num(out_h, nan=0.0).backward(g)
+    assert all(bool(t.grad.isfinite().all()) for t in qh)
 
 
 @gpu
@@ -121,4 +129,13 @@ def test_install_in_decoder_layers():  # CPU: class swap only
     assert n == cfg.decoder_layers - 1
     assert all(type(m) is masked_attention.HipMultiheadAttention for m in dec.modules()
                if isinstance(m, nn.MultiheadAttention))
+    # output_attentions=True on a decoder layer: its cross-attention takes torch's path, which
+    # returns the weights HF then hands back (the pre-hook install() registers)
+    layer = dec.layers[0]
+    masked_attention._layer_pre_hook(layer, (), {"output_attentions": True})
+    assert layer.cross_attn._weights_consumed
+    masked_attention._layer_pre_hook(layer, (), {"output_attentions": False})
+    assert not layer.cross_attn._weights_consumed
+    assert all(getattr(m, "_rgbd_attn_hook", None) is not None for m in dec.layers)
     assert masked_attention.uninstall(dec) == n
+    assert all(getattr(m, "_rgbd_attn_hook", None) is None for m in dec.layers)

@@ -95,3 +95,30 @@ def test_install_swaps_loss_and_matcher():
     assert isinstance(holder.criterion, point_loss.HipMask2FormerLoss)
     assert isinstance(holder.criterion.matcher, matcher.HipHungarianMatcher)
     assert point_loss.uninstall(holder) == 1 and type(holder.criterion) is Mask2FormerLoss
+
+
+def test_loss_all_images_empty_matches_reference():
+    """A batch without any target instance: the whole Mask2FormerLoss (matcher, mask
+    terms, classification term) equals HF's, mask and dice terms 0, and the backward runs."""
+    from transformers import Mask2FormerConfig
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerLoss
+    cfg = Mask2FormerConfig(num_labels=48)
+    wd = {"loss_cross_entropy": 2.0, "loss_mask": 5.0, "loss_dice": 5.0}
+    ref_loss, hip_loss = Mask2FormerLoss(cfg, weight_dict=wd), Mask2FormerLoss(cfg, weight_dict=wd)
+    holder = torch.nn.Module()
+    holder.criterion = hip_loss
+    assert point_loss.install(holder) == 1
+    masks, classes, ml, cl = _case(9, B=2, L=49, counts=(0, 0))
+    mr = masks.clone().requires_grad_(True)
+    mh = masks.clone().requires_grad_(True)
+    torch.manual_seed(11)
+    r = ref_loss(mr, classes, ml, cl)
+    torch.manual_seed(11)
+    h = holder.criterion(mh, classes, ml, cl)
+    assert set(r) == set(h)
+    for k in r:
+        assert abs(float(h[k]) - float(r[k])) <= 1e-5 * abs(float(r[k])) + 1e-7, (k, float(h[k]), float(r[k]))
+    assert float(h["loss_mask"]) == 0.0 and float(h["loss_dice"]) == 0.0
+    sum(h.values()).backward()
+    sum(r.values()).backward()
+    assert torch.equal(mh.grad, mr.grad)

@@ -76,3 +76,38 @@ def test_rejects_bad_arguments():
     outs = types.SimpleNamespace(class_queries_logits=torch.zeros((1, 4, 3)), masks_queries_logits=torch.zeros((1, 4, 8, 8)))
     with pytest.raises(ValueError):
         post_process_instance_segmentation(outs, return_coco_annotation=True, return_binary_maps=True)
+
+
+@pytest.mark.parametrize("target", [None, [(480, 640), (97, 131)]])
+@pytest.mark.parametrize("threshold", [0.3, 1.1])
+def test_binary_maps_match_hf(target, threshold):
+    """return_binary_maps=True, as the reference's Evaluator calls it (model_essential_part.py:87-92):
+    the kept masks stacked in segment order, bit-identical; the -1 map when nothing is kept."""
+    from rgbd_amd.postprocess import post_process_instance_segmentation
+    rng = np.random.default_rng(17)
+    B, Q, C, h, w = 2, 100, 48, 120, 160
+    cl = rng.standard_normal((B, Q, C + 1)).astype(np.float32) * 4
+    cl[:, ::3, 5] += 7.0
+    ml = rng.standard_normal((B, Q, h, w)).astype(np.float32) * 3
+    ref = _ref(cl, ml, target_sizes=target, threshold=threshold, return_binary_maps=True)
+    outs = types.SimpleNamespace(class_queries_logits=torch.from_numpy(cl), masks_queries_logits=torch.from_numpy(ml))
+    got = post_process_instance_segmentation(outs, target_sizes=target, threshold=threshold, return_binary_maps=True)
+    if threshold > 1.0:
+        assert all(len(r["segments_info"]) == 0 for r in ref)
+    else:
+        assert all(r["segmentation"].dim() == 3 for r in ref)
+    _compare(ref, got)
+
+
+def test_install_falls_back_to_hf_outside_the_device_path():
+    """A class table too large for the LDS top-k takes the processor's own method."""
+    from transformers.models.mask2former.image_processing_pil_mask2former import Mask2FormerImageProcessorPil
+    from rgbd_amd.postprocess import install
+    rng = np.random.default_rng(3)
+    cl = rng.standard_normal((1, 100, 301)).astype(np.float32) * 4  # 100 x 300 x 8 B > 160 KiB
+    ml = rng.standard_normal((1, 100, 30, 40)).astype(np.float32) * 3
+    outs = types.SimpleNamespace(class_queries_logits=torch.from_numpy(cl), masks_queries_logits=torch.from_numpy(ml))
+    ref = Mask2FormerImageProcessorPil().post_process_instance_segmentation(outs, threshold=0.0, return_binary_maps=True)
+    proc = install(Mask2FormerImageProcessorPil())
+    got = proc.post_process_instance_segmentation(outs, threshold=0.0, return_binary_maps=True)
+    _compare(ref, got)
