@@ -201,7 +201,7 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False):
     from rgbd_amd import ops
     from rgbd_amd.distributed import (BufferBroadcaster, InBackwardOptimizer, OverlappedGradReducer,
                                       hot_path_grad_groups)
-    from rgbd_amd.hot_path import hot_path
+    from rgbd_amd.hot_path import hot_path, prepare
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
     groups = hot_path_grad_groups(ctx["dsams"], ctx["dg"])
     # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
@@ -221,8 +221,10 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False):
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
         if bcast is not None:  # DDP broadcast_buffers: every forward starts from rank 0's BN stats
             bcast.sync()
+        prep = prepare(pv, ctx["colors"], ctx["dtype"])  # ratio-free decomposition beside the ratio predictor
         ratio = ctx["rp"](pv[:, 3:6])
-        feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], grad_hook=hook)
+        feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], grad_hook=hook,
+                         prepared=prep)
         torch.autograd.backward(feats, ctx["gouts"])
         if reducer is not None and not overlap_opt:  # DDP gradient exchange (RCCL over xGMI)
             reducer.finish()
@@ -242,13 +244,14 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False):
 
 def make_step(ctx, world, inference=False, graph=False):
     from rgbd_amd import ops
-    from rgbd_amd.hot_path import hot_path
+    from rgbd_amd.hot_path import hot_path, prepare
     if inference:
         def istep():
             pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
             with torch.no_grad():
+                prep = prepare(pv, ctx["colors"], ctx["dtype"])
                 ratio = ctx["rp"](pv[:, 3:6])
-                return hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"])
+                return hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], prepared=prep)
         return istep
     if graph:  # single process: the whole step replayed from a HIP graph, captured on first use
         from rgbd_amd.train_graph import CapturedTrainStep

@@ -3,20 +3,25 @@
 // Reference: DSAModule (mask2former/utils/custom_model.py:622-798), which per sample and per
 // DSAM copies the grey depth to the host, runs np.histogram(512) + scipy find_peaks, builds
 // full-resolution numpy masks and copies them back.  Here the same discrete decisions are
-// made on device in four stream-ordered launches (no host sync):
+// made on device in stream-ordered launches (no host sync), split in two phases:
+//  phase A, rgbd_edsam_modes (does not depend on the ratio: runs beside the ratio predictor)
 //   1. k_grey_minmax : grey = 0.299 d0 + 0.587 d1 + 0.114 d2 (f32, one rounding per op,
-//                      :466-480) and nanmin/nanmax via order-preserving uint atomics (:715)
-//   2. k_hist        : numpy's uniform-bin fast path (index = int((x-first)/(last-first)*512)
-//                      with the +-1 edge corrections), LDS-privatised 512-bin histogram
-//   3. k_peaks       : one 512-thread workgroup per image: plateau-aware local maxima
+//                      :466-480), written once to the workspace (4 B/px), and nanmin/nanmax via
+//                      order-preserving uint keys (:715)
+//   2. k_hist        : numpy's uniform-bin fast path over the grey plane (index =
+//                      int((x-first)/(last-first)*512) with the +-1 edge corrections),
+//                      LDS-privatised 512-bin histogram
+//   3. k_modes       : one 512-thread workgroup per image: plateau-aware local maxima
 //                      (scipy _local_maxima_1d), wave-cooperative prominence search
 //                      (scipy _peak_prominences, wlen = whole signal), threshold
-//                      0.01*max(hist) in float64, top-3 by (count, centre), windows (:754-772)
-//   4. k_codes_pool  : per-pixel 4-bit region code (bit i <-> conv_layers[i], :774-798) OR-pooled
-//                      over the adaptive_max_pool2d bins of each DSAM input resolution (:687)
+//                      0.01*max(hist) in float64, top-3 by (count, centre) and the centres
+//  phase B, rgbd_edsam_codes (after the ratio): one launch
+//   4. k_codes_pyramid / k_codes_pool: the windows from the centres and the ratio (:754-772),
+//                      then the per-pixel 4-bit region code (bit i <-> conv_layers[i],
+//                      :774-798) of the grey plane OR-pooled over the adaptive_max_pool2d bins
+//                      of each DSAM input resolution (:687)
 // Every float op that feeds a discrete decision uses an explicitly rounded intrinsic, so the
 // result is bit-exact to the numpy 2.2 / scipy 1.15 reference.
-#include <cstdlib>
 #include "common.hpp"
 #include "timing.hpp"
 
@@ -72,17 +77,16 @@ __device__ __forceinline__ float edge_at(const Range& r, int i) {
 // blocks x 8 images of same-line atomics this replaced serialised for ~20 us).
 __global__ __launch_bounds__(256) void k_grey_minmax(const float* __restrict__ depth3, long long bstride,
                                                      long long HW, int nch, uint2* __restrict__ part,
-                                                     rgbd_decomp_info* __restrict__ info, uint32_t* __restrict__ cmask,
-                                                     int ncmask) {
+                                                     rgbd_decomp_info* __restrict__ info, float* __restrict__ grey) {
   const int b = blockIdx.y;
-  if (blockIdx.x == 0) {  // k_hist adds into the histogram; the code-presence masks are OR-ed into
+  if (blockIdx.x == 0)  // k_hist adds into the histogram
     for (int i = threadIdx.x; i < RGBD_NBINS; i += 256) info[b].hist[i] = 0;
-    if (b == 0 && cmask && threadIdx.x < ncmask) cmask[threadIdx.x] = 0u;
-  }
   const float* d = depth3 + b * bstride;
+  float* gout = grey ? grey + b * HW : nullptr;
   uint32_t kmin = 0xffffffffu, kmax = 0u;
   for (long long p = blockIdx.x * 256ll + threadIdx.x; p < HW; p += 256ll * gridDim.x) {
     const float g = grey_at(d, HW, p, nch);
+    if (gout) gout[p] = g;
     if (!isnan(g)) {  // np.nanmin / np.nanmax
       const uint32_t k = f32_key(g);
       kmin = min(kmin, k);
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(256) void k_hist(const float* __restrict__ depth3, 
   __shared__ uint32_t h[RGBD_NBINS];
   const int b = blockIdx.y;
   const DecWs mm = reduce_parts(part + (long long)b * gridDim.x, gridDim.x);
-  if (blockIdx.x == 0 && threadIdx.x == 0) ws[b] = mm;  // for k_peaks / k_codes_pool
+  if (blockIdx.x == 0 && threadIdx.x == 0) ws[b] = mm;  // for k_modes
   const Range r = make_range(mm);
   if (r.status != 0) return;  // uniform per block
   for (int i = threadIdx.x; i < RGBD_NBINS; i += 256) h[i] = 0;
@@ -165,8 +169,7 @@ __device__ __forceinline__ long long wave_max_i64(long long v) {
   return v;
 }
 
-__global__ __launch_bounds__(512) void k_peaks(const DecWs* ws, const float* __restrict__ ratio,
-                                               rgbd_decomp_info* info) {
+__global__ __launch_bounds__(512) void k_modes(const DecWs* ws, rgbd_decomp_info* info) {
   __shared__ int x[RGBD_NBINS];
   __shared__ int peaks[RGBD_NBINS];
   __shared__ int is_kept[RGBD_NBINS];
@@ -259,20 +262,14 @@ __global__ __launch_bounds__(512) void k_peaks(const DecWs* ws, const float* __r
     __syncthreads();
   }
   if (t == 0) {
-    const float rr = ratio[b];
     int n = 0;
     for (int m = 0; m < RGBD_MAX_MODES; ++m) {
       const int p = sel[m];
       if (p < 0) break;
       const float e0 = edge_at(r, p), e1 = edge_at(r, p + 1);
-      const float c = __fadd_rn(e0, __fmul_rn(__fsub_rn(e1, e0), 0.5f));  // edge + diff/2 (:745)
-      const float half = __fmul_rn(__fmul_rn(c, rr), 0.5f);                // c * r / 2 (:768)
-      float lo = __fsub_rn(c, half);
-      if (!(lo > 0.f)) lo = 0.f;                                            // max(0, .) (:769)
       out->peak_bin[m] = p;
-      out->center[m] = c;
-      out->lo[m] = lo;
-      out->hi[m] = __fadd_rn(c, half);                                       // (:770)
+      out->center[m] = __fadd_rn(e0, __fmul_rn(__fsub_rn(e1, e0), 0.5f));  // edge + diff/2 (:745)
+      out->lo[m] = out->hi[m] = 0.f;                                       // phase B (the ratio)
       ++n;
     }
     for (int m = n; m < RGBD_MAX_MODES; ++m) {
@@ -287,6 +284,39 @@ __global__ __launch_bounds__(512) void k_peaks(const DecWs* ws, const float* __r
   }
 }
 
+// The depth-interval windows of an image (custom_model.py:754-772) from its centres and ratio:
+// half = c * r / 2 in f32, lo = max(0, c - half) (0 when clamped), hi = c + half.  Every block of
+// a codes launch computes them; ``publish`` (one thread of the launch) also stores them in the
+// image's record.
+struct Windows {
+  int n;
+  float lo[RGBD_MAX_MODES], hi[RGBD_MAX_MODES];
+};
+__device__ __forceinline__ Windows windows_of(rgbd_decomp_info* info, const float* __restrict__ ratio, int b,
+                                              bool publish) {
+  Windows w;
+  w.n = info[b].n_modes;
+  const float rr = ratio[b];
+  for (int m = 0; m < RGBD_MAX_MODES; ++m) {
+    float lo = 0.f, hi = 0.f;
+    if (m < w.n) {
+      const float c = info[b].center[m];
+      const float half = __fmul_rn(__fmul_rn(c, rr), 0.5f);  // c * r / 2 (:768)
+      lo = __fsub_rn(c, half);
+      if (!(lo > 0.f)) lo = 0.f;                             // max(0, .) (:769)
+      hi = __fadd_rn(c, half);                               // (:770)
+    }
+    w.lo[m] = lo;
+    w.hi[m] = hi;
+  }
+  if (publish)
+    for (int m = 0; m < RGBD_MAX_MODES; ++m) {
+      info[b].lo[m] = w.lo[m];
+      info[b].hi[m] = w.hi[m];
+    }
+  return w;
+}
+
 __device__ __forceinline__ uint32_t pixel_code(float g, int n, const float* lo, const float* hi) {
   if (n == 0) return 0u;  // no mode: four all-zero masks (:676-678)
   uint32_t c = 0u;
@@ -297,18 +327,17 @@ __device__ __forceinline__ uint32_t pixel_code(float g, int n, const float* lo, 
 }
 
 __global__ __launch_bounds__(256) void k_codes_pool(const float* __restrict__ depth3, long long bstride,
-                                                    int H, int W, int nch, int oh, int ow,
-                                                    const rgbd_decomp_info* info, uint8_t* __restrict__ code) {
+                                                    int H, int W, int nch, int oh, int ow, rgbd_decomp_info* info,
+                                                    const float* __restrict__ ratio, int publish,
+                                                    uint8_t* __restrict__ code) {
   const int b = blockIdx.y;
   const int q = blockIdx.x * 256 + threadIdx.x;
+  const Windows win = windows_of(info, ratio, b, publish && blockIdx.x == 0 && threadIdx.x == 0);
   if (q >= oh * ow) return;
   const int i = q / ow, j = q % ow;
-  const int n = info[b].n_modes;
-  float lo[RGBD_MAX_MODES], hi[RGBD_MAX_MODES];
-  for (int t = 0; t < RGBD_MAX_MODES; ++t) {
-    lo[t] = info[b].lo[t];
-    hi[t] = info[b].hi[t];
-  }
+  const int n = win.n;
+  const float* lo = win.lo;
+  const float* hi = win.hi;
   // adaptive_max_pool2d bins: [floor(i*H/oh), ceil((i+1)*H/oh))
   const int y0 = (i * H) / oh, y1 = ((i + 1) * H + oh - 1) / oh;
   const int x0 = (j * W) / ow, x1 = ((j + 1) * W + ow - 1) / ow;
@@ -328,19 +357,19 @@ __global__ __launch_bounds__(256) void k_codes_pool(const float* __restrict__ de
 // from its pixels, OR-pools 2 x 2 cells twice through LDS (exactly adaptive_max_pool2d of the
 // full-resolution masks, bins nesting), and ORs 1 << code into the per-level presence masks.
 __global__ __launch_bounds__(256) void k_codes_pyramid(const float* __restrict__ depth3, long long bstride, int H, int W,
-                                                       int nch, int oh0, int ow0, const rgbd_decomp_info* info,
+                                                       int nch, int oh0, int ow0, rgbd_decomp_info* info,
+                                                       const float* __restrict__ ratio,
                                                        uint8_t* __restrict__ c0, uint8_t* __restrict__ c1,
                                                        uint8_t* __restrict__ c2, uint32_t* __restrict__ cmask) {
   __shared__ uint8_t s0[16][17], s1[8][9];
   __shared__ uint32_t smask[3];
   const int b = blockIdx.z, tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int i = blockIdx.y * 16 + ty, j = blockIdx.x * 16 + tx;
-  const int n = info[b].n_modes;
-  float lo[RGBD_MAX_MODES], hi[RGBD_MAX_MODES];
-  for (int t = 0; t < RGBD_MAX_MODES; ++t) {
-    lo[t] = info[b].lo[t];
-    hi[t] = info[b].hi[t];
-  }
+  const Windows win =
+      windows_of(info, ratio, b, blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0);
+  const int n = win.n;
+  const float* lo = win.lo;
+  const float* hi = win.hi;
   if (threadIdx.x < 3) smask[threadIdx.x] = 0u;
   const int fy = H / oh0, fx = W / ow0;
   const long long HW = (long long)H * W;
@@ -402,46 +431,56 @@ __global__ __launch_bounds__(256) void k_codes_or_pool(const uint8_t* __restrict
   code[(long long)b * oh * ow + q] = (uint8_t)c;
 }
 
-}  // namespace
+// Windows only (a codes call without output planes): one thread per image.
+__global__ void k_windows(rgbd_decomp_info* info, const float* __restrict__ ratio, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) (void)windows_of(info, ratio, b, true);
+}
 
-extern "C" {
-
-size_t rgbd_edsam_decompose_workspace_size(int B) {
+size_t ws_head(int B) {
   const size_t nb = (size_t)(B > 0 ? B : 1);
   return align256(sizeof(DecWs) * nb) + align256(sizeof(uint2) * kDecParts * nb);
 }
 
-static int decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
-                     const float* ratio, int n_scales, const int* out_h_host, const int* out_w_host,
-                     uint8_t* const* codes_host, rgbd_decomp_info* info, uint32_t* code_masks, void* ws,
-                     void* stream) {
-  RGBD_REQUIRE(depth3 && ratio && info && ws, RGBD_E_ARG);
-  RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && n_scales >= 0 && n_scales <= 8, RGBD_E_ARG);
-  RGBD_REQUIRE(depth_channels == 1 || depth_channels == 3, RGBD_E_SHAPE);
-  const int nch = depth_channels;
-  for (int s = 0; s < n_scales; ++s) {
-    RGBD_REQUIRE(out_h_host && out_w_host && codes_host && codes_host[s], RGBD_E_ARG);
-    RGBD_REQUIRE(out_h_host[s] > 0 && out_w_host[s] > 0 && out_h_host[s] <= H && out_w_host[s] <= W,
-                 RGBD_E_SHAPE);
-  }
-  hipStream_t st = (hipStream_t)stream;
+// phase A: grey (into ``grey`` when given), min/max, histogram, modes
+int modes_impl(const float* depth3, long long batch_stride, int nch, int B, int H, int W, rgbd_decomp_info* info,
+               void* ws, float* grey, hipStream_t st) {
   DecWs* w = (DecWs*)ws;
   const long long HW = (long long)H * W;
-  TimerScope ts("decompose", st);
   dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), kDecParts), B);
   uint2* part = (uint2*)((char*)ws + align256(sizeof(DecWs) * (size_t)B));
-  k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, info, code_masks, n_scales);
-  k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, w, info);
-  k_peaks<<<B, 512, 0, st>>>(w, ratio, info);
+  k_grey_minmax<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, info, grey);
+  if (grey)
+    k_hist<<<grid, 256, 0, st>>>(grey, HW, HW, 1, part, w, info);
+  else
+    k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, w, info);
+  k_modes<<<B, 512, 0, st>>>(w, info);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+// phase B: windows + region codes of the (grey or 3-plane) depth at the given resolutions
+int codes_impl(const float* src, long long sstride, int nch, int B, int H, int W, const float* ratio, int n_scales,
+               const int* out_h_host, const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
+               uint32_t* code_masks, hipStream_t st) {
+  TimerScope ts("decompose", st);
+  if (code_masks && n_scales > 0) {
+    const hipError_t e = hipMemsetAsync(code_masks, 0, sizeof(uint32_t) * n_scales, st);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (n_scales == 0) {
+    k_windows<<<ceil_div(B, 64), 64, 0, st>>>(info, ratio, B);
+    RGBD_CHECK_LAUNCH();
+    return RGBD_OK;
+  }
   // the Swin pyramid (each level half the previous, level 0 whole pixel blocks): one launch
-  const char* pe = getenv("RGBD_DECOMP_PYRAMID");  // A/B switch (read per call)
-  const bool pyramid = !(pe && atoi(pe) == 0) && n_scales == 3 && H % out_h_host[0] == 0 && W % out_w_host[0] == 0 &&
-                       out_h_host[0] % 4 == 0 && out_w_host[0] % 4 == 0 && out_h_host[1] * 2 == out_h_host[0] &&
+  const bool pyramid = n_scales == 3 && H % out_h_host[0] == 0 && W % out_w_host[0] == 0 && out_h_host[0] % 4 == 0 &&
+                       out_w_host[0] % 4 == 0 && out_h_host[1] * 2 == out_h_host[0] &&
                        out_w_host[1] * 2 == out_w_host[0] && out_h_host[2] * 2 == out_h_host[1] &&
                        out_w_host[2] * 2 == out_w_host[1];
   if (pyramid) {
     dim3 g3(ceil_div(out_w_host[0], 16), ceil_div(out_h_host[0], 16), B);
-    k_codes_pyramid<<<g3, 256, 0, st>>>(depth3, batch_stride, H, W, nch, out_h_host[0], out_w_host[0], info,
+    k_codes_pyramid<<<g3, 256, 0, st>>>(src, sstride, H, W, nch, out_h_host[0], out_w_host[0], info, ratio,
                                         codes_host[0], codes_host[1], codes_host[2], code_masks);
     RGBD_CHECK_LAUNCH();
     return RGBD_OK;
@@ -450,15 +489,16 @@ static int decompose(const float* depth3, long long batch_stride, int depth_chan
     const int oh = out_h_host[s], ow = out_w_host[s];
     dim3 g2(ceil_div((long long)oh * ow, 256), B);
     // a previous (finer) scale whose bins nest exactly into this one's: pool its codes
-    int src = -1;
+    int srcs = -1;
     for (int t = 0; t < s; ++t) {
       const int fh = out_h_host[t], fw = out_w_host[t];
-      if (fh >= oh && fw >= ow && fh % oh == 0 && fw % ow == 0 && H % fh == 0 && W % fw == 0) src = t;
+      if (fh >= oh && fw >= ow && fh % oh == 0 && fw % ow == 0 && H % fh == 0 && W % fw == 0) srcs = t;
     }
-    if (src >= 0)
-      k_codes_or_pool<<<g2, 256, 0, st>>>(codes_host[src], out_h_host[src], out_w_host[src], oh, ow, codes_host[s]);
-    else
-      k_codes_pool<<<g2, 256, 0, st>>>(depth3, batch_stride, H, W, nch, oh, ow, info, codes_host[s]);
+    if (srcs >= 0)
+      k_codes_or_pool<<<g2, 256, 0, st>>>(codes_host[srcs], out_h_host[srcs], out_w_host[srcs], oh, ow,
+                                          codes_host[s]);
+    else  // scale 0 always pools the pixels: its launch also publishes the windows
+      k_codes_pool<<<g2, 256, 0, st>>>(src, sstride, H, W, nch, oh, ow, info, ratio, s == 0, codes_host[s]);
     if (code_masks) {
       const long long nb = (long long)B * oh * ow;
       k_codes_presence<<<(unsigned)std::min<long long>(ceil_div(nb, 256 * 8), 256), 256, 0, st>>>(codes_host[s], nb,
@@ -467,6 +507,41 @@ static int decompose(const float* depth3, long long batch_stride, int depth_chan
   }
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
+}
+
+int check_scales(int B, int H, int W, int n_scales, const int* out_h_host, const int* out_w_host,
+                 uint8_t* const* codes_host) {
+  RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && n_scales >= 0 && n_scales <= 8, RGBD_E_ARG);
+  for (int s = 0; s < n_scales; ++s) {
+    RGBD_REQUIRE(out_h_host && out_w_host && codes_host && codes_host[s], RGBD_E_ARG);
+    RGBD_REQUIRE(out_h_host[s] > 0 && out_w_host[s] > 0 && out_h_host[s] <= H && out_w_host[s] <= W, RGBD_E_SHAPE);
+  }
+  return RGBD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t rgbd_edsam_decompose_workspace_size(int B) { return ws_head(B); }
+
+size_t rgbd_edsam_modes_workspace_size(int B, int H, int W) {
+  return ws_head(B) + align256(sizeof(float) * (size_t)(B > 0 ? B : 1) * (H > 0 ? H : 1) * (W > 0 ? W : 1));
+}
+
+static int decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
+                     const float* ratio, int n_scales, const int* out_h_host, const int* out_w_host,
+                     uint8_t* const* codes_host, rgbd_decomp_info* info, uint32_t* code_masks, void* ws,
+                     void* stream) {
+  RGBD_REQUIRE(depth3 && ratio && info && ws, RGBD_E_ARG);
+  RGBD_REQUIRE(depth_channels == 1 || depth_channels == 3, RGBD_E_SHAPE);
+  const int rc = check_scales(B, H, W, n_scales, out_h_host, out_w_host, codes_host);
+  if (rc != RGBD_OK) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const int ra = modes_impl(depth3, batch_stride, depth_channels, B, H, W, info, ws, nullptr, st);
+  if (ra != RGBD_OK) return ra;
+  return codes_impl(depth3, batch_stride, depth_channels, B, H, W, ratio, n_scales, out_h_host, out_w_host, codes_host,
+                    info, code_masks, st);
 }
 
 int rgbd_edsam_decompose(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
@@ -484,6 +559,27 @@ int rgbd_edsam_decompose_masks(const float* depth3, long long batch_stride, int 
   RGBD_REQUIRE(code_masks, RGBD_E_ARG);
   return decompose(depth3, batch_stride, depth_channels, B, H, W, ratio, n_scales, out_h_host, out_w_host, codes_host,
                    info, code_masks, ws, stream);
+}
+
+int rgbd_edsam_modes(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
+                     rgbd_decomp_info* info, void* ws, void* stream) {
+  RGBD_REQUIRE(depth3 && info && ws, RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(depth_channels == 1 || depth_channels == 3, RGBD_E_SHAPE);
+  TimerScope ts("decompose_modes", (hipStream_t)stream);
+  float* grey = (float*)((char*)ws + ws_head(B));
+  return modes_impl(depth3, batch_stride, depth_channels, B, H, W, info, ws, grey, (hipStream_t)stream);
+}
+
+int rgbd_edsam_codes(const void* ws, int B, int H, int W, const float* ratio, int n_scales, const int* out_h_host,
+                     const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
+                     uint32_t* code_masks, void* stream) {
+  RGBD_REQUIRE(ws && ratio && info, RGBD_E_ARG);
+  const int rc = check_scales(B, H, W, n_scales, out_h_host, out_w_host, codes_host);
+  if (rc != RGBD_OK) return rc;
+  const float* grey = (const float*)((const char*)ws + ws_head(B));
+  return codes_impl(grey, (long long)H * W, 1, B, H, W, ratio, n_scales, out_h_host, out_w_host, codes_host, info,
+                    code_masks, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -18,7 +18,7 @@ from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPix
                                                                   Mask2FormerPixelLevelModuleOutput)
 
 from . import deform_attn, mask_predictor, masked_attention, point_loss
-from .hot_path import hot_path
+from .hot_path import hot_path, prepare
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
 SUPPORTED_VERSIONS = ("0.4.0", "0.0.0")
@@ -71,11 +71,13 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
     def hot_path_features(self, pixel_values: Tensor, color_feature_map, ratios=None, status_sink=None):
         """custom_model.py:325-355 on the HIP kernels: returns the 4 backbone features.
         ``status_sink``: see hot_path.hot_path (None = raise the reference's ValueError at once)."""
+        # the ratio-free part (decomposition modes, bf16 colour layouts) beside the ratio predictor
+        prep = prepare(pixel_values, list(color_feature_map), self.compute_dtype)
         if ratios is None:
             ratios = self.ratio_predictor(pixel_values[:, 3:6])       # :336 (no grad, Q2)
         feats = hot_path(pixel_values, ratios, list(color_feature_map), [self.dsam0, self.dsam1, self.dsam2],
                          self.depth_gradient_injection, dtype=self.compute_dtype,
-                         check_status=status_sink is None, status_sink=status_sink)
+                         check_status=status_sink is None, status_sink=status_sink, prepared=prep)
         dt = color_feature_map[0].dtype
         return [f.to(dt) for f in feats]
 

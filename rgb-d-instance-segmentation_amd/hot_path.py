@@ -134,25 +134,60 @@ class _PackCache:
         return self.val
 
 
+class Prepared:
+    """What the hot path needs before the ratio exists (``prepare``): phase A of the depth
+    decomposition (grey plane, histogram, modes: ops.edsam_modes) and, in bf16, the NHWC copies
+    of the colour maps — launched on the side stream so they run beside the ratio predictor."""
+
+    def __init__(self, side, pixel_values, modes, colors, nhwc, dtype):
+        self.side, self.pixel_values, self.modes = side, pixel_values, modes
+        self.colors, self.nhwc, self.dtype = colors, nhwc, dtype
+
+    def join(self):
+        self.side.join()
+
+
+def prepare(pixel_values, colors, dtype=torch.float32):
+    """Launch the ratio-independent part of the hot path (call it before the ratio predictor,
+    pass the result to ``hot_path(..., prepared=)``).  bf16 on the GPU: on the side stream."""
+    pv = pixel_values.detach().float().contiguous()
+    cols = [c.detach().to(dtype).contiguous() for c in colors]
+    bf16 = dtype == torch.bfloat16
+    side = _Side(pv.device, bf16 and pv.is_cuda)
+    held = {}
+
+    def work():
+        held["modes"] = m = ops.edsam_modes(pv)
+        nhwc = [ops.nchw_to_nhwc(c) for c in cols] if bf16 else None
+        return [m.info, m.ws, nhwc]
+    _, _, nhwc = side.run(work, pv, *cols)
+    return Prepared(side, pv, held["modes"], cols, nhwc, dtype)
+
+
 class HotPathFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pixel_values, ratio, cfg, c0, c1, c2, c3, *params):
         dtype = cfg["dtype"]
-        colors = [c.detach().to(dtype).contiguous() for c in (c0, c1, c2, c3)]
+        prepared = cfg.get("prepared")
+        if prepared is None:
+            prepared = prepare(pixel_values, (c0, c1, c2, c3), dtype)
+        if prepared.dtype != dtype:
+            raise ValueError("hot_path: prepared for another compute dtype")
+        colors = prepared.colors
         dsam_p = [params[9 * k:9 * k + 9] for k in range(3)]
         dggm_p = params[27:35]
         sizes = [tuple(c.shape[2:]) for c in colors[:3]]
         bf16 = dtype == torch.bfloat16
-        # bf16 on the GPU: the colour-map layout changes run beside the decomposition, the dsam1 /
-        # dsam2 packing beside dsam0 and the dW plans beside dsam1 / dsam2 (side stream; joined
-        # before their consumers)
+        # bf16 on the GPU: the decomposition's modes and the colour-map layout changes ran beside
+        # the ratio predictor (prepare); the dsam1 / dsam2 packing runs beside dsam0 and the dW
+        # plans beside dsam1 / dsam2 (side stream; joined before their consumers)
         side = _Side(pixel_values.device, bf16 and pixel_values.is_cuda and cfg.get("overlap", True))
-        if bf16:
-            nhwc = side.run(lambda: [ops.nchw_to_nhwc(c) for c in colors], *colors)
+        prepared.join()
+        nhwc = prepared.nhwc
         if bf16:  # the code-presence masks the bf16 filter packing needs come out of the decomposition
-            codes, info, masks = ops.edsam_decompose(pixel_values, ratio.detach(), sizes, code_masks=True)
+            codes, info, masks = ops.edsam_codes(prepared.modes, ratio.detach(), sizes, code_masks=True)
         else:
-            codes, info = ops.edsam_decompose(pixel_values, ratio.detach(), sizes)
+            codes, info = ops.edsam_codes(prepared.modes, ratio.detach(), sizes)
             masks = None
         if cfg.get("check_status"):
             ops.raise_on_status(info)
@@ -176,7 +211,6 @@ class HotPathFunction(torch.autograd.Function):
         cp1 = [colors[0]]
         if bf16:
             packs = [pack(0)]
-            side.join()  # the NHWC colour maps
             packs += side.run(lambda: [pack(1), pack(2)], masks)
             x_nhwc = [nhwc[0]]
             res_nhwc = nhwc[1:]
@@ -284,7 +318,7 @@ class HotPathFunction(torch.autograd.Function):
 
 
 def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch.float32, check_status=False,
-             grad_hook=None, status_sink=None):
+             grad_hook=None, status_sink=None, prepared=None):
     """Run the fused hot path.  ``dsam_modules``: the three DSAModule instances;
     ``dggm_module``: the DepthGradientInjectionResidual instance.  ``check_status`` raises the
     reference's ValueError for a degenerate depth histogram right away (synchronising);
@@ -292,7 +326,9 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
     ``grad_hook(i, grads)``, if
     given, is called during backward as each parameter group's gradients are enqueued, in the
     order of ``distributed.hot_path_grad_groups`` (dsam2, dsam1, dsam0 + DGGM) — the data-parallel
-    reducer uses it to overlap the gradient all-reduce with the rest of the backward."""
+    reducer uses it to overlap the gradient all-reduce with the rest of the backward.
+    ``prepared``: ``prepare(pixel_values, colors, dtype)``, launched before the ratio predictor
+    (the same pixel_values / colours), so the ratio-free work overlaps it; None = inline."""
     params = []
     for m in dsam_modules:
         for i in range(4):
@@ -302,6 +338,6 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
         conv = dggm_module.depth_enhancement_layers[i][0]
         params += [conv.weight, conv.bias]
     cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook, "status_sink": status_sink,
-           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": True}
-    pv = pixel_values.detach().float().contiguous()
+           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": True, "prepared": prepared}
+    pv = prepared.pixel_values if prepared is not None else pixel_values.detach().float().contiguous()
     return list(HotPathFunction.apply(pv, ratio, cfg, *colors, *params))

@@ -22,11 +22,11 @@ mask, dropout in training, head_dim != 32, batch_first) also go through torch's 
 ``install(model)`` swaps the class of the decoder layers' ``cross_attn`` modules in place (same
 parameters, same state_dict keys).
 
-A query row whose every key is masked: torch's softmax gives NaN for the row and its backward
-spreads NaN into dq, dk and dv of that batch-head; the kernels return the NaN row in the forward
-but no gradient from it (its log-sum-exp is +inf, so its probabilities are 0 in the backward).
-HF's decoder un-masks such rows before the call (modeling_mask2former.py:2054-2055), so the model
-never reaches this case.
+A query row whose every key is masked: torch's softmax gives NaN for the row, and so do the
+kernels (log-sum-exp +inf).  In the backward the row's delta = rowsum(dO * O) is NaN, so NaN
+reaches the key gradient of that batch-head (and through it the projections' gradients), as
+NaN reaches torch's (which also spreads it into dq and dv).  HF's decoder un-masks such rows
+before the call (modeling_mask2former.py:2054-2055), so the model never reaches this case.
 """
 import math
 

@@ -83,6 +83,33 @@ def assemble_pixel_values(depth_u8: torch.Tensor, rgb_u8: torch.Tensor = None, o
 
 
 # ------------------------------------------------------------------ K3 decomposition
+def _depth_planes(pixel_values):
+    _need_cuda(pixel_values)
+    if pixel_values.dtype != torch.float32:
+        raise TypeError("the decomposition consumes float32 depth (SURVEY §7 (i))")
+    B, C, H, W = pixel_values.shape
+    nch = 1 if C == 1 else 3
+    depth3 = pixel_values if C in (1, 3) else pixel_values[:, 3:6]
+    return depth3, nch, B, H, W
+
+
+def _ratio_vec(ratio, B):
+    _need_cuda(ratio)
+    r = ratio.reshape(-1).to(torch.float32).contiguous()
+    if r.numel() != B:
+        raise ValueError("one ratio per image expected")
+    return r
+
+
+def _scale_args(sizes, B, dev):
+    n = len(sizes)
+    codes = [torch.empty((B, h, w), dtype=torch.uint8, device=dev) for (h, w) in sizes]
+    oh = (ctypes.c_int * max(n, 1))(*[s[0] for s in sizes])
+    ow = (ctypes.c_int * max(n, 1))(*[s[1] for s in sizes])
+    cp = (ctypes.c_void_p * max(n, 1))(*[c.data_ptr() for c in codes])
+    return n, codes, oh, ow, cp
+
+
 def edsam_decompose(pixel_values: torch.Tensor, ratio: torch.Tensor, sizes, code_masks=False):
     """Depth decomposition of every image, once for all DSAMs.
 
@@ -90,23 +117,14 @@ def edsam_decompose(pixel_values: torch.Tensor, ratio: torch.Tensor, sizes, code
     [B,3,H,W] depth tensor, or a [B,1,H,W] already-grey map; ratio: float32 [B] or [B,1] on device; sizes: list of (h, w).
     Returns (codes list of uint8 [B,h,w], info uint8 [B, 2116] device tensor); with
     ``code_masks`` also the int32 device tensor [len(sizes)] of dsam_code_masks(codes), made by
-    the decomposition itself (rgbd_edsam_decompose_masks)."""
-    _need_cuda(pixel_values, ratio)
-    if pixel_values.dtype != torch.float32:
-        raise TypeError("the decomposition consumes float32 depth (SURVEY §7 (i))")
-    B, C, H, W = pixel_values.shape
-    nch = 1 if C == 1 else 3
-    depth3 = pixel_values if C in (1, 3) else pixel_values[:, 3:6]
-    r = ratio.reshape(-1).to(torch.float32).contiguous()
-    if r.numel() != B:
-        raise ValueError("one ratio per image expected")
+    the decomposition itself (rgbd_edsam_decompose_masks).  Both phases on the current stream;
+    ``edsam_modes`` + ``edsam_codes`` split them (the hot path runs the first beside the ratio
+    predictor)."""
+    depth3, nch, B, H, W = _depth_planes(pixel_values)
+    r = _ratio_vec(ratio, B)
     dev = pixel_values.device
-    codes = [torch.empty((B, h, w), dtype=torch.uint8, device=dev) for (h, w) in sizes]
+    n, codes, oh, ow, cp = _scale_args(sizes, B, dev)
     info = torch.empty((B, DECOMP_INFO_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-    n = len(sizes)
-    oh = (ctypes.c_int * max(n, 1))(*[s[0] for s in sizes])
-    ow = (ctypes.c_int * max(n, 1))(*[s[1] for s in sizes])
-    cp = (ctypes.c_void_p * max(n, 1))(*[c.data_ptr() for c in codes])
     L = _lib.lib()
     ws = _workspace(dev, L.rgbd_edsam_decompose_workspace_size(B), "decompose")
     if code_masks:
@@ -118,6 +136,43 @@ def edsam_decompose(pixel_values: torch.Tensor, ratio: torch.Tensor, sizes, code
     check(L.rgbd_edsam_decompose(ctypes.c_void_p(depth3.data_ptr()), depth3.stride(0), nch, B, H, W, _p(r), n,
                                  oh, ow, cp, _p(info), _p(ws), _stream(dev)), "rgbd_edsam_decompose")
     return codes, info
+
+
+class EdsamModes:
+    """Phase A of the decomposition (rgbd_edsam_modes): the grey plane, histogram and modes of
+    every image — everything that does not depend on the ratio.  ``info`` holds the per-image
+    records (status, histogram, centres); ``ws`` the grey plane phase B reads."""
+
+    def __init__(self, info, ws, B, H, W):
+        self.info, self.ws, self.B, self.H, self.W = info, ws, B, H, W
+
+
+def edsam_modes(pixel_values: torch.Tensor) -> EdsamModes:
+    """Launch phase A on the current stream (the hot path puts it on its side stream, beside
+    the ratio predictor).  The workspace is per (device, stream): one EdsamModes per stream
+    may be pending at a time."""
+    depth3, nch, B, H, W = _depth_planes(pixel_values)
+    dev = pixel_values.device
+    info = torch.empty((B, DECOMP_INFO_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    L = _lib.lib()
+    ws = _workspace(dev, L.rgbd_edsam_modes_workspace_size(B, H, W), "edsam_modes")
+    check(L.rgbd_edsam_modes(ctypes.c_void_p(depth3.data_ptr()), depth3.stride(0), nch, B, H, W, _p(info), _p(ws),
+                             _stream(dev)), "rgbd_edsam_modes")
+    return EdsamModes(info, ws, B, H, W)
+
+
+def edsam_codes(modes: EdsamModes, ratio: torch.Tensor, sizes, code_masks=False):
+    """Phase B (rgbd_edsam_codes) on the current stream, after ``modes`` (stream-ordered by
+    the caller): the windows at ``ratio`` and the region codes at ``sizes`` from the grey
+    plane.  Returns what edsam_decompose returns."""
+    B, H, W = modes.B, modes.H, modes.W
+    r = _ratio_vec(ratio, B)
+    dev = modes.info.device
+    n, codes, oh, ow, cp = _scale_args(sizes, B, dev)
+    masks = torch.empty((max(n, 1),), dtype=torch.int32, device=dev) if code_masks else None
+    check(_lib.lib().rgbd_edsam_codes(_p(modes.ws), B, H, W, _p(r), n, oh, ow, cp, _p(modes.info), _p(masks),
+                                      _stream(dev)), "rgbd_edsam_codes")
+    return (codes, modes.info, masks[:n]) if code_masks else (codes, modes.info)
 
 
 def decode_info(info: torch.Tensor) -> np.ndarray:

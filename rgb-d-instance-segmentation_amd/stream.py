@@ -16,7 +16,7 @@ outside the hot path).
 import torch
 
 from . import ops
-from .hot_path import hot_path
+from .hot_path import hot_path, prepare
 
 
 class StreamingHotPath:
@@ -40,8 +40,9 @@ class StreamingHotPath:
 
     def _run(self):
         pv = ops.assemble_pixel_values(self.depth_u8, self.rgb_u8)
+        prep = prepare(pv, self.colors, self.dtype)  # decomposition modes beside the ratio predictor
         ratio = self.rp(pv[:, 3:6])
-        return hot_path(pv, ratio, self.colors, self.dsams, self.dg, dtype=self.dtype), ratio
+        return hot_path(pv, ratio, self.colors, self.dsams, self.dg, dtype=self.dtype, prepared=prep), ratio
 
     def capture(self):
         """Warm up (packs weights, sizes workspaces) on a side stream, then capture the path."""

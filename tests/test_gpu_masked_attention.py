@@ -97,14 +97,17 @@ def test_fully_masked_row_is_nan_like_torch():
     assert bool(out_r[2, 0].isnan().all()) and bool(out_h[2, 0].isnan().all())
     ok = ~out_r.isnan()
     assert float((out_h[ok] - out_r[ok]).abs().max()) <= 1e-5 * (1 + float(out_r[ok].abs().max()))
-    # backward (documented divergence, masked_attention.py docstring): torch spreads NaN into the
-    # whole batch-head; the kernels give that row no gradient and keep every other one finite
+    # backward (masked_attention.py docstring): the row's delta = rowsum(dO * O) is NaN, so NaN
+    # reaches the gradients as in torch's backward (no silently finite gradient)
+    qr = [t.clone().requires_grad_() for t in (query, key, value)]
     qh = [t.clone().requires_grad_() for t in (query, key, value)]
+    out_r, _ = ref(*qr, attn_mask=mask)
     out_h, _ = hip(*qh, attn_mask=mask)
     g = torch.ones_like(out_h)
     g[2] = 0.0  # the NaN query row carries no upstream gradient
+    torch.nan_to_num(out_r, nan=0.0).backward(g)
     torch.nan_to_num(out_h, nan=0.0).backward(g)
-    assert all(bool(t.grad.isfinite().all()) for t in qh)
+    assert not bool(qr[1].grad.isfinite().all()) and not bool(qh[1].grad.isfinite().all())
 
 
 @gpu

@@ -55,15 +55,25 @@ def test_assemble_degenerate_depth():
 CASES = gi.decomposition_cases()
 
 
+def _decompose(split, pv, ratio, sizes, code_masks=False):
+    """The single-call decomposition, or its two phases (rgbd_edsam_modes, then
+    rgbd_edsam_codes on the grey plane the first one kept) as the hot path runs them."""
+    ops = _ops()
+    if not split:
+        return ops.edsam_decompose(pv, ratio, sizes, code_masks=code_masks)
+    return ops.edsam_codes(ops.edsam_modes(pv), ratio, sizes, code_masks=code_masks)
+
+
+@pytest.mark.parametrize("split", [False, True], ids=["one_call", "two_phases"])
 @pytest.mark.parametrize("i", range(len(CASES)), ids=[c[0] for c in CASES])
-def test_decomposition_matches_reference_fixture(golden, i):
+def test_decomposition_matches_reference_fixture(golden, i, split):
     ops = _ops()
     g1 = golden("g1_decompose")
     name, d3, r = CASES[i]
     H, W = d3.shape[1:]
     sizes = gi.pool_sizes(H, W)
-    codes, info = ops.edsam_decompose(torch.from_numpy(d3)[None].to(DEV),
-                                      torch.tensor([r], dtype=torch.float32, device=DEV), sizes)
+    codes, info = _decompose(split, torch.from_numpy(d3)[None].to(DEV),
+                             torch.tensor([r], dtype=torch.float32, device=DEV), sizes)
     rec = ops.decode_info(info)[0]
     if str(g1["error"][i]):
         assert rec["status"] != 0
@@ -83,14 +93,22 @@ def test_decomposition_matches_reference_fixture(golden, i):
         np.testing.assert_array_equal(codes[s][0].cpu().numpy(), g1[f"{i}_pooled{s}"])
 
 
-def test_decomposition_batch_full_size():
+@pytest.mark.parametrize("split", [False, True], ids=["one_call", "two_phases"])
+def test_decomposition_batch_full_size(split):
     """Batch of 8 NYUv2-shaped (480x640) scenes, ratios in [0.01, 0.5]: every image matches
-    the oracle bit-for-bit when decomposed together in one launch sequence."""
+    the oracle bit-for-bit when decomposed together in one launch sequence (or in the hot
+    path's two phases); the code-presence masks equal the codes' own."""
     ops = _ops()
     planes, _, _ = synthetic.make_batch(2, 8, 480, 640)
     ratios = np.linspace(0.01, 0.5, 8).astype(np.float32)
     sizes = gi.pool_sizes(480, 640)
-    codes, info = ops.edsam_decompose(torch.from_numpy(planes).to(DEV), torch.from_numpy(ratios).to(DEV), sizes)
+    codes, info, masks = _decompose(split, torch.from_numpy(planes).to(DEV), torch.from_numpy(ratios).to(DEV), sizes,
+                                    code_masks=True)
+    for s in range(3):
+        want = 0
+        for v in np.unique(codes[s].cpu().numpy()):
+            want |= 1 << int(v)
+        assert int(masks[s]) == want
     rec = ops.decode_info(info)
     for b in range(8):
         dec = edsam.decompose(planes[b, 3:6], float(ratios[b]))

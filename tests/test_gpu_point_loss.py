@@ -104,7 +104,7 @@ def test_loss_all_images_empty_matches_reference():
     from transformers.models.mask2former.modeling_mask2former import Mask2FormerLoss
     cfg = Mask2FormerConfig(num_labels=48)
     wd = {"loss_cross_entropy": 2.0, "loss_mask": 5.0, "loss_dice": 5.0}
-    ref_loss, hip_loss = Mask2FormerLoss(cfg, weight_dict=wd), Mask2FormerLoss(cfg, weight_dict=wd)
+    ref_loss, hip_loss = Mask2FormerLoss(cfg, weight_dict=wd).to(DEV), Mask2FormerLoss(cfg, weight_dict=wd).to(DEV)
     holder = torch.nn.Module()
     holder.criterion = hip_loss
     assert point_loss.install(holder) == 1

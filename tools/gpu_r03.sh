@@ -15,7 +15,7 @@ case "$stage" in
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
     rc=$?; tail -2 "$O/smoke.log"; exit $rc ;;
   tests)
-    timeout -k 10 1000 python -u -m pytest -m gpu -q -rf --timeout 400 --timeout-method thread -p no:cacheprovider "${@:-tests}" > "$O/tests.log" 2>&1
+    timeout -k 10 1000 python -u -m pytest -m gpu -q -rfP --timeout 400 --timeout-method thread -p no:cacheprovider "${@:-tests}" > "$O/tests.log" 2>&1
     rc=$?; tail -25 "$O/tests.log"; exit $rc ;;
   bench)
     timeout -k 10 600 python bench.py "$@" > "$O/bench.json" 2> "$O/bench.err"
