@@ -537,6 +537,9 @@ def main():
     L.rgbd_timing_enable(0)
     use_graph = bool(args.graph) and world == 1
     dt = timed(make_step(ctx, world, graph=True), args.steps, args.warmup, world) if use_graph else dt_eager
+    # N > 1 runs eagerly (the overlapped RCCL reducer is not captured): the same eager step with
+    # no collective on every rank at once gives the line's own scaling reference
+    dt_local = timed(make_step(ctx, 1), args.steps, args.warmup, world) if world > 1 else None
     B = args.batch
     step_ms = dt / args.steps * 1e3
     raw, per, fracs = kernel_fractions(timings, ctx, B, args.height, args.width, step_ms, world)
@@ -574,8 +577,16 @@ def main():
                         "backend": (dist.get_backend() if world > 1 else None),
                         "collectives_per_step": ("3 async all-reduce (grad buckets dsam2, dsam1, dsam0+DGGM) + "
                                                  "2 broadcasts (ratio-predictor BN buffers)") if world > 1 else None},
+        "optimizer": ("AdamW (lr 1e-5, HF Trainer defaults) on the hot-path parameters, stepped inside the backward; "
+                      "no gradient-norm clip: the reference Trainer's max_grad_norm=1.0 clips the norm of the whole "
+                      "model's gradients (37.3 M parameters, most of them outside this path)"),
         "graph": use_graph,
         "eager_img_s": round(B * world * args.steps / dt_eager, 2),
+        "scaling_baseline_img_s": (None if dt_local is None else round(B * world * args.steps / dt_local, 2)),
+        "scaling_baseline_note": ("N > 1: the step is eager (collectives not captured); scaling_baseline_img_s = "
+                                  "the same eager step with no all-reduce / broadcast on every rank at once, so "
+                                  "value / scaling_baseline_img_s is the cost of the data-parallel exchange; the "
+                                  "N=1 line replays a HIP graph (its eager_img_s is the eager N=1 rate)"),
         "inference_img_s": inf,
         "kernel_ms": per,
         "roofline": {"bound": "mfma", "kernel": "k_rp_conv3x3 (3x3 128->256, custom_model.py:1413)",

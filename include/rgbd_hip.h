@@ -106,14 +106,15 @@ int rgbd_edsam_decompose_masks(const float* depth3, long long batch_stride, int 
 /* The same decomposition in two phases, for callers that overlap the ratio-free part with the
  * ratio predictor (the hot path: phase A on a side stream beside K4, phase B after it).
  * Phase A, rgbd_edsam_modes: grey plane (kept in ws, 4 B/px), nanmin/nanmax, histogram, modes
- * and centres into info (status, hist, n_modes, n_masks, peak_bin, center, edges; lo/hi zero).
+ * and centres into info (status, hist, n_modes, n_masks, peak_bin, center, edges; lo/hi zero);
+ * code_masks (may be NULL; device uint32 [n_masks]) is zeroed for phase B.
  * Phase B, rgbd_edsam_codes: the windows at ratio (info lo/hi) and the region codes at each
  * resolution from phase A's grey plane; code_masks as in rgbd_edsam_decompose_masks (may be
- * NULL).  ws: rgbd_edsam_modes_workspace_size(B, H, W) bytes, phase B on the workspace phase A
+ * NULL; when given, the array phase A zeroed, n_masks >= n_scales).  ws: rgbd_edsam_modes_workspace_size(B, H, W) bytes, phase B on the workspace phase A
  * filled, stream-ordered after it.  Results identical to rgbd_edsam_decompose(_masks). */
 size_t rgbd_edsam_modes_workspace_size(int B, int H, int W);
 int rgbd_edsam_modes(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
-                     rgbd_decomp_info* info, void* ws, void* stream);
+                     rgbd_decomp_info* info, uint32_t* code_masks, int n_masks, void* ws, void* stream);
 int rgbd_edsam_codes(const void* ws, int B, int H, int W, const float* ratio, int n_scales, const int* out_h_host,
                      const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
                      uint32_t* code_masks, void* stream);

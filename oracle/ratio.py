@@ -21,8 +21,9 @@ def _cbr(x, p, pre, pad, training):
     return F.relu(_bn(y, p, pre + ".1", training))
 
 
-def ratio_forward(depth: torch.Tensor, p: dict, training: bool = False) -> torch.Tensor:
-    """depth [B,3,H,W] f32 -> ratio [B,1] f32 in [0.01, 0.5] (custom_model.py:1444-1487)."""
+def ratio_forward(depth: torch.Tensor, p: dict, training: bool = False, return_logit: bool = False) -> torch.Tensor:
+    """depth [B,3,H,W] f32 -> ratio [B,1] f32 in [0.01, 0.5] (custom_model.py:1444-1487);
+    ``return_logit``: the pre-sigmoid output of fc_layers.8 instead (test instrumentation)."""
     s1 = _cbr(depth, p, "scale1_conv", 1, training)                       # :1458
     s2 = _cbr(depth, p, "scale2_conv", 2, training)                       # :1459
     s3 = _cbr(depth, p, "scale3_conv", 3, training)                       # :1460
@@ -41,6 +42,8 @@ def ratio_forward(depth: torch.Tensor, p: dict, training: bool = False) -> torch
     h = F.relu(F.linear(h, p["fc_layers.3.weight"], p["fc_layers.3.bias"]))
     h = F.relu(F.linear(h, p["fc_layers.6.weight"], p["fc_layers.6.bias"]))
     raw = F.linear(h, p["fc_layers.8.weight"], p["fc_layers.8.bias"])     # :1482
+    if return_logit:
+        return raw
     return 0.01 + (0.5 - 0.01) * torch.sigmoid(raw)                       # :1485
 
 

@@ -43,7 +43,7 @@ SIGNATURES = {
     "rgbd_edsam_decompose": (_I, [_P, _LL, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_edsam_decompose_masks": (_I, [_P, _LL, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "rgbd_edsam_modes_workspace_size": (_SZ, [_I, _I, _I]),
-    "rgbd_edsam_modes": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _P]),
+    "rgbd_edsam_modes": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _I, _P, _P]),
     "rgbd_edsam_codes": (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_dggm_fuse_fwd": (_I, [_I, _P, _P, _P, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rgbd_dggm_fuse_bwd_workspace_size": (_SZ, [_I, _I, _I, _I]),

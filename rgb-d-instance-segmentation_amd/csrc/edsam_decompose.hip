@@ -169,7 +169,8 @@ __device__ __forceinline__ long long wave_max_i64(long long v) {
   return v;
 }
 
-__global__ __launch_bounds__(512) void k_modes(const DecWs* ws, rgbd_decomp_info* info) {
+__global__ __launch_bounds__(512) void k_modes(const DecWs* ws, rgbd_decomp_info* info, uint32_t* __restrict__ cmask,
+                                               int ncmask) {
   __shared__ int x[RGBD_NBINS];
   __shared__ int peaks[RGBD_NBINS];
   __shared__ int is_kept[RGBD_NBINS];
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(512) void k_modes(const DecWs* ws, rgbd_decomp_info
   __shared__ int sel[RGBD_MAX_MODES];
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (b == 0 && cmask && t < ncmask) cmask[t] = 0u;  // phase B ORs the code-presence masks into it
   rgbd_decomp_info* out = info + b;
   Range r = make_range(ws[b]);
   x[t] = out->hist[t];
@@ -356,6 +358,7 @@ __global__ __launch_bounds__(256) void k_codes_pool(const float* __restrict__ de
 // multiples of 4 cells and level 0 has exactly 4x the level-2 cells), computes each level-0 code
 // from its pixels, OR-pools 2 x 2 cells twice through LDS (exactly adaptive_max_pool2d of the
 // full-resolution masks, bins nesting), and ORs 1 << code into the per-level presence masks.
+template <bool kF4>
 __global__ __launch_bounds__(256) void k_codes_pyramid(const float* __restrict__ depth3, long long bstride, int H, int W,
                                                        int nch, int oh0, int ow0, rgbd_decomp_info* info,
                                                        const float* __restrict__ ratio,
@@ -376,9 +379,20 @@ __global__ __launch_bounds__(256) void k_codes_pyramid(const float* __restrict__
   const float* d = depth3 + b * bstride;
   uint32_t c = 0u;
   const bool in0 = i < oh0 && j < ow0;
-  if (in0 && n > 0)
+  if (kF4) {  // the grey plane, 4 x 4-pixel cells (the Swin stride): one 16-byte load per cell row
+    if (in0 && n > 0) {
+      float4 v[4];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) v[y] = *reinterpret_cast<const float4*>(d + (long long)(4 * i + y) * W + 4 * j);
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+        c |= pixel_code(v[y].x, n, lo, hi) | pixel_code(v[y].y, n, lo, hi) | pixel_code(v[y].z, n, lo, hi) |
+             pixel_code(v[y].w, n, lo, hi);
+    }
+  } else if (in0 && n > 0) {
     for (int y = i * fy; y < (i + 1) * fy; ++y)
       for (int x = j * fx; x < (j + 1) * fx; ++x) c |= pixel_code(grey_at(d, HW, (long long)y * W + x, nch), n, lo, hi);
+  }
   s0[ty][tx] = (uint8_t)c;
   __syncthreads();
   if (in0) {
@@ -444,7 +458,7 @@ size_t ws_head(int B) {
 
 // phase A: grey (into ``grey`` when given), min/max, histogram, modes
 int modes_impl(const float* depth3, long long batch_stride, int nch, int B, int H, int W, rgbd_decomp_info* info,
-               void* ws, float* grey, hipStream_t st) {
+               void* ws, float* grey, uint32_t* code_masks, int n_scales, hipStream_t st) {
   DecWs* w = (DecWs*)ws;
   const long long HW = (long long)H * W;
   dim3 grid((unsigned)std::min<long long>(ceil_div(HW, 256), kDecParts), B);
@@ -454,7 +468,7 @@ int modes_impl(const float* depth3, long long batch_stride, int nch, int B, int 
     k_hist<<<grid, 256, 0, st>>>(grey, HW, HW, 1, part, w, info);
   else
     k_hist<<<grid, 256, 0, st>>>(depth3, batch_stride, HW, nch, part, w, info);
-  k_modes<<<B, 512, 0, st>>>(w, info);
+  k_modes<<<B, 512, 0, st>>>(w, info, code_masks, n_scales);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -464,10 +478,6 @@ int codes_impl(const float* src, long long sstride, int nch, int B, int H, int W
                const int* out_h_host, const int* out_w_host, uint8_t* const* codes_host, rgbd_decomp_info* info,
                uint32_t* code_masks, hipStream_t st) {
   TimerScope ts("decompose", st);
-  if (code_masks && n_scales > 0) {
-    const hipError_t e = hipMemsetAsync(code_masks, 0, sizeof(uint32_t) * n_scales, st);
-    if (e != hipSuccess) return (int)e;
-  }
   if (n_scales == 0) {
     k_windows<<<ceil_div(B, 64), 64, 0, st>>>(info, ratio, B);
     RGBD_CHECK_LAUNCH();
@@ -480,8 +490,15 @@ int codes_impl(const float* src, long long sstride, int nch, int B, int H, int W
                        out_w_host[2] * 2 == out_w_host[1];
   if (pyramid) {
     dim3 g3(ceil_div(out_w_host[0], 16), ceil_div(out_h_host[0], 16), B);
-    k_codes_pyramid<<<g3, 256, 0, st>>>(src, sstride, H, W, nch, out_h_host[0], out_w_host[0], info, ratio,
-                                        codes_host[0], codes_host[1], codes_host[2], code_masks);
+    // 16-byte loads: one grey plane (nch 1), 4 x 4 cells, rows 16-byte aligned
+    const bool f4 = nch == 1 && H == 4 * out_h_host[0] && W == 4 * out_w_host[0] && W % 4 == 0 && sstride % 4 == 0 &&
+                    ((uintptr_t)src & 15) == 0;
+    if (f4)
+      k_codes_pyramid<true><<<g3, 256, 0, st>>>(src, sstride, H, W, nch, out_h_host[0], out_w_host[0], info, ratio,
+                                                codes_host[0], codes_host[1], codes_host[2], code_masks);
+    else
+      k_codes_pyramid<false><<<g3, 256, 0, st>>>(src, sstride, H, W, nch, out_h_host[0], out_w_host[0], info, ratio,
+                                                 codes_host[0], codes_host[1], codes_host[2], code_masks);
     RGBD_CHECK_LAUNCH();
     return RGBD_OK;
   }
@@ -538,7 +555,7 @@ static int decompose(const float* depth3, long long batch_stride, int depth_chan
   const int rc = check_scales(B, H, W, n_scales, out_h_host, out_w_host, codes_host);
   if (rc != RGBD_OK) return rc;
   hipStream_t st = (hipStream_t)stream;
-  const int ra = modes_impl(depth3, batch_stride, depth_channels, B, H, W, info, ws, nullptr, st);
+  const int ra = modes_impl(depth3, batch_stride, depth_channels, B, H, W, info, ws, nullptr, code_masks, n_scales, st);
   if (ra != RGBD_OK) return ra;
   return codes_impl(depth3, batch_stride, depth_channels, B, H, W, ratio, n_scales, out_h_host, out_w_host, codes_host,
                     info, code_masks, st);
@@ -562,13 +579,14 @@ int rgbd_edsam_decompose_masks(const float* depth3, long long batch_stride, int 
 }
 
 int rgbd_edsam_modes(const float* depth3, long long batch_stride, int depth_channels, int B, int H, int W,
-                     rgbd_decomp_info* info, void* ws, void* stream) {
+                     rgbd_decomp_info* info, uint32_t* code_masks, int n_masks, void* ws, void* stream) {
   RGBD_REQUIRE(depth3 && info && ws, RGBD_E_ARG);
-  RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(B > 0 && H > 0 && W > 0 && n_masks >= 0 && n_masks <= 8, RGBD_E_ARG);
   RGBD_REQUIRE(depth_channels == 1 || depth_channels == 3, RGBD_E_SHAPE);
   TimerScope ts("decompose_modes", (hipStream_t)stream);
   float* grey = (float*)((char*)ws + ws_head(B));
-  return modes_impl(depth3, batch_stride, depth_channels, B, H, W, info, ws, grey, (hipStream_t)stream);
+  return modes_impl(depth3, batch_stride, depth_channels, B, H, W, info, ws, grey, code_masks, n_masks,
+                    (hipStream_t)stream);
 }
 
 int rgbd_edsam_codes(const void* ws, int B, int H, int W, const float* ratio, int n_scales, const int* out_h_host,

@@ -159,8 +159,8 @@ def prepare(pixel_values, colors, dtype=torch.float32):
     def work():
         held["modes"] = m = ops.edsam_modes(pv)
         nhwc = [ops.nchw_to_nhwc(c) for c in cols] if bf16 else None
-        return [m.info, m.ws, nhwc]
-    _, _, nhwc = side.run(work, pv, *cols)
+        return [m.info, m.ws, m.masks, nhwc]
+    _, _, _, nhwc = side.run(work, pv, *cols)
     return Prepared(side, pv, held["modes"], cols, nhwc, dtype)
 
 

@@ -143,22 +143,24 @@ class EdsamModes:
     every image — everything that does not depend on the ratio.  ``info`` holds the per-image
     records (status, histogram, centres); ``ws`` the grey plane phase B reads."""
 
-    def __init__(self, info, ws, B, H, W):
-        self.info, self.ws, self.B, self.H, self.W = info, ws, B, H, W
+    def __init__(self, info, ws, masks, B, H, W):
+        self.info, self.ws, self.masks, self.B, self.H, self.W = info, ws, masks, B, H, W
 
 
-def edsam_modes(pixel_values: torch.Tensor) -> EdsamModes:
+def edsam_modes(pixel_values: torch.Tensor, n_masks: int = 3) -> EdsamModes:
     """Launch phase A on the current stream (the hot path puts it on its side stream, beside
-    the ratio predictor).  The workspace is per (device, stream): one EdsamModes per stream
-    may be pending at a time."""
+    the ratio predictor); ``n_masks``: code-presence masks (zeroed here) for up to that many
+    scales of the codes call.  The workspace is per (device, stream): one EdsamModes per
+    stream may be pending at a time."""
     depth3, nch, B, H, W = _depth_planes(pixel_values)
     dev = pixel_values.device
     info = torch.empty((B, DECOMP_INFO_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    masks = torch.empty((max(n_masks, 1),), dtype=torch.int32, device=dev)
     L = _lib.lib()
     ws = _workspace(dev, L.rgbd_edsam_modes_workspace_size(B, H, W), "edsam_modes")
-    check(L.rgbd_edsam_modes(ctypes.c_void_p(depth3.data_ptr()), depth3.stride(0), nch, B, H, W, _p(info), _p(ws),
-                             _stream(dev)), "rgbd_edsam_modes")
-    return EdsamModes(info, ws, B, H, W)
+    check(L.rgbd_edsam_modes(ctypes.c_void_p(depth3.data_ptr()), depth3.stride(0), nch, B, H, W, _p(info), _p(masks),
+                             n_masks, _p(ws), _stream(dev)), "rgbd_edsam_modes")
+    return EdsamModes(info, ws, masks, B, H, W)
 
 
 def edsam_codes(modes: EdsamModes, ratio: torch.Tensor, sizes, code_masks=False):
@@ -169,7 +171,11 @@ def edsam_codes(modes: EdsamModes, ratio: torch.Tensor, sizes, code_masks=False)
     r = _ratio_vec(ratio, B)
     dev = modes.info.device
     n, codes, oh, ow, cp = _scale_args(sizes, B, dev)
-    masks = torch.empty((max(n, 1),), dtype=torch.int32, device=dev) if code_masks else None
+    masks = None
+    if code_masks:
+        if modes.masks.numel() < n:
+            raise ValueError(f"edsam_codes: the modes call zeroed {modes.masks.numel()} code masks, {n} needed")
+        masks = modes.masks
     check(_lib.lib().rgbd_edsam_codes(_p(modes.ws), B, H, W, _p(r), n, oh, ow, cp, _p(modes.info), _p(masks),
                                       _stream(dev)), "rgbd_edsam_codes")
     return (codes, modes.info, masks[:n]) if code_masks else (codes, modes.info)

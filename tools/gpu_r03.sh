@@ -24,5 +24,12 @@ case "$stage" in
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --cpu-baseline 0 --inference 0 --c5-stream 0 --parity 0 "$@" > "$O/prof.log" 2>&1
     rc=$?; tail -3 "$O/prof.log"; exit $rc ;;
+  fullprof)  # the whole drop-in model's training step (tools/bench_full_model.py) under the kernel trace
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/fullprof" -o run --output-format csv -- python3 "$R/tools/bench_full_model.py" --arms hip --steps 3 "$@" > "$O/fullprof.log" 2>&1
+    rc=$?; tail -3 "$O/fullprof.log"; exit $rc ;;
+  full)  # the whole drop-in model's step, both arms, no profiler
+    timeout -k 10 500 python tools/bench_full_model.py "$@" > "$O/full.json" 2> "$O/full.err"
+    rc=$?; cat "$O/full.json"; [ $rc -eq 0 ] || tail -20 "$O/full.err"; exit $rc ;;
   *) echo "unknown stage $stage"; exit 2 ;;
 esac
