@@ -358,8 +358,8 @@ int rgbd_mask_attention(int dtype, const void* logits, int B, int Q, int H, int 
 
 /* ---------------------------------------------------------------- f1 masked cross-attention
  * The attention core of nn.MultiheadAttention's math path as the masked-attention decoder layers
- * call it (transformers 5.15 modeling_mask2former.py:1640-1647 with the mask of :2048-2055), all
- * float32: per bh (= batch * heads + head), S = (q * scale) k^T, masked entries -inf,
+ * call it (transformers 5.15 modeling_mask2former.py:1640-1647 with the mask of :2048-2055),
+ * float32 arithmetic: per bh (= batch * heads + head), S = (q * scale) k^T, masked entries -inf,
  * P = softmax(S), out = P v.  Sequence-major, as the module's projections lay them out:
  * q [Q][BH][head_dim], k / v [L][BH][head_dim], out [Q][BH][head_dim], lse [Q][BH] (log-sum-exp
  * of the masked scaled scores, saved for the backward); mask bool bytes [BH][Q][L] (1 = not
@@ -367,14 +367,17 @@ int rgbd_mask_attention(int dtype, const void* logits, int B, int Q, int H, int 
  * ws: rgbd_masked_attn_fwd_workspace_size(BH, Q, L) bytes (per-key-split partials).
  * rgbd_masked_attn_bwd: dq, dk, dv (OVERWRITTEN) from dout; deterministic (no atomics);
  *   ws: rgbd_masked_attn_bwd_workspace_size(BH, Q, L) bytes.
- * q, k, v, out, dout, dk, dv 16-byte aligned. */
+ * q, k, v, out, dout, dk, dv 16-byte aligned;
+ * dtype (RGBD_F32 / RGBD_BF16) is the type of q, k, v, out, dout, dq, dk, dv (bf16: the
+ * module under torch.autocast, whose projections produce bf16); the arithmetic is float32 on
+ * the widened operands either way, lse / delta float32. */
 size_t rgbd_masked_attn_fwd_workspace_size(int BH, int Q, int L);
-int rgbd_masked_attn_fwd(const float* q, const float* k, const float* v, const uint8_t* mask, int BH, int Q, int L,
-                         int head_dim, float scale, float* out, float* lse, void* ws, void* stream);
+int rgbd_masked_attn_fwd(int dtype, const void* q, const void* k, const void* v, const uint8_t* mask, int BH, int Q,
+                         int L, int head_dim, float scale, void* out, float* lse, void* ws, void* stream);
 size_t rgbd_masked_attn_bwd_workspace_size(int BH, int Q, int L);
-int rgbd_masked_attn_bwd(const float* q, const float* k, const float* v, const uint8_t* mask, const float* out,
-                         const float* lse, const float* dout, int BH, int Q, int L, int head_dim, float scale,
-                         float* dq, float* dk, float* dv, void* ws, void* stream);
+int rgbd_masked_attn_bwd(int dtype, const void* q, const void* k, const void* v, const uint8_t* mask, const void* out,
+                         const float* lse, const void* dout, int BH, int Q, int L, int head_dim, float scale,
+                         void* dq, void* dk, void* dv, void* ws, void* stream);
 
 /* ---------------------------------------------------------------- f4 instance post-processing
  * Replaces Mask2FormerImageProcessor.post_process_instance_segmentation (transformers 5.15

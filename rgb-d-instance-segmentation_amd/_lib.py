@@ -81,9 +81,9 @@ SIGNATURES = {
     "rgbd_mask_logits": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "rgbd_mask_attention": (_I, [_I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "rgbd_masked_attn_fwd_workspace_size": (_SZ, [_I, _I, _I]),
-    "rgbd_masked_attn_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, ctypes.c_float, _P, _P, _P, _P]),
+    "rgbd_masked_attn_fwd": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.c_float, _P, _P, _P, _P]),
     "rgbd_masked_attn_bwd_workspace_size": (_SZ, [_I, _I, _I]),
-    "rgbd_masked_attn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.c_float, _P, _P, _P, _P,
+    "rgbd_masked_attn_bwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.c_float, _P, _P, _P, _P,
                                   _P]),
     "rgbd_timing_enable": (_I, [_I]),
     "rgbd_timing_read": (ctypes.c_double, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),

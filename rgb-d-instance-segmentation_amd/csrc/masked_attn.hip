@@ -1,4 +1,5 @@
-// f1: the masked cross-attention core of the Mask2Former decoder layers (gfx950, float32).
+// f1: the masked cross-attention core of the Mask2Former decoder layers (gfx950; float32 or
+// bfloat16 operands, float32 arithmetic).
 //
 // Reference (third-party, in the model the reference trains, custom_model.py:37-53):
 // transformers 5.15 Mask2FormerMaskedAttentionDecoderLayer.forward_post (modeling_mask2former.py
@@ -12,18 +13,18 @@
 //
 // Shapes here are few queries (100) against many keys (300 .. 19 200 per level), so the forward
 // and dQ split the work over KEY ranges (flash-decoding style) to fill 256 CUs; partials are merged
-// in split order (no atomics anywhere: the backward is deterministic).  Default kernels run on fp32
-// MFMA (v_mfma_f32_16x16x4_f32, exact f32 products and sums):
+// in split order (no atomics anywhere: the backward is deterministic).  The kernels run on fp32
+// MFMA (v_mfma_f32_16x16x4_f32, exact f32 products and sums) over operands of type T: float32, or
+// bfloat16 under torch.autocast (the projections then produce bf16 q / k / v; each element is
+// widened exactly on load, so the core adds no rounding of its own beyond torch's bf16 path —
+// the outputs o / dq / dk / dv are rounded to T once; lse and delta stay float32):
 //   k_attn_fwd_mfma     wave = 16 queries; S^T = K q_scaled^T, online softmax per query column,
 //                       O^T += V^T P^T with P^T taken straight from the accumulators; partial
 //                       (max, sum, o) per split -> k_attn_merge (also writes the row log-sum-exp)
 //   k_attn_bwd_kv_mfma  wave = 16 keys over all queries; S, dP, then dV^T += dO^T P, dK^T +=
 //                       q_scaled^T dS, K / V tiles held in registers
 //   k_attn_bwd_q_mfma   the forward's tiling: dq^T += K^T dS^T, partial per split -> k_attn_dq_sum
-// The earlier packed-fp32 VALU kernels (thread per query / per key, K / V rows as scalar loads)
-// stay selectable with RGBD_ATTN_FWD=valu / RGBD_ATTN_KV=valu (A/B and diagnosis).
 #include <cmath>
-#include <cstdlib>
 
 #include "common.hpp"
 
@@ -32,17 +33,16 @@ using namespace rgbd;
 namespace {
 
 constexpr int HD = 32;      // head dim (hidden 256 / 8 heads)
-constexpr int QW = 128;     // queries per forward / dQ workgroup (one per thread)
+constexpr int QW = 64;      // queries per forward / dQ workgroup (4 waves x 16)
 constexpr int KS = 64;      // key-split granularity
-constexpr int KC = 16;      // keys per online-softmax chunk
-constexpr int KVW = 256;    // keys per dK / dV workgroup (one per thread)
 
+template <typename T>
 struct AttnArgs {
-  const float* q;        // [Q][BH][HD] (unscaled)
-  const float* k;        // [L][BH][HD]
-  const float* v;        // [L][BH][HD]
+  const T* q;            // [Q][BH][HD] (unscaled)
+  const T* k;            // [L][BH][HD]
+  const T* v;            // [L][BH][HD]
   const uint8_t* mask;   // [BH][Q][L] bool, true = not allowed
-  float* o;              // [Q][BH][HD]
+  T* o;                  // [Q][BH][HD]
   float* lse;            // [Q][BH] log-sum-exp of the scaled, masked scores
   float* part_o;         // [nsplit][Q][BH][HD]
   float* part_ml;        // [nsplit][Q][BH][2] = (max, sum)
@@ -52,116 +52,6 @@ struct AttnArgs {
   bool vec_mask;         // mask rows 16-byte aligned (L % 16 == 0)
 };
 
-// Rows of K / V (forward, dQ) and of q_scaled / dO (dK / dV) are the same for every lane of a
-// wave: they are read through the constant address space, so they arrive as scalar loads into
-// SGPRs and feed the FMAs as scalar operands — no LDS staging, no broadcast traffic.
-typedef const float __attribute__((address_space(4))) cfloat;
-
-__device__ __forceinline__ const cfloat* uniform_row(const float* base, long long row, int BH, int bh) {
-  return (const cfloat*)(base + (row * BH + bh) * HD);
-}
-
-// Packed fp32 (v_pk_fma_f32): a 32-wide row is 16 float pairs; dot products keep two partial
-// sums (even / odd dims) added at the end.
-typedef float f2 __attribute__((ext_vector_type(2)));
-constexpr int HP = HD / 2;
-
-__device__ __forceinline__ f2 pair(const cfloat* row, int c) { return f2{row[2 * c], row[2 * c + 1]}; }
-
-__device__ __forceinline__ float dot_row(const f2 (&x)[HP], const cfloat* row) {
-  f2 acc = {0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < HP; ++c) acc = __builtin_elementwise_fma(x[c], pair(row, c), acc);
-  return acc.x + acc.y;
-}
-
-__device__ __forceinline__ void axpy_row(f2 (&acc)[HP], float a, const cfloat* row) {
-  const f2 a2 = {a, a};
-#pragma unroll
-  for (int c = 0; c < HP; ++c) acc[c] = __builtin_elementwise_fma(a2, pair(row, c), acc[c]);
-}
-
-__device__ __forceinline__ void load_row(f2 (&x)[HP], const float* row, bool ok, float mul) {
-#pragma unroll
-  for (int c = 0; c < HP; ++c) {
-    const float2 t = ok ? *reinterpret_cast<const float2*>(row + 2 * c) : make_float2(0.f, 0.f);
-    x[c] = f2{t.x * mul, t.y * mul};
-  }
-}
-
-__device__ __forceinline__ void store_row(float* row, const f2 (&x)[HP]) {
-#pragma unroll
-  for (int c = 0; c < HD / 4; ++c)
-    *reinterpret_cast<float4*>(row + 4 * c) = make_float4(x[2 * c].x, x[2 * c].y, x[2 * c + 1].x, x[2 * c + 1].y);
-}
-
-// bit j = key c0 + j masked (or past ke), from the lane's own mask row: one 16-byte load when
-// the row is 16-byte aligned (vec), else byte loads.
-__device__ __forceinline__ uint32_t mask_bits16(const uint8_t* mrow, int c0, int ke, bool vec) {
-  uint32_t bits = 0;
-  if (vec && c0 + KC <= ke) {
-    const uint4 w = *reinterpret_cast<const uint4*>(mrow + c0);
-    const uint32_t x[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) bits |= ((x[i] >> (8 * b)) & 1u) << (4 * i + b);
-  } else {
-    for (int j = 0; j < KC; ++j)
-      if (c0 + j >= ke || mrow[c0 + j]) bits |= 1u << j;
-  }
-  return bits;
-}
-
-// grid (nsplit, BH, ceil(Q / QW)), QW threads
-__global__ __launch_bounds__(QW) void k_attn_fwd(AttnArgs a) {
-  const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
-  const int qrow = blockIdx.z * QW + tid;
-  const bool qv = qrow < a.Q;
-  f2 qr[HP], o[HP];
-  load_row(qr, a.q + ((long long)qrow * a.BH + bh) * HD, qv, a.scale);  // q * scale, as torch forms it
-#pragma unroll
-  for (int c = 0; c < HP; ++c) o[c] = f2{0.f, 0.f};
-  const int kb = split * a.span, ke = min(a.L, kb + a.span);
-  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
-  float m = -INFINITY, l = 0.f;
-  uint32_t next_bits = kb < ke ? mask_bits16(mrow, kb, ke, a.vec_mask) : 0u;
-  for (int c0 = kb; c0 < ke; c0 += KC) {
-    const uint32_t bits = next_bits;  // mask bits one chunk ahead, so the load latency overlaps a chunk
-    if (c0 + KC < ke) next_bits = mask_bits16(mrow, c0 + KC, ke, a.vec_mask);
-    float s[KC];
-    float cmax = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < KC; ++j) {
-      s[j] = -INFINITY;
-      if (c0 + j < ke) {
-        const float acc = dot_row(qr, uniform_row(a.k, c0 + j, a.BH, bh));
-        if (!((bits >> j) & 1u)) s[j] = acc;
-      }
-      cmax = fmaxf(cmax, s[j]);
-    }
-    if (cmax != -INFINITY) {  // else the whole chunk is masked for this query
-      const float mn = fmaxf(m, cmax);
-      const float alpha = expf(m - mn);  // m == -inf -> 0 (l, o are 0 then)
-      l *= alpha;
-#pragma unroll
-      for (int c = 0; c < HP; ++c) o[c] *= alpha;
-      m = mn;
-    }
-#pragma unroll
-    for (int j = 0; j < KC; ++j) {
-      if (c0 + j >= ke) break;
-      const float p = s[j] == -INFINITY ? 0.f : expf(s[j] - m);  // masked: exactly 0, as torch's softmax
-      l += p;
-      axpy_row(o, p, uniform_row(a.v, c0 + j, a.BH, bh));
-    }
-  }
-  if (!qv) return;
-  const long long row = ((long long)split * a.Q + qrow) * a.BH + bh;
-  store_row(a.part_o + row * HD, o);
-  *reinterpret_cast<float2*>(a.part_ml + row * 2) = make_float2(m, l);
-}
-
 // K / V tile staging for the MFMA forward and dQ: 64 keys x 32 dims of each, two float4 per
 // thread per matrix, loaded one tile ahead into registers so the global loads overlap the
 // current tile's MFMAs.
@@ -169,15 +59,33 @@ struct KVTile {
   float4 k[2], v[2];
 };
 
-__device__ __forceinline__ void kv_load(KVTile& t, const float* K, const float* V, int k0, int ke, int BH, int bh,
-                                        int tid) {
+// 4 consecutive elements (16-byte aligned float4, or 8-byte aligned bf16 x4) widened to float
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const bf16_t* p) {
+  const uint2 w = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                     __uint_as_float(w.y & 0xffff0000u));
+}
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t* p) { return bf16_to_f32(*p); }
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void st4(bf16_t* p, float a, float b, float c, float d) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(a, b), pack_bf16x2(c, d));
+}
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16_t* p, float v) { *p = f32_to_bf16(v); }
+
+template <typename T>
+__device__ __forceinline__ void kv_load(KVTile& t, const T* K, const T* V, int k0, int ke, int BH, int bh, int tid) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int idx = tid + 256 * j, row = idx >> 3, c = idx & 7, key = k0 + row;
     const bool ok = key < ke;
     const long long off = ((long long)key * BH + bh) * HD + 4 * c;
-    t.k[j] = ok ? *reinterpret_cast<const float4*>(K + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-    t.v[j] = ok ? *reinterpret_cast<const float4*>(V + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    t.k[j] = ok ? ld4(K + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    t.v[j] = ok ? ld4(V + off) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -200,7 +108,8 @@ __device__ __forceinline__ void kv_store(float (*sk)[HD + 1], float (*sv)[HD + 1
 // Every accumulator of a lane belongs to its query column, so the rescale is a per-lane multiply.
 typedef float f4m __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs a) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs<T> a) {
   __shared__ float sk[64][HD + 1];
   __shared__ float sv[64][HD + 1];
   const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -209,7 +118,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs a) {
   const bool qv = qrow < a.Q;
   float qb[8];  // B operand: q_scaled^T [d = 4c + lg][query lc]
 #pragma unroll
-  for (int c = 0; c < 8; ++c) qb[c] = qv ? a.q[((long long)qrow * a.BH + bh) * HD + 4 * c + lg] * a.scale : 0.f;
+  for (int c = 0; c < 8; ++c) qb[c] = qv ? ld1(a.q + ((long long)qrow * a.BH + bh) * HD + 4 * c + lg) * a.scale : 0.f;
   f4m o[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
   float m = -INFINITY, lsum = 0.f;
   const int kb = split * a.span, ke = min(a.L, kb + a.span);
@@ -279,7 +188,8 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs a) {
 }
 
 // One 32-lane group per (q, bh) row: merge the splits' partials; o = sum_s e_s o_s / sum_s e_s l_s.
-__global__ __launch_bounds__(256) void k_attn_merge(AttnArgs a) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_merge(AttnArgs<T> a) {
   const long long rows = (long long)a.Q * a.BH;
   const long long r = blockIdx.x * 8ll + (threadIdx.x >> 5);
   const int d = threadIdx.x & 31;
@@ -297,22 +207,23 @@ __global__ __launch_bounds__(256) void k_attn_merge(AttnArgs a) {
     }
   }
   // a fully masked row: 0 / 0 = NaN, as torch's softmax gives
-  a.o[r * HD + d] = M == -INFINITY ? __builtin_nanf("") : acc / Ls;
+  st1(a.o + r * HD + d, M == -INFINITY ? __builtin_nanf("") : acc / Ls);
   if (d == 0) a.lse[r] = M == -INFINITY ? INFINITY : M + logf(Ls);
 }
 
+template <typename T>
 struct AttnBwdArgs {
-  const float* q;
-  const float* k;
-  const float* v;
+  const T* q;
+  const T* k;
+  const T* v;
   const uint8_t* mask;
   const float* lse;     // [Q][BH]
   const float* delta;   // [Q][BH] = rowsum(dO * O)
-  const float* dout;    // [Q][BH][HD]
+  const T* dout;        // [Q][BH][HD]
   const float* qs;      // [Q][BH][HD] = q * scale (k_attn_delta)
-  float* dq;            // [Q][BH][HD]
-  float* dk;            // [L][BH][HD]
-  float* dv;            // [L][BH][HD]
+  T* dq;                // [Q][BH][HD]
+  T* dk;                // [L][BH][HD]
+  T* dv;                // [L][BH][HD]
   float* part_dq;       // [nsplit][Q][BH][HD]
   int BH, Q, L;
   int nsplit, span;
@@ -321,58 +232,20 @@ struct AttnBwdArgs {
 };
 
 // One 32-lane group per (q, bh) row: delta = sum_d dO * O, and q_scaled = q * scale (fp32, as
-// torch forms it) for the dK / dV kernel's scalar reads.
-__global__ __launch_bounds__(256) void k_attn_delta(AttnBwdArgs a, const float* __restrict__ o, float* delta,
+// torch forms it) for the dK / dV kernel's LDS staging.
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_delta(AttnBwdArgs<T> a, const T* __restrict__ o, float* delta,
                                                     float* qs) {
   const long long rows = (long long)a.Q * a.BH;
   const long long r = blockIdx.x * 8ll + (threadIdx.x >> 5);
   const int d = threadIdx.x & 31;
   float v = 0.f;
   if (r < rows) {
-    v = o[r * HD + d] * a.dout[r * HD + d];
-    qs[r * HD + d] = a.q[r * HD + d] * a.scale;
+    v = ld1(o + r * HD + d) * ld1(a.dout + r * HD + d);
+    qs[r * HD + d] = ld1(a.q + r * HD + d) * a.scale;
   }
   for (int s = 16; s > 0; s >>= 1) v += __shfl_xor(v, s, 32);
   if (r < rows && d == 0) delta[r] = v;
-}
-
-// grid (ceil(L / KVW), BH), KVW threads: thread = key; q_scaled / dO rows of each query are
-// wave-uniform scalar reads.
-__global__ __launch_bounds__(KVW) void k_attn_bwd_kv(AttnBwdArgs a) {
-  const int bh = blockIdx.y, tid = threadIdx.x;
-  const int key = blockIdx.x * KVW + tid;
-  const bool kv = key < a.L;
-  f2 kr[HP], vr[HP], dk[HP], dv[HP];
-  load_row(kr, a.k + ((long long)key * a.BH + bh) * HD, kv, 1.f);
-  load_row(vr, a.v + ((long long)key * a.BH + bh) * HD, kv, 1.f);
-#pragma unroll
-  for (int c = 0; c < HP; ++c) dk[c] = dv[c] = f2{0.f, 0.f};
-  const cfloat* lse = (const cfloat*)a.lse;
-  const cfloat* del = (const cfloat*)a.delta;
-  const uint8_t* mcol = a.mask + (long long)bh * a.Q * a.L + (kv ? key : 0);
-  for (int q0 = 0; q0 < a.Q; q0 += 16) {
-    // the next 16 queries' mask bytes for this key, all loads in flight at once
-    uint32_t bits = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (q0 + j < a.Q && (!kv || mcol[(long long)(q0 + j) * a.L])) bits |= 1u << j;
-    const int qn = min(16, a.Q - q0);
-#pragma unroll 2
-    for (int j = 0; j < qn; ++j) {
-      const int qi = q0 + j;
-      const cfloat* qr = uniform_row(a.qs, qi, a.BH, bh);
-      const cfloat* dor = uniform_row(a.dout, qi, a.BH, bh);
-      const float s = dot_row(kr, qr);
-      const float dp = dot_row(vr, dor);
-      const float p = ((bits >> j) & 1u) ? 0.f : expf(s - lse[(long long)qi * a.BH + bh]);
-      const float ds = p * (dp - del[(long long)qi * a.BH + bh]);
-      axpy_row(dv, p, dor);
-      axpy_row(dk, ds, qr);  // dK = dS^T (q * scale)
-    }
-  }
-  if (!kv) return;
-  store_row(a.dk + ((long long)key * a.BH + bh) * HD, dk);
-  store_row(a.dv + ((long long)key * a.BH + bh) * HD, dv);
 }
 
 // dK / dV on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact f32): a wave owns 16 keys, a workgroup 64;
@@ -388,7 +261,8 @@ __global__ __launch_bounds__(KVW) void k_attn_bwd_kv(AttnBwdArgs a) {
 typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int QB = 64;
 
-__global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs a) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs<T> a) {
   __shared__ float sq[QB][HD + 1];
   __shared__ float sdo[QB][HD + 1];
   __shared__ float slse[QB], sdel[QB];
@@ -399,8 +273,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs a) {
   float kb[8], vb[8];  // B operands: K^T / V^T [d = 4c + lg][key lc]
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    kb[c] = kv ? a.k[((long long)keyl * a.BH + bh) * HD + 4 * c + lg] : 0.f;
-    vb[c] = kv ? a.v[((long long)keyl * a.BH + bh) * HD + 4 * c + lg] : 0.f;
+    kb[c] = kv ? ld1(a.k + ((long long)keyl * a.BH + bh) * HD + 4 * c + lg) : 0.f;
+    vb[c] = kv ? ld1(a.v + ((long long)keyl * a.BH + bh) * HD + 4 * c + lg) : 0.f;
   }
   f4v dv[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
   f4v dk[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
@@ -411,7 +285,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs a) {
       const int r = i / HD, d = i % HD, qrow = qb0 + r;
       const bool ok = qrow < a.Q;
       sq[r][d] = ok ? a.qs[((long long)qrow * a.BH + bh) * HD + d] : 0.f;
-      sdo[r][d] = ok ? a.dout[((long long)qrow * a.BH + bh) * HD + d] : 0.f;
+      sdo[r][d] = ok ? ld1(a.dout + ((long long)qrow * a.BH + bh) * HD + d) : 0.f;
     }
     if (tid < QB) {
       const int qrow = qb0 + tid;
@@ -447,51 +321,20 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs a) {
   }
   if (!kv) return;
   // accumulators: row = d = h*16 + lg*4 + j, col = key lc
-  float* dkr = a.dk + ((long long)keyl * a.BH + bh) * HD;
-  float* dvr = a.dv + ((long long)keyl * a.BH + bh) * HD;
+  T* dkr = a.dk + ((long long)keyl * a.BH + bh) * HD;
+  T* dvr = a.dv + ((long long)keyl * a.BH + bh) * HD;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    *reinterpret_cast<float4*>(dkr + h * 16 + lg * 4) = make_float4(dk[h][0], dk[h][1], dk[h][2], dk[h][3]);
-    *reinterpret_cast<float4*>(dvr + h * 16 + lg * 4) = make_float4(dv[h][0], dv[h][1], dv[h][2], dv[h][3]);
+    st4(dkr + h * 16 + lg * 4, dk[h][0], dk[h][1], dk[h][2], dk[h][3]);
+    st4(dvr + h * 16 + lg * 4, dv[h][0], dv[h][1], dv[h][2], dv[h][3]);
   }
-}
-
-// grid (nsplit, BH, ceil(Q / QW)), QW threads: thread = query; partial sum_k ds k over the split.
-__global__ __launch_bounds__(QW) void k_attn_bwd_q(AttnBwdArgs a) {
-  const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
-  const int qrow = blockIdx.z * QW + tid;
-  const bool qv = qrow < a.Q;
-  f2 qr[HP], dor[HP], g[HP];
-  load_row(qr, a.q + ((long long)qrow * a.BH + bh) * HD, qv, a.scale);
-  load_row(dor, a.dout + ((long long)qrow * a.BH + bh) * HD, qv, 1.f);
-#pragma unroll
-  for (int c = 0; c < HP; ++c) g[c] = f2{0.f, 0.f};
-  const float lse = qv ? a.lse[(long long)qrow * a.BH + bh] : 0.f;
-  const float del = qv ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
-  const int kb = split * a.span, ke = min(a.L, kb + a.span);
-  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
-  uint32_t next_bits = kb < ke ? mask_bits16(mrow, kb, ke, a.vec_mask) : 0u;
-  for (int c0 = kb; c0 < ke; c0 += KC) {
-    const uint32_t bits = next_bits;  // mask bits one chunk ahead, so the load latency overlaps a chunk
-    if (c0 + KC < ke) next_bits = mask_bits16(mrow, c0 + KC, ke, a.vec_mask);
-#pragma unroll 4
-    for (int j = 0; j < KC; ++j) {
-      if (c0 + j >= ke) break;
-      const cfloat* kr = uniform_row(a.k, c0 + j, a.BH, bh);
-      const float s = dot_row(qr, kr);
-      const float dp = dot_row(dor, uniform_row(a.v, c0 + j, a.BH, bh));
-      const float ds = ((bits >> j) & 1u) ? 0.f : expf(s - lse) * (dp - del);
-      axpy_row(g, ds, kr);
-    }
-  }
-  if (!qv) return;
-  store_row(a.part_dq + (((long long)split * a.Q + qrow) * a.BH + bh) * HD, g);
 }
 
 // dQ on fp32 MFMA, the forward's tiling: per 16-key block S^T = K . q_scaled^T and
 // dP^T = V . dO^T (8 + 8 MFMAs), dS^T = exp(S^T - lse) (dP^T - delta) in the accumulator layout,
 // then dq^T += K^T . dS^T (8 MFMAs, dS^T as the B operand); partial per key split.
-__global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs a) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs<T> a) {
   __shared__ float sk[64][HD + 1];
   __shared__ float sv[64][HD + 1];
   const int split = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -501,8 +344,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs a) {
   float qb[8], db[8];  // B operands: q_scaled^T, dO^T [d = 4c + lg][query lc]
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    qb[c] = qv ? a.q[((long long)qrow * a.BH + bh) * HD + 4 * c + lg] * a.scale : 0.f;
-    db[c] = qv ? a.dout[((long long)qrow * a.BH + bh) * HD + 4 * c + lg] : 0.f;
+    qb[c] = qv ? ld1(a.q + ((long long)qrow * a.BH + bh) * HD + 4 * c + lg) * a.scale : 0.f;
+    db[c] = qv ? ld1(a.dout + ((long long)qrow * a.BH + bh) * HD + 4 * c + lg) : 0.f;
   }
   const float lse = qv ? a.lse[(long long)qrow * a.BH + bh] : 0.f;
   const float del = qv ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
@@ -553,24 +396,22 @@ __global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs a) {
 }
 
 // dq = scale * sum over splits (split order, deterministic)
-__global__ __launch_bounds__(256) void k_attn_dq_sum(AttnBwdArgs a) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_dq_sum(AttnBwdArgs<T> a) {
   const long long n = (long long)a.Q * a.BH * HD;
   const long long i = blockIdx.x * 256ll + threadIdx.x;
   if (i >= n) return;
   float acc = 0.f;
   for (int s = 0; s < a.nsplit; ++s) acc += a.part_dq[s * n + i];
-  a.dq[i] = acc * a.scale;
+  st1(a.dq + i, acc * a.scale);
 }
 
 // Key splits: ~1024 x (Q / 128) workgroups (swept 512..4096 at B=8, L=4800: fewer splits make the
 // merge cheaper, more leave the MFMA kernels no faster), >= KS keys each.
 void split_keys(int BH, int Q, int L, int* nsplit, int* span) {
-  const long long base = (long long)BH * ((Q + QW - 1) / QW);
+  const long long base = (long long)BH * ((Q + 127) / 128);
   const int max_split = (L + KS - 1) / KS;
-  static const long long target = [] {  // workgroups to aim for (RGBD_ATTN_WG_TARGET, tuning)
-    const char* e = getenv("RGBD_ATTN_WG_TARGET");
-    return e ? std::max(1LL, atoll(e)) : 1024LL;
-  }();
+  const long long target = 1024;
   int ns = (int)std::min<long long>(max_split, std::max<long long>(1, (target + base - 1) / base));
   int sp = (L + ns - 1) / ns;
   sp = (sp + KS - 1) / KS * KS;
@@ -583,9 +424,52 @@ bool attn_shape_ok(const void* q, const void* k, const void* v, int BH, int Q, i
          ((uintptr_t)v % 16) == 0;
 }
 
+template <typename T>
+int attn_fwd(const void* q, const void* k, const void* v, const uint8_t* mask, int BH, int Q, int L, float scale,
+             void* out, float* lse, void* ws, hipStream_t s);
+template <typename T>
+int attn_bwd(const void* q, const void* k, const void* v, const uint8_t* mask, const void* out, const float* lse,
+             const void* dout, int BH, int Q, int L, float scale, void* dq, void* dk, void* dv, void* ws,
+             hipStream_t s);
+
 size_t attn_align(size_t x) { return (x + 255) / 256 * 256; }
 
 bool mask_vec(const uint8_t* mask, int L) { return (L % 16) == 0 && ((uintptr_t)mask % 16) == 0; }
+
+template <typename T>
+int attn_fwd(const void* q, const void* k, const void* v, const uint8_t* mask, int BH, int Q, int L, float scale,
+             void* out, float* lse, void* ws, hipStream_t s) {
+  AttnArgs<T> a = {(const T*)q, (const T*)k, (const T*)v, mask, (T*)out, lse, nullptr, nullptr, BH, Q, L, 0, 0,
+                   scale, mask_vec(mask, L)};
+  split_keys(BH, Q, L, &a.nsplit, &a.span);
+  const size_t rows = (size_t)a.nsplit * Q * BH;
+  a.part_o = (float*)ws;
+  a.part_ml = (float*)((char*)ws + attn_align(rows * HD * sizeof(float)));
+  k_attn_fwd_mfma<T><<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), 256, 0, s>>>(a);
+  const long long orows = (long long)Q * BH;
+  k_attn_merge<T><<<(unsigned)((orows + 7) / 8), 256, 0, s>>>(a);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+template <typename T>
+int attn_bwd(const void* q, const void* k, const void* v, const uint8_t* mask, const void* out, const float* lse,
+             const void* dout, int BH, int Q, int L, float scale, void* dq, void* dk, void* dv, void* ws,
+             hipStream_t s) {
+  const long long rows = (long long)BH * Q;
+  float* delta = (float*)ws;
+  float* qs = (float*)((char*)ws + attn_align((size_t)rows * sizeof(float)));
+  AttnBwdArgs<T> a = {(const T*)q, (const T*)k, (const T*)v, mask, lse, delta, (const T*)dout, qs, (T*)dq, (T*)dk,
+                      (T*)dv, nullptr, BH, Q, L, 0, 0, scale, mask_vec(mask, L)};
+  split_keys(BH, Q, L, &a.nsplit, &a.span);
+  a.part_dq = (float*)((char*)qs + attn_align((size_t)rows * HD * sizeof(float)));
+  k_attn_delta<T><<<(unsigned)((rows + 7) / 8), 256, 0, s>>>(a, (const T*)out, delta, qs);
+  k_attn_bwd_kv_mfma<T><<<dim3((L + 63) / 64, BH), 256, 0, s>>>(a);
+  k_attn_bwd_q_mfma<T><<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), 256, 0, s>>>(a);
+  k_attn_dq_sum<T><<<(unsigned)((rows * HD + 255) / 256), 256, 0, s>>>(a);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
 
 }  // namespace
 
@@ -599,25 +483,14 @@ size_t rgbd_masked_attn_fwd_workspace_size(int BH, int Q, int L) {
   return attn_align(rows * HD * sizeof(float)) + attn_align(rows * 2 * sizeof(float));
 }
 
-int rgbd_masked_attn_fwd(const float* q, const float* k, const float* v, const uint8_t* mask, int BH, int Q, int L,
-                         int head_dim, float scale, float* out, float* lse, void* ws, void* stream) {
+int rgbd_masked_attn_fwd(int dtype, const void* q, const void* k, const void* v, const uint8_t* mask, int BH, int Q,
+                         int L, int head_dim, float scale, void* out, float* lse, void* ws, void* stream) {
   RGBD_REQUIRE(q && k && v && mask && out && lse && ws && BH > 0 && Q > 0 && L > 0, RGBD_E_ARG);
   RGBD_REQUIRE(attn_shape_ok(q, k, v, BH, Q, L, head_dim) && ((uintptr_t)out % 16) == 0, RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
-  AttnArgs a = {q, k, v, mask, out, lse, nullptr, nullptr, BH, Q, L, 0, 0, scale, mask_vec(mask, L)};
-  split_keys(BH, Q, L, &a.nsplit, &a.span);
-  const size_t rows = (size_t)a.nsplit * Q * BH;
-  a.part_o = (float*)ws;
-  a.part_ml = (float*)((char*)ws + attn_align(rows * HD * sizeof(float)));
-  static const char* fwd_env = getenv("RGBD_ATTN_FWD");  // "valu": the thread-per-query kernel
-  if (fwd_env && fwd_env[0] == 'v')
-    k_attn_fwd<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
-  else
-    k_attn_fwd_mfma<<<dim3(a.nsplit, BH, (Q + 63) / 64), 256, 0, s>>>(a);
-  const long long orows = (long long)Q * BH;
-  k_attn_merge<<<(unsigned)((orows + 7) / 8), 256, 0, s>>>(a);
-  RGBD_CHECK_LAUNCH();
-  return RGBD_OK;
+  if (dtype == RGBD_F32) return attn_fwd<float>(q, k, v, mask, BH, Q, L, scale, out, lse, ws, s);
+  if (dtype == RGBD_BF16) return attn_fwd<bf16_t>(q, k, v, mask, BH, Q, L, scale, out, lse, ws, s);
+  return RGBD_E_DTYPE;
 }
 
 size_t rgbd_masked_attn_bwd_workspace_size(int BH, int Q, int L) {
@@ -628,35 +501,18 @@ size_t rgbd_masked_attn_bwd_workspace_size(int BH, int Q, int L) {
          attn_align((size_t)ns * Q * BH * HD * sizeof(float));
 }
 
-int rgbd_masked_attn_bwd(const float* q, const float* k, const float* v, const uint8_t* mask, const float* out,
-                         const float* lse, const float* dout, int BH, int Q, int L, int head_dim, float scale,
-                         float* dq, float* dk, float* dv, void* ws, void* stream) {
+int rgbd_masked_attn_bwd(int dtype, const void* q, const void* k, const void* v, const uint8_t* mask, const void* out,
+                         const float* lse, const void* dout, int BH, int Q, int L, int head_dim, float scale,
+                         void* dq, void* dk, void* dv, void* ws, void* stream) {
   RGBD_REQUIRE(q && k && v && mask && out && lse && dout && dq && dk && dv && ws && BH > 0 && Q > 0 && L > 0,
                RGBD_E_ARG);
   RGBD_REQUIRE(attn_shape_ok(q, k, v, BH, Q, L, head_dim) && ((uintptr_t)dout % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
                    ((uintptr_t)dk % 16) == 0 && ((uintptr_t)dv % 16) == 0,
                RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
-  const long long rows = (long long)BH * Q;
-  float* delta = (float*)ws;
-  float* qs = (float*)((char*)ws + attn_align((size_t)rows * sizeof(float)));
-  AttnBwdArgs a = {q, k, v, mask, lse, delta, dout, qs, dq, dk, dv, nullptr, BH, Q, L, 0, 0, scale,
-                   mask_vec(mask, L)};
-  split_keys(BH, Q, L, &a.nsplit, &a.span);
-  a.part_dq = (float*)((char*)qs + attn_align((size_t)rows * HD * sizeof(float)));
-  k_attn_delta<<<(unsigned)((rows + 7) / 8), 256, 0, s>>>(a, out, delta, qs);
-  static const char* kv_env = getenv("RGBD_ATTN_KV");  // "valu": the thread-per-key kernel
-  if (kv_env && kv_env[0] == 'v')
-    k_attn_bwd_kv<<<dim3((L + KVW - 1) / KVW, BH), KVW, 0, s>>>(a);
-  else
-    k_attn_bwd_kv_mfma<<<dim3((L + 63) / 64, BH), 256, 0, s>>>(a);
-  if (kv_env && kv_env[0] == 'v')
-    k_attn_bwd_q<<<dim3(a.nsplit, BH, (Q + QW - 1) / QW), QW, 0, s>>>(a);
-  else
-    k_attn_bwd_q_mfma<<<dim3(a.nsplit, BH, (Q + 63) / 64), 256, 0, s>>>(a);
-  k_attn_dq_sum<<<(unsigned)((rows * HD + 255) / 256), 256, 0, s>>>(a);
-  RGBD_CHECK_LAUNCH();
-  return RGBD_OK;
+  if (dtype == RGBD_F32) return attn_bwd<float>(q, k, v, mask, out, lse, dout, BH, Q, L, scale, dq, dk, dv, ws, s);
+  if (dtype == RGBD_BF16) return attn_bwd<bf16_t>(q, k, v, mask, out, lse, dout, BH, Q, L, scale, dq, dk, dv, ws, s);
+  return RGBD_E_DTYPE;
 }
 
 }  // extern "C"

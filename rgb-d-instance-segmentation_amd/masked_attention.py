@@ -18,7 +18,10 @@ or not anyone reads the weights, so the module takes torch's path (weights retur
 they are consumed: ``need_weights_output`` set on the module, or the decoder layer called with
 ``output_attentions=True`` (``install`` registers a forward pre-hook on each decoder layer that
 tells its ``cross_attn`` so).  Inputs the kernels do not cover (a key padding mask, a float
-mask, dropout in training, head_dim != 32, batch_first) also go through torch's path unchanged.
+mask, dropout in training, head_dim != 32, batch_first, float16) also go through torch's path
+unchanged.  Under torch.autocast(bfloat16) the projections run as autocast runs them (bf16
+GEMMs) and the core reads their bf16 q / k / v (float32 arithmetic, bf16 output, as torch's
+autocast math path returns).
 ``install(model)`` swaps the class of the decoder layers' ``cross_attn`` modules in place (same
 parameters, same state_dict keys).
 
@@ -36,23 +39,26 @@ from torch import nn
 
 from . import _lib
 from ._lib import check
-from .ops import _need_cuda, _p, _stream
+from .ops import _dtype_code, _need_cuda, _p, _stream
 
 
 class MaskedAttentionFunction(torch.autograd.Function):
-    """q [Q, BH, 32], k / v [L, BH, 32] float32 (contiguous), mask bool [BH, Q, L] -> o [Q, BH, 32]."""
+    """q [Q, BH, 32], k / v [L, BH, 32] float32 or bfloat16 (one dtype, contiguous), mask bool
+    [BH, Q, L] -> o [Q, BH, 32] of the same dtype (float32 arithmetic either way)."""
 
     @staticmethod
     def forward(ctx, q, k, v, mask, scale):
         _need_cuda(q, k, v, mask)
+        if not (q.dtype == k.dtype == v.dtype) or q.dtype not in (torch.float32, torch.bfloat16):
+            raise TypeError("masked attention: q, k, v must share one dtype, float32 or bfloat16")
         Q, BH, hd = q.shape
         L = k.shape[0]
         out = torch.empty_like(q)
         lse = torch.empty((Q, BH), dtype=torch.float32, device=q.device)
         L_ = _lib.lib()
         ws = torch.empty((L_.rgbd_masked_attn_fwd_workspace_size(BH, Q, L),), dtype=torch.uint8, device=q.device)
-        check(L_.rgbd_masked_attn_fwd(_p(q), _p(k), _p(v), _p(mask), BH, Q, L, hd, float(scale), _p(out), _p(lse),
-                                      _p(ws), _stream(q.device)), "rgbd_masked_attn_fwd")
+        check(L_.rgbd_masked_attn_fwd(_dtype_code(q), _p(q), _p(k), _p(v), _p(mask), BH, Q, L, hd, float(scale),
+                                      _p(out), _p(lse), _p(ws), _stream(q.device)), "rgbd_masked_attn_fwd")
         ctx.save_for_backward(q, k, v, mask, out, lse)
         ctx.scale = float(scale)
         return out
@@ -62,12 +68,12 @@ class MaskedAttentionFunction(torch.autograd.Function):
         q, k, v, mask, out, lse = ctx.saved_tensors
         Q, BH, hd = q.shape
         L = k.shape[0]
-        g = gout.float().contiguous()
+        g = gout.to(q.dtype).contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         L_ = _lib.lib()
         ws = torch.empty((L_.rgbd_masked_attn_bwd_workspace_size(BH, Q, L),), dtype=torch.uint8, device=q.device)
-        check(L_.rgbd_masked_attn_bwd(_p(q), _p(k), _p(v), _p(mask), _p(out), _p(lse), _p(g), BH, Q, L, hd,
-                                      ctx.scale, _p(dq), _p(dk), _p(dv), _p(ws), _stream(q.device)),
+        check(L_.rgbd_masked_attn_bwd(_dtype_code(q), _p(q), _p(k), _p(v), _p(mask), _p(out), _p(lse), _p(g), BH, Q,
+                                      L, hd, ctx.scale, _p(dq), _p(dk), _p(dv), _p(ws), _stream(q.device)),
               "rgbd_masked_attn_bwd")
         return dq, dk, dv, None, None
 
@@ -82,14 +88,18 @@ class HipMultiheadAttention(nn.MultiheadAttention):
 
     def _hip_ok(self, query, key, value, key_padding_mask, attn_mask, is_causal):
         E = self.embed_dim
-        return (query.is_cuda and query.dtype == key.dtype == value.dtype == torch.float32
+        # float32 or bfloat16 inputs; under autocast only bfloat16 (the projections then produce
+        # bf16 q / k / v, and the kernels read them as such)
+        amp = torch.is_autocast_enabled("cuda")
+        return (query.is_cuda and query.dtype == key.dtype == value.dtype
+                and query.dtype in (torch.float32, torch.bfloat16)
+                and (not amp or torch.get_autocast_dtype("cuda") == torch.bfloat16)
                 and not self.batch_first and self._qkv_same_embed_dim and self.in_proj_bias is not None
                 and self.bias_k is None and not self.add_zero_attn and key_padding_mask is None
                 and not is_causal and E // self.num_heads == 32 and (self.dropout == 0.0 or not self.training)
                 and attn_mask is not None and attn_mask.dtype == torch.bool and attn_mask.dim() == 3
                 and query.dim() == 3 and key.shape == value.shape
-                and tuple(attn_mask.shape) == (query.shape[1] * self.num_heads, query.shape[0], key.shape[0])
-                and not torch.is_autocast_enabled("cuda"))
+                and tuple(attn_mask.shape) == (query.shape[1] * self.num_heads, query.shape[0], key.shape[0]))
 
     def forward(self, query, key, value, key_padding_mask=None, need_weights=True, attn_mask=None,
                 average_attn_weights=True, is_causal=False):

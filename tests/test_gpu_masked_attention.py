@@ -88,6 +88,40 @@ def test_module_matches_torch_multihead_attention(shape):
 
 
 @gpu
+@pytest.mark.parametrize("shape", SHAPES)
+def test_module_bf16_autocast_vs_torch(shape):
+    """Under torch.autocast(bfloat16) — the bf16 configuration of the whole model — the module
+    runs the kernels on the projections' bf16 q / k / v (weights None: not torch's path).  Stated
+    tolerance: its error against the float32 module (outputs and every input / parameter
+    gradient, max-abs relative to the max) is within 1.5x torch's own autocast error on the same
+    inputs (+1e-3 slack: a handful of bf16 roundings either way)."""
+    B, Q, L = shape
+    ref, hip = _modules()
+    query, key, value, mask = _inputs(B, Q, L, seed=7 * B + Q + L)
+
+    def run(mod, amp):
+        xs = [t.clone().requires_grad_() for t in (query, key, value)]
+        mod.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out, w = mod(*xs, attn_mask=mask, key_padding_mask=None)
+        g = torch.randn(out.shape, generator=torch.Generator(device="cuda").manual_seed(5), device="cuda")
+        out.float().backward(g)
+        return out, w, [t.grad for t in xs] + [p.grad for p in mod.parameters()]
+    o32, _, g32 = run(ref, False)
+    ot, wt, gt = run(ref, True)
+    oh, wh, gh = run(hip, True)
+    assert wh is None and wt is not None and oh.dtype == ot.dtype == torch.bfloat16
+
+    def rel(a, e):
+        return float((a.float() - e).abs().max()) / (float(e.abs().max()) + 1e-12)
+    et, eh = rel(ot, o32), rel(oh, o32)
+    print(f"{shape}: output rel err torch-autocast {et:.3g}, hip {eh:.3g}")
+    assert eh <= 1.5 * et + 1e-3
+    for a, b, e in zip(gt, gh, g32):
+        assert rel(b, e) <= 1.5 * rel(a, e) + 1e-3, (rel(b, e), rel(a, e))
+
+
+@gpu
 def test_fully_masked_row_is_nan_like_torch():
     ref, hip = _modules()
     query, key, value, mask = _inputs(1, 6, 40)
