@@ -419,7 +419,12 @@ __global__ __launch_bounds__(256) void k_codes_pyramid(const float* __restrict__
     }
   }
   __syncthreads();
-  if (cmask && threadIdx.x < 3 && smask[threadIdx.x]) atomicOr(cmask + threadIdx.x, smask[threadIdx.x]);
+  // every block ORs into the same three words: skip the atomic when the bits are already there
+  // (the words only gain bits during the launch, so a stale read can only cause an extra atomic)
+  if (cmask && threadIdx.x < 3 && smask[threadIdx.x]) {
+    const uint32_t seen = __hip_atomic_load(cmask + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((seen | smask[threadIdx.x]) != seen) atomicOr(cmask + threadIdx.x, smask[threadIdx.x]);
+  }
 }
 
 // Presence masks of code planes the pyramid kernel did not build (the general path).

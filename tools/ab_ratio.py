@@ -19,18 +19,20 @@ from rgbd_amd import _lib, init as winit, synthetic  # noqa: E402
 from rgbd_amd.modules import EnhancedDepthImageRatioPredictor  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("other")
+ap.add_argument("others", nargs="+")
 ap.add_argument("--rounds", type=int, default=8)
 ap.add_argument("--iters", type=int, default=10)
 a = ap.parse_args()
 
 new = _lib.lib()
-h = ctypes.CDLL(os.path.join(_R, a.other))
-for name, (res, args) in _lib.SIGNATURES.items():
-    if hasattr(h, name):
-        fn = getattr(h, name)
-        fn.restype, fn.argtypes = res, args
-libs = {"new": new, "old": h}
+libs = {"new": new}
+for other in a.others:
+    h = ctypes.CDLL(os.path.join(_R, other))
+    for name, (res, args) in _lib.SIGNATURES.items():
+        if hasattr(h, name):
+            fn = getattr(h, name)
+            fn.restype, fn.argtypes = res, args
+    libs[os.path.basename(other)] = h
 
 m = EnhancedDepthImageRatioPredictor(3)
 winit.init_deterministic(m, prefix="model.pixel_level_module.ratio_predictor.")
@@ -61,5 +63,13 @@ for rnd in range(a.rounds + 1):
         L.rgbd_timing_enable(0)
         if rnd:
             res[tag]["total"].append(e0.elapsed_time(e1) / a.iters)
+# same inputs, eval mode (deterministic): every build must give the in-tree build's ratio bitwise
+m.eval()
+outs = {}
+for tag, L in libs.items():
+    _lib._lib = L
+    outs[tag] = m(d).cpu()
+_lib._lib = new
+m.train()
 for tag in libs:
-    print(tag, "  ".join(f"{n} {statistics.median(v):.4f} ms (min {min(v):.4f})" for n, v in res[tag].items()))
+    print(tag, "ratio==new:", bool(torch.equal(outs[tag], outs["new"])), "  ".join(f"{n} {statistics.median(v):.4f} ms (min {min(v):.4f})" for n, v in res[tag].items()))
