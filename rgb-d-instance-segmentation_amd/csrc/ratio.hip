@@ -1291,11 +1291,17 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           }
         }
 #else
+#if !(C5_VAR & 4)
         if (st + 1 < C3_STEPS)
           issue_b(st + 1);
         else if (has_next)
           issue_b(0);
+#endif
+#if C5_VAR & 8
+        if (false) {
+#else
         if (st < 6) {
+#endif
           const int j = wave + 8 * st;
           if (j < C3_APIECES) {
             issue_a(t, 1, j);
@@ -1338,12 +1344,17 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
       }
       // own DMA landed (except the A pieces just issued), own LDS reads done, then the barrier
+#if C5_VAR & 16
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      (void)a_issued;
+#else
       if (a_issued == 2)
         asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else if (a_issued == 1)
         asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
     }
     // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
     // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
