@@ -402,6 +402,18 @@ int rgbd_pp_instance(const float* class_logits, const float* mask_logits, int B,
 int rgbd_pp_binary_maps(const void* ws, int B, int Q, int b, int Ht, int Wt, const int* seg_id, float* out,
                         void* stream);
 
+/* ---------------------------------------------------------------- f4 segm mAP: mask IoU
+ * The mask IoU of torchmetrics MeanAveragePrecision(iou_type="segm") as the reference's
+ * Evaluator uses it (model_essential_part.py:56-157; pycocotools maskApi rleIou underneath).
+ * rgbd_pack_mask_bits: masks uint8 [n][npx] ({0, nonzero}) -> bits u64 [n][ceil(npx / 64)]
+ *   (bit j of word w = pixel 64 w + j) and area int32 [n] (OVERWRITTEN).
+ * rgbd_mask_intersections: inter int32 [na][nb] = popcount(a_i AND b_j) over packed masks of the
+ *   same npx.  IoU = inter / (area_a + area_b - inter), 0 when inter == 0 (rleIou). */
+int rgbd_pack_mask_bits(const uint8_t* masks, int n, long long npx, unsigned long long* bits, int* area,
+                        void* stream);
+int rgbd_mask_intersections(const unsigned long long* a, int na, const unsigned long long* b, int nb, long long npx,
+                            int* inter, void* stream);
+
 /* ---------------------------------------------------------------- kernel timing (bench only)
  * When enabled, launch functions bracket their main kernel with hipEvents recorded on the
  * launch stream; rgbd_timing_read synchronises those events and returns the summed

@@ -39,6 +39,8 @@ SIGNATURES = {
     "rgbd_pp_instance_workspace_size": (_SZ, [_I, _I]),
     "rgbd_pp_instance": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, ctypes.c_double, _P, _P, _P, _P, _P, _P]),
     "rgbd_pp_binary_maps": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "rgbd_pack_mask_bits": (_I, [_P, _I, _LL, _P, _P, _P]),
+    "rgbd_mask_intersections": (_I, [_P, _I, _P, _I, _LL, _P, _P]),
     "rgbd_edsam_decompose_workspace_size": (_SZ, [_I]),
     "rgbd_edsam_decompose": (_I, [_P, _LL, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_edsam_decompose_masks": (_I, [_P, _LL, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
