@@ -205,7 +205,9 @@ __global__ __launch_bounds__(256) void k_msda_bwd_query(const T* __restrict__ va
 // value gradient belongs to exactly one workgroup: plain stores, no memset, no global atomics
 // (grid_sample's backward scatters with global atomics; at the C2 shape those were 2.5 GB of
 // atomic traffic per call).  Thread = (query, channel pair); 128 queries per pass, 8 waves per
-// workgroup (the tile is the only LDS user: one workgroup per CU, so it brings its own waves).
+// workgroup (the tile is the only LDS user: one workgroup per CU, so it brings its own waves);
+// each thread keeps the loads of 4 queries in flight (the scan is latency-bound: per query 48
+// scattered bytes of locations / weights / gradient).
 constexpr int MSDA_C = 8;                                         // channels per workgroup
 constexpr int MSDA_BAND = 163840 / (MSDA_C * (int)sizeof(float));  // pixels per LDS tile (160 KiB)
 
@@ -217,7 +219,7 @@ struct MsdaBands {
 template <typename T, int D>
 __global__ __launch_bounds__(512) void k_msda_bwd_value(MsdaLevels lv, MsdaBands bd, int S, int Q, int NH, int P,
                                                         const float* __restrict__ loc, const float* __restrict__ attw,
-                                                        const T* __restrict__ gout, int BNH,
+                                                        const T* __restrict__ gout, int BNH, int vec4,
                                                         float* __restrict__ gvalue) {
   extern __shared__ float tile[];  // [band px][MSDA_C]
   constexpr int NCH = D / MSDA_C;
@@ -235,24 +237,52 @@ __global__ __launch_bounds__(512) void k_msda_bwd_value(MsdaLevels lv, MsdaBands
   __syncthreads();
   const int cp = threadIdx.x & 3;  // channel pair 2cp, 2cp+1 of the chunk
   const int c0 = chunk * MSDA_C + 2 * cp;
-  for (int q = threadIdx.x >> 2; q < Q; q += 128) {
-    const long long qh = ((long long)b * Q + q) * NH + h;
-    const float* lq = loc + (qh * lv.L + l) * P * 2;
-    const float* wq = attw + (qh * lv.L + l) * P;
-    const T* gq = gout + qh * D + c0;
-    const float g0 = Num<T>::to_f(gq[0]), g1 = Num<T>::to_f(gq[1]);
-    for (int p = 0; p < P; ++p) {
-      const Tap t = msda_tap(lq[2 * p], lq[2 * p + 1], H, W);
-      const float a = wq[p];
+  auto add_point = [&](float lx, float ly, float a, float g0, float g1) {
+    const Tap t = msda_tap(lx, ly, H, W);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ix = t.idx[e] - lo;
-        if (t.idx[e] >= 0 && ix >= 0 && ix < n) {
-          const float f = a * t.w[e];
-          atomicAdd(&tile[ix * MSDA_C + 2 * cp], f * g0);
-          atomicAdd(&tile[ix * MSDA_C + 2 * cp + 1], f * g1);
+    for (int e = 0; e < 4; ++e) {
+      const int ix = t.idx[e] - lo;
+      if (t.idx[e] >= 0 && ix >= 0 && ix < n) {
+        const float f = a * t.w[e];
+        atomicAdd(&tile[ix * MSDA_C + 2 * cp], f * g0);
+        atomicAdd(&tile[ix * MSDA_C + 2 * cp + 1], f * g1);
+      }
+    }
+  };
+  constexpr int U = 4;  // queries per thread in flight: their loads issue together (latency-bound)
+  if (vec4) {  // P == 4, locations / weights 16-byte aligned
+    for (int q0 = threadIdx.x >> 2; q0 < Q; q0 += 128 * U) {
+      float4 la[U], lb[U], wa[U];
+      float ga[U], gb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + 128 * u;
+        if (q < Q) {
+          const long long qh = ((long long)b * Q + q) * NH + h;
+          const float* lq = loc + (qh * lv.L + l) * 8;  // 4 points x (x, y): 32 B, 32-B aligned
+          la[u] = *reinterpret_cast<const float4*>(lq);
+          lb[u] = *reinterpret_cast<const float4*>(lq + 4);
+          wa[u] = *reinterpret_cast<const float4*>(attw + (qh * lv.L + l) * 4);
+          ga[u] = Num<T>::to_f(gout[qh * D + c0]);
+          gb[u] = Num<T>::to_f(gout[qh * D + c0 + 1]);
         }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q0 + 128 * u >= Q) break;
+        add_point(la[u].x, la[u].y, wa[u].x, ga[u], gb[u]);
+        add_point(la[u].z, la[u].w, wa[u].y, ga[u], gb[u]);
+        add_point(lb[u].x, lb[u].y, wa[u].z, ga[u], gb[u]);
+        add_point(lb[u].z, lb[u].w, wa[u].w, ga[u], gb[u]);
+      }
+    }
+  } else {
+    for (int q = threadIdx.x >> 2; q < Q; q += 128) {
+      const long long qh = ((long long)b * Q + q) * NH + h;
+      const float* lq = loc + (qh * lv.L + l) * P * 2;
+      const float* wq = attw + (qh * lv.L + l) * P;
+      const float g0 = Num<T>::to_f(gout[qh * D + c0]), g1 = Num<T>::to_f(gout[qh * D + c0 + 1]);
+      for (int p = 0; p < P; ++p) add_point(lq[2 * p], lq[2 * p + 1], wq[p], g0, g1);
     }
   }
   __syncthreads();
@@ -304,7 +334,8 @@ int launch_bwd(const void* value, const MsdaLevels& lv, int B, int S, int Q, int
   static const hipError_t attr = hipFuncSetAttribute((const void*)k_msda_bwd_value<T, D>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   if (attr != hipSuccess) return (int)attr;
-  k_msda_bwd_value<T, D><<<work, 512, lds, s>>>(lv, bd, S, Q, NH, P, loc, attw, (const T*)gout, B * NH, gvalue);
+  const int vec4 = P == 4 && ((uintptr_t)loc & 15) == 0 && ((uintptr_t)attw & 15) == 0;
+  k_msda_bwd_value<T, D><<<work, 512, lds, s>>>(lv, bd, S, Q, NH, P, loc, attw, (const T*)gout, B * NH, vec4, gvalue);
   return RGBD_OK;
 }
 
