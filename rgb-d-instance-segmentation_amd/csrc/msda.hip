@@ -12,10 +12,10 @@
 // grid_sample's align_corners=False rule with zero padding), reads the four taps as D contiguous
 // channels of the [B][S][heads][D] value (16 bytes per lane), and accumulates weight * sample in
 // registers — no per-level copy, no [.., Q, L*P] intermediate.
-// Backward in two launches: k_msda_bwd_query reduces, per (level, point), go . sample
-// (attention-weight gradient) and go . d sample / d(ix, iy) (sampling-location gradient);
-// k_msda_bwd_value gathers the value gradient into LDS tiles (no global atomics).  Bound: gather /
-// L2 latency (the value of a level is at most a few MB per image) and LDS atomics.
+// Backward (k_msda_bwd): per (level, point) the group reduces go . sample (attention-weight
+// gradient) and go . d sample / d(ix, iy) (sampling-location gradient) with shuffles, and
+// scatters weight * tap weight * go into the value gradient with float atomics (as
+// grid_sample's backward does).  Bound: the atomic byte rate.
 #include <algorithm>
 
 #include "common.hpp"
@@ -132,18 +132,23 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-// Backward, per query: the attention-weight gradient go . sample and the sampling-location
-// gradient go . d sample / d(ix, iy), the forward's lane groups reducing over their 8-channel
-// slices with shuffles.  No atomics: the value gradient is k_msda_bwd_value's.
+// Backward: one group of D lanes per (image, query, head), lane c = channel c (a tap's value
+// row is one 128-byte line in f32): per (level, point) the group reduces go . sample (attention-
+// weight gradient) and go . d sample / d(ix, iy) (sampling-location gradient) with shuffles and
+// scatters a * w_tap * go into the value gradient with float atomics, each wave-instruction two
+// 128-byte row segments (MI355X_MICROARCH "Global float atomics": the full-rate shape).  Bound:
+// the atomic byte rate (~1.3 TB/s; 2.5 GB at the C2 pixel decoder).  Measured alternative
+// (r03): the value gradient gathered into a float32 LDS tile per (image, head, level, 8
+// channels) with ds_add_f32 — 1.4x SLOWER (2.7 vs 1.9 ms at C2): LDS float atomics ran at about
+// a tenth of plain LDS read-modify-write (same kernel with racy plain adds: 0.27 ms), with or
+// without same-address conflicts.
 template <typename T, int D>
-__global__ __launch_bounds__(256) void k_msda_bwd_query(const T* __restrict__ value, MsdaLevels lv, int S, int Q,
-                                                        int NH, int P, const float* __restrict__ loc,
-                                                        const float* __restrict__ attw, const T* __restrict__ gout,
-                                                        long long nqh, float* __restrict__ gloc,
-                                                        float* __restrict__ gattw) {
-  constexpr int G = D / 8;
-  const int j = threadIdx.x % G;
-  const long long qh = (long long)blockIdx.x * (256 / G) + threadIdx.x / G;
+__global__ __launch_bounds__(256) void k_msda_bwd(const T* __restrict__ value, MsdaLevels lv, int S, int Q, int NH,
+                                                  int P, const float* __restrict__ loc, const float* __restrict__ attw,
+                                                  const T* __restrict__ gout, long long nqh, float* __restrict__ gvalue,
+                                                  float* __restrict__ gloc, float* __restrict__ gattw) {
+  const int c = threadIdx.x % D;
+  const long long qh = (long long)blockIdx.x * (256 / D) + threadIdx.x / D;
   // every lane of a group takes part in the shuffles: out-of-range groups run with zero weight
   const bool live = qh < nqh;
   const long long q0 = live ? qh : 0;
@@ -151,146 +156,40 @@ __global__ __launch_bounds__(256) void k_msda_bwd_query(const T* __restrict__ va
   const long long b = (q0 / NH) / Q;
   const float* lq = loc + q0 * lv.L * P * 2;
   const float* wq = attw + q0 * lv.L * P;
-  const T* vb = value + b * S * NH * D + (long long)h * D + 8 * j;
-  float go[8];
-  ld8(gout + q0 * D + 8 * j, go);
-  if (!live)
-#pragma unroll
-    for (int c = 0; c < 8; ++c) go[c] = 0.f;
+  const long long voff = b * S * NH * D + (long long)h * D + c;
+  const T* vb = value + voff;
+  float* gvb = gvalue + voff;
+  const float go = live ? Num<T>::to_f(gout[q0 * D + c]) : 0.f;
   for (int l = 0; l < lv.L; ++l) {
     const int H = lv.H[l], W = lv.W[l];
-    const T* vl = vb + (long long)lv.start[l] * NH * D;
+    const long long lo = (long long)lv.start[l] * NH * D;
     for (int p = 0; p < P; ++p) {
       const int k = l * P + p;
       const Tap t = msda_tap(lq[2 * k], lq[2 * k + 1], H, W);
-      float v[4][8];
+      const float a = wq[k];
+      float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (t.idx[e] >= 0) {
-          ld8(vl + (long long)t.idx[e] * NH * D, v[e]);
-        } else {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) v[e][c] = 0.f;
+      for (int e = 0; e < 4; ++e) v[e] = t.idx[e] >= 0 ? Num<T>::to_f(vb[lo + (long long)t.idx[e] * NH * D]) : 0.f;
+      const float s = t.w[0] * v[0] + t.w[1] * v[1] + t.w[2] * v[2] + t.w[3] * v[3];
+      // d sample / d ix, d iy (zero-padded taps are zeros)
+      const float dsx = (1.f - t.ly) * (v[1] - v[0]) + t.ly * (v[3] - v[2]);
+      const float dsy = (1.f - t.lx) * (v[2] - v[0]) + t.lx * (v[3] - v[1]);
+      const float gw = group_sum<D>(go * s);
+      const float gx = group_sum<D>(go * dsx);
+      const float gy = group_sum<D>(go * dsy);
+      if (live) {
+        if (c == 0) {
+          gattw[q0 * lv.L * P + k] = gw;
+          // ix = loc * W - 1/2 through grid = 2 loc - 1: d ix / d loc = W
+          gloc[(q0 * lv.L * P + k) * 2] = a * gx * (float)W;
+          gloc[(q0 * lv.L * P + k) * 2 + 1] = a * gy * (float)H;
         }
-      }
-      float gw = 0.f, gx = 0.f, gy = 0.f;
+        const float ga = a * go;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const float smp = t.w[0] * v[0][c] + t.w[1] * v[1][c] + t.w[2] * v[2][c] + t.w[3] * v[3][c];
-        // d sample / d ix, d iy (zero-padded taps are zeros)
-        const float dsx = (1.f - t.ly) * (v[1][c] - v[0][c]) + t.ly * (v[3][c] - v[2][c]);
-        const float dsy = (1.f - t.lx) * (v[2][c] - v[0][c]) + t.lx * (v[3][c] - v[1][c]);
-        gw += go[c] * smp;
-        gx += go[c] * dsx;
-        gy += go[c] * dsy;
-      }
-      gw = group_sum<G>(gw);
-      gx = group_sum<G>(gx);
-      gy = group_sum<G>(gy);
-      if (live && j == 0) {
-        const float a = wq[k];
-        gattw[q0 * lv.L * P + k] = gw;
-        // ix = loc * W - 1/2 through grid = 2 loc - 1: d ix / d loc = W
-        gloc[(q0 * lv.L * P + k) * 2] = a * gx * (float)W;
-        gloc[(q0 * lv.L * P + k) * 2 + 1] = a * gy * (float)H;
+        for (int e = 0; e < 4; ++e)
+          if (t.idx[e] >= 0) atomicAdd(gvb + lo + (long long)t.idx[e] * NH * D, ga * t.w[e]);
       }
     }
-  }
-}
-
-// Backward, value gradient, gathered per value band instead of scattered per query: a workgroup
-// owns (image, head, level, 8-channel chunk, band of MSDA_BAND pixels of the level) as a float32
-// tile in LDS, runs over every query of its image, and adds a * w_tap * go into the tile for each
-// tap that falls in its band (LDS atomics); then writes the tile once.  Every element of the
-// value gradient belongs to exactly one workgroup: plain stores, no memset, no global atomics
-// (grid_sample's backward scatters with global atomics; at the C2 shape those were 2.5 GB of
-// atomic traffic per call).  Thread = (query, channel pair); 128 queries per pass, 8 waves per
-// workgroup (the tile is the only LDS user: one workgroup per CU, so it brings its own waves);
-// each thread keeps the loads of 4 queries in flight (the scan is latency-bound: per query 48
-// scattered bytes of locations / weights / gradient).
-constexpr int MSDA_C = 8;                                         // channels per workgroup
-constexpr int MSDA_BAND = 163840 / (MSDA_C * (int)sizeof(float));  // pixels per LDS tile (160 KiB)
-
-struct MsdaBands {
-  int nb[MSDA_MAX_L];     // bands per level
-  int first[MSDA_MAX_L];  // first work index of the level (levels in order, largest first in grid)
-};
-
-template <typename T, int D>
-__global__ __launch_bounds__(512) void k_msda_bwd_value(MsdaLevels lv, MsdaBands bd, int S, int Q, int NH, int P,
-                                                        const float* __restrict__ loc, const float* __restrict__ attw,
-                                                        const T* __restrict__ gout, int BNH, int vec4,
-                                                        float* __restrict__ gvalue) {
-  extern __shared__ float tile[];  // [band px][MSDA_C]
-  constexpr int NCH = D / MSDA_C;
-  // work index -> (level, band, chunk, b * NH + h); within a level: bh fastest
-  int w = blockIdx.x, l = 0;
-  while (l + 1 < lv.L && w >= bd.first[l + 1]) ++l;
-  w -= bd.first[l];
-  const int bh = w % BNH;
-  const int chunk = (w / BNH) % NCH;
-  const int band = w / (BNH * NCH);
-  const int h = bh % NH, b = bh / NH;
-  const int H = lv.H[l], W = lv.W[l], HW = H * W;
-  const int lo = band * MSDA_BAND, hi = min(HW, lo + MSDA_BAND), n = hi - lo;
-  for (int i = threadIdx.x; i < n * MSDA_C; i += 512) tile[i] = 0.f;
-  __syncthreads();
-  const int cp = threadIdx.x & 3;  // channel pair 2cp, 2cp+1 of the chunk
-  const int c0 = chunk * MSDA_C + 2 * cp;
-  auto add_point = [&](float lx, float ly, float a, float g0, float g1) {
-    const Tap t = msda_tap(lx, ly, H, W);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int ix = t.idx[e] - lo;
-      if (t.idx[e] >= 0 && ix >= 0 && ix < n) {
-        const float f = a * t.w[e];
-        atomicAdd(&tile[ix * MSDA_C + 2 * cp], f * g0);
-        atomicAdd(&tile[ix * MSDA_C + 2 * cp + 1], f * g1);
-      }
-    }
-  };
-  constexpr int U = 4;  // queries per thread in flight: their loads issue together (latency-bound)
-  if (vec4) {  // P == 4, locations / weights 16-byte aligned
-    for (int q0 = threadIdx.x >> 2; q0 < Q; q0 += 128 * U) {
-      float4 la[U], lb[U], wa[U];
-      float ga[U], gb[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int q = q0 + 128 * u;
-        if (q < Q) {
-          const long long qh = ((long long)b * Q + q) * NH + h;
-          const float* lq = loc + (qh * lv.L + l) * 8;  // 4 points x (x, y): 32 B, 32-B aligned
-          la[u] = *reinterpret_cast<const float4*>(lq);
-          lb[u] = *reinterpret_cast<const float4*>(lq + 4);
-          wa[u] = *reinterpret_cast<const float4*>(attw + (qh * lv.L + l) * 4);
-          ga[u] = Num<T>::to_f(gout[qh * D + c0]);
-          gb[u] = Num<T>::to_f(gout[qh * D + c0 + 1]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (q0 + 128 * u >= Q) break;
-        add_point(la[u].x, la[u].y, wa[u].x, ga[u], gb[u]);
-        add_point(la[u].z, la[u].w, wa[u].y, ga[u], gb[u]);
-        add_point(lb[u].x, lb[u].y, wa[u].z, ga[u], gb[u]);
-        add_point(lb[u].z, lb[u].w, wa[u].w, ga[u], gb[u]);
-      }
-    }
-  } else {
-    for (int q = threadIdx.x >> 2; q < Q; q += 128) {
-      const long long qh = ((long long)b * Q + q) * NH + h;
-      const float* lq = loc + (qh * lv.L + l) * P * 2;
-      const float* wq = attw + (qh * lv.L + l) * P;
-      const float g0 = Num<T>::to_f(gout[qh * D + c0]), g1 = Num<T>::to_f(gout[qh * D + c0 + 1]);
-      for (int p = 0; p < P; ++p) add_point(lq[2 * p], lq[2 * p + 1], wq[p], g0, g1);
-    }
-  }
-  __syncthreads();
-  float* gv = gvalue + (((long long)b * S + lv.start[l] + lo) * NH + h) * D + chunk * MSDA_C;
-  for (int i = threadIdx.x; i < n * 2; i += 512) {  // 16 B (4 channels) per store
-    const int px = i >> 1, half = i & 1;
-    *reinterpret_cast<float4*>(gv + (long long)px * NH * D + 4 * half) =
-        *reinterpret_cast<const float4*>(&tile[px * MSDA_C + 4 * half]);
   }
 }
 
@@ -319,23 +218,11 @@ template <typename T, int D>
 int launch_bwd(const void* value, const MsdaLevels& lv, int B, int S, int Q, int NH, int P, const float* loc,
                const float* attw, const void* gout, float* gvalue, float* gloc, float* gattw, hipStream_t s) {
   const long long nqh = (long long)B * Q * NH;
-  k_msda_bwd_query<T, D><<<(unsigned)ceil_div(nqh, 256 / (D / 8)), 256, 0, s>>>(
-      (const T*)value, lv, S, Q, NH, P, loc, attw, (const T*)gout, nqh, gloc, gattw);
-  MsdaBands bd;
-  int work = 0, max_px = 0;
-  for (int l = 0; l < lv.L; ++l) {
-    const int hw = lv.H[l] * lv.W[l];
-    bd.nb[l] = (hw + MSDA_BAND - 1) / MSDA_BAND;
-    bd.first[l] = work;
-    work += bd.nb[l] * (D / MSDA_C) * B * NH;
-    max_px = std::max(max_px, std::min(hw, MSDA_BAND));
-  }
-  const size_t lds = (size_t)max_px * MSDA_C * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute((const void*)k_msda_bwd_value<T, D>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  if (attr != hipSuccess) return (int)attr;
-  const int vec4 = P == 4 && ((uintptr_t)loc & 15) == 0 && ((uintptr_t)attw & 15) == 0;
-  k_msda_bwd_value<T, D><<<work, 512, lds, s>>>(lv, bd, S, Q, NH, P, loc, attw, (const T*)gout, B * NH, vec4, gvalue);
+  // the value gradient is accumulated with atomics: zero it first (stream-ordered)
+  const hipError_t e = hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * NH * D, s);
+  if (e != hipSuccess) return (int)e;
+  k_msda_bwd<T, D><<<(unsigned)ceil_div(nqh, 256 / D), 256, 0, s>>>((const T*)value, lv, S, Q, NH, P, loc, attw,
+                                                                   (const T*)gout, nqh, gvalue, gloc, gattw);
   return RGBD_OK;
 }
 

@@ -18,8 +18,7 @@ CASES = [
     (1, [(16, 12)], 2, 16, 2, 33),
     # queries = value pixels (the encoder case)
     (2, [(30, 40), (15, 20), (8, 10)], 8, 32, 4, 1580),
-    # the C5 (1280x720) first level, 90 x 160 = 14 400 pixels: the value gradient's LDS tiles
-    # cover it in three bands
+    # the C5 (1280x720) pixel decoder's first two levels (90 x 160, 45 x 80)
     (1, [(90, 160), (45, 80)], 2, 32, 2, 700),
 ]
 
