@@ -363,7 +363,8 @@ int rgbd_mask_attention(int dtype, const void* logits, int B, int Q, int H, int 
  * P = softmax(S), out = P v.  Sequence-major, as the module's projections lay them out:
  * q [Q][BH][head_dim], k / v [L][BH][head_dim], out [Q][BH][head_dim], lse [Q][BH] (log-sum-exp
  * of the masked scaled scores, saved for the backward); mask bool bytes [BH][Q][L] (1 = not
- * allowed).  head_dim == 32.  A fully masked row gives NaN, as torch's softmax does.
+ * allowed; NULL = no mask: the decoder layers' self-attention, Mask2FormerAttention :1525-1570).
+ * head_dim == 32.  A fully masked row gives NaN, as torch's softmax does.
  * ws: rgbd_masked_attn_fwd_workspace_size(BH, Q, L) bytes (per-key-split partials).
  * rgbd_masked_attn_bwd: dq, dk, dv (OVERWRITTEN) from dout; deterministic (no atomics);
  *   ws: rgbd_masked_attn_bwd_workspace_size(BH, Q, L) bytes.
@@ -413,6 +414,62 @@ int rgbd_pack_mask_bits(const uint8_t* masks, int n, long long npx, unsigned lon
                         void* stream);
 int rgbd_mask_intersections(const unsigned long long* a, int na, const unsigned long long* b, int nb, long long npx,
                             int* inter, void* stream);
+
+/* ---------------------------------------------------------------- f1 / f2 dense layers
+ * The nn.Linear layers of the Mask2Former decoder (transformers 5.15 modeling_mask2former.py:
+ * self_attn q/k/v/out_proj :1480-1483, fc1/fc2 :1711-1714), of the pixel decoder's encoder
+ * layers (value_proj / sampling_offsets / attention_weights / output_proj :862-868, fc1/fc2
+ * :1030-1036) and of Swin-T (modeling_swin.py qkv :420-424, output :540, MLP :560/574, patch
+ * merging :344), forward and backward, as one MFMA GEMM family (csrc/gemm.hip):
+ *   C[b][m][n] = act(sum_k op(A)[m][k] op(B)[k][n] + bias[n]) (+ R[b][m][n])
+ *   a_t = 0: A stored [M][lda] (K contiguous); a_t = 1: A stored [K][lda] (M contiguous)
+ *   b_t = 0: B stored [N][ldb] (K contiguous, an nn.Linear weight); b_t = 1: [K][ldb]
+ *   forward Y = X W^T + b: (0, 0); dX = dY W: (0, 1); dW = dY^T X: (1, 1)
+ *   act RGBD_ACT_RELU_GRAD: C = acc where R > 0 else 0 (ReLU backward; bias must be NULL).
+ *   A and B share dtype (RGBD_F32 / RGBD_BF16); C is that dtype, or float32 with c_f32 = 1
+ *   (weight gradients of bf16 GEMMs, autocast's float32 residual streams); R has C's dtype.  bias: float32 [N] or NULL.  batch strides sa / sb / sr / sc
+ *   in elements.  splits > 1: split-K with float32 partials in ws (rgbd_gemm_workspace_size),
+ *   summed in split order (deterministic).  bf16: float32 accumulation; f32: exact f32 MFMA. */
+#define RGBD_ACT_NONE 0
+#define RGBD_ACT_RELU 1
+#define RGBD_ACT_GELU 2
+#define RGBD_ACT_RELU_GRAD 3
+size_t rgbd_gemm_workspace_size(int M, int N, int batch, int splits);
+int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, long long lda, long long sa,
+              const void* B, long long ldb, long long sb, const float* bias, int act, const void* R, long long ldr,
+              long long sr, void* C, long long ldc, long long sc, int c_f32, int batch, int splits, void* ws,
+              void* stream);
+/* rgbd_colsum: out[n] = sum over rows m of y[m * ld + n] (the bias gradient), float32, fixed order. */
+int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* stream);
+/* LayerNorm over the last dimension (nn.LayerNorm(C, eps) of the decoder layers :1700-1719, the
+ * pixel decoder's encoder layers :1022-1040, Swin's layernorm_before / _after :602-640):
+ *   y = (x - mean) * rstd * gamma + beta, mean / rstd float32 [rows] saved for the backward.
+ *   x_dtype / y_dtype: RGBD_F32 or RGBD_BF16 each (under torch.autocast a bf16 input gives a
+ *   float32 output); gamma / beta float32 [C].  Statistics in float32, two passes over the
+ *   register-resident row (C <= 1536).
+ * rgbd_layernorm_bwd: dx = rstd * (g - mean_c(g) - xhat * mean_c(g * xhat)), g = gamma * dy,
+ *   dx in x_dtype; dgamma = sum_rows dy * xhat, dbeta = sum_rows dy, float32 [C] (OVERWRITTEN;
+ *   per-block partials in ws summed in block order: deterministic). */
+int rgbd_layernorm_fwd(int x_dtype, const void* x, const float* gamma, const float* beta, int rows, int C,
+                       float eps, int y_dtype, void* y, float* mean, float* rstd, void* stream);
+size_t rgbd_layernorm_bwd_workspace_size(int rows, int C);
+int rgbd_layernorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy, const float* gamma,
+                       const float* mean, const float* rstd, int rows, int C, void* dx, float* dgamma,
+                       float* dbeta, void* ws, void* stream);
+
+/* ---------------------------------------------------------------- f2 Swin-T window attention
+ * The (shifted-)window self-attention core of every SwinLayer of the backbone
+ * (transformers 5.15 modeling_swin.py SwinLayer.forward :529-582 with SwinAttention :418-468):
+ * pad to multiples of the window, roll by -shift, 7x7 windows, softmax(q k^T * scale +
+ * relative-position bias + shift mask (-100)) v, un-window, roll back, crop — by index
+ * arithmetic on the original token layout.  q / k / v: dtype rows [B*H*W][ldq] (head h at
+ * columns 32 h .. 32 h + 31; ldq = 3C when one GEMM produced all three), the projections of
+ * the LayerNorm'ed map; bq / bk / bv float32 [C] (the projections of the zero padding rows; may
+ * be NULL); table float32 [169][heads] (relative_position_bias_table); out dtype [B*H*W][ldo].
+ * window == 7, 0 <= shift < 7, head_dim 32; rows 16-byte aligned. */
+int rgbd_swin_window_attn(int dtype, const void* q, const void* k, const void* v, long long ldq, const float* bq,
+                          const float* bk, const float* bv, const float* table, int B, int H, int W, int heads,
+                          int window, int shift, float scale, void* out, long long ldo, void* stream);
 
 /* ---------------------------------------------------------------- kernel timing (bench only)
  * When enabled, launch functions bracket their main kernel with hipEvents recorded on the

@@ -87,6 +87,15 @@ SIGNATURES = {
     "rgbd_masked_attn_bwd_workspace_size": (_SZ, [_I, _I, _I]),
     "rgbd_masked_attn_bwd": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.c_float, _P, _P, _P, _P,
                                   _P]),
+    "rgbd_gemm_workspace_size": (_SZ, [_I, _I, _I, _I]),
+    "rgbd_gemm": (_I, [_I, _I, _I, _I, _I, _I, _P, _LL, _LL, _P, _LL, _LL, _P, _I, _P, _LL, _LL, _P, _LL, _LL, _I,
+                       _I, _I, _P, _P]),
+    "rgbd_colsum": (_I, [_I, _P, _I, _I, _LL, _P, _P]),
+    "rgbd_layernorm_fwd": (_I, [_I, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P]),
+    "rgbd_layernorm_bwd_workspace_size": (_SZ, [_I, _I]),
+    "rgbd_layernorm_bwd": (_I, [_I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "rgbd_swin_window_attn": (_I, [_I, _P, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
+                                   _LL, _P]),
     "rgbd_timing_enable": (_I, [_I]),
     "rgbd_timing_read": (ctypes.c_double, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "rgbd_ratio_packed_size": (_SZ, [_I]),

@@ -1,0 +1,445 @@
+// f1 / f2: the dense layers of the Mask2Former decoder, pixel decoder and Swin
+// backbone — nn.Linear forward and backward — as one MFMA GEMM family with fused epilogues.
+//
+// Reference call sites (transformers 5.15 modeling_mask2former.py / modeling_swin.py):
+//   decoder layer   self_attn q/k/v/out_proj (:1480-1483), fc1 -> relu -> fc2 (:1711-1714)
+//   pixel decoder   value_proj / sampling_offsets / attention_weights / output_proj
+//                   (:862-868), fc1 -> relu -> fc2 of each encoder layer (:1030-1036)
+//   Swin-T          qkv (query/key/value), attention output dense, intermediate dense -> gelu,
+//                   output dense, patch-merging reduction (modeling_swin.py:420-424, 540, 560,
+//                   574, 344)
+//
+// C[M][N] = act(sum_k op(A)[m][k] op(B)[k][n] + bias[n]) (+ R[m][n]), batched, with
+//   A: a_t = 0 -> stored [M][lda] (K contiguous: activations); a_t = 1 -> [K][lda] (M
+//      contiguous: dY^T of a weight gradient)
+//   B: b_t = 0 -> stored [N][ldb] (K contiguous: nn.Linear's weight); b_t = 1 -> [K][ldb]
+//      (N contiguous: the weight in dX = dY W, the activations in dW = dY^T X)
+// so the three GEMMs of a linear layer are (a_t, b_t) = (0, 0) forward, (0, 1) dX, (1, 1) dW.
+//
+// Tiling: 256 threads = 4 waves, workgroup tile TM x TN (128 x 128 or 64 x 64), wave tile
+// (TM/2) x (TN/2) of 16x16 MFMA fragments, K staged per 128-byte step (64 bf16 / 32 f32) into
+// double-buffered LDS through registers (the next step's 16-byte global loads are in flight
+// during the current step's MFMAs; one barrier per step).  K-contiguous tiles are [rows][128 B]
+// with 16-byte chunk c at slot c ^ (row & 7); M/N-contiguous tiles are [k][rows] read back
+// k-major with ds_read_b64_tr_b16 (bf16, 32-byte blocks XOR-swizzled by row bits 0-1 and 3)
+// or ds_read_b32 (f32, 64-byte blocks swizzled by row bit 3) — the layouts of mask_predict.hip.
+// The MFMA's A operand is the N side and its B operand the M side, so a lane's four accumulator
+// registers are four consecutive n of one row m: 8-byte (bf16) / 16-byte (f32) stores.
+// bf16: v_mfma_f32_16x16x32_bf16, float32 sums; f32: v_mfma_f32_16x16x4_f32 (exact products).
+// Split-K (splits > 1): per split a float32 partial tile into the workspace, then one pass sums
+// the splits in order (deterministic) and applies the epilogue.
+#include "common.hpp"
+#include "mfma.hpp"
+
+#include <algorithm>
+
+namespace rgbd {
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short g_v4s;
+
+constexpr int G_THREADS = 256;
+
+template <typename T> struct GCfg;
+template <> struct GCfg<bf16_t> {
+  static constexpr int KS = 64;    // K elements per stage (128 bytes)
+  static constexpr int VEC = 8;    // elements per 16-byte chunk
+  static constexpr int TROW = 256; // bytes per k row of an M/N-contiguous tile (128 elements)
+  static __device__ __forceinline__ int toff(int row, int byte) {
+    const int swz = (row & 3) | (((row >> 3) & 1) << 2);
+    return row * TROW + (((byte >> 5) ^ swz) << 5) + (byte & 31);
+  }
+};
+template <> struct GCfg<float> {
+  static constexpr int KS = 32;
+  static constexpr int VEC = 4;
+  static constexpr int TROW = 512;
+  static __device__ __forceinline__ int toff(int row, int byte) {
+    return row * TROW + (((byte >> 6) ^ ((row >> 3) & 1)) << 6) + (byte & 63);
+  }
+};
+
+__device__ __forceinline__ int koff(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
+
+// fragment i (rows 16i..16i+15 of the tile) of k-step ks from a K-contiguous tile
+__device__ __forceinline__ Frag<bf16_t> frag_k(const char* s, int i, int ks, int lane) {
+  const int row = 16 * i + (lane & 15), g = lane >> 4;
+  Frag<bf16_t> f;
+  f.v = *reinterpret_cast<const uint4*>(s + koff(row, 4 * ks + g));
+  return f;
+}
+__device__ __forceinline__ Frag<float> frag_k_f32(const char* s, int i, int lane) {
+  const int row = 16 * i + (lane & 15), g = lane >> 4;
+  Frag<float> f;
+  f.lo = *reinterpret_cast<const float4*>(s + koff(row, 2 * g));
+  f.hi = *reinterpret_cast<const float4*>(s + koff(row, 2 * g + 1));
+  return f;
+}
+// the same fragment from an M/N-contiguous tile [k][rows] (transposed reads)
+__device__ __forceinline__ Frag<bf16_t> frag_t(const char* s, int i, int ks, int lane) {
+  using Cfg = GCfg<bf16_t>;
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int row0 = 32 * ks + 8 * g + q4, row1 = row0 + 4;
+  const int byte = (16 * i + 4 * p4) * 2;
+  g_v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) g_v4s*)(s + Cfg::toff(row0, byte)));
+  g_v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) g_v4s*)(s + Cfg::toff(row1, byte)));
+  Frag<bf16_t> f;
+  f.v = make_uint4((uint32_t)(uint16_t)t0.x | ((uint32_t)(uint16_t)t0.y << 16),
+                   (uint32_t)(uint16_t)t0.z | ((uint32_t)(uint16_t)t0.w << 16),
+                   (uint32_t)(uint16_t)t1.x | ((uint32_t)(uint16_t)t1.y << 16),
+                   (uint32_t)(uint16_t)t1.z | ((uint32_t)(uint16_t)t1.w << 16));
+  return f;
+}
+__device__ __forceinline__ Frag<float> frag_t_f32(const char* s, int i, int lane) {
+  using Cfg = GCfg<float>;
+  const int r = lane & 15, g = lane >> 4;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(s + Cfg::toff(8 * g + j, (16 * i + r) * 4));
+  Frag<float> f;
+  f.from8(v);
+  return f;
+}
+
+// One operand's stage: ROWS (M or N) x KS (K) elements through registers into LDS.
+// KC: stored [row][ld] with K contiguous; else [k][ld] with the rows contiguous.
+template <typename T, bool KC, int ROWS>
+struct GStage {
+  using Cfg = GCfg<T>;
+  static constexpr int KS = Cfg::KS, VEC = Cfg::VEC;
+  static constexpr int CHUNKS = ROWS * KS / VEC;             // 16-byte chunks per stage
+  static constexpr int PER = (CHUNKS + G_THREADS - 1) / G_THREADS;
+  static constexpr int CPR = KC ? KS / VEC : ROWS / VEC;     // chunks per stored row
+  uint4 v[PER];
+
+  // rows [row0, row0 + ROWS) of nrows, k [k0, k0 + KS) of klim; vec: 16-byte loads allowed
+  __device__ __forceinline__ void load(const T* __restrict__ base, long long ld, int row0, int nrows, int k0,
+                                       int klim, bool vec, int tid) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + G_THREADS * u;
+      v[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (CHUNKS % G_THREADS != 0 && c >= CHUNKS) continue;
+      const int major = c / CPR, minor = (c % CPR) * VEC;
+      const int row = KC ? row0 + major : row0 + minor;  // first row of the chunk
+      const int k = KC ? k0 + minor : k0 + major;        // first k of the chunk
+      const T* src = KC ? base + (long long)row * ld + k : base + (long long)k * ld + row;
+      if (vec) {
+        if (KC ? (row < nrows && k < klim) : (k < klim && row < nrows)) v[u] = *reinterpret_cast<const uint4*>(src);
+      } else {
+        T e[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const bool ok = KC ? (row < nrows && k + j < klim) : (k < klim && row + j < nrows);
+          e[j] = ok ? src[j] : T(0);
+        }
+        __builtin_memcpy(&v[u], e, 16);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* s, int tid) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + G_THREADS * u;
+      if (CHUNKS % G_THREADS != 0 && c >= CHUNKS) continue;
+      const int major = c / CPR, minor = c % CPR;
+      if (KC)
+        *reinterpret_cast<uint4*>(s + koff(major, minor)) = v[u];
+      else
+        *reinterpret_cast<uint4*>(s + Cfg::toff(major, minor * 16)) = v[u];
+    }
+  }
+  static constexpr int bytes() { return KC ? ROWS * 128 : KS * Cfg::TROW; }
+};
+
+template <typename T, bool KC>
+__device__ __forceinline__ Frag<T> gfrag(const char* s, int i, int ks, int lane) {
+  if constexpr (sizeof(T) == 2)
+    return KC ? frag_k(s, i, ks, lane) : frag_t(s, i, ks, lane);
+  else
+    return KC ? frag_k_f32(s, i, lane) : frag_t_f32(s, i, lane);
+}
+
+struct GArgs {
+  int M, N, K;
+  const void* A;
+  long long lda, sa;
+  const void* B;
+  long long ldb, sb;
+  const float* bias;
+  int act;
+  const void* R;
+  long long ldr, sr;
+  void* C;
+  long long ldc, sc;
+  int c_f32;
+  int splits, kchunk;
+  float* part;  // split-K partials [batch*splits][M][N]
+  int vec_a, vec_b;
+};
+
+__device__ __forceinline__ float g_act(float v, int act) {
+  if (act == RGBD_ACT_RELU) return fmaxf(v, 0.f);
+  if (act == RGBD_ACT_GELU) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  return v;
+}
+
+// R in C's dtype: float32 when C is written as float32, else the operand dtype
+template <typename T>
+__device__ __forceinline__ float g_r(const GArgs& a, long long ridx) {
+  return a.c_f32 ? reinterpret_cast<const float*>(a.R)[ridx] : Num<T>::to_f(reinterpret_cast<const T*>(a.R)[ridx]);
+}
+
+// epilogue of one value: act(v + bias) (+ R) | v * (R > 0)
+template <typename T>
+__device__ __forceinline__ float g_epi(float v, int n, long long ridx, const GArgs& a) {
+  if (a.act == RGBD_ACT_RELU_GRAD) return g_r<T>(a, ridx) > 0.f ? v : 0.f;
+  if (a.bias) v += a.bias[n];
+  v = g_act(v, a.act);
+  if (a.R) v += g_r<T>(a, ridx);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void g_store(const GArgs& a, int bz, int m, int n0, const float (&v)[4]) {
+  // four consecutive n of row m
+  if (a.c_f32) {
+    float* c = reinterpret_cast<float*>(a.C) + (long long)bz * a.sc + (long long)m * a.ldc + n0;
+    if (n0 + 3 < a.N && ((a.ldc | n0) & 3) == 0 && (((uintptr_t)a.C) & 15) == 0 && (a.sc & 3) == 0)
+      *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+    else
+      for (int e = 0; e < 4; ++e)
+        if (n0 + e < a.N) c[e] = v[e];
+  } else {
+    T* c = reinterpret_cast<T*>(a.C) + (long long)bz * a.sc + (long long)m * a.ldc + n0;
+    if constexpr (sizeof(T) == 2) {
+      if (n0 + 3 < a.N && ((a.ldc | n0) & 3) == 0 && (((uintptr_t)a.C) & 7) == 0 && (a.sc & 3) == 0) {
+        *reinterpret_cast<uint2*>(c) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        return;
+      }
+    }
+    for (int e = 0; e < 4; ++e)
+      if (n0 + e < a.N) c[e] = Num<T>::from_f(v[e]);
+  }
+}
+
+template <typename T, int TM, int TN, bool AT, bool BT>
+__global__ __launch_bounds__(G_THREADS) void k_gemm(GArgs a) {
+  using Cfg = GCfg<T>;
+  constexpr int KS = Cfg::KS;
+  using SA = GStage<T, !AT, TM>;
+  using SB = GStage<T, !BT, TN>;
+  constexpr int A_BYTES = SA::bytes(), B_BYTES = SB::bytes();
+  constexpr int FM = TM / 32, FN = TN / 32;  // fragments per wave (2 x 2 waves)
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int n_base = blockIdx.x * TN, m_base = blockIdx.y * TM;
+  const int bz = blockIdx.z, b = bz / a.splits, sp = bz % a.splits;
+  const int kbeg = sp * a.kchunk, kend = min(a.K, kbeg + a.kchunk);
+  const T* Ab = reinterpret_cast<const T*>(a.A) + (long long)b * a.sa;
+  const T* Bb = reinterpret_cast<const T*>(a.B) + (long long)b * a.sb;
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  SA sa;
+  SB sb;
+  const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
+  if (nk > 0) {
+    sa.load(Ab, a.lda, m_base, a.M, kbeg, kend, a.vec_a, tid);
+    sb.load(Bb, a.ldb, n_base, a.N, kbeg, kend, a.vec_b, tid);
+    sa.store(smem, tid);
+    sb.store(smem + A_BYTES, tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * KS;
+      sa.load(Ab, a.lda, m_base, a.M, k0, kend, a.vec_a, tid);
+      sb.load(Bb, a.ldb, n_base, a.N, k0, kend, a.vec_b, tid);
+    }
+    const char* s_a = smem + buf * (A_BYTES + B_BYTES);
+    const char* s_b = s_a + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < KS / 32; ++ks) {
+      Frag<T> fm[FM], fn[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fm[i] = gfrag<T, !AT>(s_a, wm * FM + i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fn[j] = gfrag<T, !BT>(s_b, wn * FN + j, ks, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i) mma(acc[j][i], fn[j], fm[i]);
+    }
+    if (more) {
+      char* d = smem + (buf ^ 1) * (A_BYTES + B_BYTES);
+      sa.store(d, tid);
+      sb.store(d + A_BYTES, tid);
+    }
+    __syncthreads();
+  }
+
+  // lane (r, g): acc[j][i][e] = C[m = 16 (wm FM + i) + r][n = 16 (wn FN + j) + 4 g + e]
+  const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m_base + 16 * (wm * FM + i) + r;
+    if (m >= a.M) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n0 = n_base + 16 * (wn * FN + j) + 4 * g;
+      if (n0 >= a.N) continue;
+      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
+      if (a.splits > 1) {
+        float* p = a.part + ((long long)bz * a.M + m) * a.N + n0;
+        if (n0 + 3 < a.N && (a.N & 3) == 0)
+          *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+        else
+          for (int e = 0; e < 4; ++e)
+            if (n0 + e < a.N) p[e] = v[e];
+        continue;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n0 + e < a.N) v[e] = g_epi<T>(v[e], n0 + e, (long long)b * a.sr + (long long)m * a.ldr + n0 + e, a);
+      g_store<T>(a, b, m, n0, v);
+    }
+  }
+}
+
+// split-K reduction (splits summed in order) + epilogue; thread = 4 consecutive n
+template <typename T>
+__global__ __launch_bounds__(256) void k_gemm_splitk_reduce(GArgs a, int batch) {
+  const long long quads_per_row = (a.N + 3) / 4;
+  const long long total = (long long)batch * a.M * quads_per_row;
+  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int b = (int)(t / ((long long)a.M * quads_per_row));
+    const long long rem = t % ((long long)a.M * quads_per_row);
+    const int m = (int)(rem / quads_per_row), n0 = (int)(rem % quads_per_row) * 4;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < a.splits; ++s) {
+      const float* p = a.part + (((long long)b * a.splits + s) * a.M + m) * a.N + n0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n0 + e < a.N) v[e] += p[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (n0 + e < a.N) v[e] = g_epi<T>(v[e], n0 + e, (long long)b * a.sr + (long long)m * a.ldr + n0 + e, a);
+    g_store<T>(a, b, m, n0, v);
+  }
+}
+
+// bias gradient: out[n] = sum_m dY[b][m][n] over batch and rows, float32, fixed order.
+// block = 64 columns x 4 row groups; the row groups fold in a fixed order through LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int rows, int N, long long ld, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < N)
+    for (int m = rg; m < rows; m += 4) s += Num<T>::to_f(y[(long long)m * ld + c]);
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < N) out[c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+template <typename T, int TM, int TN, bool AT, bool BT>
+void launch_t(const GArgs& a, int batch, hipStream_t s) {
+  dim3 grid(ceil_div(a.N, TN), ceil_div(a.M, TM), batch * a.splits);
+  hipLaunchKernelGGL((k_gemm<T, TM, TN, AT, BT>), grid, dim3(G_THREADS), 0, s, a);
+}
+
+template <typename T, int TM, int TN>
+void launch_layout(const GArgs& a, int at, int bt, int batch, hipStream_t s) {
+  if (!at && !bt) launch_t<T, TM, TN, false, false>(a, batch, s);
+  else if (!at && bt) launch_t<T, TM, TN, false, true>(a, batch, s);
+  else if (at && !bt) launch_t<T, TM, TN, true, false>(a, batch, s);
+  else launch_t<T, TM, TN, true, true>(a, batch, s);
+}
+
+template <typename T>
+int gemm_t(GArgs a, int at, int bt, int batch, hipStream_t s) {
+  // 128 x 128 tiles when they give the chip enough workgroups, else 64 x 64
+  const long long big = (long long)ceil_div(a.N, 128) * ceil_div(a.M, 128) * batch * a.splits;
+  if (big >= 256)
+    launch_layout<T, 128, 128>(a, at, bt, batch, s);
+  else
+    launch_layout<T, 64, 64>(a, at, bt, batch, s);
+  RGBD_CHECK_LAUNCH();
+  if (a.splits > 1) {
+    const long long quads = (long long)batch * a.M * ((a.N + 3) / 4);
+    const int blocks = (int)std::min<long long>((quads + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_gemm_splitk_reduce<T>, dim3(blocks), dim3(256), 0, s, a, batch);
+    RGBD_CHECK_LAUNCH();
+  }
+  return RGBD_OK;
+}
+
+}  // namespace
+}  // namespace rgbd
+
+using namespace rgbd;
+
+extern "C" {
+
+size_t rgbd_gemm_workspace_size(int M, int N, int batch, int splits) {
+  if (splits <= 1) return 0;
+  return (size_t)batch * splits * M * N * sizeof(float);
+}
+
+int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, long long lda, long long sa,
+              const void* B, long long ldb, long long sb, const float* bias, int act, const void* R, long long ldr,
+              long long sr, void* C, long long ldc, long long sc, int c_f32, int batch, int splits, void* ws,
+              void* stream) {
+  RGBD_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && splits > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_ARG);
+  RGBD_REQUIRE(act >= RGBD_ACT_NONE && act <= RGBD_ACT_RELU_GRAD, RGBD_E_ARG);
+  RGBD_REQUIRE(act != RGBD_ACT_RELU_GRAD || (R && !bias), RGBD_E_ARG);
+  RGBD_REQUIRE(splits == 1 || ws, RGBD_E_ARG);
+  RGBD_REQUIRE(lda >= (a_t ? M : K) && ldb >= (b_t ? N : K) && ldc >= N && (!R || ldr >= N), RGBD_E_SHAPE);
+  const int esz = dtype == RGBD_BF16 ? 2 : 4, vec = 16 / esz;
+  const int ks = dtype == RGBD_BF16 ? 64 : 32;
+  GArgs a;
+  a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda = lda; a.sa = sa;
+  a.B = B; a.ldb = ldb; a.sb = sb;
+  a.bias = bias; a.act = act;
+  a.R = R; a.ldr = ldr; a.sr = sr;
+  a.C = C; a.ldc = ldc; a.sc = sc; a.c_f32 = c_f32 || dtype == RGBD_F32;
+  a.splits = splits;
+  a.kchunk = ((K + splits - 1) / splits + ks - 1) / ks * ks;
+  a.part = (float*)ws;
+  // 16-byte loads: the contiguous extent, the leading dimension, the batch stride and the base
+  // all multiples of 16 bytes
+  auto vec_ok = [&](const void* p, long long ld, long long st, int extent) {
+    return (((uintptr_t)p) & 15) == 0 && ld % vec == 0 && (batch == 1 || st % vec == 0) && extent % vec == 0;
+  };
+  a.vec_a = vec_ok(A, lda, sa, a_t ? M : K);
+  a.vec_b = vec_ok(B, ldb, sb, b_t ? N : K);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_BF16) return gemm_t<bf16_t>(a, a_t, b_t, batch, s);
+  return gemm_t<float>(a, a_t, b_t, batch, s);
+}
+
+int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* stream) {
+  RGBD_REQUIRE(y && out && rows > 0 && N > 0 && ld >= N, RGBD_E_ARG);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(ceil_div(N, 64));
+  if (dtype == RGBD_BF16)
+    hipLaunchKernelGGL(k_colsum<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)y, rows, N, ld, out);
+  else
+    hipLaunchKernelGGL(k_colsum<float>, grid, dim3(256), 0, s, (const float*)y, rows, N, ld, out);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+}  // extern "C"

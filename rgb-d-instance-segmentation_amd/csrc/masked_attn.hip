@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs<T> a) {
   f4m o[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
   float m = -INFINITY, lsum = 0.f;
   const int kb = split * a.span, ke = min(a.L, kb + a.span);
-  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  const uint8_t* mrow = a.mask ? a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L : nullptr;
   KVTile nxt;
   if (kb < ke) kv_load(nxt, a.k, a.v, kb, ke, a.BH, bh, tid);
   for (int k0 = kb; k0 < ke; k0 += 64) {
@@ -138,7 +138,9 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs<T> a) {
       // this lane's 4 keys: k0 + r0 + lg*4 + i, query qrow
       const int kbase = k0 + r0 + lg * 4;
       uint32_t mb = 0;
-      if (a.vec_mask && kbase + 4 <= ke) {
+      if (!a.mask) {
+        // no mask (the decoder's self-attention): only keys past the range are excluded
+      } else if (a.vec_mask && kbase + 4 <= ke) {
         mb = *reinterpret_cast<const uint32_t*>(mrow + kbase);
       } else {
 #pragma unroll
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs<T> a) {
   }
   f4v dv[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
   f4v dk[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
-  const uint8_t* mcol = a.mask + (long long)bh * a.Q * a.L + (kv ? keyl : 0);
+  const uint8_t* mcol = a.mask ? a.mask + (long long)bh * a.Q * a.L + (kv ? keyl : 0) : nullptr;
   for (int qb0 = 0; qb0 < a.Q; qb0 += QB) {
     __syncthreads();
     for (int i = tid; i < QB * HD; i += 256) {
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs<T> a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int rr = r0 + lg * 4 + i, qq = qb0 + rr;
-        const bool masked = !kv || qq >= a.Q || mcol[(long long)(qq < a.Q ? qq : 0) * a.L];
+        const bool masked = !kv || qq >= a.Q || (mcol && mcol[(long long)(qq < a.Q ? qq : 0) * a.L]);
         p[i] = masked ? 0.f : expf(S[i] - slse[rr]);
         ds[i] = p[i] * (DP[i] - sdel[rr]);
       }
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs<T> a) {
   const float del = qv ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
   f4m g[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
   const int kb = split * a.span, ke = min(a.L, kb + a.span);
-  const uint8_t* mrow = a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L;
+  const uint8_t* mrow = a.mask ? a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L : nullptr;
   KVTile nxt;
   if (kb < ke) kv_load(nxt, a.k, a.v, kb, ke, a.BH, bh, tid);
   for (int k0 = kb; k0 < ke; k0 += 64) {
@@ -369,7 +371,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs<T> a) {
       }
       const int kbase = k0 + r0 + lg * 4;
       uint32_t mb = 0;
-      if (a.vec_mask && kbase + 4 <= ke) {
+      if (!a.mask) {
+        // no mask (the decoder's self-attention): only keys past the range are excluded
+      } else if (a.vec_mask && kbase + 4 <= ke) {
         mb = *reinterpret_cast<const uint32_t*>(mrow + kbase);
       } else {
 #pragma unroll
@@ -434,7 +438,7 @@ int attn_bwd(const void* q, const void* k, const void* v, const uint8_t* mask, c
 
 size_t attn_align(size_t x) { return (x + 255) / 256 * 256; }
 
-bool mask_vec(const uint8_t* mask, int L) { return (L % 16) == 0 && ((uintptr_t)mask % 16) == 0; }
+bool mask_vec(const uint8_t* mask, int L) { return mask && (L % 16) == 0 && ((uintptr_t)mask % 16) == 0; }
 
 template <typename T>
 int attn_fwd(const void* q, const void* k, const void* v, const uint8_t* mask, int BH, int Q, int L, float scale,
@@ -485,7 +489,7 @@ size_t rgbd_masked_attn_fwd_workspace_size(int BH, int Q, int L) {
 
 int rgbd_masked_attn_fwd(int dtype, const void* q, const void* k, const void* v, const uint8_t* mask, int BH, int Q,
                          int L, int head_dim, float scale, void* out, float* lse, void* ws, void* stream) {
-  RGBD_REQUIRE(q && k && v && mask && out && lse && ws && BH > 0 && Q > 0 && L > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(q && k && v && out && lse && ws && BH > 0 && Q > 0 && L > 0, RGBD_E_ARG);
   RGBD_REQUIRE(attn_shape_ok(q, k, v, BH, Q, L, head_dim) && ((uintptr_t)out % 16) == 0, RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32) return attn_fwd<float>(q, k, v, mask, BH, Q, L, scale, out, lse, ws, s);
@@ -504,7 +508,7 @@ size_t rgbd_masked_attn_bwd_workspace_size(int BH, int Q, int L) {
 int rgbd_masked_attn_bwd(int dtype, const void* q, const void* k, const void* v, const uint8_t* mask, const void* out,
                          const float* lse, const void* dout, int BH, int Q, int L, int head_dim, float scale,
                          void* dq, void* dk, void* dv, void* ws, void* stream) {
-  RGBD_REQUIRE(q && k && v && mask && out && lse && dout && dq && dk && dv && ws && BH > 0 && Q > 0 && L > 0,
+  RGBD_REQUIRE(q && k && v && out && lse && dout && dq && dk && dv && ws && BH > 0 && Q > 0 && L > 0,
                RGBD_E_ARG);
   RGBD_REQUIRE(attn_shape_ok(q, k, v, BH, Q, L, head_dim) && ((uintptr_t)dout % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
                    ((uintptr_t)dk % 16) == 0 && ((uintptr_t)dv % 16) == 0,

@@ -1,0 +1,379 @@
+"""f1 / f2: the dense layers around the HIP attention cores — nn.Linear, the
+fc1 -> ReLU -> fc2 feed-forward blocks and nn.LayerNorm — on the HIP GEMM / LayerNorm kernels
+(csrc/gemm.hip, csrc/layernorm.hip), forward and backward.
+
+Reference call sites (transformers 5.15, the modules the reference model instantiates through
+``CustomMask2FormerForUniversalSegmentation``, custom_model.py:37-53):
+  * masked-attention decoder layer ``Mask2FormerMaskedAttentionDecoderLayer.forward_post``
+    (modeling_mask2former.py:1627-1683): cross-attention projections, self-attention
+    (``Mask2FormerAttention`` :1487-1585, no mask: the HIP attention core with a NULL mask),
+    fc1 -> relu -> fc2, three post-norm LayerNorms;
+  * pixel decoder encoder layer ``Mask2FormerPixelDecoderEncoderLayer.forward`` (:1036-1102):
+    deformable-attention projections, fc1 -> relu -> fc2, two LayerNorms;
+  * Swin-T (modeling_swin.py): every nn.Linear / nn.LayerNorm of the backbone (forward only in
+    v0.4.0: the reference detaches the colour features, custom_model.py:332-333).
+
+Precision follows the module being replaced: float32 inputs run the exact-f32 MFMA GEMMs; under
+torch.autocast(bfloat16) the GEMMs take bf16 operands (activations cast, weights cast once per
+weight version) with float32 sums and a bf16 output — what autocast's linear returns — and
+LayerNorm returns float32, as autocast's layer_norm does.  Weight gradients are written in
+float32 straight from the bf16 GEMM (autocast's path rounds them to bf16 first).
+
+``install(model)`` swaps module classes in place (parameters and state_dict keys unchanged):
+nn.Linear -> HipLinear, nn.LayerNorm -> HipLayerNorm, the decoder and pixel-decoder encoder
+layers -> classes whose forward fuses the ReLU into fc1's epilogue and its gradient into
+fc2's dX epilogue.  Inputs the kernels do not cover (CPU tensors, float16, LayerNorm width
+> 1536, dropout in training, GELU with gradients) take the module's own torch path.
+"""
+import math
+import weakref
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib
+from ._lib import RGBD_BF16, RGBD_F32, check
+from .ops import _p, _stream, _workspace
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_GRAD = 0, 1, 2, 3
+_CODE = {torch.float32: RGBD_F32, torch.bfloat16: RGBD_BF16}
+
+
+def compute_dtype(x: torch.Tensor):
+    """The dtype a replaced module computes in for input x (None: not covered)."""
+    if torch.is_autocast_enabled("cuda"):
+        return torch.bfloat16 if torch.get_autocast_dtype("cuda") == torch.bfloat16 else None
+    return x.dtype if x.dtype in _CODE else None
+
+
+_wcache = weakref.WeakKeyDictionary()
+
+
+def cast_weight(w: torch.Tensor, dt):
+    """w (a parameter) in dtype dt, cast once per weight version (as autocast's cast cache does
+    within a region); never cached while a graph is being captured."""
+    if w.dtype == dt:
+        return w.detach()
+    if torch.cuda.is_current_stream_capturing():
+        return w.detach().to(dt)
+    ent = _wcache.get(w)
+    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
+        return ent[2]
+    t = w.detach().to(dt)
+    _wcache[w] = (w._version, w.data_ptr(), t)
+    return t
+
+
+def _splits(M, N, K):
+    """split-K count: enough workgroups for the chip when the output tile grid is small."""
+    tiles = math.ceil(M / 128) * math.ceil(N / 128)
+    if tiles >= 256 or K < 1024:
+        return 1
+    return int(max(1, min(16, 256 // max(tiles, 1), K // 512)))
+
+
+def gemm(A, B, a_t, b_t, M, N, K, bias=None, act=ACT_NONE, R=None, c_f32=False, batch=1, sa=0, sb=0, sr=0,
+         out=None):
+    """C [batch][M][N] = act(op(A) op(B) + bias) (+ R) on the HIP GEMM (see rgbd_gemm in
+    include/rgbd_hip.h for a_t / b_t).  A, B (and R) 2-D with unit inner stride (or 3-D batched
+    with the given batch strides); returns C contiguous."""
+    dt = A.dtype
+    c_dt = torch.float32 if (c_f32 or dt == torch.float32) else dt
+    if B.dtype != dt or dt not in _CODE or (R is not None and R.dtype != c_dt):
+        raise TypeError(f"gemm: A / B must share float32 / bfloat16 and R must have C's dtype, got {A.dtype}, "
+                        f"{B.dtype}, {None if R is None else R.dtype}")
+    for t in (A, B, R):
+        if t is not None and (not t.is_cuda or t.stride(-1) != 1):
+            raise RuntimeError("gemm: CUDA tensors with unit inner stride expected")
+    dev = A.device
+    shape = (M, N) if batch == 1 else (batch, M, N)
+    if out is None:
+        out = torch.empty(shape, dtype=c_dt, device=dev)
+    splits = _splits(M, N, K)
+    L = _lib.lib()
+    ws = None
+    if splits > 1:
+        ws = _workspace(dev, L.rgbd_gemm_workspace_size(M, N, batch, splits), "gemm")
+    b32 = None if bias is None else bias.detach().float().contiguous()
+    check(L.rgbd_gemm(_CODE[dt], int(a_t), int(b_t), M, N, K, _p(A), A.stride(-2), sa, _p(B), B.stride(-2), sb,
+                      _p(b32), act, _p(R), 0 if R is None else R.stride(-2), sr, _p(out), N, M * N,
+                      int(c_f32), batch, splits, _p(ws), _stream(dev)), "rgbd_gemm")
+    return out
+
+
+def colsum(y2):
+    out = torch.empty((y2.shape[1],), dtype=torch.float32, device=y2.device)
+    check(_lib.lib().rgbd_colsum(_CODE[y2.dtype], _p(y2), y2.shape[0], y2.shape[1], y2.stride(0), _p(out),
+                                 _stream(y2.device)), "rgbd_colsum")
+    return out
+
+
+def _rows(x, dt):
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.dtype != dt:
+        x2 = x2.to(dt)
+    return x2.contiguous()
+
+
+class LinearFunction(torch.autograd.Function):
+    """y = act(x W^T + b), act none / relu / gelu (gelu: forward only)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act, dt):
+        N, K = w.shape
+        x2 = _rows(x, dt)
+        wc = cast_weight(w, dt)
+        y = gemm(x2, wc, 0, 0, x2.shape[0], N, K, bias=b, act=act)
+        ctx.save_for_backward(x2, wc, y if act == ACT_RELU else None)
+        ctx.act, ctx.x_dtype, ctx.w_dtype, ctx.has_b = act, x.dtype, w.dtype, b is not None
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, wc, y = ctx.saved_tensors
+        if ctx.act == ACT_GELU:
+            raise RuntimeError("HipLinear: the fused GELU epilogue is forward-only")
+        M, K = x2.shape
+        N = wc.shape[0]
+        g2 = _rows(gy, x2.dtype)
+        if ctx.act == ACT_RELU:
+            g2 = g2 * (y > 0)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(g2, wc, 0, 1, M, K, N).to(ctx.x_dtype).view(*gy.shape[:-1], K)
+        if ctx.needs_input_grad[1]:
+            dw = gemm(g2, x2, 1, 1, N, K, M, c_f32=True).to(ctx.w_dtype)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = colsum(g2)
+        return dx, dw, db, None, None
+
+
+class FFNFunction(torch.autograd.Function):
+    """fc2(relu(fc1(x))): the ReLU in fc1's epilogue, its gradient in fc2's dX epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, dt):
+        F_, K = w1.shape
+        N = w2.shape[0]
+        x2 = _rows(x, dt)
+        w1c, w2c = cast_weight(w1, dt), cast_weight(w2, dt)
+        M = x2.shape[0]
+        h = gemm(x2, w1c, 0, 0, M, F_, K, bias=b1, act=ACT_RELU)
+        y = gemm(h, w2c, 0, 0, M, N, F_, bias=b2)
+        ctx.save_for_backward(x2, h, w1c, w2c)
+        ctx.x_dtype, ctx.w_dtypes = x.dtype, (w1.dtype, w2.dtype)
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, h, w1c, w2c = ctx.saved_tensors
+        M, K = x2.shape
+        F_, N = h.shape[1], w2c.shape[0]
+        g2 = _rows(gy, x2.dtype)
+        dh = gemm(g2, w2c, 0, 1, M, F_, N, act=ACT_RELU_GRAD, R=h)
+        dw2 = gemm(g2, h, 1, 1, N, F_, M, c_f32=True).to(ctx.w_dtypes[1])
+        db2 = colsum(g2)
+        dx = gemm(dh, w1c, 0, 1, M, K, F_).to(ctx.x_dtype).view(*gy.shape[:-1], K)
+        dw1 = gemm(dh, x2, 1, 1, F_, K, M, c_f32=True).to(ctx.w_dtypes[0])
+        db1 = colsum(dh)
+        return dx, dw1, db1, dw2, db2, None
+
+
+class LayerNormFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, y_dtype):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        if x2.dtype not in _CODE:
+            x2 = x2.float()
+        x2 = x2.contiguous()
+        rows = x2.shape[0]
+        y = torch.empty((rows, C), dtype=y_dtype, device=x.device)
+        mean = torch.empty((rows,), dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        g32 = None if gamma is None else gamma.detach().float().contiguous()
+        b32 = None if beta is None else beta.detach().float().contiguous()
+        check(_lib.lib().rgbd_layernorm_fwd(_CODE[x2.dtype], _p(x2), _p(g32), _p(b32), rows, C, float(eps),
+                                            _CODE[y_dtype], _p(y), _p(mean), _p(rstd), _stream(x.device)),
+              "rgbd_layernorm_fwd")
+        ctx.save_for_backward(x2, g32, mean, rstd)
+        ctx.x_dtype, ctx.has_g, ctx.has_b = x.dtype, gamma is not None, beta is not None
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, g32, mean, rstd = ctx.saved_tensors
+        rows, C = x2.shape
+        g2 = gy.reshape(rows, C)
+        if g2.dtype not in _CODE:
+            g2 = g2.float()
+        g2 = g2.contiguous()
+        dx = torch.empty_like(x2)
+        dg = torch.empty((C,), dtype=torch.float32, device=x2.device)
+        db = torch.empty_like(dg)
+        L = _lib.lib()
+        ws = _workspace(x2.device, L.rgbd_layernorm_bwd_workspace_size(rows, C), "ln_bwd")
+        check(L.rgbd_layernorm_bwd(_CODE[x2.dtype], _p(x2), _CODE[g2.dtype], _p(g2), _p(g32), _p(mean), _p(rstd),
+                                   rows, C, _p(dx), _p(dg), _p(db), _p(ws), _stream(x2.device)), "rgbd_layernorm_bwd")
+        return (dx.to(ctx.x_dtype).view(gy.shape), dg if ctx.has_g else None, db if ctx.has_b else None, None, None)
+
+
+def linear(x, w, b=None, act=ACT_NONE):
+    dt = compute_dtype(x)
+    return LinearFunction.apply(x, w, b, act, dt)
+
+
+def ffn(x, fc1, fc2):
+    return FFNFunction.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, compute_dtype(x))
+
+
+def layer_norm(x, ln):
+    y_dtype = torch.float32 if torch.is_autocast_enabled("cuda") else x.dtype
+    return LayerNormFunction.apply(x, ln.weight, ln.bias, ln.eps, y_dtype)
+
+
+def _cuda_ok(x):
+    return x.is_cuda and compute_dtype(x) is not None and x.numel() > 0
+
+
+class HipLinear(nn.Linear):
+    def forward(self, x):
+        if not _cuda_ok(x):
+            return super().forward(x)
+        return linear(x, self.weight, self.bias)
+
+
+class HipLayerNorm(nn.LayerNorm):
+    def forward(self, x):
+        if (not x.is_cuda or x.numel() == 0 or len(self.normalized_shape) != 1 or self.normalized_shape[0] > 1536
+                or x.dtype not in _CODE):
+            return super().forward(x)
+        return layer_norm(x, self)
+
+
+# ----------------------------------------------------------------- decoder layer (f1)
+def self_attention(attn, h, pos):
+    """Mask2FormerAttention.forward (modeling_mask2former.py:1487-1585) for the decoder's
+    self-attention, seq-first h [Q, B, E]: q / k from h + pos, v from h, softmax(q k^T / sqrt(d))
+    v per head on the HIP attention core (no mask), out_proj."""
+    from .masked_attention import masked_attention
+    Q, B, E = h.shape
+    H = attn.num_heads
+    hq = h if pos is None else h + pos
+    q = linear(hq, attn.q_proj.weight, attn.q_proj.bias).view(Q, B * H, E // H)
+    k = linear(hq, attn.k_proj.weight, attn.k_proj.bias).view(Q, B * H, E // H)
+    v = linear(h, attn.v_proj.weight, attn.v_proj.bias).view(Q, B * H, E // H)
+    o = masked_attention(q, k, v, None, attn.scaling)
+    return linear(o.view(Q, B, E), attn.out_proj.weight, attn.out_proj.bias)
+
+
+def _decoder_layer_covered(layer, h):
+    return (h.is_cuda and compute_dtype(h) is not None and not layer.pre_norm
+            and (not layer.training or (layer.dropout == 0.0 and layer.self_attn.dropout == 0.0))
+            and layer.config.activation_function == "relu" and layer.self_attn.head_dim == 32)
+
+
+def _install_class(m, base, cls):
+    if type(m) is base:
+        m.__class__ = cls
+        return 1
+    return 0
+
+
+def _make_decoder_layer_class():
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerMaskedAttentionDecoderLayer as _L
+
+    class HipMaskedAttentionDecoderLayer(_L):
+        def forward_post(self, hidden_states, level_index=None, attention_mask=None, position_embeddings=None,
+                         query_position_embeddings=None, encoder_hidden_states=None, encoder_attention_mask=None,
+                         output_attentions=False):
+            if output_attentions or not _decoder_layer_covered(self, hidden_states):
+                return super().forward_post(hidden_states, level_index, attention_mask, position_embeddings,
+                                            query_position_embeddings, encoder_hidden_states,
+                                            encoder_attention_mask, output_attentions)
+            residual = hidden_states
+            hidden_states, _ = self.cross_attn(
+                query=self.with_pos_embed(hidden_states, query_position_embeddings),
+                key=self.with_pos_embed(encoder_hidden_states[level_index], position_embeddings[level_index]),
+                value=encoder_hidden_states[level_index], attn_mask=encoder_attention_mask, key_padding_mask=None)
+            hidden_states = self.cross_attn_layer_norm(residual + hidden_states)
+            residual = hidden_states
+            hidden_states = self_attention(self.self_attn, hidden_states, query_position_embeddings)
+            hidden_states = self.self_attn_layer_norm(residual + hidden_states)
+            residual = hidden_states
+            hidden_states = ffn(hidden_states, self.fc1, self.fc2)
+            hidden_states = self.final_layer_norm(residual + hidden_states)
+            return (hidden_states,)
+
+    return _L, HipMaskedAttentionDecoderLayer
+
+
+def _make_encoder_layer_class():
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerPixelDecoderEncoderLayer as _L
+
+    class HipPixelDecoderEncoderLayer(_L):
+        def forward(self, hidden_states, attention_mask, position_embeddings=None, reference_points=None,
+                    spatial_shapes_list=None, level_start_index=None, output_attentions=False):
+            if (not hidden_states.is_cuda or compute_dtype(hidden_states) is None
+                    or (self.training and self.dropout > 0.0)):
+                return super().forward(hidden_states, attention_mask, position_embeddings, reference_points,
+                                       spatial_shapes_list, level_start_index, output_attentions)
+            residual = hidden_states
+            hidden_states, attn_weights = self.self_attn(
+                hidden_states=hidden_states, attention_mask=attention_mask, encoder_hidden_states=hidden_states,
+                encoder_attention_mask=attention_mask, position_embeddings=position_embeddings,
+                reference_points=reference_points, spatial_shapes_list=spatial_shapes_list,
+                level_start_index=level_start_index, output_attentions=output_attentions)
+            hidden_states = self.self_attn_layer_norm(residual + hidden_states)
+            residual = hidden_states
+            hidden_states = ffn(hidden_states, self.fc1, self.fc2)
+            hidden_states = self.final_layer_norm(residual + hidden_states)
+            if self.training:
+                # the reference clamps when any value is non-finite (:1094-1097, a host sync per
+                # layer); clamping unconditionally is the same map (identity on finite float32,
+                # +-inf -> +-(max - 1000) = +-max, NaN kept) without the sync
+                c = torch.finfo(hidden_states.dtype).max - 1000
+                hidden_states = torch.clamp(hidden_states, min=-c, max=c)
+            outputs = (hidden_states,)
+            if output_attentions:
+                outputs += (attn_weights.transpose(1, 0),)
+            return outputs
+
+    return _L, HipPixelDecoderEncoderLayer
+
+
+_CLASSES = {}
+
+
+def _classes():
+    if not _CLASSES:
+        _CLASSES["decoder"] = _make_decoder_layer_class()
+        _CLASSES["encoder"] = _make_encoder_layer_class()
+    return _CLASSES
+
+
+def install(model: nn.Module) -> int:
+    """Swap nn.Linear / nn.LayerNorm and the decoder / pixel-decoder encoder layers inside
+    ``model`` for the HIP classes; returns the number of modules swapped."""
+    cls = _classes()
+    n = 0
+    for m in model.modules():
+        n += _install_class(m, nn.Linear, HipLinear)
+        n += _install_class(m, nn.LayerNorm, HipLayerNorm)
+        n += _install_class(m, *cls["decoder"])
+        n += _install_class(m, *cls["encoder"])
+    return n
+
+
+def uninstall(model: nn.Module) -> int:
+    cls = _classes()
+    back = {HipLinear: nn.Linear, HipLayerNorm: nn.LayerNorm, cls["decoder"][1]: cls["decoder"][0],
+            cls["encoder"][1]: cls["encoder"][0]}
+    n = 0
+    for m in model.modules():
+        b = back.get(type(m))
+        if b is not None:
+            m.__class__ = b
+            n += 1
+    return n

@@ -79,7 +79,8 @@ class MaskedAttentionFunction(torch.autograd.Function):
 
 
 def masked_attention(q, k, v, mask, scale):
-    return MaskedAttentionFunction.apply(q.contiguous(), k.contiguous(), v.contiguous(), mask.contiguous(), scale)
+    return MaskedAttentionFunction.apply(q.contiguous(), k.contiguous(), v.contiguous(),
+                                         None if mask is None else mask.contiguous(), scale)
 
 
 class HipMultiheadAttention(nn.MultiheadAttention):

@@ -1,0 +1,242 @@
+"""f1 / f2 dense layers on the HIP GEMM and LayerNorm kernels (csrc/gemm.hip, csrc/layernorm.hip;
+rgbd_amd/dense.py) against plain PyTorch references.
+
+* rgbd_gemm in every operand layout (forward / dX / dW of a linear layer), float32 and bf16,
+  aligned and ragged shapes (N = 49: the class predictor's 48 labels + 1), batched, split-K,
+  every epilogue — against a float64 matmul of the same operands.  Bars: float32 (exact f32
+  products, f32 sums) 2e-5 relative to the max |C|; bf16 operands (exact products, f32 sums, one
+  bf16 rounding of C) 1e-2 relative.
+* LayerNorm forward / backward vs torch.nn.functional.layer_norm in float64.
+* HipLinear / FFN / HipLayerNorm modules and the installed decoder and pixel-decoder encoder
+  layers vs the Hugging Face modules they replace (same parameters): outputs and every gradient,
+  float32 2e-5 (relative to the max), bf16 autocast 3e-2.
+"""
+import copy
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+import _rgbd_import  # noqa: E402,F401
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+F32_TOL, BF16_TOL = 2e-5, 1e-2
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+def _ref(A, B, a_t, b_t, bias=None, act=0, R=None):
+    a = A.double().transpose(-1, -2) if a_t else A.double()
+    b = B.double() if b_t else B.double().transpose(-1, -2)
+    c = a @ b
+    if act == 3:
+        return c * (R.double() > 0)
+    if bias is not None:
+        c = c + bias.double()
+    if act == 1:
+        c = c.clamp_min(0)
+    elif act == 2:
+        c = torch.nn.functional.gelu(c)
+    if R is not None:
+        c = c + R.double()
+    return c
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (800, 49, 256), (1000, 192, 96), (37, 130, 72), (3, 5, 7)])
+def test_gemm_layouts(dt, a_t, b_t, M, N, K):
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn((K, M) if a_t else (M, K), generator=g).to(DEV, dt)
+    B = torch.randn((K, N) if b_t else (N, K), generator=g).to(DEV, dt)
+    C = dense.gemm(A, B, a_t, b_t, M, N, K)
+    tol = F32_TOL if dt == torch.float32 else BF16_TOL
+    assert C.shape == (M, N)
+    assert _rel(C, _ref(A, B, a_t, b_t)) < tol
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("act", [0, 1, 2, 3], ids=["none", "relu", "gelu", "relu_grad"])
+def test_gemm_epilogues(dt, act):
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(act)
+    M, N, K = 300, 200, 160
+    A = torch.randn((M, K), generator=g).to(DEV, dt)
+    B = torch.randn((N, K), generator=g).to(DEV, dt)
+    bias = None if act == 3 else torch.randn((N,), generator=g).to(DEV)
+    R = torch.randn((M, N), generator=g).to(DEV, dt)
+    C = dense.gemm(A, B, 0, 0, M, N, K, bias=bias, act=act, R=R)
+    ref = _ref(A, B, 0, 0, bias, act, R)
+    tol = F32_TOL if dt == torch.float32 else BF16_TOL
+    assert _rel(C, ref) < tol * (3 if act == 2 else 1)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_gemm_split_k_weight_gradient(dt):
+    """dW = dY^T X with a long reduction (50 400 pixel-decoder tokens) and a small output: the
+    split-K path (float32 partials summed in split order), float32 output; deterministic."""
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(5)
+    M, N, K = 50400, 256, 256  # rows of dY / X
+    dY = torch.randn((M, N), generator=g).to(DEV, dt)
+    X = torch.randn((M, K), generator=g).to(DEV, dt)
+    assert dense._splits(N, K, M) > 1
+    dW = dense.gemm(dY, X, 1, 1, N, K, M, c_f32=True)
+    assert dW.dtype == torch.float32
+    ref = dY.double().t() @ X.double()
+    assert _rel(dW, ref) < (1e-5 if dt == torch.float32 else 2e-3)
+    assert torch.equal(dW, dense.gemm(dY, X, 1, 1, N, K, M, c_f32=True))
+
+
+def test_gemm_batched():
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(9)
+    b, M, N, K = 4, 100, 256, 300
+    A = torch.randn((b, M, K), generator=g).to(DEV)
+    B = torch.randn((b, K, N), generator=g).to(DEV)
+    C = dense.gemm(A, B, 0, 1, M, N, K, batch=b, sa=M * K, sb=K * N)
+    assert C.shape == (b, M, N)
+    assert _rel(C, A.double() @ B.double()) < F32_TOL
+
+
+def test_colsum():
+    from rgbd_amd import dense
+    y = torch.randn((1234, 77), device=DEV)
+    assert _rel(dense.colsum(y), y.double().sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("C", [96, 256, 768, 1000])
+def test_layernorm_fwd_bwd(dt, C):
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(C)
+    ln = torch.nn.LayerNorm(C, eps=1e-5).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(C, generator=g))
+        ln.bias.copy_(torch.randn(C, generator=g))
+    x = (torch.randn((333, C), generator=g) * 3 + 1).to(DEV, dt).requires_grad_()
+    y = dense.layer_norm(x, ln)
+    assert y.dtype == dt
+    gy = torch.randn(y.shape, generator=g).to(DEV, dt)
+    y.backward(gy)
+    x64 = x.detach().double().requires_grad_()
+    w64, b64 = ln.weight.detach().double().requires_grad_(), ln.bias.detach().double().requires_grad_()
+    y64 = torch.nn.functional.layer_norm(x64, (C,), w64, b64, 1e-5)
+    y64.backward(gy.double())
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert _rel(y, y64) < tol
+    assert _rel(x.grad, x64.grad) < tol * 2
+    assert _rel(ln.weight.grad, w64.grad) < 1e-5
+    assert _rel(ln.bias.grad, b64.grad) < 1e-5
+
+
+def _grads(m):
+    return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("amp", [False, True], ids=["f32", "bf16_autocast"])
+def test_linear_and_ffn_modules(amp):
+    from rgbd_amd import dense
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential(torch.nn.Linear(256, 2048), torch.nn.ReLU(), torch.nn.Linear(2048, 256)).to(DEV)
+    hip = copy.deepcopy(ref)
+    x = torch.randn((100, 8, 256), device=DEV)
+    gy = torch.randn((100, 8, 256), device=DEV)
+    xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        ya = ref(xa)
+        yb = dense.ffn(xb, hip[0], hip[2])
+    assert ya.dtype == yb.dtype
+    ya.float().backward(gy)
+    yb.float().backward(gy)
+    tol = 3e-2 if amp else F32_TOL
+    assert _rel(yb, ya) < tol
+    assert _rel(xb.grad, xa.grad) < tol
+    ga, gb = _grads(ref), _grads(hip)
+    assert ga.keys() == gb.keys()
+    for n in ga:
+        assert _rel(gb[n], ga[n]) < tol, n
+    # the plain module swap
+    lin = torch.nn.Linear(256, 49).to(DEV)
+    hl = copy.deepcopy(lin)
+    hl.__class__ = dense.HipLinear
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        assert _rel(hl(x), lin(x)) < tol
+
+
+def _hf_config():
+    from rgbd_amd.config import standard_config
+    return standard_config(48)
+
+
+@pytest.mark.parametrize("amp", [False, True], ids=["f32", "bf16_autocast"])
+def test_decoder_layer_matches_hf(amp):
+    """The installed masked-attention decoder layer (HIP cross-attention core, self-attention,
+    FFN, LayerNorms) vs the HF layer with the same parameters on a C2-shaped call (B = 8, 100
+    queries, level-2 memory of 4 800 keys), outputs and all gradients."""
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerMaskedAttentionDecoderLayer
+    from rgbd_amd import dense, masked_attention
+    torch.manual_seed(1)
+    cfg = _hf_config()
+    ref = Mask2FormerMaskedAttentionDecoderLayer(cfg).to(DEV).train()
+    hip = copy.deepcopy(ref)
+    assert dense.install(hip) > 0 and masked_attention.install(hip) == 0  # cross_attn swapped below
+    masked_attention.install_module(hip.cross_attn)
+    Q, B, E, L = 100, 8, 256, 4800
+    h = torch.randn((Q, B, E), device=DEV)
+    qpos = torch.randn((Q, B, E), device=DEV)
+    mem = [torch.randn((L, B, E), device=DEV)] * 3
+    pos = [torch.randn((L, B, E), device=DEV)] * 3
+    mask = torch.rand((B * 8, Q, L), device=DEV) < 0.3
+    gy = torch.randn((Q, B, E), device=DEV)
+    outs, grads = [], []
+    for m in (ref, hip):
+        hh = h.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = m(hh, 2, None, pos, qpos, mem, encoder_attention_mask=mask)[0]
+        y.float().backward(gy)
+        outs.append((y.float(), hh.grad))
+        grads.append(_grads(m))
+    tol = 3e-2 if amp else 2e-4
+    assert _rel(outs[1][0], outs[0][0]) < tol
+    assert _rel(outs[1][1], outs[0][1]) < tol
+    for n in grads[0]:
+        assert _rel(grads[1][n], grads[0][n]) < tol * 2, n
+
+
+@pytest.mark.parametrize("amp", [False, True], ids=["f32", "bf16_autocast"])
+def test_pixel_decoder_encoder_matches_hf(amp):
+    """The pixel decoder with the installed encoder layers (HIP deformable attention, linear
+    projections, FFN, LayerNorms) vs the HF pixel decoder on Swin-shaped features at 320x240."""
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerPixelDecoder
+    from rgbd_amd import deform_attn, dense
+    torch.manual_seed(2)
+    cfg = _hf_config()
+    ref = Mask2FormerPixelDecoder(cfg, feature_channels=[96, 192, 384, 768]).to(DEV).train()
+    hip = copy.deepcopy(ref)
+    assert dense.install(hip) > 0 and deform_attn.install(hip) > 0
+    B = 2
+    feats = [torch.randn((B, c, 60 // s, 80 // s), device=DEV) for c, s in zip([96, 192, 384, 768], [1, 2, 4, 8])]
+    res = []
+    for m in (ref, hip):
+        fs = [f.clone().requires_grad_() for f in feats]
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out = m(fs)
+        loss = out.mask_features.float().square().mean() + sum(t.float().square().mean()
+                                                               for t in out.multi_scale_features)
+        loss.backward()
+        res.append((out.mask_features.float(), [f.grad for f in fs], _grads(m)))
+    tol = 5e-2 if amp else 2e-4
+    assert _rel(res[1][0], res[0][0]) < tol
+    for a, b in zip(res[1][1], res[0][1]):
+        assert _rel(a, b) < tol * 2
+    for n in res[0][2]:
+        assert _rel(res[1][2][n], res[0][2][n]) < tol * 2, n

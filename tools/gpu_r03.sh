@@ -15,8 +15,9 @@ case "$stage" in
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
     rc=$?; tail -2 "$O/smoke.log"; exit $rc ;;
   tests)
-    timeout -k 10 1000 python -u -m pytest -m gpu -q -rfP --timeout 400 --timeout-method thread -p no:cacheprovider "${@:-tests}" > "$O/tests.log" 2>&1
-    rc=$?; tail -25 "$O/tests.log"; exit $rc ;;
+    log="$O/${TESTLOG:-tests}.log"
+    timeout -k 10 1000 python -u -m pytest -m gpu -q -rfP --timeout 400 --timeout-method thread -p no:cacheprovider "${@:-tests}" > "$log" 2>&1
+    rc=$?; tail -25 "$log"; exit $rc ;;
   bench)
     timeout -k 10 600 python bench.py "$@" > "$O/bench.json" 2> "$O/bench.err"
     rc=$?; cat "$O/bench.json"; [ $rc -eq 0 ] || tail -20 "$O/bench.err"; exit $rc ;;
