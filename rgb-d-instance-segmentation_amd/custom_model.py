@@ -3,10 +3,12 @@
 
 Same class names, constructor signatures (``version`` kwarg), ``config_class``,
 ``main_input_name``, forward signatures, output dataclass and state_dict keys, so a
-checkpoint of the reference loads unchanged.  Everything outside the hot path (Swin
-encoder, MSDeformAttn pixel decoder, masked-attention transformer decoder, loss) is the
-installed Hugging Face Mask2Former, exactly as in the reference (SURVEY §8(f) rows are the
-next milestones).
+checkpoint of the reference loads unchanged.  Outside the hot path the model is the installed
+Hugging Face Mask2Former with its modules swapped in place for the HIP ones of SURVEY §8(f):
+Swin-T layers (f2), pixel-decoder deformable attention and encoder layers (f2), the masked-
+attention decoder layers and mask predictor (f1), every nn.Linear / nn.LayerNorm (f1 / f2),
+the loss's matcher costs, assignment and point-sampled mask terms (f3).  The convolutions of
+the pixel decoder's input projections / FPN and the Swin patch embedding stay torch (MIOpen).
 """
 import random
 
@@ -17,7 +19,7 @@ from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation,
 from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
                                                                   Mask2FormerPixelLevelModuleOutput)
 
-from . import deform_attn, mask_predictor, masked_attention, point_loss
+from . import deform_attn, dense, mask_predictor, masked_attention, point_loss, swin
 from .hot_path import hot_path, prepare
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
@@ -86,7 +88,10 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
             backbone_features = list(self.encoder(pixel_values).feature_maps)
         else:
             rgb = pixel_values[:, 0:3, :, :]
-            color_feature_map = self.encoder(rgb).feature_maps          # :330 (Swin, HF)
+            # :330 — Swin-T on the HIP layers (f2).  Its maps are detached at :332-333 (Q1), so no
+            # graph is recorded for it: identical values, the fused forward-only kernels apply.
+            with torch.no_grad():
+                color_feature_map = self.encoder(rgb).feature_maps
             statuses = []
             backbone_features = self.hot_path_features(pixel_values, color_feature_map, status_sink=statuses)
         decoder_output = self.decoder(backbone_features, output_hidden_states=output_hidden_states)
@@ -119,6 +124,11 @@ class CustomMask2FormerModel(Mask2FormerModel):
         masked_attention.install(self.transformer_module)
         # f2: the pixel decoder's deformable-attention core on the fused HIP gather kernels
         deform_attn.install(self.pixel_level_module.decoder)
+        # f1 / f2: the dense layers — every nn.Linear and nn.LayerNorm, the decoder and pixel-
+        # decoder encoder layers (fused FFN), the Swin-T layers (window attention) — on the HIP
+        # GEMM / LayerNorm / attention kernels
+        swin.install(self.pixel_level_module.encoder)
+        dense.install(self)
 
 
 class CustomMask2FormerForUniversalSegmentation(Mask2FormerForUniversalSegmentation):

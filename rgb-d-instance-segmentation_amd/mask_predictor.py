@@ -10,15 +10,15 @@ binarised attention mask of the next masked-attention decoder layer (:1896, :192
     outputs_mask    = einsum(bqc,bchw->bqhw)                       K: rgbd_mask_logits (MFMA)
     attention_mask  = bilinear -> sigmoid -> < 0.5, x heads        K: rgbd_mask_attention
 Backward of the einsum (grads for the mask embeddings and the pixel-decoder mask features) is
-two plain batched GEMMs on the library BLAS; the attention mask is detached as in the
-reference.  ``install(model)`` swaps the class of the decoder's predictor in place (no
+two batched HIP GEMMs (csrc/gemm.hip: d_emb = g pix^T split over the pixels, d_pix = emb^T g);
+the attention mask is detached as in the reference.  ``install(model)`` swaps the class of the decoder's predictor in place (no
 re-initialisation, no parameter change).
 """
 import torch
 from torch import nn
 from transformers.models.mask2former.modeling_mask2former import Mask2FormerMaskPredictor
 
-from . import ops
+from . import dense, ops
 
 
 class MaskLogitsFunction(torch.autograd.Function):
@@ -31,10 +31,15 @@ class MaskLogitsFunction(torch.autograd.Function):
     def backward(ctx, g):
         emb, pix = ctx.saved_tensors
         B, Q, C = emb.shape
-        g2 = g.reshape(B, Q, -1).to(pix.dtype)
-        p2 = pix.reshape(B, C, -1)
-        d_emb = torch.bmm(g2, p2.transpose(1, 2)) if ctx.needs_input_grad[0] else None
-        d_pix = torch.bmm(emb.transpose(1, 2), g2).reshape(pix.shape) if ctx.needs_input_grad[1] else None
+        emb = emb.contiguous()
+        g2 = g.reshape(B, Q, -1).to(pix.dtype).contiguous()
+        P = g2.shape[2]
+        p2 = pix.reshape(B, C, P).contiguous()
+        d_emb = d_pix = None
+        if ctx.needs_input_grad[0]:   # d_emb[b] = g[b] pix[b]^T: K = pixels, split-K
+            d_emb = dense.gemm(g2, p2, 0, 0, Q, C, P, batch=B, sa=Q * P, sb=C * P)
+        if ctx.needs_input_grad[1]:   # d_pix[b] = emb[b]^T g[b]: K = queries
+            d_pix = dense.gemm(emb, g2, 1, 1, C, P, Q, batch=B, sa=Q * C, sb=Q * P).reshape(pix.shape)
         return d_emb, d_pix
 
 

@@ -7,7 +7,7 @@ torch's math path (need_weights=True, F.multi_head_attention_forward) does, per 
     q, k, v = linear(query / key / value, in_proj chunks)            library GEMMs
     S = (q * head_dim^-1/2) k^T + where(mask, -inf, 0); P = softmax(S); O = P v
     out = linear(O, out_proj)                                         library GEMM
-``HipMultiheadAttention`` keeps the projections as the module's GEMMs and runs the masked
+``HipMultiheadAttention`` runs the projections on the HIP GEMMs (rgbd_amd/dense.py) and the masked
 softmax-attention core (scores, mask, softmax, P.V and the backward) as the HIP kernels
 ``rgbd_masked_attn_fwd`` / ``_bwd`` (csrc/masked_attn.hip), on the projections' own
 sequence-major layout (no head transposes, no [BH, Q, L] score tensor in HBM).
@@ -34,7 +34,6 @@ before the call (modeling_mask2former.py:2054-2055), so the model never reaches 
 import math
 
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
@@ -114,12 +113,13 @@ class HipMultiheadAttention(nn.MultiheadAttention):
         H = self.num_heads
         w_q, w_k, w_v = self.in_proj_weight.chunk(3)
         b_q, b_k, b_v = self.in_proj_bias.chunk(3)
-        q = F.linear(query, w_q, b_q).view(Q, B * H, E // H)
-        k = F.linear(key, w_k, b_k).view(L, B * H, E // H)
-        v = F.linear(value, w_v, b_v).view(L, B * H, E // H)
+        from .dense import linear  # the projections on the HIP GEMMs (f1 dense layers)
+        q = linear(query, w_q, b_q).view(Q, B * H, E // H)
+        k = linear(key, w_k, b_k).view(L, B * H, E // H)
+        v = linear(value, w_v, b_v).view(L, B * H, E // H)
         scale = math.sqrt(1.0 / float(E // H))  # torch's q scaling
         o = masked_attention(q, k, v, attn_mask, scale)
-        out = F.linear(o.view(Q * B, E), self.out_proj.weight, self.out_proj.bias).view(Q, B, E)
+        out = linear(o.view(Q * B, E), self.out_proj.weight, self.out_proj.bias).view(Q, B, E)
         return out, None
 
 

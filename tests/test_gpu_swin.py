@@ -48,19 +48,32 @@ def _backbones(train):
 @pytest.mark.parametrize("train", [False, True], ids=["eval", "train_droppath"])
 @pytest.mark.parametrize("hw", [(480, 640), (240, 320)], ids=["640x480", "320x240"])
 def test_swin_backbone_matches_hf(amp, train, hw):
+    """HIP arm in the given precision vs the HF backbone in float32 (the reference's arithmetic),
+    and, in bf16, also vs the HF backbone under the same autocast when that arm is finite."""
     ref, hip = _backbones(train)
     x = torch.randn((2, 3, *hw), device=DEV)
-    outs = []
-    for m in (ref, hip):
+
+    def run(m, amp_):
         torch.manual_seed(11)
-        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            outs.append([f.float() for f in m(x).feature_maps])
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp_):
+            return [f.float() for f in m(x).feature_maps]
+    ref32, got = run(ref, False), run(hip, amp)
+    for k, f in enumerate(got):
+        assert torch.isfinite(f).all(), f"HIP arm: stage {k + 1} not finite"
     tol = 5e-2 if amp else 1e-4
-    for k, (a, b) in enumerate(zip(outs[1], outs[0])):
+    for k, (a, b) in enumerate(zip(got, ref32)):
         assert a.shape == b.shape
         err = _rel(a, b)
-        print(f"stage {k + 1} {tuple(a.shape)}: rel err {err:.3g}")
+        print(f"stage {k + 1} {tuple(a.shape)}: rel err vs HF float32 {err:.3g}")
         assert err < tol, f"stage {k + 1}"
+    if amp:
+        ref16 = run(ref, True)
+        if all(torch.isfinite(f).all() for f in ref16):
+            for k, (a, b) in enumerate(zip(got, ref16)):
+                print(f"stage {k + 1}: rel err vs HF bf16 autocast {_rel(a, b):.3g}")
+                assert _rel(a, b) < tol
+        else:
+            print("HF bf16 autocast arm not finite on this device: compared with float32 only")
 
 
 def test_swin_layer_takes_hf_path_with_grad():

@@ -27,7 +27,8 @@ def main():
     ap.add_argument("--amp", type=int, default=1)
     ap.add_argument("--arms", default="hip,hf")
     args = ap.parse_args()
-    from rgbd_amd import deform_attn, init as winit, mask_predictor, masked_attention, point_loss, ops, synthetic
+    from rgbd_amd import (deform_attn, dense, init as winit, mask_predictor, masked_attention, point_loss, ops, swin,
+                          synthetic)
     from rgbd_amd.config import standard_config
     from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
     dev = torch.device("cuda")
@@ -48,6 +49,8 @@ def main():
             masked_attention.uninstall(m)
             deform_attn.uninstall(m)
             point_loss.uninstall(m)
+            dense.uninstall(m)
+            swin.uninstall(m)
         opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, fused=True)
 
         def step():
