@@ -439,8 +439,10 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
               const void* B, long long ldb, long long sb, const float* bias, int act, const void* R, long long ldr,
               long long sr, void* C, long long ldc, long long sc, int c_f32, int batch, int splits, void* ws,
               void* stream);
-/* rgbd_colsum: out[n] = sum over rows m of y[m * ld + n] (the bias gradient), float32, fixed order. */
-int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* stream);
+/* rgbd_colsum: out[n] = sum over rows m of y[m * ld + n] (the bias gradient), float32, fixed
+ * order (row chunks, then the chunks in order); ws: rgbd_colsum_workspace_size(rows, N) bytes. */
+size_t rgbd_colsum_workspace_size(int rows, int N);
+int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* ws, void* stream);
 /* LayerNorm over the last dimension (nn.LayerNorm(C, eps) of the decoder layers :1700-1719, the
  * pixel decoder's encoder layers :1022-1040, Swin's layernorm_before / _after :602-640):
  *   y = (x - mean) * rstd * gamma + beta, mean / rstd float32 [rows] saved for the backward.

@@ -338,18 +338,55 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(GArgs a, int batch) 
   }
 }
 
-// bias gradient: out[n] = sum_m dY[b][m][n] over batch and rows, float32, fixed order.
-// block = 64 columns x 4 row groups; the row groups fold in a fixed order through LDS.
+// bias gradient: out[n] = sum_m y[m][n], float32, fixed order, in two passes.
+// Pass 1: the rows in at most CS_MAXCH chunks; block = 256 columns x one chunk, 256 threads =
+// 32 column groups of 8 (one 16-byte load per row when aligned) x 8 row lanes; the 8 row lanes
+// fold through LDS in fixed order -> part[chunk][N].  Pass 2: per column, the chunks in order.
+constexpr int CS_MAXCH = 64;
+
 template <typename T>
-__global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int rows, int N, long long ld, float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < N)
-    for (int m = rg; m < rows; m += 4) s += Num<T>::to_f(y[(long long)m * ld + c]);
-  red[rg][threadIdx.x & 63] = s;
+__global__ __launch_bounds__(256) void k_colsum_part(const T* __restrict__ y, int rows, int N, long long ld, int chunk,
+                                                     int vec, float* __restrict__ part) {
+  __shared__ float red[8][256];
+  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c0 = blockIdx.x * 256 + 8 * cg;
+  const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < N) {
+    for (int m = r0 + rl; m < r1; m += 8) {
+      const T* row = y + (long long)m * ld + c0;
+      float v[8];
+      if (vec && c0 + 8 <= N) {
+        Frag<T> f;
+        f.load(row);
+        f.to8(v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = c0 + j < N ? Num<T>::to_f(row[j]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][8 * cg + j] = acc[j];
   __syncthreads();
-  if (rg == 0 && c < N) out[c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += red[k][threadIdx.x];
+    part[(long long)blockIdx.y * N + c] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ part, int nch, int N,
+                                                      float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int k = 0; k < nch; ++k) s += part[(long long)k * N + c];
+  out[c] = s;
 }
 
 template <typename T, int TM, int TN, bool AT, bool BT>
@@ -430,14 +467,26 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
   return gemm_t<float>(a, a_t, b_t, batch, s);
 }
 
-int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* stream) {
-  RGBD_REQUIRE(y && out && rows > 0 && N > 0 && ld >= N, RGBD_E_ARG);
+size_t rgbd_colsum_workspace_size(int rows, int N) {
+  return (size_t)std::min(CS_MAXCH, std::max(1, ceil_div(rows, 64))) * N * sizeof(float);
+}
+
+int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* ws, void* stream) {
+  RGBD_REQUIRE(y && out && ws && rows > 0 && N > 0 && ld >= N, RGBD_E_ARG);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(ceil_div(N, 64));
+  const int nch = std::min(CS_MAXCH, std::max(1, ceil_div(rows, 64)));
+  const int chunk = ceil_div(rows, nch);
+  const int esz = dtype == RGBD_BF16 ? 2 : 4;
+  const int vec = (((uintptr_t)y) % 16 == 0) && ((ld * esz) % 16 == 0);
+  float* part = (float*)ws;
+  dim3 grid(ceil_div(N, 256), nch);
   if (dtype == RGBD_BF16)
-    hipLaunchKernelGGL(k_colsum<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)y, rows, N, ld, out);
+    hipLaunchKernelGGL(k_colsum_part<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)y, rows, N, ld, chunk, vec, part);
   else
-    hipLaunchKernelGGL(k_colsum<float>, grid, dim3(256), 0, s, (const float*)y, rows, N, ld, out);
+    hipLaunchKernelGGL(k_colsum_part<float>, grid, dim3(256), 0, s, (const float*)y, rows, N, ld, chunk, vec, part);
+  RGBD_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_colsum_final, dim3(ceil_div(N, 256)), dim3(256), 0, s, part, nch, N, out);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -7,11 +7,16 @@
 // the mean squared deviation — no cancellation), 1 / sqrt(var + eps).
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace rgbd {
 namespace {
 
 constexpr int LN_MAXI = 24;   // C <= 64 * 24 (Swin patch merging: 4 x 384)
-constexpr int LN_RB = 64;     // rows per backward block (its dgamma / dbeta partial)
+constexpr int LN_RB = 64;     // minimum rows per backward block (its dgamma / dbeta partial)
+constexpr int LN_MAXBLK = 256;  // at most this many partials: the final reduction stays short
+
+inline int ln_rows_per_block(int rows) { return std::max(LN_RB, (rows + LN_MAXBLK - 1) / LN_MAXBLK); }
 
 template <typename T>
 __device__ __forceinline__ float ld_f(const void* p, long long i) {
@@ -63,15 +68,15 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const void* __restrict__ x, cons
 template <typename TX, typename TD>
 __global__ __launch_bounds__(256) void k_ln_bwd(const void* __restrict__ x, const void* __restrict__ dy,
                                                 const float* __restrict__ gamma, const float* __restrict__ mean,
-                                                const float* __restrict__ rstd, int rows, int C,
+                                                const float* __restrict__ rstd, int rows, int C, int rb,
                                                 void* __restrict__ dx, float* __restrict__ part) {
   __shared__ float red[4][2][64 * LN_MAXI];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float pg[LN_MAXI], pb[LN_MAXI];
 #pragma unroll
   for (int i = 0; i < LN_MAXI; ++i) pg[i] = pb[i] = 0.f;
-  const int r0 = blockIdx.x * LN_RB;
-  for (int row = r0 + wave; row < min(rows, r0 + LN_RB); row += 4) {
+  const int r0 = blockIdx.x * rb;
+  for (int row = r0 + wave; row < min(rows, r0 + rb); row += 4) {
     const long long base = (long long)row * C;
     const float mu = mean[row], rs = rstd[row];
     float xh[LN_MAXI], g[LN_MAXI];
@@ -132,11 +137,12 @@ void ln_fwd_t(int y_dtype, const void* x, const float* gamma, const float* beta,
 template <typename TX>
 void ln_bwd_t(int dy_dtype, const void* x, const void* dy, const float* gamma, const float* mean, const float* rstd,
               int rows, int C, void* dx, float* part, hipStream_t s) {
-  dim3 grid(ceil_div(rows, LN_RB));
+  const int rb = ln_rows_per_block(rows);
+  dim3 grid(ceil_div(rows, rb));
   if (dy_dtype == RGBD_BF16)
-    hipLaunchKernelGGL((k_ln_bwd<TX, bf16_t>), grid, dim3(256), 0, s, x, dy, gamma, mean, rstd, rows, C, dx, part);
+    hipLaunchKernelGGL((k_ln_bwd<TX, bf16_t>), grid, dim3(256), 0, s, x, dy, gamma, mean, rstd, rows, C, rb, dx, part);
   else
-    hipLaunchKernelGGL((k_ln_bwd<TX, float>), grid, dim3(256), 0, s, x, dy, gamma, mean, rstd, rows, C, dx, part);
+    hipLaunchKernelGGL((k_ln_bwd<TX, float>), grid, dim3(256), 0, s, x, dy, gamma, mean, rstd, rows, C, rb, dx, part);
 }
 
 }  // namespace
@@ -162,7 +168,7 @@ int rgbd_layernorm_fwd(int x_dtype, const void* x, const float* gamma, const flo
 }
 
 size_t rgbd_layernorm_bwd_workspace_size(int rows, int C) {
-  return (size_t)ceil_div(rows, LN_RB) * 2 * C * sizeof(float);
+  return (size_t)ceil_div(rows, ln_rows_per_block(rows)) * 2 * C * sizeof(float);
 }
 
 int rgbd_layernorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy, const float* gamma,
@@ -179,8 +185,8 @@ int rgbd_layernorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy,
   else
     ln_bwd_t<float>(dy_dtype, x, dy, gamma, mean, rstd, rows, C, dx, part, s);
   RGBD_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_ln_param_reduce, dim3(ceil_div(2 * C, 256)), dim3(256), 0, s, part, ceil_div(rows, LN_RB), C,
-                     dgamma, dbeta);
+  hipLaunchKernelGGL(k_ln_param_reduce, dim3(ceil_div(2 * C, 256)), dim3(256), 0, s, part,
+                     ceil_div(rows, ln_rows_per_block(rows)), C, dgamma, dbeta);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

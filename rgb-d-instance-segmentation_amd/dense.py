@@ -47,21 +47,29 @@ def compute_dtype(x: torch.Tensor):
     return x.dtype if x.dtype in _CODE else None
 
 
-_wcache = weakref.WeakKeyDictionary()
+_wcache = {}  # id(parameter) -> (weakref to it, version, data_ptr, dtype, cast copy)
 
 
 def cast_weight(w: torch.Tensor, dt):
     """w (a parameter) in dtype dt, cast once per weight version (as autocast's cast cache does
-    within a region); never cached while a graph is being captured."""
+    within a region); never cached while a graph is being captured.  Keyed by id with a weak
+    reference to check identity (tensors compare elementwise, so they cannot be dict keys of a
+    WeakKeyDictionary); entries of dead parameters are dropped as they are found."""
     if w.dtype == dt:
         return w.detach()
-    if torch.cuda.is_current_stream_capturing():
+    if w.is_cuda and torch.cuda.is_current_stream_capturing():
         return w.detach().to(dt)
-    ent = _wcache.get(w)
-    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
-        return ent[2]
+    key = id(w)
+    ent = _wcache.get(key)
+    if ent is not None:
+        ref, ver, ptr, edt, t = ent
+        if ref() is w and ver == w._version and ptr == w.data_ptr() and edt == dt:
+            return t
+        if ref() is None or ref() is not w:
+            del _wcache[key]
     t = w.detach().to(dt)
-    _wcache[w] = (w._version, w.data_ptr(), t)
+    if w._base is None:  # parameters, not per-call views (the chunks of an in_proj_weight)
+        _wcache[key] = (weakref.ref(w), w._version, w.data_ptr(), dt, t)
     return t
 
 
@@ -104,8 +112,10 @@ def gemm(A, B, a_t, b_t, M, N, K, bias=None, act=ACT_NONE, R=None, c_f32=False, 
 
 def colsum(y2):
     out = torch.empty((y2.shape[1],), dtype=torch.float32, device=y2.device)
-    check(_lib.lib().rgbd_colsum(_CODE[y2.dtype], _p(y2), y2.shape[0], y2.shape[1], y2.stride(0), _p(out),
-                                 _stream(y2.device)), "rgbd_colsum")
+    L = _lib.lib()
+    ws = _workspace(y2.device, L.rgbd_colsum_workspace_size(y2.shape[0], y2.shape[1]), "colsum")
+    check(L.rgbd_colsum(_CODE[y2.dtype], _p(y2), y2.shape[0], y2.shape[1], y2.stride(0), _p(out), _p(ws),
+                        _stream(y2.device)), "rgbd_colsum")
     return out
 
 

@@ -8,8 +8,9 @@ rgbd_amd/dense.py) against plain PyTorch references.
   bf16 rounding of C) 1e-2 relative.
 * LayerNorm forward / backward vs torch.nn.functional.layer_norm in float64.
 * HipLinear / FFN / HipLayerNorm modules and the installed decoder and pixel-decoder encoder
-  layers vs the Hugging Face modules they replace (same parameters): outputs and every gradient,
-  float32 2e-5 (relative to the max), bf16 autocast 3e-2.
+  layers vs the Hugging Face modules they replace (same parameters; the HF arm in float32, the
+  reference's arithmetic): outputs and every gradient, float32 2e-4 / 4e-4 (relative to the
+  max), bf16 autocast 5e-2 outputs, 0.1 / 0.2 gradients (see _grad_tol).
 """
 import copy
 import sys
@@ -144,6 +145,10 @@ def _grads(m):
 
 @pytest.mark.parametrize("amp", [False, True], ids=["f32", "bf16_autocast"])
 def test_linear_and_ffn_modules(amp):
+    """fc2(relu(fc1(x))) on the fused FFN vs torch.  The weight gradients in bf16 are checked
+    against float32 arithmetic on the same bf16-rounded operands: torch's own autocast weight
+    gradient of fc1 here is 9.4 % (relative to its max) away from that (measured,
+    tools/debug_ffn_bf16.py), ours 5.8e-4."""
     from rgbd_amd import dense
     torch.manual_seed(0)
     ref = torch.nn.Sequential(torch.nn.Linear(256, 2048), torch.nn.ReLU(), torch.nn.Linear(2048, 256)).to(DEV)
@@ -160,16 +165,42 @@ def test_linear_and_ffn_modules(amp):
     tol = 3e-2 if amp else F32_TOL
     assert _rel(yb, ya) < tol
     assert _rel(xb.grad, xa.grad) < tol
-    ga, gb = _grads(ref), _grads(hip)
+    gb = _grads(hip)
+    if amp:  # float32 arithmetic on the bf16 operands
+        r = lambda t: t.detach().bfloat16().float()  # noqa: E731
+        xr, w1, w2, g = r(x.reshape(800, 256)), r(ref[0].weight), r(ref[2].weight), r(gy.reshape(800, 256))
+        z = xr @ w1.t() + ref[0].bias.detach()
+        h = torch.relu(z).bfloat16().float()
+        dh = ((g @ w2) * (h > 0)).bfloat16().float()
+        ga = {"0.weight": dh.t() @ xr, "0.bias": dh.sum(0), "2.weight": g.t() @ h, "2.bias": g.sum(0)}
+        tol_w = 5e-3
+    else:
+        ga, tol_w = _grads(ref), F32_TOL
     assert ga.keys() == gb.keys()
     for n in ga:
-        assert _rel(gb[n], ga[n]) < tol, n
+        err = _rel(gb[n], ga[n])
+        print(f"{n}: {err:.3g}")
+        assert err < tol_w, n
     # the plain module swap
     lin = torch.nn.Linear(256, 49).to(DEV)
     hl = copy.deepcopy(lin)
     hl.__class__ = dense.HipLinear
     with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
         assert _rel(hl(x), lin(x)) < tol
+
+
+def _grad_tol(name, amp):
+    """Gradient bars against the HF float32 layer.  In bf16 the FFN's ReLU mask is taken from a
+    bf16 pre-activation: about 0.07 % of the units sit within rounding of zero and flip (measured
+    1 211 of 1.6 M at B = 8), which moves fc1's gradients by ~14 % of their max — torch's own
+    autocast path lands at the same distance (tools/debug_ffn_bf16.py: 14.1 % vs ours 14.0 %)."""
+    if not amp:
+        return 4e-4
+    if name.startswith("self_attn.sampling_offsets."):
+        # the location gradient of bilinear sampling is a difference of neighbouring values, each
+        # carrying bf16 rounding: measured 18 % of its max against float32
+        return 0.3
+    return 0.2 if name.startswith("fc1.") else 0.1
 
 
 def _hf_config():
@@ -198,21 +229,27 @@ def test_decoder_layer_matches_hf(amp):
     mask = torch.rand((B * 8, Q, L), device=DEV) < 0.3
     gy = torch.randn((Q, B, E), device=DEV)
     outs, grads = [], []
-    for m in (ref, hip):
+    for m, amp_ in ((ref, False), (hip, amp)):  # the HF arm in float32: the reference's arithmetic
         hh = h.clone().requires_grad_()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp_):
             y = m(hh, 2, None, pos, qpos, mem, encoder_attention_mask=mask)[0]
         y.float().backward(gy)
         outs.append((y.float(), hh.grad))
         grads.append(_grads(m))
-    tol = 3e-2 if amp else 2e-4
+    tol = 5e-2 if amp else 2e-4
     assert _rel(outs[1][0], outs[0][0]) < tol
     assert _rel(outs[1][1], outs[0][1]) < tol
     assert grads[0].keys() == grads[1].keys()
+    scale = max(float(g.abs().max()) for g in grads[0].values())
     for n in grads[0]:
+        if n == "self_attn.k_proj.bias":
+            # a key bias shifts every score of a query by the same q.b: softmax-invariant, so its
+            # gradient is zero in exact arithmetic and rounding noise in both arms
+            assert float(grads[1][n].abs().max()) < 1e-4 * scale
+            continue
         err = _rel(grads[1][n], grads[0][n])
         print(f"{n}: {err:.3g}")
-        assert err < tol * 2, n
+        assert err < _grad_tol(n, amp), n
 
 
 @pytest.mark.parametrize("amp", [False, True], ids=["f32", "bf16_autocast"])
@@ -242,19 +279,19 @@ def test_pixel_decoder_encoder_layer_matches_hf(amp):
     refp = torch.rand((B, S, 3, 2), device=DEV) * 0.9 + 0.05
     gy = torch.randn((B, S, 256), device=DEV)
     res = []
-    for m in (ref, hip):
+    for m, amp_ in ((ref, False), (hip, amp)):  # the HF arm in float32: the reference's arithmetic
         xx = x.clone().requires_grad_()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp_):
             y = m(xx, None, position_embeddings=pos, reference_points=refp, spatial_shapes_list=shapes,
                   level_start_index=start)[0]
         y.float().backward(gy)
         res.append((y.float(), xx.grad, _grads(m)))
     for k, arm in enumerate(("HF", "HIP")):
         assert torch.isfinite(res[k][0]).all() and torch.isfinite(res[k][1]).all(), f"{arm} arm not finite"
-    tol = 3e-2 if amp else 2e-4
+    tol = 5e-2 if amp else 2e-4
     assert _rel(res[1][0], res[0][0]) < tol
     assert _rel(res[1][1], res[0][1]) < tol
     for n in res[0][2]:
         err = _rel(res[1][2][n], res[0][2][n])
         print(f"{n}: {err:.3g}")
-        assert err < tol * 2, n
+        assert err < _grad_tol(n, amp), n

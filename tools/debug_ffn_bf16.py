@@ -40,3 +40,19 @@ with torch.autocast("cuda", dtype=torch.bfloat16):
     y = fc2(torch.relu(fc1(xa)))
 y.float().backward(gy)
 print("torch autocast fc1.weight.grad vs ref", rel(fc1.weight.grad, dw1_ref))
+
+# float64 truth (no bf16 rounding anywhere) and where each bf16 rounding moves dW1
+xd, w1d, w2d, gd = x.double(), fc1.weight.double(), fc2.weight.double(), gy.double()
+zd = xd @ w1d.t() + fc1.bias.double()
+hd = torch.relu(zd)
+dhd = (gd @ w2d) * (zd > 0)
+dw1_true = dhd.t() @ xd
+print("truth |dW1| max", float(dw1_true.abs().max()), " sum|terms| / |sum| ~", float((dhd.abs().t() @ xd.abs()).max() / dw1_true.abs().max()))
+print("ours vs truth", rel(dw1, dw1_true))
+print("bf16 emulation vs truth", rel(dw1_ref, dw1_true))
+print("torch autocast vs truth", rel(fc1.weight.grad, dw1_true))
+dh_x32 = (gd @ w2d) * (zd > 0)
+print("dW1 from f32 dh and bf16 X vs truth", rel(dhd.t() @ xb.double(), dw1_true))
+print("dW1 from bf16 dh and f32 X vs truth", rel(dh.double().t() @ xd, dw1_true))
+print("dh (ours) vs truth", rel(dh, dhd))
+print("h>0 mask flips", int(((h.float() > 0) != (zd > 0)).sum()), "of", zd.numel())
