@@ -14,8 +14,8 @@ Reference call sites (transformers 5.15, the modules the reference model instant
     v0.4.0: the reference detaches the colour features, custom_model.py:332-333).
 
 Precision follows the module being replaced: float32 inputs run the exact-f32 MFMA GEMMs; under
-torch.autocast(bfloat16) the GEMMs take bf16 operands (activations cast, weights cast once per
-weight version) with float32 sums and a bf16 output — what autocast's linear returns — and
+torch.autocast(bfloat16) the GEMMs take bf16 operands (activations and weights cast per call)
+with float32 sums and a bf16 output — what autocast's linear returns — and
 LayerNorm returns float32, as autocast's layer_norm does.  Weight gradients are written in
 float32 straight from the bf16 GEMM (autocast's path rounds them to bf16 first).
 
@@ -26,7 +26,6 @@ fc2's dX epilogue.  Inputs the kernels do not cover (CPU tensors, float16, Layer
 > 1536, dropout in training, GELU with gradients) take the module's own torch path.
 """
 import math
-import weakref
 
 import torch
 import torch.nn.functional as F
@@ -47,30 +46,14 @@ def compute_dtype(x: torch.Tensor):
     return x.dtype if x.dtype in _CODE else None
 
 
-_wcache = {}  # id(parameter) -> (weakref to it, version, data_ptr, dtype, cast copy)
-
-
 def cast_weight(w: torch.Tensor, dt):
-    """w (a parameter) in dtype dt, cast once per weight version (as autocast's cast cache does
-    within a region); never cached while a graph is being captured.  Keyed by id with a weak
-    reference to check identity (tensors compare elementwise, so they cannot be dict keys of a
-    WeakKeyDictionary); entries of dead parameters are dropped as they are found."""
+    """w (a parameter) in dtype dt for this call.  Not cached across calls: the fused AdamW step
+    updates parameters in place WITHOUT bumping their version counters (measured, torch 2.10),
+    so a copy keyed on (version, data_ptr) would silently go stale after the first step — the
+    bf16 training loss then falls visibly slower (tools/diag_bf16_model.py train)."""
     if w.dtype == dt:
         return w.detach()
-    if w.is_cuda and torch.cuda.is_current_stream_capturing():
-        return w.detach().to(dt)
-    key = id(w)
-    ent = _wcache.get(key)
-    if ent is not None:
-        ref, ver, ptr, edt, t = ent
-        if ref() is w and ver == w._version and ptr == w.data_ptr() and edt == dt:
-            return t
-        if ref() is None or ref() is not w:
-            del _wcache[key]
-    t = w.detach().to(dt)
-    if w._base is None:  # parameters, not per-call views (the chunks of an in_proj_weight)
-        _wcache[key] = (weakref.ref(w), w._version, w.data_ptr(), dt, t)
-    return t
+    return w.detach().to(dt)
 
 
 def _splits(M, N, K):

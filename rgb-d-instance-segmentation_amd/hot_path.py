@@ -114,24 +114,18 @@ def stack4(ts, view_only=False):
 
 
 class _PackCache:
-    """Packed implicit-GEMM weights.  float32 (segment form, code independent): re-packed only
-    when a parameter changes.  bfloat16 (code-merged form): packed on every call for the region
-    codes present in this batch (``code_mask``), into fresh tensors so a pending backward keeps
-    the filters its forward used; ``want_bwd`` adds the dX operand."""
-
-    def __init__(self):
-        self.key = None
-        self.val = None
+    """Packed implicit-GEMM weights, built on every call from the current parameters: float32 in
+    the segment form, bfloat16 in the code-merged form for the region codes present in this
+    batch (``code_mask``), into fresh tensors so a pending backward keeps the filters its forward
+    used; ``want_bwd`` adds the dX operand.  (No reuse keyed on parameter versions: the fused
+    AdamW step updates parameters in place without bumping their version counters, so such a
+    key would go stale after the first optimizer step.)"""
 
     def get(self, conv_ws, proj_w, dtype, code_mask=None, want_bwd=True):
         if dtype == torch.bfloat16:
             return ops.dsam_pack(stack4([w.detach() for w in conv_ws]), proj_w.detach(), dtype,
                                  code_mask=code_mask, want_bwd=want_bwd)
-        key = (dtype, proj_w.data_ptr(), proj_w._version) + tuple((w.data_ptr(), w._version) for w in conv_ws)
-        if key != self.key:
-            self.val = ops.dsam_pack(stack4([w.detach() for w in conv_ws]), proj_w.detach(), dtype)
-            self.key = key
-        return self.val
+        return ops.dsam_pack(stack4([w.detach() for w in conv_ws]), proj_w.detach(), dtype)
 
 
 class Prepared:

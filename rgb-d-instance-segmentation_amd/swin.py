@@ -29,22 +29,13 @@ from ._lib import check
 from .dense import _CODE, ACT_GELU, LayerNormFunction, cast_weight, compute_dtype, gemm
 from .ops import _p, _stream
 
-_qkv_cache = {}
-
-
 def _qkv_weights(attn, dt):
-    """[Wq; Wk; Wv] in dt and [bq; bk; bv] float32, rebuilt when a parameter version changes."""
+    """[Wq; Wk; Wv] in dt and [bq; bk; bv] float32, built per call (parameters can change in place
+    without a version bump: see dense.cast_weight)."""
     ps = (attn.q_proj.weight, attn.k_proj.weight, attn.v_proj.weight)
     bs = (attn.q_proj.bias, attn.k_proj.bias, attn.v_proj.bias)
-    key = (id(attn), dt)
-    ver = tuple((p._version, p.data_ptr()) for p in ps + tuple(b for b in bs if b is not None))
-    ent = _qkv_cache.get(key)
-    if ent is not None and ent[0] == ver and not torch.cuda.is_current_stream_capturing():
-        return ent[1], ent[2]
     w = torch.cat([cast_weight(p, dt) for p in ps], 0).contiguous()
     b = None if bs[0] is None else torch.cat([x.detach().float() for x in bs], 0).contiguous()
-    if not torch.cuda.is_current_stream_capturing():
-        _qkv_cache[key] = (ver, w, b)
     return w, b
 
 
