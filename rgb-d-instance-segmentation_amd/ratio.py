@@ -36,6 +36,10 @@ def _bns(module):
 
 
 def _packed(module, dtype):
+    # Reused while the parameters' (data_ptr, version) are unchanged.  In v0.4.0 the predictor's
+    # parameters never receive gradients (the ratio leaves the graph, Q2), so no optimizer steps
+    # them; load_state_dict copies bump the versions.  (A fused optimizer step would NOT: see
+    # dense.cast_weight — a trained predictor would need a re-pack per step.)
     ws = _weights(module)
     key = (dtype,) + tuple((w.data_ptr(), w._version) for w in ws)
     cache = getattr(module, "_rgbd_pack", None)
