@@ -112,9 +112,10 @@ struct GStage {
   static constexpr int CPR = KC ? KS / VEC : ROWS / VEC;     // chunks per stored row
   uint4 v[PER];
 
-  // rows [row0, row0 + ROWS) of nrows, k [k0, k0 + KS) of klim; vec: 16-byte loads allowed
+  // rows [row0, row0 + ROWS) of nrows, k [k0, k0 + KS) of klim; VL: 16-byte loads allowed
+  template <bool VL>
   __device__ __forceinline__ void load(const T* __restrict__ base, long long ld, int row0, int nrows, int k0,
-                                       int klim, bool vec, int tid) {
+                                       int klim, int tid) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int c = tid + G_THREADS * u;
@@ -124,7 +125,7 @@ struct GStage {
       const int row = KC ? row0 + major : row0 + minor;  // first row of the chunk
       const int k = KC ? k0 + minor : k0 + major;        // first k of the chunk
       const T* src = KC ? base + (long long)row * ld + k : base + (long long)k * ld + row;
-      if (vec) {
+      if constexpr (VL) {
         if (KC ? (row < nrows && k < klim) : (k < klim && row < nrows)) v[u] = *reinterpret_cast<const uint4*>(src);
       } else {
         T e[VEC];
@@ -223,15 +224,65 @@ __device__ __forceinline__ void g_store(const GArgs& a, int bz, int m, int n0, c
   }
 }
 
-template <typename T, int TM, int TN, bool AT, bool BT>
-__global__ __launch_bounds__(G_THREADS) void k_gemm(GArgs a) {
+// Epilogue staging: the float32 accumulator tile [TM][TN] in LDS, 16-byte chunk c of row m at
+// slot c ^ (m & (chunks - 1)) (conflict-free writes from the MFMA layout, conflict-free row reads).
+template <int TN>
+__device__ __forceinline__ int coff(int m, int chunk) {
+  constexpr int CH = TN / 4;
+  return (m * CH + (chunk ^ (m & (CH - 1)))) * 16;
+}
+
+// 8 consecutive outputs n0..n0+7 of row m: epilogue, store (16-byte stores when aligned)
+template <typename T>
+__device__ __forceinline__ void g_store8(const GArgs& a, int b, int bz, int m, int n0, float (&v)[8], bool vec_c) {
+  if (a.splits > 1) {  // float32 partial of this split, ld = N
+    float* p = a.part + ((long long)bz * a.M + m) * a.N + n0;
+    if (vec_c && n0 + 8 <= a.N) {
+      *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (n0 + e < a.N) p[e] = v[e];
+    }
+    return;
+  }
+  const long long rbase = (long long)b * a.sr + (long long)m * a.ldr + n0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (n0 + e < a.N) v[e] = g_epi<T>(v[e], n0 + e, rbase + e, a);
+  if (a.c_f32) {
+    float* c = reinterpret_cast<float*>(a.C) + (long long)b * a.sc + (long long)m * a.ldc + n0;
+    if (vec_c && n0 + 8 <= a.N) {
+      *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      for (int e = 0; e < 8; ++e)
+        if (n0 + e < a.N) c[e] = v[e];
+    }
+  } else {
+    T* c = reinterpret_cast<T*>(a.C) + (long long)b * a.sc + (long long)m * a.ldc + n0;
+    if constexpr (sizeof(T) == 2) {
+      if (vec_c && n0 + 8 <= a.N) {
+        *reinterpret_cast<uint4*>(c) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                  pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+        return;
+      }
+    }
+    for (int e = 0; e < 8; ++e)
+      if (n0 + e < a.N) c[e] = Num<T>::from_f(v[e]);
+  }
+}
+
+template <typename T, int TM, int TN, bool AT, bool BT, bool VEC>
+__global__ __launch_bounds__(G_THREADS) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_gemm(GArgs a) {
   using Cfg = GCfg<T>;
   constexpr int KS = Cfg::KS;
   using SA = GStage<T, !AT, TM>;
   using SB = GStage<T, !BT, TN>;
   constexpr int A_BYTES = SA::bytes(), B_BYTES = SB::bytes();
   constexpr int FM = TM / 32, FN = TN / 32;  // fragments per wave (2 x 2 waves)
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  constexpr int SMEM = 2 * (A_BYTES + B_BYTES) > TM * TN * 4 ? 2 * (A_BYTES + B_BYTES) : TM * TN * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
@@ -247,27 +298,27 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(GArgs a) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  SA sa;
-  SB sb;
+  // K stages through two register sets and two LDS buffers: the loads of stage kt + 2 are issued
+  // while stage kt is multiplied, and land in LDS one stage later (two stages of latency cover);
+  // the barrier between stages waits for LDS traffic only (loads stay in flight across it)
+  SA ra0, ra1;
+  SB rb0, rb1;
   const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
-  if (nk > 0) {
-    sa.load(Ab, a.lda, m_base, a.M, kbeg, kend, a.vec_a, tid);
-    sb.load(Bb, a.ldb, n_base, a.N, kbeg, kend, a.vec_b, tid);
-    sa.store(smem, tid);
-    sb.store(smem + A_BYTES, tid);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      const int k0 = kbeg + (kt + 1) * KS;
-      sa.load(Ab, a.lda, m_base, a.M, k0, kend, a.vec_a, tid);
-      sb.load(Bb, a.ldb, n_base, a.N, k0, kend, a.vec_b, tid);
-    }
+  auto load = [&](SA& ra, SB& rb, int kt) {
+    const int k0 = kbeg + kt * KS;
+    ra.template load<VEC>(Ab, a.lda, m_base, a.M, k0, kend, tid);
+    rb.template load<VEC>(Bb, a.ldb, n_base, a.N, k0, kend, tid);
+  };
+  auto put = [&](const SA& ra, const SB& rb, int buf) {
+    char* d = smem + buf * (A_BYTES + B_BYTES);
+    ra.store(d, tid);
+    rb.store(d + A_BYTES, tid);
+  };
+  auto compute = [&](int buf) {
     const char* s_a = smem + buf * (A_BYTES + B_BYTES);
     const char* s_b = s_a + A_BYTES;
-#pragma unroll
+    // one k-step's fragments live at a time (both unrolled, the 128 x 128 bf16 tile spills)
+#pragma unroll 1
     for (int ks = 0; ks < KS / 32; ++ks) {
       Frag<T> fm[FM], fn[FN];
 #pragma unroll
@@ -279,39 +330,49 @@ __global__ __launch_bounds__(G_THREADS) void k_gemm(GArgs a) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) mma(acc[j][i], fn[j], fm[i]);
     }
-    if (more) {
-      char* d = smem + (buf ^ 1) * (A_BYTES + B_BYTES);
-      sa.store(d, tid);
-      sb.store(d + A_BYTES, tid);
-    }
-    __syncthreads();
+  };
+  if (nk > 0) load(ra0, rb0, 0);
+  if (nk > 1) load(ra1, rb1, 1);
+  if (nk > 0) put(ra0, rb0, 0);
+  lds_barrier();
+  for (int kt = 0; kt < nk; kt += 2) {
+    if (kt + 2 < nk) load(ra0, rb0, kt + 2);
+    compute(0);
+    if (kt + 1 < nk) put(ra1, rb1, 1);
+    lds_barrier();
+    if (kt + 1 >= nk) break;
+    if (kt + 3 < nk) load(ra1, rb1, kt + 3);
+    compute(1);
+    if (kt + 2 < nk) put(ra0, rb0, 0);
+    lds_barrier();
   }
 
-  // lane (r, g): acc[j][i][e] = C[m = 16 (wm FM + i) + r][n = 16 (wn FN + j) + 4 g + e]
-  const int r = lane & 15, g = lane >> 4;
+  // epilogue: accumulators -> LDS (float32 tile) -> rows of 8 outputs per thread, coalesced
+  // 16-byte stores.  lane (r, g): acc[j][i][e] = C[m = 16 (wm FM + i) + r][n = 16 (wn FN + j) + 4 g + e]
+  {
+    const int r = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = m_base + 16 * (wm * FM + i) + r;
-    if (m >= a.M) continue;
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n0 = n_base + 16 * (wn * FN + j) + 4 * g;
-      if (n0 >= a.N) continue;
-      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-      if (a.splits > 1) {
-        float* p = a.part + ((long long)bz * a.M + m) * a.N + n0;
-        if (n0 + 3 < a.N && (a.N & 3) == 0)
-          *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-        else
-          for (int e = 0; e < 4; ++e)
-            if (n0 + e < a.N) p[e] = v[e];
-        continue;
+      for (int j = 0; j < FN; ++j) {
+        const int ml = 16 * (wm * FM + i) + r, ch = 4 * (wn * FN + j) + g;
+        *reinterpret_cast<f32x4*>(smem + coff<TN>(ml, ch)) = acc[j][i];
       }
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (n0 + e < a.N) v[e] = g_epi<T>(v[e], n0 + e, (long long)b * a.sr + (long long)m * a.ldr + n0 + e, a);
-      g_store<T>(a, b, m, n0, v);
-    }
+  }
+  lds_barrier();
+  const bool vec_c = a.splits > 1 ? (a.N % 4 == 0)
+                                  : ((a.N % 8 == 0) && (((uintptr_t)a.C) % 16 == 0) && (a.ldc % 8 == 0) &&
+                                     (a.sc % 8 == 0) && (!a.R || (a.ldr % 8 == 0 && a.sr % 8 == 0 && ((uintptr_t)a.R) % 16 == 0)));
+  constexpr int TPR = TN / 8, RPP = G_THREADS / TPR;  // threads per row, rows per pass
+  const int nl = (tid % TPR) * 8;
+#pragma unroll 1
+  for (int ml = tid / TPR; ml < TM; ml += RPP) {
+    const int m = m_base + ml, n0 = n_base + nl;
+    if (m >= a.M || n0 >= a.N) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4));
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4 + 1));
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    g_store8<T>(a, b, bz, m, n0, v, vec_c);
   }
 }
 
@@ -392,7 +453,10 @@ __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ 
 template <typename T, int TM, int TN, bool AT, bool BT>
 void launch_t(const GArgs& a, int batch, hipStream_t s) {
   dim3 grid(ceil_div(a.N, TN), ceil_div(a.M, TM), batch * a.splits);
-  hipLaunchKernelGGL((k_gemm<T, TM, TN, AT, BT>), grid, dim3(G_THREADS), 0, s, a);
+  if (a.vec_a && a.vec_b)
+    hipLaunchKernelGGL((k_gemm<T, TM, TN, AT, BT, true>), grid, dim3(G_THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_gemm<T, TM, TN, AT, BT, false>), grid, dim3(G_THREADS), 0, s, a);
 }
 
 template <typename T, int TM, int TN>
