@@ -80,6 +80,23 @@ int rgbd_instance_presence(const uint8_t* instance_map, int B, int H, int W, uin
 int rgbd_instance_masks(const uint8_t* instance_map, int H, int W, const int* ids, const int* image_of, int n,
                         float* masks, void* stream);
 
+/* ---------------------------------------------------------------- a11 resizes
+ * For frames not at model resolution, the resizes of map_10channel_case2 (dataloader.py:405-414):
+ * rgbd_resize_pil_bilinear: the image processor's PIL.Image.resize(BILINEAR) of uint8 images
+ *   src [B][H][W][C] (C = 3: colour / depth-as-RGB, C = 1) -> dst [B][out_h][out_w][C], bit-exact
+ *   to Pillow's Resample.c (horizontal pass first, 22-bit fixed-point coefficients);
+ * rgbd_resize_pil_nearest: PIL NEAREST (the instance map), any C;
+ * rgbd_resize_cv2_linear: cv2.resize(depth, INTER_LINEAR) of the 'L' depth [B][H][W] ->
+ *   [B][out_h][out_w] (OpenCV's 11-bit fixed-point linear resize; cv2 is absent here: unpinned).
+ * ws: rgbd_resize_workspace_size(B, H, W, C, out_h, out_w) bytes (tables + the horizontal pass). */
+size_t rgbd_resize_workspace_size(int B, int H, int W, int C, int out_h, int out_w);
+int rgbd_resize_pil_bilinear(const uint8_t* src, int B, int H, int W, int C, int out_h, int out_w, uint8_t* dst,
+                             void* ws, void* stream);
+int rgbd_resize_pil_nearest(const uint8_t* src, int B, int H, int W, int C, int out_h, int out_w, uint8_t* dst,
+                            void* ws, void* stream);
+int rgbd_resize_cv2_linear(const uint8_t* src, int B, int H, int W, int out_h, int out_w, uint8_t* dst, void* ws,
+                           void* stream);
+
 /* ---------------------------------------------------------------- K3 E-DSAM decomposition
  * Replaces, per image and ONCE for all three DSAMs, DSAModule.forward lines 661-687:
  * to_grayscale (custom_model.py:466-480) -> nanmin/nanmax -> np.histogram(512) ->

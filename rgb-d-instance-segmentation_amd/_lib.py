@@ -41,6 +41,10 @@ SIGNATURES = {
     "rgbd_pp_binary_maps": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rgbd_pack_mask_bits": (_I, [_P, _I, _LL, _P, _P, _P]),
     "rgbd_mask_intersections": (_I, [_P, _I, _P, _I, _LL, _P, _P]),
+    "rgbd_resize_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
+    "rgbd_resize_pil_bilinear": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "rgbd_resize_pil_nearest": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "rgbd_resize_cv2_linear": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rgbd_edsam_decompose_workspace_size": (_SZ, [_I]),
     "rgbd_edsam_decompose": (_I, [_P, _LL, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_edsam_decompose_masks": (_I, [_P, _LL, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P]),

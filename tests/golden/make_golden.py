@@ -21,6 +21,7 @@ Fixtures (SURVEY.md §8(c) "Golden vectors"):
   g4_ratio.npz       a3: EnhancedDepthImageRatioPredictor eval at 240x320, B=2
   g5_model.npz       a1+a12: full model eval forward at 320x240 (ratio, logits, sampled features)
   g6_grads.npz       one loss.backward() at 320x240 B=2 (eval mode): hot-path grad stats
+  g8_resize.npz      a11 for frames not at model resolution: the processor's resize (PIL)
 """
 import hashlib
 import json
@@ -310,7 +311,36 @@ def save_g1(rec):
     np.savez_compressed(OUT / "g1_decompose.npz", **out)
 
 
+def resize_fixture():
+    """G8 (a11, frames NOT at model resolution): the reference's image processor resizing a
+    scene to a square size (its PIL BILINEAR for the colour and depth-as-RGB images, NEAREST
+    for the instance map, then rescale + normalise + binary masks), as map_10channel_case2 calls
+    it (dataloader.py:405-410).  cv2.resize (:414) is absent here and not pinned."""
+    g8 = {}
+    for tag, (H, W, S) in {"small": (48, 80, 64), "c2": (480, 640, 320)}.items():
+        sc = synthetic.make_scene(synthetic.scene_seed(71, 0), H, W)
+        inst, inst2sem = golden_inputs.instance_map(sc)
+        depth_rgb = np.stack([sc["depth_u8"]] * 3, axis=-1)
+        mi = reference_processor(S, S)(images=[sc["rgb_u8"], depth_rgb], segmentation_maps=[inst, inst],
+                                        instance_id_to_semantic_id=inst2sem, return_tensors="np")
+        pv6 = mi["pixel_values"].reshape(-1, S, S).astype(np.float32)
+        masks, classes = np.asarray(mi["mask_labels"][0]).astype(np.float32), np.asarray(mi["class_labels"][0])
+        g8[f"{tag}_size"] = np.array([H, W, S])
+        g8[f"{tag}_pv6_sha"] = np.array(sha(pv6))
+        g8[f"{tag}_masks_sha"] = np.array(sha(masks))
+        g8[f"{tag}_masks_shape"] = np.array(masks.shape)
+        g8[f"{tag}_classes"] = classes.astype(np.int64)
+        if tag == "small":
+            g8["small_pv6"] = pv6
+            g8["small_masks"] = masks
+    np.savez_compressed(OUT / "g8_resize.npz", **g8)
+
+
 if __name__ == "__main__":
     sys.path.insert(0, str(Path(__file__).resolve().parent))
     import golden_inputs  # noqa: E402
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "resize":
+        resize_fixture()
+    else:
+        main()
+        resize_fixture()
