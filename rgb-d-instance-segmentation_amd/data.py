@@ -72,6 +72,7 @@ def instance_labels(instance_map: torch.Tensor, inst2sem, ignore_index: int = 0)
 
 
 def _resize(kind, src, out_h, out_w):
+    src = src.contiguous()  # frames may arrive as strided views (e.g. a channel-reversed decode)
     ops._need_cuda(src)
     if src.dtype != torch.uint8:
         raise ValueError("resize: uint8 frames expected")
