@@ -1199,9 +1199,6 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
   return o;
 }
 
-#ifndef C5_VAR
-#define C5_VAR 0
-#endif
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
                                                        bf16_t* __restrict__ y, float* __restrict__ slab) {
@@ -1269,66 +1266,29 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
     for (int st = 0; st < C3_STEPS; ++st) {
       // this step's DMA: B(st + 1) (or the next tile's B(0)), plus a piece of A (this tile's half 1
       // during steps 0-5, the next tile's half 0 during 9-14)
-      auto issue_step = [&]() -> int {
-        int na = 0;
-#if C5_VAR & 2
-        if (wave < 4) {  // loader half: waves 0-3 copy all 32 B pieces and 2 A pieces each
-          const int bs = st + 1 < C3_STEPS ? st + 1 : (has_next ? 0 : -1);
-          if (bs >= 0) {
-            const char* src = w5s + (size_t)bs * (C5 * 128) + wave * 8192 + 16 * lane;
-            const uint32_t dst = lds0 + C3_B_OFF + (bs & 1) * (C5 * 128) + wave * 8192;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) glds16(src + 1024 * k, dst + 1024 * k);
-          }
-          for (int u = 0; u < 2; ++u) {
-            if (st < 6) {
-              const int j = wave + 4 * (2 * st + u);
-              if (j < C3_APIECES) { issue_a(t, 1, j); ++na; }
-            } else if (st >= 9 && st < 15 && has_next) {
-              const int j = wave + 4 * (2 * (st - 9) + u);
-              if (j < C3_APIECES) { issue_a(tn, 0, j); ++na; }
-            }
-          }
-        }
-#else
-#if !(C5_VAR & 4)
-        if (st + 1 < C3_STEPS)
-          issue_b(st + 1);
-        else if (has_next)
-          issue_b(0);
-#endif
-#if C5_VAR & 8
-        if (false) {
-#else
-        if (st < 6) {
-#endif
-          const int j = wave + 8 * st;
-          if (j < C3_APIECES) {
-            issue_a(t, 1, j);
-            na = 1;
-          }
-        } else if (st >= 9 && st < 15 && has_next) {
-          const int j = wave + 8 * (st - 9);
-          if (j < C3_APIECES) {
-            issue_a(tn, 0, j);
-            na = 1;
-          }
-        }
-#endif
-        return na;
-      };
       int a_issued = 0;
-#if !(C5_VAR & 1)
-      a_issued = issue_step();
-#endif
+      if (st + 1 < C3_STEPS)
+        issue_b(st + 1);
+      else if (has_next)
+        issue_b(0);
+      if (st < 6) {
+        const int j = wave + 8 * st;
+        if (j < C3_APIECES) {
+          issue_a(t, 1, j);
+          a_issued = 1;
+        }
+      } else if (st >= 9 && st < 15 && has_next) {
+        const int j = wave + 8 * (st - 9);
+        if (j < C3_APIECES) {
+          issue_a(tn, 0, j);
+          a_issued = 1;
+        }
+      }
       const int h = st >= 9, tap = st - 9 * h, ky = tap / 3, kx = tap % 3;
       const char* sa = smem + h * (C3_APIX * 128);
       const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-#if C5_VAR & 1
-        if (ks == 1) a_issued = issue_step();  // MFMA-first: the DMA issue after the first half
-#endif
         Frag<bf16_t> fa[4], fb[8];
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
@@ -1344,17 +1304,10 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
       }
       // own DMA landed (except the A pieces just issued), own LDS reads done, then the barrier
-#if C5_VAR & 16
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      (void)a_issued;
-#else
-      if (a_issued == 2)
-        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (a_issued == 1)
+      if (a_issued == 1)
         asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
     }
     // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
     // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
