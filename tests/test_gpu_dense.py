@@ -115,15 +115,18 @@ def test_colsum():
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-@pytest.mark.parametrize("C", [96, 256, 768, 1000])
-def test_layernorm_fwd_bwd(dt, C):
+@pytest.mark.parametrize("C,rows", [(96, 333), (96, 20000), (192, 4097), (256, 333), (384, 3333), (768, 333),
+                                    (1536, 700), (1000, 333), (60, 777)])
+def test_layernorm_fwd_bwd(dt, C, rows):
+    """C % 4 == 0: the vectorised row-group kernels (many rows per wave, block partials of the
+    parameter gradients); C = 1000 / 60: the one-wave-per-row kernels."""
     from rgbd_amd import dense
     g = torch.Generator(device="cpu").manual_seed(C)
     ln = torch.nn.LayerNorm(C, eps=1e-5).to(DEV)
     with torch.no_grad():
         ln.weight.copy_(torch.randn(C, generator=g))
         ln.bias.copy_(torch.randn(C, generator=g))
-    x = (torch.randn((333, C), generator=g) * 3 + 1).to(DEV, dt).requires_grad_()
+    x = (torch.randn((rows, C), generator=g) * 3 + 1).to(DEV, dt).requires_grad_()
     y = dense.layer_norm(x, ln)
     assert y.dtype == dt
     gy = torch.randn(y.shape, generator=g).to(DEV, dt)
