@@ -457,7 +457,9 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
               long long sr, void* C, long long ldc, long long sc, int c_f32, int batch, int splits, void* ws,
               void* stream);
 /* rgbd_colsum: out[n] = sum over rows m of y[m * ld + n] (the bias gradient), float32, fixed
- * order (row chunks, then the chunks in order); ws: rgbd_colsum_workspace_size(rows, N) bytes. */
+ * order (row chunks, then the chunks in order), one launch; ws: rgbd_colsum_workspace_size(rows,
+ * N) bytes, ZERO before its first use (it starts with per-column-block tickets that every call
+ * leaves at zero again).  Calls sharing a workspace must be stream-ordered. */
 size_t rgbd_colsum_workspace_size(int rows, int N);
 int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* ws, void* stream);
 /* LayerNorm over the last dimension (nn.LayerNorm(C, eps) of the decoder layers :1700-1719, the

@@ -399,16 +399,27 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(GArgs a, int batch) 
   }
 }
 
-// bias gradient: out[n] = sum_m y[m][n], float32, fixed order, in two passes.
-// Pass 1: the rows in at most CS_MAXCH chunks; block = 256 columns x one chunk, 256 threads =
-// 32 column groups of 8 (one 16-byte load per row when aligned) x 8 row lanes; the 8 row lanes
-// fold through LDS in fixed order -> part[chunk][N].  Pass 2: per column, the chunks in order.
+// bias gradient: out[n] = sum_m y[m][n], float32, fixed order, in one launch.  The rows in at
+// most CS_MAXCH chunks; block = 256 columns x one chunk, 256 threads = 32 column groups of 8 (one
+// 16-byte load per row when aligned) x 8 row lanes folded through LDS in fixed order -> the
+// chunk's partial, stored write-through (sc1); the last chunk of a column block to take its
+// ticket (agent-scope counter, after every partial store drained) loads the partials sc1 and sums
+// them in chunk order (MI355X_MICROARCH.md visibility table, row 1), then rearms the ticket.
+// Bitwise the former two-pass result; one launch instead of two per bias.
 constexpr int CS_MAXCH = 64;
 
+inline int cs_chunks(int rows) { return std::min(CS_MAXCH, std::max(1, ceil_div(rows, 64))); }
+// the tickets occupy a fixed head of the workspace whatever N is, so calls of different widths on
+// one workspace never see each other's partials as tickets
+constexpr int CS_MAXBLK = 1024;  // column blocks: N <= 262 144
+inline size_t cs_ticket_bytes(int) { return CS_MAXBLK * sizeof(int); }
+
 template <typename T>
-__global__ __launch_bounds__(256) void k_colsum_part(const T* __restrict__ y, int rows, int N, long long ld, int chunk,
-                                                     int vec, float* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int rows, int N, long long ld, int chunk,
+                                                int vec, int* __restrict__ tickets, float* __restrict__ part,
+                                                float* __restrict__ out) {
   __shared__ float red[8][256];
+  __shared__ int last_s;
   const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int c0 = blockIdx.x * 256 + 8 * cg;
   const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
@@ -432,22 +443,28 @@ __global__ __launch_bounds__(256) void k_colsum_part(const T* __restrict__ y, in
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[rl][8 * cg + j] = acc[j];
   __syncthreads();
+  const int nch = gridDim.y;
+  const __amdgpu_buffer_rsrc_t prs = wt_rsrc(part, nch * N * (int)sizeof(float));
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < N) {
-    float s = 0.f;
+    float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += red[k][threadIdx.x];
-    part[(long long)blockIdx.y * N + c] = s;
+    for (int k = 0; k < 8; ++k) t += red[k][threadIdx.x];
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (blockIdx.y * N + c) * 4, 0, WT_SC1);
   }
-}
-
-__global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ part, int nch, int N,
-                                                      float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int k = 0; k < nch; ++k) s += part[(long long)k * N + c];
-  out[c] = s;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last_s = __hip_atomic_fetch_add(tickets + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
+  __syncthreads();
+  if (!last_s) return;
+  if (c < N) {
+    float t = 0.f;
+    for (int k = 0; k < nch; ++k)
+      t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (k * N + c) * 4, 0, WT_SC1));
+    out[c] = t;
+  }
+  if (threadIdx.x == 0) tickets[blockIdx.x] = 0;  // rearmed for the next call on this workspace
 }
 
 template <typename T, int TM, int TN, bool AT, bool BT>
@@ -532,25 +549,29 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
 }
 
 size_t rgbd_colsum_workspace_size(int rows, int N) {
-  return (size_t)std::min(CS_MAXCH, std::max(1, ceil_div(rows, 64))) * N * sizeof(float);
+  if (rows <= 0 || N <= 0) return 256;
+  return cs_ticket_bytes(N) + (size_t)cs_chunks(rows) * N * sizeof(float);
 }
 
 int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* ws, void* stream) {
   RGBD_REQUIRE(y && out && ws && rows > 0 && N > 0 && ld >= N, RGBD_E_ARG);
   RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  RGBD_REQUIRE(ceil_div(N, 256) <= CS_MAXBLK && (long long)cs_chunks(rows) * N * (long long)sizeof(float) < (1ll << 31),
+               RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
-  const int nch = std::min(CS_MAXCH, std::max(1, ceil_div(rows, 64)));
+  const int nch = cs_chunks(rows);
   const int chunk = ceil_div(rows, nch);
   const int esz = dtype == RGBD_BF16 ? 2 : 4;
   const int vec = (((uintptr_t)y) % 16 == 0) && ((ld * esz) % 16 == 0);
-  float* part = (float*)ws;
+  int* tickets = (int*)ws;
+  float* part = (float*)((char*)ws + cs_ticket_bytes(N));
   dim3 grid(ceil_div(N, 256), nch);
   if (dtype == RGBD_BF16)
-    hipLaunchKernelGGL(k_colsum_part<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)y, rows, N, ld, chunk, vec, part);
+    hipLaunchKernelGGL(k_colsum<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)y, rows, N, ld, chunk, vec, tickets,
+                       part, out);
   else
-    hipLaunchKernelGGL(k_colsum_part<float>, grid, dim3(256), 0, s, (const float*)y, rows, N, ld, chunk, vec, part);
-  RGBD_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_colsum_final, dim3(ceil_div(N, 256)), dim3(256), 0, s, part, nch, N, out);
+    hipLaunchKernelGGL(k_colsum<float>, grid, dim3(256), 0, s, (const float*)y, rows, N, ld, chunk, vec, tickets, part,
+                       out);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -96,7 +96,7 @@ def gemm(A, B, a_t, b_t, M, N, K, bias=None, act=ACT_NONE, R=None, c_f32=False, 
 def colsum(y2):
     out = torch.empty((y2.shape[1],), dtype=torch.float32, device=y2.device)
     L = _lib.lib()
-    ws = _workspace(y2.device, L.rgbd_colsum_workspace_size(y2.shape[0], y2.shape[1]), "colsum")
+    ws = _workspace(y2.device, L.rgbd_colsum_workspace_size(y2.shape[0], y2.shape[1]), "colsum", zeroed=True)
     check(L.rgbd_colsum(_CODE[y2.dtype], _p(y2), y2.shape[0], y2.shape[1], y2.stride(0), _p(out), _p(ws),
                         _stream(y2.device)), "rgbd_colsum")
     return out

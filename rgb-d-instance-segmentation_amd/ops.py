@@ -46,16 +46,18 @@ def _need_cuda(*ts):
             raise RuntimeError("rgbd_amd ops expect contiguous tensors")
 
 
-def _workspace(dev, nbytes: int, tag: str):
+def _workspace(dev, nbytes: int, tag: str, zeroed: bool = False):
     """Scratch buffer for one entry point, one per (device, tag, stream): launches on two
     streams never share one, and launches on one stream are ordered.  Never freed (see
-    ``_ws_retired``)."""
+    ``_ws_retired``).  ``zeroed``: a new buffer starts as zeros (entry points whose workspace
+    holds counters that each call leaves at zero, e.g. rgbd_colsum's tickets)."""
     key = (dev, tag, torch.cuda.current_stream(dev).cuda_stream)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
         if buf is not None:
             _ws_retired.append(buf)
-        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+        alloc = torch.zeros if zeroed else torch.empty
+        buf = alloc(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
         _ws_cache[key] = buf
     return buf
 

@@ -109,9 +109,16 @@ def test_gemm_batched():
 
 
 def test_colsum():
+    """One launch per call; the workspace's tickets must come back to zero after every call, so
+    repeated calls of different shapes on one workspace (and bf16) keep giving the column sums."""
     from rgbd_amd import dense
-    y = torch.randn((1234, 77), device=DEV)
-    assert _rel(dense.colsum(y), y.double().sum(0)) < 1e-6
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for rows, N, dt in [(1234, 77, torch.float32), (50400, 256, torch.bfloat16), (7, 1000, torch.float32),
+                        (1234, 77, torch.float32), (153600, 384, torch.bfloat16), (64, 3000, torch.float32)]:
+        y = torch.randn((rows, N), generator=g).to(DEV, dt)
+        first = dense.colsum(y)
+        assert _rel(first, y.double().sum(0)) < 1e-5, (rows, N, dt)
+        assert torch.equal(dense.colsum(y), first)  # deterministic, tickets rearmed
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
