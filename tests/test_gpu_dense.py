@@ -97,6 +97,29 @@ def test_gemm_split_k_weight_gradient(dt):
     assert torch.equal(dW, dense.gemm(dY, X, 1, 1, N, K, M, c_f32=True))
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_gemm_split_k_epilogue_batched_and_reuse(dt):
+    """Split-K in one launch: the last split of each output tile sums the partials in split order
+    and applies the epilogue (bias + ReLU, residual), batched, with ragged M / N; successive calls
+    of different shapes share the workspace (its tickets come back to zero)."""
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(9)
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    for batch, M, N, K in [(1, 100, 72, 8192), (3, 64, 130, 4096), (1, 256, 256, 50400), (2, 40, 24, 3000)]:
+        assert dense._splits(M, N, K) > 1, (M, N, K)
+        A = torch.randn((batch, M, K), generator=g).to(DEV, dt)
+        B = torch.randn((batch, N, K), generator=g).to(DEV, dt)
+        bias = torch.randn((N,), generator=g).to(DEV)
+        R = torch.randn((batch, M, N), generator=g).to(DEV, dt)
+        C = dense.gemm(A, B, 0, 0, M, N, K, bias=bias, act=dense.ACT_RELU, R=R, batch=batch, sa=M * K, sb=N * K,
+                       sr=M * N)
+        ref = torch.relu(A.double() @ B.double().transpose(1, 2) + bias.double()) + R.double()
+        assert _rel(C.view(batch, M, N), ref) < tol, (batch, M, N, K)
+        C2 = dense.gemm(A, B, 0, 0, M, N, K, bias=bias, act=dense.ACT_RELU, R=R, batch=batch, sa=M * K, sb=N * K,
+                        sr=M * N)
+        assert torch.equal(C, C2)
+
+
 def test_gemm_batched():
     from rgbd_amd import dense
     g = torch.Generator(device="cpu").manual_seed(9)
