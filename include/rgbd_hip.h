@@ -478,6 +478,20 @@ int rgbd_layernorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy,
                        const float* mean, const float* rstd, int rows, int C, void* dx, float* dgamma,
                        float* dbeta, void* ws, void* stream);
 
+/* f2 GroupNorm (nn.GroupNorm of the pixel decoder: the input projections, the FPN adapter and the
+ * FPN output layer — transformers 5.15 modeling_mask2former.py Mask2FormerPixelDecoder.__init__,
+ * called from Mask2FormerPixelDecoder.forward; custom_model.py:383), NCHW [B][C][HW], G groups
+ * of C / G consecutive channels, biased variance (torch).  relu = 1 fuses the ReLU that follows
+ * the FPN output layer's norm.  mean_rstd: [B][G][2] float32, written by the forward and read
+ * by the backward.  ws: rgbd_groupnorm_workspace_size(B, C) bytes (per-channel partials).
+ * Backward: dx in x's dtype; dgamma / dbeta may be NULL (no affine). */
+size_t rgbd_groupnorm_workspace_size(int B, int C);
+int rgbd_groupnorm_fwd(int x_dtype, const void* x, const float* gamma, const float* beta, int B, int C, int G, int HW,
+                       float eps, int relu, int y_dtype, void* y, float* mean_rstd, void* ws, void* stream);
+int rgbd_groupnorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy, const float* gamma, const float* beta,
+                       const float* mean_rstd, int B, int C, int G, int HW, int relu, void* dx, float* dgamma,
+                       float* dbeta, void* ws, void* stream);
+
 /* ---------------------------------------------------------------- f2 Swin-T window attention
  * The (shifted-)window self-attention core of every SwinLayer of the backbone
  * (transformers 5.15 modeling_swin.py SwinLayer.forward :529-582 with SwinAttention :418-468):

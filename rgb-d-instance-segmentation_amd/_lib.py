@@ -99,6 +99,9 @@ SIGNATURES = {
     "rgbd_layernorm_fwd": (_I, [_I, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P]),
     "rgbd_layernorm_bwd_workspace_size": (_SZ, [_I, _I]),
     "rgbd_layernorm_bwd": (_I, [_I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "rgbd_groupnorm_workspace_size": (_SZ, [_I, _I]),
+    "rgbd_groupnorm_fwd": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, ctypes.c_float, _I, _I, _P, _P, _P, _P]),
+    "rgbd_groupnorm_bwd": (_I, [_I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_swin_window_attn": (_I, [_I, _P, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
                                    _LL, _P]),
     "rgbd_timing_enable": (_I, [_I]),

@@ -212,6 +212,67 @@ class LayerNormFunction(torch.autograd.Function):
         return (dx.to(ctx.x_dtype).view(gy.shape), dg if ctx.has_g else None, db if ctx.has_b else None, None, None)
 
 
+class GroupNormFunction(torch.autograd.Function):
+    """nn.GroupNorm (+ the ReLU after it when ``relu``) on rgbd_groupnorm_fwd / _bwd, NCHW."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, groups, eps, relu, y_dtype):
+        xc = x if x.dtype in _CODE else x.float()
+        xc = xc.contiguous()
+        B, C = xc.shape[0], xc.shape[1]
+        HW = xc.numel() // max(B * C, 1)
+        y = torch.empty(xc.shape, dtype=y_dtype, device=x.device)
+        mr = torch.empty((B, groups, 2), dtype=torch.float32, device=x.device)
+        g32 = None if gamma is None else gamma.detach().float().contiguous()
+        b32 = None if beta is None else beta.detach().float().contiguous()
+        L = _lib.lib()
+        ws = _workspace(x.device, L.rgbd_groupnorm_workspace_size(B, C), "gn")
+        check(L.rgbd_groupnorm_fwd(_CODE[xc.dtype], _p(xc), _p(g32), _p(b32), B, C, groups, HW, float(eps), int(relu),
+                                   _CODE[y_dtype], _p(y), _p(mr), _p(ws), _stream(x.device)), "rgbd_groupnorm_fwd")
+        ctx.save_for_backward(xc, g32, b32, mr)
+        ctx.groups, ctx.relu, ctx.x_dtype = groups, relu, x.dtype
+        ctx.has_g, ctx.has_b = gamma is not None, beta is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, g32, b32, mr = ctx.saved_tensors
+        B, C = xc.shape[0], xc.shape[1]
+        HW = xc.numel() // max(B * C, 1)
+        g2 = gy if gy.dtype in _CODE else gy.float()
+        g2 = g2.contiguous()
+        dx = torch.empty_like(xc)
+        dg = torch.empty((C,), dtype=torch.float32, device=xc.device)
+        db = torch.empty_like(dg)
+        L = _lib.lib()
+        ws = _workspace(xc.device, L.rgbd_groupnorm_workspace_size(B, C), "gn")
+        check(L.rgbd_groupnorm_bwd(_CODE[xc.dtype], _p(xc), _CODE[g2.dtype], _p(g2), _p(g32), _p(b32), _p(mr), B, C,
+                                   ctx.groups, HW, int(ctx.relu), _p(dx), _p(dg), _p(db), _p(ws), _stream(xc.device)),
+              "rgbd_groupnorm_bwd")
+        return (dx.to(ctx.x_dtype), dg if ctx.has_g else None, db if ctx.has_b else None, None, None, None, None)
+
+
+class HipGroupNorm(nn.GroupNorm):
+    """nn.GroupNorm on the HIP kernels; ``_fused_relu`` (set by ``install`` when a ReLU follows in
+    the same nn.Sequential, Mask2FormerPixelDecoder's FPN output layer) applies that ReLU too."""
+    _fused_relu = False
+
+    def forward(self, x):
+        if not x.is_cuda or x.numel() == 0 or x.dim() < 2 or x.dtype not in _CODE:
+            y = super().forward(x)
+            return torch.relu(y) if self._fused_relu else y
+        y_dtype = torch.float32 if torch.is_autocast_enabled("cuda") else x.dtype
+        return GroupNormFunction.apply(x, self.weight if self.affine else None, self.bias if self.affine else None,
+                                       self.num_groups, self.eps, self._fused_relu, y_dtype)
+
+
+class _FusedReLU(nn.ReLU):
+    """The ReLU after a HipGroupNorm that already applied it (identity)."""
+
+    def forward(self, x):
+        return x
+
+
 def linear(x, w, b=None, act=ACT_NONE):
     dt = compute_dtype(x)
     return LinearFunction.apply(x, w, b, act, dt)
@@ -354,19 +415,29 @@ def install(model: nn.Module) -> int:
     for m in model.modules():
         n += _install_class(m, nn.Linear, HipLinear)
         n += _install_class(m, nn.LayerNorm, HipLayerNorm)
+        n += _install_class(m, nn.GroupNorm, HipGroupNorm)
         n += _install_class(m, *cls["decoder"])
         n += _install_class(m, *cls["encoder"])
+    for m in model.modules():  # GroupNorm -> ReLU pairs (the pixel decoder's FPN output layer)
+        if isinstance(m, nn.Sequential):
+            ch = list(m.children())
+            for a, b in zip(ch, ch[1:]):
+                if type(a) is HipGroupNorm and type(b) is nn.ReLU and not b.inplace:
+                    a._fused_relu = True
+                    b.__class__ = _FusedReLU
     return n
 
 
 def uninstall(model: nn.Module) -> int:
     cls = _classes()
-    back = {HipLinear: nn.Linear, HipLayerNorm: nn.LayerNorm, cls["decoder"][1]: cls["decoder"][0],
-            cls["encoder"][1]: cls["encoder"][0]}
+    back = {HipLinear: nn.Linear, HipLayerNorm: nn.LayerNorm, HipGroupNorm: nn.GroupNorm, _FusedReLU: nn.ReLU,
+            cls["decoder"][1]: cls["decoder"][0], cls["encoder"][1]: cls["encoder"][0]}
     n = 0
     for m in model.modules():
         b = back.get(type(m))
         if b is not None:
+            if isinstance(m, HipGroupNorm):
+                m.__dict__.pop("_fused_relu", None)
             m.__class__ = b
-            n += 1
+            n += b is not nn.ReLU
     return n

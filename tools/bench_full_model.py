@@ -39,7 +39,7 @@ def main():
     mask_labels = [torch.from_numpy(s["masks"].astype(np.float32)).to(dev) for s in scenes]
     class_labels = [torch.from_numpy(s["classes"]).to(dev) for s in scenes]
     res = {"batch": B, "shape": f"{W}x{H}", "amp_bf16": bool(args.amp)}
-    for arm in args.arms.split(","):
+    for ai, arm in enumerate(args.arms.split(",")):
         torch.manual_seed(0)
         m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
         winit.init_deterministic(m)
@@ -51,6 +51,13 @@ def main():
             point_loss.uninstall(m)
             dense.uninstall(m)
             swin.uninstall(m)
+        if arm == "hip_nogn":  # A/B: the pixel decoder's GroupNorms back on torch
+            for mod in m.modules():
+                if type(mod) is dense.HipGroupNorm:
+                    mod.__dict__.pop("_fused_relu", None)
+                    mod.__class__ = torch.nn.GroupNorm
+                elif type(mod) is dense._FusedReLU:
+                    mod.__class__ = torch.nn.ReLU
         opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, fused=True)
 
         def step():
@@ -69,7 +76,8 @@ def main():
             loss = step()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
-        res[arm] = {"img_s": round(B / dt, 2), "ms_per_step": round(dt * 1e3, 1), "loss": round(float(loss.detach()), 4)}
+        key = arm if arm not in res else f"{arm}_{ai}"
+        res[key] = {"img_s": round(B / dt, 2), "ms_per_step": round(dt * 1e3, 1), "loss": round(float(loss.detach()), 4)}
         del m, opt
         torch.cuda.empty_cache()
     if "hip" in res and "hf" in res:
