@@ -492,8 +492,8 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, 
 // gets the codes with bit i, proj gets all): work ~ one dense dW instead of popcount + 1 of them.
 // A unit is 64 raster-consecutive output pixels of one image.  Load balance: one code (the
 // remainder region) typically meets every unit while the others meet a few percent, so
-// k_wg_plan builds per-code lists of live units (k_code_presence) and cuts them into items of
-// about equal length; k_wg_masks precomputes, per list entry and tap, the 64-bit mask of the
+// wg_plan_body builds per-code lists of live units (code_presence_body) and cuts them into items of
+// about equal length; wg_masks_body precomputes, per list entry and tap, the 64-bit mask of the
 // unit's pixels whose source meets code k; k_dsam_wgrad_mm runs persistently over
 // (item, output tile) work.
 //
@@ -541,11 +541,11 @@ struct WgArgs {
   int dbg;                // RGBD_WG_DBG (timing experiments only): 1 = no steps, 2 = no partial stores
 };
 
-__global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict__ code, int B, int h, int w,
-                                                       uint16_t* __restrict__ pres) {
+__device__ __forceinline__ void code_presence_body(const uint8_t* __restrict__ code, int B, int h, int w,
+                                                   uint16_t* __restrict__ pres, int block) {
   // one wave per 64-px unit: OR of 1 << code over its 9-tap sources
   const int ho = (h + 1) / 2, wo = (w + 1) / 2, hwo = ho * wo, nunit = (hwo + WPX - 1) / WPX;
-  const long long u = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+  const long long u = (block * (long long)blockDim.x + threadIdx.x) >> 6;
   const int l = threadIdx.x & 63;
   uint32_t m = 0u;
   if (u < (long long)B * nunit) {
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void k_code_presence(const uint8_t* __restrict
 // Plan (one 1024-thread workgroup): per code the ordered list of live units, then items of
 // about equal length L = ceil(entries / (target / output tiles)), capped at WITEM_MAX.
 constexpr int WG_PRES_LDS = 8192;  // presence entries k_wg_plan keeps in LDS
-__global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
+__device__ __forceinline__ void wg_plan_body(const WgArgs& a) {
   __shared__ int cnt_s[16], off_s[17];
   if (threadIdx.x < LD_ZERO_BYTES / 16)
     reinterpret_cast<uint4*>(const_cast<bf16_t*>(a.zero))[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
@@ -666,8 +666,8 @@ __global__ __launch_bounds__(1024) void k_wg_plan(WgArgs a) {
 }
 
 // Tap masks of every live entry: one wave per entry, lane = pixel of the unit.
-__global__ __launch_bounds__(256) void k_wg_masks(WgArgs a) {
-  const int e = (blockIdx.x * 256 + threadIdx.x) >> 6, l = threadIdx.x & 63;
+__device__ __forceinline__ void wg_masks_body(const WgArgs& a, int block) {
+  const int e = (block * 256 + threadIdx.x) >> 6, l = threadIdx.x & 63;
   if (e >= a.counts[0]) return;  // wave-uniform
   const int v = a.list[e], u = v & 0xffffff, k = v >> 24;
   const int hwo = a.ho * a.wo, b = u / a.nunit, p = (u % a.nunit) * WPX + l;
@@ -685,6 +685,26 @@ __global__ __launch_bounds__(256) void k_wg_masks(WgArgs a) {
     const unsigned long long m = __ballot(cv[tap] == (uint32_t)k);
     if (l == 0) a.masks[(long long)e * 9 + tap] = m;
   }
+}
+
+// The dW planning of up to WG_MAXLEG legs in three launches (blockIdx.z = leg; blocks past a
+// leg's own count exit): unit presence, the per-code lists and items, the tap masks.
+constexpr int WG_MAXLEG = 4;
+struct WgLegs {
+  WgArgs a[WG_MAXLEG];
+  int max_entries[WG_MAXLEG];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_code_presence_legs(const WgLegs L) {
+  const WgArgs& a = L.a[blockIdx.z];
+  if ((long long)blockIdx.x * 256 >= (long long)a.B * a.nunit * 64) return;  // block-uniform
+  code_presence_body(a.code, a.B, a.h, a.w, const_cast<uint16_t*>(a.pres), blockIdx.x);
+}
+__global__ __launch_bounds__(1024) void k_wg_plan_legs(const WgLegs L) { wg_plan_body(L.a[blockIdx.z]); }
+__global__ __launch_bounds__(256) void k_wg_masks_legs(const WgLegs L) {
+  const WgArgs& a = L.a[blockIdx.z];
+  if ((long long)blockIdx.x * 4 >= L.max_entries[blockIdx.z]) return;  // block-uniform
+  wg_masks_body(a, blockIdx.x);
 }
 
 template <int FM>
@@ -2027,12 +2047,21 @@ static bool wg_shape_ok(int B, int Cin, int h, int w, int Cout, const WgPlan& P)
   return Cin % 32 == 0 && Cout % 32 == 0 && hwo < (1ll << 22) && (long long)B * h * w < (1ll << 31) &&
          (long long)B * P.nunit < (1 << 24);
 }
-// the code-dependent part of a dW leg: unit presence, the per-code live lists and items, tap masks
-static void wg_plan_launch(const WgArgs& a, const WgPlan& P, hipStream_t s) {
-  const long long nthr = (long long)a.B * P.nunit * 64;
-  k_code_presence<<<(int)ceil_div(nthr, 256), 256, 0, s>>>(a.code, a.B, a.h, a.w, const_cast<uint16_t*>(a.pres));
-  k_wg_plan<<<1, 1024, 0, s>>>(a);
-  k_wg_masks<<<ceil_div((long long)P.max_entries, 4), 256, 0, s>>>(a);
+// the code-dependent part of n dW legs: unit presence, the per-code live lists and items, tap
+// masks — three launches for all legs
+static void wg_plan_launch(int n, const WgArgs* a, const WgPlan* P, hipStream_t s) {
+  WgLegs L = {};
+  L.n = n;
+  long long pres_blocks = 1, mask_blocks = 1;
+  for (int i = 0; i < n; ++i) {
+    L.a[i] = a[i];
+    L.max_entries[i] = P[i].max_entries;
+    pres_blocks = std::max<long long>(pres_blocks, ceil_div((long long)a[i].B * P[i].nunit * 64, 256));
+    mask_blocks = std::max<long long>(mask_blocks, ceil_div((long long)P[i].max_entries, 4));
+  }
+  k_code_presence_legs<<<dim3((unsigned)pres_blocks, 1, n), 256, 0, s>>>(L);
+  k_wg_plan_legs<<<dim3(1, 1, n), 1024, 0, s>>>(L);
+  k_wg_masks_legs<<<dim3((unsigned)mask_blocks, 1, n), 256, 0, s>>>(L);
 }
 
 size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int w, int Cout) {
@@ -2070,7 +2099,7 @@ static int bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, c
     RGBD_REQUIRE(wg_shape_ok(B, Cin, h, w, Cout, P), RGBD_E_SHAPE);
     char* plan = planned ? (char*)planned : (char*)ws;
     const WgArgs a = wg_args(L, P, plan, partial, gout_nhwc, x_nhwc, code, B, Cin, h, w, Cout);
-    if (!planned) wg_plan_launch(a, P, s);
+    if (!planned) wg_plan_launch(1, &a, &P, s);
     const int grid = 256;  // persistent: one LDS-bound workgroup per CU
     const hipError_t e = P.fm == 6 ? launch_wg<6>(a, grid, s) : P.fm == 4 ? launch_wg<4>(a, grid, s) : launch_wg<2>(a, grid, s);
     if (e != hipSuccess) return (int)e;
@@ -2144,16 +2173,19 @@ int rgbd_dsam_plan(int n, const rgbd_dsam_leg* legs, void* stream) {
   RGBD_REQUIRE(n > 0 && legs, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
   ConvArgs conv[PLAN_MAXLEG];
-  int nconv = 0;
+  WgArgs wga[WG_MAXLEG];
+  WgPlan wgp[WG_MAXLEG];
+  int nconv = 0, nwg = 0;
   for (int i = 0; i < n; ++i) {
     const rgbd_dsam_leg& g = legs[i];
     RGBD_REQUIRE(leg_ok(g) && g.code && g.plan, RGBD_E_ARG);
     if (g.kind == RGBD_LEG_DW) {
+      RGBD_REQUIRE(nwg < WG_MAXLEG, RGBD_E_ARG);
       const WgPlan P = wg_plan(g.B, g.Cin, g.h, g.w, g.Cout);
       RGBD_REQUIRE(wg_shape_ok(g.B, g.Cin, g.h, g.w, g.Cout, P), RGBD_E_SHAPE);
       const WgradWs L = wgrad_ws(RGBD_BF16, g.B, g.Cin, g.h, g.w, g.Cout);
-      wg_plan_launch(wg_args(L, P, (char*)g.plan, nullptr, nullptr, nullptr, g.code, g.B, g.Cin, g.h, g.w, g.Cout), P,
-                     s);
+      wgp[nwg] = P;
+      wga[nwg++] = wg_args(L, P, (char*)g.plan, nullptr, nullptr, nullptr, g.code, g.B, g.Cin, g.h, g.w, g.Cout);
       continue;
     }
     RGBD_REQUIRE(nconv < PLAN_MAXLEG, RGBD_E_ARG);
@@ -2166,6 +2198,7 @@ int rgbd_dsam_plan(int n, const rgbd_dsam_leg* legs, void* stream) {
     const hipError_t e = plan_convs(nconv, conv, s);
     if (e != hipSuccess) return (int)e;
   }
+  if (nwg) wg_plan_launch(nwg, wga, wgp, s);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
