@@ -43,7 +43,6 @@ struct ConvArgs {
   void* out_nchw;                   // optional
   void* out_nhwc;                   // optional
   int ksplit;                       // unused (1)
-  int dbg;                          // diagnostics (RGBD_DSAM_DBG): 1 skip steps, 2 epilogue, 4 hand-off, 8 loop DMA
   uint16_t* tmasks;                 // bf16: [class][tile][16] per-tap code sets (k_dsam_plan)
   int* items;                       // bf16: work list of k_dsam_lds (k_dsam_items)
   int* nitems;
@@ -538,7 +537,6 @@ struct WgArgs {
   float inv_wo;
   const bf16_t* zero;     // LD_ZERO_BYTES of zeros (rows the im2col gather masks out)
   float* partial;         // [item][Cout][9*Cin] f32
-  int dbg;                // RGBD_WG_DBG (timing experiments only): 1 = no steps, 2 = no partial stores
 };
 
 __device__ __forceinline__ void code_presence_body(const uint8_t* __restrict__ code, int B, int h, int w,
@@ -755,7 +753,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
     __syncthreads();  // every thread has it before the unit ids overwrite the slot
     if (wi >= nwork) break;
     const int4 item = a.items[wi / ntile];
-    const int tile = wi % ntile, e0 = item.y, nst = (a.dbg & 1) ? 0 : item.z - item.y;
+    const int tile = wi % ntile, e0 = item.y, nst = item.z - item.y;
     const int kk0 = (tile % a.ntile_kk) * 128, o0 = (tile / a.ntile_kk) * 32 * FM;
     // stage the item's unit ids and tap masks
     for (int i = tid; i < nst; i += 256) sunits[i] = a.list[e0 + i] & 0xffffff;
@@ -836,7 +834,6 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
       else vm_wait_barrier<0>();
     }
     float* dst = a.partial + ((long long)(wi / ntile) * a.Cout) * KK;
-    if (!(a.dbg & 2))
 #pragma unroll
     for (int mi = 0; mi < FM; ++mi)
 #pragma unroll
@@ -1324,7 +1321,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   const int* steptab = (const int*)(smem + Cfg::STEPTAB);
   const bf16_t* zrow = a.zero + achk;
   const int s0 = (int)((long long)chunk * total / nc), s1 = (int)((long long)(chunk + 1) * total / nc);
-  const int nst = (a.dbg & 1) ? 0 : s1 - s0;
+  const int nst = s1 - s0;
   auto issue = [&](int slot, int s) {  // step s (absolute)
     const int e = __builtin_amdgcn_readfirstlane(steptab[s]);
     const int t = e & 15, cg = (e >> 4) & 255, code = e >> 12;
@@ -1359,7 +1356,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   else vm_wait_barrier<0>();
 #pragma unroll 1
   for (int s = 0; s < nst; ++s) {
-    if (s + S - 1 < nst && !(a.dbg & 8)) issue((s + S - 1) % S, s0 + s + S - 1);  // bit 8: no DMA in the loop
+    if (s + S - 1 < nst) issue((s + S - 1) % S, s0 + s + S - 1);
     const char* sa = smem + (s % S) * Cfg::STAGE;
     // fragments of chunk kc+1 are read while chunk kc's 12 MFMAs run
     Frag<bf16_t> fa[2][4], fb[2][3];
@@ -1389,7 +1386,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     if (ahead <= 0) vm_wait_barrier<0>();
     else vm_wait_barrier_dyn(ahead * cnt);
   }
-  if (nc > 1 && !(a.dbg & 4)) {  // RGBD_DSAM_DBG bit 4: no hand-off (timing experiments only)
+  if (nc > 1) {
     // Multi-chunk tile: publish this chunk's fragment-native partial ([wave][mi][nj][lane][4] f32),
     // take a ticket; the chunk that draws nc-1 sums all partials in chunk order (deterministic)
     // and runs the epilogue.  The hand-off is write-through: every partial byte is stored and
@@ -1438,7 +1435,6 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   // ---- epilogue (same contract as k_conv_igemm), staged through LDS in two 96-column halves:
   // pass 1 runs along pixels (NCHW residual loads and stores), pass 2 along channels (NHWC);
   // every thread's loads of a pass are independent and issued together.
-  if (a.dbg & 2) return;  // RGBD_DSAM_DBG=2: no epilogue (timing experiments only)
   if (!a.out_nchw) {
     // NHWC-only epilogue (the hot path's forward cascade and dX): one pass.  The accumulators go
     // to an LDS image [128 rows][196] f32 (rows = tile pixels; the 4-float pad makes the 4 rows
@@ -1624,21 +1620,11 @@ __global__ __launch_bounds__(512, 1) void k_dsam_lds(ConvArgs a) {
 long long conv_mmax(const ConvArgs& a) {
   return a.transposed ? (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2) : (long long)a.B * a.Ho * a.Wo;
 }
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-int ld_kc(int C) {
-  static const int force = env_int("RGBD_DSAM_KC", 0);  // tuning override
-  if (force == 1 || (force == 2 && C % 64 == 0) || (force == 3 && C % 96 == 0)) return force;
-  return C % 96 == 0 ? 3 : (C % 64 == 0 ? 2 : 1);
-}
+int ld_kc(int C) { return C % 96 == 0 ? 3 : (C % 64 == 0 ? 2 : 1); }
 // k_dsam_lds tiling of a conv: tiles of the largest parity class, N tiles
 // Linear tiles when 8 x 16 blocks would leave more than 15 % of the rows dead (the small grids:
-// dsam1 / dsam2 outputs, their dX parity classes); RGBD_DSAM_LINEAR=0/1 forces (A/B)
+// dsam1 / dsam2 outputs, their dX parity classes)
 int ld_linear(int Hc, int Wc) {
-  static const int force = env_int("RGBD_DSAM_LINEAR", -1);
-  if (force >= 0) return force;
   const long long blk = (long long)((Hc + 7) / 8 * 8) * ((Wc + 15) / 16 * 16);
   return (long long)Hc * Wc * 100 < 85 * blk;
 }
@@ -1654,10 +1640,10 @@ LdPlan ld_plan(const ConvArgs& a) {
   p.ntiles0 = p.linear ? (int)(((long long)a.B * Hc0 * Wc0 + LD_BM - 1) / LD_BM) : a.B * ((Hc0 + 7) / 8) * ((Wc0 + 15) / 16);
   p.ntn = ceil_div(a.N, LD_BN);
   p.kc = ld_kc(a.C);
-  // chunk length in steps: pct % of a dense tile (one code per tap); tuning override
-  static const int pct = env_int("RGBD_DSAM_CHUNK_PCT", 100);
+  // chunk length in steps: one dense tile (one code per tap); 60 % and 150 % measured slower
+  // (K5 0.74 / 0.78 vs 0.71 ms per step, round 3)
   const int ntap = a.transposed ? 4 : 9;  // class 3 of dX has 4 live taps
-  p.chunk_len = std::max(1, (ntap * (a.C / (32 * p.kc)) * pct + 99) / 100);
+  p.chunk_len = std::max(1, ntap * (a.C / (32 * p.kc)));
   p.tmask_bytes = align256((size_t)nclass * p.ntiles0 * 16 * sizeof(uint16_t));
   p.items_bytes = align256(((size_t)nclass * p.ntiles0 * LD_CH + 1) * sizeof(int));
   p.ticket_bytes = align256((size_t)(nclass * p.ntiles0 * p.ntn + 64) * sizeof(int)) + LD_ZERO_BYTES;  // + work counters
@@ -1674,8 +1660,6 @@ size_t v2_partial_bytes(const ConvArgs& a) {
 ConvArgs conv_carve(const ConvArgs& a, const LdPlan& P, char* plan, float* partial) {
   ConvArgs b = a;
   const int nclass = a.transposed ? 4 : 1;
-  static const int dbg = env_int("RGBD_DSAM_DBG", 0);
-  b.dbg = dbg;
   b.tmasks = (uint16_t*)plan;
   b.items = (int*)(plan + P.tmask_bytes);
   b.nitems = b.items + (size_t)nclass * P.ntiles0 * LD_CH;
@@ -1739,7 +1723,7 @@ int launch_conv(const ConvArgs& a, hipStream_t s, const void* planned = nullptr)
       if (pe != hipSuccess) return (int)pe;
     }
     // persistent: about one workgroup per CU (LDS-bound) over all N tiles
-    static const int pers = env_int("RGBD_DSAM_PERSIST", 256);
+    constexpr int pers = 256;  // persistent: one LDS-bound workgroup per CU
     dim3 grid2(std::max(1, pers / P.ntn), P.ntn, 1);
     const hipError_t e = P.kc == 3 ? launch_ld<3>(b, grid2, s) : P.kc == 2 ? launch_ld<2>(b, grid2, s) : launch_ld<1>(b, grid2, s);
     if (e != hipSuccess) return (int)e;
@@ -1773,8 +1757,6 @@ static WgPlan wg_plan(int B, int Cin, int h, int w, int Cout) {
 // 384 for layers with many output tiles (dsam2's 108: units of ~3 items balance better under the
 // dynamic assignment), 192 for layers with few (dsam0's 7) — measured per layer at 640x480
 static int wg_target(const WgPlan& p) {
-  static const int t = getenv("RGBD_WG_TARGET") ? atoi(getenv("RGBD_WG_TARGET")) : 0;
-  if (t > 0) return t;
   const int tiles = p.ntile_kk * p.ntile_o;
   return tiles >= 64 ? 384 : (tiles <= 8 ? 192 : 256);
 }
@@ -2038,8 +2020,6 @@ static WgArgs wg_args(const WgradWs& L, const WgPlan& P, char* plan, float* part
   a.inv_wo = 1.0f / (float)a.wo;
   a.zero = (const bf16_t*)(plan + L.zero);
   a.partial = partial;
-  static const int wdbg = env_int("RGBD_WG_DBG", 0);
-  a.dbg = wdbg;
   return a;
 }
 static bool wg_shape_ok(int B, int Cin, int h, int w, int Cout, const WgPlan& P) {

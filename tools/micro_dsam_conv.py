@@ -61,4 +61,4 @@ for k, (ci, co) in enumerate([(96, 192), (192, 384), (384, 768)]):
         torch.cuda.synchronize()
         res.append(f"{name} {e0.elapsed_time(e1) / a.iters * 1e3:.1f}us")
         del gr
-print(f"DBG={os.environ.get('RGBD_DSAM_DBG', '0')}: " + "  ".join(res))
+print("  ".join(res))
