@@ -272,6 +272,26 @@ int rgbd_dsam_bwd_weight_planned(int dtype, const void* gout_nchw, const void* g
                                  const void* x_nhwc, const uint8_t* code, const rgbd_decomp_info* info,
                                  int B, int Cin, int h, int w, int Cout, float* dconv_w, float* dproj_w,
                                  float* dbias, const void* plan, void* ws, void* stream);
+/* dW of several bf16 DSAM legs that are ready together (the hot path's dsam1 and dsam0 once the dX
+ * cascade has finished; hot_path.py): one persistent GEMM launch over the legs' joint work list —
+ * two back-to-back whole-chip launches would each drain on a partly idle chip — then each leg's
+ * bias sums and combine.  Per leg the results are bitwise those of rgbd_dsam_bwd_weight_planned
+ * with gout_nchw = NULL (the autograd of DSAModule.forward, custom_model.py:682-699).  n: 1 or 2;
+ * every run has its own plan and ws (rgbd_dsam_run_workspace_size(RGBD_LEG_DW, ...)).  Legs of
+ * different output tile shapes run one launch each. */
+typedef struct rgbd_dsam_dw_run {
+  const void* gout_nhwc;   /* upstream gradient [B][ho][wo][Cout] bf16 (device) */
+  const void* x_nhwc;      /* the DSAM's input [B][h][w][Cin] bf16 (device) */
+  const uint8_t* code;     /* region codes [B][h][w] (device) */
+  int B, Cin, h, w, Cout;
+  float* dconv_w;          /* [4][Cout][Cin][3][3] */
+  float* dproj_w;          /* [Cout][Cin][3][3] */
+  float* dbias;            /* [4][Cout] */
+  const void* plan;        /* this leg's RGBD_LEG_DW plan (rgbd_dsam_plan) */
+  void* ws;
+} rgbd_dsam_dw_run;
+int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, const rgbd_decomp_info* info,
+                                       void* stream);  /* runs: host array */
 
 /* ---------------------------------------------------------------- K4 ratio predictor
  * EnhancedDepthImageRatioPredictor.forward (custom_model.py:1444-1487) for the batch:

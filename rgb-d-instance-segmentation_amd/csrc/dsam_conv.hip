@@ -705,8 +705,18 @@ __global__ __launch_bounds__(256) void k_wg_masks_legs(const WgLegs L) {
   wg_masks_body(a, blockIdx.x);
 }
 
-template <int FM>
-__global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
+// NL legs of one output tile shape in one persistent launch: every workgroup drains leg 0's work
+// counter, then leg 1's, ..., so legs that are ready together share the CUs instead of queueing
+// whole-chip launches behind each other (the loop body is instantiated per leg: each leg's
+// arguments stay scalar kernel arguments).
+template <int NL>
+struct WgMulti {
+  WgArgs a[NL];
+  int n;  // legs in use, 1..NL
+};
+
+template <int FM, int NL>
+__global__ __launch_bounds__(256) void k_dsam_wgrad_mm(const WgMulti<NL> L) {
   using Cfg = WgCfg<FM>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   int* sunits = (int*)(smem + Cfg::OFF_UNITS);
@@ -715,10 +725,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int wm = wave & 1, wn = wave >> 1;
-  const int KK = 9 * a.Cin, hwo = a.ho * a.wo;
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  const int ntile = a.ntile_kk * a.ntile_o;
-  const int nwork = a.counts[1] * ntile;
   // per-lane copy roles: pixel row pr of every block, 16-byte chunk q
   const int pr = 16 * wave + (lane >> 2);
   const int qch = 8 * ((lane & 3) ^ wg_swz(pr));
@@ -744,109 +751,116 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(WgArgs a) {
     return f;
   };
   int* next_s = (int*)(smem + Cfg::OFF_UNITS) + WITEM_MAX - 1;  // unit ids are staged after the read
-  for (;;) {
-    // dynamic assignment of (item, tile) work: items differ in live units per code
-    __syncthreads();
-    if (tid == 0) *next_s = __hip_atomic_fetch_add(a.counts + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int wi = *next_s;
-    __syncthreads();  // every thread has it before the unit ids overwrite the slot
-    if (wi >= nwork) break;
-    const int4 item = a.items[wi / ntile];
-    const int tile = wi % ntile, e0 = item.y, nst = item.z - item.y;
-    const int kk0 = (tile % a.ntile_kk) * 128, o0 = (tile / a.ntile_kk) * 32 * FM;
-    // stage the item's unit ids and tap masks
-    for (int i = tid; i < nst; i += 256) sunits[i] = a.list[e0 + i] & 0xffffff;
-    for (int i = tid; i < nst * 9; i += 256) smasks[i] = a.masks[(long long)e0 * 9 + i];
-    __syncthreads();
-    // X block j: (tap, channel offset) uniform; source offset dy*w + dx from the row's origin
-    int xtap[4], xoff[4], xc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kk = kk0 + 32 * j;
-      const bool ok = kk < KK;
-      xtap[j] = ok ? kk / a.Cin : -1;
-      const int tp = ok ? xtap[j] : 0;
-      xoff[j] = (tp / 3) * a.w + tp % 3;
-      xc[j] = ok ? kk % a.Cin : 0;
-    }
-    const bf16_t* zrow = a.zero + qch;
-    // One step = one unit: G rows (its 64 output pixels) and X rows (their im2col sources).  A
-    // row of X whose source is outside the input, past the image, or of another code than the
-    // item's reads the zero row: it contributes exactly zero, no masking in registers.
-    auto issue = [&](int slot, int it) {
-      const int u = __builtin_amdgcn_readfirstlane(sunits[it]);
-      const int b = u / a.nunit;
-      const int p = (u - b * a.nunit) * WPX + pr;
-      const int pc = p < hwo ? p : hwo - 1;
-      const int oy = (int)(((float)pc + 0.5f) * a.inv_wo), ox = pc - oy * a.wo;
-      const uint32_t sb = lds0 + slot * Cfg::STAGE + wave * 1024;
-      const bf16_t* gsrc = a.gout + ((long long)b * hwo + pc) * a.Cout + qch;
-#pragma unroll
-      for (int ob = 0; ob < FM; ++ob) dma_lds16(gsrc + min(o0 + 32 * ob, a.Cout - 32), sb + ob * 4096);
-      const int org = (b * a.h + 2 * oy - 1) * a.w + 2 * ox - 1;
+  auto run_leg = [&](const WgArgs& a) {
+    const int KK = 9 * a.Cin, hwo = a.ho * a.wo, ntile = a.ntile_kk * a.ntile_o;
+    const int nwork = a.counts[1] * ntile;
+    for (;;) {
+      // dynamic assignment of (item, tile) work: items differ in live units per code
+      __syncthreads();
+      if (tid == 0) *next_s = __hip_atomic_fetch_add(a.counts + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int wi = *next_s;
+      __syncthreads();  // every thread has it before the unit ids overwrite the slot
+      if (wi >= nwork) break;
+      const int4 item = a.items[wi / ntile];
+      const int tile = wi % ntile, e0 = item.y, nst = item.z - item.y;
+      const int kk0 = (tile % a.ntile_kk) * 128, o0 = (tile / a.ntile_kk) * 32 * FM;
+      // stage the item's unit ids and tap masks
+      for (int i = tid; i < nst; i += 256) sunits[i] = a.list[e0 + i] & 0xffffff;
+      for (int i = tid; i < nst * 9; i += 256) smasks[i] = a.masks[(long long)e0 * 9 + i];
+      __syncthreads();
+      // X block j: (tap, channel offset) uniform; source offset dy*w + dx from the row's origin
+      int xtap[4], xoff[4], xc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const unsigned long long m = xtap[j] >= 0 ? smasks[it * 9 + xtap[j]] : 0ull;
-        const bool live = (m >> pr) & 1ull;
-        const bf16_t* src = live ? a.x + (long long)(org + xoff[j]) * a.Cin + xc[j] + qch : zrow;
-        dma_lds16(src, sb + (FM + j) * 4096);
+        const int kk = kk0 + 32 * j;
+        const bool ok = kk < KK;
+        xtap[j] = ok ? kk / a.Cin : -1;
+        const int tp = ok ? xtap[j] : 0;
+        xoff[j] = (tp / 3) * a.w + tp % 3;
+        xc[j] = ok ? kk % a.Cin : 0;
       }
-    };
-    f32x4 acc[FM][4];
+      const bf16_t* zrow = a.zero + qch;
+      // One step = one unit: G rows (its 64 output pixels) and X rows (their im2col sources).  A
+      // row of X whose source is outside the input, past the image, or of another code than the
+      // item's reads the zero row: it contributes exactly zero, no masking in registers.
+      auto issue = [&](int slot, int it) {
+        const int u = __builtin_amdgcn_readfirstlane(sunits[it]);
+        const int b = u / a.nunit;
+        const int p = (u - b * a.nunit) * WPX + pr;
+        const int pc = p < hwo ? p : hwo - 1;
+        const int oy = (int)(((float)pc + 0.5f) * a.inv_wo), ox = pc - oy * a.wo;
+        const uint32_t sb = lds0 + slot * Cfg::STAGE + wave * 1024;
+        const bf16_t* gsrc = a.gout + ((long long)b * hwo + pc) * a.Cout + qch;
 #pragma unroll
-    for (int mi = 0; mi < FM; ++mi)
+        for (int ob = 0; ob < FM; ++ob) dma_lds16(gsrc + min(o0 + 32 * ob, a.Cout - 32), sb + ob * 4096);
+        const int org = (b * a.h + 2 * oy - 1) * a.w + 2 * ox - 1;
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int npro = nst < Cfg::S - 1 ? nst : Cfg::S - 1;
-    for (int i = 0; i < npro; ++i) issue(i, i);
-    if (npro >= 3) vm_wait_barrier<2 * Cfg::PER>();
-    else if (npro == 2) vm_wait_barrier<Cfg::PER>();
-    else vm_wait_barrier<0>();
-#pragma unroll 1
-    for (int s = 0; s < nst; ++s) {
-      if (s + Cfg::S - 1 < nst) issue((s + Cfg::S - 1) % Cfg::S, s + Cfg::S - 1);
-      int st = (s % Cfg::S) * Cfg::STAGE;
-      asm volatile("" : "+s"(st));  // no strength reduction of the slot offset into per-read registers
-      b0 = lsm + st + tbase0;
-      b16 = lsm + st + tbase16;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        Frag<bf16_t> fa[FM], fb[4];
-#pragma unroll
-        for (int mi = 0; mi < FM; ++mi) {
-          const int ol = wm * 16 * FM + 16 * mi;
-          fa[mi] = trfrag((ol >> 5) * 4096, kb, ol & 31);
+        for (int j = 0; j < 4; ++j) {
+          const unsigned long long m = xtap[j] >= 0 ? smasks[it * 9 + xtap[j]] : 0ull;
+          const bool live = (m >> pr) & 1ull;
+          const bf16_t* src = live ? a.x + (long long)(org + xoff[j]) * a.Cin + xc[j] + qch : zrow;
+          dma_lds16(src, sb + (FM + j) * 4096);
         }
+      };
+      f32x4 acc[FM][4];
 #pragma unroll
-        for (int nj = 0; nj < 4; ++nj) {
-          const int kl = wn * 64 + 16 * nj;
-          fb[nj] = trfrag((FM + (kl >> 5)) * 4096, kb, kl & 31);
-        }
+      for (int mi = 0; mi < FM; ++mi)
 #pragma unroll
-        for (int mi = 0; mi < FM; ++mi)
-#pragma unroll
-          for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
-      }
-      const int ahead = (nst - 1 < s + Cfg::S - 1 ? nst - 1 : s + Cfg::S - 1) - (s + 1);
-      if (ahead >= 2) vm_wait_barrier<2 * Cfg::PER>();
-      else if (ahead == 1) vm_wait_barrier<Cfg::PER>();
+        for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int npro = nst < Cfg::S - 1 ? nst : Cfg::S - 1;
+      for (int i = 0; i < npro; ++i) issue(i, i);
+      if (npro >= 3) vm_wait_barrier<2 * Cfg::PER>();
+      else if (npro == 2) vm_wait_barrier<Cfg::PER>();
       else vm_wait_barrier<0>();
-    }
-    float* dst = a.partial + ((long long)(wi / ntile) * a.Cout) * KK;
+#pragma unroll 1
+      for (int s = 0; s < nst; ++s) {
+        if (s + Cfg::S - 1 < nst) issue((s + Cfg::S - 1) % Cfg::S, s + Cfg::S - 1);
+        int st = (s % Cfg::S) * Cfg::STAGE;
+        asm volatile("" : "+s"(st));  // no strength reduction of the slot offset into per-read registers
+        b0 = lsm + st + tbase0;
+        b16 = lsm + st + tbase16;
 #pragma unroll
-    for (int mi = 0; mi < FM; ++mi)
+        for (int kb = 0; kb < 2; ++kb) {
+          Frag<bf16_t> fa[FM], fb[4];
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int o = o0 + wm * 16 * FM + 16 * mi + 4 * g + reg;
+          for (int mi = 0; mi < FM; ++mi) {
+            const int ol = wm * 16 * FM + 16 * mi;
+            fa[mi] = trfrag((ol >> 5) * 4096, kb, ol & 31);
+          }
 #pragma unroll
-        for (int nj = 0; nj < 4; ++nj) {
-          const int c = kk0 + wn * 64 + 16 * nj + r;
-          if (o < a.Cout && c < KK) dst[(long long)o * KK + c] = acc[mi][nj][reg];
+          for (int nj = 0; nj < 4; ++nj) {
+            const int kl = wn * 64 + 16 * nj;
+            fb[nj] = trfrag((FM + (kl >> 5)) * 4096, kb, kl & 31);
+          }
+#pragma unroll
+          for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+            for (int nj = 0; nj < 4; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
         }
+        const int ahead = (nst - 1 < s + Cfg::S - 1 ? nst - 1 : s + Cfg::S - 1) - (s + 1);
+        if (ahead >= 2) vm_wait_barrier<2 * Cfg::PER>();
+        else if (ahead == 1) vm_wait_barrier<Cfg::PER>();
+        else vm_wait_barrier<0>();
       }
-    __syncthreads();  // staged ids / masks and the ring are free for the next work unit
-  }
+      float* dst = a.partial + ((long long)(wi / ntile) * a.Cout) * KK;
+#pragma unroll
+      for (int mi = 0; mi < FM; ++mi)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int o = o0 + wm * 16 * FM + 16 * mi + 4 * g + reg;
+#pragma unroll
+          for (int nj = 0; nj < 4; ++nj) {
+            const int c = kk0 + wn * 64 + 16 * nj + r;
+            if (o < a.Cout && c < KK) dst[(long long)o * KK + c] = acc[mi][nj][reg];
+          }
+        }
+      __syncthreads();  // staged ids / masks and the ring are free for the next work unit
+    }
+  };
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+    if (l < L.n) run_leg(L.a[l]);
 }
 
 // dW_k (per item partials) -> the reference filters, fixed summation order (items in list
@@ -1766,14 +1780,19 @@ static size_t wg_max_items(const WgPlan& p) {
   return (size_t)std::min<long long>(p.max_entries, want + 16 + p.max_entries / WITEM_MAX);
 }
 
-template <int FM>
-hipError_t launch_wg(const WgArgs& a, int grid, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)k_dsam_wgrad_mm<FM>,
+template <int FM, int NL>
+hipError_t launch_wg(const WgMulti<NL>& m, int grid, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_dsam_wgrad_mm<FM, NL>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      (int)WgCfg<FM>::SMEM);
   if (attr != hipSuccess) return attr;
-  k_dsam_wgrad_mm<FM><<<grid, 256, WgCfg<FM>::SMEM, s>>>(a);
+  k_dsam_wgrad_mm<FM, NL><<<grid, 256, WgCfg<FM>::SMEM, s>>>(m);
   return hipSuccess;
+}
+template <int NL>
+hipError_t launch_wg_fm(int fm, const WgMulti<NL>& m, hipStream_t s) {
+  const int grid = 256;  // persistent: one LDS-bound workgroup per CU
+  return fm == 6 ? launch_wg<6, NL>(m, grid, s) : fm == 4 ? launch_wg<4, NL>(m, grid, s) : launch_wg<2, NL>(m, grid, s);
 }
 
 int dsam_wgrad_splits(int B, int Cin, int Cout) {
@@ -2049,6 +2068,28 @@ size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int
   return wgrad_ws(dtype, B, Cin, h, w, Cout).total;
 }
 
+// bf16 dW after the GEMM: the upstream gradient's channel sums (bias), then the combine of the
+// item partials into the reference filters (it also writes the bias gradients)
+static int wg_finish(const WgArgs& a, const void* gout_nchw, float* csum, const rgbd_decomp_info* info,
+                     float* dconv_w, float* dproj_w, float* dbias, hipStream_t s) {
+  const int hwo = a.ho * a.wo;
+  if (gout_nchw)
+    k_chan_sum<bf16_t><<<a.B * a.Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
+  else
+    k_chan_sum_nhwc<<<dim3(a.B, ceil_div(a.Cout, 64), chan_sum_splits(hwo)), 256, 0, s>>>(a.gout, hwo, a.Cout, csum);
+  const int csmem = 5 * 9 * a.Cin * (int)sizeof(float);
+  constexpr int kCombineDyn = 163840 - 1024 * 4;  // the kernel's static item -> code table
+  static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
+  if (cattr != hipSuccess) return (int)cattr;
+  RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
+  const int nsplit_bf = gout_nchw ? 1 : chan_sum_splits(hwo);
+  k_dsam_wgrad_combine<<<a.Cout, 256, csmem, s>>>(a.partial, a.items, a.counts, a.Cin, a.Cout, dconv_w, dproj_w, csum,
+                                                  info, a.B, nsplit_bf, dbias);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
 static int bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, const void* x_nhwc,
                       const uint8_t* code, const rgbd_decomp_info* info, int B, int Cin, int h, int w, int Cout,
                       float* dconv_w, float* dproj_w, float* dbias, const void* planned, void* ws, void* stream) {
@@ -2078,27 +2119,13 @@ static int bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, c
     const WgPlan P = wg_plan(B, Cin, h, w, Cout);
     RGBD_REQUIRE(wg_shape_ok(B, Cin, h, w, Cout, P), RGBD_E_SHAPE);
     char* plan = planned ? (char*)planned : (char*)ws;
-    const WgArgs a = wg_args(L, P, plan, partial, gout_nhwc, x_nhwc, code, B, Cin, h, w, Cout);
-    if (!planned) wg_plan_launch(1, &a, &P, s);
-    const int grid = 256;  // persistent: one LDS-bound workgroup per CU
-    const hipError_t e = P.fm == 6 ? launch_wg<6>(a, grid, s) : P.fm == 4 ? launch_wg<4>(a, grid, s) : launch_wg<2>(a, grid, s);
+    WgMulti<1> m;
+    m.a[0] = wg_args(L, P, plan, partial, gout_nhwc, x_nhwc, code, B, Cin, h, w, Cout);
+    m.n = 1;
+    if (!planned) wg_plan_launch(1, &m.a[0], &P, s);
+    const hipError_t e = launch_wg_fm(P.fm, m, s);
     if (e != hipSuccess) return (int)e;
-    if (gout_nchw)
-      k_chan_sum<bf16_t><<<B * Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
-    else
-      k_chan_sum_nhwc<<<dim3(B, ceil_div(Cout, 64), chan_sum_splits(hwo)), 256, 0, s>>>((const bf16_t*)gout_nhwc, hwo,
-                                                                                       Cout, csum);
-    const int csmem = 5 * 9 * Cin * (int)sizeof(float);
-    constexpr int kCombineDyn = 163840 - 1024 * 4;  // the kernel's static item -> code table
-    static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
-    if (cattr != hipSuccess) return (int)cattr;
-    RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
-    const int nsplit_bf = gout_nchw ? 1 : chan_sum_splits(hwo);
-    k_dsam_wgrad_combine<<<Cout, 256, csmem, s>>>(partial, a.items, a.counts, Cin, Cout, dconv_w, dproj_w, csum, info,
-                                                  B, nsplit_bf, dbias);
-    RGBD_CHECK_LAUNCH();
-    return RGBD_OK;  // the combine also wrote the bias gradients
+    return wg_finish(m.a[0], gout_nchw, csum, info, dconv_w, dproj_w, dbias, s);
   } else {
     return RGBD_E_DTYPE;
   }
@@ -2121,6 +2148,50 @@ int rgbd_dsam_bwd_weight_planned(int dtype, const void* gout_nchw, const void* g
   RGBD_REQUIRE(plan && dtype == RGBD_BF16, RGBD_E_ARG);
   return bwd_weight(dtype, gout_nchw, gout_nhwc, x_nhwc, code, info, B, Cin, h, w, Cout, dconv_w, dproj_w, dbias,
                     plan, ws, stream);
+}
+
+int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, const rgbd_decomp_info* info,
+                                       void* stream) {
+  RGBD_REQUIRE(n >= 1 && n <= 2 && runs && info, RGBD_E_ARG);
+  hipStream_t s = (hipStream_t)stream;
+  TimerScope ts("dsam_wgrad", s);
+  WgMulti<2> m;
+  int fm[2];
+  for (int i = 0; i < n; ++i) {
+    const rgbd_dsam_dw_run& r = runs[i];
+    RGBD_REQUIRE(r.gout_nhwc && r.x_nhwc && r.code && r.dconv_w && r.dproj_w && r.dbias && r.plan && r.ws, RGBD_E_ARG);
+    RGBD_REQUIRE(r.B > 0 && r.h > 0 && r.w > 0 && r.Cout > 0 && r.Cin > 0 && r.Cin % 8 == 0, RGBD_E_SHAPE);
+    const WgradWs L = wgrad_ws(RGBD_BF16, r.B, r.Cin, r.h, r.w, r.Cout);
+    const WgPlan P = wg_plan(r.B, r.Cin, r.h, r.w, r.Cout);
+    RGBD_REQUIRE(wg_shape_ok(r.B, r.Cin, r.h, r.w, r.Cout, P), RGBD_E_SHAPE);
+    float* partial = (float*)((char*)r.ws + L.partial - L.plan_total);
+    m.a[i] = wg_args(L, P, (char*)r.plan, partial, r.gout_nhwc, r.x_nhwc, r.code, r.B, r.Cin, r.h, r.w, r.Cout);
+    fm[i] = P.fm;
+  }
+  for (int i = 0; i + 1 < n; ++i)  // distinct buffers: the legs run together
+    RGBD_REQUIRE(runs[i].ws != runs[i + 1].ws && runs[i].plan != runs[i + 1].plan, RGBD_E_ARG);
+  hipError_t e;
+  if (n == 2 && fm[0] == fm[1]) {
+    m.n = 2;
+    e = launch_wg_fm(fm[0], m, s);
+  } else {  // one leg, or tile shapes that differ: one launch per leg
+    e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; ++i) {
+      WgMulti<1> one;
+      one.a[0] = m.a[i];
+      one.n = 1;
+      e = launch_wg_fm(fm[i], one, s);
+    }
+  }
+  if (e != hipSuccess) return (int)e;
+  for (int i = 0; i < n; ++i) {
+    const rgbd_dsam_dw_run& r = runs[i];
+    const WgradWs L = wgrad_ws(RGBD_BF16, r.B, r.Cin, r.h, r.w, r.Cout);
+    float* csum = (float*)((char*)r.ws + L.csum - L.plan_total);
+    const int rc = wg_finish(m.a[i], nullptr, csum, info, r.dconv_w, r.dproj_w, r.dbias, s);
+    if (rc != RGBD_OK) return rc;
+  }
+  return RGBD_OK;
 }
 
 // ---- planning ahead (bf16): the code-dependent set-up of a leg depends only on the region codes,

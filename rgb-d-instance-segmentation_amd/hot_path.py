@@ -51,6 +51,11 @@ def side_stream(dev):
     return s
 
 
+# bf16 backward: the dW GEMMs of dsam1 and dsam0 in one launch (rgbd_dsam_bwd_weight_planned_multi);
+# False runs them as two launches, dW1 on the side stream (bitwise the same gradients)
+JOINT_DW = True
+
+
 class _Side:
     """Fork/join of launches onto the side stream (works eagerly and under graph capture: the side
     stream joins the capture through the fork's event).  One side stream, and never two forks
@@ -261,8 +266,8 @@ class HotPathFunction(torch.autograd.Function):
                                    if shape is None else "missing gradient for scale 0")
             G.append(g.to(dtype).contiguous())
         bf16 = dtype == torch.bfloat16
-        # bf16 on the GPU: the main stream runs dX2 -> dX1 -> dW1 -> dW0; the DGGM backward and the
-        # dW of dsam2 run beside it on the side stream (their persistent kernels take CUs as the
+        # bf16 on the GPU: the main stream runs dX2 -> dX1 -> dW1 + dW0 (one launch); the DGGM backward
+        # and the dW of dsam2 run beside it on the side stream (their persistent kernels take CUs as the
         # other stream's work drains; every kernel assigns its work dynamically)
         side = _Side(G[0].device, bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True))
 
@@ -284,6 +289,9 @@ class HotPathFunction(torch.autograd.Function):
                                                       plan=ctx.dw_plans[k] if ctx.dw_plans else None)
             if k == 0:  # dW0 needs nothing from the side stream; the hook and the caller do
                 side.join()
+            return dsam_dw_grads(k, dconv, dproj, dbias)
+
+        def dsam_dw_grads(k, dconv, dproj, dbias):
             gk = []
             for i in range(4):
                 gk += [dconv[i], dbias[i]]
@@ -304,9 +312,19 @@ class HotPathFunction(torch.autograd.Function):
         grads_dsam[2] = side.run(lambda: dsam_dw(2, dcp, dcp_nhwc), dcp_nhwc, ctx.x_nhwc[2], ctx.codes[2], ctx.info)
         dcp1, dcp1_nhwc = dsam_dx(2, dcp, dcp_nhwc)
         dcp0, dcp0_nhwc = dsam_dx(1, dcp1, dcp1_nhwc)
-        grads_dsam[1] = side.run(lambda: dsam_dw(1, dcp1, dcp1_nhwc), dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1],
-                                 ctx.info)
-        grads_dsam[0] = dsam_dw(0, dcp0, dcp0_nhwc)  # the last launches of the backward, the join after them
+        if bf16 and ctx.dw_plans and JOINT_DW:
+            # dW1 and dW0 are ready together: their GEMMs share one persistent launch (two
+            # whole-chip launches queue behind each other and each drains on a partly idle chip)
+            (dw1, dw0) = ops.dsam_bwd_weight_multi([(dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1], ctx.dw_plans[1]),
+                                                    (dcp0_nhwc, ctx.x_nhwc[0], ctx.codes[0], ctx.dw_plans[0])],
+                                                   ctx.info)
+            side.join()  # the last launches of the backward, the join after them
+            grads_dsam[1] = dsam_dw_grads(1, *dw1)
+            grads_dsam[0] = dsam_dw_grads(0, *dw0)
+        else:
+            grads_dsam[1] = side.run(lambda: dsam_dw(1, dcp1, dcp1_nhwc), dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1],
+                                     ctx.info)
+            grads_dsam[0] = dsam_dw(0, dcp0, dcp0_nhwc)  # the last launches of the backward, the join after them
         pgrads = grads_dsam[0] + grads_dsam[1] + grads_dsam[2] + grads_dggm
         return (None, None, None, None, None, None, None, *pgrads)
 

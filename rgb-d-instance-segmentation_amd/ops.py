@@ -538,6 +538,44 @@ def dsam_bwd_weight(gout_nchw, x_nhwc, code, info, gout_nhwc=None, plan=None):
     return dconv, dproj, dbias
 
 
+class _DwRun(ctypes.Structure):  # rgbd_dsam_dw_run
+    _fields_ = [("gout_nhwc", ctypes.c_void_p), ("x_nhwc", ctypes.c_void_p), ("code", ctypes.c_void_p),
+                ("B", ctypes.c_int), ("Cin", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
+                ("Cout", ctypes.c_int), ("dconv_w", ctypes.c_void_p), ("dproj_w", ctypes.c_void_p),
+                ("dbias", ctypes.c_void_p), ("plan", ctypes.c_void_p), ("ws", ctypes.c_void_p)]
+
+
+def dsam_bwd_weight_multi(runs, info):
+    """dW/db of bfloat16 DSAM legs that are ready together, their GEMMs in one persistent launch
+    (rgbd_dsam_bwd_weight_planned_multi).  ``runs``: up to two (gout_nhwc [B,ho,wo,Co], x_nhwc
+    [B,h,w,Ci], code [B,h,w], plan) tuples, each plan from dsam_plan(LEG_DW); returns per run
+    (dconv, dproj, dbias), bitwise those of dsam_bwd_weight(None, ..., gout_nhwc=, plan=)."""
+    if not 1 <= len(runs) <= 2:
+        raise ValueError("dsam_bwd_weight_multi: one or two runs")
+    L = _lib.lib()
+    arr = (_DwRun * len(runs))()
+    outs = []
+    for j, (gout_nhwc, x_nhwc, code, plan) in enumerate(runs):
+        _need_cuda(gout_nhwc, x_nhwc, code, plan, info)
+        if gout_nhwc.dtype != torch.bfloat16 or x_nhwc.dtype != torch.bfloat16:
+            raise ValueError("dsam_bwd_weight_multi: bfloat16 legs only")
+        B, ho, wo, Co = gout_nhwc.shape
+        _, h, w, Ci = x_nhwc.shape
+        if (ho, wo) != ((h + 1) // 2, (w + 1) // 2) or tuple(code.shape) != (B, h, w):
+            raise ValueError(f"dsam_bwd_weight_multi: run {j} shapes {tuple(gout_nhwc.shape)} {tuple(x_nhwc.shape)}")
+        dev = gout_nhwc.device
+        dconv = torch.empty((4, Co, Ci, 3, 3), dtype=torch.float32, device=dev)
+        dproj = torch.empty((Co, Ci, 3, 3), dtype=torch.float32, device=dev)
+        dbias = torch.empty((4, Co), dtype=torch.float32, device=dev)
+        ws = _workspace(dev, L.rgbd_dsam_run_workspace_size(LEG_DW, B, Ci, h, w, Co), f"dsam_wgrad_run{j}")
+        arr[j] = _DwRun(gout_nhwc.data_ptr(), x_nhwc.data_ptr(), code.data_ptr(), B, Ci, h, w, Co, dconv.data_ptr(),
+                        dproj.data_ptr(), dbias.data_ptr(), plan.data_ptr(), ws.data_ptr())
+        outs.append((dconv, dproj, dbias))
+    check(L.rgbd_dsam_bwd_weight_planned_multi(len(runs), arr, _p(info), _stream(runs[0][0].device)),
+          "rgbd_dsam_bwd_weight_planned_multi")
+    return outs
+
+
 # ------------------------------------------------------------------ f1 mask predictor
 def mask_logits(emb: torch.Tensor, pix: torch.Tensor) -> torch.Tensor:
     """einsum("bqc,bchw->bqhw", emb, pix) (modeling_mask2former.py:2046) on the MFMA kernel.

@@ -83,3 +83,54 @@ def test_decompose_code_masks(H, W, B):
     for a, b in zip(c0, c1):
         assert torch.equal(a, b)
     assert torch.equal(m1, ops.dsam_code_masks(c0))
+
+
+@pytest.mark.parametrize("H,W,B,pairs", [(480, 640, 8, [(1, 0), (2, 1), (0,)]), (97, 131, 3, [(1, 0), (2, 0)])])
+def test_joint_dw_bitwise(H, W, B, pairs):
+    """rgbd_dsam_bwd_weight_planned_multi: the dW GEMMs of two legs in one persistent launch give
+    per leg bitwise the gradients of the one-leg planned entry point (the hot path runs dsam1 and
+    dsam0 this way; hot_path.JOINT_DW)."""
+    planes, _, _ = synthetic.make_batch(11, B, H, W)
+    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
+    sizes = _sizes(H, W)
+    codes, info = ops.edsam_decompose(d3, torch.linspace(0.05, 0.45, B, device=DEV), sizes)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(13)
+    xs, gys = [], []
+    for k in range(3):
+        ci, co = CH[k]
+        h, w = sizes[k]
+        xs.append(torch.randn((B, h, w, ci), generator=g, device=DEV).bfloat16())
+        gys.append((torch.randn((B, (h + 1) // 2, (w + 1) // 2, co), generator=g, device=DEV) * 0.1).bfloat16())
+    for pair in pairs:
+        plans = ops.dsam_plan([(ops.LEG_DW, codes[k], *CH[k]) for k in pair])
+        got = ops.dsam_bwd_weight_multi([(gys[k], xs[k], codes[k], plans[j]) for j, k in enumerate(pair)], info)
+        for j, k in enumerate(pair):
+            want = ops.dsam_bwd_weight(None, xs[k], codes[k], info, gout_nhwc=gys[k])
+            for a, b, name in zip(got[j], want, ("dconv", "dproj", "dbias")):
+                assert torch.equal(a, b), f"joint {pair} leg {k} {name}"
+
+
+def test_joint_dw_mixed_tile_shapes():
+    """Legs whose output tiles differ (Cout 192 -> 6 sub-tiles, 256 -> 4) run one launch each
+    behind the same entry point, with the same results."""
+    B, H, W = 2, 96, 128
+    planes, _, _ = synthetic.make_batch(3, B, H, W)
+    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
+    sizes = _sizes(H, W)
+    codes, info = ops.edsam_decompose(d3, torch.full((B,), 0.2, device=DEV), sizes)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(2)
+    legs = [(0, 96, 192), (1, 96, 256)]
+    runs, ref = [], []
+    plans = ops.dsam_plan([(ops.LEG_DW, codes[k], ci, co) for k, ci, co in legs])
+    for j, (k, ci, co) in enumerate(legs):
+        h, w = sizes[k]
+        x = torch.randn((B, h, w, ci), generator=g, device=DEV).bfloat16()
+        gy = (torch.randn((B, (h + 1) // 2, (w + 1) // 2, co), generator=g, device=DEV) * 0.1).bfloat16()
+        runs.append((gy, x, codes[k], plans[j]))
+        ref.append(ops.dsam_bwd_weight(None, x, codes[k], info, gout_nhwc=gy))
+    got = ops.dsam_bwd_weight_multi(runs, info)
+    for j in range(2):
+        for a, b in zip(got[j], ref[j]):
+            assert torch.equal(a, b), f"leg {j}"

@@ -282,6 +282,36 @@ def test_hot_path_fused_vs_oracle(dtype):
         assert err < (2e-4 if dtype == torch.float32 else BF16_REL), f"{n}: rel err {err}"
 
 
+def test_hot_path_joint_dw_bitwise():
+    """bfloat16 backward: dsam1's and dsam0's dW GEMMs in one launch (hot_path.JOINT_DW) give
+    bitwise the parameter gradients of the two-launch schedule."""
+    from rgbd_amd import hot_path as hp
+    H, W, B = 240, 320, 2
+    pv = torch.from_numpy(gi.pixel_values(7, B, H, W)).to(DEV)
+    ratios = torch.tensor([[0.2], [0.07]], dtype=torch.float32, device=DEV)
+    sizes = gi.swin_sizes(H, W)
+    colors = [torch.from_numpy(gi.feature(f"hp.c{k}", (B, c, *sizes[k]))).to(DEV)
+              for k, c in enumerate([96, 192, 384, 768])]
+    gouts = [torch.from_numpy(gi.feature(f"hp.g{k}", tuple(c.shape))).to(DEV, torch.bfloat16) for k, c in
+             enumerate(colors)]
+    dsams, dg = _hot_modules(torch.bfloat16)
+    params = [p for m in dsams for p in m.parameters()] + list(dg.parameters())
+    grads = []
+    old = hp.JOINT_DW
+    try:
+        for joint in (True, False):
+            hp.JOINT_DW = joint
+            for p in params:
+                p.grad = None
+            outs = hp.hot_path(pv, ratios, colors, dsams, dg, dtype=torch.bfloat16)
+            torch.autograd.backward(outs, gouts)
+            grads.append([p.grad.clone() for p in params])
+    finally:
+        hp.JOINT_DW = old
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
 # ------------------------------------------------------------------ C5: RealSense 1280x720
 def test_c5_assemble_and_decompose_1280x720():
     """BASELINE config C5 (RealSense 1280x720): 10-channel assembly incl. the DGGM Sobel planes
