@@ -182,6 +182,15 @@ int rgbd_dggm_fuse_bwd_multi(int dtype, int n, const void* const* dout_host, con
 /* ---------------------------------------------------------------- layout helpers */
 int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H, int W,
                       void* stream);
+/* Up to four bf16 conversions as rgbd_nchw_to_nhwc in one launch (the hot path's colour maps in
+ * the forward, its upstream gradients G[1..3] in the backward); C % 8 == 0.  Bitwise the
+ * per-tensor results. */
+typedef struct rgbd_nhwc_job {
+  const void* src;  /* [B][C][H][W] bf16 (device) */
+  void* dst;        /* [B][H][W][C] bf16 (device) */
+  int B, C, H, W;
+} rgbd_nhwc_job;
+int rgbd_nchw_to_nhwc_multi(int n, const rgbd_nhwc_job* jobs, void* stream);  /* jobs: host array */
 /* Packs DSAModule weights (conv_layers[0..3].weight, rgb_projection.weight; float32
  * [4][Cout][Cin][3][3] and [Cout][Cin][3][3]) into the implicit-GEMM B operands.
  * RGBD_F32 (segment form):

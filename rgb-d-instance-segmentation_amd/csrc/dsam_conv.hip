@@ -398,6 +398,61 @@ __global__ __launch_bounds__(256) void k_nchw_to_nhwc_v8(const bf16_t* __restric
   }
 }
 
+// Several bf16 NCHW -> NHWC conversions in one launch (the hot path's four colour maps in the
+// forward, its three upstream gradients in the backward): a 1-D grid of 64 x 64 tiles over all
+// jobs; a job whose HW is not a multiple of 8 loads its pixels one by one (same tile, same stores).
+constexpr int NHWC_MAXJOB = 4;
+struct NhwcJobs {
+  const bf16_t* src[NHWC_MAXJOB];
+  bf16_t* dst[NHWC_MAXJOB];
+  int C[NHWC_MAXJOB], HW[NHWC_MAXJOB], tp[NHWC_MAXJOB], tc[NHWC_MAXJOB];
+  int block0[NHWC_MAXJOB + 1];  // first block of each job; block0[n] = grid
+  int n;
+};
+__global__ __launch_bounds__(256) void k_nchw_to_nhwc_multi(const NhwcJobs J) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[64][72];
+  int j = 0;
+#pragma unroll
+  for (int i = 1; i < NHWC_MAXJOB; ++i)
+    if (i < J.n && (int)blockIdx.x >= J.block0[i]) j = i;
+  const bf16_t* src = J.src[j];
+  bf16_t* dst = J.dst[j];
+  const int C = J.C[j], HW = J.HW[j], per = J.tp[j] * J.tc[j];
+  const int idx = blockIdx.x - J.block0[j], b = idx / per, t = idx - b * per;
+  const int p0 = (t % J.tp[j]) * 64, c0 = (t / J.tp[j]) * 64;
+  const bool vec = (HW & 7) == 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = threadIdx.x + 256 * k, cl = v >> 3, pl = (v & 7) * 8;  // channel, 8-pixel group
+    const int c = c0 + cl, p = p0 + pl;
+    const bf16_t* row = src + ((long long)b * C + c) * HW;
+    bf16_t e8[8];
+    if (vec) {
+      uint4 u = make_uint4(0u, 0u, 0u, 0u);
+      if (c < C && p < HW) u = *reinterpret_cast<const uint4*>(row + p);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        e8[2 * e] = (bf16_t)(w[e] & 0xffffu);
+        e8[2 * e + 1] = (bf16_t)(w[e] >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) e8[e] = (c < C && p + e < HW) ? row[p + e] : (bf16_t)0;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[pl + e][cl] = e8[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = threadIdx.x + 256 * k, pl = v >> 3, cl = (v & 7) * 8;  // pixel, 8-channel group
+    const int p = p0 + pl, c = c0 + cl;
+    if (p < HW && c < C)
+      *reinterpret_cast<uint4*>(dst + ((long long)b * HW + p) * C + c) = *reinterpret_cast<const uint4*>(&tile[pl][cl]);
+  }
+}
+
 // ----------------------------------------------------------------------- dW
 // D[o][kk] = sum_m G[m][o] * X[m][kk],  kk = (seg*9 + tap)*Cin + c,  per split z (images).
 template <typename T>
@@ -1823,6 +1878,31 @@ int rgbd_nchw_to_nhwc(int dtype, const void* src, void* dst, int B, int C, int H
     k_nchw_to_nhwc<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)src, (bf16_t*)dst, C, H * W);
   else
     return RGBD_E_DTYPE;
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_nchw_to_nhwc_multi(int n, const rgbd_nhwc_job* jobs, void* stream) {
+  RGBD_REQUIRE(n >= 1 && n <= NHWC_MAXJOB && jobs, RGBD_E_ARG);
+  NhwcJobs J;
+  long long blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const rgbd_nhwc_job& q = jobs[i];
+    RGBD_REQUIRE(q.src && q.dst && q.B > 0 && q.C > 0 && q.H > 0 && q.W > 0, RGBD_E_ARG);
+    RGBD_REQUIRE(q.C % 8 == 0, RGBD_E_SHAPE);  // 16-byte NHWC stores
+    J.src[i] = (const bf16_t*)q.src;
+    J.dst[i] = (bf16_t*)q.dst;
+    J.C[i] = q.C;
+    J.HW[i] = q.H * q.W;
+    J.tp[i] = ceil_div((long long)q.H * q.W, 64);
+    J.tc[i] = ceil_div(q.C, 64);
+    J.block0[i] = (int)blocks;
+    blocks += (long long)q.B * J.tp[i] * J.tc[i];
+  }
+  RGBD_REQUIRE(blocks < (1ll << 31), RGBD_E_SHAPE);
+  J.block0[n] = (int)blocks;
+  J.n = n;
+  k_nchw_to_nhwc_multi<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(J);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -157,7 +157,7 @@ def prepare(pixel_values, colors, dtype=torch.float32):
 
     def work():
         held["modes"] = m = ops.edsam_modes(pv)
-        nhwc = [ops.nchw_to_nhwc(c) for c in cols] if bf16 else None
+        nhwc = ops.nchw_to_nhwc_multi(cols) if bf16 else None
         return [m.info, m.ws, m.masks, nhwc]
     _, _, _, nhwc = side.run(work, pv, *cols)
     return Prepared(side, pv, held["modes"], cols, nhwc, dtype)
@@ -281,7 +281,9 @@ class HotPathFunction(torch.autograd.Function):
         # NHWC (dX written NHWC only, its residual G[k] converted once; bias sums from NHWC).
         hook = ctx.cfg.get("grad_hook")
         dcp = G[3]
-        dcp_nhwc = ops.nchw_to_nhwc(dcp)
+        # bf16: the three upstream gradients the cascade reads in NHWC, converted by one launch
+        g_nhwc = dict(zip((3, 2, 1), ops.nchw_to_nhwc_multi([G[3], G[2], G[1]]))) if bf16 else {}
+        dcp_nhwc = g_nhwc[3] if bf16 else ops.nchw_to_nhwc(dcp)
         grads_dsam = [None, None, None]
         def dsam_dw(k, dcp, dcp_nhwc):
             dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
@@ -303,7 +305,7 @@ class HotPathFunction(torch.autograd.Function):
         def dsam_dx(k, dcp, dcp_nhwc):
             if bf16:
                 return ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], None, want_nhwc=True,
-                                         want_nchw=False, gin_nhwc=ops.nchw_to_nhwc(G[k]), plan=ctx.dx_plans.get(k))
+                                         want_nchw=False, gin_nhwc=g_nhwc[k], plan=ctx.dx_plans.get(k))
             return ops.dsam_bwd_data(dcp_nhwc, ctx.codes[k], ctx.packs[k][1], G[k], want_nhwc=(k > 1))
         # dW2 beside the cascade; dX2, dX1, then dW1 and dW0 on the main stream (the side stream
         # already carries the DGGM backward, dW2 and, with in-backward optimizer steps, the

@@ -339,6 +339,30 @@ def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
+class _NhwcJob(ctypes.Structure):  # rgbd_nhwc_job
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("B", ctypes.c_int), ("C", ctypes.c_int),
+                ("H", ctypes.c_int), ("W", ctypes.c_int)]
+
+
+def nchw_to_nhwc_multi(xs):
+    """Up to four bfloat16 NCHW tensors -> their NHWC copies in one launch
+    (rgbd_nchw_to_nhwc_multi); bitwise nchw_to_nhwc of each."""
+    if not 1 <= len(xs) <= 4:
+        raise ValueError("nchw_to_nhwc_multi: one to four tensors")
+    _need_cuda(*xs)
+    arr = (_NhwcJob * len(xs))()
+    ys = []
+    for i, x in enumerate(xs):
+        if x.dtype != torch.bfloat16 or x.dim() != 4:
+            raise ValueError("nchw_to_nhwc_multi: bfloat16 [B,C,H,W] tensors")
+        B, C, H, W = x.shape
+        y = torch.empty((B, H, W, C), dtype=x.dtype, device=x.device)
+        arr[i] = _NhwcJob(x.data_ptr(), y.data_ptr(), B, C, H, W)
+        ys.append(y)
+    check(_lib.lib().rgbd_nchw_to_nhwc_multi(len(xs), arr, _stream(xs[0].device)), "rgbd_nchw_to_nhwc_multi")
+    return ys
+
+
 def dsam_code_masks(codes):
     """codes: list of uint8 region-code maps -> uint32 device tensor [len(codes)], bit k set when
     code k occurs in map i (the codes the bf16 packed filters are needed for)."""

@@ -162,6 +162,23 @@ def test_nchw_to_nhwc_exact(shape, dtype):
     assert torch.equal(ops.nchw_to_nhwc(x), x.permute(0, 2, 3, 1).contiguous())
 
 
+@pytest.mark.parametrize("shapes", [
+    [(8, 768, 15, 20), (8, 384, 30, 40), (8, 192, 60, 80)],                    # the backward's G[3..1]
+    [(8, 96, 120, 160), (8, 192, 60, 80), (8, 384, 30, 40), (8, 768, 15, 20)],  # the forward's colour maps
+    [(3, 40, 7, 9), (1, 8, 1, 1), (2, 136, 33, 65)],                            # ragged tiles, HW % 8 != 0
+])
+def test_nchw_to_nhwc_multi_exact(shapes):
+    """rgbd_nchw_to_nhwc_multi: every job an exact NHWC copy (16-byte loads where h*w % 8 == 0,
+    element loads otherwise), one launch for all."""
+    g = torch.Generator(device=DEV)
+    g.manual_seed(17)
+    xs = [torch.randn(s, generator=g, device=DEV).bfloat16() for s in shapes]
+    for x, y in zip(xs, ops.nchw_to_nhwc_multi(xs)):
+        assert torch.equal(y, x.permute(0, 2, 3, 1).contiguous())
+    with pytest.raises(ops._lib.RgbdHipError):  # C % 8 != 0
+        ops.nchw_to_nhwc_multi([torch.zeros((1, 12, 5, 5), device=DEV, dtype=torch.bfloat16)])
+
+
 @pytest.mark.parametrize("k", [0, 1, 2])
 def test_dsam_fwd_nhwc_equals_nchw_path(k):
     """rgbd_dsam_fwd_nhwc (NHWC residual in, NHWC out only: the hot path's bf16 cascade) gives
