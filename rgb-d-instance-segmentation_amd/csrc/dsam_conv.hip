@@ -708,6 +708,7 @@ __device__ __forceinline__ void wg_plan_body(const WgArgs& a) {
     a.counts[0] = total;
     a.counts[1] = ni;
     a.counts[2] = 0;  // k_dsam_wgrad_mm's next-work counter
+    a.counts[3] = 0;  // ... and its next channel-sum unit (fold)
   }
   __syncthreads();
   for (int it = tid; it < ibase[16]; it += 1024) {
@@ -760,14 +761,56 @@ __global__ __launch_bounds__(256) void k_wg_masks_legs(const WgLegs L) {
   wg_masks_body(a, blockIdx.x);
 }
 
+// out[(split*B + b)*C + c] = sum over pixel range `split` of g[b][p][c], NHWC bf16 g: workgroup
+// (b, 64 channels, split), thread = channel pair x one of 8 pixel strides, fixed-order combine.
+constexpr int CS_SPLIT_MAX = 16;
+__host__ __device__ inline int chan_sum_splits(int HW) {
+  const int sp = HW / 256;
+  return sp < 1 ? 1 : (sp > CS_SPLIT_MAX ? CS_SPLIT_MAX : sp);
+}
+// one workgroup's share: image b, channels [64 cb, 64 cb + 64), pixel range sp of nsp
+__device__ __forceinline__ void chan_sum_body(const bf16_t* __restrict__ g, int HW, int C, int B, int b, int cb,
+                                              int sp, int nsp, float* __restrict__ out, float2 (*red)[32]) {
+  const int cp = threadIdx.x & 31, sub = threadIdx.x >> 5;
+  const int c = cb * 64 + 2 * cp;
+  const int p0 = (int)((long long)sp * HW / nsp), p1 = (int)((long long)(sp + 1) * HW / nsp);
+  float2 acc = make_float2(0.f, 0.f);
+  if (c < C) {
+    const bf16_t* base = g + (long long)b * HW * C + c;
+#pragma unroll 4
+    for (int p = p0 + sub; p < p1; p += 8) {
+      const uint32_t u = *reinterpret_cast<const uint32_t*>(base + (long long)p * C);
+      acc.x += __uint_as_float(u << 16);
+      acc.y += __uint_as_float(u & 0xffff0000u);
+    }
+  }
+  red[sub][cp] = acc;
+  __syncthreads();
+  if (sub == 0 && c < C) {
+    float2 t = red[0][cp];
+    for (int q = 1; q < 8; ++q) {
+      t.x += red[q][cp].x;
+      t.y += red[q][cp].y;
+    }
+    float* o = out + ((long long)sp * B + b) * C + c;
+    o[0] = t.x;
+    if (c + 1 < C) o[1] = t.y;
+  }
+}
 // NL legs of one output tile shape in one persistent launch: every workgroup drains leg 0's work
 // counter, then leg 1's, ..., so legs that are ready together share the CUs instead of queueing
 // whole-chip launches behind each other (the loop body is instantiated per leg: each leg's
 // arguments stay scalar kernel arguments).
+//
+// With fold set, the workgroups then drain the legs' bias channel sums (chan_sum_body units of the
+// upstream gradient, counter counts[3]) — work that would otherwise be one more launch after the
+// GEMM's drain tail.
 template <int NL>
 struct WgMulti {
   WgArgs a[NL];
-  int n;  // legs in use, 1..NL
+  float* csum[NL];  // [nsplit][B][Cout] channel sums (fold)
+  int n;            // legs in use, 1..NL
+  int fold;
 };
 
 template <int FM, int NL>
@@ -916,20 +959,52 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(const WgMulti<NL> L) {
 #pragma unroll
   for (int l = 0; l < NL; ++l)
     if (l < L.n) run_leg(L.a[l]);
+  if (!L.fold) return;
+  float2(*red)[32] = reinterpret_cast<float2(*)[32]>(smem);  // the ring is free: every wave left the loop
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    if (l >= L.n) break;
+    const WgArgs& a = L.a[l];
+    const int hwo = a.ho * a.wo, nsp = chan_sum_splits(hwo), ncb = (a.Cout + 63) / 64;
+    const int nunit = a.B * ncb * nsp;
+    for (;;) {
+      __syncthreads();
+      if (tid == 0) *next_s = __hip_atomic_fetch_add(a.counts + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int u = *next_s;
+      if (u >= nunit) break;  // uniform: every thread read the same slot
+      const int b = u % a.B, cb = (u / a.B) % ncb, sp = u / (a.B * ncb);
+      chan_sum_body(a.gout, hwo, a.Cout, a.B, b, cb, sp, nsp, L.csum[l], red);
+    }
+  }
 }
 
 // dW_k (per item partials) -> the reference filters, fixed summation order (items in list
 // order: codes ascending, units ascending).  One block per output channel o: the five sums of
 // the row are formed in (tap, c) order with every item's load of a thread in flight together,
 // parked in LDS, then written in the OIHW (c, tap) order.
-__global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restrict__ partial, const int4* __restrict__ items,
-                                                            const int* __restrict__ counts, int Cin, int Cout,
-                                                            float* __restrict__ dconv_w, float* __restrict__ dproj_w,
-                                                            const float* __restrict__ csum, const rgbd_decomp_info* info,
-                                                            int B, int nsplit, float* __restrict__ dbias) {
-  extern __shared__ float srow[];  // [5][9*Cin]
-  __shared__ int scode[1024];      // item -> code, staged once
-  const int KK = 9 * Cin, o = blockIdx.x, ni = counts[1];
+struct CombArgs {
+  const float* partial;
+  const int4* items;
+  const int* counts;
+  int Cin, Cout;
+  float* dconv_w;
+  float* dproj_w;
+  const float* csum;
+  const rgbd_decomp_info* info;
+  int B, nsplit;
+  float* dbias;
+};
+__device__ __forceinline__ void combine_body(const CombArgs& A, int o, float* srow, int* scode) {
+  const float* __restrict__ partial = A.partial;
+  const int4* __restrict__ items = A.items;
+  const int Cin = A.Cin, Cout = A.Cout, B = A.B, nsplit = A.nsplit;
+  float* __restrict__ dconv_w = A.dconv_w;
+  float* __restrict__ dproj_w = A.dproj_w;
+  const float* __restrict__ csum = A.csum;
+  const rgbd_decomp_info* info = A.info;
+  float* __restrict__ dbias = A.dbias;
+  const int KK = 9 * Cin, ni = A.counts[1];
   for (int it = threadIdx.x; it < ni && it < 1024; it += 256) scode[it] = items[it].x;
   __syncthreads();
   // 4 consecutive kk per thread (16-byte loads), 8 items' loads in flight per iteration
@@ -981,6 +1056,20 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const float* __restr
     if (lane == 0) dbias[wv * Cout + o] = sb;
   }
 }
+__global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const CombArgs A) {
+  extern __shared__ float srow[];  // [5][9*Cin]
+  __shared__ int scode[1024];      // item -> code, staged once
+  combine_body(A, blockIdx.x, srow, scode);
+}
+// the combines of two legs in one launch: blocks [0, Cout0) leg 0, then leg 1
+__global__ __launch_bounds__(256) void k_dsam_wgrad_combine2(const CombArgs A0, const CombArgs A1) {
+  extern __shared__ float srow[];
+  __shared__ int scode[1024];
+  if ((int)blockIdx.x < A0.Cout)
+    combine_body(A0, blockIdx.x, srow, scode);
+  else
+    combine_body(A1, blockIdx.x - A0.Cout, srow, scode);
+}
 
 __global__ void k_dsam_wgrad_final(const float* __restrict__ partial, int splits, int Cin, int Cout,
                                    float* __restrict__ dconv_w, float* __restrict__ dproj_w) {
@@ -1013,38 +1102,10 @@ __global__ __launch_bounds__(256) void k_chan_sum(const T* __restrict__ g, int H
   if (threadIdx.x == 0) out[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// out[(split*B + b)*C + c] = sum over pixel range `split` of g[b][p][c], NHWC bf16 g: workgroup
-// (b, 64 channels, split), thread = channel pair x one of 8 pixel strides, fixed-order combine.
-constexpr int CS_SPLIT_MAX = 16;
-inline int chan_sum_splits(int HW) { return std::max(1, std::min(CS_SPLIT_MAX, HW / 256)); }
 __global__ __launch_bounds__(256) void k_chan_sum_nhwc(const bf16_t* __restrict__ g, int HW, int C,
                                                        float* __restrict__ out) {
   __shared__ float2 red[8][32];
-  const int b = blockIdx.x, cp = threadIdx.x & 31, sub = threadIdx.x >> 5, sp = blockIdx.z;
-  const int c = blockIdx.y * 64 + 2 * cp;
-  const int p0 = (int)((long long)sp * HW / gridDim.z), p1 = (int)((long long)(sp + 1) * HW / gridDim.z);
-  float2 acc = make_float2(0.f, 0.f);
-  if (c < C) {
-    const bf16_t* base = g + (long long)b * HW * C + c;
-#pragma unroll 4
-    for (int p = p0 + sub; p < p1; p += 8) {
-      const uint32_t u = *reinterpret_cast<const uint32_t*>(base + (long long)p * C);
-      acc.x += __uint_as_float(u << 16);
-      acc.y += __uint_as_float(u & 0xffff0000u);
-    }
-  }
-  red[sub][cp] = acc;
-  __syncthreads();
-  if (sub == 0 && c < C) {
-    float2 t = red[0][cp];
-    for (int q = 1; q < 8; ++q) {
-      t.x += red[q][cp].x;
-      t.y += red[q][cp].y;
-    }
-    float* o = out + ((long long)sp * gridDim.x + b) * C + c;
-    o[0] = t.x;
-    if (c + 1 < C) o[1] = t.y;
-  }
+  chan_sum_body(g, HW, C, gridDim.x, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, out, red);
 }
 
 __global__ __launch_bounds__(256) void k_dsam_bias_grad(const float* __restrict__ csum, const rgbd_decomp_info* info,
@@ -2148,24 +2209,41 @@ size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int
   return wgrad_ws(dtype, B, Cin, h, w, Cout).total;
 }
 
+constexpr int kCombineDyn = 163840 - 1024 * 4;  // the combine's static item -> code table
+static CombArgs comb_args(const WgArgs& a, bool nchw_sums, const float* csum, const rgbd_decomp_info* info,
+                          float* dconv_w, float* dproj_w, float* dbias) {
+  CombArgs c;
+  c.partial = a.partial;
+  c.items = a.items;
+  c.counts = a.counts;
+  c.Cin = a.Cin;
+  c.Cout = a.Cout;
+  c.dconv_w = dconv_w;
+  c.dproj_w = dproj_w;
+  c.csum = csum;
+  c.info = info;
+  c.B = a.B;
+  c.nsplit = nchw_sums ? 1 : chan_sum_splits(a.ho * a.wo);
+  c.dbias = dbias;
+  return c;
+}
+
 // bf16 dW after the GEMM: the upstream gradient's channel sums (bias), then the combine of the
 // item partials into the reference filters (it also writes the bias gradients)
 static int wg_finish(const WgArgs& a, const void* gout_nchw, float* csum, const rgbd_decomp_info* info,
-                     float* dconv_w, float* dproj_w, float* dbias, hipStream_t s) {
+                     float* dconv_w, float* dproj_w, float* dbias, hipStream_t s, bool sums_folded) {
   const int hwo = a.ho * a.wo;
   if (gout_nchw)
     k_chan_sum<bf16_t><<<a.B * a.Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
-  else
+  else if (!sums_folded)
     k_chan_sum_nhwc<<<dim3(a.B, ceil_div(a.Cout, 64), chan_sum_splits(hwo)), 256, 0, s>>>(a.gout, hwo, a.Cout, csum);
   const int csmem = 5 * 9 * a.Cin * (int)sizeof(float);
-  constexpr int kCombineDyn = 163840 - 1024 * 4;  // the kernel's static item -> code table
   static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
   if (cattr != hipSuccess) return (int)cattr;
   RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
-  const int nsplit_bf = gout_nchw ? 1 : chan_sum_splits(hwo);
-  k_dsam_wgrad_combine<<<a.Cout, 256, csmem, s>>>(a.partial, a.items, a.counts, a.Cin, a.Cout, dconv_w, dproj_w, csum,
-                                                  info, a.B, nsplit_bf, dbias);
+  k_dsam_wgrad_combine<<<a.Cout, 256, csmem, s>>>(comb_args(a, gout_nchw != nullptr, csum, info, dconv_w, dproj_w,
+                                                            dbias));
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -2202,10 +2280,12 @@ static int bwd_weight(int dtype, const void* gout_nchw, const void* gout_nhwc, c
     WgMulti<1> m;
     m.a[0] = wg_args(L, P, plan, partial, gout_nhwc, x_nhwc, code, B, Cin, h, w, Cout);
     m.n = 1;
+    m.csum[0] = csum;
+    m.fold = gout_nchw == nullptr;  // NHWC bias sums drained by the GEMM's workgroups
     if (!planned) wg_plan_launch(1, &m.a[0], &P, s);
     const hipError_t e = launch_wg_fm(P.fm, m, s);
     if (e != hipSuccess) return (int)e;
-    return wg_finish(m.a[0], gout_nchw, csum, info, dconv_w, dproj_w, dbias, s);
+    return wg_finish(m.a[0], gout_nchw, csum, info, dconv_w, dproj_w, dbias, s, m.fold);
   } else {
     return RGBD_E_DTYPE;
   }
@@ -2237,6 +2317,7 @@ int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, cons
   TimerScope ts("dsam_wgrad", s);
   WgMulti<2> m;
   int fm[2];
+  m.fold = 1;
   for (int i = 0; i < n; ++i) {
     const rgbd_dsam_dw_run& r = runs[i];
     RGBD_REQUIRE(r.gout_nhwc && r.x_nhwc && r.code && r.dconv_w && r.dproj_w && r.dbias && r.plan && r.ws, RGBD_E_ARG);
@@ -2246,6 +2327,7 @@ int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, cons
     RGBD_REQUIRE(wg_shape_ok(r.B, r.Cin, r.h, r.w, r.Cout, P), RGBD_E_SHAPE);
     float* partial = (float*)((char*)r.ws + L.partial - L.plan_total);
     m.a[i] = wg_args(L, P, (char*)r.plan, partial, r.gout_nhwc, r.x_nhwc, r.code, r.B, r.Cin, r.h, r.w, r.Cout);
+    m.csum[i] = (float*)((char*)r.ws + L.csum - L.plan_total);
     fm[i] = P.fm;
   }
   for (int i = 0; i + 1 < n; ++i)  // distinct buffers: the legs run together
@@ -2259,18 +2341,26 @@ int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, cons
     for (int i = 0; i < n && e == hipSuccess; ++i) {
       WgMulti<1> one;
       one.a[0] = m.a[i];
+      one.csum[0] = m.csum[i];
       one.n = 1;
+      one.fold = 1;
       e = launch_wg_fm(fm[i], one, s);
     }
   }
   if (e != hipSuccess) return (int)e;
-  for (int i = 0; i < n; ++i) {
-    const rgbd_dsam_dw_run& r = runs[i];
-    const WgradWs L = wgrad_ws(RGBD_BF16, r.B, r.Cin, r.h, r.w, r.Cout);
-    float* csum = (float*)((char*)r.ws + L.csum - L.plan_total);
-    const int rc = wg_finish(m.a[i], nullptr, csum, info, r.dconv_w, r.dproj_w, r.dbias, s);
-    if (rc != RGBD_OK) return rc;
-  }
+  if (n == 1)  // the bias sums were drained by the GEMM's workgroups (fold)
+    return wg_finish(m.a[0], nullptr, m.csum[0], info, runs[0].dconv_w, runs[0].dproj_w, runs[0].dbias, s, true);
+  // both legs' combines in one launch
+  const int csmem = 5 * 9 * std::max(runs[0].Cin, runs[1].Cin) * (int)sizeof(float);
+  static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine2,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
+  if (cattr != hipSuccess) return (int)cattr;
+  RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
+  CombArgs c[2];
+  for (int i = 0; i < 2; ++i)
+    c[i] = comb_args(m.a[i], false, m.csum[i], info, runs[i].dconv_w, runs[i].dproj_w, runs[i].dbias);
+  k_dsam_wgrad_combine2<<<runs[0].Cout + runs[1].Cout, 256, csmem, s>>>(c[0], c[1]);
+  RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
 
