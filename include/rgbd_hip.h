@@ -283,8 +283,8 @@ int rgbd_dsam_bwd_weight_planned(int dtype, const void* gout_nchw, const void* g
                                  float* dbias, const void* plan, void* ws, void* stream);
 /* dW of several bf16 DSAM legs that are ready together (the hot path's dsam1 and dsam0 once the dX
  * cascade has finished; hot_path.py): one persistent GEMM launch over the legs' joint work list —
- * two back-to-back whole-chip launches would each drain on a partly idle chip — then each leg's
- * bias sums and combine.  Per leg the results are bitwise those of rgbd_dsam_bwd_weight_planned
+ * two back-to-back whole-chip launches would each drain on a partly idle chip; its workgroups
+ * then drain the legs' bias channel sums — and one launch for both legs' combines.  Per leg the results are bitwise those of rgbd_dsam_bwd_weight_planned
  * with gout_nchw = NULL (the autograd of DSAModule.forward, custom_model.py:682-699).  n: 1 or 2;
  * every run has its own plan and ws (rgbd_dsam_run_workspace_size(RGBD_LEG_DW, ...)).  Legs of
  * different output tile shapes run one launch each. */
