@@ -302,6 +302,15 @@ typedef struct rgbd_dsam_dw_run {
 int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, const rgbd_decomp_info* info,
                                        void* stream);  /* runs: host array */
 
+/* ---------------------------------------------------------------- optimizer step
+ * AdamW (the HF Trainer's optimizer, finetuning.py:98, lr 1e-5 constant per config.json:12-13) over
+ * n <= 48 fp32 tensors in one launch, the element update of torch.optim.AdamW (decoupled weight
+ * decay, no amsgrad): params, grads, exp_avg, exp_avg_sq, numel are host arrays of device
+ * pointers / sizes; step points at the (already incremented) step count on the device. */
+int rgbd_adamw_multi(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                     float* const* exp_avg_sq, const long long* numel, const float* step, double lr, double beta1,
+                     double beta2, double eps, double weight_decay, void* stream);
+
 /* ---------------------------------------------------------------- K4 ratio predictor
  * EnhancedDepthImageRatioPredictor.forward (custom_model.py:1444-1487) for the batch:
  * depth3 (float32 planes as for the decomposition) -> ratio float32 [B] in [0.01, 0.5],
