@@ -202,6 +202,7 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False):
     from rgbd_amd.distributed import (BufferBroadcaster, InBackwardOptimizer, OverlappedGradReducer,
                                       hot_path_grad_groups)
     from rgbd_amd.hot_path import hot_path, prepare
+    from rgbd_amd.optim import HipAdamW
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
     groups = hot_path_grad_groups(ctx["dsams"], ctx["dg"])
     # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
@@ -211,11 +212,10 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False):
     if overlap_opt:
         # dsam2's update as soon as its gradients are in (under the rest of the backward), the
         # rest in one launch at the end
-        inb = InBackwardOptimizer(groups, lambda g: torch.optim.AdamW(g, lr=1e-5, fused=True, capturable=capturable),
-                                  reducer, steps=((0,), (1, 2)))
+        inb = InBackwardOptimizer(groups, lambda g: HipAdamW(g, lr=1e-5), reducer, steps=((0,), (1, 2)))
         hook, opt = inb.hook, None
     else:
-        opt = torch.optim.AdamW(params, lr=1e-5, fused=True, capturable=capturable)
+        opt = HipAdamW(params, lr=1e-5)  # AdamW on HIP (rgbd_adamw_multi); always capturable
 
     def forward_backward():
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])

@@ -4,7 +4,7 @@ update (decoupled weight decay, no amsgrad, no maximize).  One launch per group 
 tensors; the step count lives on the device, so the step can be captured into a HIP graph
 (``capturable`` is always true).  fp32 parameters and gradients on the GPU only.
 
-Not yet the bench's optimizer: DESIGN.md §9 (the fused torch AdamW at the step's tail)."""
+bench.py's optimizer (in-backward groups and the captured step); DESIGN.md §9."""
 import ctypes
 
 import torch

@@ -80,6 +80,7 @@ def test_captured_step_needs_capturable_optimizer():
     from rgbd_amd.train_graph import CapturedTrainStep
     args = bench.parse(["--height", "64", "--width", "96", "--batch", "2"])
     ctx = _ctx(bench, args)
-    fb, ob, _, _ = bench.make_parts(ctx, 1)
+    fb, _, _, _ = bench.make_parts(ctx, 1)  # (bench's own optimizer, HipAdamW, is always capturable)
+    params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
     with pytest.raises(ValueError, match="capturable"):
-        CapturedTrainStep(fb, ob.opt)
+        CapturedTrainStep(fb, torch.optim.AdamW(params, lr=1e-5, fused=True))
