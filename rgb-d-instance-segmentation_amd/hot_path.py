@@ -138,12 +138,26 @@ class Prepared:
     decomposition (grey plane, histogram, modes: ops.edsam_modes) and, in bf16, the NHWC copies
     of the colour maps — launched on the side stream so they run beside the ratio predictor."""
 
-    def __init__(self, side, pixel_values, modes, colors, nhwc, dtype):
+    def __init__(self, side, pixel_values, modes, colors, nhwc, dtype, sources):
         self.side, self.pixel_values, self.modes = side, pixel_values, modes
         self.colors, self.nhwc, self.dtype = colors, nhwc, dtype
+        self.sources = sources  # (data_ptr, shape) of the pixel_values and colour maps it was built from
+
+    def check(self, pixel_values, colors):
+        """Refuse a Prepared built from other tensors than the ones hot_path() is given: it would
+        silently compute features of another batch (the autograd inputs would not be the
+        tensors whose copies the kernels read)."""
+        got = _sources(pixel_values, colors)
+        if got != self.sources:
+            raise ValueError("hot_path: `prepared` was built from other pixel_values / colour maps than the ones "
+                             "passed (prepare() and hot_path() must get the same tensors)")
 
     def join(self):
         self.side.join()
+
+
+def _sources(pixel_values, colors):
+    return tuple((t.data_ptr(), tuple(t.shape)) for t in (pixel_values, *colors))
 
 
 def prepare(pixel_values, colors, dtype=torch.float32):
@@ -160,7 +174,7 @@ def prepare(pixel_values, colors, dtype=torch.float32):
         nhwc = ops.nchw_to_nhwc_multi(cols) if bf16 else None
         return [m.info, m.ws, m.masks, nhwc]
     _, _, _, nhwc = side.run(work, pv, *cols)
-    return Prepared(side, pv, held["modes"], cols, nhwc, dtype)
+    return Prepared(side, pv, held["modes"], cols, nhwc, dtype, _sources(pixel_values, colors))
 
 
 class HotPathFunction(torch.autograd.Function):
@@ -353,5 +367,7 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
         params += [conv.weight, conv.bias]
     cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook, "status_sink": status_sink,
            "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": True, "prepared": prepared}
+    if prepared is not None:
+        prepared.check(pixel_values, colors)
     pv = prepared.pixel_values if prepared is not None else pixel_values.detach().float().contiguous()
     return list(HotPathFunction.apply(pv, ratio, cfg, *colors, *params))

@@ -7,10 +7,11 @@ runs ``COCOeval`` (``evaluate`` / ``accumulate`` / ``summarize``).  Neither libr
 here, so this module restates that evaluation:
 
   * update(): every image's detection and ground-truth masks are packed into bitmaps on the GPU
-    with their areas (csrc/mask_iou.hip ``rgbd_pack_mask_bits``) and kept there;
-  * compute(): per image, the intersections of every (detection, ground truth) pair in one
-    launch (``rgbd_mask_intersections``), IoU = inter / union (0 when inter == 0, as rleIou),
-    then COCOeval's per (image, category) greedy matching at the 10 IoU thresholds
+    with their areas (csrc/mask_iou.hip ``rgbd_pack_mask_bits``), the intersections of every
+    (detection, ground truth) pair follow in one launch per image (``rgbd_mask_intersections``),
+    and one device-to-host copy per update keeps only those small arrays (the bitmaps are
+    freed; torchmetrics likewise keeps compact RLEs, not masks);
+  * compute(): per image IoU = inter / union (0 when inter == 0, as rleIou), then COCOeval's per (image, category) greedy matching at the 10 IoU thresholds
     0.50:0.05:0.95 and the area ranges all / small (< 32^2) / medium / large (> 96^2), detections
     ordered by score (stable) and capped at 100, the 101-point interpolated precision and the
     recall per category, and the 12 summary numbers; with ``class_metrics`` the per-category
@@ -202,22 +203,31 @@ class MeanAveragePrecision:
     def update(self, preds, target):
         if len(preds) != len(target):
             raise ValueError("preds and target must have the same number of images")
+        parts, shapes = [], []
         for p, t in zip(preds, target):
             det = _Packed(p["masks"], self.device)
             gt = _Packed(t["masks"], self.device)
+            inter = _intersections(det, gt, self.device)
+            parts += [inter.reshape(-1), det.area, gt.area]
+            shapes.append((det.n, gt.n))
             self._images.append({
-                "det": det, "gt": gt,
                 "scores": np.asarray(torch.as_tensor(p["scores"]).float().cpu().numpy(), dtype=np.float64).reshape(-1),
-                "dlab": np.asarray(torch.as_tensor(p["labels"]).cpu().numpy()).astype(np.int64).reshape(-1),
-                "glab": np.asarray(torch.as_tensor(t["labels"]).cpu().numpy()).astype(np.int64).reshape(-1)})
+                "det_labels": np.asarray(torch.as_tensor(p["labels"]).cpu().numpy()).astype(np.int64).reshape(-1),
+                "gt_labels": np.asarray(torch.as_tensor(t["labels"]).cpu().numpy()).astype(np.int64).reshape(-1)})
+        if not shapes:
+            return
+        flat = torch.cat(parts).cpu().numpy()  # the update's one copy back; bitmaps die with det / gt
+        off = 0
+        for im, (nd, ng) in zip(self._images[len(self._images) - len(shapes):], shapes):
+            im["inter"] = flat[off:off + nd * ng].reshape(nd, ng)
+            off += nd * ng
+            im["det_area"] = flat[off:off + nd]
+            off += nd
+            im["gt_area"] = flat[off:off + ng]
+            off += ng
 
     def compute(self):
-        recs = []
-        for im in self._images:
-            recs.append({"inter": _intersections(im["det"], im["gt"], self.device).cpu().numpy(),
-                         "det_area": im["det"].area.cpu().numpy(), "gt_area": im["gt"].area.cpu().numpy(),
-                         "scores": im["scores"], "det_labels": im["dlab"], "gt_labels": im["glab"]})
-        return coco_segm_summary(recs, self.class_metrics)
+        return coco_segm_summary(self._images, self.class_metrics)
 
 
 def coco_segm_summary(records, class_metrics=False):

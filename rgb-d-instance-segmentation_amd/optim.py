@@ -1,8 +1,12 @@
-"""AdamW on the HIP kernel (csrc/adamw.hip, rgbd_adamw_multi): the optimizer the reference's HF
-Trainer builds (finetuning.py:98; lr 1e-5 constant, config.json:12-13), with torch.optim.AdamW's
-update (decoupled weight decay, no amsgrad, no maximize).  One launch per group of up to 48
-tensors; the step count lives on the device, so the step can be captured into a HIP graph
+"""AdamW on the HIP kernel (csrc/adamw.hip, rgbd_adamw_multi), with torch.optim.AdamW's update
+(decoupled weight decay, no amsgrad, no maximize).  One launch per group of up to 48 tensors;
+the step count lives on the device, so the step can be captured into a HIP graph
 (``capturable`` is always true).  fp32 parameters and gradients on the GPU only.
+
+The constructor defaults are torch's (weight_decay 1e-2).  The optimizer the reference's HF
+Trainer builds (finetuning.py:98) is ``HipAdamW(params, **HF_TRAINER_ADAMW)``: lr 1e-5 constant
+(mask2former/config.json:12-13) and TrainingArguments' defaults for the rest — weight_decay
+0.0 (config.json does not set it), betas (0.9, 0.999), eps 1e-8.
 
 bench.py's optimizer (in-backward groups and the captured step); DESIGN.md §9."""
 import ctypes
@@ -14,6 +18,9 @@ from ._lib import check
 from .ops import _stream
 
 _MAXT = 48
+# HF TrainingArguments' AdamW (adam_beta1/2, adam_epsilon, weight_decay defaults) at the
+# reference's learning rate (mask2former/config.json:12)
+HF_TRAINER_ADAMW = dict(lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0)
 
 
 class HipAdamW(torch.optim.Optimizer):
@@ -23,15 +30,21 @@ class HipAdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, capturable=True))
 
     def _group_state(self, group):
-        """The group's parameters with gradients; their moments, and ONE step count per group
-        (every parameter of a training step gets a gradient every step, as here; a parameter
-        that first receives one later joins the group's count instead of starting its own)."""
+        """The group's parameters with gradients, their moments, and ONE step count per group
+        (one device tensor, so a captured graph advances every parameter's step with one kernel).
+        That is torch's per-parameter count only while every parameter of the group is stepped
+        every time; a parameter that would join a group whose count already runs (its first
+        gradient arriving after other parameters' first step) would inherit the group's count
+        and a wrong bias correction, so it is refused."""
         params = [p for p in group["params"] if p.grad is not None]
         shared = None
         for p in group["params"]:
             if p in self.state and "step" in self.state[p]:
                 shared = self.state[p]["step"]
                 break
+        if shared is not None and any(not self.state[p] for p in params):
+            raise RuntimeError("HipAdamW: a parameter received its first gradient after the rest of its group "
+                               "had stepped; its step count would not be its own (put it in its own group)")
         for p in params:
             if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous():
                 raise RuntimeError("HipAdamW: contiguous float32 CUDA parameters only (no CPU fallback)")
@@ -71,4 +84,26 @@ class HipAdamW(torch.optim.Optimizer):
                 check(L.rgbd_adamw_multi(n, P, G, M, V, N, ctypes.c_void_p(step.data_ptr()), float(group["lr"]),
                                          float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
                                          _stream(run[0].device)), "rgbd_adamw_multi")
+            # the kernel wrote through raw pointers: bump the version counters (host only, safe
+            # under capture) so autograd's saved-tensor checks and version-keyed caches see it
+            torch.autograd.graph.increment_version(params)
         return loss
+
+    def load_state_dict(self, state_dict):
+        """torch's load, then the one-step-count-per-group invariant restored: torch moves each
+        parameter's ``step`` separately, which would untie them (after which only the first
+        parameter's count would advance).  Every parameter of a group gets the group's first
+        stored count as its (shared) step tensor; the counts of a group must agree."""
+        super().load_state_dict(state_dict)
+        for group in self.param_groups:
+            steps = [self.state[p]["step"] for p in group["params"] if p in self.state and "step" in self.state[p]]
+            if not steps:
+                continue
+            vals = {float(s) for s in steps}
+            if len(vals) != 1:
+                raise ValueError(f"HipAdamW.load_state_dict: parameters of one group at different steps {sorted(vals)}")
+            dev = group["params"][0].device
+            shared = steps[0].detach().to(device=dev, dtype=torch.float32).clone()
+            for p in group["params"]:
+                if p in self.state and "step" in self.state[p]:
+                    self.state[p]["step"] = shared

@@ -16,6 +16,7 @@ outside the hot path).
 import torch
 
 from . import ops
+from .graph_guard import check_and_instantiate
 from .hot_path import hot_path, prepare
 
 
@@ -53,9 +54,10 @@ class StreamingHotPath:
                 for _ in range(2):
                     self._run()
             torch.cuda.current_stream().wait_stream(s)
-            self.graph = torch.cuda.CUDAGraph()
+            self.graph = torch.cuda.CUDAGraph(keep_graph=True)
             with torch.cuda.graph(self.graph):
                 self.outs = self._run()
+            self.width = check_and_instantiate(self.graph, "StreamingHotPath")
         return self
 
     def __call__(self, depth_u8=None, rgb_u8=None, colors=None):

@@ -21,6 +21,8 @@ Single process only: with data parallelism the step's gradient all-reduce runs t
 """
 import torch
 
+from .graph_guard import check_and_instantiate
+
 
 class CapturedTrainStep:
     """``fb()`` runs forward + backward and leaves the gradients in ``p.grad``; ``opt`` is the
@@ -50,11 +52,13 @@ class CapturedTrainStep:
                     self.opt.step()
                 clear()
         torch.cuda.current_stream().wait_stream(self.stream)
-        self.graph = torch.cuda.CUDAGraph()
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(self.graph, stream=self.stream):
             self.outs = self.fb()
             if opt is not None:
                 self.opt.step()
+        # at most two concurrent branches, or the bundled runtime's first launch crashes (§5.1)
+        self.width = check_and_instantiate(self.graph, "CapturedTrainStep")
 
     def __call__(self):
         self.graph.replay()

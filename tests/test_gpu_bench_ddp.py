@@ -1,5 +1,7 @@
-"""Row (e) on the GPU: bench.py's data-parallel step at world size 2 (both ranks on the one
-MI355X of the test box, gloo — RCCL refuses two ranks on one device).
+"""Row (e) on the GPU: bench.py's data-parallel step at world size 2 — gloo with both ranks on
+the one MI355X of a one-GPU test box (RCCL refuses two ranks on one device), and RCCL ("nccl",
+one rank per device) when the box shows two or more GPUs (skipped otherwise), so the driver's
+multi-GPU scaling run is not the first execution of the RCCL path.
 
 * the launcher: ``bench.py --gpus 2`` spawns two ranks and reports n_gpus 2 / global batch 16;
 * DDP semantics of the step (the reference's Trainer, finetuning.py:98-113): after the
@@ -22,12 +24,22 @@ pytestmark = pytest.mark.gpu
 REPO = Path(__file__).resolve().parents[1]
 
 
+def _need_devices(backend):
+    if backend == "nccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs one device per rank: this box shows fewer than 2 GPUs")
+
+
+BACKENDS = ["gloo", "nccl"]
+
+
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("backend", BACKENDS)
 @pytest.mark.parametrize("H,W", [(96, 128), (480, 640)], ids=["96x128", "C3_640x480"])
-def test_bench_launcher_world2_json(H, W):
+def test_bench_launcher_world2_json(H, W, backend):
     """bench.py --gpus 2 end to end (its own launcher, 8 images per rank), incl. BASELINE's C3
-    shape; gloo, both ranks on the test box's one GPU."""
-    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "2",
+    shape; gloo with both ranks on the test box's one GPU, or RCCL on two GPUs."""
+    _need_devices(backend)
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", backend, "--steps", "2",
                         "--warmup", "1", "--cpu-baseline", "0", "--c5-stream", "0", "--inference", "0", "--parity", "0",
                         "--height", str(H), "--width", str(W)],
                        capture_output=True, text=True, timeout=280, cwd=REPO)
@@ -37,6 +49,7 @@ def test_bench_launcher_world2_json(H, W):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 16
     assert out["distributed"]["world_size"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["distributed"]["backend"] == backend
     assert out["value"] > 0
 
 
@@ -48,14 +61,19 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, shape):
+def _worker(rank, world, port, q, shape, backend):
     try:
         import torch.distributed as dist
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if backend == "nccl":  # RCCL: one device per rank
+            dev = torch.device("cuda", rank)
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dev = torch.device("cuda:0")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         sys.path.insert(0, str(REPO))
         import bench
-        dev = torch.device("cuda:0")
         H, W, B = shape
         args = bench.parse(["--height", str(H), "--width", str(W), "--batch", str(B)])
         # standalone gradients of both shards (ratio predictor in eval: a deterministic ratio)
@@ -86,7 +104,8 @@ def _worker(rank, world, port, q, shape):
         ctx["rp"].register_forward_pre_hook(lambda m, a: seen.__setitem__("bufs", [b.clone() for b in m.buffers()]))
         fb, _, _, _ = bench.make_parts(ctx, world)
         fb()
-        flat = torch.cat([b.double().reshape(-1) for b in seen["bufs"]]).cpu()
+        flat = torch.cat([b.double().reshape(-1) for b in seen["bufs"]])
+        flat = flat.to(dev) if backend == "nccl" else flat.cpu()
         other = flat.clone()
         dist.broadcast(other, src=0)
         buf_err = float((flat - other).abs().max())
@@ -111,14 +130,17 @@ def _worker(rank, world, port, q, shape):
 
 
 @pytest.mark.timeout(400)
+@pytest.mark.parametrize("backend", BACKENDS)
 @pytest.mark.parametrize("shape", [(96, 128, 3), (480, 640, 8)], ids=["96x128_b3", "C3_640x480_b8"])
-def test_ddp_step_gradients_and_buffers_world2(shape):
+def test_ddp_step_gradients_and_buffers_world2(shape, backend):
     """Small shape, and BASELINE configs[2] (C3) at its workload: 640x480, 8 images per rank, bf16,
-    world size 2 (global batch 16) — gloo with both ranks on the one GPU of the test box."""
+    world size 2 (global batch 16) — gloo with both ranks on the one GPU of the test box, or RCCL
+    with one rank per GPU where the box has two."""
+    _need_devices(backend)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shape)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shape, backend)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=360) for _ in procs)

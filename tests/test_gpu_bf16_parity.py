@@ -142,3 +142,21 @@ def test_bf16_full_model_mask_logits_vs_g7_640x480():
     assert f32["input_sha_match"] and b16["input_sha_match"]
     assert f32["mask_logit_max_abs_err"] <= 1e-3
     assert b16["mask_logit_max_rel_err"] <= bench.BF16_LOGIT_REL_TOL
+
+
+@pytest.mark.timeout(240)
+def test_bf16_error_split_flips_vs_arithmetic_g7():
+    """The bf16 mask-logit error at G7 split into its two sources: (a) the region-code cells the
+    bf16 ratio flips (decomposition at the bf16 ratio vs at the reference's float32 ratio), and
+    (b) the bf16 DSAM / DGGM arithmetic alone, with the ratio predictor in float32 (the
+    reference's ratio: no decision flips).  (b) is bounded by the same relative tolerance; with
+    no flips (a = 0) the two runs must agree on every decision."""
+    import bench
+    b16 = bench.parity(torch.device(DEV), torch.bfloat16)
+    arith = bench.parity(torch.device(DEV), torch.bfloat16, ratio_fp32=True)
+    print(f"G7 bf16: flipped region-code cells {b16['region_code_cells_flipped']}, rel err {b16['mask_logit_max_rel_err']:.3g}; "
+          f"float32 ratio: flipped {arith['region_code_cells_flipped']}, rel err {arith['mask_logit_max_rel_err']:.3g}")
+    assert arith["ratio_rel_err"] == 0.0
+    assert arith["region_code_cells_flipped"] == [0.0, 0.0, 0.0]
+    assert arith["mask_logit_max_rel_err"] <= bench.BF16_LOGIT_REL_TOL
+    assert max(b16["region_code_cells_flipped"]) <= FLIP_FRAC_SPREAD
