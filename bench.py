@@ -99,6 +99,8 @@ def parse(argv=None):
                     help="also report the C5 RealSense 1280x720 B=1 streaming inference rate (rank 0, N=1)")
     ap.add_argument("--parity", type=int, default=1,
                     help="report the fp32 mask-logit max-abs-err vs the committed 640x480 fixture (rank 0)")
+    ap.add_argument("--full-model", type=int, default=1,
+                    help="also report the whole drop-in model's bf16 training step at 640x480 B=8 (rank 0, N=1)")
     ap.add_argument("--graph", type=int, default=1,
                     help="N=1: time the step replayed from a HIP graph (rgbd_amd/train_graph.py); the eager "
                          "rate and the per-kernel HIP-event timings come from an eager pass beside it")
@@ -490,6 +492,71 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False):
     return res
 
 
+def full_model(dev, B=8, H=480, W=640, steps=5, warmup=2):
+    """The whole drop-in model (CustomMask2FormerForUniversalSegmentation v0.4.0: Swin-T, the hot
+    path, the MSDeformAttn pixel decoder, the masked-attention decoder, the Hungarian-matched
+    loss with 9 auxiliary outputs; custom_model.py:37-53), one bf16-autocast training step
+    (forward with labels, backward, AdamW lr 1e-5) on synthetic NYUv2-shaped scenes with their
+    instance masks, deterministic random-init weights (48 labels).  Eager; ``kernel_ms`` = the
+    five kernels with the most device time in one step (torch.profiler over the HIP runtime)."""
+    from rgbd_amd import init as winit, ops, synthetic
+    from rgbd_amd.config import standard_config
+    from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
+    scenes = [synthetic.make_scene(synthetic.scene_seed(4, i), H, W) for i in range(B)]
+    depth = torch.from_numpy(np.stack([s["depth_u8"] for s in scenes])).to(dev)
+    rgb = torch.from_numpy(np.stack([s["rgb_u8"] for s in scenes])).contiguous().to(dev)
+    mask_labels = [torch.from_numpy(s["masks"].astype(np.float32)).to(dev) for s in scenes]
+    class_labels = [torch.from_numpy(s["classes"]).to(dev) for s in scenes]
+    torch.manual_seed(0)
+    m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
+    winit.init_deterministic(m)
+    m.set_compute_dtype(torch.bfloat16).to(dev).train()
+    opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, fused=True)
+
+    def step():
+        pv = ops.assemble_pixel_values(depth, rgb)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m(pixel_values=pv, mask_labels=mask_labels, class_labels=class_labels)
+        out.loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return out.loss
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    kernels = None
+    try:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            step()
+            torch.cuda.synchronize()
+        tot, cnt = {}, {}
+        for ev in prof.events():
+            if ev.device_type.name == "CUDA" or getattr(ev, "device_time", 0):
+                t = getattr(ev, "device_time", None) or getattr(ev, "cuda_time", 0)
+                if t:
+                    tot[ev.name] = tot.get(ev.name, 0.0) + t
+                    cnt[ev.name] = cnt.get(ev.name, 0) + 1
+        top = sorted(tot.items(), key=lambda kv: -kv[1])[:5]
+        kernels = {"kernel_ms_top5": {k[:90]: round(v / 1e3, 3) for k, v in top},
+                   "launches_top5": {k[:90]: cnt[k] for k, _ in top},
+                   "kernel_ms_total": round(sum(tot.values()) / 1e3, 2), "launches": int(sum(cnt.values()))}
+    except Exception as e:  # the profiler is a report, not the measurement
+        kernels = {"profiler_error": repr(e)[:200]}
+    res = {"workload": "whole drop-in model training step (Swin-T + hot path + pixel decoder + masked-attention "
+                       "decoder + Hungarian-matched loss, 9 aux outputs, AdamW), bf16 autocast, eager",
+           "batch": B, "shape": f"{W}x{H}", "img_s": round(B / dt, 2), "ms_per_step": round(dt * 1e3, 2),
+           "steps": steps, "loss": round(float(loss.detach()), 4), **kernels}
+    del m, opt
+    torch.cuda.empty_cache()
+    return res
+
+
 def read_timings(L):
     """{scope: (total ms, launches)} of the HIP-event timers since rgbd_timing_enable(1)."""
     cnt = ctypes.c_int(0)
@@ -631,6 +698,8 @@ def main():
         out["parity"]["bf16_ratio_fp32"] = parity(dev, torch.bfloat16, ratio_fp32=True)
     if rank == 0 and world == 1 and args.c5_stream:
         out["c5_stream"] = c5_stream(ctx)
+    if rank == 0 and world == 1 and args.full_model:
+        out["full_model"] = full_model(dev)
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, args)
     if rank == 0:

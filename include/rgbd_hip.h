@@ -489,6 +489,9 @@ int rgbd_mask_intersections(const unsigned long long* a, int na, const unsigned 
 #define RGBD_ACT_RELU 1
 #define RGBD_ACT_GELU 2
 #define RGBD_ACT_RELU_GRAD 3
+/* OR'ed into act: bias is indexed by the row m instead of the column n (float32 [M]) — the
+ * output channel of a convolution computed as C[b][o][p] = W[o][k] col[b][k][p] (NCHW). */
+#define RGBD_BIAS_M 16
 size_t rgbd_gemm_workspace_size(int M, int N, int batch, int splits);
 int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, long long lda, long long sa,
               const void* B, long long ldb, long long sb, const float* bias, int act, const void* R, long long ldr,
@@ -515,6 +518,16 @@ size_t rgbd_layernorm_bwd_workspace_size(int rows, int C);
 int rgbd_layernorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy, const float* gamma,
                        const float* mean, const float* rstd, int rows, int C, void* dx, float* dgamma,
                        float* dbeta, void* ws, void* stream);
+
+/* f2 convolutions as GEMMs (csrc/conv.hip): the im2col operand of
+ *   Y[b][o][p] = sum_k W[o][k] col[b][k][p] (+ bias[o])  (rgbd_gemm, RGBD_BIAS_M),
+ * k = (c*KH + ky)*KW + kx (torch unfold's row order = the flattened OIHW weight's columns), for
+ *   kernel 3: 3x3, stride 1, padding 1 (Mask2FormerPixelDecoder's FPN output convolution; its dX
+ *             is the same convolution of dY with the flipped, transposed weight);
+ *   kernel 4: 4x4, stride 4, padding 0, H and W multiples of 4 (SwinPatchEmbeddings.projection,
+ *             modeling_swin.py; custom_model.py:330).
+ * x NCHW [B][C][H][W]; col [B][C*k*k][Ho*Wo] in x's dtype (RGBD_F32 / RGBD_BF16). */
+int rgbd_im2col(int dtype, const void* x, int B, int C, int H, int W, int kernel, void* col, void* stream);
 
 /* f2 GroupNorm (nn.GroupNorm of the pixel decoder: the input projections, the FPN adapter and the
  * FPN output layer — transformers 5.15 modeling_mask2former.py Mask2FormerPixelDecoder.__init__,

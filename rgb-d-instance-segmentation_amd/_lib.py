@@ -98,6 +98,7 @@ SIGNATURES = {
     "rgbd_gemm_workspace_size": (_SZ, [_I, _I, _I, _I]),
     "rgbd_gemm": (_I, [_I, _I, _I, _I, _I, _I, _P, _LL, _LL, _P, _LL, _LL, _P, _I, _P, _LL, _LL, _P, _LL, _LL, _I,
                        _I, _I, _P, _P]),
+    "rgbd_im2col": (_I, [_I, _P, _I, _I, _I, _I, _I, _P, _P]),
     "rgbd_colsum_workspace_size": (_SZ, [_I, _I]),
     "rgbd_colsum": (_I, [_I, _P, _I, _I, _LL, _P, _P, _P]),
     "rgbd_layernorm_fwd": (_I, [_I, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P]),

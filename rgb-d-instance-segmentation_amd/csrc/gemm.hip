@@ -168,7 +168,7 @@ struct GArgs {
   const void* B;
   long long ldb, sb;
   const float* bias;
-  int act;
+  int act, bias_m;
   const void* R;
   long long ldr, sr;
   void* C;
@@ -191,11 +191,12 @@ __device__ __forceinline__ float g_r(const GArgs& a, long long ridx) {
   return a.c_f32 ? reinterpret_cast<const float*>(a.R)[ridx] : Num<T>::to_f(reinterpret_cast<const T*>(a.R)[ridx]);
 }
 
-// epilogue of one value: act(v + bias) (+ R) | v * (R > 0)
+// epilogue of one value: act(v + bias) (+ R) | v * (R > 0); bias indexed by n (nn.Linear) or,
+// with bias_m, by m (a 1x1 / im2col convolution's output channel in NCHW)
 template <typename T>
-__device__ __forceinline__ float g_epi(float v, int n, long long ridx, const GArgs& a) {
+__device__ __forceinline__ float g_epi(float v, int m, int n, long long ridx, const GArgs& a) {
   if (a.act == RGBD_ACT_RELU_GRAD) return g_r<T>(a, ridx) > 0.f ? v : 0.f;
-  if (a.bias) v += a.bias[n];
+  if (a.bias) v += a.bias[a.bias_m ? m : n];
   v = g_act(v, a.act);
   if (a.R) v += g_r<T>(a, ridx);
   return v;
@@ -249,7 +250,7 @@ __device__ __forceinline__ void g_store8(const GArgs& a, int b, int bz, int m, i
   const long long rbase = (long long)b * a.sr + (long long)m * a.ldr + n0;
 #pragma unroll
   for (int e = 0; e < 8; ++e)
-    if (n0 + e < a.N) v[e] = g_epi<T>(v[e], n0 + e, rbase + e, a);
+    if (n0 + e < a.N) v[e] = g_epi<T>(v[e], m, n0 + e, rbase + e, a);
   if (a.c_f32) {
     float* c = reinterpret_cast<float*>(a.C) + (long long)b * a.sc + (long long)m * a.ldc + n0;
     if (vec_c && n0 + 8 <= a.N) {
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(GArgs a, int batch) 
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      if (n0 + e < a.N) v[e] = g_epi<T>(v[e], n0 + e, (long long)b * a.sr + (long long)m * a.ldr + n0 + e, a);
+      if (n0 + e < a.N) v[e] = g_epi<T>(v[e], m, n0 + e, (long long)b * a.sr + (long long)m * a.ldr + n0 + e, a);
     g_store<T>(a, b, m, n0, v);
   }
 }
@@ -520,6 +521,8 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
               void* stream) {
   RGBD_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && splits > 0, RGBD_E_ARG);
   RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_ARG);
+  const int bias_m = (act & RGBD_BIAS_M) != 0;
+  act &= ~RGBD_BIAS_M;
   RGBD_REQUIRE(act >= RGBD_ACT_NONE && act <= RGBD_ACT_RELU_GRAD, RGBD_E_ARG);
   RGBD_REQUIRE(act != RGBD_ACT_RELU_GRAD || (R && !bias), RGBD_E_ARG);
   RGBD_REQUIRE(splits == 1 || ws, RGBD_E_ARG);
@@ -530,7 +533,7 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
   a.M = M; a.N = N; a.K = K;
   a.A = A; a.lda = lda; a.sa = sa;
   a.B = B; a.ldb = ldb; a.sb = sb;
-  a.bias = bias; a.act = act;
+  a.bias = bias; a.act = act; a.bias_m = bias_m;
   a.R = R; a.ldr = ldr; a.sr = sr;
   a.C = C; a.ldc = ldc; a.sc = sc; a.c_f32 = c_f32 || dtype == RGBD_F32;
   a.splits = splits;

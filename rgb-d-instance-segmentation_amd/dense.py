@@ -20,7 +20,7 @@ LayerNorm returns float32, as autocast's layer_norm does.  Weight gradients are 
 float32 straight from the bf16 GEMM (autocast's path rounds them to bf16 first).
 
 ``install(model)`` swaps module classes in place (parameters and state_dict keys unchanged):
-nn.Linear -> HipLinear, nn.LayerNorm -> HipLayerNorm, the decoder and pixel-decoder encoder
+nn.Conv2d -> conv.HipConv2d (1x1, 3x3 and Swin's 4x4 patch embedding as GEMMs), nn.Linear -> HipLinear, nn.LayerNorm -> HipLayerNorm, the decoder and pixel-decoder encoder
 layers -> classes whose forward fuses the ReLU into fc1's epilogue and its gradient into
 fc2's dX epilogue.  Inputs the kernels do not cover (CPU tensors, float16, LayerNorm width
 > 1536, dropout in training, GELU with gradients) take the module's own torch path.
@@ -46,14 +46,38 @@ def compute_dtype(x: torch.Tensor):
     return x.dtype if x.dtype in _CODE else None
 
 
+_STEP_HOOK = []
+
+
+def _note_optimizer_step(opt, args, kwargs):
+    """Global optimizer post-step hook: every parameter the step updated (the ones holding a
+    gradient: AdamW skips the rest) advances its own step epoch."""
+    for g in opt.param_groups:
+        for p in g["params"]:
+            if p.grad is not None:
+                p._rgbd_epoch = getattr(p, "_rgbd_epoch", 0) + 1
+
+
 def cast_weight(w: torch.Tensor, dt):
-    """w (a parameter) in dtype dt for this call.  Not cached across calls: the fused AdamW step
-    updates parameters in place WITHOUT bumping their version counters (measured, torch 2.10),
-    so a copy keyed on (version, data_ptr) would silently go stale after the first step — the
-    bf16 training loss then falls visibly slower (tools/diag_bf16_model.py train)."""
+    """w (a parameter) in dtype dt, cached on the parameter.  The key is (storage address,
+    version counter, optimizer-step epoch): torch's fused AdamW updates parameters in place
+    WITHOUT bumping their version counters (measured, torch 2.10; a version-keyed cache went
+    stale after the first step and the bf16 loss fell visibly slower, tools/diag_bf16_model.py),
+    so every optimizer step advances the epoch of the parameters it updated (a global
+    post-step hook).  Parameters no optimizer steps — the frozen Swin-T (the reference detaches
+    its features, custom_model.py:332-333, Q1) — are cast once."""
     if w.dtype == dt:
         return w.detach()
-    return w.detach().to(dt)
+    if not _STEP_HOOK:
+        from torch.optim.optimizer import register_optimizer_step_post_hook
+        _STEP_HOOK.append(register_optimizer_step_post_hook(_note_optimizer_step))
+    key = (w.data_ptr(), w._version, getattr(w, "_rgbd_epoch", 0), dt)
+    hit = getattr(w, "_rgbd_cast", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    c = w.detach().to(dt)
+    w._rgbd_cast = (key, c)
+    return c
 
 
 def _splits(M, N, K):
@@ -410,9 +434,11 @@ def _classes():
 def install(model: nn.Module) -> int:
     """Swap nn.Linear / nn.LayerNorm and the decoder / pixel-decoder encoder layers inside
     ``model`` for the HIP classes; returns the number of modules swapped."""
+    from .conv import HipConv2d
     cls = _classes()
     n = 0
     for m in model.modules():
+        n += _install_class(m, nn.Conv2d, HipConv2d)
         n += _install_class(m, nn.Linear, HipLinear)
         n += _install_class(m, nn.LayerNorm, HipLayerNorm)
         n += _install_class(m, nn.GroupNorm, HipGroupNorm)
@@ -429,8 +455,9 @@ def install(model: nn.Module) -> int:
 
 
 def uninstall(model: nn.Module) -> int:
+    from .conv import HipConv2d
     cls = _classes()
-    back = {HipLinear: nn.Linear, HipLayerNorm: nn.LayerNorm, HipGroupNorm: nn.GroupNorm, _FusedReLU: nn.ReLU,
+    back = {HipConv2d: nn.Conv2d, HipLinear: nn.Linear, HipLayerNorm: nn.LayerNorm, HipGroupNorm: nn.GroupNorm, _FusedReLU: nn.ReLU,
             cls["decoder"][1]: cls["decoder"][0], cls["encoder"][1]: cls["encoder"][0]}
     n = 0
     for m in model.modules():

@@ -30,12 +30,18 @@ from .dense import _CODE, ACT_GELU, LayerNormFunction, cast_weight, compute_dtyp
 from .ops import _p, _stream
 
 def _qkv_weights(attn, dt):
-    """[Wq; Wk; Wv] in dt and [bq; bk; bv] float32, built per call (parameters can change in place
-    without a version bump: see dense.cast_weight)."""
+    """[Wq; Wk; Wv] in dt and [bq; bk; bv] float32, cached on the attention module under the
+    same key as dense.cast_weight (address, version, optimizer-step epoch of all six tensors):
+    the backbone is frozen in v0.4.0 (Q1), so this is built once."""
     ps = (attn.q_proj.weight, attn.k_proj.weight, attn.v_proj.weight)
     bs = (attn.q_proj.bias, attn.k_proj.bias, attn.v_proj.bias)
+    key = tuple((t.data_ptr(), t._version, getattr(t, "_rgbd_epoch", 0)) for t in ps + bs if t is not None) + (dt,)
+    hit = getattr(attn, "_rgbd_qkv", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
     w = torch.cat([cast_weight(p, dt) for p in ps], 0).contiguous()
     b = None if bs[0] is None else torch.cat([x.detach().float() for x in bs], 0).contiguous()
+    attn._rgbd_qkv = (key, (w, b))
     return w, b
 
 

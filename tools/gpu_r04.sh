@@ -23,7 +23,7 @@ case "$stage" in
     rc=$?; cat "$O/bench.json"; [ $rc -eq 0 ] || tail -20 "$O/bench.err"; exit $rc ;;
   prof)
     cd /tmp && export TMPDIR=/tmp
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --cpu-baseline 0 --inference 0 --c5-stream 0 --parity 0 "$@" > "$O/prof.log" 2>&1
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --cpu-baseline 0 --inference 0 --c5-stream 0 --parity 0 --full-model 0 "$@" > "$O/prof.log" 2>&1
     rc=$?; tail -3 "$O/prof.log"; exit $rc ;;
   fullprof)  # the whole drop-in model's training step (tools/bench_full_model.py) under the kernel trace
     cd /tmp && export TMPDIR=/tmp
