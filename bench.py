@@ -104,6 +104,8 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=1,
                     help="N=1: time the step replayed from a HIP graph (rgbd_amd/train_graph.py); the eager "
                          "rate and the per-kernel HIP-event timings come from an eager pass beside it")
+    ap.add_argument("--pipeline-report", type=int, default=1,
+                    help="N=1: also time the captured step software-pipelined across batches (pipelined_img_s)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -192,14 +194,22 @@ def build(args, dev, rank=0):
                 gouts=gouts, scenes=scenes, sizes=sizes)
 
 
-def make_parts(ctx, world, capturable=False, overlap_opt=False):
+def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False):
     """(forward_backward, optimizer_step, reducer, broadcaster) of one training step.
     forward_backward() leaves the (all-reduced, for N > 1) gradients in p.grad;
     optimizer_step.opt is the AdamW instance (``capturable`` for graph capture).
     ``overlap_opt``: the AdamW steps run inside the backward instead, one per parameter group as
     its gradients are enqueued (distributed.InBackwardOptimizer; bitwise the same update);
     forward_backward() then trains and optimizer_step() only clears the gradients
-    (optimizer_step.opt None, optimizer_step.opts the per-group optimizers)."""
+    (optimizer_step.opt None, optimizer_step.opts the per-group optimizers).
+    ``pipeline``: software-pipelined across batches — the ratio predictor (K1 assembly + K4) of
+    the NEXT batch runs on a second stream beside this batch's decomposition / DSAM / DGGM
+    forward, backward and AdamW, and this batch uses the ratio the previous step computed.  The
+    predictor is forward-only and never trained (its output leaves autograd through .item(),
+    custom_model.py:339-351, Q2) and nothing of batch k's backward feeds batch k+1's predictor,
+    so every parameter, BatchNorm buffer and dropout draw is bitwise that of the sequential
+    schedule (tests/test_gpu_train_graph.py).  The hot path then keeps all its own launches on the
+    main stream (two concurrent branches when captured)."""
     from rgbd_amd import ops
     from rgbd_amd.distributed import (BufferBroadcaster, InBackwardOptimizer, OverlappedGradReducer,
                                       hot_path_grad_groups)
@@ -219,7 +229,33 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False):
     else:
         opt = HipAdamW(params, **HF_TRAINER_ADAMW)  # AdamW on HIP (rgbd_adamw_multi); always capturable
 
+    if pipeline:
+        from rgbd_amd.hot_path import side_stream
+        dev = ctx["depth_u8"].device
+        side = side_stream(dev)
+        # static buffers (outside any captured graph): the next batch's ratio, and this batch's copy
+        ratio_next = torch.empty((ctx["depth_u8"].shape[0], 1), dtype=torch.float32, device=dev)
+        ratio_cur = torch.empty_like(ratio_next)
+
+        def next_ratio():  # the next batch's K1 + K4 (the bench's synthetic stream repeats its batch)
+            pvn = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
+            ratio_next.copy_(ctx["rp"](pvn[:, 3:6]))
+        next_ratio()  # prime the pipeline with the first batch's ratio
+
     def forward_backward():
+        if pipeline:
+            main = torch.cuda.current_stream(dev)
+            ratio_cur.copy_(ratio_next)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                next_ratio()
+            pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
+            prep = prepare(pv, ctx["colors"], ctx["dtype"], overlap=False)
+            feats = hot_path(pv, ratio_cur, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"],
+                             grad_hook=hook, prepared=prep, overlap=False)
+            torch.autograd.backward(feats, ctx["gouts"])
+            main.wait_stream(side)
+            return feats
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
         if bcast is not None:  # DDP broadcast_buffers: every forward starts from rank 0's BN stats
             bcast.sync()
@@ -244,7 +280,7 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False):
     return forward_backward, optimizer_step, reducer, bcast
 
 
-def make_step(ctx, world, inference=False, graph=False):
+def make_step(ctx, world, inference=False, graph=False, pipeline=False):
     from rgbd_amd import ops
     from rgbd_amd.hot_path import hot_path, prepare
     if inference:
@@ -257,7 +293,7 @@ def make_step(ctx, world, inference=False, graph=False):
         return istep
     if graph:  # single process: the whole step replayed from a HIP graph, captured on first use
         from rgbd_amd.train_graph import CapturedTrainStep
-        fb, ostep, _, _ = make_parts(ctx, world, capturable=True, overlap_opt=True)
+        fb, ostep, _, _ = make_parts(ctx, world, capturable=True, overlap_opt=True, pipeline=pipeline)
         held = {}
 
         def gstep():
@@ -631,6 +667,9 @@ def main():
     L.rgbd_timing_enable(0)
     use_graph = bool(args.graph) and world == 1
     dt = timed(make_step(ctx, world, graph=True), args.steps, args.warmup, world) if use_graph else dt_eager
+    # the same captured step software-pipelined across batches (make_parts ``pipeline``)
+    dt_pipe = timed(make_step(ctx, world, graph=True, pipeline=True), args.steps, args.warmup, world) \
+        if use_graph and args.pipeline_report else None
     # N > 1 runs eagerly (the overlapped RCCL reducer is not captured): the same eager step with
     # no collective on every rank at once gives the line's own scaling reference
     dt_local = timed(make_step(ctx, 1), args.steps, args.warmup, world) if world > 1 else None
@@ -676,6 +715,10 @@ def main():
                       "model's gradients (37.3 M parameters, most of them outside this path)"),
         "graph": use_graph,
         "eager_img_s": round(B * world * args.steps / dt_eager, 2),
+        "pipelined_img_s": None if dt_pipe is None else round(B * world * args.steps / dt_pipe, 2),
+        "pipelined_note": ("the captured step with the next batch's ratio predictor on a second stream beside this "
+                           "batch's DSAM / DGGM forward, backward and AdamW (bitwise the sequential schedule's "
+                           "parameters: the predictor is forward-only and frozen, Q2)"),
         "scaling_baseline_img_s": (None if dt_local is None else round(B * world * args.steps / dt_local, 2)),
         "scaling_baseline_note": ("N > 1: the step is eager (collectives not captured); scaling_baseline_img_s = "
                                   "the same eager step with no all-reduce / broadcast on every rank at once, so "

@@ -160,13 +160,14 @@ def _sources(pixel_values, colors):
     return tuple((t.data_ptr(), tuple(t.shape)) for t in (pixel_values, *colors))
 
 
-def prepare(pixel_values, colors, dtype=torch.float32):
+def prepare(pixel_values, colors, dtype=torch.float32, overlap=True):
     """Launch the ratio-independent part of the hot path (call it before the ratio predictor,
-    pass the result to ``hot_path(..., prepared=)``).  bf16 on the GPU: on the side stream."""
+    pass the result to ``hot_path(..., prepared=)``).  bf16 on the GPU: on the side stream
+    (``overlap`` False: on the current stream)."""
     pv = pixel_values.detach().float().contiguous()
     cols = [c.detach().to(dtype).contiguous() for c in colors]
     bf16 = dtype == torch.bfloat16
-    side = _Side(pv.device, bf16 and pv.is_cuda)
+    side = _Side(pv.device, bf16 and pv.is_cuda and overlap)
     held = {}
 
     def work():
@@ -346,7 +347,7 @@ class HotPathFunction(torch.autograd.Function):
 
 
 def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch.float32, check_status=False,
-             grad_hook=None, status_sink=None, prepared=None):
+             grad_hook=None, status_sink=None, prepared=None, overlap=True):
     """Run the fused hot path.  ``dsam_modules``: the three DSAModule instances;
     ``dggm_module``: the DepthGradientInjectionResidual instance.  ``check_status`` raises the
     reference's ValueError for a degenerate depth histogram right away (synchronising);
@@ -356,7 +357,10 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
     order of ``distributed.hot_path_grad_groups`` (dsam2, dsam1, dsam0 + DGGM) — the data-parallel
     reducer uses it to overlap the gradient all-reduce with the rest of the backward.
     ``prepared``: ``prepare(pixel_values, colors, dtype)``, launched before the ratio predictor
-    (the same pixel_values / colours), so the ratio-free work overlaps it; None = inline."""
+    (the same pixel_values / colours), so the ratio-free work overlaps it; None = inline.
+    ``overlap`` False keeps every launch on the current stream (no side stream of the hot path's
+    own: a caller that runs other work beside it on a stream of its own, e.g. the next batch's
+    ratio predictor, stays within two concurrent branches when captured)."""
     params = []
     for m in dsam_modules:
         for i in range(4):
@@ -366,7 +370,7 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
         conv = dggm_module.depth_enhancement_layers[i][0]
         params += [conv.weight, conv.bias]
     cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook, "status_sink": status_sink,
-           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": True, "prepared": prepared}
+           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": overlap, "prepared": prepared}
     if prepared is not None:
         prepared.check(pixel_values, colors)
     pv = prepared.pixel_values if prepared is not None else pixel_values.detach().float().contiguous()

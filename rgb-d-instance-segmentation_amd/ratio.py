@@ -41,7 +41,7 @@ def _packed(module, dtype):
     # them; load_state_dict copies bump the versions.  (A fused optimizer step would NOT: see
     # dense.cast_weight — a trained predictor would need a re-pack per step.)
     ws = _weights(module)
-    key = (dtype,) + tuple((w.data_ptr(), w._version) for w in ws)
+    key = (dtype,) + tuple((w.data_ptr(), w._version, getattr(w, "_rgbd_epoch", 0)) for w in ws)
     cache = getattr(module, "_rgbd_pack", None)
     if cache is not None and cache[0] == key:
         return cache[1]

@@ -84,3 +84,30 @@ def test_captured_step_needs_capturable_optimizer():
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
     with pytest.raises(ValueError, match="capturable"):
         CapturedTrainStep(fb, torch.optim.AdamW(params, lr=1e-5, fused=True))
+
+
+def test_pipelined_captured_step_equals_sequential_steps():
+    """bench.py's pipelined step (make_parts pipeline=True): the next batch's ratio predictor on
+    a second stream beside this batch's hot path, captured; after 4 training steps every trained
+    parameter is bitwise that of 4 sequential eager steps, and — the pipeline having run one
+    ratio forward ahead — the BatchNorm buffers and dropout counter equal the sequential arm's
+    after one more forward."""
+    import bench
+    from rgbd_amd.train_graph import CapturedTrainStep
+    args = bench.parse(["--height", "96", "--width", "128", "--batch", "3"])
+    a, b = _ctx(bench, args), _ctx(bench, args)
+    fa, oa, _, _ = bench.make_parts(a, 1, capturable=True)
+    for _ in range(4):
+        fa()
+        oa()
+    from rgbd_amd import ops
+    a["rp"](ops.assemble_pixel_values(a["depth_u8"], a["rgb_u8"])[:, 3:6])  # the pipeline's read-ahead
+    fb, ob, _, _ = bench.make_parts(b, 1, capturable=True, overlap_opt=True, pipeline=True)
+    step = CapturedTrainStep(fb, None, warmup=2, opts=ob.opts, clear=ob)
+    assert step.width <= 2
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    assert int(a["rp"]._rgbd_dropout_ctr.item()) == 5 == int(b["rp"]._rgbd_dropout_ctr.item())
+    for i, (x, y) in enumerate(zip(_state(a), _state(b))):
+        assert torch.equal(x, y), f"state tensor {i} differs after 4 steps"
