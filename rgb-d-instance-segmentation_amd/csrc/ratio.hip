@@ -1322,14 +1322,56 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       // resident for the whole channel half) are read under this sub-step's MFMAs; the step's
       // DMA (B(st+1), one A piece) is issued after the first channel blocks' MFMAs instead of in
       // front of every MFMA.  After the barrier only the step's ks-0 B reads are exposed.
+      // SCHED 2: the same, with waves 4-7 (each SIMD's second wave) staggered by half a step: their
+      // ks-1 MFMAs of step st run after the barrier that ends st (every operand they need is
+      // already in registers, so nothing they read can be overwritten by the next DMA), and they
+      // issue step st+1's DMA at the start of that segment.  Each SIMD then has one wave on
+      // register-fed MFMAs while its partner waits for the fresh ks-0 fragment reads.
+      const bool late = SCHED == 2 && wave >= 4;
       Frag<bf16_t> fa[4], fa1[4], fb[8];
       auto a_off = [&](int stp, int ks, int mi) {
         const int hh = stp >= 9, tp = stp - 9 * hh, yy = tp / 3, xx = tp % 3;
         const int p = (2 * wm + (mi >> 1) + yy) * C3_PW + (mi & 1) * 16 + r + xx;
         return hh * (C3_APIX * 128) + (int)c3_off(p, 4 * ks + g);
       };
+      auto dma = [&](int st) {  // B(st+1) or the next tile's B(0), and this step's A piece
+        if (st + 1 < C3_STEPS)
+          issue_b(st + 1);
+        else if (has_next)
+          issue_b(0);
+        if (st < 6) {
+          const int j = wave + 8 * st;
+          if (j < C3_APIECES) {
+            issue_a(t, 1, j);
+            return 1;
+          }
+        } else if (st >= 9 && st < 15 && has_next) {
+          const int j = wave + 8 * (st - 9);
+          if (j < C3_APIECES) {
+            issue_a(tn, 0, j);
+            return 1;
+          }
+        }
+        return 0;
+      };
+      // ks 1 of step st from registers; reads the ks-0 A fragments of step nst under it
+      auto m1 = [&](int nst, bool prefetch) {
+#pragma unroll
+        for (int nj = 0; nj < 8; ++nj) {
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], fa1[mi], fb[nj]);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+          if (prefetch && nj >= 2 && nj < 6) {
+            fa[nj - 2].v = *reinterpret_cast<const uint4*>(smem + a_off(nst, 0, nj - 2));
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+        }
+      };
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) fa[mi].v = *reinterpret_cast<const uint4*>(smem + a_off(0, 0, mi));
+      // one instruction stream for both halves; only the barrier's place differs: early waves
+      // [ks-0 reads, ks 0, ks 1 | barrier], late waves [ks-0 reads, ks 0 | barrier | ks 1]
+      int a_pending = 0;  // late waves: an A piece issued in the previous segment
 #pragma unroll 1
       for (int st = 0; st < C3_STEPS; ++st) {
         const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
@@ -1339,8 +1381,8 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) fa1[mi].v = *reinterpret_cast<const uint4*>(smem + a_off(st, 1, mi));
         __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // all of them before the first MFMA
-        int a_issued = 0;
-        // ---- ks 0
+        const bool dma_here = !late || st == 0;
+        // ---- ks 0, the ks-1 B fragments read as their registers free up
 #pragma unroll
         for (int nj = 0; nj < 8; ++nj) {
 #pragma unroll
@@ -1348,44 +1390,24 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
           fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, 4 + g));
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if (nj == 1) {
-            if (st + 1 < C3_STEPS)
-              issue_b(st + 1);
-            else if (has_next)
-              issue_b(0);
-          } else if (nj == 3) {
-            if (st < 6) {
-              const int j = wave + 8 * st;
-              if (j < C3_APIECES) {
-                issue_a(t, 1, j);
-                a_issued = 1;
-              }
-            } else if (st >= 9 && st < 15 && has_next) {
-              const int j = wave + 8 * (st - 9);
-              if (j < C3_APIECES) {
-                issue_a(tn, 0, j);
-                a_issued = 1;
-              }
-            }
-          }
+          if (nj == 1 && dma_here) a_pending = dma(st);
+        }
+        if (late) {
+          if (a_pending == 1)
+            asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          a_pending = st + 1 < C3_STEPS ? dma(st + 1) : 0;  // the next step's DMA under this ks 1
         }
         // ---- ks 1; the next step's ks-0 A fragments are read under it (the tile's first step
         // reads its own after the tile's prologue barrier)
-        const int nst = st + 1 < C3_STEPS ? st + 1 : st;
-#pragma unroll
-        for (int nj = 0; nj < 8; ++nj) {
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], fa1[mi], fb[nj]);
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-          if (nj >= 2 && nj < 6) {
-            fa[nj - 2].v = *reinterpret_cast<const uint4*>(smem + a_off(nst, 0, nj - 2));
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
+        m1(st + 1 < C3_STEPS ? st + 1 : st, st + 1 < C3_STEPS);
+        if (!late) {
+          if (a_pending == 1)
+            asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        if (a_issued == 1)
-          asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
     }
     // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
@@ -1977,13 +1999,18 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
           (const void*)k_rp_conv3x3_v3<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       static const hipError_t attr1 = hipFuncSetAttribute(
           (const void*)k_rp_conv3x3_v3<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
+      static const hipError_t attr2 = hipFuncSetAttribute(
+          (const void*)k_rp_conv3x3_v3<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       if (attr0 != hipSuccess) return (int)attr0;
       if (attr1 != hipSuccess) return (int)attr1;
+      if (attr2 != hipSuccess) return (int)attr2;
       gcv = conv3_grid(B, H, W);
       if (sched == 0)
         k_rp_conv3x3_v3<0><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
-      else
+      else if (sched == 1)
         k_rp_conv3x3_v3<1><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+      else
+        k_rp_conv3x3_v3<2><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
     } else {
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);

@@ -9,11 +9,12 @@ Reference: mask2former/predictor.py — ``convert_model_a_to_json_format`` (:335
      "counts": <pycocotools compressed RLE string>}]}
 
 The reference builds every instance's binary mask on the host (``segmentation == id``), its
-bounding box, and ``pycocotools.mask.encode`` of it.  Here the per-instance run boundaries and
-boxes come from one pass over the map on whatever device holds it (the device post-processing
-leaves the maps on the GPU with ``keep_on_device``): the map is read column-major once per
-instance as a boolean vector, run boundaries are the positions where it changes; the compressed
-string (maskApi.c ``rleToString``) is formed on the host from the counts.  pycocotools is not
+bounding box, and ``pycocotools.mask.encode`` of it.  Here the run boundaries and boxes of all
+of an image's instances come from one pass on whatever device holds the map (the device
+post-processing leaves the maps on the GPU with ``keep_on_device``): the stacked masks are read
+column-major, run boundaries are the positions where a mask changes (one nonzero over all of
+them), and one copy brings boundaries and boxes to the host, where the compressed string
+(maskApi.c ``rleToString``) is formed from the counts.  pycocotools is not
 installed here: the encoding is pinned against a step-for-step restatement of maskApi.c
 (oracle/rle.py) and its decode round trip (tests/test_export.py).
 """
@@ -44,33 +45,44 @@ def _to_string(counts) -> str:
     return "".join(out)
 
 
-def _runs(colmajor: torch.Tensor):
-    """Counts of a column-major boolean vector: zeros first (0 when it starts set)."""
-    n = colmajor.numel()
-    change = torch.nonzero(colmajor[1:] != colmajor[:-1]).reshape(-1) + 1
-    bounds = torch.cat([change.new_zeros(1), change, change.new_full((1,), n)]).cpu().numpy()
-    counts = np.diff(bounds).tolist()
-    if bool(colmajor[0]):
-        counts = [0] + counts
-    return counts
-
-
 def encode_masks(masks: torch.Tensor):
     """masks bool/0-1 [N, h, w] (any device) -> list of (rle dict, bbox [x, y, w, h] or None), the
-    pycocotools.mask.encode + _calculate_bbox_from_mask pair of the reference per mask."""
+    pycocotools.mask.encode + _calculate_bbox_from_mask pair of the reference per mask.
+
+    All N masks at once on their device: the column-major change positions of every mask come
+    from one nonzero over the [N, h*w - 1] change map, the boxes from the row / column
+    occupancy, and the whole result reaches the host in one copy (no per-mask sync)."""
     N, h, w = masks.shape
+    if N == 0:
+        return []
+    L = h * w
+    mb = masks.bool()
+    cm = mb.transpose(1, 2).reshape(N, L)                      # column-major per mask
+    pos = torch.nonzero(cm[:, 1:] != cm[:, :-1])              # [M, 2]: (mask, change index - 1)
+    rows, cols = mb.any(dim=2), mb.any(dim=1)                 # [N, h], [N, w]
+    ar_h = torch.arange(h, device=mb.device)
+    ar_w = torch.arange(w, device=mb.device)
+    big = max(h, w) + 1
+    y0 = torch.where(rows, ar_h, big).amin(1)
+    y1 = torch.where(rows, ar_h, -1).amax(1)
+    x0 = torch.where(cols, ar_w, big).amin(1)
+    x1 = torch.where(cols, ar_w, -1).amax(1)
+    meta = torch.stack([cm[:, 0].long(), y0, y1, x0, x1], 1)  # [N, 5]
+    flat = torch.cat([meta.reshape(-1), pos.reshape(-1).long()]).cpu().numpy()
+    meta_h = flat[:5 * N].reshape(N, 5)
+    pos_h = flat[5 * N:].reshape(-1, 2)
+    starts = np.searchsorted(pos_h[:, 0], np.arange(N + 1), side="left")
     out = []
-    cm = masks.bool().transpose(1, 2).reshape(N, -1)  # column-major per mask
-    rows = masks.bool().any(dim=2)
-    cols = masks.bool().any(dim=1)
     for i in range(N):
-        counts = _runs(cm[i])
-        r = torch.nonzero(rows[i]).reshape(-1)
-        c = torch.nonzero(cols[i]).reshape(-1)
+        change = pos_h[starts[i]:starts[i + 1], 1] + 1
+        bounds = np.concatenate([[0], change, [L]])
+        counts = np.diff(bounds).tolist()
+        if meta_h[i, 0]:
+            counts = [0] + counts
         bbox = None
-        if r.numel():
-            y0, y1, x0, x1 = int(r[0]), int(r[-1]), int(c[0]), int(c[-1])
-            bbox = [float(x0), float(y0), float(x1 - x0 + 1), float(y1 - y0 + 1)]
+        if meta_h[i, 2] >= 0:
+            yy0, yy1, xx0, xx1 = (int(v) for v in meta_h[i, 1:])
+            bbox = [float(xx0), float(yy0), float(xx1 - xx0 + 1), float(yy1 - yy0 + 1)]
         out.append(({"size": [int(h), int(w)], "counts": _to_string(counts)}, bbox))
     return out
 
