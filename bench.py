@@ -250,7 +250,7 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False):
             with torch.cuda.stream(side):
                 next_ratio()
             pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
-            prep = prepare(pv, ctx["colors"], ctx["dtype"], overlap=False)
+            prep = prepare(pv, ctx["colors"], ctx["dtype"], overlap=False, dsam_modules=ctx["dsams"])
             feats = hot_path(pv, ratio_cur, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"],
                              grad_hook=hook, prepared=prep, overlap=False)
             torch.autograd.backward(feats, ctx["gouts"])
@@ -259,7 +259,7 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False):
         pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
         if bcast is not None:  # DDP broadcast_buffers: every forward starts from rank 0's BN stats
             bcast.sync()
-        prep = prepare(pv, ctx["colors"], ctx["dtype"])  # ratio-free decomposition beside the ratio predictor
+        prep = prepare(pv, ctx["colors"], ctx["dtype"], dsam_modules=ctx["dsams"])  # beside the ratio predictor
         ratio = ctx["rp"](pv[:, 3:6])
         feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], grad_hook=hook,
                          prepared=prep)
@@ -287,7 +287,7 @@ def make_step(ctx, world, inference=False, graph=False, pipeline=False):
         def istep():
             pv = ops.assemble_pixel_values(ctx["depth_u8"], ctx["rgb_u8"])
             with torch.no_grad():
-                prep = prepare(pv, ctx["colors"], ctx["dtype"])
+                prep = prepare(pv, ctx["colors"], ctx["dtype"], dsam_modules=ctx["dsams"])
                 ratio = ctx["rp"](pv[:, 3:6])
                 return hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], prepared=prep)
         return istep

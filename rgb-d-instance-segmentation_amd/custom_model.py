@@ -74,7 +74,8 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
         """custom_model.py:325-355 on the HIP kernels: returns the 4 backbone features.
         ``status_sink``: see hot_path.hot_path (None = raise the reference's ValueError at once)."""
         # the ratio-free part (decomposition modes, bf16 colour layouts) beside the ratio predictor
-        prep = prepare(pixel_values, list(color_feature_map), self.compute_dtype)
+        prep = prepare(pixel_values, list(color_feature_map), self.compute_dtype,
+                       dsam_modules=[self.dsam0, self.dsam1, self.dsam2])
         if ratios is None:
             ratios = self.ratio_predictor(pixel_values[:, 3:6])       # :336 (no grad, Q2)
         feats = hot_path(pixel_values, ratios, list(color_feature_map), [self.dsam0, self.dsam1, self.dsam2],

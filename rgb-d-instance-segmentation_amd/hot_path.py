@@ -138,9 +138,10 @@ class Prepared:
     decomposition (grey plane, histogram, modes: ops.edsam_modes) and, in bf16, the NHWC copies
     of the colour maps — launched on the side stream so they run beside the ratio predictor."""
 
-    def __init__(self, side, pixel_values, modes, colors, nhwc, dtype, sources):
+    def __init__(self, side, pixel_values, modes, colors, nhwc, dtype, sources, packs=None):
         self.side, self.pixel_values, self.modes = side, pixel_values, modes
         self.colors, self.nhwc, self.dtype = colors, nhwc, dtype
+        self.packs = packs or {}  # DSAM index -> bf16 packed filters for all 16 codes
         self.sources = sources  # (data_ptr, shape) of the pixel_values and colour maps it was built from
 
     def check(self, pixel_values, colors):
@@ -160,10 +161,24 @@ def _sources(pixel_values, colors):
     return tuple((t.data_ptr(), tuple(t.shape)) for t in (pixel_values, *colors))
 
 
-def prepare(pixel_values, colors, dtype=torch.float32, overlap=True):
+# DSAMs whose bf16 filters prepare() packs for all 16 region codes beside the ratio predictor
+# (small: 5 MB / 42 MB; off the critical path), instead of for the codes present after the
+# decomposition; dsam2's (16 x 21 MB) stays packed for the present codes only, beside dsam0
+PREPACK = (0, 1)
+
+
+def _pack_all(m, k, dtype):
+    conv_ws = [m.conv_layers[i].weight for i in range(4)]
+    want_bwd = k > 0 and torch.is_grad_enabled() and m.rgb_projection.weight.requires_grad
+    return m._pack_cache.get(conv_ws, m.rgb_projection.weight, dtype, code_mask=None, want_bwd=want_bwd)
+
+
+def prepare(pixel_values, colors, dtype=torch.float32, overlap=True, dsam_modules=None):
     """Launch the ratio-independent part of the hot path (call it before the ratio predictor,
     pass the result to ``hot_path(..., prepared=)``).  bf16 on the GPU: on the side stream
-    (``overlap`` False: on the current stream)."""
+    (``overlap`` False: on the current stream).  With ``dsam_modules`` (bf16) the filters of the
+    PREPACK DSAMs are packed here too, from the parameters as they are now (after the previous
+    optimizer step)."""
     pv = pixel_values.detach().float().contiguous()
     cols = [c.detach().to(dtype).contiguous() for c in colors]
     bf16 = dtype == torch.bfloat16
@@ -173,9 +188,14 @@ def prepare(pixel_values, colors, dtype=torch.float32, overlap=True):
     def work():
         held["modes"] = m = ops.edsam_modes(pv)
         nhwc = ops.nchw_to_nhwc_multi(cols) if bf16 else None
-        return [m.info, m.ws, m.masks, nhwc]
-    _, _, _, nhwc = side.run(work, pv, *cols)
-    return Prepared(side, pv, held["modes"], cols, nhwc, dtype, _sources(pixel_values, colors))
+        packs = {}
+        if bf16 and dsam_modules is not None:
+            for k in PREPACK:
+                packs[k] = _pack_all(dsam_modules[k], k, dtype)
+        held["packs"] = packs
+        return [m.info, m.ws, m.masks, nhwc, [t for pk in packs.values() for t in pk if t is not None]]
+    _, _, _, nhwc, _ = side.run(work, pv, *cols)
+    return Prepared(side, pv, held["modes"], cols, nhwc, dtype, _sources(pixel_values, colors), held["packs"])
 
 
 class HotPathFunction(torch.autograd.Function):
@@ -219,6 +239,9 @@ class HotPathFunction(torch.autograd.Function):
             conv_plans = ops.dsam_plan(legs)
 
         def pack(k):
+            pre = prepared.packs.get(k)
+            if pre is not None and (pre[1] is not None or not (training and k > 0)):
+                return pre  # packed for all codes beside the ratio predictor
             return cfg["pack_cache"][k].get(dsam_p[k][0:8:2], dsam_p[k][8], dtype,
                                             code_mask=None if masks is None else masks[k:k + 1],
                                             want_bwd=training and k > 0)  # dsam0's input takes no gradient
@@ -230,12 +253,18 @@ class HotPathFunction(torch.autograd.Function):
             res_nhwc = nhwc[1:]
             # bf16 cascade entirely in NHWC: each DSAM adds its residual colour map in NHWC and writes
             # cp1[k+1] once, in the layout the next DSAM reads and the DGGM pass accepts
+            dggm_early = None
             for k in range(3):
                 if k == 1:
                     side.join()  # the dsam1 / dsam2 packs
                     if training:  # dW plans beside the rest of the forward
                         dw_plans = side.run(lambda: ops.dsam_plan([(ops.LEG_DW, codes[j], *chans[j]) for j in range(3)]),
                                             *codes)
+                if k == 2:  # DGGM gate + sum of scales 0-2 beside dsam2 (their cp1 are final now)
+                    dggm_early = side.run(lambda: ops.dggm_fuse_fwd_multi(cp1[0:3], colors[0:3], pixel_values,
+                                                                          dggm_p[0:6:2], dggm_p[1:6:2],
+                                                                          cp1_nhwc=(1, 2)),
+                                          *cp1[0:3], *colors[0:3], pixel_values)
                 bias4 = stack4([b.detach() for b in dsam_p[k][1:8:2]])
                 out_nhwc = ops.dsam_fwd_nhwc(x_nhwc[k], codes[k], info, packs[k][0], bias4, residual_nhwc=res_nhwc[k],
                                              plan=conv_plans[k])
@@ -254,9 +283,12 @@ class HotPathFunction(torch.autograd.Function):
                 if k < 2:
                     x_nhwc.append(out_nhwc)
             cp1_nhwc = ()
-        # DGGM gate + final sum of all four scales in one launch
-        outs = ops.dggm_fuse_fwd_multi(cp1, colors, pixel_values, dggm_p[0::2], dggm_p[1::2], cp1_nhwc=cp1_nhwc)
-        side.join()  # the dW plans
+        if bf16:  # scale 3 after dsam2; scales 0-2 ran beside it
+            outs = dggm_early + ops.dggm_fuse_fwd_multi(cp1[3:], colors[3:], pixel_values, dggm_p[6::2], dggm_p[7::2],
+                                                        cp1_nhwc=(0,))
+        else:  # DGGM gate + final sum of all four scales in one launch
+            outs = ops.dggm_fuse_fwd_multi(cp1, colors, pixel_values, dggm_p[0::2], dggm_p[1::2], cp1_nhwc=cp1_nhwc)
+        side.join()  # the dW plans, DGGM scales 0-2
         ctx.cfg = cfg
         ctx.dx_plans = {1: conv_plans[3], 2: conv_plans[4]} if conv_plans and training else {}
         ctx.dw_plans = dw_plans

@@ -41,7 +41,7 @@ class StreamingHotPath:
 
     def _run(self):
         pv = ops.assemble_pixel_values(self.depth_u8, self.rgb_u8)
-        prep = prepare(pv, self.colors, self.dtype)  # decomposition modes beside the ratio predictor
+        prep = prepare(pv, self.colors, self.dtype, dsam_modules=self.dsams)  # beside the ratio predictor
         ratio = self.rp(pv[:, 3:6])
         return hot_path(pv, ratio, self.colors, self.dsams, self.dg, dtype=self.dtype, prepared=prep), ratio
 
