@@ -79,7 +79,7 @@ class ConvFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             col = _col(xc, k)
             dwb = gemm(g, col, 0, 0, O, K, N, c_f32=True, batch=B, sa=O * N, sb=K * N)
-            dw = dwb.sum(0).reshape(ctx.w_shape).to(ctx.w_dtype)
+            dw = dwb.view(B, O, K).sum(0).reshape(ctx.w_shape).to(ctx.w_dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = g.float().sum((0, 2))
         if ctx.needs_input_grad[0]:

@@ -47,9 +47,17 @@ __global__ __launch_bounds__(256) void k_adamw_multi(const AwTable T, const floa
   int t = 0;
   for (int i = 1; i < T.nt; ++i)
     if ((int)blockIdx.x >= T.block0[i]) t = i;
-  const double st = *step;
-  const double bc1 = 1.0 - pow(h.b1d, st), bc2 = 1.0 - pow(h.b2d, st);
-  const float step_size = (float)(h.lr / bc1), bc2_sqrt = (float)sqrt(bc2);
+  // the bias corrections in double once per workgroup (one lane; double pow is hundreds of
+  // instructions), broadcast through LDS
+  __shared__ float s_corr[2];
+  if (threadIdx.x == 0) {
+    const double st = *step;
+    const double bc1 = 1.0 - pow(h.b1d, st), bc2 = 1.0 - pow(h.b2d, st);
+    s_corr[0] = (float)(h.lr / bc1);
+    s_corr[1] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const float step_size = s_corr[0], bc2_sqrt = s_corr[1];
   const long long n = T.n[t];
   const long long e0 = (long long)(blockIdx.x - T.block0[t]) * AW_CHUNK;
   float* __restrict__ P = T.p[t];
