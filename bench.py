@@ -104,7 +104,7 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=1,
                     help="N=1: time the step replayed from a HIP graph (rgbd_amd/train_graph.py); the eager "
                          "rate and the per-kernel HIP-event timings come from an eager pass beside it")
-    ap.add_argument("--pipeline-report", type=int, default=1,
+    ap.add_argument("--pipeline-report", type=int, default=0,
                     help="N=1: also time the captured step software-pipelined across batches (pipelined_img_s)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)

@@ -1172,8 +1172,7 @@ constexpr int C3_STEPS = 18;
 constexpr int C3_A_BYTES = 2 * C3_APIX * 128;
 constexpr int C3_B_OFF = C3_A_BYTES, C3_B_BYTES = 2 * C5 * 128;
 constexpr int C3_BIAS_OFF = C3_B_OFF + C3_B_BYTES;
-constexpr int C3_RED_OFF = C3_BIAS_OFF + C5 * 4;  // [4 wm][256 n][2] f32 statistics (SCHED 1)
-constexpr size_t C3_SMEM = C3_RED_OFF + 4 * C5 * 2 * 4;
+constexpr size_t C3_SMEM = C3_BIAS_OFF + C5 * 4;
 static_assert(C3_SMEM <= 163840, "conv5 v3 LDS budget");
 
 __device__ __forceinline__ uint32_t c3_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 6)); }
@@ -1200,7 +1199,6 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
   return o;
 }
 
-template <int SCHED>
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
                                                        bf16_t* __restrict__ y, float* __restrict__ slab) {
@@ -1214,9 +1212,6 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   const char* zero16 = blob + L.zero;
   float* sbias = (float*)(smem + C3_BIAS_OFF);
   for (int i = tid; i < C5; i += 512) sbias[i] = ((const float*)(blob + L.b5))[i];
-  float* sred = (float*)(smem + C3_RED_OFF);
-  if constexpr (SCHED != 0)
-    for (int i = tid; i < 4 * C5 * 2; i += 512) sred[i] = 0.f;
   const int tiles_x = (W + C3_TW - 1) / C3_TW, tiles_y = (H + C3_TH - 1) / C3_TH;
   const long long ntiles = (long long)B * tiles_x * tiles_y;
 
@@ -1240,9 +1235,9 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 
   // BN statistics per channel as (even, odd) pixel pairs: packed adds / FMAs, one instruction
   // per value for the sum and the sum of squares together
-  f32x2 ssum_k[8], ssq_k[8];
+  f32x2 ssum[8], ssq[8];
 #pragma unroll
-  for (int nj = 0; nj < 8; ++nj) ssum_k[nj] = ssq_k[nj] = f32x2{0.f, 0.f};
+  for (int nj = 0; nj < 8; ++nj) ssum[nj] = ssq[nj] = f32x2{0.f, 0.f};
 
   // static priority for the second-dispatched half of the workgroup (the arbitration loser of
   // every step with two waves per SIMD; MI355X_MICROARCH "two waves per SIMD", item 4)
@@ -1267,7 +1262,6 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 #pragma unroll
       for (int nj = 0; nj < 8; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (SCHED == 0) {
 #pragma unroll 1
     for (int st = 0; st < C3_STEPS; ++st) {
       // this step's DMA: B(st + 1) (or the next tile's B(0)), plus a piece of A (this tile's half 1
@@ -1315,112 +1309,10 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    } else {
-      // SCHED 1: software-pipelined step.  MFMAs channel-block (nj) major, so each B fragment dies
-      // after its 4 MFMAs and its registers take the next K sub-step's fragment right away; the
-      // next sub-step's A fragments (and, at ks 1, the NEXT step's ks-0 A fragments: the halo is
-      // resident for the whole channel half) are read under this sub-step's MFMAs; the step's
-      // DMA (B(st+1), one A piece) is issued after the first channel blocks' MFMAs instead of in
-      // front of every MFMA.  After the barrier only the step's ks-0 B reads are exposed.
-      // SCHED 2: the same, with waves 4-7 (each SIMD's second wave) staggered by half a step: their
-      // ks-1 MFMAs of step st run after the barrier that ends st (every operand they need is
-      // already in registers, so nothing they read can be overwritten by the next DMA), and they
-      // issue step st+1's DMA at the start of that segment.  Each SIMD then has one wave on
-      // register-fed MFMAs while its partner waits for the fresh ks-0 fragment reads.
-      const bool late = SCHED == 2 && wave >= 4;
-      Frag<bf16_t> fa[4], fa1[4], fb[8];
-      auto a_off = [&](int stp, int ks, int mi) {
-        const int hh = stp >= 9, tp = stp - 9 * hh, yy = tp / 3, xx = tp % 3;
-        const int p = (2 * wm + (mi >> 1) + yy) * C3_PW + (mi & 1) * 16 + r + xx;
-        return hh * (C3_APIX * 128) + (int)c3_off(p, 4 * ks + g);
-      };
-      auto dma = [&](int st) {  // B(st+1) or the next tile's B(0), and this step's A piece
-        if (st + 1 < C3_STEPS)
-          issue_b(st + 1);
-        else if (has_next)
-          issue_b(0);
-        if (st < 6) {
-          const int j = wave + 8 * st;
-          if (j < C3_APIECES) {
-            issue_a(t, 1, j);
-            return 1;
-          }
-        } else if (st >= 9 && st < 15 && has_next) {
-          const int j = wave + 8 * (st - 9);
-          if (j < C3_APIECES) {
-            issue_a(tn, 0, j);
-            return 1;
-          }
-        }
-        return 0;
-      };
-      // ks 1 of step st from registers; reads the ks-0 A fragments of step nst under it
-      auto m1 = [&](int nst, bool prefetch) {
-#pragma unroll
-        for (int nj = 0; nj < 8; ++nj) {
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], fa1[mi], fb[nj]);
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-          if (prefetch && nj >= 2 && nj < 6) {
-            fa[nj - 2].v = *reinterpret_cast<const uint4*>(smem + a_off(nst, 0, nj - 2));
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
-        }
-      };
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) fa[mi].v = *reinterpret_cast<const uint4*>(smem + a_off(0, 0, mi));
-      // one instruction stream for both halves; only the barrier's place differs: early waves
-      // [ks-0 reads, ks 0, ks 1 | barrier], late waves [ks-0 reads, ks 0 | barrier | ks 1]
-      int a_pending = 0;  // late waves: an A piece issued in the previous segment
-#pragma unroll 1
-      for (int st = 0; st < C3_STEPS; ++st) {
-        const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
-#pragma unroll
-        for (int nj = 0; nj < 8; ++nj)
-          fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, g));
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) fa1[mi].v = *reinterpret_cast<const uint4*>(smem + a_off(st, 1, mi));
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // all of them before the first MFMA
-        const bool dma_here = !late || st == 0;
-        // ---- ks 0, the ks-1 B fragments read as their registers free up
-#pragma unroll
-        for (int nj = 0; nj < 8; ++nj) {
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], fa[mi], fb[nj]);
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-          fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, 4 + g));
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if (nj == 1 && dma_here) a_pending = dma(st);
-        }
-        if (late) {
-          if (a_pending == 1)
-            asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          a_pending = st + 1 < C3_STEPS ? dma(st + 1) : 0;  // the next step's DMA under this ks 1
-        }
-        // ---- ks 1; the next step's ks-0 A fragments are read under it (the tile's first step
-        // reads its own after the tile's prologue barrier)
-        m1(st + 1 < C3_STEPS ? st + 1 : st, st + 1 < C3_STEPS);
-        if (!late) {
-          if (a_pending == 1)
-            asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-      }
-    }
     // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
     // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
     bf16_t* yt = y + (((tile * 8 + wave) * 4) * 4) * 512;  // [mi][nj/2][lane][8]
     const bool interior = t.y0 + C3_TH <= H && t.x0 + C3_TW <= W;
-    // SCHED 1: the statistics live in registers for this tile's epilogue only (they would cost the
-    // step loop 32 registers) and are added to the wave's own LDS slots afterwards
-    f32x2 tsum[8], tsq[8];
-#pragma unroll
-    for (int nj = 0; nj < 8; ++nj) tsum[nj] = tsq[nj] = f32x2{0.f, 0.f};
-    f32x2(&ssum)[8] = SCHED == 0 ? ssum_k : tsum;
-    f32x2(&ssq)[8] = SCHED == 0 ? ssq_k : tsq;
 #pragma unroll
     for (int np = 0; np < 4; ++np) {
       const float b0 = sbias[wn * 128 + 32 * np + r], b1 = sbias[wn * 128 + 32 * np + 16 + r];
@@ -1466,35 +1358,14 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
         }
       }
     }
-    if constexpr (SCHED != 0) {
-      // this tile's sums: lanes of equal r, then the wave's own slots (no other wave writes them)
-#pragma unroll
-      for (int nj = 0; nj < 8; ++nj) {
-        float a = tsum[nj].x + tsum[nj].y, q = tsq[nj].x + tsq[nj].y;
-        a += __shfl_xor(a, 16);
-        a += __shfl_xor(a, 32);
-        q += __shfl_xor(q, 16);
-        q += __shfl_xor(q, 32);
-        if (g == 0) {
-          float2* slot = reinterpret_cast<float2*>(sred) + wm * C5 + wn * 128 + 16 * nj + r;
-          const float2 o = *slot;
-          *slot = make_float2(o.x + a, o.y + q);
-        }
-      }
-    }
   }
   // ---- statistics: lanes of equal r, then the 4 row-pair waves in fixed order
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (SCHED != 0) {
-    for (int i = tid; i < C5 * 2; i += 512)
-      slab[(long long)blockIdx.x * C5 * 2 + i] = sred[i] + sred[C5 * 2 + i] + sred[2 * C5 * 2 + i] + sred[3 * C5 * 2 + i];
-    return;
-  }
   float* red = (float*)smem;  // [4 wm][256 n][2]
 #pragma unroll
   for (int nj = 0; nj < 8; ++nj) {
-    float a = ssum_k[nj].x + ssum_k[nj].y, q = ssq_k[nj].x + ssq_k[nj].y;
+    float a = ssum[nj].x + ssum[nj].y, q = ssq[nj].x + ssq[nj].y;
     a += __shfl_xor(a, 16);
     a += __shfl_xor(a, 32);
     q += __shfl_xor(q, 16);
@@ -1993,24 +1864,11 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   {
     TimerScope ts("rp_conv3x3", s);
     if constexpr (sizeof(T) == 2) {
-      const char* sched_env = getenv("RGBD_C3_SCHED");  // development A/B (read per call)
-      const int sched = sched_env ? atoi(sched_env) : 0;
-      static const hipError_t attr0 = hipFuncSetAttribute(
-          (const void*)k_rp_conv3x3_v3<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
-      static const hipError_t attr1 = hipFuncSetAttribute(
-          (const void*)k_rp_conv3x3_v3<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
-      static const hipError_t attr2 = hipFuncSetAttribute(
-          (const void*)k_rp_conv3x3_v3<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
-      if (attr0 != hipSuccess) return (int)attr0;
-      if (attr1 != hipSuccess) return (int)attr1;
-      if (attr2 != hipSuccess) return (int)attr2;
+      static const hipError_t attr = hipFuncSetAttribute(
+          (const void*)k_rp_conv3x3_v3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
+      if (attr != hipSuccess) return (int)attr;
       gcv = conv3_grid(B, H, W);
-      if (sched == 0)
-        k_rp_conv3x3_v3<0><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
-      else if (sched == 1)
-        k_rp_conv3x3_v3<1><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
-      else
-        k_rp_conv3x3_v3<2><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+      k_rp_conv3x3_v3<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
     } else {
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
