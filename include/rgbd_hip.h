@@ -470,6 +470,18 @@ int rgbd_pack_mask_bits(const uint8_t* masks, int n, long long npx, unsigned lon
 int rgbd_mask_intersections(const unsigned long long* a, int na, const unsigned long long* b, int nb, long long npx,
                             int* inter, void* stream);
 
+/* dW of up to three bf16 DSAM legs as ONE segment GEMM (k_dsam_segw): per leg the five filters'
+ * gradients straight from the reference's form — conv_i's from x * bit_i of the source pixel's
+ * region code, the projection's from x (custom_model.py:682-699) — accumulated together over all
+ * output pixels, without the code-merged path's planning, per-code partials and combine; a leg
+ * whose output tiles are too few for the chip splits its pixel range (fixed order sum).  Same
+ * outputs as rgbd_dsam_bwd_weight_planned_multi up to float32 summation order.  runs[i].plan is
+ * not used; runs[i].ws: rgbd_dsam_seg_workspace_size bytes, distinct per run.  Cin % 32 == 0,
+ * Cout % 64 == 0. */
+size_t rgbd_dsam_seg_workspace_size(int B, int Cin, int h, int w, int Cout);
+int rgbd_dsam_bwd_weight_seg(int n, const rgbd_dsam_dw_run* runs, const rgbd_decomp_info* info,
+                             void* stream);
+
 /* ---------------------------------------------------------------- f1 / f2 dense layers
  * The nn.Linear layers of the Mask2Former decoder (transformers 5.15 modeling_mask2former.py:
  * self_attn q/k/v/out_proj :1480-1483, fc1/fc2 :1711-1714), of the pixel decoder's encoder

@@ -600,6 +600,35 @@ def dsam_bwd_weight_multi(runs, info):
     return outs
 
 
+def dsam_bwd_weight_seg(runs, info):
+    """dW/db of up to three bfloat16 DSAM legs as one segment GEMM launch (rgbd_dsam_bwd_weight_seg:
+    no planning, no per-code partials).  ``runs``: (gout_nhwc [B,ho,wo,Co], x_nhwc [B,h,w,Ci],
+    code [B,h,w]) tuples; returns per run (dconv, dproj, dbias)."""
+    if not 1 <= len(runs) <= 3:
+        raise ValueError("dsam_bwd_weight_seg: one to three runs")
+    L = _lib.lib()
+    arr = (_DwRun * len(runs))()
+    outs = []
+    for j, (gout_nhwc, x_nhwc, code) in enumerate(runs):
+        _need_cuda(gout_nhwc, x_nhwc, code, info)
+        if gout_nhwc.dtype != torch.bfloat16 or x_nhwc.dtype != torch.bfloat16:
+            raise ValueError("dsam_bwd_weight_seg: bfloat16 legs only")
+        B, ho, wo, Co = gout_nhwc.shape
+        _, h, w, Ci = x_nhwc.shape
+        if (ho, wo) != ((h + 1) // 2, (w + 1) // 2) or tuple(code.shape) != (B, h, w):
+            raise ValueError(f"dsam_bwd_weight_seg: run {j} shapes {tuple(gout_nhwc.shape)} {tuple(x_nhwc.shape)}")
+        dev = gout_nhwc.device
+        dconv = torch.empty((4, Co, Ci, 3, 3), dtype=torch.float32, device=dev)
+        dproj = torch.empty((Co, Ci, 3, 3), dtype=torch.float32, device=dev)
+        dbias = torch.empty((4, Co), dtype=torch.float32, device=dev)
+        ws = _workspace(dev, L.rgbd_dsam_seg_workspace_size(B, Ci, h, w, Co), f"dsam_segw{j}")
+        arr[j] = _DwRun(gout_nhwc.data_ptr(), x_nhwc.data_ptr(), code.data_ptr(), B, Ci, h, w, Co, dconv.data_ptr(),
+                        dproj.data_ptr(), dbias.data_ptr(), None, ws.data_ptr())
+        outs.append((dconv, dproj, dbias))
+    check(L.rgbd_dsam_bwd_weight_seg(len(runs), arr, _p(info), _stream(runs[0][0].device)), "rgbd_dsam_bwd_weight_seg")
+    return outs
+
+
 # ------------------------------------------------------------------ f1 mask predictor
 def mask_logits(emb: torch.Tensor, pix: torch.Tensor) -> torch.Tensor:
     """einsum("bqc,bchw->bqhw", emb, pix) (modeling_mask2former.py:2046) on the MFMA kernel.
