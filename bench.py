@@ -731,7 +731,11 @@ def main():
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
                      "traffic": None if traffic is None else round(traffic[0]),
                      "traffic_unit": "bytes/launch", "traffic_source": None if traffic is None else traffic[1],
-                     "algorithmic_bytes": (128 + 256) * 2 * B * args.height * args.width},
+                     "algorithmic_bytes": (128 + 256) * 2 * B * args.height * args.width,
+                     "timing": ("HIP events around each conv5 launch on its stream over the eager timed steps, no "
+                                "profiler attached; the committed rocprofv3 kernel_stats of the bench step "
+                                "(profiles/r04_*) average every conv5 launch under the profiler, which costs "
+                                "the kernel 6-12 % (DESIGN.md §5.8)")},
         "kernels": fracs,
     }
     if rank == 0 and args.parity:
