@@ -55,8 +55,9 @@ def side_stream(dev):
 # False runs them as two launches, dW1 on the side stream (bitwise the same gradients)
 JOINT_DW = True
 # bf16 backward: every dW as the segment GEMM (rgbd_dsam_bwd_weight_seg: five accumulators over
-# all pixels, no dW planning, no per-code partials or combine); False: the code-merged planned path
-SEG_DW = True
+# all pixels, no dW planning, no per-code partials); False: the code-merged planned path.  Off:
+# measured 2.3x slower on the bench step (r04: 713 vs 309 us for the three legs' dW)
+SEG_DW = False
 
 
 class _Side:
