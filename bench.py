@@ -528,16 +528,20 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False):
     return res
 
 
-def full_model(dev, B=8, H=480, W=640, steps=5, warmup=2):
+def full_model(dev, B=8, H=480, W=640, steps=5, warmup=2, graph=True):
     """The whole drop-in model (CustomMask2FormerForUniversalSegmentation v0.4.0: Swin-T, the hot
     path, the MSDeformAttn pixel decoder, the masked-attention decoder, the Hungarian-matched
     loss with 9 auxiliary outputs; custom_model.py:37-53), one bf16-autocast training step
-    (forward with labels, backward, AdamW lr 1e-5) on synthetic NYUv2-shaped scenes with their
-    instance masks, deterministic random-init weights (48 labels).  Eager; ``kernel_ms`` = the
-    five kernels with the most device time in one step (torch.profiler over the HIP runtime)."""
+    (forward with labels, backward, the HF Trainer's AdamW) on synthetic NYUv2-shaped scenes with
+    their instance masks, deterministic random-init weights (48 labels).  Timed eagerly and as
+    one captured HIP graph (train_graph.CapturedTrainStep, at most two concurrent branches);
+    ``img_s`` is the captured step when the capture succeeds.  ``kernel_ms`` = the five kernels
+    with the most device time in one eager step (torch.profiler over the HIP runtime)."""
     from rgbd_amd import init as winit, ops, synthetic
     from rgbd_amd.config import standard_config
     from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
+    from rgbd_amd.optim import HF_TRAINER_ADAMW, HipAdamW
+    from rgbd_amd.train_graph import CapturedTrainStep
     scenes = [synthetic.make_scene(synthetic.scene_seed(4, i), H, W) for i in range(B)]
     depth = torch.from_numpy(np.stack([s["depth_u8"] for s in scenes])).to(dev)
     rgb = torch.from_numpy(np.stack([s["rgb_u8"] for s in scenes])).contiguous().to(dev)
@@ -547,25 +551,51 @@ def full_model(dev, B=8, H=480, W=640, steps=5, warmup=2):
     m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
     winit.init_deterministic(m)
     m.set_compute_dtype(torch.bfloat16).to(dev).train()
-    opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, fused=True)
+    opt = HipAdamW([p for p in m.parameters() if p.requires_grad], **HF_TRAINER_ADAMW)
 
-    def step():
+    def fb():
         pv = ops.assemble_pixel_values(depth, rgb)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = m(pixel_values=pv, mask_labels=mask_labels, class_labels=class_labels)
         out.loss.backward()
+        return out.loss.detach()
+
+    def step():
+        loss = fb()
         opt.step()
         opt.zero_grad(set_to_none=True)
-        return out.loss
+        return loss
+
+    def timed(fn, n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            out = fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n, out
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        loss = step()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    kernels = None
+    dt_eager, loss = timed(step, steps)
+    res = {"workload": "whole drop-in model training step (Swin-T + hot path + pixel decoder + masked-attention "
+                       "decoder + Hungarian-matched loss, 9 aux outputs, AdamW), bf16 autocast",
+           "batch": B, "shape": f"{W}x{H}", "steps": steps, "eager_img_s": round(B / dt_eager, 2),
+           "eager_ms_per_step": round(dt_eager * 1e3, 2), "loss": round(float(loss), 4)}
+    dt, how = dt_eager, "eager"
+    if graph:
+        try:
+            cs = CapturedTrainStep(fb, opt, warmup=1)
+            for _ in range(warmup):
+                cs()
+            dt_graph, loss_g = timed(cs, steps)
+            m.model.pixel_level_module.check_statuses()
+            res.update({"graph_img_s": round(B / dt_graph, 2), "graph_ms_per_step": round(dt_graph * 1e3, 2),
+                        "graph_branches": cs.width, "graph_loss": round(float(loss_g), 4)})
+            dt, how = dt_graph, "captured graph"
+            del cs
+        except Exception as e:  # reported; the eager number stands
+            res["graph_error"] = repr(e)[:300]
+    res["img_s"], res["ms_per_step"] = round(B / dt, 2), round(dt * 1e3, 2)
+    res["timed"] = how
     try:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CUDA]) as prof:
@@ -579,15 +609,11 @@ def full_model(dev, B=8, H=480, W=640, steps=5, warmup=2):
                     tot[ev.name] = tot.get(ev.name, 0.0) + t
                     cnt[ev.name] = cnt.get(ev.name, 0) + 1
         top = sorted(tot.items(), key=lambda kv: -kv[1])[:5]
-        kernels = {"kernel_ms_top5": {k[:90]: round(v / 1e3, 3) for k, v in top},
-                   "launches_top5": {k[:90]: cnt[k] for k, _ in top},
-                   "kernel_ms_total": round(sum(tot.values()) / 1e3, 2), "launches": int(sum(cnt.values()))}
+        res.update({"kernel_ms_top5": {k[:90]: round(v / 1e3, 3) for k, v in top},
+                    "launches_top5": {k[:90]: cnt[k] for k, _ in top},
+                    "kernel_ms_total": round(sum(tot.values()) / 1e3, 2), "launches": int(sum(cnt.values()))})
     except Exception as e:  # the profiler is a report, not the measurement
-        kernels = {"profiler_error": repr(e)[:200]}
-    res = {"workload": "whole drop-in model training step (Swin-T + hot path + pixel decoder + masked-attention "
-                       "decoder + Hungarian-matched loss, 9 aux outputs, AdamW), bf16 autocast, eager",
-           "batch": B, "shape": f"{W}x{H}", "img_s": round(B / dt, 2), "ms_per_step": round(dt * 1e3, 2),
-           "steps": steps, "loss": round(float(loss.detach()), 4), **kernels}
+        res["profiler_error"] = repr(e)[:200]
     del m, opt
     torch.cuda.empty_cache()
     return res

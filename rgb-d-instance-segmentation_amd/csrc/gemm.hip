@@ -400,16 +400,21 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(GArgs a, int batch) 
   }
 }
 
-// bias gradient: out[n] = sum_m y[m][n], float32, fixed order, in one launch.  The rows in at
-// most CS_MAXCH chunks; block = 256 columns x one chunk, 256 threads = 32 column groups of 8 (one
-// 16-byte load per row when aligned) x 8 row lanes folded through LDS in fixed order -> the
-// chunk's partial, stored write-through (sc1); the last chunk of a column block to take its
-// ticket (agent-scope counter, after every partial store drained) loads the partials sc1 and sums
-// them in chunk order (MI355X_MICROARCH.md visibility table, row 1), then rearms the ticket.
-// Bitwise the former two-pass result; one launch instead of two per bias.
-constexpr int CS_MAXCH = 64;
+// bias gradient: out[n] = sum_m y[m][n], float32, fixed order, in one launch.  The rows in
+// chunks sized so that the launch has about CS_TARGET blocks (at least 32 rows per chunk, at most
+// CS_MAXCH chunks): a [50400 x 256] bias gradient gets 256 chunks, not one block per CU quarter.
+// Block = 256 columns x one chunk, 256 threads = 32 column groups of 8 (one 16-byte load per row
+// when aligned, four rows in flight) x 8 row lanes folded through LDS in fixed order -> the
+// chunk's partial, stored write-through (sc1); the last chunk of a column block to take its ticket
+// (agent-scope counter, after every partial store drained) sums the partials in chunk order with
+// the same 8-row-lane x 32-column-group split (loads sc1, MI355X_MICROARCH.md visibility table,
+// row 1), then rearms the ticket.  Deterministic for a given shape.
+constexpr int CS_MAXCH = 256, CS_TARGET = 1024;
 
-inline int cs_chunks(int rows) { return std::min(CS_MAXCH, std::max(1, ceil_div(rows, 64))); }
+inline int cs_chunks(int rows, int N) {
+  const int nbx = std::max(1, ceil_div(N, 256));
+  return std::min({CS_MAXCH, std::max(1, ceil_div(rows, 32)), std::max(1, ceil_div(CS_TARGET, nbx))});
+}
 // the tickets occupy a fixed head of the workspace whatever N is, so calls of different widths on
 // one workspace never see each other's partials as tickets
 constexpr int CS_MAXBLK = 1024;  // column blocks: N <= 262 144
@@ -426,19 +431,22 @@ __global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int row
   const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c0 < N) {
-    for (int m = r0 + rl; m < r1; m += 8) {
-      const T* row = y + (long long)m * ld + c0;
-      float v[8];
-      if (vec && c0 + 8 <= N) {
+    if (vec && c0 + 8 <= N) {
+#pragma unroll 4
+      for (int m = r0 + rl; m < r1; m += 8) {
         Frag<T> f;
-        f.load(row);
+        f.load(y + (long long)m * ld + c0);
+        float v[8];
         f.to8(v);
-      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = c0 + j < N ? Num<T>::to_f(row[j]) : 0.f;
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
       }
+    } else {
+      for (int m = r0 + rl; m < r1; m += 8) {
+        const T* row = y + (long long)m * ld + c0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+        for (int j = 0; j < 8; ++j) acc[j] += c0 + j < N ? Num<T>::to_f(row[j]) : 0.f;
+      }
     }
   }
 #pragma unroll
@@ -459,10 +467,22 @@ __global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int row
     last_s = __hip_atomic_fetch_add(tickets + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
   __syncthreads();
   if (!last_s) return;
+  // the chunks' partials: row lane rl takes chunks rl, rl + 8, ... (in order), then the 8 lanes
+  // fold in fixed order
+  float t8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k = rl; k < nch; k += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (c0 + j < N) t8[j] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (k * N + c0 + j) * 4, 0, WT_SC1));
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][8 * cg + j] = t8[j];
+  __syncthreads();
   if (c < N) {
     float t = 0.f;
-    for (int k = 0; k < nch; ++k)
-      t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (k * N + c) * 4, 0, WT_SC1));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][threadIdx.x];
     out[c] = t;
   }
   if (threadIdx.x == 0) tickets[blockIdx.x] = 0;  // rearmed for the next call on this workspace
@@ -553,16 +573,16 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
 
 size_t rgbd_colsum_workspace_size(int rows, int N) {
   if (rows <= 0 || N <= 0) return 256;
-  return cs_ticket_bytes(N) + (size_t)cs_chunks(rows) * N * sizeof(float);
+  return cs_ticket_bytes(N) + (size_t)cs_chunks(rows, N) * N * sizeof(float);
 }
 
 int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* out, void* ws, void* stream) {
   RGBD_REQUIRE(y && out && ws && rows > 0 && N > 0 && ld >= N, RGBD_E_ARG);
   RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
-  RGBD_REQUIRE(ceil_div(N, 256) <= CS_MAXBLK && (long long)cs_chunks(rows) * N * (long long)sizeof(float) < (1ll << 31),
+  RGBD_REQUIRE(ceil_div(N, 256) <= CS_MAXBLK && (long long)cs_chunks(rows, N) * N * (long long)sizeof(float) < (1ll << 31),
                RGBD_E_SHAPE);
   hipStream_t s = (hipStream_t)stream;
-  const int nch = cs_chunks(rows);
+  const int nch = cs_chunks(rows, N);
   const int chunk = ceil_div(rows, nch);
   const int esz = dtype == RGBD_BF16 ? 2 : 4;
   const int vec = (((uintptr_t)y) % 16 == 0) && ((ld * esz) % 16 == 0);

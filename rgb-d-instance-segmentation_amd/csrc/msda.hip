@@ -193,6 +193,114 @@ __global__ __launch_bounds__(256) void k_msda_bwd(const T* __restrict__ value, M
   }
 }
 
+// Backward over runs of R consecutive queries of one (image, head), per group of D lanes (lane c =
+// channel c), for the reference configuration's L levels x P points (compile-time, so the
+// per-slot state lives in registers).  Neighbouring queries sample neighbouring places: a query
+// one pixel further right samples, per (level, point), the same bilinear cells shifted by one
+// cell on its own level and by half / a quarter of a cell on the coarser ones, so two or all four
+// of its taps are cells the previous query also scattered into.  Each (level, point) slot keeps
+// the previous query's four (cell, a * w_tap * go) contributions in registers; a new query's tap
+// on one of those cells adds the held value to its own, and only contributions whose cell the
+// next query does not touch are flushed with a float atomic (same full-rate shape: two 128-byte
+// row segments per wave-instruction).  The sums are the same (float addition order aside: the
+// atomics already leave it unspecified); how many atomics are saved depends on how smoothly the
+// sampling offsets vary across neighbouring queries (spatially constant at the pixel decoder's
+// initialisation: about 60 % fewer at C2).
+template <typename T, int D, int L, int P, int R>
+__global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ value, MsdaLevels lv, int S, int Q,
+                                                       int NH, const float* __restrict__ loc,
+                                                       const float* __restrict__ attw, const T* __restrict__ gout,
+                                                       long long ngroups, int nrun, float* __restrict__ gvalue,
+                                                       float* __restrict__ gloc, float* __restrict__ gattw) {
+  constexpr int LP = L * P;
+  const int c = threadIdx.x % D;
+  const long long gid = (long long)blockIdx.x * (256 / D) + threadIdx.x / D;
+  // every lane of a group takes part in the shuffles: out-of-range groups run with zero weight
+  const bool glive = gid < ngroups;
+  const long long g0 = glive ? gid : 0;
+  const int h = (int)(g0 % NH);
+  const long long br = g0 / NH;
+  const int run = (int)(br % nrun);
+  const long long b = br / nrun;
+  const int qa = run * R, qn = min(R, Q - qa);
+  const long long voff = b * S * NH * D + (long long)h * D + c;
+  const T* vb = value + voff;
+  float* gvb = gvalue + voff;
+  float gos[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+    gos[i] = glive && i < qn ? Num<T>::to_f(gout[((b * Q + qa + i) * NH + h) * D + c]) : 0.f;
+  // slot-major: one (level, point) slot over the run's queries, its held taps in 8 registers
+  for (int k = 0; k < LP; ++k) {
+    const int l = k / P;
+    const int H = lv.H[l], W = lv.W[l];
+    const long long lo = (long long)lv.start[l] * NH * D;
+    int pidx[4] = {-1, -1, -1, -1};
+    float pval[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const bool live = glive && i < qn;  // group-uniform
+      const long long q0 = live ? (b * Q + qa + i) * NH + h : 0;
+      const float go = gos[i];
+      const Tap t = msda_tap(loc[(q0 * LP + k) * 2], loc[(q0 * LP + k) * 2 + 1], H, W);
+      const float a = live ? attw[q0 * LP + k] : 0.f;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = t.idx[e] >= 0 ? Num<T>::to_f(vb[lo + (long long)t.idx[e] * NH * D]) : 0.f;
+      const float s = t.w[0] * v[0] + t.w[1] * v[1] + t.w[2] * v[2] + t.w[3] * v[3];
+      const float dsx = (1.f - t.ly) * (v[1] - v[0]) + t.ly * (v[3] - v[2]);
+      const float dsy = (1.f - t.lx) * (v[2] - v[0]) + t.lx * (v[3] - v[1]);
+      const float gw = group_sum<D>(go * s);
+      const float gx = group_sum<D>(go * dsx);
+      const float gy = group_sum<D>(go * dsy);
+      if (live && c == 0) {
+        gattw[q0 * LP + k] = gw;
+        gloc[(q0 * LP + k) * 2] = a * gx * (float)W;
+        gloc[(q0 * LP + k) * 2 + 1] = a * gy * (float)H;
+      }
+      const float ga = a * go;
+      int nidx[4];
+      float nv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        nidx[e] = live ? t.idx[e] : -1;
+        nv[e] = nidx[e] >= 0 ? ga * t.w[e] : 0.f;
+      }
+      // the held contributions: carried into a tap on the same cell, else flushed
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bool carried = false;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (pidx[j] >= 0 && nidx[e] == pidx[j]) {
+            nv[e] += pval[j];
+            carried = true;
+          }
+        if (pidx[j] >= 0 && !carried) atomicAdd(gvb + lo + (long long)pidx[j] * NH * D, pval[j]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pidx[e] = nidx[e];
+        pval[e] = nv[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (pidx[e] >= 0) atomicAdd(gvb + lo + (long long)pidx[e] * NH * D, pval[e]);
+  }
+}
+
+constexpr int MSDA_RUN = 8;  // queries per run of k_msda_bwd_runs
+
+// RGBD_MSDA_RUNS=0 selects the per-query backward (A/B); read once
+inline bool msda_runs_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RGBD_MSDA_RUNS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int msda_levels(int L, const int* shapes_host, MsdaLevels& lv, int& S) {
   if (L < 1 || L > MSDA_MAX_L || !shapes_host) return RGBD_E_SHAPE;
   lv.L = L;
@@ -221,6 +329,13 @@ int launch_bwd(const void* value, const MsdaLevels& lv, int B, int S, int Q, int
   // the value gradient is accumulated with atomics: zero it first (stream-ordered)
   const hipError_t e = hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * NH * D, s);
   if (e != hipSuccess) return (int)e;
+  if (lv.L == 3 && P == 4 && msda_runs_enabled()) {  // the reference configuration (3 levels x 4 points)
+    const int nrun = ceil_div(Q, MSDA_RUN);
+    const long long ngroups = (long long)B * nrun * NH;
+    k_msda_bwd_runs<T, D, 3, 4, MSDA_RUN><<<(unsigned)ceil_div(ngroups, 256 / D), 256, 0, s>>>(
+        (const T*)value, lv, S, Q, NH, loc, attw, (const T*)gout, ngroups, nrun, gvalue, gloc, gattw);
+    return RGBD_OK;
+  }
   k_msda_bwd<T, D><<<(unsigned)ceil_div(nqh, 256 / D), 256, 0, s>>>((const T*)value, lv, S, Q, NH, P, loc, attw,
                                                                    (const T*)gout, nqh, gvalue, gloc, gattw);
   return RGBD_OK;

@@ -19,7 +19,7 @@ from transformers import Mask2FormerConfig, Mask2FormerForUniversalSegmentation,
 from transformers.models.mask2former.modeling_mask2former import (Mask2FormerPixelLevelModule,
                                                                   Mask2FormerPixelLevelModuleOutput)
 
-from . import deform_attn, dense, mask_predictor, masked_attention, point_loss, swin
+from . import deform_attn, dense, mask_predictor, masked_attention, ops, point_loss, swin
 from .hot_path import hot_path, prepare
 from .modules import DSAModule, DepthGradientInjectionResidual, EnhancedDepthImageRatioPredictor
 
@@ -84,6 +84,12 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
         dt = color_feature_map[0].dtype
         return [f.to(dt) for f in feats]
 
+    def check_statuses(self):
+        """After a replay of a captured step (its stream synchronised): raise the reference's
+        ValueError for an image whose depth range the decomposition rejected."""
+        for st in getattr(self, "captured_statuses", ()):
+            st.check()
+
     def forward(self, pixel_values: Tensor, output_hidden_states: bool = False) -> Mask2FormerPixelLevelModuleOutput:
         if self.version == "0.0.0":
             backbone_features = list(self.encoder(pixel_values).feature_maps)
@@ -95,14 +101,19 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
                 color_feature_map = self.encoder(rgb).feature_maps
             statuses = []
             backbone_features = self.hot_path_features(pixel_values, color_feature_map, status_sink=statuses)
-        decoder_output = self.decoder(backbone_features, output_hidden_states=output_hidden_states)
+        with ops.host_constants():  # the pixel decoder's level-shape tensor (modeling_mask2former.py:1347)
+            decoder_output = self.decoder(backbone_features, output_hidden_states=output_hidden_states)
         if self.version != "0.0.0":
             # The reference raises numpy's ValueError for a non-finite or too-narrow depth range
             # (custom_model.py:715-717).  The decomposition status was copied to the host behind
             # the decomposition; waiting for it here lets the DSAM / DGGM / pixel-decoder kernels
             # already enqueued keep the GPU busy.
-            for st in statuses:
-                st.check()
+            if torch.cuda.is_current_stream_capturing():
+                # a captured step: the statuses are read after each replay (check_statuses())
+                self.captured_statuses = statuses
+            else:
+                for st in statuses:
+                    st.check()
         return Mask2FormerPixelLevelModuleOutput(
             encoder_last_hidden_state=backbone_features[-1],
             encoder_hidden_states=tuple(backbone_features) if output_hidden_states else None,

@@ -57,8 +57,7 @@ class HipMSDeformAttn(_HFMSDA):
         weights = self.attention_weights(hidden_states).view(B, Q, self.n_heads, self.n_levels * self.n_points)
         weights = nn.functional.softmax(weights, -1).view(B, Q, self.n_heads, self.n_levels, self.n_points)
         if reference_points.shape[-1] == 2:
-            norm = torch.tensor([[w, h] for h, w in spatial_shapes_list], dtype=torch.long,
-                                device=reference_points.device)
+            norm = ops.device_const([[w, h] for h, w in spatial_shapes_list], torch.long, reference_points.device)
             loc = reference_points[:, :, None, :, None, :] + offsets / norm[None, None, None, :, None, :]
         elif reference_points.shape[-1] == 4:
             loc = (reference_points[:, :, None, :, None, :2]

@@ -5,11 +5,11 @@ memory is plumbing), passes raw pointers + the current HIP stream to the C ABI a
 ``RgbdHipError`` on a non-zero return.  Nothing here synchronises with the device except
 ``decode_info`` (explicitly a host read-back for tests/diagnostics).
 """
+import contextlib
 import ctypes
 import math
 
 import numpy as np
-
 import torch
 
 from . import _lib
@@ -60,6 +60,61 @@ def _workspace(dev, nbytes: int, tag: str, zeroed: bool = False):
         buf = alloc(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
         _ws_cache[key] = buf
     return buf
+
+
+# ------------------------------------------------------------------ small host constants
+# Shapes, offsets and counts the model builds from Python numbers every step (the pixel decoder's
+# level shapes, the matcher's per-image offsets, the loss's instance count) would each be a
+# blocking host->device copy — torch synchronises the stream behind a pageable copy, draining the
+# GPU queue — and cannot be captured into a graph.  They are the same numbers step after step,
+# so each distinct value is copied once and the device tensor reused (read-only by contract).
+_consts = {}
+
+
+def _freeze(v):
+    if isinstance(v, (list, tuple)):
+        return tuple(_freeze(x) for x in v)
+    if isinstance(v, (bool, int, float)):
+        return v
+    raise TypeError("device_const: numbers or nested lists / tuples of numbers only")
+
+
+def device_const(values, dtype, device):
+    """A device tensor holding ``values`` (numbers, nested lists / tuples), copied once per
+    distinct (values, dtype, device) and shared: callers must not modify it."""
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (_freeze(values), dtype, device)
+    t = _consts.get(key)
+    if t is None:
+        if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("device_const: a new constant during graph capture (run the step eagerly first)")
+        t = torch.tensor(values, dtype=dtype).to(device)
+        _consts[key] = t
+    return t
+
+
+@contextlib.contextmanager
+def host_constants():
+    """Inside the block, ``torch.as_tensor(numbers, device=cuda)`` returns the shared
+    ``device_const`` (library code outside this package calls it on every forward, e.g. the HF
+    pixel decoder's level shapes, modeling_mask2former.py:1347); anything else goes to torch."""
+    orig = torch.as_tensor
+
+    def as_tensor(data, dtype=None, device=None):
+        if device is not None and torch.device(device).type == "cuda" and not isinstance(data, torch.Tensor):
+            try:
+                frozen = _freeze(data)
+            except TypeError:
+                return orig(data, dtype=dtype, device=device)
+            return device_const(frozen, orig(data, dtype=dtype).dtype, device)
+        return orig(data, dtype=dtype, device=device)
+    torch.as_tensor = as_tensor
+    try:
+        yield
+    finally:
+        torch.as_tensor = orig
 
 
 # ------------------------------------------------------------------ K1 DGGM-pre / assembly
@@ -208,15 +263,30 @@ class DeferredStatus:
     after it keep running) and raises the reference's ValueError; the drop-in module calls it
     at the end of its forward, after the pixel decoder has been enqueued."""
 
+    _captured_hosts = {}  # (device, shape): the pinned buffer a captured graph copies into
+
     def __init__(self, info: torch.Tensor):
         st = info.view(torch.int32)[:, 0]  # rgbd_decomp_info.status, the record's first word
-        self.host = torch.empty(st.shape, dtype=torch.int32, pin_memory=True)
+        self.captured = torch.cuda.is_current_stream_capturing()
+        if self.captured:
+            # the graph's copy node writes this buffer on every replay: one per shape, kept alive
+            key = (info.device, tuple(st.shape))
+            host = DeferredStatus._captured_hosts.get(key)
+            if host is None:
+                host = DeferredStatus._captured_hosts[key] = torch.empty(st.shape, dtype=torch.int32, pin_memory=True)
+            self.host = host
+        else:
+            self.host = torch.empty(st.shape, dtype=torch.int32, pin_memory=True)
         self.host.copy_(st, non_blocking=True)
-        self.event = torch.cuda.Event()
-        self.event.record(torch.cuda.current_stream(info.device))
+        self.event = None if self.captured else torch.cuda.Event()
+        if self.event is not None:
+            self.event.record(torch.cuda.current_stream(info.device))
 
     def check(self):
-        self.event.synchronize()
+        """Eager: wait for the copy and raise.  Captured: call after the replay has finished
+        (e.g. after synchronising its stream): the buffer then holds that replay's statuses."""
+        if self.event is not None:
+            self.event.synchronize()
         _raise_statuses(self.host.tolist())
 
 
@@ -687,7 +757,7 @@ def linear_sum_assignment_batch(costs, validate=False, return_status=False):
     if max(mr, mc) > 2048:
         raise ValueError("rgbd_lsa_batch: matrices up to 2048 on a side")
     cost = torch.cat(flat) if coff > 0 else torch.zeros(1, dtype=torch.float32, device=dev)
-    meta_t = torch.tensor(meta, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    meta_t = device_const(meta, torch.int64, dev)
     # zero-initialised: a matrix the kernel rejects (status != 0) leaves valid indices behind,
     # never uninitialised ones
     rows = torch.zeros(max(ooff, 1), dtype=torch.int64, device=dev)

@@ -19,7 +19,7 @@ from transformers.models.mask2former.modeling_mask2former import Mask2FormerHung
 
 from . import _lib
 from ._lib import check
-from .ops import _need_cuda, _p, _stream
+from .ops import _need_cuda, _p, _stream, device_const
 
 
 def point_sample(maps: torch.Tensor, coords: torch.Tensor) -> torch.Tensor:
@@ -116,23 +116,84 @@ def match_costs(matcher, masks_queries_logits, class_queries_logits, mask_labels
     tgt = torch.cat(tgts) if toff[-1] else torch.zeros((1, P), device=dev)
     cls = torch.cat(ccls) if coff[-1] else torch.zeros((1,), device=dev)
     cost = torch.empty((max(coff[-1], 1),), dtype=torch.float32, device=dev)
-    toff_t = torch.tensor(toff, dtype=torch.int32).to(dev, non_blocking=True)
-    coff_t = torch.tensor(coff[:-1], dtype=torch.int64).to(dev, non_blocking=True)
+    toff_t = device_const(toff, torch.int32, dev)
+    coff_t = device_const(coff[:-1], torch.int64, dev)
     check(_lib.lib().rgbd_match_cost(_p(pred), B, Q, P, _p(tgt), _p(toff_t), _p(cls), _p(coff_t),
                                      float(matcher.cost_mask), float(matcher.cost_class), float(matcher.cost_dice),
                                      _p(cost), _stream(dev)), "rgbd_match_cost")
     return [cost[coff[i]:coff[i + 1]].view(Q, toff[i + 1] - toff[i]) for i in range(B)]
 
 
+class _MatchedRows(torch.autograd.Function):
+    """``x[batch_idx, query_idx]`` for the matcher's indices (modeling_mask2former.py:601) as one
+    row gather of x viewed [B*Q, ...]; backward scatters the rows into zeros with index_copy_.
+    The matched (image, query) pairs are distinct (a one-to-one assignment), so that is the
+    gradient advanced indexing gives, without its accumulate path's index sort."""
+
+    @staticmethod
+    def forward(ctx, x, flat):
+        ctx.shape = x.shape
+        ctx.save_for_backward(flat)
+        return x.reshape(-1, *x.shape[2:]).index_select(0, flat)
+
+    @staticmethod
+    def backward(ctx, g):
+        (flat,) = ctx.saved_tensors
+        shape = ctx.shape
+        gx = g.new_zeros((shape[0] * shape[1], *shape[2:]))
+        gx.index_copy_(0, flat, g)
+        return gx.view(shape), None
+
+
 class HipMask2FormerLoss(Mask2FormerLoss):
     """Mask2FormerLoss with loss_masks' sampling and reductions on the GPU kernels."""
 
+    def get_num_masks(self, class_labels, device):
+        """modeling_mask2former.py:782-795 with the count as a shared device constant (no blocking
+        copy per step); the accelerate all-reduce branch stays the library's."""
+        try:
+            from accelerate import PartialState
+            distributed = PartialState._shared_state != {}
+        except ImportError:
+            distributed = False
+        if distributed:
+            return super().get_num_masks(class_labels, device)
+        num_masks = device_const(float(sum(len(c) for c in class_labels)), torch.float32, device)
+        return torch.clamp(num_masks, min=1)
+
+    def _target_rows(self, mask_labels, dtype):
+        """Every image's target masks cast like the reference (``.to(pred_masks)``), as float32
+        rows [sum T, H, W] and their image offsets — built once per set of labels (the final and
+        the nine auxiliary outputs share them), None when the images differ in size (then the
+        reference's zero-padded batch is used)."""
+        key = (dtype, tuple((m.data_ptr(), m._version, tuple(m.shape)) for m in mask_labels))
+        cached = getattr(self, "_rgbd_targets", None)
+        if cached is not None and cached[0] == key:
+            return cached[1], cached[2]
+        rows = offs = None
+        if mask_labels and len({tuple(m.shape[-2:]) for m in mask_labels}) == 1:
+            rows = torch.cat([m.reshape(-1, *m.shape[-2:]) for m in mask_labels]).to(dtype).float()
+            offs, o = [], 0
+            for m in mask_labels:
+                offs.append(o)
+                o += m.shape[0]
+        self._rgbd_targets = (key, rows, offs)
+        return rows, offs
+
     def loss_masks(self, masks_queries_logits, mask_labels, indices, num_masks):
         src_idx = self._get_predictions_permutation_indices(indices)
-        tgt_idx = self._get_targets_permutation_indices(indices)
-        pred_masks = masks_queries_logits[src_idx]  # [N, h, w]
-        target_masks, _ = self._pad_images_to_max_in_batch(mask_labels)
-        target_masks = target_masks[tgt_idx]
+        B, Q = masks_queries_logits.shape[:2]
+        pred_masks = _MatchedRows.apply(masks_queries_logits, src_idx[0] * Q + src_idx[1])  # [N, h, w]
+        rows, offs = self._target_rows(mask_labels, masks_queries_logits.dtype)
+        if rows is not None:
+            dev = masks_queries_logits.device
+            tflat = torch.cat([j.to(dev) + offs[i] for i, (_, j) in enumerate(indices)]) if indices else \
+                torch.zeros((0,), dtype=torch.long, device=dev)
+            target_masks = rows.index_select(0, tflat)  # float32, already rounded to the logits' dtype
+        else:
+            tgt_idx = self._get_targets_permutation_indices(indices)
+            target_masks, _ = self._pad_images_to_max_in_batch(mask_labels)
+            target_masks = target_masks[tgt_idx].to(masks_queries_logits.dtype)
         N = pred_masks.shape[0]
         P = self.num_points
         if N == 0:
@@ -152,7 +213,7 @@ class HipMask2FormerLoss(Mask2FormerLoss):
             coords = coords.view(-1, 2)[idx.view(-1), :].view(N, k, 2)
             if P - k > 0:
                 coords = torch.cat([coords, torch.rand(N, P - k, 2, device=pred_masks.device)], dim=1)
-            labels = _sample(target_masks.to(pred_masks).reshape(N, *target_masks.shape[-2:]), coords)
+            labels = _sample(target_masks.reshape(N, *target_masks.shape[-2:]), coords)
         logits = point_sample(pred_masks, coords)
         ce, dice = _PointLosses.apply(logits, labels)
         return {"loss_mask": ce.sum() / num_masks, "loss_dice": dice.sum() / num_masks}

@@ -54,6 +54,46 @@ def test_msda_forward_backward_f32(case):
         assert err < 1e-4, (name, err)
 
 
+def _encoder_locations(B, shapes, NH, P, g, jitter=0.0):
+    """Every value pixel as a query at its own reference point plus an offset per (head, level,
+    point) that is the same for every query (the MSDeformAttn initialisation's grid), optionally
+    jittered per query: neighbouring queries then sample shifted copies of the same cells, the
+    case k_msda_bwd_runs carries contributions across."""
+    refs = []
+    for H, W in shapes:
+        ys, xs = torch.meshgrid(torch.arange(H, device=DEV), torch.arange(W, device=DEV), indexing="ij")
+        refs.append(torch.stack([(xs.reshape(-1) + 0.5) / W, (ys.reshape(-1) + 0.5) / H], -1))
+    ref = torch.cat(refs)
+    S, L = ref.shape[0], len(shapes)
+    norm = torch.tensor([[w, h] for h, w in shapes], device=DEV, dtype=torch.float32)
+    off = torch.randn((1, 1, NH, L, P, 2), generator=g, device=DEV) * 2.0
+    off = off + torch.randn((B, S, NH, L, P, 2), generator=g, device=DEV) * jitter
+    return ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]
+
+
+@pytest.mark.parametrize("jitter", [0.0, 0.3])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_msda_backward_carried_taps_vs_hf(jitter, dtype):
+    """Encoder-shaped queries (Q = S, 3 levels x 4 points: the run-carrying backward) with
+    spatially constant / jittered offsets against grid_sample's backward."""
+    B, shapes, NH, D, P = 2, [(30, 40), (15, 20), (8, 10)], 8, 32, 4
+    S = sum(h * w for h, w in shapes)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    value = torch.randn((B, S, NH, D), generator=g, device=DEV).to(dtype)
+    loc = _encoder_locations(B, shapes, NH, P, g, jitter)
+    attw = torch.softmax(torch.randn((B, S, NH, 3 * P), generator=g, device=DEV), -1).view(B, S, NH, 3, P)
+    vr, lr, ar = (t.clone().float().requires_grad_(True) for t in (value, loc, attw))
+    vh, lh, ah = (t.clone().requires_grad_(True) for t in (value, loc, attw))
+    go = torch.randn((B, S, NH * D), generator=g, device=DEV)
+    (hf_msda(vr, shapes, lr, ar) * go).sum().backward()
+    out_h = deform_attn.multi_scale_deformable_attention(vh, shapes, lh, ah)
+    (out_h.float() * go).sum().backward()
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    for a, b, name in ((vh.grad, vr.grad, "value"), (lh.grad, lr.grad, "loc"), (ah.grad, ar.grad, "attw")):
+        err = float((a.float() - b).abs().max()) / (float(b.abs().max()) + 1e-12)
+        assert err < tol, (name, err)
+
+
 def test_msda_bf16_value():
     B, shapes, NH, D, P, Q = CASES[0]
     value, loc, attw = _inputs(B, shapes, NH, D, P, Q, dtype=torch.bfloat16, seed=3)

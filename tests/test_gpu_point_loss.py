@@ -85,6 +85,42 @@ def test_loss_masks_and_grad_match_reference():
     assert _rel(mh.grad, mr.grad) <= 1e-4, _rel(mh.grad, mr.grad)
 
 
+@pytest.mark.parametrize("ragged", [False, True], ids=["same_size", "ragged"])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_loss_masks_repeated_outputs_match_reference(ragged, dt):
+    """The final and auxiliary outputs call loss_masks with the same labels and different
+    matches: the cached target rows (same-size images) or the reference's padded batch (ragged
+    sizes), the sort-free matched-row gather and its gradient, each call against HF's."""
+    from transformers import Mask2FormerConfig
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerLoss
+    cfg = Mask2FormerConfig(num_labels=48)
+    wd = {"loss_cross_entropy": 2.0, "loss_mask": 5.0, "loss_dice": 5.0}
+    ref_loss, hip_loss = Mask2FormerLoss(cfg, weight_dict=wd), Mask2FormerLoss(cfg, weight_dict=wd)
+    hip_loss.__class__ = point_loss.HipMask2FormerLoss
+    masks, classes, ml, cl = _case(4, B=2, counts=(6, 9))
+    if ragged:
+        ml[1] = ml[1][:, :200, :300].contiguous()
+    masks = masks.to(dt)
+    for call in range(3):
+        g = torch.Generator(device=DEV).manual_seed(30 + call)
+        indices = [(torch.randperm(100, generator=g, device=DEV)[:n], torch.randperm(n, generator=g, device=DEV))
+                   for n in (6, 9)]
+        mr = masks.clone().requires_grad_(True)
+        mh = masks.clone().requires_grad_(True)
+        # bf16 logits as the model produces them: under autocast (grid_sample runs in float32)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dt == torch.bfloat16):
+            torch.manual_seed(40 + call)
+            r = ref_loss.loss_masks(mr, ml, indices, num_masks=15.0)
+            torch.manual_seed(40 + call)
+            h = hip_loss.loss_masks(mh, ml, indices, num_masks=15.0)
+        for k in ("loss_mask", "loss_dice"):
+            assert abs(float(h[k]) - float(r[k])) <= 1e-5 * abs(float(r[k])) + 1e-7, (call, k, float(h[k]), float(r[k]))
+        (r["loss_mask"] * 5 + r["loss_dice"] * 5).backward()
+        (h["loss_mask"] * 5 + h["loss_dice"] * 5).backward()
+        assert mh.grad.dtype == dt
+        assert _rel(mh.grad.float(), mr.grad.float()) <= (1e-4 if dt == torch.float32 else 1e-2), call
+
+
 def test_install_swaps_loss_and_matcher():
     from transformers import Mask2FormerConfig
     from transformers.models.mask2former.modeling_mask2former import Mask2FormerLoss

@@ -1,0 +1,35 @@
+"""ops.device_const / ops.host_constants: the per-step host numbers (level shapes, per-image
+offsets, instance counts) are copied to the device once per distinct value and shared."""
+import pytest
+import torch
+
+from rgbd_amd import ops
+
+
+def test_device_const_is_shared_per_value_and_dtype():
+    a = ops.device_const([[80, 60], [40, 30]], torch.long, "cpu")
+    b = ops.device_const([[80, 60], [40, 30]], torch.long, "cpu")
+    c = ops.device_const([[80, 60], [40, 30]], torch.int32, "cpu")
+    d = ops.device_const(((80, 60), (40, 31)), torch.long, "cpu")
+    assert a is b and a is not c and a is not d
+    assert a.tolist() == [[80, 60], [40, 30]] and c.dtype == torch.int32
+
+
+def test_device_const_rejects_non_numbers():
+    with pytest.raises(TypeError):
+        ops.device_const(["a"], torch.long, "cpu")
+
+
+def test_host_constants_patch_is_scoped():
+    orig = torch.as_tensor
+    with ops.host_constants():
+        assert torch.as_tensor is not orig
+        # not a device constant: CPU targets and tensors go to torch unchanged
+        assert torch.as_tensor([1, 2], device="cpu").tolist() == [1, 2]
+        t = torch.ones(2)
+        assert torch.as_tensor(t) is t
+    assert torch.as_tensor is orig
+    with pytest.raises(ValueError):
+        with ops.host_constants():
+            raise ValueError("restored on error too")
+    assert torch.as_tensor is orig

@@ -40,12 +40,15 @@ def main():
         refs.append(torch.stack([(xs.reshape(-1) + 0.5) / W, (ys.reshape(-1) + 0.5) / H], -1))
     ref = torch.cat(refs)
     norm = torch.tensor([[w, h] for h, w in shapes], device=dev, dtype=torch.float32)
-    off = torch.randn((B, S, NH, 3, P, 2), generator=g, device=dev) * 2.0
+    if "--const-offsets" in sys.argv:  # the MSDeformAttn initialisation: one offset per (head, level, point)
+        off = (torch.randn((1, 1, NH, 3, P, 2), generator=g, device=dev) * 2.0).expand(B, S, NH, 3, P, 2)
+    else:
+        off = torch.randn((B, S, NH, 3, P, 2), generator=g, device=dev) * 2.0
     loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).requires_grad_(True)
     attw = torch.softmax(torch.randn((B, S, NH, 3 * P), generator=g, device=dev), -1).view(B, S, NH, 3, P)
     attw.requires_grad_(True)
     go = torch.randn((B, S, NH * D), generator=g, device=dev)
-    res = {}
+    res = {"offsets": "const" if "--const-offsets" in sys.argv else "random"}
     for name, fn in (("hip", deform_attn.multi_scale_deformable_attention), ("hf_grid_sample", hf)):
         with torch.no_grad():
             res[name + "_fwd_us"] = t_us(lambda: fn(value, shapes, loc, attw))
