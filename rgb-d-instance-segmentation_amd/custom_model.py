@@ -108,7 +108,7 @@ class CustomMask2FormerPixelLevelModule(Mask2FormerPixelLevelModule):
             # (custom_model.py:715-717).  The decomposition status was copied to the host behind
             # the decomposition; waiting for it here lets the DSAM / DGGM / pixel-decoder kernels
             # already enqueued keep the GPU busy.
-            if torch.cuda.is_current_stream_capturing():
+            if ops.capturing():
                 # a captured step: the statuses are read after each replay (check_statuses())
                 self.captured_statuses = statuses
             else:

@@ -71,6 +71,11 @@ def _workspace(dev, nbytes: int, tag: str, zeroed: bool = False):
 _consts = {}
 
 
+def capturing() -> bool:
+    """True while the current stream is being captured into a graph (False without a GPU)."""
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 def _freeze(v):
     if isinstance(v, (list, tuple)):
         return tuple(_freeze(x) for x in v)
@@ -88,7 +93,7 @@ def device_const(values, dtype, device):
     key = (_freeze(values), dtype, device)
     t = _consts.get(key)
     if t is None:
-        if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        if device.type == "cuda" and capturing():
             raise RuntimeError("device_const: a new constant during graph capture (run the step eagerly first)")
         t = torch.tensor(values, dtype=dtype).to(device)
         _consts[key] = t
@@ -267,7 +272,7 @@ class DeferredStatus:
 
     def __init__(self, info: torch.Tensor):
         st = info.view(torch.int32)[:, 0]  # rgbd_decomp_info.status, the record's first word
-        self.captured = torch.cuda.is_current_stream_capturing()
+        self.captured = capturing()
         if self.captured:
             # the graph's copy node writes this buffer on every replay: one per shape, kept alive
             key = (info.device, tuple(st.shape))
