@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad(const T* __restrict__ gout, 
 
 // bf16 dW, code-merged:
 //   dW_k[o][tap][c] = sum over output px p with code(src(p, tap)) == k of G[p][o] X[src][c]
-// for every region code k present, folded by k_dsam_wgrad_combine into the five filters (conv_i
+// for every region code k present, folded by k_dsam_wgrad_fold into the five filters (conv_i
 // gets the codes with bit i, proj gets all): work ~ one dense dW instead of popcount + 1 of them.
 // A unit is 64 raster-consecutive output pixels of one image.  Load balance: one code (the
 // remainder region) typically meets every unit while the others meet a few percent, so
@@ -980,9 +980,7 @@ __global__ __launch_bounds__(256) void k_dsam_wgrad_mm(const WgMulti<NL> L) {
 }
 
 // dW_k (per item partials) -> the reference filters, fixed summation order (items in list
-// order: codes ascending, units ascending).  One block per output channel o: the five sums of
-// the row are formed in (tap, c) order with every item's load of a thread in flight together,
-// parked in LDS, then written in the OIHW (c, tap) order.
+// order: codes ascending, units ascending).
 struct CombArgs {
   const float* partial;
   const int4* items;
@@ -995,27 +993,26 @@ struct CombArgs {
   int B, nsplit;
   float* dbias;
 };
-__device__ __forceinline__ void combine_body(const CombArgs& A, int o, float* srow, int* scode) {
+// One block per (output channel o, 32-channel chunk of the input): 72 threads each own four
+// consecutive kk of one tap and walk the items in list order (the summation order of the former
+// one-block-per-row combine, so the same bits), the chunk's five [9 tap][32 c] rows are parked in LDS (5.6 KB) and written back as five
+// contiguous (c, tap) runs of 288 floats.  A block is small, so many are resident per CU and the
+// partial reads stream at HBM speed (the per-row form needs 5 x 9 Cin floats of LDS per block:
+// two blocks per CU).  Blocks of chunk 0 also write o's bias gradients.  grid (Cin / 32, Cout, legs).
+constexpr int FOLD_C = 32, FOLD_T = 128;
+__device__ __forceinline__ void fold_body(const CombArgs& A, int o, int c0, float (*srow)[9 * FOLD_C]) {
   const float* __restrict__ partial = A.partial;
   const int4* __restrict__ items = A.items;
-  const int Cin = A.Cin, Cout = A.Cout, B = A.B, nsplit = A.nsplit;
-  float* __restrict__ dconv_w = A.dconv_w;
-  float* __restrict__ dproj_w = A.dproj_w;
-  const float* __restrict__ csum = A.csum;
-  const rgbd_decomp_info* info = A.info;
-  float* __restrict__ dbias = A.dbias;
-  const int KK = 9 * Cin, ni = A.counts[1];
-  for (int it = threadIdx.x; it < ni && it < 1024; it += 256) scode[it] = items[it].x;
-  __syncthreads();
-  // 4 consecutive kk per thread (16-byte loads), 8 items' loads in flight per iteration
-  for (int k4 = 4 * threadIdx.x; k4 < KK; k4 += 1024) {
-    float4 seg[4], pr;
+  const int Cin = A.Cin, Cout = A.Cout, KK = 9 * Cin, ni = A.counts[1];
+  const int t = threadIdx.x;
+  if (t < 9 * FOLD_C / 4) {
+    const int tap = t / (FOLD_C / 4), q = t % (FOLD_C / 4);
+    const long long kk = (long long)tap * Cin + c0 + 4 * q;
+    const float* src = partial + (long long)o * KK + kk;
+    const long long istr = (long long)Cout * KK;
+    float4 seg[4], pr = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < 4; ++i) seg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    pr = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* src = partial + (long long)o * KK + k4;
-    const long long istr = (long long)Cout * KK;
-    int it = 0;
     auto acc = [&](const float4 v, int k) {
       pr.x += v.x; pr.y += v.y; pr.z += v.z; pr.w += v.w;
 #pragma unroll
@@ -1024,51 +1021,54 @@ __device__ __forceinline__ void combine_body(const CombArgs& A, int o, float* sr
           seg[i].x += v.x; seg[i].y += v.y; seg[i].z += v.z; seg[i].w += v.w;
         }
     };
+    int it = 0;
     for (; it + 8 <= ni; it += 8) {
       float4 v[8];
+      int k[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(src + (it + q) * istr);
+      for (int j = 0; j < 8; ++j) {
+        v[j] = *reinterpret_cast<const float4*>(src + (it + j) * istr);
+        k[j] = items[it + j].x;
+      }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc(v[q], it + q < 1024 ? scode[it + q] : items[it + q].x);
+      for (int j = 0; j < 8; ++j) acc(v[j], k[j]);
     }
-    for (; it < ni; ++it) acc(*reinterpret_cast<const float4*>(src + it * istr), it < 1024 ? scode[it] : items[it].x);
+    for (; it < ni; ++it) acc(*reinterpret_cast<const float4*>(src + it * istr), items[it].x);
+    const int r = tap * FOLD_C + 4 * q;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(srow + i * KK + k4) = seg[i];
-    *reinterpret_cast<float4*>(srow + 4 * KK + k4) = pr;
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&srow[i][r]) = seg[i];
+    *reinterpret_cast<float4*>(&srow[4][r]) = pr;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < KK; e += 256) {  // e = c*9 + tap (OIHW order)
-    const int c = e / 9, tap = e % 9, kk = tap * Cin + c;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dconv_w[((long long)i * Cout + o) * KK + e] = srow[i * KK + kk];
-    dproj_w[(long long)o * KK + e] = srow[4 * KK + kk];
+  // OIHW: element (o, c0 + c, tap) at o * KK + (c0 + c) * 9 + tap — a contiguous run per filter
+  for (int e = t; e < 5 * 9 * FOLD_C; e += FOLD_T) {
+    const int i = e / (9 * FOLD_C), f = e % (9 * FOLD_C), c = f / 9, tap = f % 9;
+    const float v = srow[i][tap * FOLD_C + c];
+    if (i < 4)
+      A.dconv_w[((long long)i * Cout + o) * KK + (long long)c0 * 9 + f] = v;
+    else
+      A.dproj_w[(long long)o * KK + (long long)c0 * 9 + f] = v;
   }
-  // the biases' gradients of o (csum [nsplit][B][Cout]; conv_layers[i] only where i < len(masks)),
-  // wave i in k_dsam_bias_grad's fixed order
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (dbias && wv < 4) {
-    float sb = 0.f;
-    for (int q = lane; q < nsplit * B; q += 64) {
-      const int b = q % B;
-      if (wv < info[b].n_masks) sb += csum[(long long)q * Cout + o];
+  // o's bias gradients (csum [nsplit][B][Cout]; conv_layers[i] only where i < len(masks)): the
+  // former combine's wave sums, waves 0 / 1 taking i = 0, 2 / 1, 3
+  if (c0 == 0 && A.dbias) {
+    const int wv = t >> 6, lane = t & 63;
+    for (int i = wv; i < 4; i += FOLD_T / 64) {
+      float sb = 0.f;
+      for (int q = lane; q < A.nsplit * A.B; q += 64) {
+        const int b = q % A.B;
+        if (i < A.info[b].n_masks) sb += A.csum[(long long)q * Cout + o];
+      }
+      sb = wave_sum(sb);
+      if (lane == 0) A.dbias[i * Cout + o] = sb;
     }
-    sb = wave_sum(sb);
-    if (lane == 0) dbias[wv * Cout + o] = sb;
   }
 }
-__global__ __launch_bounds__(256) void k_dsam_wgrad_combine(const CombArgs A) {
-  extern __shared__ float srow[];  // [5][9*Cin]
-  __shared__ int scode[1024];      // item -> code, staged once
-  combine_body(A, blockIdx.x, srow, scode);
-}
-// the combines of two legs in one launch: blocks [0, Cout0) leg 0, then leg 1
-__global__ __launch_bounds__(256) void k_dsam_wgrad_combine2(const CombArgs A0, const CombArgs A1) {
-  extern __shared__ float srow[];
-  __shared__ int scode[1024];
-  if ((int)blockIdx.x < A0.Cout)
-    combine_body(A0, blockIdx.x, srow, scode);
-  else
-    combine_body(A1, blockIdx.x - A0.Cout, srow, scode);
+__global__ __launch_bounds__(FOLD_T) void k_dsam_wgrad_fold(const CombArgs A0, const CombArgs A1) {
+  __shared__ __attribute__((aligned(16))) float srow[5][9 * FOLD_C];
+  const CombArgs& A = blockIdx.z == 0 ? A0 : A1;
+  if ((int)blockIdx.y >= A.Cout || (int)blockIdx.x * FOLD_C >= A.Cin) return;  // block-uniform
+  fold_body(A, blockIdx.y, blockIdx.x * FOLD_C, srow);
 }
 
 __global__ void k_dsam_wgrad_final(const float* __restrict__ partial, int splits, int Cin, int Cout,
@@ -2454,7 +2454,6 @@ size_t rgbd_dsam_bwd_weight_workspace_size(int dtype, int B, int Cin, int h, int
   return wgrad_ws(dtype, B, Cin, h, w, Cout).total;
 }
 
-constexpr int kCombineDyn = 163840 - 1024 * 4;  // the combine's static item -> code table
 static CombArgs comb_args(const WgArgs& a, bool nchw_sums, const float* csum, const rgbd_decomp_info* info,
                           float* dconv_w, float* dproj_w, float* dbias) {
   CombArgs c;
@@ -2482,13 +2481,9 @@ static int wg_finish(const WgArgs& a, const void* gout_nchw, float* csum, const 
     k_chan_sum<bf16_t><<<a.B * a.Cout, 256, 0, s>>>((const bf16_t*)gout_nchw, hwo, csum);
   else if (!sums_folded)
     k_chan_sum_nhwc<<<dim3(a.B, ceil_div(a.Cout, 64), chan_sum_splits(hwo)), 256, 0, s>>>(a.gout, hwo, a.Cout, csum);
-  const int csmem = 5 * 9 * a.Cin * (int)sizeof(float);
-  static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
-  if (cattr != hipSuccess) return (int)cattr;
-  RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
-  k_dsam_wgrad_combine<<<a.Cout, 256, csmem, s>>>(comb_args(a, gout_nchw != nullptr, csum, info, dconv_w, dproj_w,
-                                                            dbias));
+  RGBD_REQUIRE(a.Cin % FOLD_C == 0, RGBD_E_SHAPE);
+  const CombArgs c = comb_args(a, gout_nchw != nullptr, csum, info, dconv_w, dproj_w, dbias);
+  k_dsam_wgrad_fold<<<dim3(a.Cin / FOLD_C, a.Cout, 1), FOLD_T, 0, s>>>(c, c);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -2595,16 +2590,13 @@ int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, cons
   if (e != hipSuccess) return (int)e;
   if (n == 1)  // the bias sums were drained by the GEMM's workgroups (fold)
     return wg_finish(m.a[0], nullptr, m.csum[0], info, runs[0].dconv_w, runs[0].dproj_w, runs[0].dbias, s, true);
-  // both legs' combines in one launch
-  const int csmem = 5 * 9 * std::max(runs[0].Cin, runs[1].Cin) * (int)sizeof(float);
-  static const hipError_t cattr = hipFuncSetAttribute((const void*)k_dsam_wgrad_combine2,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kCombineDyn);
-  if (cattr != hipSuccess) return (int)cattr;
-  RGBD_REQUIRE(csmem <= kCombineDyn, RGBD_E_SHAPE);
+  // both legs' folds in one launch
+  RGBD_REQUIRE(runs[0].Cin % FOLD_C == 0 && runs[1].Cin % FOLD_C == 0, RGBD_E_SHAPE);
   CombArgs c[2];
   for (int i = 0; i < 2; ++i)
     c[i] = comb_args(m.a[i], false, m.csum[i], info, runs[i].dconv_w, runs[i].dproj_w, runs[i].dbias);
-  k_dsam_wgrad_combine2<<<runs[0].Cout + runs[1].Cout, 256, csmem, s>>>(c[0], c[1]);
+  k_dsam_wgrad_fold<<<dim3(std::max(runs[0].Cin, runs[1].Cin) / FOLD_C, std::max(runs[0].Cout, runs[1].Cout), 2),
+                      FOLD_T, 0, s>>>(c[0], c[1]);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
