@@ -488,6 +488,161 @@ __global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int row
   if (threadIdx.x == 0) tickets[blockIdx.x] = 0;  // rearmed for the next call on this workspace
 }
 
+// ---- bf16, both operands K-contiguous (forward: X [M][K] W [N][K]; dX with the weight's
+// cached transpose), batch 1, no split: the conv5 recipe (ratio.hip k_rp_conv3x3_v3) on a plain
+// GEMM.  512 threads = 8 waves as 2 (M) x 4 (N), wave tile (TM/2) x (TN/4); K staged 64 at a
+// time (128-byte rows, 16-byte chunk c at slot c ^ (row & 7)) by LDS-DMA straight from global
+// memory (global_load_lds_dwordx4: no VGPR staging, no ds_write) into a 3-stage ring issued two
+// stages ahead, one barrier per stage; rows past M / N and chunks past K read a zero line.  The
+// blockIdx -> tile map keeps the N tiles of one M tile on one XCD (workgroup i runs on XCD
+// i % 8), so X is fetched from HBM once and re-read from that XCD's L2.  Epilogue: the
+// accumulator tile through LDS, 16-byte row stores with bias / act / residual / ReLU-mask.
+__device__ uint4 g_zero_line[4];  // 64 zero bytes (never written)
+
+__device__ __forceinline__ void gl_dma16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_base)
+               : "memory");
+}
+
+constexpr int GL_THREADS = 512, GL_S = 3;
+template <int TM, int TN>
+struct GlCfg {
+  static constexpr int FM = TM / 32, FN = TN / 64;  // fragments per wave: 2 (M) x 4 (N) waves
+  static constexpr int A_BYTES = TM * 128, B_BYTES = TN * 128, STAGE = A_BYTES + B_BYTES;
+  static constexpr int PIECES = STAGE / 1024, PER_WAVE = PIECES / 8;
+  static constexpr int SMEM = GL_S * STAGE > TM * TN * 4 ? GL_S * STAGE : TM * TN * 4;
+  static_assert(PIECES % 8 == 0 && SMEM <= 163840, "LDS-DMA GEMM tile");
+};
+
+template <int TM, int TN>
+__global__ __launch_bounds__(GL_THREADS) void k_gemm_lds(GArgs a) {
+  using C = GlCfg<TM, TN>;
+  constexpr int FM = C::FM, FN = C::FN;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  // tile of this workgroup: XCD-major over consecutive tiles (n fastest)
+  const int ntn = (a.N + TN - 1) / TN;
+  const int T = ntn * ((a.M + TM - 1) / TM), full = T / 8 * 8;
+  const int bid = blockIdx.x;
+  const int t = bid < full ? (bid % 8) * (full / 8) + bid / 8 : bid;
+  const int m_base = (t / ntn) * TM, n_base = (t % ntn) * TN;
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(a.A);
+  const bf16_t* B = reinterpret_cast<const bf16_t*>(a.B);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const int nk = (a.K + 63) / 64;
+
+  // piece p of a stage: 8 rows of A (p < TM / 8) or of B; lane -> row p*8 + lane/8, slot lane%8
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * 64;
+#pragma unroll
+    for (int u = 0; u < C::PER_WAVE; ++u) {
+      const int p = wave * C::PER_WAVE + u;
+      const bool is_a = p < TM / 8;
+      const int row = (is_a ? p : p - TM / 8) * 8 + (lane >> 3);
+      const int q = (lane & 7) ^ (row & 7);
+      const int gr = (is_a ? m_base : n_base) + row, k = k0 + 8 * q;
+      const void* src = g_zero_line;
+      if (gr < (is_a ? a.M : a.N) && k < a.K)
+        src = is_a ? (const void*)(A + (long long)gr * a.lda + k) : (const void*)(B + (long long)gr * a.ldb + k);
+      gl_dma16(src, lds0 + buf * C::STAGE + p * 1024);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  if (nk > 1) {
+    if constexpr (C::PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 2 < nk;
+    if (more) issue(kt + 2, (kt + 2) % GL_S);
+    const char* sa = smem + (kt % GL_S) * C::STAGE;
+    const char* sb = sa + C::A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      Frag<bf16_t> fm[FM], fn[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fm[i] = frag_k(sa, wm * FM + i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fn[j] = frag_k(sb, wn * FN + j, ks, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i) mma(acc[j][i], fn[j], fm[i]);
+    }
+    // the next stage landed (this wave's pieces; the barrier covers the others'), reads done
+    if (more) {
+      if constexpr (C::PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+
+  // epilogue as k_gemm's: lane (r, g): acc[j][i][e] = C[m = 16 (wm FM + i) + r][n = 16 (wn FN + j) + 4 g + e]
+  {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int ml = 16 * (wm * FM + i) + r, ch = 4 * (wn * FN + j) + g;
+        *reinterpret_cast<f32x4*>(smem + coff<TN>(ml, ch)) = acc[j][i];
+      }
+  }
+  __syncthreads();
+  const bool vec_c = (a.N % 8 == 0) && (((uintptr_t)a.C) % 16 == 0) && (a.ldc % 8 == 0) &&
+                     (!a.R || (a.ldr % 8 == 0 && ((uintptr_t)a.R) % 16 == 0));
+  constexpr int TPR = TN / 8, RPP = GL_THREADS / TPR;
+  const int nl = (tid % TPR) * 8;
+#pragma unroll 1
+  for (int ml = tid / TPR; ml < TM; ml += RPP) {
+    const int m = m_base + ml, n0 = n_base + nl;
+    if (m >= a.M || n0 >= a.N) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4));
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4 + 1));
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    g_store8<bf16_t>(a, 0, 0, m, n0, v, vec_c);
+  }
+}
+
+template <int TM, int TN>
+int launch_lds(const GArgs& a, hipStream_t s) {
+  using C = GlCfg<TM, TN>;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)k_gemm_lds<TM, TN>, hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+  if (attr != hipSuccess) return (int)attr;
+  const int T = ceil_div(a.N, TN) * ceil_div(a.M, TM);
+  k_gemm_lds<TM, TN><<<T, GL_THREADS, C::SMEM, s>>>(a);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+// RGBD_GEMM_LDS=0 keeps every bf16 GEMM on k_gemm (A/B); read once
+inline bool gemm_lds_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RGBD_GEMM_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <typename T, int TM, int TN, bool AT, bool BT>
 void launch_t(const GArgs& a, int batch, hipStream_t s) {
   dim3 grid(ceil_div(a.N, TN), ceil_div(a.M, TM), batch * a.splits);
@@ -507,6 +662,12 @@ void launch_layout(const GArgs& a, int at, int bt, int batch, hipStream_t s) {
 
 template <typename T>
 int gemm_t(GArgs a, int at, int bt, int batch, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    // the LDS-DMA kernel: bf16, both operands K-contiguous and 16-byte aligned, one GEMM, no split
+    if (!at && !bt && batch == 1 && a.splits == 1 && a.vec_a && a.vec_b && a.K % 8 == 0 && !a.bias_m &&
+        a.M >= 1024 && gemm_lds_enabled())
+      return a.N % 256 == 0 ? launch_lds<128, 256>(a, s) : launch_lds<128, 128>(a, s);
+  }
   // 128 x 128 tiles when they give the chip enough workgroups, else 64 x 64
   const long long big = (long long)ceil_div(a.N, 128) * ceil_div(a.M, 128) * batch * a.splits;
   if (big >= 256)

@@ -133,6 +133,15 @@ def _rows(x, dt):
     return x2.contiguous()
 
 
+def _dx(g2, wc, M, K, N, act=ACT_NONE, R=None):
+    """dX [M][K] = dY [M][N] W [N][K].  bf16 with many rows: W transposed once (a [K][N] copy,
+    0.1-2 MB) so both operands are K-contiguous and the GEMM takes the LDS-DMA kernel
+    (csrc/gemm.hip k_gemm_lds); otherwise the transposed-operand layout (0, 1)."""
+    if g2.dtype == torch.bfloat16 and M >= 1024 and K % 8 == 0 and N % 8 == 0:
+        return gemm(g2, wc.t().contiguous(), 0, 0, M, K, N, act=act, R=R)
+    return gemm(g2, wc, 0, 1, M, K, N, act=act, R=R)
+
+
 class LinearFunction(torch.autograd.Function):
     """y = act(x W^T + b), act none / relu / gelu (gelu: forward only)."""
 
@@ -158,7 +167,7 @@ class LinearFunction(torch.autograd.Function):
             g2 = g2 * (y > 0)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = gemm(g2, wc, 0, 1, M, K, N).to(ctx.x_dtype).view(*gy.shape[:-1], K)
+            dx = _dx(g2, wc, M, K, N).to(ctx.x_dtype).view(*gy.shape[:-1], K)
         if ctx.needs_input_grad[1]:
             dw = gemm(g2, x2, 1, 1, N, K, M, c_f32=True).to(ctx.w_dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
@@ -188,10 +197,10 @@ class FFNFunction(torch.autograd.Function):
         M, K = x2.shape
         F_, N = h.shape[1], w2c.shape[0]
         g2 = _rows(gy, x2.dtype)
-        dh = gemm(g2, w2c, 0, 1, M, F_, N, act=ACT_RELU_GRAD, R=h)
+        dh = _dx(g2, w2c, M, F_, N, act=ACT_RELU_GRAD, R=h)
         dw2 = gemm(g2, h, 1, 1, N, F_, M, c_f32=True).to(ctx.w_dtypes[1])
         db2 = colsum(g2)
-        dx = gemm(dh, w1c, 0, 1, M, K, F_).to(ctx.x_dtype).view(*gy.shape[:-1], K)
+        dx = _dx(dh, w1c, M, K, F_).to(ctx.x_dtype).view(*gy.shape[:-1], K)
         dw1 = gemm(dh, x2, 1, 1, F_, K, M, c_f32=True).to(ctx.w_dtypes[0])
         db1 = colsum(dh)
         return dx, dw1, db1, dw2, db2, None

@@ -80,6 +80,27 @@ def test_gemm_epilogues(dt, act):
     assert _rel(C, ref) < tol * (3 if act == 2 else 1)
 
 
+@pytest.mark.parametrize("M,N,K", [(50400, 256, 1024), (50400, 1024, 256), (4000, 384, 96), (2000, 200, 96),
+                                   (1500, 100, 72), (1029, 264, 200)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3], ids=["none", "relu", "gelu", "relu_grad"])
+def test_gemm_lds_dma_path(M, N, K, act):
+    """bf16, both operands K-contiguous, M >= 1024: the LDS-DMA kernel (k_gemm_lds; 128 x 256 tiles
+    when N % 256 == 0, else 128 x 128), ragged M / N / K (K % 64 != 0: zero lines past K; N % 8
+    != 0: scalar stores), every epilogue, against float64 on the same bf16 operands."""
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + act)
+    A = torch.randn((M, K), generator=g).to(DEV, torch.bfloat16)
+    B = torch.randn((N, K), generator=g).to(DEV, torch.bfloat16)
+    bias = None if act == 3 else torch.randn((N,), generator=g).to(DEV)
+    R = torch.randn((M, N), generator=g).to(DEV, torch.bfloat16) if act in (0, 3) else None
+    C = dense.gemm(A, B, 0, 0, M, N, K, bias=bias, act=act, R=R)
+    ref = _ref(A, B, 0, 0, bias, act, R)
+    assert C.shape == (M, N) and C.dtype == torch.bfloat16
+    assert _rel(C, ref) < BF16_TOL * (3 if act == 2 else 1)
+    Cf = dense.gemm(A, B, 0, 0, M, N, K, bias=bias, act=act, R=None if R is None else R.float(), c_f32=True)
+    assert Cf.dtype == torch.float32 and _rel(Cf, ref) < 2e-5 * (3 if act == 2 else 1) * K ** 0.5
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
 def test_gemm_split_k_weight_gradient(dt):
     """dW = dY^T X with a long reduction (50 400 pixel-decoder tokens) and a small output: the

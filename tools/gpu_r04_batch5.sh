@@ -9,6 +9,10 @@ for runs in 0 1; do for off in "" "--const-offsets"; do
   RGBD_MSDA_RUNS=$runs timeout -k 10 120 python tools/micro_msda.py $off > $O/msda_${runs}${off}.json 2>&1 || { tail -5 $O/msda_${runs}${off}.json; exit 1; }
   echo "runs=$runs $off: $(tail -1 $O/msda_${runs}${off}.json)"
 done; done
+for lds in 0 1; do
+  RGBD_GEMM_LDS=$lds timeout -k 10 180 python tools/micro_gemm.py > $O/micro_gemm_lds$lds.jsonl 2>&1 || { tail -5 $O/micro_gemm_lds$lds.jsonl; exit 1; }
+done
+cat $O/micro_gemm_lds1.jsonl
 bash tools/gpu_r04.sh bench --full-model 0 || exit 1
 bash tools/gpu_r04.sh prof || exit 1
 timeout -k 10 600 python tools/run_full_model.py > $O/full_model.json 2> $O/full_model.err || { tail -20 $O/full_model.err; exit 1; }

@@ -41,6 +41,8 @@ for name, M, K, N in SHAPES:
     cases = {
         "fwd": (lambda: dense.gemm(x, w, 0, 0, M, N, K), lambda: x @ w.t(), (M * K + N * K + M * N) * 2),
         "dX": (lambda: dense.gemm(gy, w, 0, 1, M, K, N), lambda: gy @ w, (M * N + N * K + M * K) * 2),
+        # dX as the backward now runs it: the weight transposed (included), then the (0, 0) layout
+        "dX_t": (lambda: dense._dx(gy, w, M, K, N), lambda: gy @ w, (M * N + N * K + M * K) * 2),
         "dW": (lambda: dense.gemm(gy, x, 1, 1, N, K, M, c_f32=True), lambda: gy.t() @ x,
                (M * N + M * K) * 2 + N * K * 4),
     }
