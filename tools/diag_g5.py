@@ -7,6 +7,12 @@ from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
 g5 = np.load('tests/golden/g5_model.npz')
 m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
 winit.init_deterministic(m)
+import os
+if os.environ.get("RGBD_DIAG_NOCONV") == "1":  # the f2 convolutions back on torch (A/B)
+    from rgbd_amd.conv import HipConv2d
+    for mod in m.modules():
+        if type(mod) is HipConv2d:
+            mod.__class__ = torch.nn.Conv2d
 m = m.cuda().eval()
 plm = m.model.pixel_level_module
 caps = {}
