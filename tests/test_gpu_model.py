@@ -224,12 +224,50 @@ def test_full_model_mask_logits_fp32(golden):
         d = attn_g != attn_ref
         flips += int(d.sum())
         explained &= bool((val[d].abs() < 1e-3).all())
-    print(f"mask-logit max-abs-err (fp32): hot path {err:.3g}; everything on the GPU {gpu:.3g} "
-          f"({flips} near-threshold attention-mask flips)")
-    assert err <= 1e-3
+    # The same count for the hot-path run against the reference's own attention masks (the
+    # oracle CPU model, pinned to G5 by test_oracle_full_model_matches_g5): backbone features a
+    # few 1e-6 from the reference's (the Swin-T and hot-path arithmetic on the GPU) can move a
+    # mask logit sitting within that distance of 0 across the binarisation threshold too.
+    ocalls = _oracle_mask_calls(pv_cpu)
+    assert len(ocalls) == len(calls)
+    rflips, rexplained = 0, True
+    for ((_, _, size), (mask_ref, attn_ref)), (mask_o, attn_o) in zip(calls, ocalls):
+        val = torch.nn.functional.interpolate(mask_o, size=size, mode="bilinear", align_corners=False).flatten(2)
+        val = val.unsqueeze(1).expand(-1, hip_pred.num_heads, -1, -1).flatten(0, 1)
+        d = attn_ref != attn_o
+        rflips += int(d.sum())
+        rexplained &= bool((val[d].abs() < 1e-3).all())
+    print(f"mask-logit max-abs-err (fp32): hot path {err:.3g} ({rflips} near-threshold flips against the "
+          f"reference's masks); everything on the GPU {gpu:.3g} ({flips} near-threshold attention-mask flips)")
+    assert rexplained, "an attention-mask bit of the hot-path run flipped away from the threshold"
     assert explained, "an attention-mask bit flipped away from the threshold"
-    assert gpu <= (1e-3 if flips == 0 else 1e-2)
-    np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-3)
+    assert err <= (1e-3 if rflips == 0 else 1e-2)
+    assert gpu <= (1e-3 if flips == 0 and rflips == 0 else 1e-2)
+    np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-3 if rflips == 0 else 1e-2)
+
+
+def _oracle_mask_calls(pv_cpu):
+    """(mask logits, attention mask) of every mask-predictor call of the reference computation:
+    the drop-in model on the CPU with the HF modules and the oracle hot path (as
+    tests/test_oracle_model.py runs it)."""
+    from oracle import hot_path as hot_o
+    mo = _full_model().cpu().eval()
+    for mod in (mask_predictor, masked_attention, deform_attn):
+        mod.uninstall(mo)
+    plm = mo.model.pixel_level_module
+    sd = dict(plm.state_dict())
+    sd.update(dict(plm.named_parameters()))
+    plm.hot_path_features = lambda pv_, colors, ratios=None, **kw: hot_o.hot_path_forward(
+        list(colors), pv_, sd, training=False)[0]
+    calls = []
+    h = mo.model.transformer_module.decoder.mask_predictor.register_forward_hook(
+        lambda mod, inp, out: calls.append((out[0], out[1])))
+    try:
+        with torch.no_grad():
+            mo(pixel_values=pv_cpu)
+    finally:
+        h.remove()
+    return calls
 
 
 def test_full_model_mask_logits_bf16(golden):
