@@ -26,6 +26,7 @@ fc2's dX epilogue.  Inputs the kernels do not cover (CPU tensors, float16, Layer
 > 1536, dropout in training, GELU with gradients) take the module's own torch path.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -133,10 +134,33 @@ def _rows(x, dt):
     return x2.contiguous()
 
 
+# Plain bf16 GEMMs — no epilogue but a bias (projections, FFN fc2's forward) and the unmasked
+# dX products — go to the vendor library (hipBLASLt through torch.mm / addmm): on the drop-in
+# model's shapes it runs them 1.6-2.3x faster than csrc/gemm.hip (tools/micro_gemm.py,
+# profiles/r04_*/micro_gemm*.jsonl).  The fused epilogues (ReLU / GELU, ReLU-mask backward) and
+# every weight gradient (split-K, 2.8-3x faster than the library's) stay on csrc/gemm.hip.
+# RGBD_DENSE_LIB=0 keeps everything on csrc/gemm.hip (A/B).
+LIB_PLAIN = os.environ.get("RGBD_DENSE_LIB", "1") != "0"
+
+
+def _lib_plain(x2):
+    return LIB_PLAIN and x2.dtype == torch.bfloat16 and x2.is_cuda
+
+
+def _fwd(x2, wc, b, act, M, N, K):
+    """y [M][N] = act(x W^T + b) for a Linear layer."""
+    if act == ACT_NONE and _lib_plain(x2):
+        return torch.mm(x2, wc.t()) if b is None else torch.addmm(b.to(x2.dtype), x2, wc.t())
+    return gemm(x2, wc, 0, 0, M, N, K, bias=b, act=act)
+
+
 def _dx(g2, wc, M, K, N, act=ACT_NONE, R=None):
-    """dX [M][K] = dY [M][N] W [N][K].  bf16 with many rows: W transposed once (a [K][N] copy,
-    0.1-2 MB) so both operands are K-contiguous and the GEMM takes the LDS-DMA kernel
-    (csrc/gemm.hip k_gemm_lds); otherwise the transposed-operand layout (0, 1)."""
+    """dX [M][K] = dY [M][N] W [N][K] (act ACT_RELU_GRAD: times R > 0).  Plain bf16: the
+    library; masked bf16 with many rows: W transposed once (a [K][N] copy, 0.1-2 MB) so both
+    operands are K-contiguous for the LDS-DMA kernel (csrc/gemm.hip k_gemm_lds); otherwise the
+    transposed-operand layout (0, 1)."""
+    if act == ACT_NONE and _lib_plain(g2):
+        return torch.mm(g2, wc)
     if g2.dtype == torch.bfloat16 and M >= 1024 and K % 8 == 0 and N % 8 == 0:
         return gemm(g2, wc.t().contiguous(), 0, 0, M, K, N, act=act, R=R)
     return gemm(g2, wc, 0, 1, M, K, N, act=act, R=R)
@@ -150,7 +174,7 @@ class LinearFunction(torch.autograd.Function):
         N, K = w.shape
         x2 = _rows(x, dt)
         wc = cast_weight(w, dt)
-        y = gemm(x2, wc, 0, 0, x2.shape[0], N, K, bias=b, act=act)
+        y = _fwd(x2, wc, b, act, x2.shape[0], N, K)
         ctx.save_for_backward(x2, wc, y if act == ACT_RELU else None)
         ctx.act, ctx.x_dtype, ctx.w_dtype, ctx.has_b = act, x.dtype, w.dtype, b is not None
         return y.view(*x.shape[:-1], N)
@@ -186,7 +210,7 @@ class FFNFunction(torch.autograd.Function):
         w1c, w2c = cast_weight(w1, dt), cast_weight(w2, dt)
         M = x2.shape[0]
         h = gemm(x2, w1c, 0, 0, M, F_, K, bias=b1, act=ACT_RELU)
-        y = gemm(h, w2c, 0, 0, M, N, F_, bias=b2)
+        y = _fwd(h, w2c, b2, ACT_NONE, M, N, F_)
         ctx.save_for_backward(x2, h, w1c, w2c)
         ctx.x_dtype, ctx.w_dtypes = x.dtype, (w1.dtype, w2.dtype)
         return y.view(*x.shape[:-1], N)

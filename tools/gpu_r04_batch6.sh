@@ -1,10 +1,15 @@
 #!/bin/bash
-# Round-4 batch 6: the flip-aware fp32 model test, the capture bisection of the whole-model
-# step, and the eager whole-model step's kernel trace.
+# Round-4 batch 6: the flip-aware fp32 model test + dense / trainer tests, the capture bisection
+# of the whole-model step, the full_model block with plain GEMMs on the library vs on
+# csrc/gemm.hip, and the eager whole-model step's kernel trace.
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r04; mkdir -p $O
-TESTLOG=tests6 bash tools/gpu_r04.sh tests tests/test_gpu_model.py::test_full_model_mask_logits_fp32
+TESTLOG=tests6 bash tools/gpu_r04.sh tests tests/test_gpu_model.py tests/test_gpu_dense.py tests/test_gpu_trainer.py tests/test_gpu_layers.py
 rc=$?; [ $rc -ge 124 ] && exit $rc
 timeout -k 10 400 python tools/debug_full_capture.py > $O/capture_debug.txt 2>&1; rc=$?
-cat $O/capture_debug.txt | grep -E "OK|FAIL"; [ $rc -ge 124 ] && exit $rc
+grep -E "OK|FAIL" $O/capture_debug.txt; [ $rc -ge 124 ] && exit $rc
+for lib in 1 0; do
+  RGBD_DENSE_LIB=$lib timeout -k 10 400 python tools/run_full_model.py --no-graph > $O/full_model_lib$lib.json 2> $O/full_model_lib$lib.err || { tail -5 $O/full_model_lib$lib.err; exit 1; }
+  echo "lib=$lib"; cut -c1-400 $O/full_model_lib$lib.json
+done
 bash tools/gpu_r04.sh fullprof || exit 1
