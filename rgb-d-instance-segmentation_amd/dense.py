@@ -26,7 +26,6 @@ fc2's dX epilogue.  Inputs the kernels do not cover (CPU tensors, float16, Layer
 > 1536, dropout in training, GELU with gradients) take the module's own torch path.
 """
 import math
-import os
 
 import torch
 import torch.nn.functional as F
@@ -134,33 +133,17 @@ def _rows(x, dt):
     return x2.contiguous()
 
 
-# Plain bf16 GEMMs — no epilogue but a bias (projections, FFN fc2's forward) and the unmasked
-# dX products — go to the vendor library (hipBLASLt through torch.mm / addmm): on the drop-in
-# model's shapes it runs them 1.6-2.3x faster than csrc/gemm.hip (tools/micro_gemm.py,
-# profiles/r04_*/micro_gemm*.jsonl).  The fused epilogues (ReLU / GELU, ReLU-mask backward) and
-# every weight gradient (split-K, 2.8-3x faster than the library's) stay on csrc/gemm.hip.
-# RGBD_DENSE_LIB=0 keeps everything on csrc/gemm.hip (A/B).
-LIB_PLAIN = os.environ.get("RGBD_DENSE_LIB", "1") != "0"
-
-
-def _lib_plain(x2):
-    return LIB_PLAIN and x2.dtype == torch.bfloat16 and x2.is_cuda
-
-
 def _fwd(x2, wc, b, act, M, N, K):
-    """y [M][N] = act(x W^T + b) for a Linear layer."""
-    if act == ACT_NONE and _lib_plain(x2):
-        return torch.mm(x2, wc.t()) if b is None else torch.addmm(b.to(x2.dtype), x2, wc.t())
+    """y [M][N] = act(x W^T + b) for a Linear layer.  (Measured: the plain bf16 products on the
+    vendor library through torch.mm / addmm made the whole-model step slower, 100.0 vs
+    109.8 img/s, profiles/r04_v3/full_model_lib_ab.txt, so every product stays here.)"""
     return gemm(x2, wc, 0, 0, M, N, K, bias=b, act=act)
 
 
 def _dx(g2, wc, M, K, N, act=ACT_NONE, R=None):
-    """dX [M][K] = dY [M][N] W [N][K] (act ACT_RELU_GRAD: times R > 0).  Plain bf16: the
-    library; masked bf16 with many rows: W transposed once (a [K][N] copy, 0.1-2 MB) so both
-    operands are K-contiguous for the LDS-DMA kernel (csrc/gemm.hip k_gemm_lds); otherwise the
-    transposed-operand layout (0, 1)."""
-    if act == ACT_NONE and _lib_plain(g2):
-        return torch.mm(g2, wc)
+    """dX [M][K] = dY [M][N] W [N][K] (act ACT_RELU_GRAD: times R > 0).  bf16 with many rows: W
+    transposed once (a [K][N] copy, 0.1-2 MB) so both operands are K-contiguous for the LDS-DMA
+    kernel (csrc/gemm.hip k_gemm_lds); otherwise the transposed-operand layout (0, 1)."""
     if g2.dtype == torch.bfloat16 and M >= 1024 and K % 8 == 0 and N % 8 == 0:
         return gemm(g2, wc.t().contiguous(), 0, 0, M, K, N, act=act, R=R)
     return gemm(g2, wc, 0, 1, M, K, N, act=act, R=R)

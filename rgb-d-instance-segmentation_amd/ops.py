@@ -268,30 +268,26 @@ class DeferredStatus:
     after it keep running) and raises the reference's ValueError; the drop-in module calls it
     at the end of its forward, after the pixel decoder has been enqueued."""
 
-    _captured_hosts = {}  # (device, shape): the pinned buffer a captured graph copies into
-
     def __init__(self, info: torch.Tensor):
         st = info.view(torch.int32)[:, 0]  # rgbd_decomp_info.status, the record's first word
         self.captured = capturing()
         if self.captured:
-            # the graph's copy node writes this buffer on every replay: one per shape, kept alive
-            key = (info.device, tuple(st.shape))
-            host = DeferredStatus._captured_hosts.get(key)
-            if host is None:
-                host = DeferredStatus._captured_hosts[key] = torch.empty(st.shape, dtype=torch.int32, pin_memory=True)
-            self.host = host
-        else:
-            self.host = torch.empty(st.shape, dtype=torch.int32, pin_memory=True)
+            # inside a graph: a device copy (a pinned-host copy breaks the capture); the replay
+            # rewrites it, check() reads it back after the replay
+            self.dev = st.clone()
+            return
+        self.host = torch.empty(st.shape, dtype=torch.int32, pin_memory=True)
         self.host.copy_(st, non_blocking=True)
-        self.event = None if self.captured else torch.cuda.Event()
-        if self.event is not None:
-            self.event.record(torch.cuda.current_stream(info.device))
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(info.device))
 
     def check(self):
-        """Eager: wait for the copy and raise.  Captured: call after the replay has finished
-        (e.g. after synchronising its stream): the buffer then holds that replay's statuses."""
-        if self.event is not None:
-            self.event.synchronize()
+        """Eager: wait for the copy and raise.  Captured: call after the replay has finished;
+        reads that replay's statuses (synchronises)."""
+        if self.captured:
+            _raise_statuses(self.dev.tolist())
+            return
+        self.event.synchronize()
         _raise_statuses(self.host.tolist())
 
 
