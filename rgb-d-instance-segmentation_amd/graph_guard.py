@@ -26,18 +26,18 @@ def _hip():
 
 
 def dag_width(n, edges):
-    """Width (maximum antichain size) of a DAG with nodes 0..n-1 and ``edges`` (a, b): a before b."""
-    succ = [0] * n
-    for a, b in edges:
-        succ[a] |= 1 << b
-    # transitive closure, nodes in a topological order (Kahn)
+    """Width (maximum antichain size) of a DAG with nodes 0..n-1 and ``edges`` (a, b): a before b.
+
+    n - (maximum matching in the bipartite graph of the transitive closure).  A captured training
+    step has thousands of nodes, so the matching starts from a greedy chain cover (nodes in
+    topological order, each appended to the first chain whose tail reaches it) and is completed
+    with iterative augmenting-path searches over reachability bitsets (no recursion)."""
+    adj = [[] for _ in range(n)]
     indeg = [0] * n
     for a, b in edges:
+        adj[a].append(b)
         indeg[b] += 1
     order, ready = [], [i for i in range(n) if indeg[i] == 0]
-    adj = [[] for _ in range(n)]
-    for a, b in edges:
-        adj[a].append(b)
     while ready:
         v = ready.pop()
         order.append(v)
@@ -47,30 +47,51 @@ def dag_width(n, edges):
                 ready.append(w)
     if len(order) != n:
         raise ValueError("graph has a cycle")
-    reach = [0] * n
+    reach = [0] * n  # descendants of v as a bitset
     for v in reversed(order):
-        r = succ[v]
+        r = 0
         for w in adj[v]:
-            r |= reach[w]
+            r |= reach[w] | (1 << w)
         reach[v] = r
-    # maximum bipartite matching (left v -> right w if v reaches w), Kuhn's algorithm
-    match_r = [-1] * n
+    match_l, match_r = [-1] * n, [-1] * n  # left v -> right w (v before w on one chain)
+    tails = []
+    for v in order:
+        for i, t in enumerate(tails):
+            if (reach[t] >> v) & 1:
+                match_l[t], match_r[v] = v, t
+                tails[i] = v
+                break
+        else:
+            tails.append(v)
 
-    def augment(v, seen):
-        r = reach[v]
-        while r:
+    def augment(u):
+        seen, parent = 0, {}
+        stack = [[u, reach[u]]]
+        while stack:
+            top = stack[-1]
+            r = top[1] & ~seen
+            if not r:
+                stack.pop()
+                continue
             low = r & -r
             w = low.bit_length() - 1
-            r ^= low
-            if seen[w]:
-                continue
-            seen[w] = True
-            if match_r[w] < 0 or augment(match_r[w], seen):
-                match_r[w] = v
-                return True
+            top[1] = r ^ low
+            seen |= low
+            parent[w] = top[0]
+            if match_r[w] < 0:
+                while True:  # flip the alternating path back to u
+                    v = parent[w]
+                    prev = match_l[v]
+                    match_l[v], match_r[w] = w, v
+                    if v == u:
+                        return True
+                    w = prev
+            stack.append([match_r[w], reach[match_r[w]]])
         return False
-    matched = sum(1 for v in range(n) if augment(v, [False] * n))
-    return n - matched
+    for u in range(n):
+        if match_l[u] < 0:
+            augment(u)
+    return n - sum(1 for v in range(n) if match_l[v] >= 0)
 
 
 def graph_width(graph_handle):
