@@ -37,6 +37,7 @@ namespace rgbd {
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) short g_v4s;
+typedef __attribute__((ext_vector_type(4))) unsigned int v4u;
 
 constexpr int G_THREADS = 256;
 
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int row
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c0 < N) {
     if (vec && c0 + 8 <= N) {
-#pragma unroll 4
+#pragma unroll 8
       for (int m = r0 + rl; m < r1; m += 8) {
         Frag<T> f;
         f.load(y + (long long)m * ld + c0);
@@ -470,11 +471,25 @@ __global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int row
   // the chunks' partials: row lane rl takes chunks rl, rl + 8, ... (in order), then the 8 lanes
   // fold in fixed order
   float t8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int k = rl; k < nch; k += 8)
+  if ((N & 3) == 0 && c0 + 8 <= N) {
+    // two 16-byte loads per partial row, eight rows' loads in flight
+#pragma unroll 8
+    for (int k = rl; k < nch; k += 8) {
+      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(prs, (k * N + c0) * 4, 0, WT_SC1);
+      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(prs, (k * N + c0 + 4) * 4, 0, WT_SC1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (c0 + j < N) t8[j] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (k * N + c0 + j) * 4, 0, WT_SC1));
+      for (int j = 0; j < 4; ++j) {
+        t8[j] += __uint_as_float(a[j]);
+        t8[4 + j] += __uint_as_float(b[j]);
+      }
+    }
+  } else {
+#pragma unroll 4
+    for (int k = rl; k < nch; k += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < N) t8[j] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (k * N + c0 + j) * 4, 0, WT_SC1));
+  }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[rl][8 * cg + j] = t8[j];
