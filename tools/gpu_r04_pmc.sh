@@ -4,6 +4,7 @@
 #   ratio:  the ratio predictor (tools/micro_ratio.py, train mode, bench shape) — conv5, chain,
 #           gate, pool: HBM bytes, MFMA busy, wave-state counters.
 #   dsam:   the hot path's K5 legs (tools/micro_dsam.py, the bench's step): the same counters.
+#   step:   the bench's default step itself (bench.py, short run): every kernel of the step.
 # Tables: tools/traffic_table.py -> gpurun_out/r04/pmc_<which>.json (+ pmc_table.py text).
 cd "$GRAFT_REPO_ROOT" || exit 1
 R="$GRAFT_REPO_ROOT"
@@ -19,6 +20,7 @@ for which in "$@"; do
   case "$which" in
     ratio) drv="$R/tools/micro_ratio.py --iters 3" ;;
     dsam)  drv="$R/tools/micro_dsam.py --iters 2" ;;
+    step)  drv="$R/bench.py --steps 3 --warmup 1 --cpu-baseline 0 --inference 0 --c5-stream 0 --parity 0 --full-model 0" ;;
     *) echo "unknown $which"; exit 2 ;;
   esac
   rm -rf "$O/pmc_$which"; mkdir -p "$O/pmc_$which"
