@@ -357,6 +357,10 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
  *   rgbd_point_losses_bwd: glogits [N][P] from the per-row upstream gradients g_ce, g_dice [N]. */
 int rgbd_point_sample(const float* maps, int nmaps, int h, int w, const float* coords, int maps_per_coord, int P,
                       float* out, void* stream);
+/* the same sample from maps of dtype RGBD_F32 or RGBD_BF16 (widened exactly: the bf16 logits
+ * the model produces under autocast are sampled without a float32 copy); f32 output */
+int rgbd_point_sample_t(int dtype, const void* maps, int nmaps, int h, int w, const float* coords, int maps_per_coord,
+                        int P, float* out, void* stream);
 int rgbd_point_sample_bwd(const float* gout, int nmaps, int h, int w, const float* coords, int maps_per_coord,
                           int P, float* gmaps, void* stream);
 int rgbd_match_cost(const float* pred, int B, int Q, int P, const float* tgt, const int* toff,

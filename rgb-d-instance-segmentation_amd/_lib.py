@@ -82,6 +82,7 @@ SIGNATURES = {
     "rgbd_dsam_seg_workspace_size": (_SZ, [_I, _I, _I, _I, _I]),
     "rgbd_dsam_bwd_weight_seg": (_I, [_I, _P, _P, _P]),
     "rgbd_point_sample": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P]),
+    "rgbd_point_sample_t": (_I, [_I, _P, _I, _I, _I, _P, _I, _I, _P, _P]),
     "rgbd_point_sample_bwd": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P]),
     "rgbd_match_cost": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P]),
     "rgbd_point_losses": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),

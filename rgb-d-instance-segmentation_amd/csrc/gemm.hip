@@ -522,19 +522,22 @@ __device__ __forceinline__ void gl_dma16(const void* gsrc, uint32_t lds_base) {
                : "memory");
 }
 
-constexpr int GL_THREADS = 512, GL_S = 3;
-template <int TM, int TN>
+constexpr int GL_THREADS = 512;
+template <int TM, int TN, int S>
 struct GlCfg {
   static constexpr int FM = TM / 32, FN = TN / 64;  // fragments per wave: 2 (M) x 4 (N) waves
   static constexpr int A_BYTES = TM * 128, B_BYTES = TN * 128, STAGE = A_BYTES + B_BYTES;
   static constexpr int PIECES = STAGE / 1024, PER_WAVE = PIECES / 8;
-  static constexpr int SMEM = GL_S * STAGE > TM * TN * 4 ? GL_S * STAGE : TM * TN * 4;
+  static constexpr int SMEM = S * STAGE > TM * TN * 4 ? S * STAGE : TM * TN * 4;
   static_assert(PIECES % 8 == 0 && SMEM <= 163840, "LDS-DMA GEMM tile");
 };
 
-template <int TM, int TN>
-__global__ __launch_bounds__(GL_THREADS) void k_gemm_lds(GArgs a) {
-  using C = GlCfg<TM, TN>;
+// s_waitcnt immediate (gfx9 encoding): vmcnt(vm), lgkmcnt(lgkm), expcnt not waited
+constexpr int gl_waitcnt(int vm, int lgkm) { return (vm & 15) | (7 << 4) | ((lgkm & 15) << 8) | ((vm >> 4) << 14); }
+
+template <int TM, int TN, int S>
+__global__ __launch_bounds__(GL_THREADS, S == 2 ? 2 : 1) void k_gemm_lds(GArgs a) {
+  using C = GlCfg<TM, TN, S>;
   constexpr int FM = C::FM, FN = C::FN;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -574,20 +577,20 @@ __global__ __launch_bounds__(GL_THREADS) void k_gemm_lds(GArgs a) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  if (nk > 1) {
-    if constexpr (C::PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  // stages 0 .. S-2 ahead; stage kt + S - 1 is issued at the start of step kt
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j)
+    if (j < nk) issue(j, j);
+  if (S == 3 && nk > 1)
+    __builtin_amdgcn_s_waitcnt(gl_waitcnt(C::PER_WAVE, 15));
+  else
+    __builtin_amdgcn_s_waitcnt(gl_waitcnt(0, 15));
   __syncthreads();
 #pragma unroll 1
   for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 2 < nk;
-    if (more) issue(kt + 2, (kt + 2) % GL_S);
-    const char* sa = smem + (kt % GL_S) * C::STAGE;
+    const bool more = kt + S - 1 < nk;
+    if (more) issue(kt + S - 1, (kt + S - 1) % S);
+    const char* sa = smem + (kt % S) * C::STAGE;
     const char* sb = sa + C::A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -602,12 +605,11 @@ __global__ __launch_bounds__(GL_THREADS) void k_gemm_lds(GArgs a) {
         for (int i = 0; i < FM; ++i) mma(acc[j][i], fn[j], fm[i]);
     }
     // the next stage landed (this wave's pieces; the barrier covers the others'), reads done
-    if (more) {
-      if constexpr (C::PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
+    if (S == 3 && more)
+      __builtin_amdgcn_s_waitcnt(gl_waitcnt(C::PER_WAVE, 0));
+    else
+      __builtin_amdgcn_s_waitcnt(gl_waitcnt(0, 0));
+    __builtin_amdgcn_s_barrier();
   }
 
   // epilogue as k_gemm's: lane (r, g): acc[j][i][e] = C[m = 16 (wm FM + i) + r][n = 16 (wn FN + j) + 4 g + e]
@@ -637,25 +639,26 @@ __global__ __launch_bounds__(GL_THREADS) void k_gemm_lds(GArgs a) {
   }
 }
 
-template <int TM, int TN>
+template <int TM, int TN, int S>
 int launch_lds(const GArgs& a, hipStream_t s) {
-  using C = GlCfg<TM, TN>;
+  using C = GlCfg<TM, TN, S>;
   static const hipError_t attr =
-      hipFuncSetAttribute((const void*)k_gemm_lds<TM, TN>, hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+      hipFuncSetAttribute((const void*)k_gemm_lds<TM, TN, S>, hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
   if (attr != hipSuccess) return (int)attr;
   const int T = ceil_div(a.N, TN) * ceil_div(a.M, TM);
-  k_gemm_lds<TM, TN><<<T, GL_THREADS, C::SMEM, s>>>(a);
+  k_gemm_lds<TM, TN, S><<<T, GL_THREADS, C::SMEM, s>>>(a);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
 
-// RGBD_GEMM_LDS=0 keeps every bf16 GEMM on k_gemm (A/B); read once
-inline bool gemm_lds_enabled() {
-  static const bool on = [] {
+// RGBD_GEMM_LDS: 0 keeps every bf16 GEMM on k_gemm; 2 takes 128 x 128 tiles with a 2-stage ring
+// (64 KB of LDS: two workgroups per CU) for every shape (A/B); default 1; read once
+inline int gemm_lds_mode() {
+  static const int mode = [] {
     const char* e = getenv("RGBD_GEMM_LDS");
-    return !(e && e[0] == '0');
+    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
   }();
-  return on;
+  return mode;
 }
 
 template <typename T, int TM, int TN, bool AT, bool BT>
@@ -680,8 +683,10 @@ int gemm_t(GArgs a, int at, int bt, int batch, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     // the LDS-DMA kernel: bf16, both operands K-contiguous and 16-byte aligned, one GEMM, no split
     if (!at && !bt && batch == 1 && a.splits == 1 && a.vec_a && a.vec_b && a.K % 8 == 0 && !a.bias_m &&
-        a.M >= 1024 && gemm_lds_enabled())
-      return a.N % 256 == 0 ? launch_lds<128, 256>(a, s) : launch_lds<128, 128>(a, s);
+        a.M >= 1024 && gemm_lds_mode() != 0) {
+      if (gemm_lds_mode() == 2) return launch_lds<128, 128, 2>(a, s);
+      return a.N % 256 == 0 ? launch_lds<128, 256, 3>(a, s) : launch_lds<128, 128, 3>(a, s);
+    }
   }
   // 128 x 128 tiles when they give the chip enough workgroups, else 64 x 64
   const long long big = (long long)ceil_div(a.N, 128) * ceil_div(a.M, 128) * batch * a.splits;

@@ -55,7 +55,8 @@ __device__ __forceinline__ Taps taps(float cx, float cy, int h, int w) {
 
 // out[m][p] = bilinear sample of map m at coords[m / per][p] (x = width, y = height): a point set
 // per group of `per` consecutive maps
-__global__ __launch_bounds__(256) void k_point_sample(const float* __restrict__ maps, int nmaps, int h, int w,
+template <typename T>
+__global__ __launch_bounds__(256) void k_point_sample(const T* __restrict__ maps, int nmaps, int h, int w,
                                                       const float* __restrict__ coords, int per, int P,
                                                       float* __restrict__ out) {
   const long long i = blockIdx.x * 256ll + threadIdx.x;
@@ -63,13 +64,14 @@ __global__ __launch_bounds__(256) void k_point_sample(const float* __restrict__ 
   const int m = (int)(i / P), p = (int)(i % P);
   const float2 c = reinterpret_cast<const float2*>(coords)[(long long)(m / per) * P + p];
   const Taps t = taps(c.x, c.y, h, w);
-  const float* mp = maps + (long long)m * h * w;
+  const T* mp = maps + (long long)m * h * w;
   auto in = [&](int y, int x) { return x >= 0 && x < w && y >= 0 && y < h; };
+  auto at = [&](int y, int x) { return Num<T>::to_f(mp[y * w + x]); };  // bf16 widens exactly
   float v = 0.f;  // ATen accumulates nw, ne, sw, se in that order (contracted to FMAs)
-  if (in(t.y0, t.x0)) v = __builtin_fmaf(mp[t.y0 * w + t.x0], t.nw, v);
-  if (in(t.y0, t.x0 + 1)) v = __builtin_fmaf(mp[t.y0 * w + t.x0 + 1], t.ne, v);
-  if (in(t.y0 + 1, t.x0)) v = __builtin_fmaf(mp[(t.y0 + 1) * w + t.x0], t.sw, v);
-  if (in(t.y0 + 1, t.x0 + 1)) v = __builtin_fmaf(mp[(t.y0 + 1) * w + t.x0 + 1], t.se, v);
+  if (in(t.y0, t.x0)) v = __builtin_fmaf(at(t.y0, t.x0), t.nw, v);
+  if (in(t.y0, t.x0 + 1)) v = __builtin_fmaf(at(t.y0, t.x0 + 1), t.ne, v);
+  if (in(t.y0 + 1, t.x0)) v = __builtin_fmaf(at(t.y0 + 1, t.x0), t.sw, v);
+  if (in(t.y0 + 1, t.x0 + 1)) v = __builtin_fmaf(at(t.y0 + 1, t.x0 + 1), t.se, v);
   out[i] = v;
 }
 
@@ -223,8 +225,23 @@ int rgbd_point_sample(const float* maps, int nmaps, int h, int w, const float* c
   const long long n = (long long)nmaps * P;
   if (n == 0) return RGBD_OK;
   RGBD_REQUIRE(maps && coords && out, RGBD_E_ARG);
-  k_point_sample<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(maps, nmaps, h, w, coords,
-                                                                               maps_per_coord, P, out);
+  k_point_sample<float><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(maps, nmaps, h, w, coords,
+                                                                                      maps_per_coord, P, out);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_point_sample_t(int dtype, const void* maps, int nmaps, int h, int w, const float* coords, int maps_per_coord,
+                        int P, float* out, void* stream) {
+  if (dtype == RGBD_F32)
+    return rgbd_point_sample((const float*)maps, nmaps, h, w, coords, maps_per_coord, P, out, stream);
+  RGBD_REQUIRE(dtype == RGBD_BF16, RGBD_E_DTYPE);
+  RGBD_REQUIRE(nmaps >= 0 && h > 0 && w > 0 && P >= 0 && maps_per_coord > 0, RGBD_E_ARG);
+  const long long n = (long long)nmaps * P;
+  if (n == 0) return RGBD_OK;
+  RGBD_REQUIRE(maps && coords && out, RGBD_E_ARG);
+  k_point_sample<bf16_t><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const bf16_t*)maps, nmaps, h, w, coords, maps_per_coord, P, out);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -47,7 +47,7 @@ class HipHungarianMatcher(Mask2FormerHungarianMatcher):
         # point sampling + pair-wise CE / dice of all images on the GPU kernels (point_loss.py),
         # the same torch.rand draws as the reference; matching_cost above is the torch form
         from .point_loss import match_costs
-        costs = match_costs(self, masks_queries_logits.float(), class_queries_logits, mask_labels, class_labels)
+        costs = match_costs(self, masks_queries_logits, class_queries_logits, mask_labels, class_labels)
         return ops.linear_sum_assignment_batch(costs)
 
 

@@ -18,7 +18,7 @@ from torch import nn
 from transformers.models.mask2former.modeling_mask2former import Mask2FormerHungarianMatcher, Mask2FormerLoss
 
 from . import _lib
-from ._lib import check
+from ._lib import RGBD_BF16, RGBD_F32, check
 from .ops import _need_cuda, _p, _stream, device_const
 
 
@@ -30,7 +30,11 @@ def point_sample(maps: torch.Tensor, coords: torch.Tensor) -> torch.Tensor:
 
 
 def _sample(maps, coords):
-    maps = maps.detach().float().contiguous()
+    """float32 samples of float32 or bfloat16 maps (bf16 sampled in place: no float32 copy)."""
+    maps = maps.detach()
+    if maps.dtype not in (torch.float32, torch.bfloat16):
+        maps = maps.float()
+    maps = maps.contiguous()
     coords = coords.detach().float().contiguous()
     _need_cuda(maps, coords)
     N, h, w = maps.shape
@@ -39,8 +43,9 @@ def _sample(maps, coords):
         raise ValueError(f"point_sample: {N} maps for {G} point sets")
     out = torch.empty((N, P), dtype=torch.float32, device=maps.device)
     if N:
-        check(_lib.lib().rgbd_point_sample(_p(maps), N, h, w, _p(coords), N // G, P, _p(out), _stream(maps.device)),
-              "rgbd_point_sample")
+        code = RGBD_BF16 if maps.dtype == torch.bfloat16 else RGBD_F32
+        check(_lib.lib().rgbd_point_sample_t(code, _p(maps), N, h, w, _p(coords), N // G, P, _p(out),
+                                             _stream(maps.device)), "rgbd_point_sample_t")
     return out
 
 

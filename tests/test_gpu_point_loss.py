@@ -48,6 +48,15 @@ def _case(seed, B=3, Q=100, L=49, H=60, W=80, counts=(5, 0, 23)):
     return masks, classes, mask_labels, class_labels
 
 
+def test_point_sample_bf16_maps_equal_widened_float32():
+    """rgbd_point_sample_t on bf16 maps (the logits under autocast, no float32 copy) gives the
+    bits of the float32 kernel on the same maps widened."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    maps = torch.randn((12, 120, 160), generator=g, device=DEV).to(torch.bfloat16)
+    coords = torch.rand((3, 5000, 2), generator=g, device=DEV) * 1.2 - 0.1
+    assert torch.equal(point_loss._sample(maps, coords), point_loss._sample(maps.float(), coords))
+
+
 @pytest.mark.parametrize("seed", [0, 1])
 def test_match_costs_match_reference(seed):
     from transformers.models.mask2former.modeling_mask2former import Mask2FormerHungarianMatcher
