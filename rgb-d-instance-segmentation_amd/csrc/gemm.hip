@@ -503,12 +503,12 @@ __global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ y, int row
   if (threadIdx.x == 0) tickets[blockIdx.x] = 0;  // rearmed for the next call on this workspace
 }
 
-// ---- bf16, both operands K-contiguous (forward: X [M][K] W [N][K]; dX with the weight's
-// cached transpose), batch 1, no split: the conv5 recipe (ratio.hip k_rp_conv3x3_v3) on a plain
+// ---- bf16, both operands K-contiguous (forward: X [M][K] W [N][K]; dX with the weight
+// transposed), batch 1, no split: the conv5 recipe (ratio.hip k_rp_conv3x3_v3) on a plain
 // GEMM.  512 threads = 8 waves as 2 (M) x 4 (N), wave tile (TM/2) x (TN/4); K staged 64 at a
 // time (128-byte rows, 16-byte chunk c at slot c ^ (row & 7)) by LDS-DMA straight from global
-// memory (global_load_lds_dwordx4: no VGPR staging, no ds_write) into a 3-stage ring issued two
-// stages ahead, one barrier per stage; rows past M / N and chunks past K read a zero line.  The
+// memory (global_load_lds_dwordx4: no VGPR staging, no ds_write) into an S-stage ring issued
+// S - 1 stages ahead, one barrier per stage; rows past M / N and chunks past K read a zero line.  The
 // blockIdx -> tile map keeps the N tiles of one M tile on one XCD (workgroup i runs on XCD
 // i % 8), so X is fetched from HBM once and re-read from that XCD's L2.  Epilogue: the
 // accumulator tile through LDS, 16-byte row stores with bias / act / residual / ReLU-mask.
@@ -651,12 +651,15 @@ int launch_lds(const GArgs& a, hipStream_t s) {
   return RGBD_OK;
 }
 
-// RGBD_GEMM_LDS: 0 keeps every bf16 GEMM on k_gemm; 2 takes 128 x 128 tiles with a 2-stage ring
-// (64 KB of LDS: two workgroups per CU) for every shape (A/B); default 1; read once
+// RGBD_GEMM_LDS (A/B, read once): default / 2 = 128 x 128 tiles with a 2-stage ring (64 KB of LDS:
+// two workgroups per CU, one's prologue and epilogue under the other's MFMAs); 3 = one workgroup
+// per CU with a 3-stage ring (128 x 256 tiles when N % 256 == 0); 0 = k_gemm for every shape.
+// Measured (tools/micro_gemm.py, profiles/r04_v3/micro_gemm_lds.txt): the 2-stage form is
+// 1.2-1.6x faster than the 3-stage one on the drop-in model's shapes.
 inline int gemm_lds_mode() {
   static const int mode = [] {
     const char* e = getenv("RGBD_GEMM_LDS");
-    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
+    return e && (e[0] == '0' || e[0] == '3') ? e[0] - '0' : 2;
   }();
   return mode;
 }
@@ -684,8 +687,9 @@ int gemm_t(GArgs a, int at, int bt, int batch, hipStream_t s) {
     // the LDS-DMA kernel: bf16, both operands K-contiguous and 16-byte aligned, one GEMM, no split
     if (!at && !bt && batch == 1 && a.splits == 1 && a.vec_a && a.vec_b && a.K % 8 == 0 && !a.bias_m &&
         a.M >= 1024 && gemm_lds_mode() != 0) {
-      if (gemm_lds_mode() == 2) return launch_lds<128, 128, 2>(a, s);
-      return a.N % 256 == 0 ? launch_lds<128, 256, 3>(a, s) : launch_lds<128, 128, 3>(a, s);
+      if (gemm_lds_mode() == 3)
+        return a.N % 256 == 0 ? launch_lds<128, 256, 3>(a, s) : launch_lds<128, 128, 3>(a, s);
+      return launch_lds<128, 128, 2>(a, s);
     }
   }
   // 128 x 128 tiles when they give the chip enough workgroups, else 64 x 64
