@@ -77,7 +77,8 @@ def test_groupnorm_relu_fused_by_install():
     hip = torch.nn.Sequential(torch.nn.Conv2d(16, 256, 1, bias=False), torch.nn.GroupNorm(32, 256),
                               torch.nn.ReLU()).to(DEV)
     hip.load_state_dict(ref.state_dict())
-    assert dense.install(hip) == 1
+    assert dense.install(hip) == 2  # the 1x1 convolution (f2, conv.HipConv2d) and the GroupNorm
+    assert type(hip[0]).__name__ == "HipConv2d"
     assert hip[1]._fused_relu and type(hip[2]).__name__ == "_FusedReLU"
     x = torch.randn((2, 16, 30, 40), generator=g).to(DEV)
     gy = torch.randn((2, 256, 30, 40), generator=g).to(DEV)
@@ -87,6 +88,7 @@ def test_groupnorm_relu_fused_by_install():
     yb.backward(gy)
     for (na, pa), (nb, pb) in zip(hip.named_parameters(), ref.named_parameters()):
         assert _rel(pa.grad, pb.grad) < 1e-4, na
-    assert dense.uninstall(hip) == 1
+    assert dense.uninstall(hip) == 2
+    assert type(hip[0]) is torch.nn.Conv2d
     assert type(hip[1]) is torch.nn.GroupNorm and type(hip[2]) is torch.nn.ReLU
     assert _rel(hip(x), yb) < 1e-5

@@ -3,6 +3,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r04; mkdir -p $O
 bash tools/gpu_r04.sh smoke || exit 1
-TESTLOG=tests_full timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread -p no:cacheprovider > $O/tests_full.log 2>&1
+TESTLOG=tests_full timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rf --timeout 400 --timeout-method thread -p no:cacheprovider > $O/tests_full.log 2>&1
 rc=$?; tail -5 $O/tests_full.log; [ $rc -ne 0 ] && exit $rc
 bash tools/gpu_r04.sh bench || exit 1
