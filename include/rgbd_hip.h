@@ -580,6 +580,10 @@ int rgbd_swin_window_attn(int dtype, const void* q, const void* k, const void* v
  * "dsam_dx", "dsam_wgrad", "decompose", "dggm_fwd", "dggm_bwd", "assemble"), then resets.
  * Do not enable while a stream is being captured into a graph. */
 int rgbd_timing_enable(int on);
+/* Diagnostics: buf (device, >= 2 * 18 * 8 * 5 uint64) receives, for workgroup 0 of every later
+ * conv5 launch (k_rp_conv3x3_v3), s_memtime stamps per wave and K step of its first two tiles
+ * (step top, after the DMA issue, after k-step 0 / 1's MFMAs, after the closing wait); NULL stops. */
+int rgbd_debug_conv5_stamps(void* buf);
 double rgbd_timing_read(const char* name, int* count);
 
 #ifdef __cplusplus

@@ -113,6 +113,7 @@ SIGNATURES = {
     "rgbd_swin_window_attn": (_I, [_I, _P, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
                                    _LL, _P]),
     "rgbd_timing_enable": (_I, [_I]),
+    "rgbd_debug_conv5_stamps": (_I, [_P]),
     "rgbd_timing_read": (ctypes.c_double, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "rgbd_ratio_packed_size": (_SZ, [_I]),
     "rgbd_ratio_pack": (_I, [_I, _P, _P, _P]),

@@ -1199,6 +1199,21 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
   return o;
 }
 
+// Diagnostics (rgbd_debug_conv5_stamps): when set, workgroup 0 records per step of its first two
+// tiles, per wave (lane 0, vector stores), s_memtime at: step top (after the barrier), after the
+// DMA issue, after k-step 0's MFMAs are issued, after k-step 1's, after the closing wait:
+// stamps[(tile * 18 + step) * 8 + wave][5].  A separate instantiation (STAMPS = true), launched
+// only while a buffer is set: the production kernel's code is unchanged.
+__device__ unsigned long long* g_c3_stamps = nullptr;
+static bool c3_stamps_on = false;
+__device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) st[idx] = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool STAMPS>
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
                                                        bf16_t* __restrict__ y, float* __restrict__ slab) {
@@ -1251,9 +1266,12 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (; tile < ntiles; tile += gridDim.x) {
+  unsigned long long* const stamps = (STAMPS && blockIdx.x == 0) ? g_c3_stamps : nullptr;
+  int tcount = 0;
+  for (; tile < ntiles; tile += gridDim.x, ++tcount) {
     const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
     const long long ntile = tile + gridDim.x;
+    unsigned long long* const sts = (STAMPS && stamps && tcount < 2) ? stamps : nullptr;
     const bool has_next = ntile < ntiles;
     const C3Tile tn = c3_tile(has_next ? ntile : tile, tiles_x, tiles_y);
     f32x4 acc[4][8];
@@ -1264,6 +1282,8 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 
 #pragma unroll 1
     for (int st = 0; st < C3_STEPS; ++st) {
+      const long long sidx = ((long long)(tcount * C3_STEPS + st) * 8 + wave) * 5;
+      if (STAMPS && sts) c3_stamp(sts, sidx + 0);
       // this step's DMA: B(st + 1) (or the next tile's B(0)), plus a piece of A (this tile's half 1
       // during steps 0-5, the next tile's half 0 during 9-14)
       int a_issued = 0;
@@ -1287,6 +1307,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       const int h = st >= 9, tap = st - 9 * h, ky = tap / 3, kx = tap % 3;
       const char* sa = smem + h * (C3_APIX * 128);
       const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
+      if (STAMPS && sts) c3_stamp(sts, sidx + 1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         Frag<bf16_t> fa[4], fb[8];
@@ -1302,12 +1323,22 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
+        if (STAMPS && sts) c3_stamp(sts, sidx + 2 + ks);
       }
       // own DMA landed (except the A pieces just issued), own LDS reads done, then the barrier
-      if (a_issued == 1)
-        asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (STAMPS) {
+        if (a_issued == 1)
+          asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (sts) c3_stamp(sts, sidx + 4);
+        __builtin_amdgcn_s_barrier();
+      } else {
+        if (a_issued == 1)
+          asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
     }
     // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
     // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
@@ -1865,10 +1896,17 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
     TimerScope ts("rp_conv3x3", s);
     if constexpr (sizeof(T) == 2) {
       static const hipError_t attr = hipFuncSetAttribute(
-          (const void*)k_rp_conv3x3_v3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
+          (const void*)k_rp_conv3x3_v3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       if (attr != hipSuccess) return (int)attr;
       gcv = conv3_grid(B, H, W);
-      k_rp_conv3x3_v3<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+      if (c3_stamps_on) {
+        static const hipError_t sattr = hipFuncSetAttribute((const void*)k_rp_conv3x3_v3<true>,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
+        (void)sattr;
+        k_rp_conv3x3_v3<true><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+      } else {
+        k_rp_conv3x3_v3<false><<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+      }
     } else {
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
@@ -1895,6 +1933,14 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
 }  // namespace
 
 extern "C" {
+
+int rgbd_debug_conv5_stamps(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_c3_stamps), &p, sizeof(p));
+  if (e != hipSuccess) return (int)e;
+  c3_stamps_on = p != nullptr;
+  return RGBD_OK;
+}
 
 size_t rgbd_ratio_packed_size(int dtype) { return make_layout(dtype == RGBD_BF16 ? 2 : 4).total; }
 
