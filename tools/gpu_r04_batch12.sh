@@ -9,4 +9,4 @@ done
 for i in 1 2 3; do for sp in 0 1; do
   echo "spread=$sp $(RGBD_C3_SPREAD=$sp timeout -k 10 120 python tools/micro_ratio.py --iters 30 2>&1 | tail -1)" || exit 1
 done; done
-RGBD_C3_SPREAD=1 TESTLOG=tests12 bash tools/gpu_r04.sh tests tests/test_gpu_ratio.py tests/test_gpu_model.py::test_bf16_train_mode_batchnorm_stats
+RGBD_C3_SPREAD=1 TESTLOG=tests12 bash tools/gpu_r04.sh tests tests/test_gpu_model.py tests/test_gpu_bf16_parity.py tests/test_gpu_c2.py
