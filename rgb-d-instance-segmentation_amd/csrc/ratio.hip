@@ -1206,14 +1206,6 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
 // only while a buffer is set: the production kernel's code is unchanged.
 __device__ unsigned long long* g_c3_stamps = nullptr;
 static bool c3_stamps_on = false;
-// RGBD_C3_SPREAD=1: the step's DMA pieces issued between k-step 0's MFMA groups (A/B); read once
-inline bool c3_spread() {
-  static const bool on = [] {
-    const char* e = getenv("RGBD_C3_SPREAD");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 __device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) {
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -1221,7 +1213,7 @@ __device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) 
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool STAMPS, bool SPREAD>
+template <bool STAMPS>
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
                                                        bf16_t* __restrict__ y, float* __restrict__ slab) {
@@ -1247,11 +1239,6 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
     if (p < C3_NPIX && yy >= 0 && yy < H && xx >= 0 && xx < W)
       src = (const char*)(x + (((long long)t.b * H + yy) * W + xx) * FUS_C + 64 * h + 8 * (q ^ (p & 6)));
     glds16(src, lds0 + h * (C3_APIX * 128) + j * 1024);
-  };
-  // one of them (k of 4)
-  auto issue_b_piece = [&](int st, int k) {
-    glds16(w5s + (size_t)st * (C5 * 128) + wave * 4096 + 16 * lane + 1024 * k,
-           lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 4096 + 1024 * k);
   };
   // B pieces of step st: 32 x 1 KiB, wave w copies pieces 4w..4w+3
   auto issue_b = [&](int st) {
@@ -1304,11 +1291,9 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       const int b_st = st + 1 < C3_STEPS ? st + 1 : 0;
       const int a_j = st < 6 ? wave + 8 * st : wave + 8 * (st - 9);
       const int a_kind = (st < 6 && a_j < C3_APIECES) ? 1 : ((st >= 9 && st < 15 && has_next && a_j < C3_APIECES) ? 2 : 0);
-      if constexpr (!SPREAD) {
-        if (b_next) issue_b(b_st);
-        if (a_kind == 1) issue_a(t, 1, a_j);
-        if (a_kind == 2) issue_a(tn, 0, a_j);
-      }
+      if (b_next) issue_b(b_st);
+      if (a_kind == 1) issue_a(t, 1, a_j);
+      if (a_kind == 2) issue_a(tn, 0, a_j);
       a_issued = a_kind != 0;
       const int h = st >= 9, tap = st - 9 * h, ky = tap / 3, kx = tap % 3;
       const char* sa = smem + h * (C3_APIX * 128);
@@ -1326,20 +1311,9 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
         for (int nj = 0; nj < 8; ++nj)
           fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, 4 * ks + g));
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
+        for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
-          if constexpr (SPREAD) {
-            // the step's DMA spread over k-step 0's MFMA groups (a burst of 8 waves x 5 pieces at
-            // the step top kept every SIMD's matrix pipe idle ~600-800 cycles: conv5_stamps.py),
-            // B piece mi after group mi; the A piece after k-step 1's first group
-            if (ks == 0 && b_next) issue_b_piece(b_st, mi);
-            if (ks == 1 && mi == 0) {
-              if (a_kind == 1) issue_a(t, 1, a_j);
-              if (a_kind == 2) issue_a(tn, 0, a_j);
-            }
-          }
-        }
         if (STAMPS && sts) c3_stamp(sts, sidx + 2 + ks);
       }
       // own DMA landed (except the A pieces just issued), own LDS reads done, then the barrier
@@ -1913,10 +1887,9 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
     TimerScope ts("rp_conv3x3", s);
     if constexpr (sizeof(T) == 2) {
       static const hipError_t attr = hipFuncSetAttribute(
-          (const void*)k_rp_conv3x3_v3<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
+          (const void*)k_rp_conv3x3_v3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       if (attr != hipSuccess) return (int)attr;
       gcv = conv3_grid(B, H, W);
-      const bool spread = c3_spread();
       auto go = [&](auto kern) {
         static const hipError_t sattr =
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
@@ -1924,9 +1897,9 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
         kern<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
       };
       if (c3_stamps_on)
-        spread ? go(k_rp_conv3x3_v3<true, true>) : go(k_rp_conv3x3_v3<true, false>);
+        go(k_rp_conv3x3_v3<true>);
       else
-        spread ? go(k_rp_conv3x3_v3<false, true>) : go(k_rp_conv3x3_v3<false, false>);
+        go(k_rp_conv3x3_v3<false>);
     } else {
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
