@@ -519,7 +519,20 @@ template <int PH> constexpr size_t c2w_smem() { return c2w_off_patch<PH>() + (si
 static_assert(c2w_smem<1>() <= 163840, "chain v2 LDS budget");
 static_assert(2 * c2w_smem<0>() <= 163840, "chain v2 phase 0: two workgroups per CU");
 
-template <int PHASE>
+// Diagnostics (rgbd_debug_chain_stamps): the STAMPS instantiation records, for workgroup 0's first
+// four tiles, s_memtime per wave at: tile top, patch staged (after the second barrier), next
+// patch's loads issued, stem MFMAs issued (phase 0: statistics done), stem ReLU/pack done, fusion
+// MFMAs issued, tile end (statistics + stores): stamps[((phase * 4 + tile) * 8 + wave) * 7 + point].
+__device__ unsigned long long* g_c2_stamps = nullptr;
+static bool c2_stamps_on = false;
+__device__ __forceinline__ void c2_stamp(unsigned long long* st, long long idx) {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) st[idx] = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int PHASE, bool STAMPS = false>
 __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const float* __restrict__ depth3, long long bstride, int B,
                                                      int H, int W, const char* __restrict__ blob, Layout L,
                                                      const float2* __restrict__ aff1, const float2* __restrict__ aff2,
@@ -623,7 +636,11 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
       }
   };
   fetch_patch(blockIdx.x);
-  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  int tcount = 0;
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++tcount) {
+    unsigned long long* const sts = (STAMPS && blockIdx.x == 0 && tcount < 4) ? g_c2_stamps : nullptr;
+    const long long sidx = ((long long)PHASE * 32 + (long long)tcount * 8 + wave) * 7;
+    if (STAMPS && sts) c2_stamp(sts, sidx + 0);
     const int b = (int)(tile / ((long long)tiles_x * tiles_y));
     const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
     const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
@@ -634,7 +651,9 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
       if (i < PATCH_N) patch[(i / C2W_PW) * C2W_PWP + i % C2W_PW] = f32_to_bf16(pre[k]);
     }
     lds_barrier();
+    if (STAMPS && sts) c2_stamp(sts, sidx + 1);
     fetch_patch(tile + gridDim.x);
+    if (STAMPS && sts) c2_stamp(sts, sidx + 2);
     const int py = y0 + wave;
     const bool row_ok = py < H;
     const bool full = row_ok && x0 + C2W_TW <= W;  // wave-uniform
@@ -690,6 +709,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
         }
         add_stats(ssum[t], ssq[t], a1, full, x0, row_ok);
       }
+      if (STAMPS && sts) c2_stamp(sts, sidx + 3);
       continue;
     }
     // phases 1, 2: K step outermost (one B fragment pair live), all 12 channel groups accumulate
@@ -711,6 +731,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
         mma(a1[t][1], af, bfr[1]);
       }
     }
+    if (STAMPS && sts) c2_stamp(sts, sidx + 3);
     Frag<bf16_t> f1[6][2];
 #pragma unroll
     for (int s = 0; s < 6; ++s)
@@ -721,6 +742,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
         for (int e = 0; e < 8; ++e) vv[e] = fmaxf(a1[2 * s + (e >> 2)][u][e & 3], 0.f);  // BN1 folded into W1
         f1[s][u].from8(vv);
       }
+    if (STAMPS && sts) c2_stamp(sts, sidx + 4);
     // ---- fusion (phase 1: operands swapped for the statistics)
     f32x4 a2[8][2];
 #pragma unroll
@@ -745,6 +767,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
         }
       }
     }
+    if (STAMPS && sts) c2_stamp(sts, sidx + 5);
     if constexpr (PHASE == 1) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) add_stats(ssum[t], ssq[t], a2[t], full, x0, row_ok);
@@ -756,6 +779,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
               make_uint4(pack_bf16x2(a2[t][0][0], a2[t][0][1]), pack_bf16x2(a2[t][0][2], a2[t][0][3]),
                          pack_bf16x2(a2[t][1][0], a2[t][1][1]), pack_bf16x2(a2[t][1][2], a2[t][1][3]));
       }
+      if (STAMPS && sts) c2_stamp(sts, sidx + 6);
       continue;
     }
     if constexpr (PHASE == 2) {
@@ -1847,7 +1871,14 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   }
 #define CHAIN_LAUNCH(PH, A1, A2, SL, OUT)                                                                          \
   do {                                                                                                            \
-    if (v2)                                                                                                       \
+    if (v2 && c2_stamps_on && PH < 2) {                                                                           \
+      static const hipError_t sattr = hipFuncSetAttribute((const void*)k_rp_chain_v2<PH, true>,                  \
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize,             \
+                                                          (int)c2w_smem<PH>());                                   \
+      (void)sattr;                                                                                                \
+      k_rp_chain_v2<PH, true><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(                                 \
+          depth3, bstride, B, H, W, blob, L, A1, A2, fold, SL, (bf16_t*)(OUT));                                   \
+    } else if (v2)                                                                                                \
       k_rp_chain_v2<PH><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, \
                                                                         fold, SL, (bf16_t*)(OUT));                \
     else                                                                                                          \
@@ -1926,6 +1957,14 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
 }  // namespace
 
 extern "C" {
+
+int rgbd_debug_chain_stamps(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_c2_stamps), &p, sizeof(p));
+  if (e != hipSuccess) return (int)e;
+  c2_stamps_on = p != nullptr;
+  return RGBD_OK;
+}
 
 int rgbd_debug_conv5_stamps(void* buf) {
   unsigned long long* p = (unsigned long long*)buf;
