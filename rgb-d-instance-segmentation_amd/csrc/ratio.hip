@@ -489,6 +489,16 @@ __global__ __launch_bounds__(256) void k_rp_fold(const char* __restrict__ blob, 
   }
 }
 
+// tile index -> (image, first row, first column) with 32-bit unsigned divisions (the 64-bit
+// ones cost ~150 scalar instructions per decode, twice per tile in the chain kernels)
+struct TileDec {
+  int b, y0, x0;
+};
+__device__ __forceinline__ TileDec tile_dec(unsigned t, unsigned per, unsigned tiles_x, int th, int tw) {
+  const unsigned b = t / per, rem = t - b * per, ty = rem / tiles_x;
+  return TileDec{(int)b, (int)ty * th, (int)(rem - ty * tiles_x) * tw};
+}
+
 // ------------------------------------------------------------------ chain v2 (bf16)
 // 512 threads = 8 waves; persistent; ALL chain weights (143 KB bf16) live in LDS for the
 // workgroup's lifetime; a wave owns 32 pixels (one row of a 8x32 tile, two 16-px MFMA
@@ -602,15 +612,15 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
 #pragma unroll
   for (int i = 0; i < NST; ++i) ssum[i] = ssq[i] = 0.f;
   const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
-  const long long ntiles = (long long)B * tiles_x * tiles_y;
+  const unsigned per = (unsigned)(tiles_x * tiles_y);
+  const int ntiles = B * tiles_x * tiles_y;  // < 2^31 (rgbd_ratio_predict checks the shape)
   const long long HW = (long long)H * W;
   // the next tile's depth patch is prefetched into registers while the current one computes
   constexpr int PATCH_N = 3 * C2W_PH * C2W_PW, PATCH_PER = (PATCH_N + 511) / 512;
   float pre[PATCH_PER];
-  auto fetch_patch = [&](long long t) {
-    const int b = (int)(t / ((long long)tiles_x * tiles_y));
-    const int trem = (int)(t % ((long long)tiles_x * tiles_y));
-    const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
+  auto fetch_patch = [&](int t) {
+    const TileDec td = tile_dec((unsigned)t, per, (unsigned)tiles_x, C2W_TH, C2W_TW);
+    const int b = td.b, y0 = td.y0, x0 = td.x0;
 #pragma unroll
     for (int k = 0; k < PATCH_PER; ++k) {
       const int i = tid + 512 * k;
@@ -637,13 +647,12 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
   };
   fetch_patch(blockIdx.x);
   int tcount = 0;
-  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++tcount) {
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++tcount) {
     unsigned long long* const sts = (STAMPS && blockIdx.x == 0 && tcount < 4) ? g_c2_stamps : nullptr;
     const long long sidx = ((long long)PHASE * 32 + (long long)tcount * 8 + wave) * 7;
     if (STAMPS && sts) c2_stamp(sts, sidx + 0);
-    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
-    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
-    const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
+    const TileDec td = tile_dec((unsigned)tile, per, (unsigned)tiles_x, C2W_TH, C2W_TW);
+    const int b = td.b, y0 = td.y0, x0 = td.x0;
     lds_barrier();  // everyone is done with the previous patch
 #pragma unroll
     for (int k = 0; k < PATCH_PER; ++k) {
@@ -772,7 +781,7 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
 #pragma unroll
       for (int t = 0; t < 8; ++t) add_stats(ssum[t], ssq[t], a2[t], full, x0, row_ok);
       if (att) {  // raw fusion output for k_rp_gate: [tile][wave][t][lane][u][4 px], 1 KiB per store
-        bf16_t* ft = att + ((tile * 8 + wave) * 16) * 256;
+        bf16_t* ft = att + (((long long)tile * 8 + wave) * 16) * 256;
 #pragma unroll
         for (int t = 0; t < 8; ++t)
           *reinterpret_cast<uint4*>(ft + (t * 64 + lane) * 8) =
@@ -911,15 +920,16 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
   }
   __syncthreads();
   const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
-  const long long ntiles = (long long)B * tiles_x * tiles_y;
+  const unsigned per = (unsigned)(tiles_x * tiles_y);
+  const int ntiles = B * tiles_x * tiles_y;
   const long long HW = (long long)H * W;
   // this wave's raw fusion output of a tile ([t][lane][u][4 px]): lane (r, g) has channel 16t + r,
   // pixels 16u + 4g + j;
   // the next tile's 8 KB are loaded while the current one computes
   uint2 nxt[8][2];
-  auto fetch = [&](long long tl) {
+  auto fetch = [&](int tl) {
     if (tl >= ntiles) return;
-    const bf16_t* ft = fus + ((tl * 8 + wave) * 16) * 256;
+    const bf16_t* ft = fus + (((long long)tl * 8 + wave) * 16) * 256;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // read once: non-temporal, 16 B per lane (1 KiB per wave load)
       const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ft + (t * 64 + lane) * 8));
@@ -928,10 +938,9 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
     }
   };
   fetch(blockIdx.x);
-  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int b = (int)(tile / ((long long)tiles_x * tiles_y));
-    const int trem = (int)(tile % ((long long)tiles_x * tiles_y));
-    const int y0 = (trem / tiles_x) * C2W_TH, x0 = (trem % tiles_x) * C2W_TW;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const TileDec td = tile_dec((unsigned)tile, per, (unsigned)tiles_x, C2W_TH, C2W_TW);
+    const int b = td.b, y0 = td.y0, x0 = td.x0;
     const int py = y0 + wave;
     uint2 raw[8][2];
 #pragma unroll
@@ -2008,6 +2017,7 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
   RGBD_REQUIRE(depth3 && packed && bn_host && ratio && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
   RGBD_REQUIRE(B <= 32, RGBD_E_SHAPE);  // k_rp_tail_fc1 / k_rp_tail_head hold the batch in LDS
+  RGBD_REQUIRE((long long)B * ((H + 7) / 8) * ((W + 31) / 32) < (1ll << 30), RGBD_E_SHAPE);  // 32-bit tile indices
   BnPtrs bn;
   for (int i = 0; i < RGBD_RATIO_NBN * 4; ++i) {
     RGBD_REQUIRE(bn_host[i], RGBD_E_ARG);
