@@ -585,7 +585,7 @@ int rgbd_timing_enable(int on);
  * (step top, after the DMA issue, after k-step 0 / 1's MFMAs, after the closing wait); NULL stops. */
 int rgbd_debug_conv5_stamps(void* buf);
 /* The same for the bf16 chain kernels (k_rp_chain_v2 phases 0 and 1): buf (device, >= 2 * 4 * 8 * 7
- * uint64) receives workgroup 0's stamps for its first four tiles (tile top, patch staged, next
+ * uint64) receives workgroup 0's stamps for its tiles 8-11 (tile top, patch staged, next
  * patch issued, stem MFMAs issued, stem ReLU/pack, fusion MFMAs issued, tile end), phase-major
  * (phase 0 writes the first four points).  NULL stops. */
 int rgbd_debug_chain_stamps(void* buf);

@@ -529,8 +529,8 @@ template <int PH> constexpr size_t c2w_smem() { return c2w_off_patch<PH>() + (si
 static_assert(c2w_smem<1>() <= 163840, "chain v2 LDS budget");
 static_assert(2 * c2w_smem<0>() <= 163840, "chain v2 phase 0: two workgroups per CU");
 
-// Diagnostics (rgbd_debug_chain_stamps): the STAMPS instantiation records, for workgroup 0's first
-// four tiles, s_memtime per wave at: tile top, patch staged (after the second barrier), next
+// Diagnostics (rgbd_debug_chain_stamps): the STAMPS instantiation records, for workgroup 0's tiles
+// 8-11, s_memtime per wave at: tile top, patch staged (after the second barrier), next
 // patch's loads issued, stem MFMAs issued (phase 0: statistics done), stem ReLU/pack done, fusion
 // MFMAs issued, tile end (statistics + stores): stamps[((phase * 4 + tile) * 8 + wave) * 7 + point].
 __device__ unsigned long long* g_c2_stamps = nullptr;
@@ -648,8 +648,9 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
   fetch_patch(blockIdx.x);
   int tcount = 0;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++tcount) {
-    unsigned long long* const sts = (STAMPS && blockIdx.x == 0 && tcount < 4) ? g_c2_stamps : nullptr;
-    const long long sidx = ((long long)PHASE * 32 + (long long)tcount * 8 + wave) * 7;
+    // tiles 8..11 of workgroup 0 (past the start-up: weights landing, every workgroup's first loads)
+    unsigned long long* const sts = (STAMPS && blockIdx.x == 0 && tcount >= 8 && tcount < 12) ? g_c2_stamps : nullptr;
+    const long long sidx = ((long long)PHASE * 32 + (long long)(tcount - 8) * 8 + wave) * 7;
     if (STAMPS && sts) c2_stamp(sts, sidx + 0);
     const TileDec td = tile_dec((unsigned)tile, per, (unsigned)tiles_x, C2W_TH, C2W_TW);
     const int b = td.b, y0 = td.y0, x0 = td.x0;
