@@ -535,9 +535,14 @@ struct GlCfg {
 // s_waitcnt immediate (gfx9 encoding): vmcnt(vm), lgkmcnt(lgkm), expcnt not waited
 constexpr int gl_waitcnt(int vm, int lgkm) { return (vm & 15) | (7 << 4) | ((lgkm & 15) << 8) | ((vm >> 4) << 14); }
 
-template <int TM, int TN, int S>
+// TT: both operands stored [K][rows] with the rows contiguous (a_t = b_t = 1: a weight gradient
+// dY^T X, K = tokens), split-K over blockIdx.y.  Stages of 64 k-rows x 256 bytes per operand,
+// read back k-major with ds_read_tr16_b64 (frag_t, GCfg<bf16_t>::toff's 32-byte-block swizzle
+// applied on the DMA's per-lane source addresses).
+template <int TM, int TN, int S, bool TT = false>
 __global__ __launch_bounds__(GL_THREADS, S == 2 ? 2 : 1) void k_gemm_lds(GArgs a) {
   using C = GlCfg<TM, TN, S>;
+  static_assert(!TT || (TM == 128 && TN == 128), "TT stages: 128 columns = 256-byte rows");
   constexpr int FM = C::FM, FN = C::FN;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -552,21 +557,35 @@ __global__ __launch_bounds__(GL_THREADS, S == 2 ? 2 : 1) void k_gemm_lds(GArgs a
   const bf16_t* A = reinterpret_cast<const bf16_t*>(a.A);
   const bf16_t* B = reinterpret_cast<const bf16_t*>(a.B);
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  const int nk = (a.K + 63) / 64;
+  const int sp = TT ? (int)blockIdx.y : 0;
+  const int kbeg = TT ? sp * a.kchunk : 0, kend = TT ? min(a.K, kbeg + a.kchunk) : a.K;
+  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
 
-  // piece p of a stage: 8 rows of A (p < TM / 8) or of B; lane -> row p*8 + lane/8, slot lane%8
   auto issue = [&](int kt, int buf) {
-    const int k0 = kt * 64;
+    const int k0 = kbeg + kt * 64;
 #pragma unroll
     for (int u = 0; u < C::PER_WAVE; ++u) {
       const int p = wave * C::PER_WAVE + u;
-      const bool is_a = p < TM / 8;
-      const int row = (is_a ? p : p - TM / 8) * 8 + (lane >> 3);
-      const int q = (lane & 7) ^ (row & 7);
-      const int gr = (is_a ? m_base : n_base) + row, k = k0 + 8 * q;
+      const bool is_a = p < C::A_BYTES / 1024;
       const void* src = g_zero_line;
-      if (gr < (is_a ? a.M : a.N) && k < a.K)
-        src = is_a ? (const void*)(A + (long long)gr * a.lda + k) : (const void*)(B + (long long)gr * a.ldb + k);
+      if constexpr (TT) {
+        // piece = 4 k-rows x 256 B; lane -> row 4p + lane/16, physical 16-byte slot lane%16 of the
+        // row, which holds logical 32-byte block (slot/2) ^ swz(row)
+        const int row = (is_a ? p : p - C::A_BYTES / 1024) * 4 + (lane >> 4);
+        const int slot = lane & 15;
+        const int swz = (row & 3) | (((row >> 3) & 1) << 2);
+        const int col = (((slot >> 1) ^ swz) << 4) + 8 * (slot & 1);
+        const int gk = k0 + row, gc = (is_a ? m_base : n_base) + col;
+        if (gk < kend && gc < (is_a ? a.M : a.N))
+          src = is_a ? (const void*)(A + (long long)gk * a.lda + gc) : (const void*)(B + (long long)gk * a.ldb + gc);
+      } else {
+        // piece p of a stage: 8 rows of A (p < TM / 8) or of B; lane -> row p*8 + lane/8, slot lane%8
+        const int row = (is_a ? p : p - TM / 8) * 8 + (lane >> 3);
+        const int q = (lane & 7) ^ (row & 7);
+        const int gr = (is_a ? m_base : n_base) + row, k = k0 + 8 * q;
+        if (gr < (is_a ? a.M : a.N) && k < a.K)
+          src = is_a ? (const void*)(A + (long long)gr * a.lda + k) : (const void*)(B + (long long)gr * a.ldb + k);
+      }
       gl_dma16(src, lds0 + buf * C::STAGE + p * 1024);
     }
   };
@@ -596,9 +615,9 @@ __global__ __launch_bounds__(GL_THREADS, S == 2 ? 2 : 1) void k_gemm_lds(GArgs a
     for (int ks = 0; ks < 2; ++ks) {
       Frag<bf16_t> fm[FM], fn[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) fm[i] = frag_k(sa, wm * FM + i, ks, lane);
+      for (int i = 0; i < FM; ++i) fm[i] = TT ? frag_t(sa, wm * FM + i, ks, lane) : frag_k(sa, wm * FM + i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) fn[j] = frag_k(sb, wn * FN + j, ks, lane);
+      for (int j = 0; j < FN; ++j) fn[j] = TT ? frag_t(sb, wn * FN + j, ks, lane) : frag_k(sb, wn * FN + j, ks, lane);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -624,8 +643,9 @@ __global__ __launch_bounds__(GL_THREADS, S == 2 ? 2 : 1) void k_gemm_lds(GArgs a
       }
   }
   __syncthreads();
-  const bool vec_c = (a.N % 8 == 0) && (((uintptr_t)a.C) % 16 == 0) && (a.ldc % 8 == 0) &&
-                     (!a.R || (a.ldr % 8 == 0 && ((uintptr_t)a.R) % 16 == 0));
+  const bool vec_c = a.splits > 1 ? (a.N % 4 == 0)
+                                  : ((a.N % 8 == 0) && (((uintptr_t)a.C) % 16 == 0) && (a.ldc % 8 == 0) &&
+                                     (!a.R || (a.ldr % 8 == 0 && ((uintptr_t)a.R) % 16 == 0)));
   constexpr int TPR = TN / 8, RPP = GL_THREADS / TPR;
   const int nl = (tid % TPR) * 8;
 #pragma unroll 1
@@ -635,19 +655,25 @@ __global__ __launch_bounds__(GL_THREADS, S == 2 ? 2 : 1) void k_gemm_lds(GArgs a
     const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4));
     const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4 + 1));
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    g_store8<bf16_t>(a, 0, 0, m, n0, v, vec_c);
+    g_store8<bf16_t>(a, 0, sp, m, n0, v, vec_c);  // splits > 1: the split's float32 partial
   }
 }
 
-template <int TM, int TN, int S>
+template <int TM, int TN, int S, bool TT = false>
 int launch_lds(const GArgs& a, hipStream_t s) {
   using C = GlCfg<TM, TN, S>;
-  static const hipError_t attr =
-      hipFuncSetAttribute((const void*)k_gemm_lds<TM, TN, S>, hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_gemm_lds<TM, TN, S, TT>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
   if (attr != hipSuccess) return (int)attr;
   const int T = ceil_div(a.N, TN) * ceil_div(a.M, TM);
-  k_gemm_lds<TM, TN, S><<<T, GL_THREADS, C::SMEM, s>>>(a);
+  k_gemm_lds<TM, TN, S, TT><<<dim3(T, TT ? a.splits : 1), GL_THREADS, C::SMEM, s>>>(a);
   RGBD_CHECK_LAUNCH();
+  if (TT && a.splits > 1) {
+    const long long quads = (long long)a.M * ((a.N + 3) / 4);
+    const int blocks = (int)std::min<long long>((quads + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_gemm_splitk_reduce<bf16_t>, dim3(blocks), dim3(256), 0, s, a, 1);
+    RGBD_CHECK_LAUNCH();
+  }
   return RGBD_OK;
 }
 
@@ -656,6 +682,13 @@ int launch_lds(const GArgs& a, hipStream_t s) {
 // per CU with a 3-stage ring (128 x 256 tiles when N % 256 == 0); 0 = k_gemm for every shape.
 // Measured (tools/micro_gemm.py, profiles/r04_v3/micro_gemm_lds.txt): the 2-stage form is
 // 1.2-1.6x faster than the 3-stage one on the drop-in model's shapes.
+inline bool gemm_lds_tt_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RGBD_GEMM_LDS_TT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 inline int gemm_lds_mode() {
   static const int mode = [] {
     const char* e = getenv("RGBD_GEMM_LDS");
@@ -691,6 +724,11 @@ int gemm_t(GArgs a, int at, int bt, int batch, hipStream_t s) {
         return a.N % 256 == 0 ? launch_lds<128, 256, 3>(a, s) : launch_lds<128, 128, 3>(a, s);
       return launch_lds<128, 128, 2>(a, s);
     }
+    // weight gradients (both operands token-major): the LDS-DMA kernel with transposed fragment
+    // reads; RGBD_GEMM_LDS_TT=0 keeps them on k_gemm (A/B)
+    if (at && bt && batch == 1 && a.vec_a && a.vec_b && a.M % 8 == 0 && a.N % 8 == 0 && !a.bias_m && !a.R &&
+        a.K >= 1024 && gemm_lds_tt_enabled())
+      return launch_lds<128, 128, 2, true>(a, s);
   }
   // 128 x 128 tiles when they give the chip enough workgroups, else 64 x 64
   const long long big = (long long)ceil_div(a.N, 128) * ceil_div(a.M, 128) * batch * a.splits;

@@ -101,6 +101,23 @@ def test_gemm_lds_dma_path(M, N, K, act):
     assert Cf.dtype == torch.float32 and _rel(Cf, ref) < 2e-5 * (3 if act == 2 else 1) * K ** 0.5
 
 
+@pytest.mark.parametrize("N,K,M", [(1024, 256, 50400), (256, 256, 50400), (264, 96, 3000), (96, 384, 1200),
+                                   (136, 200, 1100)])
+@pytest.mark.parametrize("c_f32", [True, False], ids=["f32_out", "bf16_out"])
+def test_gemm_lds_dma_weight_gradient(N, K, M, c_f32):
+    """dW [N][K] = dY^T [N][M] X [M][K] in bf16 (layout (1, 1), M >= 1024 tokens): the LDS-DMA
+    kernel with transposed fragment reads and split-K over the tokens, ragged N / K / M, against
+    float64 on the same bf16 operands."""
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(N + K + M)
+    gy = torch.randn((M, N), generator=g).to(DEV, torch.bfloat16)
+    x = torch.randn((M, K), generator=g).to(DEV, torch.bfloat16)
+    dW = dense.gemm(gy, x, 1, 1, N, K, M, c_f32=c_f32)
+    ref = gy.double().t() @ x.double()
+    assert dW.shape == (N, K) and dW.dtype == (torch.float32 if c_f32 else torch.bfloat16)
+    assert _rel(dW, ref) < (2e-5 if c_f32 else BF16_TOL)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
 def test_gemm_split_k_weight_gradient(dt):
     """dW = dY^T X with a long reduction (50 400 pixel-decoder tokens) and a small output: the
