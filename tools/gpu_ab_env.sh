@@ -7,7 +7,7 @@ var=$1; vals=$2
 : > gpurun_out/ab_env.txt
 for rep in 1 2 3; do
   for v in $vals; do
-    env "$var=$v" timeout -k 10 300 python bench.py --cpu-baseline 0 --c5-stream 0 --parity 0 --inference 0 > gpurun_out/ab_env.json 2> gpurun_out/ab_env.err || { echo "bench failed"; tail -5 gpurun_out/ab_env.err; exit 1; }
+    env "$var=$v" timeout -k 10 300 python bench.py --cpu-baseline 0 --c5-stream 0 --parity 0 --inference 0 --full-model 0 > gpurun_out/ab_env.json 2> gpurun_out/ab_env.err || { echo "bench failed"; tail -5 gpurun_out/ab_env.err; exit 1; }
     python - "$var=$v" >> gpurun_out/ab_env.txt <<'PY'
 import json, sys; d = json.load(open("gpurun_out/ab_env.json"))
 k = d["kernel_ms"]
