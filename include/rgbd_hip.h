@@ -589,6 +589,12 @@ int rgbd_debug_conv5_stamps(void* buf);
  * patch issued, stem MFMAs issued, stem ReLU/pack, fusion MFMAs issued, tile end), phase-major
  * (phase 0 writes the first four points).  NULL stops. */
 int rgbd_debug_chain_stamps(void* buf);
+/* The same for the DSAM conv legs (k_dsam_lds, the forward cascade and dX): buf (device, >= launches
+ * * 256 * 4 * 8 uint64) receives, for the next `launches` launches, per workgroup and for its first
+ * four work items: s_memtime at item taken, tables built, first DMA landed, K loop done, partial
+ * hand-off done, epilogue done; steps | chunks << 16 | chunk << 24; the item word.  (NULL, 0)
+ * stops. */
+int rgbd_debug_dsam_stamps(void* buf, int launches);
 double rgbd_timing_read(const char* name, int* count);
 
 #ifdef __cplusplus

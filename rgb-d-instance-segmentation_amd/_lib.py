@@ -115,6 +115,7 @@ SIGNATURES = {
     "rgbd_timing_enable": (_I, [_I]),
     "rgbd_debug_conv5_stamps": (_I, [_P]),
     "rgbd_debug_chain_stamps": (_I, [_P]),
+    "rgbd_debug_dsam_stamps": (_I, [_P, _I]),
     "rgbd_timing_read": (ctypes.c_double, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "rgbd_ratio_packed_size": (_SZ, [_I]),
     "rgbd_ratio_pack": (_I, [_I, _P, _P, _P]),

@@ -55,6 +55,7 @@ struct ConvArgs {
                                     // over the batch instead of 8 x 16 blocks (small grids)
   float* partial;                   // bf16: partial tiles of multi-chunk tiles (reduced by their last chunk)
   const bf16_t* zero;               // bf16: LD_ZERO_BYTES of zeros (zeroed by k_dsam_plan)
+  unsigned long long* stamps;       // diagnostics only (rgbd_debug_dsam_stamps); null otherwise
 };
 
 constexpr int BM = 64, BN = 64;
@@ -1364,9 +1365,24 @@ __device__ __forceinline__ void items_body(const ConvArgs& a) {
 }
 __global__ __launch_bounds__(1024) void k_dsam_items(const PlanLegs L) { items_body(L.a[blockIdx.x]); }
 
+// Diagnostics (rgbd_debug_dsam_stamps): the STAMPS instantiation of k_dsam_lds has wave 0 of every
+// workgroup record, for its first LD_STAMP_ITEMS items, s_memtime at: item taken, prologue tables
+// built, first DMA landed, K loop done, partial hand-off done (or the early return of a non-last
+// chunk), epilogue done; then the item's steps | chunks << 16 | chunk << 24 and the item word:
+// stamps[(wg * LD_STAMP_ITEMS + k) * 8 + field].  The production instantiation has none of it.
+constexpr int LD_STAMP_ITEMS = 4;
+__device__ __forceinline__ void ld_stamp(unsigned long long* st, int f) {
+  if (!st) return;
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) st[f] = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // One (tile, chunk) item of k_dsam_lds for N tile ntile (of ntn).
 template <int KC>
-__device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, int chunk, int ntile, int ntn) {
+__device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, int chunk, int ntile, int ntn,
+                                        int* next_s, int nitems, unsigned long long* st = nullptr) {
   using Cfg = LdCfg<KC>;
   constexpr int S = Cfg::S;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -1393,14 +1409,8 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   const bf16_t* xp = (const bf16_t*)a.x;
   const bf16_t* wp = (const bf16_t*)a.w;
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  // ---- prologue: row table (threads 0..127), code lists per tap, bias prefix sums of this N tile
-  for (int e = tid; e < 5 * LD_BN; e += 512) {
-    const int k = e / LD_BN, nl = e - k * LD_BN, n = n0 + nl;
-    float s = 0.f;
-    if (a.bias4 && n < a.N)
-      for (int sb = 0; sb < k; ++sb) s += a.bias4[sb * a.N + n];
-    bsum[e] = s;
-  }
+  // ---- prologue: row table (threads 0..127), code lists per tap (the N tile's bias prefix sums
+  // were built once per workgroup by k_dsam_lds)
   // step table, tap major, then chunk group, then code (ascending): one thread per (tap, chunk
   // group) writes its run from registers (no LDS round trips)
   for (int q = tid; q < G.ntap * ncg; q += 512) {
@@ -1434,6 +1444,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     rowout[tid] = make_int4(obase, opix, nmk, 0);
   }
   __syncthreads();
+  ld_stamp(st, 1);
   // DMA role: A rows 16*wave + lane/4 of every chunk, slot lane%4.  A row that is outside the
   // input at the step's tap, or whose source code is not the step's code, is read from the zero
   // row instead: it contributes exactly zero, with no masking of fragments in registers.
@@ -1452,6 +1463,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   const bf16_t* zrow = a.zero + achk;
   const int s0 = (int)((long long)chunk * total / nc), s1 = (int)((long long)(chunk + 1) * total / nc);
   const int nst = s1 - s0;
+  if (st && threadIdx.x == 0) st[6] = (unsigned long long)(nst | (nc << 16) | (chunk << 24));
   auto issue = [&](int slot, int s) {  // step s (absolute)
     const int e = __builtin_amdgcn_readfirstlane(steptab[s]);
     const int t = e & 15, cg = (e >> 4) & 255, code = e >> 12;
@@ -1484,6 +1496,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   for (int i = 0; i < npro; ++i) issue(i, s0 + i);
   if (npro >= 2) vm_wait_barrier_dyn((npro - 1) * cnt);  // step 0 landed, later ones may fly
   else vm_wait_barrier<0>();
+  ld_stamp(st, 2);
 #pragma unroll 1
   for (int s = 0; s < nst; ++s) {
     if (s + S - 1 < nst) issue((s + S - 1) % S, s0 + s + S - 1);
@@ -1516,6 +1529,25 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     if (ahead <= 0) vm_wait_barrier<0>();
     else vm_wait_barrier_dyn(ahead * cnt);
   }
+  ld_stamp(st, 3);
+  // the workgroup's next item, taken now so the counter and work-list reads overlap the hand-off
+  // and the epilogue; published in LDS at every exit (k_dsam_lds's barrier orders it)
+  int nxt = 0, nxv = 0;
+  bool have = false;
+  if (tid == 0) nxt = __hip_atomic_fetch_add(a.work + ntile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto fetch_word = [&] {  // the next item's work-list word (waits for the counter)
+    if (tid == 0 && !have) {
+      nxv = nxt < nitems ? a.items[nxt] : 0;
+      have = true;
+    }
+  };
+  auto publish = [&] {
+    fetch_word();
+    if (tid == 0) {
+      next_s[0] = nxt;
+      next_s[1] = nxv;
+    }
+  };
   if (nc > 1) {
     // Multi-chunk tile: publish this chunk's fragment-native partial ([wave][mi][nj][lane][4] f32),
     // take a ticket; the chunk that draws nc-1 sums all partials in chunk order (deterministic)
@@ -1542,7 +1574,11 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
       *last_s = old == nc - 1;
     }
     __syncthreads();
-    if (!*last_s) return;
+    if (!*last_s) {
+      ld_stamp(st, 4);
+      publish();
+      return;
+    }
     // every partial of the tile in flight at once, then summed in chunk order
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -1562,6 +1598,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
         for (int nj = 0; nj < 3; ++nj) acc[mi][nj] += __builtin_bit_cast(f32x4, pv[mi][nj]);
     }
   }
+  ld_stamp(st, 4);
   // ---- epilogue (same contract as k_conv_igemm), staged through LDS in two 96-column halves:
   // pass 1 runs along pixels (NCHW residual loads and stores), pass 2 along channels (NHWC);
   // every thread's loads of a pass are independent and issued together.
@@ -1576,6 +1613,16 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     constexpr int NIT = LD_BM * NCH / 512;
     static_assert(LD_BM * LDE * 4 <= Cfg::ROWTAB, "epilogue image must not overlap the row tables");
     float* et = (float*)smem;
+    const bf16_t* rnhwc = (const bf16_t*)a.residual_nhwc;
+    bf16_t* onhwc = (bf16_t*)a.out_nhwc;
+    uint4 rv[NIT];  // residual loads first: in flight while the accumulators go through LDS
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int it = tid + 512 * i, ml = it / NCH, n = n0 + 8 * (it % NCH);
+      const int4 ro = rowout[ml];
+      rv[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (rnhwc && ro.x >= 0 && n < a.N) rv[i] = *reinterpret_cast<const uint4*>(rnhwc + (long long)ro.y * a.N + n);
+    }
     __syncthreads();  // ring reads done
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -1585,16 +1632,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
         for (int reg = 0; reg < 4; ++reg)
           et[(wm * 64 + 16 * mi + 4 * g + reg) * LDE + wn * 48 + 16 * nj + r] = acc[mi][nj][reg];
     __syncthreads();
-    const bf16_t* rnhwc = (const bf16_t*)a.residual_nhwc;
-    bf16_t* onhwc = (bf16_t*)a.out_nhwc;
-    uint4 rv[NIT];
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-      const int it = tid + 512 * i, ml = it / NCH, n = n0 + 8 * (it % NCH);
-      const int4 ro = rowout[ml];
-      rv[i] = make_uint4(0u, 0u, 0u, 0u);
-      if (rnhwc && ro.x >= 0 && n < a.N) rv[i] = *reinterpret_cast<const uint4*>(rnhwc + (long long)ro.y * a.N + n);
-    }
+    fetch_word();
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int it = tid + 512 * i, ml = it / NCH, nl = 8 * (it % NCH), n = n0 + nl;
@@ -1615,6 +1653,8 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
       *reinterpret_cast<uint4*>(onhwc + (long long)ro.y * a.N + n) =
           make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
     }
+    ld_stamp(st, 5);
+    publish();
     return;
   }
   float* et = (float*)smem;  // [96 n][LD_EPI_LD] f32
@@ -1723,26 +1763,51 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
       }
     }
   }
+  ld_stamp(st, 5);
+  publish();
 }
 
 // Persistent: grid (workgroups, N tiles); each workgroup takes the next item of its N tile's list
 // from a counter (items differ up to ~5x in steps: dynamic assignment balances the tail; the
 // multi-chunk reductions stay in chunk order, so results do not depend on who ran what).
-template <int KC>
+template <int KC, bool STAMPS = false>
 __global__ __launch_bounds__(512, 1) void k_dsam_lds(ConvArgs a) {
   using Cfg = LdCfg<KC>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
-  int* next_s = (int*)(smem + Cfg::TMASK + 216);  // free bytes behind the per-tap code lists
+  int* next_s = (int*)(smem + Cfg::TMASK + 216);  // free bytes behind the per-tap code lists: item, word
   const int nitems = *a.nitems;
+  const int ntile = blockIdx.y;
+  {  // the N tile's bias prefix sums over the four conv biases, kept for every item
+    float* bsum = (float*)(smem + Cfg::BSUM);
+    const int n0 = ntile * LD_BN;
+    for (int e = threadIdx.x; e < 5 * LD_BN; e += 512) {
+      const int k = e / LD_BN, nl = e - k * LD_BN, n = n0 + nl;
+      float s = 0.f;
+      if (a.bias4 && n < a.N)
+        for (int sb = 0; sb < k; ++sb) s += a.bias4[sb * a.N + n];
+      bsum[e] = s;
+    }
+  }
+  if (threadIdx.x == 0) {
+    const int it = __hip_atomic_fetch_add(a.work + ntile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    next_s[0] = it;
+    next_s[1] = it < nitems ? a.items[it] : 0;
+  }
+  int done = 0;
   for (;;) {
-    if (threadIdx.x == 0)
-      *next_s = __hip_atomic_fetch_add(a.work + blockIdx.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int it = *next_s;
+    unsigned long long* st = nullptr;
+    if constexpr (STAMPS) {
+      if (done < LD_STAMP_ITEMS)
+        st = a.stamps + ((long long)(blockIdx.x + blockIdx.y * gridDim.x) * LD_STAMP_ITEMS + done) * 8;
+      ++done;
+    }
+    __syncthreads();  // next_s published (first item: above; later: by the previous item)
+    const int it = next_s[0], v = next_s[1];
     if (it >= nitems) break;  // workgroup-uniform
-    const int v = a.items[it];
-    ld_item<KC>(a, v & 3, v >> 5, (v >> 2) & 7, blockIdx.y, gridDim.y);
-    __syncthreads();  // LDS of this item no longer read, next_s read by every thread
+    ld_stamp(st, 0);
+    if (st && threadIdx.x == 0) st[7] = (unsigned long long)v;
+    // next_s is rewritten only after the item's K loop, behind its prologue barrier
+    ld_item<KC>(a, v & 3, v >> 5, (v >> 2) & 7, ntile, gridDim.y, next_s, nitems, st);
   }
 }
 
@@ -1750,6 +1815,9 @@ __global__ __launch_bounds__(512, 1) void k_dsam_lds(ConvArgs a) {
 long long conv_mmax(const ConvArgs& a) {
   return a.transposed ? (long long)a.B * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2) : (long long)a.B * a.Ho * a.Wo;
 }
+// chunks per step: three where C allows (two-stage ring).  Two (three-stage ring) measured slower
+// (round 4: 2 300 cycles per 64-channel step vs 2 840 per 96-channel step; K5 0.707 vs 0.676 ms):
+// the step is bound by LDS traffic (fragment reads + DMA writes), not by the DMA latency
 int ld_kc(int C) { return C % 96 == 0 ? 3 : (C % 64 == 0 ? 2 : 1); }
 // k_dsam_lds tiling of a conv: tiles of the largest parity class, N tiles
 // Linear tiles when 8 x 16 blocks would leave more than 15 % of the rows dead (the small grids:
@@ -1825,12 +1893,23 @@ hipError_t plan_convs(int n, const ConvArgs* legs, hipStream_t s) {
   return hipGetLastError();
 }
 
+// rgbd_debug_dsam_stamps: buffer, its capacity in launches, launches stamped so far
+unsigned long long* g_ld_stamps = nullptr;
+int g_ld_stamp_cap = 0, g_ld_stamp_n = 0;
 template <int KC>
 hipError_t launch_ld(const ConvArgs& b, dim3 grid, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)k_dsam_lds<KC>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)LdCfg<KC>::SMEM);
-  if (attr != hipSuccess) return attr;
+  static const hipError_t attr[2] = {
+      hipFuncSetAttribute((const void*)k_dsam_lds<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LdCfg<KC>::SMEM),
+      hipFuncSetAttribute((const void*)k_dsam_lds<KC, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)LdCfg<KC>::SMEM)};
+  if (attr[0] != hipSuccess) return attr[0];
+  if (g_ld_stamps && g_ld_stamp_n < g_ld_stamp_cap && grid.x * grid.y <= 256) {
+    if (attr[1] != hipSuccess) return attr[1];
+    ConvArgs c = b;
+    c.stamps = g_ld_stamps + (size_t)g_ld_stamp_n++ * 256 * LD_STAMP_ITEMS * 8;
+    k_dsam_lds<KC, true><<<grid, 512, LdCfg<KC>::SMEM, s>>>(c);
+    return hipSuccess;
+  }
   k_dsam_lds<KC><<<grid, 512, LdCfg<KC>::SMEM, s>>>(b);
   return hipSuccess;
 }
@@ -2721,6 +2800,14 @@ size_t rgbd_dsam_run_workspace_size(int kind, int B, int Cin, int h, int w, int 
   }
   return std::max<size_t>(256, ld_plan(leg_conv_args(g)).partial_bytes);
 }
+int rgbd_debug_dsam_stamps(void* buf, int launches) {
+  RGBD_REQUIRE(buf ? launches > 0 : launches == 0, RGBD_E_ARG);  // (NULL, 0) stops
+  g_ld_stamps = (unsigned long long*)buf;
+  g_ld_stamp_cap = buf ? launches : 0;
+  g_ld_stamp_n = 0;
+  return RGBD_OK;
+}
+
 int rgbd_dsam_plan(int n, const rgbd_dsam_leg* legs, void* stream) {
   RGBD_REQUIRE(n > 0 && legs, RGBD_E_ARG);
   hipStream_t s = (hipStream_t)stream;
