@@ -69,3 +69,13 @@ for li in range(NL):
           f"epi {epi[has_epi].mean() if has_epi.any() else 0:7.0f}  cycles")
     print(f"   workgroup busy span: mean {span.mean():.0f} max {span.max():.0f} min {span.min():.0f} cycles; "
           f"items with epilogue {has_epi.sum()}")
+    # the workgroups that set the launch's length: their items
+    for w in np.argsort(-(last - first))[:3]:
+        desc = []
+        for k in range(wg_items[w]):
+            r = S[w, k]
+            v = int(r[7])
+            desc.append(f"[cls {v & 3} tile {v >> 5} chunk {(v >> 2) & 7}/{(r[6] >> 16) & 0xFF} steps {r[6] & 0xFFFF}: "
+                        f"t {r[1] - r[0]} d {r[2] - r[1]} loop {r[3] - r[2]} h {(r[4] - r[3]) if r[4] else 0} "
+                        f"e {(r[5] - max(r[4], r[3])) if r[5] else 0} gap-before {r[0] - (max(S[w, k - 1][3:6]) if k else first[w])}]")
+        print(f"   wg {w} span {last[w] - first[w]}: " + " ".join(desc))
