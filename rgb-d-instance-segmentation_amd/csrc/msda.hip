@@ -109,14 +109,15 @@ __global__ __launch_bounds__(256) void k_msda_fwd(const T* __restrict__ value, M
       const int k = l * P + p;
       const Tap t = msda_tap(lq[2 * k], lq[2 * k + 1], H, W);
       float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // the four taps loaded unconditionally (a padding tap reads cell 0 and is not added), so the
+      // loads issue together instead of one branch and one memory round trip per tap
+      float v[4][8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ld8(vl + (long long)max(t.idx[e], 0) * NH * D, v[e]);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (t.idx[e] >= 0) {
-          float v[8];
-          ld8(vl + (long long)t.idx[e] * NH * D, v);
 #pragma unroll
-          for (int c = 0; c < 8; ++c) s[c] += t.w[e] * v[c];
-        }
+        for (int c = 0; c < 8; ++c) s[c] = t.idx[e] >= 0 ? s[c] + t.w[e] * v[e][c] : s[c];
       const float a = wq[k];
 #pragma unroll
       for (int c = 0; c < 8; ++c) acc[c] += a * s[c];
@@ -167,9 +168,11 @@ __global__ __launch_bounds__(256) void k_msda_bwd(const T* __restrict__ value, M
       const int k = l * P + p;
       const Tap t = msda_tap(lq[2 * k], lq[2 * k + 1], H, W);
       const float a = wq[k];
-      float v[4];
+      float v[4];  // unconditional loads (padding taps read cell 0, then count as zero)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = t.idx[e] >= 0 ? Num<T>::to_f(vb[lo + (long long)t.idx[e] * NH * D]) : 0.f;
+      for (int e = 0; e < 4; ++e) v[e] = Num<T>::to_f(vb[lo + (long long)max(t.idx[e], 0) * NH * D]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = t.idx[e] >= 0 ? v[e] : 0.f;
       const float s = t.w[0] * v[0] + t.w[1] * v[1] + t.w[2] * v[2] + t.w[3] * v[3];
       // d sample / d ix, d iy (zero-padded taps are zeros)
       const float dsx = (1.f - t.ly) * (v[1] - v[0]) + t.ly * (v[3] - v[2]);
@@ -226,10 +229,11 @@ __global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ val
   const long long voff = b * S * NH * D + (long long)h * D + c;
   const T* vb = value + voff;
   float* gvb = gvalue + voff;
-  float gos[R];
+  float gos[R];  // unconditional loads (a query past the run's end reads the run's first)
 #pragma unroll
-  for (int i = 0; i < R; ++i)
-    gos[i] = glive && i < qn ? Num<T>::to_f(gout[((b * Q + qa + i) * NH + h) * D + c]) : 0.f;
+  for (int i = 0; i < R; ++i) gos[i] = Num<T>::to_f(gout[((b * Q + qa + (i < qn ? i : 0)) * NH + h) * D + c]);
+#pragma unroll
+  for (int i = 0; i < R; ++i) gos[i] = glive && i < qn ? gos[i] : 0.f;
   // slot-major: one (level, point) slot over the run's queries, its held taps in 8 registers
   for (int k = 0; k < LP; ++k) {
     const int l = k / P;
@@ -237,16 +241,35 @@ __global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ val
     const long long lo = (long long)lv.start[l] * NH * D;
     int pidx[4] = {-1, -1, -1, -1};
     float pval[4] = {0.f, 0.f, 0.f, 0.f};
+    // the slot's locations and attention weights for the whole run, loaded together up front
+    float2 lq[R];
+    float aq[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long long q0 = glive && i < qn ? (b * Q + qa + i) * NH + h : 0;
+      lq[i] = *reinterpret_cast<const float2*>(loc + (q0 * LP + k) * 2);
+      aq[i] = attw[q0 * LP + k];
+    }
+    // every tap value of the slot's run, issued together before any of the slot's stores and
+    // atomics: those count in the same vmcnt, so a load issued after them would wait for them
+    // too (unconditional: padding taps read cell 0, then count as zero)
+    T vr[R][4];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const Tap t = msda_tap(lq[i].x, lq[i].y, H, W);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vr[i][e] = vb[lo + (long long)max(t.idx[e], 0) * NH * D];
+    }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const bool live = glive && i < qn;  // group-uniform
       const long long q0 = live ? (b * Q + qa + i) * NH + h : 0;
       const float go = gos[i];
-      const Tap t = msda_tap(loc[(q0 * LP + k) * 2], loc[(q0 * LP + k) * 2 + 1], H, W);
-      const float a = live ? attw[q0 * LP + k] : 0.f;
+      const Tap t = msda_tap(lq[i].x, lq[i].y, H, W);
+      const float a = live ? aq[i] : 0.f;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = t.idx[e] >= 0 ? Num<T>::to_f(vb[lo + (long long)t.idx[e] * NH * D]) : 0.f;
+      for (int e = 0; e < 4; ++e) v[e] = t.idx[e] >= 0 ? Num<T>::to_f(vr[i][e]) : 0.f;
       const float s = t.w[0] * v[0] + t.w[1] * v[1] + t.w[2] * v[2] + t.w[3] * v[3];
       const float dsx = (1.f - t.ly) * (v[1] - v[0]) + t.ly * (v[3] - v[2]);
       const float dsy = (1.f - t.lx) * (v[2] - v[0]) + t.lx * (v[3] - v[1]);
