@@ -209,9 +209,18 @@ __global__ __launch_bounds__(256) void k_msda_bwd(const T* __restrict__ value, M
 // atomics already leave it unspecified); how many atomics are saved depends on how smoothly the
 // sampling offsets vary across neighbouring queries (spatially constant at the pixel decoder's
 // initialisation: about 60 % fewer at C2).
+// one value element through a buffer descriptor: a 32-bit byte offset per lane instead of a 64-bit
+// address (the run's 32 tap loads in flight at once would otherwise hold 64 address registers)
+__device__ __forceinline__ bf16_t buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t e, bf16_t*) {
+  return (bf16_t)__builtin_amdgcn_raw_buffer_load_b16(r, e * 2u, 0, 0);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t e, float*) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, e * 4u, 0, 0));
+}
+
 template <typename T, int D, int L, int P, int R>
-__global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ value, MsdaLevels lv, int S, int Q,
-                                                       int NH, const float* __restrict__ loc,
+__global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ value, int vbytes, MsdaLevels lv, int S,
+                                                       int Q, int NH, const float* __restrict__ loc,
                                                        const float* __restrict__ attw, const T* __restrict__ gout,
                                                        long long ngroups, int nrun, float* __restrict__ gvalue,
                                                        float* __restrict__ gloc, float* __restrict__ gattw) {
@@ -227,8 +236,8 @@ __global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ val
   const long long b = br / nrun;
   const int qa = run * R, qn = min(R, Q - qa);
   const long long voff = b * S * NH * D + (long long)h * D + c;
-  const T* vb = value + voff;
   float* gvb = gvalue + voff;
+  const __amdgpu_buffer_rsrc_t vrs = wt_rsrc(value, vbytes);  // the host checks vbytes < 2^31
   float gos[R];  // unconditional loads (a query past the run's end reads the run's first)
 #pragma unroll
   for (int i = 0; i < R; ++i) gos[i] = Num<T>::to_f(gout[((b * Q + qa + (i < qn ? i : 0)) * NH + h) * D + c]);
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ val
     for (int i = 0; i < R; ++i) {
       const Tap t = msda_tap(lq[i].x, lq[i].y, H, W);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) vr[i][e] = vb[lo + (long long)max(t.idx[e], 0) * NH * D];
+      for (int e = 0; e < 4; ++e) vr[i][e] = buf_ld(vrs, (uint32_t)(voff + lo + (long long)max(t.idx[e], 0) * NH * D), (T*)nullptr);
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -352,11 +361,12 @@ int launch_bwd(const void* value, const MsdaLevels& lv, int B, int S, int Q, int
   // the value gradient is accumulated with atomics: zero it first (stream-ordered)
   const hipError_t e = hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * NH * D, s);
   if (e != hipSuccess) return (int)e;
-  if (lv.L == 3 && P == 4 && msda_runs_enabled()) {  // the reference configuration (3 levels x 4 points)
+  const long long vbytes = (long long)B * S * NH * D * (long long)sizeof(T);
+  if (lv.L == 3 && P == 4 && vbytes < (1ll << 31) && msda_runs_enabled()) {  // the reference configuration (3 levels x 4 points)
     const int nrun = ceil_div(Q, MSDA_RUN);
     const long long ngroups = (long long)B * nrun * NH;
     k_msda_bwd_runs<T, D, 3, 4, MSDA_RUN><<<(unsigned)ceil_div(ngroups, 256 / D), 256, 0, s>>>(
-        (const T*)value, lv, S, Q, NH, loc, attw, (const T*)gout, ngroups, nrun, gvalue, gloc, gattw);
+        (const T*)value, (int)vbytes, lv, S, Q, NH, loc, attw, (const T*)gout, ngroups, nrun, gvalue, gloc, gattw);
     return RGBD_OK;
   }
   k_msda_bwd<T, D><<<(unsigned)ceil_div(nqh, 256 / D), 256, 0, s>>>((const T*)value, lv, S, Q, NH, P, loc, attw,
