@@ -66,12 +66,15 @@ __global__ __launch_bounds__(256) void k_point_sample(const T* __restrict__ maps
   const Taps t = taps(c.x, c.y, h, w);
   const T* mp = maps + (long long)m * h * w;
   auto in = [&](int y, int x) { return x >= 0 && x < w && y >= 0 && y < h; };
-  auto at = [&](int y, int x) { return Num<T>::to_f(mp[y * w + x]); };  // bf16 widens exactly
+  // the four taps loaded unconditionally (an outside tap reads element 0 and is not added), so
+  // they are in flight together instead of one branch and one memory round trip each
+  auto at = [&](int y, int x) { return Num<T>::to_f(mp[in(y, x) ? y * w + x : 0]); };  // bf16 widens exactly
+  const float a0 = at(t.y0, t.x0), a1 = at(t.y0, t.x0 + 1), a2 = at(t.y0 + 1, t.x0), a3 = at(t.y0 + 1, t.x0 + 1);
   float v = 0.f;  // ATen accumulates nw, ne, sw, se in that order (contracted to FMAs)
-  if (in(t.y0, t.x0)) v = __builtin_fmaf(at(t.y0, t.x0), t.nw, v);
-  if (in(t.y0, t.x0 + 1)) v = __builtin_fmaf(at(t.y0, t.x0 + 1), t.ne, v);
-  if (in(t.y0 + 1, t.x0)) v = __builtin_fmaf(at(t.y0 + 1, t.x0), t.sw, v);
-  if (in(t.y0 + 1, t.x0 + 1)) v = __builtin_fmaf(at(t.y0 + 1, t.x0 + 1), t.se, v);
+  v = in(t.y0, t.x0) ? __builtin_fmaf(a0, t.nw, v) : v;
+  v = in(t.y0, t.x0 + 1) ? __builtin_fmaf(a1, t.ne, v) : v;
+  v = in(t.y0 + 1, t.x0) ? __builtin_fmaf(a2, t.sw, v) : v;
+  v = in(t.y0 + 1, t.x0 + 1) ? __builtin_fmaf(a3, t.se, v) : v;
   out[i] = v;
 }
 
