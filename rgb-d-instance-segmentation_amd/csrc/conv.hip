@@ -35,6 +35,15 @@ __global__ __launch_bounds__(256) void k_im2col3(const T* __restrict__ x, int C,
   r /= H;  // = b * C + c
   const int x0 = q * 8;
   const T* src = x + r * H * W;
+  // all 30 loads unconditional (clamped addresses, zeroed after): behind per-element branches the
+  // compiler waited for each one where it was issued, 30 memory round trips per thread
+  T raw[3][10];
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int yc = min(max(y + dy - 1, 0), H - 1);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) raw[dy][j] = src[(long long)yc * W + min(max(x0 + j - 1, 0), W - 1)];
+  }
   float v[3][10];
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy) {
@@ -43,7 +52,7 @@ __global__ __launch_bounds__(256) void k_im2col3(const T* __restrict__ x, int C,
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
       const int xx = x0 + j - 1;
-      v[dy][j] = (row_ok && xx >= 0 && xx < W) ? Num<T>::to_f(src[(long long)yy * W + xx]) : 0.f;
+      v[dy][j] = (row_ok && xx >= 0 && xx < W) ? Num<T>::to_f(raw[dy][j]) : 0.f;
     }
   }
   const long long HW = (long long)H * W;

@@ -611,7 +611,8 @@ __device__ __forceinline__ void code_presence_body(const uint8_t* __restrict__ c
       for (int tap = 0; tap < 9; ++tap) {
         const int iy = 2 * oy - 1 + tap / 3, ix = 2 * ox - 1 + tap % 3;
         const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
-        cv[tap] = ok ? (1u << code[((long long)b * h + (ok ? iy : 0)) * w + (ok ? ix : 0)]) : 0u;
+        cv[tap] = code[((long long)b * h + (ok ? iy : 0)) * w + (ok ? ix : 0)];  // unconditional: one round trip
+        cv[tap] = ok ? 1u << cv[tap] : 0u;
       }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) m |= cv[tap];
@@ -733,7 +734,8 @@ __device__ __forceinline__ void wg_masks_body(const WgArgs& a, int block) {
   for (int tap = 0; tap < 9; ++tap) {
     const int iy = 2 * oy - 1 + tap / 3, ix = 2 * ox - 1 + tap % 3;
     const bool ok = pv && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
-    cv[tap] = ok ? a.code[((long long)b * a.h + iy) * a.w + ix] : 0xffu;
+    cv[tap] = a.code[((long long)b * a.h + (ok ? iy : 0)) * a.w + (ok ? ix : 0)];  // unconditional: one round trip
+    cv[tap] = ok ? cv[tap] : 0xffu;
   }
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
@@ -1396,9 +1398,15 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   const LdGeom G = ld_geom(a, cls);
   const int ncg = a.C / (32 * KC);  // chunk groups
   const uint16_t* tmg = a.tmasks + ((long long)cls * a.ntiles0 + tile) * 16;
+  // the tile's 16 u16 code sets in two 16-byte loads (one round trip; per-element loads behind
+  // `t < ntap` were nine serialized ones, most of the item's table time)
   uint32_t tmask[9];
+  {
+    const uint4 q0 = reinterpret_cast<const uint4*>(tmg)[0], q1 = reinterpret_cast<const uint4*>(tmg)[1];
+    const uint32_t w[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
 #pragma unroll
-  for (int t = 0; t < 9; ++t) tmask[t] = t < G.ntap ? (uint32_t)tmg[t] : 0u;
+    for (int t = 0; t < 9; ++t) tmask[t] = t < G.ntap ? (w[t >> 1] >> (16 * (t & 1))) & 0xffffu : 0u;
+  }
   int tb[10];
   tb[0] = 0;
 #pragma unroll

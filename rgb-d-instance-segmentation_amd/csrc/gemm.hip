@@ -249,9 +249,40 @@ __device__ __forceinline__ void g_store8(const GArgs& a, int b, int bz, int m, i
     return;
   }
   const long long rbase = (long long)b * a.sr + (long long)m * a.ldr + n0;
+  if (vec_c && n0 + 8 <= a.N && (a.R || a.bias)) {
+    // whole row piece: the residual / bias values loaded together (wide loads) before use; per
+    // element behind `n0 + e < N` each load was its own memory round trip.  Same arithmetic as
+    // g_epi.  (vec_c implies 16-byte aligned R rows.)
+    float rr[8], bb[8];
+    if (a.R) {
+      if (a.c_f32) {
+        const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.R) + rbase);
+        const float4 y = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.R) + rbase + 4);
+        rr[0] = x.x; rr[1] = x.y; rr[2] = x.z; rr[3] = x.w; rr[4] = y.x; rr[5] = y.y; rr[6] = y.z; rr[7] = y.w;
+      } else {
 #pragma unroll
-  for (int e = 0; e < 8; ++e)
-    if (n0 + e < a.N) v[e] = g_epi<T>(v[e], m, n0 + e, rbase + e, a);
+        for (int e = 0; e < 8; ++e) rr[e] = Num<T>::to_f(reinterpret_cast<const T*>(a.R)[rbase + e]);
+      }
+    }
+    if (a.bias && a.act != RGBD_ACT_RELU_GRAD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bb[e] = a.bias[a.bias_m ? m : n0 + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (a.act == RGBD_ACT_RELU_GRAD) {
+        v[e] = rr[e] > 0.f ? v[e] : 0.f;
+        continue;
+      }
+      if (a.bias) v[e] += bb[e];
+      v[e] = g_act(v[e], a.act);
+      if (a.R) v[e] += rr[e];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (n0 + e < a.N) v[e] = g_epi<T>(v[e], m, n0 + e, rbase + e, a);
+  }
   if (a.c_f32) {
     float* c = reinterpret_cast<float*>(a.C) + (long long)b * a.sc + (long long)m * a.ldc + n0;
     if (vec_c && n0 + 8 <= a.N) {

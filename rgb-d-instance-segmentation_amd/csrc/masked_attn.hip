@@ -83,9 +83,12 @@ __device__ __forceinline__ void kv_load(KVTile& t, const T* K, const T* V, int k
   for (int j = 0; j < 2; ++j) {
     const int idx = tid + 256 * j, row = idx >> 3, c = idx & 7, key = k0 + row;
     const bool ok = key < ke;
-    const long long off = ((long long)key * BH + bh) * HD + 4 * c;
-    t.k[j] = ok ? ld4(K + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-    t.v[j] = ok ? ld4(V + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // unconditional loads of a clamped key (zeroed after): behind the branch the compiler waited
+    // for each load where it was issued, and the next tile's "prefetch" blocked the current one
+    const long long off = ((long long)(ok ? key : ke - 1) * BH + bh) * HD + 4 * c;
+    const float4 kk = ld4(K + off), vv = ld4(V + off);
+    t.k[j] = ok ? kk : make_float4(0.f, 0.f, 0.f, 0.f);
+    t.v[j] = ok ? vv : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -118,7 +121,9 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(AttnArgs<T> a) {
   const bool qv = qrow < a.Q;
   float qb[8];  // B operand: q_scaled^T [d = 4c + lg][query lc]
 #pragma unroll
-  for (int c = 0; c < 8; ++c) qb[c] = qv ? ld1(a.q + ((long long)qrow * a.BH + bh) * HD + 4 * c + lg) * a.scale : 0.f;
+  for (int c = 0; c < 8; ++c) qb[c] = ld1(a.q + ((long long)(qv ? qrow : 0) * a.BH + bh) * HD + 4 * c + lg);  // together
+#pragma unroll
+  for (int c = 0; c < 8; ++c) qb[c] = qv ? qb[c] * a.scale : 0.f;
   f4m o[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
   float m = -INFINITY, lsum = 0.f;
   const int kb = split * a.span, ke = min(a.L, kb + a.span);
@@ -274,9 +279,14 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs<T> a) {
   const bool kv = keyl < a.L;
   float kb[8], vb[8];  // B operands: K^T / V^T [d = 4c + lg][key lc]
 #pragma unroll
+  for (int c = 0; c < 8; ++c) {  // loads together (clamped key), zeroed after
+    kb[c] = ld1(a.k + ((long long)(kv ? keyl : 0) * a.BH + bh) * HD + 4 * c + lg);
+    vb[c] = ld1(a.v + ((long long)(kv ? keyl : 0) * a.BH + bh) * HD + 4 * c + lg);
+  }
+#pragma unroll
   for (int c = 0; c < 8; ++c) {
-    kb[c] = kv ? ld1(a.k + ((long long)keyl * a.BH + bh) * HD + 4 * c + lg) : 0.f;
-    vb[c] = kv ? ld1(a.v + ((long long)keyl * a.BH + bh) * HD + 4 * c + lg) : 0.f;
+    kb[c] = kv ? kb[c] : 0.f;
+    vb[c] = kv ? vb[c] : 0.f;
   }
   f4v dv[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
   f4v dk[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
@@ -286,13 +296,17 @@ __global__ __launch_bounds__(256) void k_attn_bwd_kv_mfma(AttnBwdArgs<T> a) {
     for (int i = tid; i < QB * HD; i += 256) {
       const int r = i / HD, d = i % HD, qrow = qb0 + r;
       const bool ok = qrow < a.Q;
-      sq[r][d] = ok ? a.qs[((long long)qrow * a.BH + bh) * HD + d] : 0.f;
-      sdo[r][d] = ok ? ld1(a.dout + ((long long)qrow * a.BH + bh) * HD + d) : 0.f;
+      const long long o = ((long long)(ok ? qrow : 0) * a.BH + bh) * HD + d;
+      const float qv2 = a.qs[o], dv2 = ld1(a.dout + o);
+      sq[r][d] = ok ? qv2 : 0.f;
+      sdo[r][d] = ok ? dv2 : 0.f;
     }
     if (tid < QB) {
       const int qrow = qb0 + tid;
-      slse[tid] = qrow < a.Q ? a.lse[(long long)qrow * a.BH + bh] : 0.f;
-      sdel[tid] = qrow < a.Q ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
+      const long long o = (long long)(qrow < a.Q ? qrow : 0) * a.BH + bh;
+      const float lv = a.lse[o], dl = a.delta[o];
+      slse[tid] = qrow < a.Q ? lv : 0.f;
+      sdel[tid] = qrow < a.Q ? dl : 0.f;
     }
     __syncthreads();
     const int qn = min(QB, a.Q - qb0);
@@ -345,12 +359,19 @@ __global__ __launch_bounds__(256) void k_attn_bwd_q_mfma(AttnBwdArgs<T> a) {
   const bool qv = qrow < a.Q;
   float qb[8], db[8];  // B operands: q_scaled^T, dO^T [d = 4c + lg][query lc]
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    qb[c] = qv ? ld1(a.q + ((long long)qrow * a.BH + bh) * HD + 4 * c + lg) * a.scale : 0.f;
-    db[c] = qv ? ld1(a.dout + ((long long)qrow * a.BH + bh) * HD + 4 * c + lg) : 0.f;
+  for (int c = 0; c < 8; ++c) {  // loads together (clamped query), zeroed after
+    qb[c] = ld1(a.q + ((long long)(qv ? qrow : 0) * a.BH + bh) * HD + 4 * c + lg);
+    db[c] = ld1(a.dout + ((long long)(qv ? qrow : 0) * a.BH + bh) * HD + 4 * c + lg);
   }
-  const float lse = qv ? a.lse[(long long)qrow * a.BH + bh] : 0.f;
-  const float del = qv ? a.delta[(long long)qrow * a.BH + bh] : 0.f;
+  const float lse0 = a.lse[(long long)(qv ? qrow : 0) * a.BH + bh];
+  const float del0 = a.delta[(long long)(qv ? qrow : 0) * a.BH + bh];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    qb[c] = qv ? qb[c] * a.scale : 0.f;
+    db[c] = qv ? db[c] : 0.f;
+  }
+  const float lse = qv ? lse0 : 0.f;
+  const float del = qv ? del0 : 0.f;
   f4m g[2] = {f4m{0.f, 0.f, 0.f, 0.f}, f4m{0.f, 0.f, 0.f, 0.f}};
   const int kb = split * a.span, ke = min(a.L, kb + a.span);
   const uint8_t* mrow = a.mask ? a.mask + ((long long)bh * a.Q + (qv ? qrow : 0)) * a.L : nullptr;

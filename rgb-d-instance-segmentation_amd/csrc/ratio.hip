@@ -618,19 +618,32 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
   // the next tile's depth patch is prefetched into registers while the current one computes
   constexpr int PATCH_N = 3 * C2W_PH * C2W_PW, PATCH_PER = (PATCH_N + 511) / 512;
   float pre[PATCH_PER];
+  // Phases 1-2: the loads go through a buffer descriptor, unconditionally; an element outside the
+  // image or the patch gets an offset past the descriptor's end, which the hardware returns as
+  // zero.  Behind per-element branches (phase 0's form) the compiler waits for each load right
+  // where it is issued, so the "prefetch" stalled every phase-1 tile by a memory round trip
+  // (3 600 of 18 700 cycles in the stamps); this way nothing reads pre[] before the next tile's
+  // staging.  Phase 0 keeps the branches: at four workgroups per CU its waits are hidden, and
+  // the other form spilled it past its 128-register budget.
+  const long long dbytes = ((long long)(B - 1) * bstride + 3 * HW) * 4;
+  const bool dbuf = PHASE >= 1 && dbytes < (1ll << 31);  // 32-bit byte offsets cover the input
+  const __amdgpu_buffer_rsrc_t drs = wt_rsrc(depth3, dbuf ? (int)dbytes : 0);
   auto fetch_patch = [&](int t) {
     const TileDec td = tile_dec((unsigned)t, per, (unsigned)tiles_x, C2W_TH, C2W_TW);
-    const int b = td.b, y0 = td.y0, x0 = td.x0;
 #pragma unroll
     for (int k = 0; k < PATCH_PER; ++k) {
       const int i = tid + 512 * k;
-      float v = 0.f;
-      if (i < PATCH_N && t < ntiles) {
-        const int c = i / (C2W_PH * C2W_PW), yy = (i / C2W_PW) % C2W_PH, xx = i % C2W_PW;
-        const int yv = y0 + yy - 3, xv = x0 + xx - 3;
-        if (yv >= 0 && yv < H && xv >= 0 && xv < W) v = depth3[b * bstride + c * HW + (long long)yv * W + xv];
+      const int c = i / (C2W_PH * C2W_PW), yy = (i / C2W_PW) % C2W_PH, xx = i % C2W_PW;
+      const int yv = td.y0 + yy - 3, xv = td.x0 + xx - 3;
+      const bool ok = i < PATCH_N && t < ntiles && yv >= 0 && yv < H && xv >= 0 && xv < W;
+      if (dbuf) {
+        const uint32_t off = ok ? (uint32_t)((td.b * bstride + c * HW + (long long)yv * W + xv) * 4) : 0x80000000u;
+        pre[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(drs, off, 0, 0));
+      } else {
+        float v = 0.f;
+        if (ok) v = depth3[td.b * bstride + c * HW + (long long)yv * W + xv];
+        pre[k] = v;
       }
-      pre[k] = v;
     }
   };
   // per-lane statistics of a transposed accumulator tile (pixel validity only on ragged tiles)

@@ -108,22 +108,18 @@ __global__ __launch_bounds__(64 * SW_WAVES) void k_swin_attn(SwinArgs a) {
     const int t = lane;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      float e[8];
-      if (t < SW_T) {
-        const long long row = token_row(t, nullptr);
-        const int d0 = h * SW_HD + 8 * c;
-        if (row >= 0) {
-          Frag<T> f;
-          f.load(reinterpret_cast<const T*>(a.v) + row * a.ldq + d0);
-          f.to8(e);
-        } else {
+      // both sources loaded unconditionally (a clamped row; the bias when present), then
+      // selected: behind the branch each iteration's loads were waited for where issued
+      float e[8], fe[8], be[8];
+      const long long row = t < SW_T ? token_row(t, nullptr) : -1;
+      const int d0 = h * SW_HD + 8 * c;
+      Frag<T> f;
+      f.load(reinterpret_cast<const T*>(a.v) + (row >= 0 ? row : 0) * a.ldq + d0);
+      f.to8(fe);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) e[j] = a.bv ? Num<T>::to_f(Num<T>::from_f(a.bv[d0 + j])) : 0.f;
-        }
-      } else {
+      for (int j = 0; j < 8; ++j) be[j] = a.bv ? Num<T>::to_f(Num<T>::from_f(a.bv[d0 + j])) : 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = 0.f;
-      }
+      for (int j = 0; j < 8; ++j) e[j] = t < SW_T ? (row >= 0 ? fe[j] : be[j]) : 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) vt[(8 * c + j) * SwT<T>::VT_S + t] = Num<T>::from_f(e[j]);
     }
