@@ -419,15 +419,46 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(GArgs a, int batch) 
     const long long rem = t % ((long long)a.M * quads_per_row);
     const int m = (int)(rem / quads_per_row), n0 = (int)(rem % quads_per_row) * 4;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < a.splits; ++s) {
-      const float* p = a.part + (((long long)b * a.splits + s) * a.M + m) * a.N + n0;
+    const long long rbase = (long long)b * a.sr + (long long)m * a.ldr + n0;
+    if ((a.N & 3) == 0 && (((uintptr_t)a.part) & 15) == 0) {
+      // whole quads (16-byte aligned partial rows): one load per split, no branches, so the
+      // splits' loads and the epilogue's residual / bias loads are in flight together (behind
+      // per-element branches each was a memory round trip); same summation order
+#pragma unroll 4
+      for (int s = 0; s < a.splits; ++s) {
+        const float4 q = *reinterpret_cast<const float4*>(a.part + (((long long)b * a.splits + s) * a.M + m) * a.N + n0);
+        v[0] += q.x;
+        v[1] += q.y;
+        v[2] += q.z;
+        v[3] += q.w;
+      }
+      float rr[4], bb[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        rr[e] = a.R ? g_r<T>(a, rbase + e) : 0.f;
+        bb[e] = a.bias && a.act != RGBD_ACT_RELU_GRAD ? a.bias[a.bias_m ? m : n0 + e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (a.act == RGBD_ACT_RELU_GRAD) {
+          v[e] = rr[e] > 0.f ? v[e] : 0.f;
+          continue;
+        }
+        if (a.bias) v[e] += bb[e];
+        v[e] = g_act(v[e], a.act);
+        if (a.R) v[e] += rr[e];
+      }
+    } else {
+      for (int s = 0; s < a.splits; ++s) {
+        const float* p = a.part + (((long long)b * a.splits + s) * a.M + m) * a.N + n0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n0 + e < a.N) v[e] += p[e];
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (n0 + e < a.N) v[e] += p[e];
+        if (n0 + e < a.N) v[e] = g_epi<T>(v[e], m, n0 + e, rbase + e, a);
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (n0 + e < a.N) v[e] = g_epi<T>(v[e], m, n0 + e, (long long)b * a.sr + (long long)m * a.ldr + n0 + e, a);
     g_store<T>(a, b, m, n0, v);
   }
 }
