@@ -76,7 +76,8 @@ def pmc_traffic(kernel, default_shape):
     best = None
     for path in sorted((REPO / "profiles").glob("*/pmc_traffic.json")):
         for key, row in json.loads(path.read_text()).items():
-            if key.split(" grid=")[0] == kernel and "hbm_bytes" in row:
+            name = key.split(" grid=")[0]  # a template argument list (e.g. "<false>") aside
+            if (name == kernel or name.split("<")[0] == kernel) and "hbm_bytes" in row:
                 best = (row["hbm_bytes"], str(path.relative_to(REPO)))
     return best
 
