@@ -84,21 +84,23 @@ __global__ __launch_bounds__(64 * SW_WAVES) void k_swin_attn(SwinArgs a) {
     return ((long long)b * a.H + py) * a.W + px;
   };
   // 8 consecutive head dims (8g..8g+7) of token t's q / k / v row
+  // The row's load is unconditional (a clamped row) and only the rare lanes of padded tokens
+  // overwrite it: with the load inside an if / else the compiler waited for it at the join, so
+  // every call was a memory round trip.
   auto frag_of = [&](const void* base, const float* bias, int t) -> Frag<T> {
     Frag<T> f;
-    if (t >= SW_T) {
-      f.zero();
-      return f;
-    }
-    const long long row = token_row(t, nullptr);
+    const long long row = t < SW_T ? token_row(t, nullptr) : -1;
     const int d0 = h * SW_HD + 8 * g;
-    if (row >= 0) {
-      f.load(reinterpret_cast<const T*>(base) + row * a.ldq + d0);
-    } else {
-      float e[8];
+    f.load(reinterpret_cast<const T*>(base) + (row >= 0 ? row : 0) * a.ldq + d0);
+    if (row < 0) {
+      if (t >= SW_T) {
+        f.zero();
+      } else {
+        float e[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = bias ? bias[d0 + j] : 0.f;
-      f.from8(e);  // the GEMM output of a zero row: bias (rounded to the operand dtype)
+        for (int j = 0; j < 8; ++j) e[j] = bias ? bias[d0 + j] : 0.f;
+        f.from8(e);  // the GEMM output of a zero row: bias (rounded to the operand dtype)
+      }
     }
     return f;
   };
@@ -106,20 +108,23 @@ __global__ __launch_bounds__(64 * SW_WAVES) void k_swin_attn(SwinArgs a) {
   // V^T into LDS: lane = token, its 32 dims as four 8-dim fragments
   {
     const int t = lane;
+    // the row's four fragments loaded first and unconditionally (a clamped row), then converted;
+    // only the rare lanes of padded tokens overwrite them with the bias (as frag_of): inside an
+    // if / else, or converted as they arrive, each load was a memory round trip of its own
+    const long long row = t < SW_T ? token_row(t, nullptr) : -1;
+    Frag<T> fv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) fv[c].load(reinterpret_cast<const T*>(a.v) + (row >= 0 ? row : 0) * a.ldq + h * SW_HD + 8 * c);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      // both sources loaded unconditionally (a clamped row; the bias when present), then
-      // selected: behind the branch each iteration's loads were waited for where issued
-      float e[8], fe[8], be[8];
-      const long long row = t < SW_T ? token_row(t, nullptr) : -1;
       const int d0 = h * SW_HD + 8 * c;
-      Frag<T> f;
-      f.load(reinterpret_cast<const T*>(a.v) + (row >= 0 ? row : 0) * a.ldq + d0);
-      f.to8(fe);
+      float e[8];
+      fv[c].to8(e);
+      if (row < 0) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) be[j] = a.bv ? Num<T>::to_f(Num<T>::from_f(a.bv[d0 + j])) : 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = t < SW_T ? (row >= 0 ? fe[j] : be[j]) : 0.f;
+        for (int j = 0; j < 8; ++j)
+          e[j] = t < SW_T && a.bv ? Num<T>::to_f(Num<T>::from_f(a.bv[d0 + j])) : 0.f;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) vt[(8 * c + j) * SwT<T>::VT_S + t] = Num<T>::from_f(e[j]);
     }
