@@ -23,3 +23,17 @@ def test_bench_launcher_propagates_failure():
     r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--launcher-selftest",
                         "--dtype", "nope"], capture_output=True, text=True, timeout=180, cwd=REPO)
     assert r.returncode != 0
+
+
+def test_bench_roofline_traffic_comes_from_the_newest_pmc_table():
+    """roofline.traffic: conv5's HBM bytes from the newest committed PMC table, whatever template
+    argument list the kernel's trace name carries (k_rp_conv3x3_v3<false> since the stamped
+    instantiation exists), and null for a non-default shape."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    tables = sorted((REPO / "profiles").glob("*/pmc_traffic.json"))
+    assert tables
+    got = bench.pmc_traffic(bench.CONV5_KERNEL, True)
+    assert got is not None and got[0] > 1e9
+    assert got[1] == str(tables[-1].relative_to(REPO))
+    assert bench.pmc_traffic(bench.CONV5_KERNEL, False) is None
