@@ -474,18 +474,6 @@ int rgbd_pack_mask_bits(const uint8_t* masks, int n, long long npx, unsigned lon
 int rgbd_mask_intersections(const unsigned long long* a, int na, const unsigned long long* b, int nb, long long npx,
                             int* inter, void* stream);
 
-/* dW of up to three bf16 DSAM legs as ONE segment GEMM (k_dsam_segw): per leg the five filters'
- * gradients straight from the reference's form — conv_i's from x * bit_i of the source pixel's
- * region code, the projection's from x (custom_model.py:682-699) — accumulated together over all
- * output pixels, without the code-merged path's planning, per-code partials and combine; a leg
- * whose output tiles are too few for the chip splits its pixel range (fixed order sum).  Same
- * outputs as rgbd_dsam_bwd_weight_planned_multi up to float32 summation order.  runs[i].plan is
- * not used; runs[i].ws: rgbd_dsam_seg_workspace_size bytes, distinct per run.  Cin % 32 == 0,
- * Cout % 64 == 0. */
-size_t rgbd_dsam_seg_workspace_size(int B, int Cin, int h, int w, int Cout);
-int rgbd_dsam_bwd_weight_seg(int n, const rgbd_dsam_dw_run* runs, const rgbd_decomp_info* info,
-                             void* stream);
-
 /* ---------------------------------------------------------------- f1 / f2 dense layers
  * The nn.Linear layers of the Mask2Former decoder (transformers 5.15 modeling_mask2former.py:
  * self_attn q/k/v/out_proj :1480-1483, fc1/fc2 :1711-1714), of the pixel decoder's encoder
@@ -580,21 +568,6 @@ int rgbd_swin_window_attn(int dtype, const void* q, const void* k, const void* v
  * "dsam_dx", "dsam_wgrad", "decompose", "dggm_fwd", "dggm_bwd", "assemble"), then resets.
  * Do not enable while a stream is being captured into a graph. */
 int rgbd_timing_enable(int on);
-/* Diagnostics: buf (device, >= 2 * 18 * 8 * 5 uint64) receives, for workgroup 0 of every later
- * conv5 launch (k_rp_conv3x3_v3), s_memtime stamps per wave and K step of its first two tiles
- * (step top, after the DMA issue, after k-step 0 / 1's MFMAs, after the closing wait); NULL stops. */
-int rgbd_debug_conv5_stamps(void* buf);
-/* The same for the bf16 chain kernels (k_rp_chain_v2 phases 0 and 1): buf (device, >= 2 * 4 * 8 * 7
- * uint64) receives workgroup 0's stamps for its tiles 8-11 (tile top, patch staged, next
- * patch issued, stem MFMAs issued, stem ReLU/pack, fusion MFMAs issued, tile end), phase-major
- * (phase 0 writes the first four points).  NULL stops. */
-int rgbd_debug_chain_stamps(void* buf);
-/* The same for the DSAM conv legs (k_dsam_lds, the forward cascade and dX): buf (device, >= launches
- * * 256 * 4 * 8 uint64) receives, for the next `launches` launches, per workgroup and for its first
- * four work items: s_memtime at item taken, tables built, first DMA landed, K loop done, partial
- * hand-off done, epilogue done; steps | chunks << 16 | chunk << 24; the item word.  (NULL, 0)
- * stops. */
-int rgbd_debug_dsam_stamps(void* buf, int launches);
 double rgbd_timing_read(const char* name, int* count);
 
 #ifdef __cplusplus

@@ -1,0 +1,32 @@
+/* Diagnostic entry points of the DIAGNOSTIC build only (librgbd_hip_diag.so, `make -C
+ * rgb-d-instance-segmentation_amd/csrc diag`, compiled with -DRGBD_DIAG).  The product library
+ * (librgbd_hip.so) neither exports these nor contains the stamped kernel instantiations; the
+ * tools that read them (tools/conv5_stamps.py, tools/chain_stamps.py, tools/dsam_stamps.py) load
+ * the diagnostic build through RGBD_HIP_LIB. */
+#ifndef RGBD_HIP_DIAG_H
+#define RGBD_HIP_DIAG_H
+#include "rgbd_hip.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Diagnostics: buf (device, >= 2 * 18 * 8 * 5 uint64) receives, for workgroup 0 of every later
+ * conv5 launch (k_rp_conv3x3_v3), s_memtime stamps per wave and K step of its first two tiles
+ * (step top, after the DMA issue, after k-step 0 / 1's MFMAs, after the closing wait); NULL stops. */
+int rgbd_debug_conv5_stamps(void* buf);
+/* The same for the bf16 chain kernels (k_rp_chain_v2 phases 0 and 1): buf (device, >= 2 * 4 * 8 * 7
+ * uint64) receives workgroup 0's stamps for its tiles 8-11 (tile top, patch staged, next
+ * patch issued, stem MFMAs issued, stem ReLU/pack, fusion MFMAs issued, tile end), phase-major
+ * (phase 0 writes the first four points).  NULL stops. */
+int rgbd_debug_chain_stamps(void* buf);
+/* The same for the DSAM conv legs (k_dsam_lds, the forward cascade and dX): buf (device, >= launches
+ * * 256 * 4 * 8 uint64) receives, for the next `launches` launches, per workgroup and for its first
+ * four work items: s_memtime at item taken, tables built, first DMA landed, K loop done, partial
+ * hand-off done, epilogue done; steps | chunks << 16 | chunk << 24; the item word.  (NULL, 0)
+ * stops. */
+int rgbd_debug_dsam_stamps(void* buf, int launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RGBD_HIP_DIAG_H */

@@ -79,8 +79,6 @@ SIGNATURES = {
     "rgbd_dsam_bwd_data_planned": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_weight_planned": (_I, [_I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_dsam_bwd_weight_planned_multi": (_I, [_I, _P, _P, _P]),
-    "rgbd_dsam_seg_workspace_size": (_SZ, [_I, _I, _I, _I, _I]),
-    "rgbd_dsam_bwd_weight_seg": (_I, [_I, _P, _P, _P]),
     "rgbd_point_sample": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P]),
     "rgbd_point_sample_t": (_I, [_I, _P, _I, _I, _I, _P, _I, _I, _P, _P]),
     "rgbd_point_sample_bwd": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P]),
@@ -113,9 +111,6 @@ SIGNATURES = {
     "rgbd_swin_window_attn": (_I, [_I, _P, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
                                    _LL, _P]),
     "rgbd_timing_enable": (_I, [_I]),
-    "rgbd_debug_conv5_stamps": (_I, [_P]),
-    "rgbd_debug_chain_stamps": (_I, [_P]),
-    "rgbd_debug_dsam_stamps": (_I, [_P, _I]),
     "rgbd_timing_read": (ctypes.c_double, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "rgbd_ratio_packed_size": (_SZ, [_I]),
     "rgbd_ratio_pack": (_I, [_I, _P, _P, _P]),
@@ -123,6 +118,14 @@ SIGNATURES = {
     "rgbd_ratio_features_offset": (_SZ, [_I, _I, _I, _I]),
     "rgbd_ratio_forward": (_I, [_I, _I, ctypes.c_float, _P, _LL, _I, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P,
                                 _P, _P]),
+}
+
+# the diagnostic build's extra entry points (include/rgbd_hip_diag.h; librgbd_hip_diag.so via
+# RGBD_HIP_LIB), bound only when the loaded library exports them
+DIAG_SIGNATURES = {
+    "rgbd_debug_conv5_stamps": (_I, [_P]),
+    "rgbd_debug_chain_stamps": (_I, [_P]),
+    "rgbd_debug_dsam_stamps": (_I, [_P, _I]),
 }
 
 _lib = None
@@ -146,6 +149,11 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in DIAG_SIGNATURES.items():
+            if hasattr(h, name):
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
         _lib = h
     return _lib
 

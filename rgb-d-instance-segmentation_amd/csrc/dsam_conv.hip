@@ -1901,23 +1901,28 @@ hipError_t plan_convs(int n, const ConvArgs* legs, hipStream_t s) {
   return hipGetLastError();
 }
 
-// rgbd_debug_dsam_stamps: buffer, its capacity in launches, launches stamped so far
+#ifdef RGBD_DIAG
+// rgbd_debug_dsam_stamps (diagnostic build only): buffer, its capacity in launches, launches
+// stamped so far
 unsigned long long* g_ld_stamps = nullptr;
 int g_ld_stamp_cap = 0, g_ld_stamp_n = 0;
+#endif
 template <int KC>
 hipError_t launch_ld(const ConvArgs& b, dim3 grid, hipStream_t s) {
-  static const hipError_t attr[2] = {
-      hipFuncSetAttribute((const void*)k_dsam_lds<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LdCfg<KC>::SMEM),
-      hipFuncSetAttribute((const void*)k_dsam_lds<KC, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)LdCfg<KC>::SMEM)};
-  if (attr[0] != hipSuccess) return attr[0];
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)k_dsam_lds<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LdCfg<KC>::SMEM);
+  if (attr != hipSuccess) return attr;
+#ifdef RGBD_DIAG
+  static const hipError_t sattr = hipFuncSetAttribute((const void*)k_dsam_lds<KC, true>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)LdCfg<KC>::SMEM);
   if (g_ld_stamps && g_ld_stamp_n < g_ld_stamp_cap && grid.x * grid.y <= 256) {
-    if (attr[1] != hipSuccess) return attr[1];
+    if (sattr != hipSuccess) return sattr;
     ConvArgs c = b;
     c.stamps = g_ld_stamps + (size_t)g_ld_stamp_n++ * 256 * LD_STAMP_ITEMS * 8;
     k_dsam_lds<KC, true><<<grid, 512, LdCfg<KC>::SMEM, s>>>(c);
     return hipSuccess;
   }
+#endif
   k_dsam_lds<KC><<<grid, 512, LdCfg<KC>::SMEM, s>>>(b);
   return hipSuccess;
 }
@@ -2004,250 +2009,6 @@ int dsam_wgrad_splits(int B, int Cin, int Cout) {
   return sp < 1 ? 1 : sp;
 }
 
-// ----------------------------------------------------------------------- bf16 dW: segment GEMM
-// dW of the five filters of a DSAModule straight from the reference's form
-//   dconv_i[o][c][tap] = sum_p G[p][o] * x[src(p, tap)][c] * bit_i(code(src(p, tap)))   (i < 4)
-//   dproj[o][c][tap]   = sum_p G[p][o] * x[src(p, tap)][c]
-// (custom_model.py:682-699: conv_i sees x * pool(m_i); the projection sees x) as ONE GEMM over
-// all output pixels p with five accumulators, instead of per-code GEMMs with per-item partials
-// and a combine.  Work item = (split of the pixel range, 64 output channels, 128 kk = four
-// 32-channel blocks, each inside one tap).  Per step (64 output pixels of one image) G rows
-// [64 px][64 o] and X rows [64 px][4 x 32 c] (zero rows where the source is outside the input or
-// the pixel past the image) arrive by LDS-DMA in a 3-stage ring; the wave of block j also
-// writes the 64 source codes of its block and their summary (the set of codes present).  A
-// segment whose bit no pixel of the block carries is skipped; a block with a single code
-// multiplies its segments unmasked; otherwise the lane zeroes, per segment, the bf16 values of
-// its 8 pixels whose code lacks the bit.  4 waves as 2 (32 o) x 2 (64 kk); acc [5][2][4].
-constexpr int SG_OT = 64, SG_KT = 128, SG_PX = 64, SG_S = 3;
-constexpr int SG_BLK = SG_PX * 64;                   // one 32-column block of 64 rows: 4 KB
-constexpr int SG_CODES = 6 * SG_BLK;                 // [4][64] u8 source codes
-constexpr int SG_SUM = SG_CODES + 4 * SG_PX;          // [4] u32 code-presence per block
-constexpr int SG_STAGE = (SG_SUM + 16 + 1023) / 1024 * 1024;  // 1 KB-aligned stages
-constexpr size_t SG_SMEM = (size_t)SG_S * SG_STAGE;
-static_assert(2 * SG_SMEM <= 163840, "segment dW: two workgroups per CU");
-constexpr int SG_MAXLEG = 3;
-
-struct SegLeg {
-  const bf16_t* gout;  // NHWC [B][ho][wo][Cout]
-  const bf16_t* x;     // NHWC [B][h][w][Cin]
-  const uint8_t* code; // [B][h][w]
-  int B, Cin, h, w, Cout, ho, wo, nunit, ntile_o, ntile_kk, nsplit, items;
-  float inv_wo;
-  const bf16_t* zero;  // LD_ZERO_BYTES of zeros
-  float* dconv;        // [4][Cout][Cin][9]   (nsplit == 1)
-  float* dproj;        // [Cout][Cin][9]      (nsplit == 1)
-  float* partial;      // [nsplit][5][Cout][9 Cin] (nsplit > 1)
-};
-struct SegLegs {
-  SegLeg l[SG_MAXLEG];
-  int first[SG_MAXLEG + 1];  // first workgroup of each leg
-  int n;
-};
-
-// 8 bf16 of a fragment kept where bit `seg` of the pixel's code is set (codes: 8 bytes, one per
-// bf16 element in order)
-__device__ __forceinline__ Frag<bf16_t> seg_mask(const Frag<bf16_t>& f, uint32_t c_lo, uint32_t c_hi, int seg) {
-  const uint32_t blo = ((c_lo >> seg) & 0x01010101u) * 0xffu, bhi = ((c_hi >> seg) & 0x01010101u) * 0xffu;
-  Frag<bf16_t> o;
-  // byte k of b* = 0xff when element k is kept: widen to 16-bit lanes ([m0 m0 m1 m1], [m2 m2 m3 m3])
-  o.v.x = f.v.x & __builtin_amdgcn_perm(blo, blo, 0x01010000u);
-  o.v.y = f.v.y & __builtin_amdgcn_perm(blo, blo, 0x03030202u);
-  o.v.z = f.v.z & __builtin_amdgcn_perm(bhi, bhi, 0x01010000u);
-  o.v.w = f.v.w & __builtin_amdgcn_perm(bhi, bhi, 0x03030202u);
-  return o;
-}
-
-__global__ __launch_bounds__(256, 2) void k_dsam_segw(const SegLegs Ls) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  int leg = 0;
-  while (leg + 1 < Ls.n && (int)blockIdx.x >= Ls.first[leg + 1]) ++leg;
-  const SegLeg& a = Ls.l[leg];
-  const int item = blockIdx.x - Ls.first[leg];
-  const int split = item / (a.ntile_o * a.ntile_kk);
-  const int tile = item % (a.ntile_o * a.ntile_kk);
-  const int o0 = (tile / a.ntile_kk) * SG_OT, kk0 = (tile % a.ntile_kk) * SG_KT;
-  const int KK = 9 * a.Cin, hwo = a.ho * a.wo, U = a.B * a.nunit;
-  const int u_begin = (int)((long long)U * split / a.nsplit), u_end = (int)((long long)U * (split + 1) / a.nsplit);
-  const int nst = u_end - u_begin;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int wm = wave & 1, wn = wave >> 1;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  // copy roles: pixel row pr, 16-byte chunk of the 64-byte row
-  const int pr = 16 * wave + (lane >> 2);
-  const int qch = 8 * ((lane & 3) ^ wg_swz(pr));
-  // X block j: tap and channel offset (uniform); live when inside 9*Cin
-  int xtap[4], xoff[4], xc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int kk = kk0 + 32 * j;
-    const bool ok = kk < KK;
-    xtap[j] = ok ? kk / a.Cin : -1;
-    const int tp = ok ? xtap[j] : 0;
-    xoff[j] = (tp / 3) * a.w + tp % 3;
-    xc[j] = ok ? kk % a.Cin : 0;
-  }
-  // transposed-fragment bases (k = 8g + j, col = c0 + r) of a [64 px][32 col] block, as k_dsam_wgrad_mm
-  const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-  const int trow = 8 * g + q4;
-  const int tbase0 = trow * 64 + 16 * ((p4 >> 1) ^ wg_swz(trow)) + (4 * p4 & 7) * 2;
-  const int tbase16 = trow * 64 + 16 * ((2 | (p4 >> 1)) ^ wg_swz(trow)) + (4 * p4 & 7) * 2;
-  typedef __attribute__((address_space(3))) char lds_char;
-  typedef __attribute__((address_space(3))) v4s lds_v4s;
-  lds_char* const lsm = (lds_char*)smem;
-  auto trfrag = [&](int st, int blk, int kb, int c0) {
-    lds_char* p = lsm + st + (c0 ? tbase16 : tbase0) + blk * SG_BLK + kb * 32 * 64;
-    const v4s t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p);
-    const v4s t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p + 4 * 64));
-    Frag<bf16_t> f;
-    const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
-    f.v = make_uint4(u0.x, u0.y, u1.x, u1.y);
-    return f;
-  };
-  const bf16_t* zrow = a.zero + qch;
-  auto issue = [&](int slot, int step) {
-    const int u = u_begin + step;
-    const int b = u / a.nunit;
-    const int p = (u - b * a.nunit) * SG_PX + pr;
-    const bool pin = p < hwo;
-    const int pc = pin ? p : hwo - 1;
-    const int oy = (int)(((float)pc + 0.5f) * a.inv_wo), ox = pc - oy * a.wo;
-    const uint32_t sb = lds0 + slot * SG_STAGE + wave * 1024;
-    const bf16_t* gsrc = a.gout + ((long long)b * hwo + pc) * a.Cout + o0 + qch;
-#pragma unroll
-    for (int ob = 0; ob < 2; ++ob) dma_lds16(pin ? gsrc + 32 * ob : zrow, sb + ob * SG_BLK);
-    const int iy0 = 2 * oy - 1, ix0 = 2 * ox - 1;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int tp = xtap[j] < 0 ? 0 : xtap[j];
-      const int iy = iy0 + tp / 3, ix = ix0 + tp % 3;
-      const bool live = pin && xtap[j] >= 0 && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
-      const bf16_t* src = live ? a.x + ((long long)(b * a.h + iy) * a.w + ix) * a.Cin + xc[j] + qch : zrow;
-      dma_lds16(src, sb + (2 + j) * SG_BLK);
-    }
-    // wave j: the 64 source codes of block j at this step and the set of codes present
-    {
-      const int j = wave;
-      const int pl = (u - b * a.nunit) * SG_PX + lane;
-      const bool ok_p = pl < hwo && xtap[j] >= 0;
-      const int pcl = ok_p ? pl : 0;
-      const int oyl = (int)(((float)pcl + 0.5f) * a.inv_wo), oxl = pcl - oyl * a.wo;
-      const int tp = xtap[j] < 0 ? 0 : xtap[j];
-      const int iy = 2 * oyl - 1 + tp / 3, ix = 2 * oxl - 1 + tp % 3;
-      const bool ok = ok_p && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
-      const uint32_t c = ok ? a.code[((long long)b * a.h + iy) * a.w + ix] & 15u : 0u;
-      char* cs = smem + slot * SG_STAGE;
-      cs[SG_CODES + j * SG_PX + lane] = (char)c;
-      uint32_t pres = ok ? (1u << c) : 0u;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) pres |= (uint32_t)__shfl_xor((int)pres, o);
-      if (lane == 0) reinterpret_cast<uint32_t*>(cs + SG_SUM)[j] = pres;
-    }
-  };
-  f32x4 acc[5][2][4];
-#pragma unroll
-  for (int sg = 0; sg < 5; ++sg)
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj) acc[sg][mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int PER = 6;  // DMA pieces per wave per step
-  const int npro = nst < SG_S - 1 ? nst : SG_S - 1;
-  for (int i = 0; i < npro; ++i) issue(i, i);
-  if (npro >= 2) vm_wait_barrier<PER>();
-  else vm_wait_barrier<0>();
-#pragma unroll 1
-  for (int s = 0; s < nst; ++s) {
-    if (s + SG_S - 1 < nst) issue((s + SG_S - 1) % SG_S, s + SG_S - 1);
-    int st = (s % SG_S) * SG_STAGE;
-    asm volatile("" : "+s"(st));
-    const uint32_t* sum = reinterpret_cast<const uint32_t*>(smem + st + SG_SUM);
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      Frag<bf16_t> fa[2];
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) fa[mi] = trfrag(st, wm, kb, 16 * mi);
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int j = 2 * wn + jj;
-        const uint32_t pres = __builtin_amdgcn_readfirstlane(sum[j]);
-        if (pres == 0u) continue;  // no live source pixel: the block adds nothing
-        Frag<bf16_t> fb[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) fb[h] = trfrag(st, 2 + j, kb, 16 * h);
-        uint32_t segs = 0u;
-#pragma unroll
-        for (int k = 1; k < 16; ++k)
-          if ((pres >> k) & 1u) segs |= (uint32_t)k;
-        const bool uniform = (pres & (pres - 1u)) == 0u;
-        const uint2 cc = *reinterpret_cast<const uint2*>(smem + st + SG_CODES + j * SG_PX + kb * 32 + 8 * g);
-#pragma unroll
-        for (int sg = 0; sg < 5; ++sg) {
-          if (sg < 4 && !((segs >> sg) & 1u)) continue;
-          Frag<bf16_t> fm[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) fm[h] = (sg == 4 || uniform) ? fb[h] : seg_mask(fb[h], cc.x, cc.y, sg);
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) mma(acc[sg][mi][2 * jj + h], fa[mi], fm[h]);
-        }
-      }
-    }
-    const int ahead = (nst - 1 < s + SG_S - 1 ? nst - 1 : s + SG_S - 1) - (s + 1);
-    if (ahead >= 1) vm_wait_barrier<PER>();
-    else vm_wait_barrier<0>();
-  }
-  // accumulator (o = o0 + wm*32 + 16 mi + 4 g + reg, kk = kk0 + wn*64 + 16 nj + r)
-#pragma unroll
-  for (int sg = 0; sg < 5; ++sg)
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int o = o0 + wm * 32 + 16 * mi + 4 * g + reg;
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj) {
-          const int kk = kk0 + wn * 64 + 16 * nj + r;
-          if (o >= a.Cout || kk >= KK) continue;
-          const float v = acc[sg][mi][nj][reg];
-          if (a.nsplit > 1) {
-            a.partial[(((long long)split * 5 + sg) * a.Cout + o) * KK + kk] = v;
-          } else {
-            const int tap = kk / a.Cin, c = kk - tap * a.Cin;
-            float* dst = sg < 4 ? a.dconv + (long long)sg * a.Cout * KK : a.dproj;
-            dst[((long long)o * a.Cin + c) * 9 + tap] = v;
-          }
-        }
-      }
-}
-
-// the split partials summed in split order into the OIHW filters; thread = (leg, seg, o, kk)
-__global__ __launch_bounds__(256) void k_dsam_segw_combine(const SegLegs Ls, long long total0, long long total1) {
-  long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-  int leg = 0;
-  if (t >= total0) {
-    t -= total0;
-    leg = 1;
-    if (t >= total1) {
-      t -= total1;
-      leg = 2;
-    }
-  }
-  const SegLeg& a = Ls.l[leg];
-  if (leg >= Ls.n || a.nsplit <= 1) return;
-  const int KK = 9 * a.Cin;
-  const long long per = 5ll * a.Cout * KK;
-  if (t >= per) return;
-  const int kk = (int)(t % KK), o = (int)((t / KK) % a.Cout), sg = (int)(t / ((long long)KK * a.Cout));
-  float s = 0.f;
-  for (int sp = 0; sp < a.nsplit; ++sp) s += a.partial[sp * per + t];
-  const int tap = kk / a.Cin, c = kk - tap * a.Cin;
-  float* dst = sg < 4 ? a.dconv + (long long)sg * a.Cout * KK : a.dproj;
-  dst[((long long)o * a.Cin + c) * 9 + tap] = s;
-}
 
 }  // namespace
 
@@ -2689,99 +2450,6 @@ int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, cons
 }
 
 
-// ---- bf16 dW as the segment GEMM (k_dsam_segw): no planning, no per-code partials
-static int seg_splits(int B, int Cin, int h, int w, int Cout) {
-  const int ho = (h + 1) / 2, wo = (w + 1) / 2;
-  const long long units = (long long)B * ceil_div(ho * wo, SG_PX);
-  const long long tiles = (long long)ceil_div(Cout, SG_OT) * ceil_div(9 * Cin, SG_KT);
-  long long sp = ceil_div(512, tiles);                     // about two workgroups per CU
-  sp = std::min<long long>(sp, std::max<long long>(1, units / 8));  // at least 8 steps per split
-  return (int)std::max<long long>(1, std::min<long long>(sp, 32));
-}
-struct SegWs {
-  size_t zero, csum, partial, total;
-};
-static SegWs seg_ws(int B, int Cin, int h, int w, int Cout) {
-  SegWs o;
-  const int ho = (h + 1) / 2, wo = (w + 1) / 2;
-  const int sp = seg_splits(B, Cin, h, w, Cout);
-  size_t off = 0;
-  o.zero = off;
-  off += align256(LD_ZERO_BYTES);
-  o.csum = off;
-  off += align256((size_t)chan_sum_splits(ho * wo) * B * Cout * sizeof(float));
-  o.partial = off;
-  off += sp > 1 ? align256((size_t)sp * 5 * Cout * 9 * Cin * sizeof(float)) : 0;
-  o.total = off;
-  return o;
-}
-
-size_t rgbd_dsam_seg_workspace_size(int B, int Cin, int h, int w, int Cout) {
-  if (B <= 0 || h <= 0 || w <= 0 || Cin <= 0 || Cout <= 0) return 256;
-  return seg_ws(B, Cin, h, w, Cout).total;
-}
-
-int rgbd_dsam_bwd_weight_seg(int n, const rgbd_dsam_dw_run* runs, const rgbd_decomp_info* info, void* stream) {
-  RGBD_REQUIRE(n >= 1 && n <= SG_MAXLEG && runs && info, RGBD_E_ARG);
-  hipStream_t s = (hipStream_t)stream;
-  TimerScope ts("dsam_wgrad", s);
-  SegLegs L;
-  L.n = n;
-  long long blocks = 0, ctot[SG_MAXLEG] = {0, 0, 0};
-  bool any_split = false;
-  float* csum[SG_MAXLEG];
-  for (int i = 0; i < n; ++i) {
-    const rgbd_dsam_dw_run& r = runs[i];
-    RGBD_REQUIRE(r.gout_nhwc && r.x_nhwc && r.code && r.dconv_w && r.dproj_w && r.dbias && r.ws, RGBD_E_ARG);
-    RGBD_REQUIRE(r.B > 0 && r.h > 0 && r.w > 0 && r.Cout > 0 && r.Cin > 0, RGBD_E_ARG);
-    RGBD_REQUIRE(r.Cin % 32 == 0 && r.Cout % SG_OT == 0, RGBD_E_SHAPE);
-    for (int k = 0; k < i; ++k) RGBD_REQUIRE(runs[k].ws != r.ws, RGBD_E_ARG);
-    const SegWs W = seg_ws(r.B, r.Cin, r.h, r.w, r.Cout);
-    SegLeg& a = L.l[i];
-    a.gout = (const bf16_t*)r.gout_nhwc;
-    a.x = (const bf16_t*)r.x_nhwc;
-    a.code = r.code;
-    a.B = r.B; a.Cin = r.Cin; a.h = r.h; a.w = r.w; a.Cout = r.Cout;
-    a.ho = (r.h + 1) / 2; a.wo = (r.w + 1) / 2;
-    a.nunit = ceil_div(a.ho * a.wo, SG_PX);
-    a.ntile_o = ceil_div(r.Cout, SG_OT);
-    a.ntile_kk = ceil_div(9 * r.Cin, SG_KT);
-    a.nsplit = seg_splits(r.B, r.Cin, r.h, r.w, r.Cout);
-    a.items = a.nsplit * a.ntile_o * a.ntile_kk;
-    a.inv_wo = 1.f / (float)a.wo;
-    a.zero = (const bf16_t*)((char*)r.ws + W.zero);
-    a.dconv = r.dconv_w;
-    a.dproj = r.dproj_w;
-    a.partial = (float*)((char*)r.ws + W.partial);
-    L.first[i] = (int)blocks;
-    blocks += a.items;
-    if (a.nsplit > 1) {
-      any_split = true;
-      ctot[i] = 5ll * r.Cout * 9 * r.Cin;
-    }
-    csum[i] = (float*)((char*)r.ws + W.csum);
-    const hipError_t ez = hipMemsetAsync((char*)r.ws + W.zero, 0, LD_ZERO_BYTES, s);
-    if (ez != hipSuccess) return (int)ez;
-    const int hwo = a.ho * a.wo;
-    k_chan_sum_nhwc<<<dim3(r.B, ceil_div(r.Cout, 64), chan_sum_splits(hwo)), 256, 0, s>>>(a.gout, hwo, r.Cout, csum[i]);
-  }
-  L.first[n] = (int)blocks;
-  RGBD_REQUIRE(blocks < (1ll << 31), RGBD_E_SHAPE);
-  static const hipError_t attr =
-      hipFuncSetAttribute((const void*)k_dsam_segw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SG_SMEM);
-  if (attr != hipSuccess) return (int)attr;
-  k_dsam_segw<<<(unsigned)blocks, 256, SG_SMEM, s>>>(L);
-  if (any_split) {
-    const long long tot = ctot[0] + ctot[1] + ctot[2];
-    k_dsam_segw_combine<<<(unsigned)ceil_div(tot, 256), 256, 0, s>>>(L, ctot[0], ctot[1]);
-  }
-  for (int i = 0; i < n; ++i) {
-    const SegLeg& a = L.l[i];
-    k_dsam_bias_grad<<<a.Cout, 256, 0, s>>>(csum[i], info, a.B, a.Cout, chan_sum_splits(a.ho * a.wo), runs[i].dbias);
-  }
-  RGBD_CHECK_LAUNCH();
-  return RGBD_OK;
-}
 // ---- planning ahead (bf16): the code-dependent set-up of a leg depends only on the region codes,
 // so the hot path plans every leg of the step once, right after the decomposition
 static ConvArgs leg_conv_args(const rgbd_dsam_leg& g) {
@@ -2808,6 +2476,7 @@ size_t rgbd_dsam_run_workspace_size(int kind, int B, int Cin, int h, int w, int 
   }
   return std::max<size_t>(256, ld_plan(leg_conv_args(g)).partial_bytes);
 }
+#ifdef RGBD_DIAG
 int rgbd_debug_dsam_stamps(void* buf, int launches) {
   RGBD_REQUIRE(buf ? launches > 0 : launches == 0, RGBD_E_ARG);  // (NULL, 0) stops
   g_ld_stamps = (unsigned long long*)buf;
@@ -2815,6 +2484,7 @@ int rgbd_debug_dsam_stamps(void* buf, int launches) {
   g_ld_stamp_n = 0;
   return RGBD_OK;
 }
+#endif
 
 int rgbd_dsam_plan(int n, const rgbd_dsam_leg* legs, void* stream) {
   RGBD_REQUIRE(n > 0 && legs, RGBD_E_ARG);

@@ -739,26 +739,6 @@ int launch_lds(const GArgs& a, hipStream_t s) {
   return RGBD_OK;
 }
 
-// RGBD_GEMM_LDS (A/B, read once): default / 2 = 128 x 128 tiles with a 2-stage ring (64 KB of LDS:
-// two workgroups per CU, one's prologue and epilogue under the other's MFMAs); 3 = one workgroup
-// per CU with a 3-stage ring (128 x 256 tiles when N % 256 == 0); 0 = k_gemm for every shape.
-// Measured (tools/micro_gemm.py, profiles/r04_v3/micro_gemm_lds.txt): the 2-stage form is
-// 1.2-1.6x faster than the 3-stage one on the drop-in model's shapes.
-inline bool gemm_lds_tt_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RGBD_GEMM_LDS_TT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-inline int gemm_lds_mode() {
-  static const int mode = [] {
-    const char* e = getenv("RGBD_GEMM_LDS");
-    return e && (e[0] == '0' || e[0] == '3') ? e[0] - '0' : 2;
-  }();
-  return mode;
-}
-
 template <typename T, int TM, int TN, bool AT, bool BT>
 void launch_t(const GArgs& a, int batch, hipStream_t s) {
   dim3 grid(ceil_div(a.N, TN), ceil_div(a.M, TM), batch * a.splits);
@@ -781,15 +761,16 @@ int gemm_t(GArgs a, int at, int bt, int batch, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     // the LDS-DMA kernel: bf16, both operands K-contiguous and 16-byte aligned, one GEMM, no split
     if (!at && !bt && batch == 1 && a.splits == 1 && a.vec_a && a.vec_b && a.K % 8 == 0 && !a.bias_m &&
-        a.M >= 1024 && gemm_lds_mode() != 0) {
-      if (gemm_lds_mode() == 3)
-        return a.N % 256 == 0 ? launch_lds<128, 256, 3>(a, s) : launch_lds<128, 128, 3>(a, s);
+        a.M >= 1024) {
+      // 128 x 128 tiles with a 2-stage ring (64 KB of LDS: two workgroups per CU, one's prologue
+      // and epilogue under the other's MFMAs); measured 1.2-1.6x faster than one workgroup per
+      // CU with a 3-stage ring on the drop-in model's shapes (profiles/r04_v3/micro_gemm_lds.txt)
       return launch_lds<128, 128, 2>(a, s);
     }
     // weight gradients (both operands token-major): the LDS-DMA kernel with transposed fragment
-    // reads; RGBD_GEMM_LDS_TT=0 keeps them on k_gemm (A/B)
+    // reads (profiles/r04_v5/micro_gemm_dw_tt_ab.txt)
     if (at && bt && batch == 1 && a.vec_a && a.vec_b && a.M % 8 == 0 && a.N % 8 == 0 && !a.bias_m && !a.R &&
-        a.K >= 1024 && gemm_lds_tt_enabled())
+        a.K >= 1024)
       return launch_lds<128, 128, 2, true>(a, s);
   }
   // 128 x 128 tiles when they give the chip enough workgroups, else 64 x 64

@@ -324,15 +324,6 @@ __global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ val
 
 constexpr int MSDA_RUN = 8;  // queries per run of k_msda_bwd_runs
 
-// RGBD_MSDA_RUNS=0 selects the per-query backward (A/B); read once
-inline bool msda_runs_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RGBD_MSDA_RUNS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 int msda_levels(int L, const int* shapes_host, MsdaLevels& lv, int& S) {
   if (L < 1 || L > MSDA_MAX_L || !shapes_host) return RGBD_E_SHAPE;
   lv.L = L;
@@ -362,7 +353,7 @@ int launch_bwd(const void* value, const MsdaLevels& lv, int B, int S, int Q, int
   const hipError_t e = hipMemsetAsync(gvalue, 0, sizeof(float) * (size_t)B * S * NH * D, s);
   if (e != hipSuccess) return (int)e;
   const long long vbytes = (long long)B * S * NH * D * (long long)sizeof(T);
-  if (lv.L == 3 && P == 4 && vbytes < (1ll << 31) && msda_runs_enabled()) {  // the reference configuration (3 levels x 4 points)
+  if (lv.L == 3 && P == 4 && vbytes < (1ll << 31)) {  // the reference configuration (3 levels x 4 points)
     const int nrun = ceil_div(Q, MSDA_RUN);
     const long long ngroups = (long long)B * nrun * NH;
     k_msda_bwd_runs<T, D, 3, 4, MSDA_RUN><<<(unsigned)ceil_div(ngroups, 256 / D), 256, 0, s>>>(

@@ -534,6 +534,13 @@ static_assert(2 * c2w_smem<0>() <= 163840, "chain v2 phase 0: two workgroups per
 // patch's loads issued, stem MFMAs issued (phase 0: statistics done), stem ReLU/pack done, fusion
 // MFMAs issued, tile end (statistics + stores): stamps[((phase * 4 + tile) * 8 + wave) * 7 + point].
 __device__ unsigned long long* g_c2_stamps = nullptr;
+// the stamped instantiations exist only in the diagnostic build (make diag); in the product
+// library the stamps branch below launches the production kernel and is never taken
+#ifdef RGBD_DIAG
+constexpr bool RGBD_DIAG_ON = true;
+#else
+constexpr bool RGBD_DIAG_ON = false;
+#endif
 static bool c2_stamps_on = false;
 __device__ __forceinline__ void c2_stamp(unsigned long long* st, long long idx) {
   __builtin_amdgcn_sched_barrier(0);
@@ -1252,7 +1259,7 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
 // stamps[(tile * 18 + step) * 8 + wave][5].  A separate instantiation (STAMPS = true), launched
 // only while a buffer is set: the production kernel's code is unchanged.
 __device__ unsigned long long* g_c3_stamps = nullptr;
-static bool c3_stamps_on = false;
+[[maybe_unused]] static bool c3_stamps_on = false;
 __device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) {
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -1894,12 +1901,12 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   }
 #define CHAIN_LAUNCH(PH, A1, A2, SL, OUT)                                                                          \
   do {                                                                                                            \
-    if (v2 && c2_stamps_on && PH < 2) {                                                                           \
-      static const hipError_t sattr = hipFuncSetAttribute((const void*)k_rp_chain_v2<PH, true>,                  \
+    if (RGBD_DIAG_ON && v2 && c2_stamps_on && PH < 2) {                                                           \
+      static const hipError_t sattr = hipFuncSetAttribute((const void*)k_rp_chain_v2<PH, RGBD_DIAG_ON>,                  \
                                                           hipFuncAttributeMaxDynamicSharedMemorySize,             \
                                                           (int)c2w_smem<PH>());                                   \
       (void)sattr;                                                                                                \
-      k_rp_chain_v2<PH, true><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(                                 \
+      k_rp_chain_v2<PH, RGBD_DIAG_ON><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(                                 \
           depth3, bstride, B, H, W, blob, L, A1, A2, fold, SL, (bf16_t*)(OUT));                                   \
     } else if (v2)                                                                                                \
       k_rp_chain_v2<PH><<<PH == 0 ? gch0 : gch, 512, c2w_smem<PH>(), s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, \
@@ -1950,9 +1957,11 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
         (void)sattr;
         kern<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
       };
+#ifdef RGBD_DIAG
       if (c3_stamps_on)
         go(k_rp_conv3x3_v3<true>);
       else
+#endif
         go(k_rp_conv3x3_v3<false>);
     } else {
       gcv = conv_grid(B, H, W);
@@ -1981,6 +1990,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
 
 extern "C" {
 
+#ifdef RGBD_DIAG
 int rgbd_debug_chain_stamps(void* buf) {
   unsigned long long* p = (unsigned long long*)buf;
   const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_c2_stamps), &p, sizeof(p));
@@ -1996,6 +2006,7 @@ int rgbd_debug_conv5_stamps(void* buf) {
   c3_stamps_on = p != nullptr;
   return RGBD_OK;
 }
+#endif
 
 size_t rgbd_ratio_packed_size(int dtype) { return make_layout(dtype == RGBD_BF16 ? 2 : 4).total; }
 

@@ -7,8 +7,9 @@ checkpoint of the reference loads unchanged.  Outside the hot path the model is 
 Hugging Face Mask2Former with its modules swapped in place for the HIP ones of SURVEY §8(f):
 Swin-T layers (f2), pixel-decoder deformable attention and encoder layers (f2), the masked-
 attention decoder layers and mask predictor (f1), every nn.Linear / nn.LayerNorm (f1 / f2),
-the loss's matcher costs, assignment and point-sampled mask terms (f3).  The convolutions of
-the pixel decoder's input projections / FPN and the Swin patch embedding stay torch (MIOpen).
+the loss's matcher costs, assignment and point-sampled mask terms (f3), and every convolution
+(conv.HipConv2d: the pixel decoder's 1x1 input projections and mask projection, the FPN 3x3 and
+Swin's 4x4 patch embedding as MFMA GEMMs, forward and backward).
 """
 import random
 

@@ -54,10 +54,6 @@ def side_stream(dev):
 # bf16 backward: the dW GEMMs of dsam1 and dsam0 in one launch (rgbd_dsam_bwd_weight_planned_multi);
 # False runs them as two launches, dW1 on the side stream (bitwise the same gradients)
 JOINT_DW = True
-# bf16 backward: every dW as the segment GEMM (rgbd_dsam_bwd_weight_seg: five accumulators over
-# all pixels, no dW planning, no per-code partials); False: the code-merged planned path.  Off:
-# measured 2.3x slower on the bench step (r04: 713 vs 309 us for the three legs' dW)
-SEG_DW = False
 
 
 class _Side:
@@ -261,7 +257,7 @@ class HotPathFunction(torch.autograd.Function):
             for k in range(3):
                 if k == 1:
                     side.join()  # the dsam1 / dsam2 packs
-                    if training and not SEG_DW:  # dW plans beside the rest of the forward
+                    if training:  # dW plans beside the rest of the forward
                         dw_plans = side.run(lambda: ops.dsam_plan([(ops.LEG_DW, codes[j], *chans[j]) for j in range(3)]),
                                             *codes)
                 if k == 2:  # DGGM gate + sum of scales 0-2 beside dsam2 (their cp1 are final now)
@@ -337,12 +333,9 @@ class HotPathFunction(torch.autograd.Function):
         dcp_nhwc = g_nhwc[3] if bf16 else ops.nchw_to_nhwc(dcp)
         grads_dsam = [None, None, None]
         def dsam_dw(k, dcp, dcp_nhwc):
-            if bf16 and SEG_DW:
-                dconv, dproj, dbias = ops.dsam_bwd_weight_seg([(dcp_nhwc, ctx.x_nhwc[k], ctx.codes[k])], ctx.info)[0]
-            else:
-                dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
-                                                          gout_nhwc=dcp_nhwc,
-                                                          plan=ctx.dw_plans[k] if ctx.dw_plans else None)
+            dconv, dproj, dbias = ops.dsam_bwd_weight(None if bf16 else dcp, ctx.x_nhwc[k], ctx.codes[k], ctx.info,
+                                                      gout_nhwc=dcp_nhwc,
+                                                      plan=ctx.dw_plans[k] if ctx.dw_plans else None)
             if k == 0:  # dW0 needs nothing from the side stream; the hook and the caller do
                 side.join()
             return dsam_dw_grads(k, dconv, dproj, dbias)
@@ -368,16 +361,12 @@ class HotPathFunction(torch.autograd.Function):
         grads_dsam[2] = side.run(lambda: dsam_dw(2, dcp, dcp_nhwc), dcp_nhwc, ctx.x_nhwc[2], ctx.codes[2], ctx.info)
         dcp1, dcp1_nhwc = dsam_dx(2, dcp, dcp_nhwc)
         dcp0, dcp0_nhwc = dsam_dx(1, dcp1, dcp1_nhwc)
-        if bf16 and JOINT_DW and (SEG_DW or ctx.dw_plans):
+        if bf16 and JOINT_DW and ctx.dw_plans:
             # dW1 and dW0 are ready together: their GEMMs share one launch (two whole-chip launches
             # queue behind each other and each drains on a partly idle chip)
-            if SEG_DW:
-                (dw1, dw0) = ops.dsam_bwd_weight_seg([(dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1]),
-                                                      (dcp0_nhwc, ctx.x_nhwc[0], ctx.codes[0])], ctx.info)
-            else:
-                (dw1, dw0) = ops.dsam_bwd_weight_multi([(dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1], ctx.dw_plans[1]),
-                                                        (dcp0_nhwc, ctx.x_nhwc[0], ctx.codes[0], ctx.dw_plans[0])],
-                                                       ctx.info)
+            (dw1, dw0) = ops.dsam_bwd_weight_multi([(dcp1_nhwc, ctx.x_nhwc[1], ctx.codes[1], ctx.dw_plans[1]),
+                                                    (dcp0_nhwc, ctx.x_nhwc[0], ctx.codes[0], ctx.dw_plans[0])],
+                                                   ctx.info)
             side.join()  # the last launches of the backward, the join after them
             grads_dsam[1] = dsam_dw_grads(1, *dw1)
             grads_dsam[0] = dsam_dw_grads(0, *dw0)

@@ -6,6 +6,7 @@ memory is plumbing), passes raw pointers + the current HIP stream to the C ABI a
 ``decode_info`` (explicitly a host read-back for tests/diagnostics).
 """
 import contextlib
+import threading
 import ctypes
 import math
 
@@ -100,26 +101,44 @@ def device_const(values, dtype, device):
     return t
 
 
+_hc_local = threading.local()
+_hc_lock = threading.Lock()
+_hc_state = {"orig": None, "users": 0}
+
+
+def _hc_as_tensor(data, dtype=None, device=None):
+    orig = _hc_state["orig"]
+    if (getattr(_hc_local, "depth", 0) > 0 and device is not None and torch.device(device).type == "cuda"
+            and not isinstance(data, torch.Tensor)):
+        try:
+            frozen = _freeze(data)
+        except TypeError:
+            return orig(data, dtype=dtype, device=device)
+        return device_const(frozen, orig(data, dtype=dtype).dtype, device)
+    return orig(data, dtype=dtype, device=device)
+
+
 @contextlib.contextmanager
 def host_constants():
-    """Inside the block, ``torch.as_tensor(numbers, device=cuda)`` returns the shared
-    ``device_const`` (library code outside this package calls it on every forward, e.g. the HF
-    pixel decoder's level shapes, modeling_mask2former.py:1347); anything else goes to torch."""
-    orig = torch.as_tensor
-
-    def as_tensor(data, dtype=None, device=None):
-        if device is not None and torch.device(device).type == "cuda" and not isinstance(data, torch.Tensor):
-            try:
-                frozen = _freeze(data)
-            except TypeError:
-                return orig(data, dtype=dtype, device=device)
-            return device_const(frozen, orig(data, dtype=dtype).dtype, device)
-        return orig(data, dtype=dtype, device=device)
-    torch.as_tensor = as_tensor
+    """Inside the block, ``torch.as_tensor(numbers, device=cuda)`` called FROM THIS THREAD returns
+    the shared ``device_const`` (library code outside this package calls it on every forward, e.g.
+    the HF pixel decoder's level shapes, modeling_mask2former.py:1347); other threads (data
+    loaders, pin-memory workers) and anything else go to torch's own function unchanged."""
+    with _hc_lock:
+        if _hc_state["users"] == 0:
+            _hc_state["orig"] = torch.as_tensor
+            torch.as_tensor = _hc_as_tensor
+        _hc_state["users"] += 1
+    _hc_local.depth = getattr(_hc_local, "depth", 0) + 1
     try:
         yield
     finally:
-        torch.as_tensor = orig
+        _hc_local.depth -= 1
+        with _hc_lock:
+            _hc_state["users"] -= 1
+            if _hc_state["users"] == 0:
+                torch.as_tensor = _hc_state["orig"]
+                _hc_state["orig"] = None
 
 
 # ------------------------------------------------------------------ K1 DGGM-pre / assembly
@@ -668,35 +687,6 @@ def dsam_bwd_weight_multi(runs, info):
         outs.append((dconv, dproj, dbias))
     check(L.rgbd_dsam_bwd_weight_planned_multi(len(runs), arr, _p(info), _stream(runs[0][0].device)),
           "rgbd_dsam_bwd_weight_planned_multi")
-    return outs
-
-
-def dsam_bwd_weight_seg(runs, info):
-    """dW/db of up to three bfloat16 DSAM legs as one segment GEMM launch (rgbd_dsam_bwd_weight_seg:
-    no planning, no per-code partials).  ``runs``: (gout_nhwc [B,ho,wo,Co], x_nhwc [B,h,w,Ci],
-    code [B,h,w]) tuples; returns per run (dconv, dproj, dbias)."""
-    if not 1 <= len(runs) <= 3:
-        raise ValueError("dsam_bwd_weight_seg: one to three runs")
-    L = _lib.lib()
-    arr = (_DwRun * len(runs))()
-    outs = []
-    for j, (gout_nhwc, x_nhwc, code) in enumerate(runs):
-        _need_cuda(gout_nhwc, x_nhwc, code, info)
-        if gout_nhwc.dtype != torch.bfloat16 or x_nhwc.dtype != torch.bfloat16:
-            raise ValueError("dsam_bwd_weight_seg: bfloat16 legs only")
-        B, ho, wo, Co = gout_nhwc.shape
-        _, h, w, Ci = x_nhwc.shape
-        if (ho, wo) != ((h + 1) // 2, (w + 1) // 2) or tuple(code.shape) != (B, h, w):
-            raise ValueError(f"dsam_bwd_weight_seg: run {j} shapes {tuple(gout_nhwc.shape)} {tuple(x_nhwc.shape)}")
-        dev = gout_nhwc.device
-        dconv = torch.empty((4, Co, Ci, 3, 3), dtype=torch.float32, device=dev)
-        dproj = torch.empty((Co, Ci, 3, 3), dtype=torch.float32, device=dev)
-        dbias = torch.empty((4, Co), dtype=torch.float32, device=dev)
-        ws = _workspace(dev, L.rgbd_dsam_seg_workspace_size(B, Ci, h, w, Co), f"dsam_segw{j}")
-        arr[j] = _DwRun(gout_nhwc.data_ptr(), x_nhwc.data_ptr(), code.data_ptr(), B, Ci, h, w, Co, dconv.data_ptr(),
-                        dproj.data_ptr(), dbias.data_ptr(), None, ws.data_ptr())
-        outs.append((dconv, dproj, dbias))
-    check(L.rgbd_dsam_bwd_weight_seg(len(runs), arr, _p(info), _stream(runs[0][0].device)), "rgbd_dsam_bwd_weight_seg")
     return outs
 
 

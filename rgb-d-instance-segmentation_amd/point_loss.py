@@ -172,10 +172,16 @@ class HipMask2FormerLoss(Mask2FormerLoss):
         rows [sum T, H, W] and their image offsets — built once per set of labels (the final and
         the nine auxiliary outputs share them), None when the images differ in size (then the
         reference's zero-padded batch is used)."""
-        key = (dtype, tuple((m.data_ptr(), m._version, tuple(m.shape)) for m in mask_labels))
+        # the cache holds the label tensors themselves and matches them by identity: while they
+        # are cached their storage cannot be freed, so a later batch's labels can never reuse the
+        # same addresses and be mistaken for them (a (data_ptr, _version) key could be)
         cached = getattr(self, "_rgbd_targets", None)
-        if cached is not None and cached[0] == key:
-            return cached[1], cached[2]
+        if cached is not None:
+            c_dtype, c_labels, c_versions, rows, offs = cached
+            if (c_dtype == dtype and len(c_labels) == len(mask_labels)
+                    and all(a is b for a, b in zip(c_labels, mask_labels))
+                    and c_versions == tuple(m._version for m in mask_labels)):
+                return rows, offs
         rows = offs = None
         if mask_labels and len({tuple(m.shape[-2:]) for m in mask_labels}) == 1:
             rows = torch.cat([m.reshape(-1, *m.shape[-2:]) for m in mask_labels]).to(dtype).float()
@@ -183,7 +189,8 @@ class HipMask2FormerLoss(Mask2FormerLoss):
             for m in mask_labels:
                 offs.append(o)
                 o += m.shape[0]
-        self._rgbd_targets = (key, rows, offs)
+        self._rgbd_targets = (dtype, tuple(mask_labels), tuple(m._version for m in mask_labels),
+                              rows, offs)
         return rows, offs
 
     def loss_masks(self, masks_queries_logits, mask_labels, indices, num_masks):
@@ -216,7 +223,9 @@ class HipMask2FormerLoss(Mask2FormerLoss):
             # the k most uncertain points as a set: the loss terms are sums over the points, so
             # their order is immaterial (up to float summation order) and topk's segmented sort
             # of the selection (~2.4 ms per whole-model step, rocprim merge sort) is skipped
-            idx = torch.topk(unc, k=k, dim=1, sorted=False)[1]
+            # deliberate deviation: unsorted; SORTED_TOPK restores the reference's
+            # sorted selection for parity runs (the same set up to ties, the reference's order)
+            idx = torch.topk(unc, k=k, dim=1, sorted=SORTED_TOPK)[1]
             shift = n_over * torch.arange(N, dtype=torch.long, device=pred_masks.device)
             idx += shift[:, None]
             coords = coords.view(-1, 2)[idx.view(-1), :].view(N, k, 2)

@@ -42,6 +42,10 @@ class CapturedTrainStep:
                 if not g.get("capturable", False):
                     raise ValueError("CapturedTrainStep needs a capturable optimizer (capturable=True)")
         self.fb, self.opt = fb, opt
+        # every parameter the step's optimizers own: a replay updates them on the device without
+        # the host-side post-step hook, so __call__ advances their step epoch itself (the casts
+        # cached under dense.cast_weight's key would otherwise go stale between replays)
+        self.params = [p for o in opts for g in o.param_groups for p in g["params"]]
         clear = clear or (lambda: [o.zero_grad(set_to_none=True) for o in opts])
         self.stream = torch.cuda.Stream()
         self.stream.wait_stream(torch.cuda.current_stream())
@@ -62,4 +66,6 @@ class CapturedTrainStep:
 
     def __call__(self):
         self.graph.replay()
+        for p in self.params:
+            p._rgbd_epoch = getattr(p, "_rgbd_epoch", 0) + 1
         return self.outs

@@ -41,3 +41,23 @@ def test_cache_hits_and_invalidation():
     assert f2 is not f1 and torch.equal(f2, frozen.detach().to(torch.bfloat16))
     assert cast_weight(a, torch.float32) is not None       # same dtype: no copy
     assert cast_weight(a, torch.float32).data_ptr() == a.data_ptr()
+
+
+def test_target_rows_cache_is_identity_keyed():
+    """point_loss's target-row cache matches label tensors by identity and
+    keeps them alive, so a new batch's labels (same shape, possibly the same recycled address)
+    never hit the previous batch's rows."""
+    from rgbd_amd.point_loss import HipMask2FormerLoss
+    loss = HipMask2FormerLoss.__new__(HipMask2FormerLoss)
+    a = [torch.zeros(2, 4, 4), torch.ones(1, 4, 4)]
+    r1, o1 = loss._target_rows(a, torch.float32)
+    assert loss._target_rows(a, torch.float32)[0] is r1          # hit: same tensors
+    assert o1 == [0, 2]
+    del a
+    b = [torch.ones(2, 4, 4), torch.zeros(1, 4, 4)]              # new labels, same shapes
+    r2, _ = loss._target_rows(b, torch.float32)
+    assert r2 is not r1 and torch.equal(r2, torch.cat(b))
+    with torch.no_grad():
+        b[0].zero_()                                             # in place: version bump
+    r3, _ = loss._target_rows(b, torch.float32)
+    assert torch.equal(r3, torch.cat(b))

@@ -134,37 +134,3 @@ def test_joint_dw_mixed_tile_shapes():
     for j in range(2):
         for a, b in zip(got[j], ref[j]):
             assert torch.equal(a, b), f"leg {j}"
-
-
-@pytest.mark.parametrize("H,W,B", [(480, 640, 8), (97, 131, 3)])
-def test_segment_dw_matches_code_merged(H, W, B):
-    """The segment-GEMM dW (rgbd_dsam_bwd_weight_seg: five accumulators over all pixels) against the
-    code-merged planned path (per-code GEMMs + combine) on the same bf16 operands: the same exact
-    bf16 products summed in float32 in another order -> within 1e-4 of the max (bias gradients,
-    the same channel sums: 1e-5).  One launch for all three legs equals three single-leg launches
-    bitwise."""
-    planes, _, _ = synthetic.make_batch(7, B, H, W)
-    d3 = torch.from_numpy(planes[:, 3:6]).to(DEV)
-    sizes = _sizes(H, W)
-    codes, info = ops.edsam_decompose(d3, torch.linspace(0.05, 0.45, B, device=DEV), sizes)
-    g = torch.Generator(device=DEV)
-    g.manual_seed(11)
-    runs = []
-    for k in range(3):
-        ci, co = CH[k]
-        h, w = sizes[k]
-        ho, wo = (h + 1) // 2, (w + 1) // 2
-        x = torch.randn((B, h, w, ci), generator=g, device=DEV).bfloat16()
-        gy = (torch.randn((B, ho, wo, co), generator=g, device=DEV) * 0.1).bfloat16()
-        runs.append((gy, x, codes[k]))
-    joint = ops.dsam_bwd_weight_seg(runs, info)
-    for k in range(3):
-        gy, x, code = runs[k]
-        single = ops.dsam_bwd_weight_seg([runs[k]], info)[0]
-        ref = ops.dsam_bwd_weight(None, x, code, info, gout_nhwc=gy)
-        for a, s1, e, name in zip(joint[k], single, ref, ("dconv", "dproj", "dbias")):
-            assert torch.equal(a, s1), f"leg {k} {name}: joint launch != single launch"
-            scale = float(e.abs().max())
-            err = float((a - e).abs().max()) / max(scale, 1e-30)
-            print(f"{H}x{W} leg {k} {name}: rel err {err:.2e}")
-            assert err < (1e-5 if name == "dbias" else 1e-4), f"leg {k} {name}: {err}"

@@ -283,9 +283,8 @@ def test_hot_path_fused_vs_oracle(dtype):
 
 
 def test_hot_path_joint_dw_bitwise():
-    """bfloat16 backward: dsam1's and dsam0's dW GEMMs in one launch (hot_path.JOINT_DW; the
-    segment GEMM under hot_path.SEG_DW) give bitwise the parameter gradients of the two-launch
-    schedule."""
+    """bfloat16 backward: dsam1's and dsam0's dW GEMMs in one launch (hot_path.JOINT_DW) give
+    bitwise the parameter gradients of the two-launch schedule."""
     from rgbd_amd import hot_path as hp
     H, W, B = 240, 320, 2
     pv = torch.from_numpy(gi.pixel_values(7, B, H, W)).to(DEV)

@@ -111,3 +111,30 @@ def test_pipelined_captured_step_equals_sequential_steps():
     assert int(a["rp"]._rgbd_dropout_ctr.item()) == 5 == int(b["rp"]._rgbd_dropout_ctr.item())
     for i, (x, y) in enumerate(zip(_state(a), _state(b))):
         assert torch.equal(x, y), f"state tensor {i} differs after 4 steps"
+
+
+def test_replay_advances_cast_cache_epoch():
+    """dense.cast_weight caches a parameter's bf16 copy under (address,
+    version, step epoch). A graph replay updates the parameters on the device without the host
+    post-step hook, so CapturedTrainStep advances the epoch itself: an eager forward after
+    replay / eager / replay sees the updated weights, not the cast cached in between."""
+    from rgbd_amd.dense import HipLinear, cast_weight
+    from rgbd_amd.train_graph import CapturedTrainStep
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(64, 32).to(DEV)
+    lin.__class__ = HipLinear
+    opt = torch.optim.AdamW(lin.parameters(), lr=1e-2, capturable=True)
+    x = torch.randn(128, 64, device=DEV)
+
+    def fb():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = lin(x)
+        y.float().square().mean().backward()
+        return (y,)
+
+    step = CapturedTrainStep(fb, opt, warmup=2)
+    for _ in range(2):
+        step()
+        torch.cuda.synchronize()
+        c = cast_weight(lin.weight, torch.bfloat16)   # the eager forward's cast
+        assert torch.equal(c, lin.weight.detach().to(torch.bfloat16)), "stale bf16 cast after replay"

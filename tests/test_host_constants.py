@@ -33,3 +33,26 @@ def test_host_constants_patch_is_scoped():
         with ops.host_constants():
             raise ValueError("restored on error too")
     assert torch.as_tensor is orig
+
+
+def test_host_constants_only_in_the_entering_thread(monkeypatch):
+    """the patch serves device constants only to the thread inside the block; other
+    threads (data loaders, pin-memory workers) get torch's own as_tensor."""
+    import threading
+    seen = []
+    monkeypatch.setattr(ops, "device_const", lambda v, dt, dev: seen.append(v) or "const")
+    other = {}
+
+    def worker():
+        try:
+            other["r"] = torch.as_tensor([3, 4], device="cuda")
+        except Exception as e:  # no GPU here: torch's own path raises, which is the point
+            other["r"] = type(e).__name__
+
+    with ops.host_constants():
+        assert torch.as_tensor([1, 2], device="cuda") == "const"
+        t = threading.Thread(target=worker)
+        t.start()
+        t.join()
+    assert seen == [(1, 2)]
+    assert other["r"] != "const"

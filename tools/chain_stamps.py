@@ -14,6 +14,8 @@ import sys
 
 _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [_R]
+# the stamped kernels live in the diagnostic build only (make -C rgb-d-instance-segmentation_amd/csrc diag)
+os.environ.setdefault("RGBD_HIP_LIB", os.path.join(_R, "rgb-d-instance-segmentation_amd", "librgbd_hip_diag.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
