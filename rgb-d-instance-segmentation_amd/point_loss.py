@@ -14,6 +14,8 @@ calls in the reference's order, so the RNG stream and the selected point set are
 ``install(model)`` swaps the HF loss (and its matcher) for ``HipMask2FormerLoss`` /
 ``matcher.HipHungarianMatcher`` in place; ``uninstall`` restores them.
 """
+import os
+
 import torch
 from torch import nn
 from transformers.models.mask2former.modeling_mask2former import Mask2FormerHungarianMatcher, Mask2FormerLoss
@@ -21,6 +23,11 @@ from transformers.models.mask2former.modeling_mask2former import Mask2FormerHung
 from . import _lib
 from ._lib import RGBD_BF16, RGBD_F32, check
 from .ops import _need_cuda, _p, _stream, device_const
+
+# loss_masks' uncertainty top-k: unsorted by default (the loss terms are sums over the point set,
+# so only the float summation order changes; the segmented sort cost ~2.4 ms per whole-model
+# step); True — or RGBD_SORTED_TOPK=1 — takes the reference's sorted selection (parity runs)
+SORTED_TOPK = os.environ.get("RGBD_SORTED_TOPK", "0") == "1"
 
 
 def point_sample(maps: torch.Tensor, coords: torch.Tensor) -> torch.Tensor:
