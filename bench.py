@@ -473,26 +473,112 @@ def _codes_flipped(pv, r_ref, r_got, H, W):
     return [round(float((a != b).float().mean()), 6) for a, b in zip(ca, cb)]
 
 
-def parity(dev, dtype=torch.float32, ratio_fp32=False):
+G9_ATTN = REPO / "tests" / "golden" / "g9_attn_masks.npz"
+FLIP_EXPLAIN_FACTOR = 4.0  # a flipped attention bit is explained when |ref logit| <= 4 x the call's |delta logit|
+
+
+class ReferenceMasks:
+    """The reference's attention masks at every mask-predictor call of the masked-attention
+    decoder (tests/golden/g9_attn_masks.npz, made by importing the reference: make_golden.py
+    attn), for the G5 (320x240) or G7 (640x480) input.  ``attach(model, force)`` hooks the
+    model's mask predictor (HF modeling_mask2former.py:1896-1933 feeds its second output to the
+    next decoder layer) and records per call the model's own mask (head 0) and its
+    interpolated logits at the fixture's near-threshold positions; with ``force`` the reference's
+    mask replaces the model's, so every decoder layer sees the reference's attention pattern and
+    the remaining logit error is arithmetic only."""
+
+    def __init__(self, tag):
+        z = np.load(G9_ATTN, allow_pickle=False)
+        self.input_sha = str(z[f"{tag}_input_sha"])
+        self.calls = []
+        for c in range(int(z[f"{tag}_ncalls"])):
+            Q, L = (int(v) for v in z[f"{tag}_c{c}_shape"])
+            bits = np.unpackbits(z[f"{tag}_c{c}_bits"], count=Q * L).astype(bool).reshape(Q, L)
+            self.calls.append({"mask": bits, "size": tuple(int(v) for v in z[f"{tag}_c{c}_size"]),
+                               "near_idx": z[f"{tag}_c{c}_near_idx"], "near_val": z[f"{tag}_c{c}_near_val"]})
+
+    def attach(self, model, force, rec):
+        import torch.nn.functional as F
+        mp = model.model.transformer_module.decoder.mask_predictor
+
+        def hook(mod, inp, out):
+            c = len(rec)
+            if c >= len(self.calls):
+                raise RuntimeError("more mask-predictor calls than the fixture holds")
+            ref = self.calls[c]
+            logits, attn = out[0], out[1]
+            if logits.shape[0] != 1:
+                raise ValueError("ReferenceMasks: batch 1 only")
+            val = F.interpolate(logits.detach().float(), size=ref["size"], mode="bilinear",
+                                align_corners=False).flatten(2)[0].reshape(-1)
+            near = torch.from_numpy(ref["near_idx"]).to(val.device)
+            nh = attn.shape[0]
+            rec.append((attn.view(nh, *attn.shape[1:])[0].cpu().numpy(), val[near].cpu().numpy()))
+            if not force:
+                return None
+            m = torch.from_numpy(ref["mask"]).to(attn.device)
+            return logits, m[None].expand(nh, *m.shape).contiguous()
+        return mp.register_forward_hook(hook)
+
+    def flips(self, rec, deltas=None, upto_first=False):
+        """Per call: flipped bits of the model's own masks against the reference's, and how many
+        are unexplained — the reference logit not within FLIP_EXPLAIN_FACTOR x that call's
+        |delta logit| (``deltas``: the forced run's per-call max |own - ref| over the fixture's
+        near-threshold positions; default this run's).  ``upto_first``: only up to the first
+        call with a flip (later calls of an unforced run inherit that flip's consequences)."""
+        total, unexplained, first = 0, 0, None
+        own_deltas = []
+        for c, (own, own_near) in enumerate(rec):
+            ref = self.calls[c]
+            own_deltas.append(float(np.abs(own_near - ref["near_val"]).max()) if own_near.size else 0.0)
+        deltas = own_deltas if deltas is None else deltas
+        for c, (own, _) in enumerate(rec):
+            ref = self.calls[c]
+            idx = np.flatnonzero((own != ref["mask"]).ravel())
+            if not idx.size:
+                continue
+            first = c if first is None else first
+            pos = np.minimum(np.searchsorted(ref["near_idx"], idx), max(ref["near_idx"].size - 1, 0))
+            vals = np.full(idx.size, np.inf)
+            if ref["near_idx"].size:
+                hit = ref["near_idx"][pos] == idx
+                vals[hit] = np.abs(ref["near_val"][pos[hit]])
+            total += int(idx.size)
+            unexplained += int((vals > FLIP_EXPLAIN_FACTOR * deltas[c]).sum())
+            if upto_first:
+                break
+        return {"flips": total, "unexplained": unexplained, "first_call": first,
+                "max_delta_logit": max(own_deltas) if own_deltas else 0.0, "deltas": own_deltas}
+
+
+def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7"):
     """BASELINE.json's second metric: the full drop-in model (HF Swin / pixel decoder /
-    transformer decoder around the HIP hot path, f1/f2 kernels installed) at 640x480, B=1, eval,
+    transformer decoder around the HIP hot path, f1/f2 kernels installed), B=1, eval,
     deterministic weights, against the reference CPU run committed as
-    tests/golden/g7_model640.npz (made by tests/golden/make_golden.py).  The 10-channel input is
-    assembled on the GPU by K1 from the scene's u8 planes; its sha256 must equal the one the
-    fixture was generated from.  ``dtype`` bfloat16: the hot path (ratio predictor, DSAM, DGGM)
-    in bf16 as the bench runs it — the ratio, and so the window decisions, come from the bf16
-    ratio predictor; the HF modules around it stay float32.  ``ratio_fp32``: the ratio
-    predictor alone in float32 (the reference's ratio, so the reference's window decisions):
-    what remains is the error of the bf16 DSAM / DGGM arithmetic."""
+    tests/golden/g7_model640.npz (640x480) or g5_model.npz (320x240, ``fixture`` "g5"), made by
+    tests/golden/make_golden.py.  The 10-channel input is assembled on the GPU by K1 from the
+    scene's u8 planes; its sha256 must equal the one the fixture was generated from.
+
+    Two runs: the model as is, and the same with the reference's attention masks forced into
+    every masked-attention decoder layer (``ReferenceMasks``, G9) — the forced run's error is
+    arithmetic only; the unforced run additionally carries every attention bit the arithmetic
+    flips across the sigmoid(logit) < 0.5 binarisation (counted: ``attention_flips``).
+
+    ``dtype`` bfloat16: the hot path (ratio predictor, DSAM, DGGM) in bf16 as the bench runs it —
+    the ratio, and so the window decisions, come from the bf16 ratio predictor; the HF modules
+    around it stay float32.  ``ratio_fp32``: the ratio predictor alone in float32 (the
+    reference's ratio, so the reference's window decisions): what remains is the error of the
+    bf16 DSAM / DGGM arithmetic."""
     import hashlib
     from rgbd_amd import init as winit, ops, synthetic
     from rgbd_amd.config import standard_config
     from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
-    g7 = np.load(REPO / "tests" / "golden" / "g7_model640.npz", allow_pickle=False)
-    sc = synthetic.make_scene(synthetic.scene_seed(7, 0), 480, 640)
+    cid, H, W, path = {"g7": (7, 480, 640, "g7_model640.npz"), "g5": (1, 240, 320, "g5_model.npz")}[fixture]
+    gz = np.load(REPO / "tests" / "golden" / path, allow_pickle=False)
+    sc = synthetic.make_scene(synthetic.scene_seed(cid, 0), H, W)
     pv = ops.assemble_pixel_values(torch.from_numpy(sc["depth_u8"][None]).to(dev),
                                    torch.from_numpy(sc["rgb_u8"][None]).contiguous().to(dev))
-    sha_ok = hashlib.sha256(pv.cpu().numpy().tobytes()).hexdigest() == str(g7["input_sha"])
+    sha_ok = hashlib.sha256(pv.cpu().numpy().tobytes()).hexdigest() == str(gz["input_sha"])
     torch.manual_seed(0)
     m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
     winit.init_deterministic(m)
@@ -500,32 +586,64 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False):
     rp = m.model.pixel_level_module.ratio_predictor
     if ratio_fp32:
         rp.compute_dtype = torch.float32
+    refm = ReferenceMasks(fixture)
+    runs = {}
+    for force in (False, True):
+        rec = []
+        h = refm.attach(m, force, rec)
+        try:
+            with torch.no_grad():
+                out = m(pixel_values=pv)
+        finally:
+            h.remove()
+        runs[force] = (out, rec)
     with torch.no_grad():
-        out = m(pixel_values=pv)
         ratio = rp(pv[:, 3:6])
-    ml = out.masks_queries_logits.float().cpu().numpy().ravel()
-    ref = g7["mask_val"]
-    err = float(np.abs(ml[g7["mask_idx"]] - ref).max())
-    cls = float(np.abs(out.class_queries_logits.float().cpu().numpy() - g7["class_logits"]).max())
-    rrel = float(np.abs(ratio.float().cpu().numpy() - g7["ratio"]).max() / np.abs(g7["ratio"]).max())
+    if fixture == "g7":
+        ref, pick = gz["mask_val"], gz["mask_idx"]
+    else:
+        ref, pick = gz["mask_logits"].ravel(), slice(None)
+
+    def err_of(out):
+        ml = out.masks_queries_logits.float().cpu().numpy().ravel()
+        return (float(np.abs(ml[pick] - ref).max()),
+                float(np.abs(out.class_queries_logits.float().cpu().numpy() - gz["class_logits"]).max()))
+    err, cls = err_of(runs[False][0])
+    ferr, fcls = err_of(runs[True][0])
+    forced = refm.flips(runs[True][1])
+    unforced = refm.flips(runs[False][1], deltas=forced["deltas"])
+    first = refm.flips(runs[False][1], deltas=forced["deltas"], upto_first=True)
+    rrel = float(np.abs(ratio.float().cpu().numpy() - gz["ratio"]).max() / np.abs(gz["ratio"]).max())
     flips = None
     if dtype != torch.float32:
-        r_ref = torch.from_numpy(np.asarray(g7["ratio"], np.float32).reshape(-1, 1)).to(dev)
-        flips = _codes_flipped(pv, r_ref, ratio.float().reshape(-1, 1), 480, 640)
+        r_ref = torch.from_numpy(np.asarray(gz["ratio"], np.float32).reshape(-1, 1)).to(dev)
+        flips = _codes_flipped(pv, r_ref, ratio.float().reshape(-1, 1), H, W)
     del m
     torch.cuda.empty_cache()
     res = {"mask_logit_max_abs_err": err, "class_logit_max_abs_err": cls, "ratio_rel_err": rrel,
-           "input_sha_match": sha_ok, "dtype": "f32" if dtype == torch.float32 else "bf16", "shape": "640x480",
-           "fixture": "tests/golden/g7_model640.npz", "sampled_logits": int(g7["mask_idx"].size)}
+           "mask_logit_max_abs_err_masks_forced": ferr, "class_logit_max_abs_err_masks_forced": fcls,
+           "attention_flips": {"unforced_run": unforced["flips"], "forced_run_own_masks": forced["flips"],
+                               "first_flipped_call": first["first_call"],
+                               "first_call_unexplained": first["unexplained"],
+                               "max_delta_logit_forced": forced["max_delta_logit"],
+                               "explain_factor": FLIP_EXPLAIN_FACTOR},
+           "input_sha_match": sha_ok, "dtype": "f32" if dtype == torch.float32 else "bf16", "shape": f"{W}x{H}",
+           "fixture": f"tests/golden/{path}", "sampled_logits": int(np.asarray(ref).size),
+           "note": ("masks_forced: the reference's attention masks (tests/golden/g9_attn_masks.npz) injected into "
+                    "every masked-attention decoder layer, so the error is arithmetic only; attention_flips: bits "
+                    "of the model's own masks that differ from the reference's (forced run: each call on the "
+                    "reference's inputs; first_call_unexplained: flips of the unforced run's first flipped call "
+                    "whose reference logit lies beyond explain_factor x the forced run's |delta logit|)")}
     if dtype == torch.float32:
         res["tolerance"] = 1e-3
     else:
-        res.update(mask_logit_max_rel_err=err / float(np.abs(ref).max()), tolerance_rel=BF16_LOGIT_REL_TOL,
-                   region_code_cells_flipped=flips,
+        scale = float(np.abs(ref).max())
+        res.update(mask_logit_max_rel_err=err / scale, mask_logit_max_rel_err_masks_forced=ferr / scale,
+                   tolerance_rel=BF16_LOGIT_REL_TOL, region_code_cells_flipped=flips,
                    ratio_predictor="float32 (reference ratio injected)" if ratio_fp32 else "bf16",
-                   note="bf16 hot path (ratio predictor, DSAM, DGGM) in the float32 HF model; rel = max-abs-err / "
-                        "max |reference logit|; region_code_cells_flipped = fraction of DSAM region-code cells "
-                        "(3 input scales) whose code differs from the decomposition at the reference ratio")
+                   note_bf16="bf16 hot path (ratio predictor, DSAM, DGGM) in the float32 HF model; rel = max-abs-err / "
+                             "max |reference logit|; region_code_cells_flipped = fraction of DSAM region-code cells "
+                             "(3 input scales) whose code differs from the decomposition at the reference ratio")
     return res
 
 
@@ -770,6 +888,8 @@ def main():
         out["parity"]["bf16"] = parity(dev, torch.bfloat16)
         # the same with the reference's float32 ratio: the bf16 error with no flipped decision
         out["parity"]["bf16_ratio_fp32"] = parity(dev, torch.bfloat16, ratio_fp32=True)
+        # G5 (C1's 320x240) beside G7, fp32
+        out["parity"]["g5_320x240"] = parity(dev, fixture="g5")
     if rank == 0 and world == 1 and args.c5_stream:
         out["c5_stream"] = c5_stream(ctx)
     if rank == 0 and world == 1 and args.full_model:

@@ -22,6 +22,9 @@ Fixtures (SURVEY.md §8(c) "Golden vectors"):
   g5_model.npz       a1+a12: full model eval forward at 320x240 (ratio, logits, sampled features)
   g6_grads.npz       one loss.backward() at 320x240 B=2 (eval mode): hot-path grad stats
   g8_resize.npz      a11 for frames not at model resolution: the processor's resize (PIL)
+  g9_attn_masks.npz  the masked-attention decoder's attention masks at G5 / G7's inputs: per
+                     mask-predictor call the reference's binarised mask (bit-packed, one head:
+                     the heads repeat it) and its near-threshold pre-binarisation logits
 """
 import hashlib
 import json
@@ -293,6 +296,45 @@ def build_model(cm):
     return model
 
 
+def attn_mask_fixture(cm):
+    """G9: every mask-predictor call of the reference model at G5's (320x240) and G7's (640x480)
+    inputs — the attention mask the HF decoder feeds the next layer (sigmoid(interpolated logits)
+    < 0.5, modeling_mask2former.py:2048-2055) bit-packed for one head, and the interpolated
+    logits within 2e-2 of the threshold (index + value) — so a run can (i) force the reference's
+    masks into every decoder layer and measure pure arithmetic error, (ii) count and explain
+    flipped bits without the reference on the GPU box."""
+    model = build_model(cm).eval()
+    calls = []
+    mp = model.model.transformer_module.decoder.mask_predictor
+    h = mp.register_forward_hook(lambda m, inp, out: calls.append((out[0].detach().clone(), out[1].detach().clone(),
+                                                                  inp[2])))
+    g9 = {}
+    for tag, (cid, H, W) in {"g5": (1, 240, 320), "g7": (7, 480, 640)}.items():
+        pv = golden_inputs.pixel_values(cid, 1, H, W)
+        calls.clear()
+        with torch.no_grad():
+            out = model(pixel_values=torch.from_numpy(pv))
+        g9[f"{tag}_input_sha"] = np.array(sha(pv))
+        g9[f"{tag}_ncalls"] = np.array(len(calls))
+        ml = out.masks_queries_logits.numpy()
+        g9[f"{tag}_mask_sum"] = np.array(ml.astype(np.float64).sum())
+        for c, (logits, attn, size) in enumerate(calls):
+            nh = attn.shape[0] // logits.shape[0]
+            a = attn.view(logits.shape[0], nh, *attn.shape[1:])
+            assert bool((a == a[:, :1]).all()), "heads differ"
+            a0 = a[0, 0].numpy()  # [Q, L] (B = 1)
+            val = F.interpolate(logits, size=size, mode="bilinear", align_corners=False).flatten(2)[0].numpy()
+            assert np.array_equal(a0, val < 0) or np.array_equal(a0, 1 / (1 + np.exp(-val)) < 0.5)
+            near = np.flatnonzero(np.abs(val.ravel()) < 2e-2)
+            g9[f"{tag}_c{c}_shape"] = np.array(a0.shape)
+            g9[f"{tag}_c{c}_size"] = np.array(size)
+            g9[f"{tag}_c{c}_bits"] = np.packbits(a0.ravel())
+            g9[f"{tag}_c{c}_near_idx"] = near.astype(np.int64)
+            g9[f"{tag}_c{c}_near_val"] = val.ravel()[near].astype(np.float32)
+    h.remove()
+    np.savez_compressed(OUT / "g9_attn_masks.npz", **g9)
+
+
 def save_g1(rec):
     out = {"names": np.array(rec["names"]), "shapes": np.array(rec["shapes"]),
            "ratios": np.array(rec["ratios"], np.float64), "input_sha": np.array(rec["input_sha"]),
@@ -341,6 +383,10 @@ if __name__ == "__main__":
     import golden_inputs  # noqa: E402
     if len(sys.argv) > 1 and sys.argv[1] == "resize":
         resize_fixture()
+    elif len(sys.argv) > 1 and sys.argv[1] == "attn":
+        torch.manual_seed(0)
+        torch.set_num_threads(8)
+        attn_mask_fixture(import_reference())
     else:
         main()
         resize_fixture()

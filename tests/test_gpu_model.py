@@ -144,24 +144,31 @@ def test_bf16_train_mode_gated_features(H, W, path, monkeypatch):
 
 
 def test_full_model_mask_logits_fp32(golden):
-    """North-star parity: mask-logit max-abs-err vs the reference CPU path <= 1e-3 (fp32 mode).
+    """North-star parity: mask-logit max-abs-err vs the reference CPU path <= 1e-3 (fp32 mode), at
+    G5 (320x240).
 
-    Two effects outside the hot path are separated out:
+    Two effects outside the hot path's arithmetic are separated out:
     * the ratio feeds discrete window decisions, and a 1e-7 relative difference between our and
       torch-CPU's float32 ratio can move a pixel whose grey depth sits within that distance of a
       window bound (SURVEY §7 hard part (v)): the ratio is checked on its own (rtol 1e-5) and the
       reference ratio is injected for the logits;
-    * the HF masked-attention decoder binarises sigmoid(mask) < 0.5 between layers, which
-      amplifies 1e-6-level GPU-vs-CPU float differences of its own GEMMs/convs into ~1e-3 logit
-      changes (measured: backbone features 5e-6 relative, full-GPU mask logits 2.3e-3).  The
-      hot-path parity is therefore measured by running the reference-identical HF stages on the
-      CPU from the backbone features the HIP hot path produced on the GPU.
-    With the pixel decoder's deformable attention, the mask predictor and the matcher on the HIP
-    kernels the fully-on-GPU end-to-end error is asserted at 1e-3 too (measured 4.6e-6; the HF
-    grid_sample path gave 2.3e-3 through one flipped attention-mask bit)."""
+    * the HF masked-attention decoder binarises sigmoid(mask) < 0.5 between layers: a logit
+      within float noise of 0 flips its attention bit and moves later logits by ~1e-3.  So the
+      1e-3 bound is asserted on runs with the REFERENCE's attention masks forced into every
+      decoder layer (tests/golden/g9_attn_masks.npz, made by importing the reference; pinned to
+      the oracle by test_oracle_attention_masks_match_g9): pure arithmetic, no binarisation —
+      (i) the reference HF stages on the CPU fed with the GPU hot-path features, (ii) everything
+      on the GPU.  Flips are counted separately: a flipped bit is explained only when the
+      reference logit lies within bench.FLIP_EXPLAIN_FACTOR (4) x the call's measured
+      pre-binarisation |delta logit| (the forced run's, at the fixture's near-threshold
+      positions) — in the forced run at every call, in the unforced run at its first flipped
+      call (later calls inherit that flip's consequences)."""
+    import bench
     g5 = golden("g5_model")
+    refm = bench.ReferenceMasks("g5")
     m = _full_model().eval()
     pv_cpu = torch.from_numpy(gi.pixel_values(1, 1, 240, 320))
+    assert hashlib.sha256(pv_cpu.numpy().tobytes()).hexdigest() == refm.input_sha == str(g5["input_sha"])
     pv = pv_cpu.to(DEV)
     plm = m.model.pixel_level_module
     with torch.no_grad():
@@ -171,30 +178,35 @@ def test_full_model_mask_logits_fp32(golden):
     caps = {}
     h1 = plm.ratio_predictor.register_forward_hook(lambda mod, inp, out: ref_ratio.clone())
     h2 = plm.decoder.register_forward_pre_hook(lambda mod, a: caps.__setitem__("bb", [t.detach().cpu() for t in a[0]]))
-    gpu_calls = []
-    h4 = m.model.transformer_module.decoder.mask_predictor.register_forward_hook(
-        lambda mod, inp, out: gpu_calls.append(out[1].cpu()))
+    runs = {}
     try:
-        with torch.no_grad():
-            out_gpu = m(pixel_values=pv)
+        for force in (False, True):
+            rec = []
+            h = refm.attach(m, force, rec)
+            try:
+                with torch.no_grad():
+                    runs[force] = (m(pixel_values=pv), rec)
+            finally:
+                h.remove()
     finally:
         h1.remove()
         h2.remove()
-        h4.remove()
-    # the same model on the CPU, fed with the GPU hot-path features
+    # (i) the reference HF stages on the CPU, fed with the GPU hot-path features, masks forced
     mc = _full_model().cpu().eval()
     assert mask_predictor.uninstall(mc) == 1  # the reference HF modules are the CPU checker
     assert deform_attn.uninstall(mc) == 6
     assert masked_attention.uninstall(mc) == 9
     mc.model.pixel_level_module.hot_path_features = lambda pv_, colors, ratios=None, **kw: caps["bb"]
-    calls = []
+    calls, rec_c = [], []
     h3 = mc.model.transformer_module.decoder.mask_predictor.register_forward_hook(
-        lambda mod, inp, out: calls.append((inp, out)))
+        lambda mod, inp, out: calls.append((inp, out)))  # before the forcing hook: the predictor's own outputs
+    h5 = refm.attach(mc, True, rec_c)
     try:
         with torch.no_grad():
             out = mc(pixel_values=pv_cpu)
     finally:
         h3.remove()
+        h5.remove()
     # f1 pinned on the reference's own calls: each of the 10 mask-predictor calls of the CPU run,
     # replayed through the HIP predictor on the GPU with the same inputs
     hip_pred = m.model.transformer_module.decoder.mask_predictor
@@ -209,65 +221,26 @@ def test_full_model_mask_logits_fp32(golden):
         assert not bool(((attn_h.cpu() != attn_ref) & ~near).any())
     print(f"f1 mask predictor (HIP vs reference CPU calls): max-abs-err {worst:.3g}")
     assert worst <= 1e-4
-    err = float(np.abs(out.masks_queries_logits.numpy() - g5["mask_logits"]).max())
-    gpu = float(np.abs(out_gpu.masks_queries_logits.cpu().numpy() - g5["mask_logits"]).max())
-    # Everything on the GPU: the HF decoder layers (GPU vs CPU GEMMs, 1e-6 apart) feed the
-    # sigmoid(mask) < 0.5 attention binarisation between layers; an attention bit whose logit
-    # sits within float noise of 0 may flip, which moves later logits by ~1e-3.  Such flips are
-    # counted against the CPU run's own interpolated logits: every flipped bit must lie within
-    # 1e-3 of the threshold, and only then is the end-to-end bound relaxed to 1e-2.
-    assert len(gpu_calls) == len(calls)
-    flips, explained = 0, True
-    for attn_g, ((_, _, size), (mask_ref, attn_ref)) in zip(gpu_calls, calls):
-        val = torch.nn.functional.interpolate(mask_ref, size=size, mode="bilinear", align_corners=False).flatten(2)
-        val = val.unsqueeze(1).expand(-1, hip_pred.num_heads, -1, -1).flatten(0, 1)
-        d = attn_g != attn_ref
-        flips += int(d.sum())
-        explained &= bool((val[d].abs() < 1e-3).all())
-    # The same count for the hot-path run against the reference's own attention masks (the
-    # oracle CPU model, pinned to G5 by test_oracle_full_model_matches_g5): backbone features a
-    # few 1e-6 from the reference's (the Swin-T and hot-path arithmetic on the GPU) can move a
-    # mask logit sitting within that distance of 0 across the binarisation threshold too.
-    ocalls = _oracle_mask_calls(pv_cpu)
-    assert len(ocalls) == len(calls)
-    rflips, rexplained = 0, True
-    for ((_, _, size), (mask_ref, attn_ref)), (mask_o, attn_o) in zip(calls, ocalls):
-        val = torch.nn.functional.interpolate(mask_o, size=size, mode="bilinear", align_corners=False).flatten(2)
-        val = val.unsqueeze(1).expand(-1, hip_pred.num_heads, -1, -1).flatten(0, 1)
-        d = attn_ref != attn_o
-        rflips += int(d.sum())
-        rexplained &= bool((val[d].abs() < 1e-3).all())
-    print(f"mask-logit max-abs-err (fp32): hot path {err:.3g} ({rflips} near-threshold flips against the "
-          f"reference's masks); everything on the GPU {gpu:.3g} ({flips} near-threshold attention-mask flips)")
-    assert rexplained, "an attention-mask bit of the hot-path run flipped away from the threshold"
-    assert explained, "an attention-mask bit flipped away from the threshold"
-    assert err <= (1e-3 if rflips == 0 else 1e-2)
-    assert gpu <= (1e-3 if flips == 0 and rflips == 0 else 1e-2)
-    np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-3 if rflips == 0 else 1e-2)
-
-
-def _oracle_mask_calls(pv_cpu):
-    """(mask logits, attention mask) of every mask-predictor call of the reference computation:
-    the drop-in model on the CPU with the HF modules and the oracle hot path (as
-    tests/test_oracle_model.py runs it)."""
-    from oracle import hot_path as hot_o
-    mo = _full_model().cpu().eval()
-    for mod in (mask_predictor, masked_attention, deform_attn):
-        mod.uninstall(mo)
-    plm = mo.model.pixel_level_module
-    sd = dict(plm.state_dict())
-    sd.update(dict(plm.named_parameters()))
-    plm.hot_path_features = lambda pv_, colors, ratios=None, **kw: hot_o.hot_path_forward(
-        list(colors), pv_, sd, training=False)[0]
-    calls = []
-    h = mo.model.transformer_module.decoder.mask_predictor.register_forward_hook(
-        lambda mod, inp, out: calls.append((out[0], out[1])))
-    try:
-        with torch.no_grad():
-            mo(pixel_values=pv_cpu)
-    finally:
-        h.remove()
-    return calls
+    ref = g5["mask_logits"]
+    hot = float(np.abs(out.masks_queries_logits.numpy() - ref).max())
+    gpu_forced = float(np.abs(runs[True][0].masks_queries_logits.cpu().numpy() - ref).max())
+    gpu = float(np.abs(runs[False][0].masks_queries_logits.cpu().numpy() - ref).max())
+    forced = refm.flips(runs[True][1])
+    first = refm.flips(runs[False][1], deltas=forced["deltas"], upto_first=True)
+    unforced = refm.flips(runs[False][1], deltas=forced["deltas"])
+    print(f"mask-logit max-abs-err (fp32, reference masks forced): hot path {hot:.3g}, everything on the GPU "
+          f"{gpu_forced:.3g}; unforced {gpu:.3g} with {unforced['flips']} flipped attention bits (first at call "
+          f"{first['first_call']}: {first['flips']} bits, {first['unexplained']} unexplained); forced run: "
+          f"{forced['flips']} own-mask flips, max near-threshold |delta logit| {forced['max_delta_logit']:.3g}")
+    assert hot <= 1e-3
+    assert gpu_forced <= 1e-3
+    np.testing.assert_allclose(out.class_queries_logits.numpy(), g5["class_logits"], atol=1e-3)
+    np.testing.assert_allclose(runs[True][0].class_queries_logits.cpu().numpy(), g5["class_logits"], atol=1e-3)
+    assert forced["unexplained"] == 0, "a bit of the model's own mask flipped away from the threshold"
+    assert first["unexplained"] == 0, "the unforced run's first flipped call has a flip beyond the arithmetic"
+    assert forced["max_delta_logit"] <= 1e-4
+    # the unforced run IS the forced one when no bit flips; otherwise its extra error is the flips'
+    assert gpu <= 1e-3 if unforced["flips"] == 0 else gpu <= 1e-2
 
 
 def test_full_model_mask_logits_bf16(golden):
@@ -278,8 +251,9 @@ def test_full_model_mask_logits_bf16(golden):
         out = m(pixel_values=pv)
     ref = g5["mask_logits"]
     rel = float(np.abs(out.masks_queries_logits.cpu().numpy() - ref).max() / np.abs(ref).max())
+    import bench
     print(f"mask-logit max-rel-err (bf16 hot path) = {rel:.3g}")
-    assert rel < 5e-2
+    assert rel < bench.BF16_LOGIT_REL_TOL  # the bench line's bound (parity.bf16.tolerance_rel)
 
 
 def test_full_model_grads_fp32(golden):

@@ -98,3 +98,30 @@ def test_oracle_grads_match_g6(golden):
         ref_norm = float(g6[n + "|norm"])
         assert abs(np.linalg.norm(g.astype(np.float64)) - ref_norm) <= 1e-3 * ref_norm + 1e-9, n
         np.testing.assert_allclose(g[g6[n + "|idx"]], g6[n + "|val"], rtol=1e-3, atol=1e-3 * (ref_norm / np.sqrt(g.size) + 1e-12))
+
+
+@pytest.mark.parametrize("tag,cid,H,W", [("g5", 1, 240, 320), ("g7", 7, 480, 640)])
+def test_oracle_attention_masks_match_g9(golden, tag, cid, H, W):
+    """G9 (the reference's own attention masks per mask-predictor call, make_golden.py attn) vs
+    the oracle composition on the CPU: every decoder layer's binarised mask bit-identical, or a
+    differing bit within FLIP_EXPLAIN_FACTOR x the call's near-threshold logit difference."""
+    import bench
+    refm = bench.ReferenceMasks(tag)
+    m = _model().eval()
+    m.model.pixel_level_module.hot_path_features = _oracle_hot(m.model.pixel_level_module, {})
+    pv = gi.pixel_values(cid, 1, H, W)
+    import hashlib
+    assert hashlib.sha256(pv.tobytes()).hexdigest() == refm.input_sha
+    rec = []
+    h = refm.attach(m, False, rec)
+    try:
+        with torch.no_grad():
+            m(pixel_values=torch.from_numpy(pv))
+    finally:
+        h.remove()
+    assert len(rec) == len(refm.calls) == 10
+    f = refm.flips(rec)
+    print(f"{tag}: oracle vs reference attention masks: {f['flips']} flipped bits, max near-threshold "
+          f"|delta logit| {f['max_delta_logit']:.3g}")
+    assert f["unexplained"] == 0 and f["flips"] <= 2
+    assert f["max_delta_logit"] <= 1e-4
