@@ -39,3 +39,23 @@ def test_bench_roofline_traffic_comes_from_the_newest_pmc_table():
                   if any(k.split(" grid=")[0].split("<")[0] == bench.CONV5_KERNEL for k in json.loads(t.read_text()))]
     assert got[1] == with_conv5[-1]
     assert bench.pmc_traffic(bench.CONV5_KERNEL, False) is None
+
+
+def test_bench_roofline_frac_comes_from_the_newest_kernel_trace():
+    """roofline.frac (verdict r04 #3): conv5's average duration from the newest committed bench-step
+    kernel trace (profiles/*/kernel_stats.csv) that has it, so the line's frac is recomputable from
+    profiles/ — 1.4496 TFLOP per launch at the default shape over that average, / 2.5 PF."""
+    import csv
+    sys.path.insert(0, str(REPO))
+    import bench
+    got = bench.profile_avg_ns(bench.CONV5_KERNEL, True)
+    assert got is not None and got[0] > 1e5
+    last = None
+    for t in sorted((REPO / "profiles").glob("*/kernel_stats.csv")):
+        for row in csv.DictReader(open(t, newline="")):
+            if bench.CONV5_KERNEL + "<" in row["Name"] or bench.CONV5_KERNEL + "(" in row["Name"]:
+                last = (float(row["AverageNs"]), str(t.relative_to(REPO)))
+    assert got[:2] == last
+    assert bench.profile_avg_ns(bench.CONV5_KERNEL, False) is None
+    frac = bench.CONV5_FLOP_PER_PX * 8 * 480 * 640 / (got[0] * 1e-9) / 1e12 / bench.MFMA_BF16_PEAK_TFLOPS
+    assert 0.2 < frac < 1.0
