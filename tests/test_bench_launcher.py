@@ -5,17 +5,21 @@ import subprocess
 import sys
 from pathlib import Path
 
+import pytest
+
 REPO = Path(__file__).resolve().parents[1]
 
 
-def test_bench_spawns_world2_ranks():
-    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--launcher-selftest"],
-                       capture_output=True, text=True, timeout=180, cwd=REPO)
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_spawns_ranks(world):
+    """C3's 2 and C4's 8 ranks from bench.py's own launcher."""
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", str(world), "--launcher-selftest"],
+                       capture_output=True, text=True, timeout=240, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out == {"world": 2, "rank_sum": 1.0, "local_rank": 0}
+    assert out == {"world": world, "rank_sum": float(world * (world - 1) // 2), "local_rank": 0}
 
 
 def test_bench_launcher_propagates_failure():

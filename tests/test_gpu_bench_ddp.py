@@ -1,7 +1,7 @@
-"""Row (e) on the GPU: bench.py's data-parallel step at world size 2 — gloo with both ranks on
-the one MI355X of a one-GPU test box (RCCL refuses two ranks on one device), and RCCL ("nccl",
-one rank per device) when the box shows two or more GPUs (skipped otherwise), so the driver's
-multi-GPU scaling run is not the first execution of the RCCL path.
+"""Row (e) on the GPU: bench.py's data-parallel step at world size 2 (BASELINE C3) and 8 (C4) — gloo
+with every rank on the one MI355X of a one-GPU test box (RCCL refuses two ranks on one device), and
+RCCL ("nccl", one rank per device) when the box shows enough GPUs (skipped otherwise), so the
+driver's multi-GPU scaling run is not the first execution of the RCCL path.
 
 * the launcher: ``bench.py --gpus 2`` spawns two ranks and reports n_gpus 2 / global batch 16;
 * DDP semantics of the step (the reference's Trainer, finetuning.py:98-113): after the
@@ -24,31 +24,33 @@ pytestmark = pytest.mark.gpu
 REPO = Path(__file__).resolve().parents[1]
 
 
-def _need_devices(backend):
-    if backend == "nccl" and torch.cuda.device_count() < 2:
-        pytest.skip("RCCL needs one device per rank: this box shows fewer than 2 GPUs")
+def _need_devices(backend, world=2):
+    if backend == "nccl" and torch.cuda.device_count() < world:
+        pytest.skip(f"RCCL needs one device per rank: this box shows fewer than {world} GPUs")
 
 
 BACKENDS = ["gloo", "nccl"]
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(400)
 @pytest.mark.parametrize("backend", BACKENDS)
-@pytest.mark.parametrize("H,W", [(96, 128), (480, 640)], ids=["96x128", "C3_640x480"])
-def test_bench_launcher_world2_json(H, W, backend):
-    """bench.py --gpus 2 end to end (its own launcher, 8 images per rank), incl. BASELINE's C3
-    shape; gloo with both ranks on the test box's one GPU, or RCCL on two GPUs."""
-    _need_devices(backend)
-    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", backend, "--steps", "2",
+@pytest.mark.parametrize("world,H,W", [(2, 96, 128), (2, 480, 640), (8, 96, 128), (8, 480, 640)],
+                         ids=["w2_96x128", "C3_w2_640x480", "w8_96x128", "C4_w8_640x480"])
+def test_bench_launcher_json(world, H, W, backend):
+    """bench.py --gpus N end to end (its own launcher, 8 images per rank) at BASELINE's C3 (2 ranks,
+    global batch 16) and C4 (8 ranks, global batch 64); gloo with every rank on the test box's one
+    GPU, or RCCL with one rank per GPU."""
+    _need_devices(backend, world)
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", str(world), "--backend", backend, "--steps", "2",
                         "--warmup", "1", "--cpu-baseline", "0", "--c5-stream", "0", "--inference", "0", "--parity", "0",
                         "--height", str(H), "--width", str(W)],
-                       capture_output=True, text=True, timeout=280, cwd=REPO)
+                       capture_output=True, text=True, timeout=380, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 16
-    assert out["distributed"]["world_size"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["n_gpus"] == world and out["config"]["global_batch"] == 8 * world
+    assert out["distributed"]["world_size"] == world and out["config"]["parallelism"] == f"dp{world}"
     assert out["distributed"]["backend"] == backend
     assert out["value"] > 0
 
@@ -84,7 +86,7 @@ def _worker(rank, world, port, q, shape, backend):
             fb, _, _, _ = bench.make_parts(ctx, 1)
             fb()
             ref.append([p.grad.clone() for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()])
-        mean = [(a + b) / 2 for a, b in zip(*ref)]
+        mean = [torch.stack(gs).sum(0) / world for gs in zip(*ref)]
         # the DDP step of this rank
         ctx = bench.build(args, dev, rank=rank)
         ctx["rp"].eval()
@@ -129,24 +131,27 @@ def _worker(rank, world, port, q, shape, backend):
         q.put((rank, traceback.format_exc() + repr(e)))
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("backend", BACKENDS)
-@pytest.mark.parametrize("shape", [(96, 128, 3), (480, 640, 8)], ids=["96x128_b3", "C3_640x480_b8"])
-def test_ddp_step_gradients_and_buffers_world2(shape, backend):
-    """Small shape, and BASELINE configs[2] (C3) at its workload: 640x480, 8 images per rank, bf16,
-    world size 2 (global batch 16) — gloo with both ranks on the one GPU of the test box, or RCCL
-    with one rank per GPU where the box has two."""
-    _need_devices(backend)
+@pytest.mark.parametrize("world,shape", [(2, (96, 128, 3)), (2, (480, 640, 8)), (8, (96, 128, 3)), (8, (480, 640, 8))],
+                         ids=["w2_96x128_b3", "C3_w2_640x480_b8", "w8_96x128_b3", "C4_w8_640x480_b8"])
+def test_ddp_step_gradients_and_buffers(world, shape, backend):
+    """Small shape, and BASELINE configs[2] / [3] (C3 / C4) at their workload: 640x480, 8 images per
+    rank, bf16, world size 2 / 8 (global batch 16 / 64) — gloo with every rank on the one GPU of the
+    test box, or RCCL with one rank per GPU where the box has enough.  Every rank's reduced
+    gradients equal the mean of all shards' standalone gradients (1e-5), the BatchNorm buffers the
+    forward sees are rank 0's (bitwise), and the in-backward AdamW equals DDP + one step (bitwise)."""
+    _need_devices(backend, world)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shape, backend)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, backend)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=360) for _ in procs)
+    res = dict(q.get(timeout=560) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    for r in (0, 1):
+    for r in range(world):
         assert isinstance(res[r], tuple), res[r]
         grad_err, buf_err, opt_err = res[r]
         assert grad_err < 1e-5, res

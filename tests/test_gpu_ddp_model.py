@@ -1,0 +1,143 @@
+"""Row (e) for the WHOLE drop-in model: the reference's only parallelism is the HF Trainer
+wrapping the whole model in DistributedDataParallel (finetuning.py:98-113; accelerate's state
+active, ``find_unused_parameters`` for the detached Swin-T and the gradient-free ratio predictor,
+Q1 / Q2).  Here ``CustomMask2FormerForUniversalSegmentation`` with every HIP module installed (the
+hot path's fused autograd Functions, the GEMM convolutions / linears, the deformable and masked
+attention, the point-sampled loss) runs under ``torch.nn.parallel.DistributedDataParallel`` over
+two 320x240 shards — gloo with both ranks on the test box's one GPU — and
+
+* every parameter that receives a gradient holds the mean of the two shards' standalone
+  gradients (1e-5 of its max), every other parameter none;
+* the loss normalises by Q16's double-divided instance count: accelerate's ``reduce`` (a MEAN
+  over ranks) inside HF ``get_num_masks`` (modeling_mask2former.py:781-794) and then ``/
+  world_size`` again — ``HipMask2FormerLoss.get_num_masks`` defers to it whenever accelerate's
+  state is set, so each of the 10 loss terms per step sees (n0 + n1) / 2 / 2.
+
+The standalone shards are computed with that same Q16 count so the two sides are the same
+function of the parameters; every forward seeds the CUDA generator per shard (the loss's point
+sampling draws torch.rand)."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK="0")  # every rank on the box's one GPU
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        sys.path[:0] = [str(REPO), str(REPO / "tests" / "golden")]
+        import golden_inputs as gi
+        import _rgbd_import  # noqa: F401
+        from accelerate import PartialState
+        from rgbd_amd import init as winit
+        from rgbd_amd.config import standard_config
+        from rgbd_amd.custom_model import CustomMask2FormerForUniversalSegmentation
+        from rgbd_amd.point_loss import HipMask2FormerLoss
+        state = PartialState(cpu=True)  # the Trainer's accelerate state: HF's get_num_masks all-reduces
+        assert PartialState._shared_state != {} and state.num_processes == world
+
+        H, W = 240, 320
+        pv = torch.from_numpy(gi.pixel_values(6, world, H, W)).to(dev)
+        masks, classes = gi.labels(6, world, H, W)
+        mask_labels = [torch.from_numpy(m).to(dev) for m in masks]
+        class_labels = [torch.from_numpy(c).to(dev) for c in classes]
+        n_total = float(sum(len(c) for c in classes))
+        q16 = max(n_total / world / world, 1.0)
+
+        def model():
+            torch.manual_seed(0)
+            m = CustomMask2FormerForUniversalSegmentation(standard_config(48), version="0.4.0")
+            winit.init_deterministic(m)
+            return m.to(dev).eval()  # eval: no dropout / drop-path draws, BN on its buffers
+
+        # standalone gradients of every shard, at Q16's instance count
+        orig = HipMask2FormerLoss.get_num_masks
+        HipMask2FormerLoss.get_num_masks = lambda self, cl, device: torch.tensor(q16, device=device)
+        try:
+            ref = []
+            for r in range(world):
+                m = model()
+                torch.manual_seed(1234 + r)
+                out = m(pixel_values=pv[r:r + 1], mask_labels=mask_labels[r:r + 1], class_labels=class_labels[r:r + 1])
+                out.loss.backward()
+                ref.append({n: (None if p.grad is None else p.grad.detach().clone()) for n, p in m.named_parameters()})
+                del m, out
+        finally:
+            HipMask2FormerLoss.get_num_masks = orig
+        # the Trainer's DDP step on this rank's shard, accelerate's count (the library's branch)
+        seen = []
+        HipMask2FormerLoss.get_num_masks = lambda self, cl, device: seen.append(orig(self, cl, device)) or seen[-1]
+        try:
+            m = model()
+            ddp = torch.nn.parallel.DistributedDataParallel(m, find_unused_parameters=True)
+            torch.manual_seed(1234 + rank)
+            out = ddp(pixel_values=pv[rank:rank + 1], mask_labels=mask_labels[rank:rank + 1],
+                      class_labels=class_labels[rank:rank + 1])
+            out.loss.backward()
+            torch.cuda.synchronize()
+        finally:
+            HipMask2FormerLoss.get_num_masks = orig
+        nm = sorted({round(float(t), 6) for t in seen})
+        worst, n_grad, bad_none = 0.0, 0, []
+        for n, p in m.named_parameters():
+            exp = [g[n] for g in ref]
+            if all(e is None for e in exp):
+                if p.grad is not None and float(p.grad.abs().max()) != 0.0:
+                    bad_none.append(n)
+                continue
+            mean = sum(torch.zeros_like(p) if e is None else e for e in exp) / world
+            if p.grad is None:
+                bad_none.append(n)
+                continue
+            n_grad += p.numel()
+            worst = max(worst, float((p.grad - mean).abs().max() / (mean.abs().max() + 1e-30)))
+        q.put((rank, {"worst": worst, "n_grad": n_grad, "bad": bad_none, "num_masks": nm, "calls": len(seen),
+                      "q16": q16}))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.timeout(600)
+def test_whole_model_ddp_equals_shard_mean_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=560) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert isinstance(res[r], dict), res[r]
+        got = res[r]
+        print(f"rank {r}: {got['n_grad']} grad-receiving parameters, worst rel err {got['worst']:.3g}, "
+              f"num_masks {got['num_masks']} over {got['calls']} loss terms (Q16: {got['q16']})")
+        assert not got["bad"], got["bad"][:10]
+        assert got["worst"] < 1e-5, got
+        # the reference model's grad-receiving parameters (37 330 321)
+        assert got["n_grad"] == 37_330_321, got["n_grad"]
+        assert got["calls"] == 10 and got["num_masks"] == [round(got["q16"], 6)], got
