@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU driver.  Stages (arguments, in order): smoke | tests [pytest args...] | bench | prof.
+# GPU driver.  Stages (arguments, in order): smoke | tests [pytest args...] | bench | prof.
 #   tests: the GPU suite (or the given test selection) without -x, so one call reports every
 #          failure; a hang ends at the per-test timeout.
 #   bench: bench.py default run (the driver's command).
@@ -7,8 +7,8 @@
 # Every GPU step has its own time limit; the chain stops at the first failing stage.
 cd "$GRAFT_REPO_ROOT" || exit 1
 R="$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r03
-O="$R/gpurun_out/r03"
+mkdir -p gpurun_out/${RUN:-r05}
+O="$R/gpurun_out/${RUN:-r05}"
 stage="$1"; shift
 case "$stage" in
   smoke)
@@ -23,7 +23,7 @@ case "$stage" in
     rc=$?; cat "$O/bench.json"; [ $rc -eq 0 ] || tail -20 "$O/bench.err"; exit $rc ;;
   prof)
     cd /tmp && export TMPDIR=/tmp
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --cpu-baseline 0 --inference 0 --c5-stream 0 --parity 0 "$@" > "$O/prof.log" 2>&1
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --cpu-baseline 0 --inference 0 --c5-stream 0 --parity 0 --full-model 0 "$@" > "$O/prof.log" 2>&1
     rc=$?; tail -3 "$O/prof.log"; exit $rc ;;
   fullprof)  # the whole drop-in model's training step (tools/bench_full_model.py) under the kernel trace
     cd /tmp && export TMPDIR=/tmp

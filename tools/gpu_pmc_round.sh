@@ -1,14 +1,14 @@
 #!/bin/bash
-# Round-4 PMC passes (kernel trace only, one counter group per pass, each pass its own time limit;
+# PMC passes (kernel trace only, one counter group per pass, each pass its own time limit;
 # MI355X_MICROARCH.md "rocprofv3 PMC slots": FETCH_SIZE and WRITE_SIZE in separate passes).
 #   ratio:  the ratio predictor (tools/micro_ratio.py, train mode, bench shape) — conv5, chain,
 #           gate, pool: HBM bytes, MFMA busy, wave-state counters.
 #   dsam:   the hot path's K5 legs (tools/micro_dsam.py, the bench's step): the same counters.
 #   step:   the bench's default step itself (bench.py, short run): every kernel of the step.
-# Tables: tools/traffic_table.py -> gpurun_out/r04/pmc_<which>.json (+ pmc_table.py text).
+# Tables: tools/traffic_table.py -> gpurun_out/<run>/pmc_<which>.json (+ pmc_table.py text).
 cd "$GRAFT_REPO_ROOT" || exit 1
 R="$GRAFT_REPO_ROOT"
-O="$R/gpurun_out/r04"
+O="$R/gpurun_out/${RUN:-r05}"
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 run_pass() {  # which driver-args group-index counters...
