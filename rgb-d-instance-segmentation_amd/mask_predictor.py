@@ -37,7 +37,7 @@ class MaskLogitsFunction(torch.autograd.Function):
         p2 = pix.reshape(B, C, P).contiguous()
         d_emb = d_pix = None
         if ctx.needs_input_grad[0]:   # d_emb[b] = g[b] pix[b]^T: K = pixels, split-K
-            d_emb = dense.gemm(g2, p2, 0, 0, Q, C, P, batch=B, sa=Q * P, sb=C * P)
+            d_emb = dense.gemm(g2, p2, 0, 0, Q, C, P, batch=B, sa=Q * P, sb=C * P).reshape(emb.shape)
         if ctx.needs_input_grad[1]:   # d_pix[b] = emb[b]^T g[b]: K = queries
             d_pix = dense.gemm(emb, g2, 1, 1, C, P, Q, batch=B, sa=Q * C, sb=Q * P).reshape(pix.shape)
         return d_emb, d_pix
