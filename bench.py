@@ -571,7 +571,7 @@ class ReferenceMasks:
                 "max_delta_logit": max(own_deltas) if own_deltas else 0.0, "deltas": own_deltas}
 
 
-def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7"):
+def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7", colour_bf16=False):
     """BASELINE.json's second metric: the full drop-in model (HF Swin / pixel decoder /
     transformer decoder around the HIP hot path, f1/f2 kernels installed), B=1, eval,
     deterministic weights, against the reference CPU run committed as
@@ -588,7 +588,9 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7"):
     the ratio, and so the window decisions, come from the bf16 ratio predictor; the HF modules
     around it stay float32.  ``ratio_fp32``: the ratio predictor alone in float32 (the
     reference's ratio, so the reference's window decisions): what remains is the error of the
-    bf16 DSAM / DGGM arithmetic."""
+    bf16 DSAM / DGGM arithmetic.  ``colour_bf16``: the float32 hot path fed with the Swin colour
+    maps rounded to bfloat16 (what the bf16 hot path takes in): the share of the bf16 error that
+    is the rounding of its inputs alone."""
     import hashlib
     from rgbd_amd import init as winit, ops, synthetic
     from rgbd_amd.config import standard_config
@@ -606,6 +608,10 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7"):
     rp = m.model.pixel_level_module.ratio_predictor
     if ratio_fp32:
         rp.compute_dtype = torch.float32
+    if colour_bf16:
+        plm = m.model.pixel_level_module
+        hpf = plm.hot_path_features
+        plm.hot_path_features = lambda pv_, colors, **kw: hpf(pv_, [c.to(torch.bfloat16).float() for c in colors], **kw)
     refm = ReferenceMasks(fixture)
     runs = {}
     for force in (False, True):
@@ -654,7 +660,11 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7"):
                     "of the model's own masks that differ from the reference's (forced run: each call on the "
                     "reference's inputs; first_call_unexplained: flips of the unforced run's first flipped call "
                     "whose reference logit lies beyond explain_factor x the forced run's |delta logit|)")}
-    if dtype == torch.float32:
+    if colour_bf16:
+        scale = float(np.abs(ref).max())
+        res.update(mask_logit_max_rel_err=err / scale, mask_logit_max_rel_err_masks_forced=ferr / scale,
+                   note_colour="float32 hot path on bf16-rounded colour maps: the input-rounding share of the bf16 error")
+    elif dtype == torch.float32:
         res["tolerance"] = 1e-3
     else:
         scale = float(np.abs(ref).max())
@@ -921,6 +931,8 @@ def main():
         out["parity"]["bf16_ratio_fp32"] = parity(dev, torch.bfloat16, ratio_fp32=True)
         # G5 (C1's 320x240) beside G7, fp32
         out["parity"]["g5_320x240"] = parity(dev, fixture="g5")
+        # bf16 error attribution: the float32 hot path on bf16-rounded colour maps
+        out["parity"]["bf16_attrib_colour_rounding"] = parity(dev, fixture="g7", colour_bf16=True)
     if rank == 0 and world == 1 and args.c5_stream:
         out["c5_stream"] = c5_stream(ctx)
     if rank == 0 and world == 1 and args.full_model:

@@ -178,6 +178,28 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
 // (sum, sum of squares), reduced in fixed order in double; running stats updated like torch.
 // one 256-thread block per channel; thread i sums slab rows i, i+256, ... in double, then a
 // fixed-shape tree reduction: deterministic for a given nslab.
+// BatchNorm from the batch sums (s, q) = (sum, sum of squares) over `count` values (train) or the
+// running stats (eval): per-channel affine, running stats updated like torch (unbiased variance)
+__device__ __forceinline__ void bn_finish(double s, double q, double count, int training, float momentum,
+                                          const float* gamma, const float* beta, float* run_mean, float* run_var,
+                                          int c, float2* __restrict__ affine) {
+  float mean, var;
+  if (training) {
+    const double m = s / count;
+    double v = q / count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    const double unb = count > 1.0 ? v * count / (count - 1.0) : v;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  } else {
+    mean = run_mean[c];
+    var = run_var[c];
+  }
+  const float sc = gamma[c] / sqrtf(var + BN_EPS);
+  affine[c] = make_float2(sc, beta[c] - mean * sc);
+}
 __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, int nslab, int row, int c_off, int c,
                                                double count, int training, float momentum, const float* gamma,
                                                const float* beta, float* run_mean, float* run_var,
@@ -200,22 +222,7 @@ __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, i
     __syncthreads();
   }
   if (threadIdx.x != 0) return;
-  float mean, var;
-  if (training) {
-    const double m = red[0][0] / count;
-    double v = red[1][0] / count - m * m;
-    if (v < 0.0) v = 0.0;
-    mean = (float)m;
-    var = (float)v;
-    const double unb = count > 1.0 ? v * count / (count - 1.0) : v;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
-  } else {
-    mean = run_mean[c];
-    var = run_var[c];
-  }
-  const float sc = gamma[c] / sqrtf(var + BN_EPS);
-  affine[c] = make_float2(sc, beta[c] - mean * sc);
+  bn_finish(red[0][0], red[1][0], count, training, momentum, gamma, beta, run_mean, run_var, c, affine);
 }
 __global__ __launch_bounds__(256) void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off,
                                                    int C, double count, int training, float momentum,
@@ -231,6 +238,355 @@ __global__ __launch_bounds__(256) void k_bn_affine_stem(const float* __restrict_
   const int l = blockIdx.x / 64, c = blockIdx.x % 64;
   bn_affine_body(slab, nslab, STEM_C, 64 * l, c, count, training, momentum, bn.p[4 * l], bn.p[4 * l + 1],
                  bn.p[4 * l + 2], bn.p[4 * l + 3], affine + 64 * l);
+}
+
+// ------------------------------------------------------------------ stem BN statistics (bf16, train)
+// The three stem BatchNorms (custom_model.py:1378-1394, 1463) need, per stem channel o, the batch
+// sums  sum_p y_o(p)  and  sum_p y_o(p)^2  of  y_o(p) = b_o + sum_k W_ok x_k(p),  x(p) the 7x7x3
+// window of the (bf16-rounded, zero-padded) depth planes at pixel p.  Both are moments of the
+// windows:  sum_p y = N b + W S1,  sum_p y^2 = N b^2 + 2 b W S1 + W S2 W^T  with
+// S1_k = sum_p x_k(p) and the Gram matrix S2_kl = sum_p x_k(p) x_l(p) (147 x 147).  S2 is a lag
+// sum: for k = (c1, a), l = (c2, a + L) it equals the full-image correlation
+//   F(c1, c2, L) = sum_{u1, v1} X_c1(u1, v1) X_c2(u1 + Ly, v1 + Lx)       (L in [-6, 6]^2)
+// minus the anchors (u1, v1) that window offset a moves outside the image (at most 3 border rows
+// and 3 border columns), so the whole Gram matrix costs 1 521 correlations instead of a stem
+// convolution: 9 MFMAs per 32 pixels (k_stem_lag: D[(c1,Ly)][(c2,Lx)] += X_c1(u - Ly, v)
+// X_c2(u, v + Lx) over rows u and 32-pixel blocks v, bf16 products exact, f32 accumulation per
+// wave, double across waves / workgroups), the border rows / columns by k_stem_frame, and
+// k_stem_s2 / k_stem_bn assemble S2, S1 and the BN affines in double.  This replaces the former
+// statistics pass over the stem (126 MFMAs per 32 pixels, 181 us per bench step).
+constexpr int SL_R = 32, SL_CW = 256, SL_PADL = 8;          // B rows per band, columns per chunk
+constexpr int SL_ROWS = SL_R + 12, SL_LD = SL_CW + 2 * SL_PADL;
+constexpr int SL_NL = 39, SL_NF = SL_NL * SL_NL;             // (channel, lag) per side; correlations
+constexpr int SL_REC = SL_NF + 3;                            // + the three plane sums
+constexpr size_t SL_SMEM = (size_t)3 * SL_ROWS * SL_LD * 2;
+static_assert(SL_SMEM >= SL_NF * sizeof(double), "k_stem_lag: LDS reused for the wave reduction");
+constexpr int SF_CH = 64;                                    // k_stem_frame: pixels per chunk
+constexpr int SF_T = 351, SF_REC = SF_T * 13 + 9;            // sums per (image, kind, chunk)
+
+struct StemGeom {
+  int nband, ncol, nwg, nfr_row, nfr_col, nfr;  // lag workgroups; frame chunks per row / col kind
+};
+inline StemGeom stem_geom(int B, int H, int W) {
+  StemGeom g;
+  g.nband = ceil_div(H, SL_R);
+  g.ncol = ceil_div(W, SL_CW);
+  g.nwg = B * g.nband * g.ncol;
+  g.nfr_row = ceil_div(W, SF_CH);
+  g.nfr_col = ceil_div(H, SF_CH);
+  g.nfr = B * 2 * (g.nfr_row + g.nfr_col);
+  return g;
+}
+inline bool stem_moments_ok(int H, int W) { return H >= 8 && W >= 8; }
+
+__device__ __forceinline__ float stem_x(const float* __restrict__ depth3, long long bstride, long long HW, int b, int c,
+                                        int H, int W, int y, int x) {
+  const bool ok = y >= 0 && y < H && x >= 0 && x < W;
+  const float v = depth3[b * bstride + c * HW + (long long)(ok ? y : 0) * W + (ok ? x : 0)];
+  return ok ? bf16_to_f32(f32_to_bf16(v)) : 0.f;
+}
+
+__global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ depth3, long long bstride, int B, int H,
+                                                  int W, int nband, int ncol, double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* X = (bf16_t*)smem;  // [3][SL_ROWS][SL_LD]: rows u0-6 .., columns cv0-8 ..
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wg = blockIdx.x, b = wg / (nband * ncol), rem = wg % (nband * ncol);
+  const int u0 = (rem / ncol) * SL_R, cv0 = (rem % ncol) * SL_CW;
+  const long long HW = (long long)H * W;
+  float tsum[3] = {0.f, 0.f, 0.f};
+  // 4 consecutive pixels per thread (16-byte loads, 8-byte LDS stores) where rows are 16-byte
+  // aligned; the groups of 4 then never straddle the image's right edge
+  const bool vec = (W & 3) == 0 && (bstride & 3) == 0 && ((uintptr_t)depth3 & 15) == 0;
+  for (int i = tid; i < 3 * SL_ROWS * (SL_LD / 4); i += 512) {
+    const int c = i / (SL_ROWS * (SL_LD / 4)), rr = (i / (SL_LD / 4)) % SL_ROWS, cc = 4 * (i % (SL_LD / 4));
+    const int yy = u0 - 6 + rr, xx = cv0 - SL_PADL + cc;
+    float v[4];
+    if (vec) {
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const float4 q = *reinterpret_cast<const float4*>(depth3 + b * bstride + c * HW + (long long)(ok ? yy : 0) * W +
+                                                         (ok ? xx : 0));
+      v[0] = ok ? bf16_to_f32(f32_to_bf16(q.x)) : 0.f;
+      v[1] = ok ? bf16_to_f32(f32_to_bf16(q.y)) : 0.f;
+      v[2] = ok ? bf16_to_f32(f32_to_bf16(q.z)) : 0.f;
+      v[3] = ok ? bf16_to_f32(f32_to_bf16(q.w)) : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = stem_x(depth3, bstride, HW, b, c, H, W, yy, xx + e);
+    }
+    *reinterpret_cast<uint2*>(X + (c * SL_ROWS + rr) * SL_LD + cc) =
+        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    // the plane sums over this workgroup's own pixels (rows [u0, u0+R), columns [cv0, cv0+CW))
+    if (rr >= 6 && rr < 6 + SL_R && cc >= SL_PADL && cc < SL_PADL + SL_CW) tsum[c] += (v[0] + v[1]) + (v[2] + v[3]);
+  }
+  __syncthreads();
+  // per-lane fragment bases: A rows m = (c1, Ly), B columns n = (c2, Lx); m, n >= 39 are zero
+  int abase[3], bbase[3];
+  bool aval[3], bval[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int m = 16 * i + r;
+    aval[i] = m < SL_NL;
+    const int c1 = aval[i] ? m / 13 : 0, ly = aval[i] ? m % 13 - 6 : 0;
+    abase[i] = (c1 * SL_ROWS + 6 - ly) * SL_LD + SL_PADL + 8 * g;     // + ur * SL_LD + (v0 - cv0)
+    bval[i] = m < SL_NL;
+    const int c2 = bval[i] ? m / 13 : 0, lx = bval[i] ? m % 13 - 6 : 0;
+    bbase[i] = (c2 * SL_ROWS + 6) * SL_LD + SL_PADL + 8 * g + lx;     // + ur * SL_LD + (v0 - cv0)
+  }
+  f32x4 acc[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nrow = min(SL_R, H - u0), nvb = (min(SL_CW, W - cv0) + 31) / 32;
+  const uint32_t* Xw = reinterpret_cast<const uint32_t*>(X);
+  for (int it = wave; it < nrow * nvb; it += 8) {
+    const int ur = it / nvb, off = ur * SL_LD + 32 * (it % nvb);
+    Frag<bf16_t> fa[3], fb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      fa[i].v = *reinterpret_cast<const uint4*>(X + abase[i] + off);
+      if (!aval[i]) fa[i].zero();
+      const int e = bbase[i] + off, w0 = e >> 1;
+      const uint32_t sh = (e & 1) * 2;
+      const uint32_t x0 = Xw[w0], x1 = Xw[w0 + 1], x2 = Xw[w0 + 2], x3 = Xw[w0 + 3], x4 = Xw[w0 + 4];
+      fb[i].v = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+      if (!bval[i]) fb[i].zero();
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) mma(acc[i][j], fa[i], fb[j]);
+  }
+  // the 8 waves' tiles summed in double, in wave order
+  __syncthreads();
+  double* red = (double*)smem;
+  for (int w = 0; w < 8; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = 16 * i + 4 * g + e, n = 16 * j + r;
+            if (m < SL_NL && n < SL_NL) {
+              const double v = (double)acc[i][j][e];
+              red[m * SL_NL + n] = w == 0 ? v : red[m * SL_NL + n] + v;
+            }
+          }
+    }
+    __syncthreads();
+  }
+  double* out = part + (long long)wg * SL_REC;
+  for (int i = tid; i < SL_NF; i += 512) out[i] = red[i];
+  __syncthreads();
+  // plane sums: per channel over the block's threads, fixed order
+  for (int c = 0; c < 3; ++c) {
+    red[tid] = (double)tsum[c];
+    __syncthreads();
+    for (int o = 256; o > 0; o >>= 1) {
+      if (tid < o) red[tid] += red[tid + o];
+      __syncthreads();
+    }
+    if (tid == 0) out[SL_NF + c] = red[0];
+    __syncthreads();
+  }
+}
+
+// Border rows / columns of every image: for the anchors of the three top (bottom) rows, per
+// (c1, c2, Ly) and anchor row j the 13 row sums over Lx of X_c1(u1, v) X_c2(u1 + Ly, v + Lx)
+// over this chunk's 64 columns; the column kinds likewise with the roles of the axes swapped; plus
+// the plain sums of X_c over the anchor rows / columns.  Workgroup = (chunk, kind, image), kind 0
+// top rows, 1 bottom rows, 2 left columns, 3 right columns.  out [image][kind][chunk][SF_REC] f32.
+__global__ __launch_bounds__(384) void k_stem_frame(const float* __restrict__ depth3, long long bstride, int B, int H,
+                                                    int W, int nfr_row, int nfr_col, float* __restrict__ out) {
+  __shared__ float S[3][15][SF_CH + 12];  // strip: 15 lines across (anchor lines +-6), 64 + 12 along
+  const int kind = blockIdx.y, b = blockIdx.z, chunk = blockIdx.x;
+  const bool rows = kind < 2;
+  const int nch = rows ? nfr_row : nfr_col;
+  if (chunk >= nch) return;
+  const long long HW = (long long)H * W;
+  const int a0 = chunk * SF_CH;                                      // first anchor along the strip
+  const int line0 = kind == 0 ? 0 : (kind == 1 ? H - 3 : (kind == 2 ? 0 : W - 3));  // first anchor line
+  for (int i = threadIdx.x; i < 3 * 15 * (SF_CH + 12); i += 384) {
+    const int c = i / (15 * (SF_CH + 12)), li = (i / (SF_CH + 12)) % 15, al = i % (SF_CH + 12);
+    const int ln = line0 - 6 + li, at = a0 - 6 + al;                // across, along
+    S[c][li][al] = rows ? stem_x(depth3, bstride, HW, b, c, H, W, ln, at) : stem_x(depth3, bstride, HW, b, c, H, W, at, ln);
+  }
+  __syncthreads();
+  const int nal = min(SF_CH, (rows ? W : H) - a0);
+  float* o = out + ((long long)(b * 4 + kind) * max(nfr_row, nfr_col) + chunk) * SF_REC;
+  const int t = threadIdx.x;
+  if (t < SF_T) {  // t = ((c1 * 3 + c2) * 13 + s1) * 3 + j: s1 the across lag, 13 along lags
+    const int j = t % 3, s1 = (t / 3) % 13, c2 = (t / 39) % 3, c1 = t / 117;
+    float acc[13];
+#pragma unroll
+    for (int q = 0; q < 13; ++q) acc[q] = 0.f;
+    float win[13];
+#pragma unroll
+    for (int q = 0; q < 13; ++q) win[q] = S[c2][6 + j + s1 - 6][q];  // along positions a - 6 .. a + 6 of a = 0
+    for (int a = 0; a < nal; ++a) {
+      const float x1 = S[c1][6 + j][6 + a];
+#pragma unroll
+      for (int q = 0; q < 13; ++q) acc[q] = __builtin_fmaf(x1, win[q], acc[q]);
+#pragma unroll
+      for (int q = 0; q < 12; ++q) win[q] = win[q + 1];
+      win[12] = S[c2][j + s1][a + 13 < SF_CH + 12 ? a + 13 : SF_CH + 11];
+    }
+#pragma unroll
+    for (int q = 0; q < 13; ++q) o[t * 13 + q] = acc[q];
+  } else if (t < SF_T + 9) {  // plain sums of X_c over anchor line j
+    const int c = (t - SF_T) / 3, j = (t - SF_T) % 3;
+    float s = 0.f;
+    for (int a = 0; a < nal; ++a) s += S[c][6 + j][6 + a];
+    o[SF_T * 13 + c * 3 + j] = s;
+  }
+}
+
+// Reduce the lag partials over workgroups (fixed order) and the frame chunks per (image, kind):
+// F [SL_REC] double, fr [image][kind][SF_REC] double.
+__global__ __launch_bounds__(256) void k_stem_reduce(const double* __restrict__ part, int nwg,
+                                                     const float* __restrict__ fchunks, int B, int nfr_row,
+                                                     int nfr_col, double* __restrict__ F, double* __restrict__ fr) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < SL_REC) {
+    double s = 0.0;
+    for (int w = 0; w < nwg; ++w) s += part[(long long)w * SL_REC + i];
+    F[i] = s;
+    return;
+  }
+  const int j = i - SL_REC;
+  if (j >= B * 4 * SF_REC) return;
+  const int e = j % SF_REC, bk = j / SF_REC, kind = bk % 4;
+  const int nch = kind < 2 ? nfr_row : nfr_col, mx = max(nfr_row, nfr_col);
+  double s = 0.0;
+  for (int c = 0; c < nch; ++c) s += (double)fchunks[((long long)bk * mx + c) * SF_REC + e];
+  fr[j] = s;
+}
+
+// S2 [147][147] and S1 [147] (k = c * 49 + ay * 7 + ax, the window offset a = (ay, ax) of
+// channel c) over the batch, double: thread per (k, l), the extra 147 threads S1.
+__global__ __launch_bounds__(256) void k_stem_s2(const double* __restrict__ F, const double* __restrict__ fr,
+                                                 const float* __restrict__ depth3, long long bstride, int B, int H,
+                                                 int W, double* __restrict__ S2, double* __restrict__ S1) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 147 * 147 + 147) return;
+  const bool is_s1 = i >= 147 * 147;
+  const int k = is_s1 ? i - 147 * 147 : i / 147, l = is_s1 ? k : i % 147;
+  const int c1 = k / 49, ay = (k % 49) / 7, ax = k % 7;
+  const int c2 = l / 49, by = (l % 49) / 7, bx = l % 7;
+  const int ly = by - ay, lx = bx - ax;
+  // excluded anchor rows / columns of offset a: top j < ay - 3, or bottom j >= ay (j = 0..2)
+  const int rkind = ay > 3 ? 0 : 1, rlo = ay > 3 ? 0 : ay, rhi = ay > 3 ? ay - 3 : (ay < 3 ? 3 : 0);
+  const int ckind = ax > 3 ? 2 : 3, clo = ax > 3 ? 0 : ax, chi = ax > 3 ? ax - 3 : (ax < 3 ? 3 : 0);
+  const long long HW = (long long)H * W;
+  double s = is_s1 ? 0.0 : F[((c1 * 13 + ly + 6) * SL_NL) + c2 * 13 + lx + 6];
+  if (is_s1) s = F[SL_NF + c1];
+  for (int b = 0; b < B; ++b) {
+    const double* rk = fr + ((long long)b * 4 + rkind) * SF_REC;
+    const double* ck = fr + ((long long)b * 4 + ckind) * SF_REC;
+    for (int j = rlo; j < rhi; ++j)
+      s -= is_s1 ? rk[SF_T * 13 + c1 * 3 + j] : rk[(((c1 * 3 + c2) * 13 + ly + 6) * 3 + j) * 13 + lx + 6];
+    for (int j = clo; j < chi; ++j)
+      s -= is_s1 ? ck[SF_T * 13 + c1 * 3 + j] : ck[(((c1 * 3 + c2) * 13 + lx + 6) * 3 + j) * 13 + ly + 6];
+    for (int jr = rlo; jr < rhi; ++jr) {  // corners: excluded in both, subtracted twice
+      const int u1 = rkind == 0 ? jr : H - 3 + jr;
+      for (int jc = clo; jc < chi; ++jc) {
+        const int v1 = ckind == 2 ? jc : W - 3 + jc;
+        const float x1 = stem_x(depth3, bstride, HW, b, c1, H, W, u1, v1);
+        s += is_s1 ? (double)x1 : (double)x1 * stem_x(depth3, bstride, HW, b, c2, H, W, u1 + ly, v1 + lx);
+      }
+    }
+  }
+  if (is_s1)
+    S1[k] = s;
+  else
+    S2[i] = s;
+}
+
+// Per stem channel o (one block each): sum y = N b + w.S1, sum y^2 = N b^2 + 2 b w.S1 + w S2 w^T,
+// then the BatchNorm of bn_affine_body (train mode) from the double sums.
+__global__ __launch_bounds__(256) void k_stem_bn(const double* __restrict__ S2, const double* __restrict__ S1,
+                                                 const char* __restrict__ blob, Layout L, double count, float momentum,
+                                                 BnPtrs bn, float2* __restrict__ affine) {
+  __shared__ double red[2][256];
+  __shared__ double w[147];
+  const int o = blockIdx.x, t = threadIdx.x;
+  const bf16_t* w1s = (const bf16_t*)(blob + L.w1s);
+  if (t < 147) w[t] = (double)bf16_to_f32(w1s[o * STEM_K2 + ((t / 49) * 7 + (t % 49) / 7) * 8 + t % 7]);
+  __syncthreads();
+  double a = 0.0, q = 0.0;
+  if (t < 147) {
+    a = w[t] * S1[t];
+    for (int l = 0; l < 147; ++l) q += w[l] * S2[l * 147 + t];  // S2 symmetric: coalesced rows
+    q *= w[t];
+  }
+  red[0][t] = a;
+  red[1][t] = q;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) {
+      red[0][t] += red[0][t + s];
+      red[1][t] += red[1][t + s];
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const double bias = (double)((const float*)(blob + L.b1))[o];
+  const double sy = count * bias + red[0][0];
+  const double sq = count * bias * bias + 2.0 * bias * red[0][0] + red[1][0];
+  const int l = o / 64, c = o % 64;
+  bn_finish(sy, sq, count, 1, momentum, bn.p[4 * l], bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], c,
+            affine + 64 * l);
+}
+
+struct StemWs {
+  size_t part, fchunks, F, fr, S2, S1, total;
+};
+inline StemWs stem_ws(int B, int H, int W) {
+  const StemGeom g = stem_geom(B, H, W);
+  StemWs s;
+  size_t o = 0;
+  auto seg = [&](size_t bytes) {
+    size_t r = o;
+    o += align256(bytes);
+    return r;
+  };
+  s.part = seg((size_t)g.nwg * SL_REC * sizeof(double));
+  s.fchunks = seg((size_t)B * 4 * std::max(g.nfr_row, g.nfr_col) * SF_REC * sizeof(float));
+  s.F = seg(SL_REC * sizeof(double));
+  s.fr = seg((size_t)B * 4 * SF_REC * sizeof(double));
+  s.S2 = seg(147 * 147 * sizeof(double));
+  s.S1 = seg(147 * sizeof(double));
+  s.total = o;
+  return s;
+}
+
+// the moments of every window and the stem BN affines (aff1) + running stats, train mode
+int stem_bn_moments(const float* depth3, long long bstride, int B, int H, int W, const char* blob, const Layout& L,
+                    float momentum, const BnPtrs& bn, float2* aff1, char* ws, hipStream_t s) {
+  const StemGeom g = stem_geom(B, H, W);
+  const StemWs w = stem_ws(B, H, W);
+  double* part = (double*)(ws + w.part);
+  float* fch = (float*)(ws + w.fchunks);
+  double* F = (double*)(ws + w.F);
+  double* fr = (double*)(ws + w.fr);
+  double* S2 = (double*)(ws + w.S2);
+  double* S1 = (double*)(ws + w.S1);
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)k_stem_lag, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL_SMEM);
+  if (attr != hipSuccess) return (int)attr;
+  k_stem_lag<<<g.nwg, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part);
+  k_stem_frame<<<dim3(std::max(g.nfr_row, g.nfr_col), 4, B), 384, 0, s>>>(depth3, bstride, B, H, W, g.nfr_row,
+                                                                           g.nfr_col, fch);
+  k_stem_reduce<<<ceil_div(SL_REC + (long long)B * 4 * SF_REC, 256), 256, 0, s>>>(part, g.nwg, fch, B, g.nfr_row,
+                                                                                  g.nfr_col, F, fr);
+  k_stem_s2<<<ceil_div(147 * 147 + 147, 256), 256, 0, s>>>(F, fr, depth3, bstride, B, H, W, S2, S1);
+  k_stem_bn<<<STEM_C, 256, 0, s>>>(S2, S1, blob, L, (double)B * H * W, momentum, bn, aff1);
+  return RGBD_OK;
 }
 
 // ------------------------------------------------------------------ chain (stem, fusion, attention)
@@ -1819,7 +2175,7 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
 }
 
 struct Ws {  // workspace carve
-  size_t aff1, aff2, aff5, slab, att, y, part, pooled, zpart, feat, h1, fold, total;
+  size_t aff1, aff2, aff5, slab, att, y, part, pooled, zpart, feat, h1, fold, stem, total;
 };
 
 inline int chain_grid(int B, int H, int W) {
@@ -1874,6 +2230,7 @@ inline Ws make_ws(int es, int B, int H, int W) {
   w.feat = seg((size_t)B * C6 * sizeof(float));
   w.h1 = seg((size_t)B * 128 * sizeof(float));
   w.fold = seg(es == 2 ? FOLD_BYTES : 0);
+  w.stem = seg(es == 2 && stem_moments_ok(H, W) ? stem_ws(B, H, W).total : 0);
   w.total = o;
   return w;
 }
@@ -1926,8 +2283,13 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
       k_rp_chain<T, PH><<<gch, 256, 0, s>>>(depth3, bstride, B, H, W, blob, L, A1, A2, SL, (T*)(OUT));            \
   } while (0)
   // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
-  if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
-  k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
+  if (training && v2 && stem_moments_ok(H, W)) {  // bf16 train: the moments of the windows (no stem pass)
+    const int e = stem_bn_moments(depth3, bstride, B, H, W, blob, L, momentum, bn, aff1, ws + w.stem, s);
+    if (e != RGBD_OK) return e;
+  } else {
+    if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
+    k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
+  }
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate

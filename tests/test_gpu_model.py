@@ -106,6 +106,43 @@ def test_bf16_train_mode_batchnorm_stats(H, W):
             assert rel <= 5e-2, (k, rel)
 
 
+@pytest.mark.parametrize("H,W", [(240, 320), (90, 125), (480, 640), (7, 9)])
+def test_bf16_stem_bn_batch_stats_exact(H, W):
+    """The stem BatchNorms' batch statistics in bf16 train mode come from the moments of the 7x7x3
+    depth windows (k_stem_lag / k_stem_frame / k_stem_s2 / k_stem_bn: lag correlations + border
+    corrections, double), not from a pass over the stem — against float64 arithmetic on the same
+    bf16-rounded depth and stem weights: batch mean to 2e-6 of the channel scale, unbiased
+    variance to 2e-5 relative (read back from the running-stat update, momentum 0.1).  (7, 9):
+    below the moments path's minimum size, the former statistics pass."""
+    import torch.nn.functional as F
+    pv = gi.pixel_values(8, 2, H, W)[:, 3:6]
+    m = _ratio_module()
+    m.compute_dtype = torch.bfloat16
+    m = m.to(DEV).train()
+    mods = dict(m.named_modules())
+    bns = [mods[f"scale{i}_conv.1"] for i in (1, 2, 3)]
+    for bn in bns:
+        bn.running_mean.zero_()
+        bn.running_var.fill_(1.0)
+    m(torch.from_numpy(pv).to(DEV))
+    torch.cuda.synchronize()
+    x = torch.from_numpy(pv).to(torch.bfloat16).double()
+    for i, bn in enumerate(bns):
+        conv = mods[f"scale{i + 1}_conv.0"]
+        w = conv.weight.detach().cpu().to(torch.bfloat16).double()
+        y = F.conv2d(x, w, conv.bias.detach().cpu().double(), padding=conv.padding)
+        mean = y.mean((0, 2, 3))
+        var = y.var((0, 2, 3), unbiased=True)
+        got_mean = bn.running_mean.detach().cpu().double() / 0.1
+        got_var = (bn.running_var.detach().cpu().double() - 0.9) / 0.1
+        scale = float(y.abs().max())
+        dm = float((got_mean - mean).abs().max())
+        dv = float(((got_var - var).abs() / var.abs().clamp_min(1e-12)).max())
+        print(f"stem BN {i}: mean err {dm:.3g} (scale {scale:.3g}), var rel err {dv:.3g}")
+        assert dm <= 2e-6 * max(scale, 1.0), (i, dm)
+        assert dv <= 2e-5, (i, dv)
+
+
 @pytest.mark.parametrize("H,W", [(64, 96), (90, 125), (240, 320)])
 @pytest.mark.parametrize("path", ["gate", "phase2"])
 def test_bf16_train_mode_gated_features(H, W, path, monkeypatch):
