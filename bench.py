@@ -571,7 +571,7 @@ class ReferenceMasks:
                 "max_delta_logit": max(own_deltas) if own_deltas else 0.0, "deltas": own_deltas}
 
 
-def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7", colour_bf16=False):
+def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7", colour_bf16=False, out_bf16=False):
     """BASELINE.json's second metric: the full drop-in model (HF Swin / pixel decoder /
     transformer decoder around the HIP hot path, f1/f2 kernels installed), B=1, eval,
     deterministic weights, against the reference CPU run committed as
@@ -590,7 +590,8 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7", colour_bf16
     reference's ratio, so the reference's window decisions): what remains is the error of the
     bf16 DSAM / DGGM arithmetic.  ``colour_bf16``: the float32 hot path fed with the Swin colour
     maps rounded to bfloat16 (what the bf16 hot path takes in): the share of the bf16 error that
-    is the rounding of its inputs alone."""
+    is the rounding of its inputs alone; ``out_bf16`` in addition rounds the hot path's four
+    output features to bfloat16 (what the bf16 hot path hands the float32 pixel decoder)."""
     import hashlib
     from rgbd_amd import init as winit, ops, synthetic
     from rgbd_amd.config import standard_config
@@ -608,10 +609,15 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7", colour_bf16
     rp = m.model.pixel_level_module.ratio_predictor
     if ratio_fp32:
         rp.compute_dtype = torch.float32
-    if colour_bf16:
+    if colour_bf16 or out_bf16:
         plm = m.model.pixel_level_module
         hpf = plm.hot_path_features
-        plm.hot_path_features = lambda pv_, colors, **kw: hpf(pv_, [c.to(torch.bfloat16).float() for c in colors], **kw)
+        rnd = (lambda ts: [t.to(torch.bfloat16).float() for t in ts])
+
+        def patched(pv_, colors, **kw):
+            feats = hpf(pv_, rnd(colors) if colour_bf16 else list(colors), **kw)
+            return rnd(feats) if out_bf16 else feats
+        plm.hot_path_features = patched
     refm = ReferenceMasks(fixture)
     runs = {}
     for force in (False, True):
@@ -660,10 +666,12 @@ def parity(dev, dtype=torch.float32, ratio_fp32=False, fixture="g7", colour_bf16
                     "of the model's own masks that differ from the reference's (forced run: each call on the "
                     "reference's inputs; first_call_unexplained: flips of the unforced run's first flipped call "
                     "whose reference logit lies beyond explain_factor x the forced run's |delta logit|)")}
-    if colour_bf16:
+    if colour_bf16 or out_bf16:
         scale = float(np.abs(ref).max())
         res.update(mask_logit_max_rel_err=err / scale, mask_logit_max_rel_err_masks_forced=ferr / scale,
-                   note_colour="float32 hot path on bf16-rounded colour maps: the input-rounding share of the bf16 error")
+                   note_attrib=("float32 hot path" + (" on bf16-rounded colour maps" if colour_bf16 else "") +
+                                (" with its outputs rounded to bf16" if out_bf16 else "") +
+                                ": that share of the bf16 error"))
     elif dtype == torch.float32:
         res["tolerance"] = 1e-3
     else:
@@ -933,6 +941,8 @@ def main():
         out["parity"]["g5_320x240"] = parity(dev, fixture="g5")
         # bf16 error attribution: the float32 hot path on bf16-rounded colour maps
         out["parity"]["bf16_attrib_colour_rounding"] = parity(dev, fixture="g7", colour_bf16=True)
+        out["parity"]["bf16_attrib_colour_and_output_rounding"] = parity(dev, fixture="g7", colour_bf16=True,
+                                                                        out_bf16=True)
     if rank == 0 and world == 1 and args.c5_stream:
         out["c5_stream"] = c5_stream(ctx)
     if rank == 0 and world == 1 and args.full_model:

@@ -310,6 +310,13 @@ int rgbd_dsam_bwd_weight_planned_multi(int n, const rgbd_dsam_dw_run* runs, cons
 int rgbd_adamw_multi(int n, float* const* params, const float* const* grads, float* const* exp_avg,
                      float* const* exp_avg_sq, const long long* numel, const float* step, double lr, double beta1,
                      double beta2, double eps, double weight_decay, void* stream);
+/* The same update, also writing each updated parameter's bfloat16 copy (round to nearest even, the
+ * bits torch's .to(torch.bfloat16) gives) into shadows[i] (a host array of device pointers; an
+ * entry may be NULL): the next forward's bf16 GEMM operands without a cast launch per weight. */
+int rgbd_adamw_multi_shadow(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                            float* const* exp_avg_sq, void* const* shadows, const long long* numel,
+                            const float* step, double lr, double beta1, double beta2, double eps,
+                            double weight_decay, void* stream);
 
 /* ---------------------------------------------------------------- K4 ratio predictor
  * EnhancedDepthImageRatioPredictor.forward (custom_model.py:1444-1487) for the batch:

@@ -63,6 +63,8 @@ SIGNATURES = {
     "rgbd_nchw_to_nhwc_multi": (_I, [_I, _P, _P]),
     "rgbd_adamw_multi": (_I, [_I, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                              ctypes.c_double, ctypes.c_double, _P]),
+    "rgbd_adamw_multi_shadow": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, _P]),
     "rgbd_dsam_packed_elems": (_LL, [_I, _I, _I]),
     "rgbd_dsam_pack_weights": (_I, [_I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "rgbd_dsam_code_masks": (_I, [_I, _P, _P, _P, _P]),

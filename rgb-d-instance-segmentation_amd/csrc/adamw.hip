@@ -8,6 +8,9 @@
 // before the launch).  HBM-bound: 16 bytes read and 12 written per element (p, g, m, v; p, m, v).
 // A workgroup takes 4096 elements of one tensor (16-byte accesses when the tensor allows them);
 // the tensor table travels as a kernel argument, so the launch holds no host-side state.
+// rgbd_adamw_multi_shadow also writes each updated parameter's bfloat16 copy (round to nearest
+// even, the bits torch's .to(bfloat16) gives) into a caller buffer: the bf16 operand the next
+// forward's GEMMs read (dense.cast_weight), without a separate cast launch per weight.
 #include "common.hpp"
 
 #include <math.h>
@@ -22,6 +25,7 @@ struct AwTable {
   const float* g[AW_MAXT];
   float* m[AW_MAXT];
   float* v[AW_MAXT];
+  bf16_t* s[AW_MAXT];  // bfloat16 shadow of p (nullptr: none)
   long long n[AW_MAXT];
   int block0[AW_MAXT + 1];  // first workgroup of each tensor
   int nt;
@@ -64,7 +68,9 @@ __global__ __launch_bounds__(256) void k_adamw_multi(const AwTable T, const floa
   const float* __restrict__ G = T.g[t];
   float* __restrict__ M = T.m[t];
   float* __restrict__ V = T.v[t];
-  const bool vec = ((((uintptr_t)P) | ((uintptr_t)G) | ((uintptr_t)M) | ((uintptr_t)V)) & 15) == 0;
+  bf16_t* __restrict__ S = T.s[t];
+  const bool vec = ((((uintptr_t)P) | ((uintptr_t)G) | ((uintptr_t)M) | ((uintptr_t)V)) & 15) == 0 &&
+                   (((uintptr_t)S) & 7) == 0;
   if (vec && e0 + AW_CHUNK <= n) {
 #pragma unroll
     for (int k = 0; k < AW_CHUNK / 1024; ++k) {
@@ -78,6 +84,7 @@ __global__ __launch_bounds__(256) void k_adamw_multi(const AwTable T, const floa
       *reinterpret_cast<float4*>(P + e) = p;
       *reinterpret_cast<float4*>(M + e) = m;
       *reinterpret_cast<float4*>(V + e) = v;
+      if (S) *reinterpret_cast<uint2*>(S + e) = make_uint2(pack_bf16x2(p.x, p.y), pack_bf16x2(p.z, p.w));
     }
     return;
   }
@@ -87,6 +94,7 @@ __global__ __launch_bounds__(256) void k_adamw_multi(const AwTable T, const floa
     P[e] = p;
     M[e] = m;
     V[e] = v;
+    if (S) S[e] = f32_to_bf16(p);
   }
 }
 
@@ -95,11 +103,9 @@ __global__ __launch_bounds__(256) void k_adamw_multi(const AwTable T, const floa
 
 using namespace rgbd;
 
-extern "C" {
-
-int rgbd_adamw_multi(int n, float* const* params, const float* const* grads, float* const* exp_avg,
-                     float* const* exp_avg_sq, const long long* numel, const float* step, double lr, double beta1,
-                     double beta2, double eps, double weight_decay, void* stream) {
+static int adamw_launch(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                        float* const* exp_avg_sq, void* const* shadows, const long long* numel, const float* step,
+                        double lr, double beta1, double beta2, double eps, double weight_decay, void* stream) {
   RGBD_REQUIRE(n >= 1 && n <= AW_MAXT && params && grads && exp_avg && exp_avg_sq && numel && step, RGBD_E_ARG);
   AwTable T;
   long long blocks = 0;
@@ -110,6 +116,7 @@ int rgbd_adamw_multi(int n, float* const* params, const float* const* grads, flo
     T.g[i] = grads[i];
     T.m[i] = exp_avg[i];
     T.v[i] = exp_avg_sq[i];
+    T.s[i] = shadows ? (bf16_t*)shadows[i] : nullptr;
     T.n[i] = numel[i];
     T.block0[i] = (int)blocks;
     blocks += (numel[i] + AW_CHUNK - 1) / AW_CHUNK;
@@ -131,6 +138,23 @@ int rgbd_adamw_multi(int n, float* const* params, const float* const* grads, flo
   k_adamw_multi<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(T, step, h);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
+}
+
+extern "C" {
+
+int rgbd_adamw_multi(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                     float* const* exp_avg_sq, const long long* numel, const float* step, double lr, double beta1,
+                     double beta2, double eps, double weight_decay, void* stream) {
+  return adamw_launch(n, params, grads, exp_avg, exp_avg_sq, nullptr, numel, step, lr, beta1, beta2, eps,
+                      weight_decay, stream);
+}
+
+int rgbd_adamw_multi_shadow(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                            float* const* exp_avg_sq, void* const* shadows, const long long* numel, const float* step,
+                            double lr, double beta1, double beta2, double eps, double weight_decay, void* stream) {
+  RGBD_REQUIRE(shadows, RGBD_E_ARG);
+  return adamw_launch(n, params, grads, exp_avg, exp_avg_sq, shadows, numel, step, lr, beta1, beta2, eps,
+                      weight_decay, stream);
 }
 
 }  // extern "C"

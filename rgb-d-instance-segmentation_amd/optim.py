@@ -8,6 +8,10 @@ Trainer builds (finetuning.py:98) is ``HipAdamW(params, **HF_TRAINER_ADAMW)``: l
 (mask2former/config.json:12-13) and TrainingArguments' defaults for the rest — weight_decay
 0.0 (config.json does not set it), betas (0.9, 0.999), eps 1e-8.
 
+A parameter that a HIP layer casts to bfloat16 (dense.cast_weight, under autocast) gets its bf16
+copy rewritten by the same launch (rgbd_adamw_multi_shadow) and re-keyed, so the next forward
+takes it without one cast launch per weight.
+
 bench.py's optimizer (in-backward groups and the captured step); DESIGN.md §9."""
 import ctypes
 
@@ -21,6 +25,19 @@ _MAXT = 48
 # HF TrainingArguments' AdamW (adam_beta1/2, adam_epsilon, weight_decay defaults) at the
 # reference's learning rate (mask2former/config.json:12)
 HF_TRAINER_ADAMW = dict(lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0)
+
+
+def _shadow(p):
+    """The bfloat16 copy of ``p`` that dense.cast_weight holds (the bf16 GEMM operand of a HIP
+    layer under autocast), re-used as the buffer the step writes the updated copy into; None when
+    the parameter has none."""
+    hit = getattr(p, "_rgbd_cast", None)
+    if hit is None or hit[0][3] != torch.bfloat16:
+        return None
+    x = hit[1]
+    if x.dtype != torch.bfloat16 or x.shape != p.shape or not x.is_contiguous() or x.device != p.device:
+        return None
+    return x
 
 
 class HipAdamW(torch.optim.Optimizer):
@@ -73,6 +90,7 @@ class HipAdamW(torch.optim.Optimizer):
                 continue
             step.add_(1.0)  # on the device: a captured graph replays the increment
             b1, b2 = group["betas"]
+            shadows = [_shadow(p) for p in params]
             for i in range(0, len(params), _MAXT):
                 run = params[i:i + _MAXT]
                 n = len(run)
@@ -81,12 +99,23 @@ class HipAdamW(torch.optim.Optimizer):
                 M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in run])
                 V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in run])
                 N = (ctypes.c_longlong * n)(*[p.numel() for p in run])
-                check(L.rgbd_adamw_multi(n, P, G, M, V, N, ctypes.c_void_p(step.data_ptr()), float(group["lr"]),
-                                         float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
-                                         _stream(run[0].device)), "rgbd_adamw_multi")
+                sh = shadows[i:i + _MAXT]
+                args = (float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
+                        _stream(run[0].device))
+                if any(x is not None for x in sh):
+                    S = (ctypes.c_void_p * n)(*[None if x is None else x.data_ptr() for x in sh])
+                    check(L.rgbd_adamw_multi_shadow(n, P, G, M, V, S, N, ctypes.c_void_p(step.data_ptr()), *args),
+                          "rgbd_adamw_multi_shadow")
+                else:
+                    check(L.rgbd_adamw_multi(n, P, G, M, V, N, ctypes.c_void_p(step.data_ptr()), *args),
+                          "rgbd_adamw_multi")
             # the kernel wrote through raw pointers: bump the version counters (host only, safe
             # under capture) so autograd's saved-tensor checks and version-keyed caches see it
             torch.autograd.graph.increment_version(params)
+            for p, x in zip(params, shadows):
+                if x is not None:  # the bf16 copy the kernel wrote is current: dense.cast_weight's key
+                    # after this step (the global post-step hook advances the epoch by one)
+                    p._rgbd_cast = ((p.data_ptr(), p._version, getattr(p, "_rgbd_epoch", 0) + 1, torch.bfloat16), x)
         return loss
 
     def load_state_dict(self, state_dict):

@@ -70,3 +70,24 @@ def test_adamw_rejects_cpu_and_bf16():
     q.grad = torch.zeros_like(q)
     with pytest.raises(RuntimeError):
         HipAdamW([q]).step()
+
+
+def test_bf16_shadow_written_by_the_step():
+    """A parameter with a cached bf16 cast (dense.cast_weight) gets that copy rewritten by the
+    AdamW launch (rgbd_adamw_multi_shadow) and re-keyed: the next cast_weight returns the same
+    tensor, bitwise p.to(bfloat16) of the updated parameter, with no cast launch."""
+    from rgbd_amd.dense import cast_weight
+    from rgbd_amd.optim import HipAdamW
+    torch.manual_seed(0)
+    a = torch.nn.Parameter(torch.randn(1000, 37, device="cuda"))
+    b = torch.nn.Parameter(torch.randn(4099, device="cuda"))  # no cast: no shadow
+    opt = HipAdamW([a, b], lr=1e-2)
+    c0 = cast_weight(a, torch.bfloat16)
+    for _ in range(3):
+        a.grad = torch.randn_like(a)
+        b.grad = torch.randn_like(b)
+        opt.step()
+        c = cast_weight(a, torch.bfloat16)
+        assert c is c0
+        assert torch.equal(c, a.detach().to(torch.bfloat16))
+    assert getattr(b, "_rgbd_cast", None) is None

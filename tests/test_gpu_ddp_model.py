@@ -98,7 +98,7 @@ def _worker(rank, world, port, q):
         finally:
             HipMask2FormerLoss.get_num_masks = orig
         nm = sorted({round(float(t), 6) for t in seen})
-        worst, n_grad, bad_none = 0.0, 0, []
+        worst, n_grad, bad_none, per = 0.0, 0, [], []
         for n, p in m.named_parameters():
             exp = [g[n] for g in ref]
             if all(e is None for e in exp):
@@ -110,9 +110,11 @@ def _worker(rank, world, port, q):
                 bad_none.append(n)
                 continue
             n_grad += p.numel()
-            worst = max(worst, float((p.grad - mean).abs().max() / (mean.abs().max() + 1e-30)))
+            e = float((p.grad - mean).abs().max() / (mean.abs().max() + 1e-30))
+            per.append((e, n))
+            worst = max(worst, e)
         q.put((rank, {"worst": worst, "n_grad": n_grad, "bad": bad_none, "num_masks": nm, "calls": len(seen),
-                      "q16": q16}))
+                      "q16": q16, "top": sorted(per, reverse=True)[:12]}))
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent
         import traceback
