@@ -260,12 +260,17 @@ constexpr int SL_ROWS = SL_R + 12, SL_LD = SL_CW + 2 * SL_PADL;
 constexpr int SL_NL = 39, SL_NF = SL_NL * SL_NL;             // (channel, lag) per side; correlations
 constexpr int SL_REC = SL_NF + 3;                            // + the three plane sums
 constexpr size_t SL_SMEM = (size_t)3 * SL_ROWS * SL_LD * 2;
+constexpr int SL_GRP = 3 * SL_ROWS * (SL_LD / 4), SL_GPT = (SL_GRP + 511) / 512;  // 4-pixel groups staged
 static_assert(SL_SMEM >= SL_NF * sizeof(double), "k_stem_lag: LDS reused for the wave reduction");
 constexpr int SF_CH = 64;                                    // k_stem_frame: pixels per chunk
-constexpr int SF_T = 351, SF_REC = SF_T * 13 + 9;            // sums per (image, kind, chunk)
+constexpr int SF_T = 351, SF_REC = SF_T * 13 + 9;            // sums per (kind, image, chunk)
+constexpr int SF_THR = 512;  // >= SF_T + 9 + 27: the sum threads, the plain sums, the plain corner values
+constexpr int SF_AL = SF_CH + 12, SF_N = 3 * 15 * SF_AL, SF_PT = (SF_N + SF_THR - 1) / SF_THR;
+static_assert(SF_THR >= SF_T + 9 + 27, "k_stem_frame thread roles");
+constexpr int SC_REC = SF_T * 39 + 27;                       // corner cells per (row kind, side, image)
 
 struct StemGeom {
-  int nband, ncol, nwg, nfr_row, nfr_col, nfr;  // lag workgroups; frame chunks per row / col kind
+  int nband, ncol, nwg, nfr_row, nfr_col, mx;  // lag workgroups; frame chunks per row / col kind
 };
 inline StemGeom stem_geom(int B, int H, int W) {
   StemGeom g;
@@ -274,16 +279,19 @@ inline StemGeom stem_geom(int B, int H, int W) {
   g.nwg = B * g.nband * g.ncol;
   g.nfr_row = ceil_div(W, SF_CH);
   g.nfr_col = ceil_div(H, SF_CH);
-  g.nfr = B * 2 * (g.nfr_row + g.nfr_col);
+  g.mx = std::max(g.nfr_row, g.nfr_col);
   return g;
 }
 inline bool stem_moments_ok(int H, int W) { return H >= 8 && W >= 8; }
 
-__device__ __forceinline__ float stem_x(const float* __restrict__ depth3, long long bstride, long long HW, int b, int c,
-                                        int H, int W, int y, int x) {
-  const bool ok = y >= 0 && y < H && x >= 0 && x < W;
-  const float v = depth3[b * bstride + c * HW + (long long)(ok ? y : 0) * W + (ok ? x : 0)];
-  return ok ? bf16_to_f32(f32_to_bf16(v)) : 0.f;
+// bf16-rounded depth value (c, y, x) of image b, 0 outside: the load always reads an in-range
+// element (clamped) and the value is selected after it, so loads issued together stay in flight
+__device__ __forceinline__ float stem_ld(const float* __restrict__ depth3, long long bstride, long long HW, int b, int c,
+                                         int H, int W, int y, int x) {
+  return depth3[b * bstride + c * HW + (long long)min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)];
+}
+__device__ __forceinline__ float stem_sel(float v, int H, int W, int y, int x) {
+  return (y >= 0 && y < H && x >= 0 && x < W) ? bf16_to_f32(f32_to_bf16(v)) : 0.f;
 }
 
 __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ depth3, long long bstride, int B, int H,
@@ -296,43 +304,48 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
   const int u0 = (rem / ncol) * SL_R, cv0 = (rem % ncol) * SL_CW;
   const long long HW = (long long)H * W;
   float tsum[3] = {0.f, 0.f, 0.f};
-  // 4 consecutive pixels per thread (16-byte loads, 8-byte LDS stores) where rows are 16-byte
-  // aligned; the groups of 4 then never straddle the image's right edge
+  // every 4-pixel group's loads issued before any is used (16-byte loads where rows are aligned:
+  // the groups then never straddle the image's right edge)
   const bool vec = (W & 3) == 0 && (bstride & 3) == 0 && ((uintptr_t)depth3 & 15) == 0;
-  for (int i = tid; i < 3 * SL_ROWS * (SL_LD / 4); i += 512) {
+  float4 q[SL_GPT];
+#pragma unroll
+  for (int k = 0; k < SL_GPT; ++k) {
+    const int i = min(tid + 512 * k, SL_GRP - 1);
     const int c = i / (SL_ROWS * (SL_LD / 4)), rr = (i / (SL_LD / 4)) % SL_ROWS, cc = 4 * (i % (SL_LD / 4));
     const int yy = u0 - 6 + rr, xx = cv0 - SL_PADL + cc;
-    float v[4];
     if (vec) {
-      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-      const float4 q = *reinterpret_cast<const float4*>(depth3 + b * bstride + c * HW + (long long)(ok ? yy : 0) * W +
-                                                         (ok ? xx : 0));
-      v[0] = ok ? bf16_to_f32(f32_to_bf16(q.x)) : 0.f;
-      v[1] = ok ? bf16_to_f32(f32_to_bf16(q.y)) : 0.f;
-      v[2] = ok ? bf16_to_f32(f32_to_bf16(q.z)) : 0.f;
-      v[3] = ok ? bf16_to_f32(f32_to_bf16(q.w)) : 0.f;
+      q[k] = *reinterpret_cast<const float4*>(depth3 + b * bstride + c * HW + (long long)min(max(yy, 0), H - 1) * W +
+                                              min(max(xx, 0), W - 4));
     } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = stem_x(depth3, bstride, HW, b, c, H, W, yy, xx + e);
+      q[k].x = stem_ld(depth3, bstride, HW, b, c, H, W, yy, xx);
+      q[k].y = stem_ld(depth3, bstride, HW, b, c, H, W, yy, xx + 1);
+      q[k].z = stem_ld(depth3, bstride, HW, b, c, H, W, yy, xx + 2);
+      q[k].w = stem_ld(depth3, bstride, HW, b, c, H, W, yy, xx + 3);
     }
-    *reinterpret_cast<uint2*>(X + (c * SL_ROWS + rr) * SL_LD + cc) =
-        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+#pragma unroll
+  for (int k = 0; k < SL_GPT; ++k) {
+    const int i = tid + 512 * k;
+    if (i >= SL_GRP) break;
+    const int c = i / (SL_ROWS * (SL_LD / 4)), rr = (i / (SL_LD / 4)) % SL_ROWS, cc = 4 * (i % (SL_LD / 4));
+    const int yy = u0 - 6 + rr, xx = cv0 - SL_PADL + cc;
+    const float v0 = stem_sel(q[k].x, H, W, yy, xx), v1 = stem_sel(q[k].y, H, W, yy, xx + 1);
+    const float v2 = stem_sel(q[k].z, H, W, yy, xx + 2), v3 = stem_sel(q[k].w, H, W, yy, xx + 3);
+    *reinterpret_cast<uint2*>(X + (c * SL_ROWS + rr) * SL_LD + cc) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
     // the plane sums over this workgroup's own pixels (rows [u0, u0+R), columns [cv0, cv0+CW))
-    if (rr >= 6 && rr < 6 + SL_R && cc >= SL_PADL && cc < SL_PADL + SL_CW) tsum[c] += (v[0] + v[1]) + (v[2] + v[3]);
+    if (rr >= 6 && rr < 6 + SL_R && cc >= SL_PADL && cc < SL_PADL + SL_CW) tsum[c] += (v0 + v1) + (v2 + v3);
   }
   __syncthreads();
   // per-lane fragment bases: A rows m = (c1, Ly), B columns n = (c2, Lx); m, n >= 39 are zero
   int abase[3], bbase[3];
-  bool aval[3], bval[3];
+  bool aval[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int m = 16 * i + r;
     aval[i] = m < SL_NL;
     const int c1 = aval[i] ? m / 13 : 0, ly = aval[i] ? m % 13 - 6 : 0;
     abase[i] = (c1 * SL_ROWS + 6 - ly) * SL_LD + SL_PADL + 8 * g;     // + ur * SL_LD + (v0 - cv0)
-    bval[i] = m < SL_NL;
-    const int c2 = bval[i] ? m / 13 : 0, lx = bval[i] ? m % 13 - 6 : 0;
-    bbase[i] = (c2 * SL_ROWS + 6) * SL_LD + SL_PADL + 8 * g + lx;     // + ur * SL_LD + (v0 - cv0)
+    bbase[i] = (c1 * SL_ROWS + 6) * SL_LD + SL_PADL + 8 * g + ly;     // (c2, Lx) decode as (c1, ly)
   }
   f32x4 acc[3][3];
 #pragma unroll
@@ -353,7 +366,7 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
       const uint32_t x0 = Xw[w0], x1 = Xw[w0 + 1], x2 = Xw[w0 + 2], x3 = Xw[w0 + 3], x4 = Xw[w0 + 4];
       fb[i].v = make_uint4(__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
                            __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
-      if (!bval[i]) fb[i].zero();
+      if (!aval[i]) fb[i].zero();
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -400,25 +413,45 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
 // (c1, c2, Ly) and anchor row j the 13 row sums over Lx of X_c1(u1, v) X_c2(u1 + Ly, v + Lx)
 // over this chunk's 64 columns; the column kinds likewise with the roles of the axes swapped; plus
 // the plain sums of X_c over the anchor rows / columns.  Workgroup = (chunk, kind, image), kind 0
-// top rows, 1 bottom rows, 2 left columns, 3 right columns.  out [image][kind][chunk][SF_REC] f32.
-__global__ __launch_bounds__(384) void k_stem_frame(const float* __restrict__ depth3, long long bstride, int B, int H,
-                                                    int W, int nfr_row, int nfr_col, float* __restrict__ out) {
-  __shared__ float S[3][15][SF_CH + 12];  // strip: 15 lines across (anchor lines +-6), 64 + 12 along
+// top rows, 1 bottom rows, 2 left columns, 3 right columns: out [kind][image][chunk][SF_REC] f32
+// (a kind's chunks past its own count write zeros).  The row kinds' first / last chunk also write
+// the corner cells of the three left / right columns: cells [row kind][side][image][SC_REC] =
+// the products [t][Lx][column] and the plain values [c][row][column].
+__global__ __launch_bounds__(SF_THR) void k_stem_frame(const float* __restrict__ depth3, long long bstride, int B, int H,
+                                                    int W, int nfr_row, int nfr_col, float* __restrict__ out,
+                                                    float* __restrict__ cells) {
+  __shared__ float S[3][15][SF_AL];  // strip: 15 lines across (anchor lines +-6), 64 + 12 along
   const int kind = blockIdx.y, b = blockIdx.z, chunk = blockIdx.x;
   const bool rows = kind < 2;
-  const int nch = rows ? nfr_row : nfr_col;
-  if (chunk >= nch) return;
+  const int nch = rows ? nfr_row : nfr_col, mx = max(nfr_row, nfr_col);
+  float* o = out + (((long long)kind * B + b) * mx + chunk) * SF_REC;
+  if (chunk >= nch) {
+    for (int i = threadIdx.x; i < SF_REC; i += SF_THR) o[i] = 0.f;
+    return;
+  }
   const long long HW = (long long)H * W;
   const int a0 = chunk * SF_CH;                                      // first anchor along the strip
   const int line0 = kind == 0 ? 0 : (kind == 1 ? H - 3 : (kind == 2 ? 0 : W - 3));  // first anchor line
-  for (int i = threadIdx.x; i < 3 * 15 * (SF_CH + 12); i += 384) {
-    const int c = i / (15 * (SF_CH + 12)), li = (i / (SF_CH + 12)) % 15, al = i % (SF_CH + 12);
+  float pre[SF_PT];
+#pragma unroll
+  for (int k = 0; k < SF_PT; ++k) {
+    const int i = min((int)threadIdx.x + SF_THR * k, SF_N - 1);
+    const int c = i / (15 * SF_AL), li = (i / SF_AL) % 15, al = i % SF_AL;
     const int ln = line0 - 6 + li, at = a0 - 6 + al;                // across, along
-    S[c][li][al] = rows ? stem_x(depth3, bstride, HW, b, c, H, W, ln, at) : stem_x(depth3, bstride, HW, b, c, H, W, at, ln);
+    pre[k] = rows ? stem_ld(depth3, bstride, HW, b, c, H, W, ln, at) : stem_ld(depth3, bstride, HW, b, c, H, W, at, ln);
+  }
+#pragma unroll
+  for (int k = 0; k < SF_PT; ++k) {
+    const int i = threadIdx.x + SF_THR * k;
+    if (i < SF_N) {
+      const int c = i / (15 * SF_AL), li = (i / SF_AL) % 15, al = i % SF_AL;
+      const int ln = line0 - 6 + li, at = a0 - 6 + al;
+      S[c][li][al] = rows ? stem_sel(pre[k], H, W, ln, at) : stem_sel(pre[k], H, W, at, ln);
+    }
   }
   __syncthreads();
-  const int nal = min(SF_CH, (rows ? W : H) - a0);
-  float* o = out + ((long long)(b * 4 + kind) * max(nfr_row, nfr_col) + chunk) * SF_REC;
+  const int along_n = rows ? W : H;
+  const int nal = min(SF_CH, along_n - a0);
   const int t = threadIdx.x;
   if (t < SF_T) {  // t = ((c1 * 3 + c2) * 13 + s1) * 3 + j: s1 the across lag, 13 along lags
     const int j = t % 3, s1 = (t / 3) % 13, c2 = (t / 39) % 3, c1 = t / 117;
@@ -427,51 +460,87 @@ __global__ __launch_bounds__(384) void k_stem_frame(const float* __restrict__ de
     for (int q = 0; q < 13; ++q) acc[q] = 0.f;
     float win[13];
 #pragma unroll
-    for (int q = 0; q < 13; ++q) win[q] = S[c2][6 + j + s1 - 6][q];  // along positions a - 6 .. a + 6 of a = 0
+    for (int q = 0; q < 13; ++q) win[q] = S[c2][j + s1][q];  // along positions a - 6 .. a + 6 of a = 0
     for (int a = 0; a < nal; ++a) {
       const float x1 = S[c1][6 + j][6 + a];
 #pragma unroll
       for (int q = 0; q < 13; ++q) acc[q] = __builtin_fmaf(x1, win[q], acc[q]);
 #pragma unroll
       for (int q = 0; q < 12; ++q) win[q] = win[q + 1];
-      win[12] = S[c2][j + s1][a + 13 < SF_CH + 12 ? a + 13 : SF_CH + 11];
+      win[12] = S[c2][j + s1][min(a + 13, SF_AL - 1)];
     }
 #pragma unroll
     for (int q = 0; q < 13; ++q) o[t * 13 + q] = acc[q];
+    if (rows) {  // corner cells: the three left (first chunk) / right (last chunk) anchor columns
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
+        if (!mine) continue;
+        float* cl = cells + (((long long)kind * 2 + side) * B + b) * SC_REC;
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) {
+          const int a = side == 0 ? ci : W - 3 + ci - a0;
+          const float x1 = S[c1][6 + j][6 + a];
+#pragma unroll
+          for (int q = 0; q < 13; ++q) cl[(t * 13 + q) * 3 + ci] = x1 * S[c2][j + s1][a + q];
+        }
+      }
+    }
   } else if (t < SF_T + 9) {  // plain sums of X_c over anchor line j
     const int c = (t - SF_T) / 3, j = (t - SF_T) % 3;
     float s = 0.f;
     for (int a = 0; a < nal; ++a) s += S[c][6 + j][6 + a];
     o[SF_T * 13 + c * 3 + j] = s;
+  } else if (rows && t < SF_T + 9 + 27) {  // plain corner values [c][row][column]
+    const int e = t - SF_T - 9, c = e / 9, j = (e / 3) % 3, ci = e % 3;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
+      if (!mine) continue;
+      const int a = side == 0 ? ci : W - 3 + ci - a0;
+      cells[(((long long)kind * 2 + side) * B + b) * SC_REC + SF_T * 39 + e] = S[c][6 + j][6 + a];
+    }
   }
 }
 
-// Reduce the lag partials over workgroups (fixed order) and the frame chunks per (image, kind):
-// F [SL_REC] double, fr [image][kind][SF_REC] double.
-__global__ __launch_bounds__(256) void k_stem_reduce(const double* __restrict__ part, int nwg,
-                                                     const float* __restrict__ fchunks, int B, int nfr_row,
-                                                     int nfr_col, double* __restrict__ F, double* __restrict__ fr) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < SL_REC) {
-    double s = 0.0;
-    for (int w = 0; w < nwg; ++w) s += part[(long long)w * SL_REC + i];
-    F[i] = s;
-    return;
+// dst[s][e] = sum_k src[s * seg_stride + k * stride + e] (k < n, fixed order: 16 groups of every
+// 16th k, then the groups in order): workgroup = 16 consecutive elements x 16 groups.
+template <typename T>
+__global__ __launch_bounds__(256) void k_stem_sum(const T* __restrict__ src, int n, long long stride,
+                                                  long long seg_stride, int seg_len, double* __restrict__ dst) {
+  __shared__ double red[16][17];
+  const int s = blockIdx.y, el = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int e = blockIdx.x * 16 + el;
+  double acc = 0.0;
+  if (e < seg_len) {
+    const T* p = src + s * seg_stride + e;
+    int k = grp;
+    for (; k + 48 < n; k += 64) {
+      const double a0 = (double)p[k * stride], a1 = (double)p[(k + 16) * stride];
+      const double a2 = (double)p[(k + 32) * stride], a3 = (double)p[(k + 48) * stride];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; k < n; k += 16) acc += (double)p[k * stride];
   }
-  const int j = i - SL_REC;
-  if (j >= B * 4 * SF_REC) return;
-  const int e = j % SF_REC, bk = j / SF_REC, kind = bk % 4;
-  const int nch = kind < 2 ? nfr_row : nfr_col, mx = max(nfr_row, nfr_col);
-  double s = 0.0;
-  for (int c = 0; c < nch; ++c) s += (double)fchunks[((long long)bk * mx + c) * SF_REC + e];
-  fr[j] = s;
+  red[grp][el] = acc;
+  __syncthreads();
+  if (grp == 0 && e < seg_len) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][el];
+    dst[(long long)s * seg_len + e] = t;
+  }
 }
 
 // S2 [147][147] and S1 [147] (k = c * 49 + ay * 7 + ax, the window offset a = (ay, ax) of
-// channel c) over the batch, double: thread per (k, l), the extra 147 threads S1.
+// channel c) over the batch, double: thread per (k, l), the extra 147 threads S1.  fr [kind][SF_REC]
+// and ce [row kind][side][SC_REC] are already summed over the images.
 __global__ __launch_bounds__(256) void k_stem_s2(const double* __restrict__ F, const double* __restrict__ fr,
-                                                 const float* __restrict__ depth3, long long bstride, int B, int H,
-                                                 int W, double* __restrict__ S2, double* __restrict__ S1) {
+                                                 const double* __restrict__ ce, double* __restrict__ S2,
+                                                 double* __restrict__ S1) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= 147 * 147 + 147) return;
   const bool is_s1 = i >= 147 * 147;
@@ -482,25 +551,16 @@ __global__ __launch_bounds__(256) void k_stem_s2(const double* __restrict__ F, c
   // excluded anchor rows / columns of offset a: top j < ay - 3, or bottom j >= ay (j = 0..2)
   const int rkind = ay > 3 ? 0 : 1, rlo = ay > 3 ? 0 : ay, rhi = ay > 3 ? ay - 3 : (ay < 3 ? 3 : 0);
   const int ckind = ax > 3 ? 2 : 3, clo = ax > 3 ? 0 : ax, chi = ax > 3 ? ax - 3 : (ax < 3 ? 3 : 0);
-  const long long HW = (long long)H * W;
-  double s = is_s1 ? 0.0 : F[((c1 * 13 + ly + 6) * SL_NL) + c2 * 13 + lx + 6];
-  if (is_s1) s = F[SL_NF + c1];
-  for (int b = 0; b < B; ++b) {
-    const double* rk = fr + ((long long)b * 4 + rkind) * SF_REC;
-    const double* ck = fr + ((long long)b * 4 + ckind) * SF_REC;
-    for (int j = rlo; j < rhi; ++j)
-      s -= is_s1 ? rk[SF_T * 13 + c1 * 3 + j] : rk[(((c1 * 3 + c2) * 13 + ly + 6) * 3 + j) * 13 + lx + 6];
-    for (int j = clo; j < chi; ++j)
-      s -= is_s1 ? ck[SF_T * 13 + c1 * 3 + j] : ck[(((c1 * 3 + c2) * 13 + lx + 6) * 3 + j) * 13 + ly + 6];
-    for (int jr = rlo; jr < rhi; ++jr) {  // corners: excluded in both, subtracted twice
-      const int u1 = rkind == 0 ? jr : H - 3 + jr;
-      for (int jc = clo; jc < chi; ++jc) {
-        const int v1 = ckind == 2 ? jc : W - 3 + jc;
-        const float x1 = stem_x(depth3, bstride, HW, b, c1, H, W, u1, v1);
-        s += is_s1 ? (double)x1 : (double)x1 * stem_x(depth3, bstride, HW, b, c2, H, W, u1 + ly, v1 + lx);
-      }
-    }
-  }
+  const double* rk = fr + (long long)rkind * SF_REC;
+  const double* ck = fr + (long long)ckind * SF_REC;
+  const double* cc = ce + ((long long)rkind * 2 + (ckind - 2)) * SC_REC;
+  const int trow = ((c1 * 3 + c2) * 13 + ly + 6) * 3, tcol = ((c1 * 3 + c2) * 13 + lx + 6) * 3;
+  double s = is_s1 ? F[SL_NF + c1] : F[(c1 * 13 + ly + 6) * SL_NL + c2 * 13 + lx + 6];
+  for (int j = rlo; j < rhi; ++j) s -= is_s1 ? rk[SF_T * 13 + c1 * 3 + j] : rk[(trow + j) * 13 + lx + 6];
+  for (int j = clo; j < chi; ++j) s -= is_s1 ? ck[SF_T * 13 + c1 * 3 + j] : ck[(tcol + j) * 13 + ly + 6];
+  for (int jr = rlo; jr < rhi; ++jr)  // corners: excluded in both, subtracted twice
+    for (int jc = clo; jc < chi; ++jc)
+      s += is_s1 ? cc[SF_T * 39 + (c1 * 3 + jr) * 3 + jc] : cc[((trow + jr) * 13 + lx + 6) * 3 + jc];
   if (is_s1)
     S1[k] = s;
   else
@@ -521,6 +581,7 @@ __global__ __launch_bounds__(256) void k_stem_bn(const double* __restrict__ S2, 
   double a = 0.0, q = 0.0;
   if (t < 147) {
     a = w[t] * S1[t];
+#pragma unroll 7
     for (int l = 0; l < 147; ++l) q += w[l] * S2[l * 147 + t];  // S2 symmetric: coalesced rows
     q *= w[t];
   }
@@ -544,7 +605,7 @@ __global__ __launch_bounds__(256) void k_stem_bn(const double* __restrict__ S2, 
 }
 
 struct StemWs {
-  size_t part, fchunks, F, fr, S2, S1, total;
+  size_t part, fchunks, cells, F, fr, ce, S2, S1, total;
 };
 inline StemWs stem_ws(int B, int H, int W) {
   const StemGeom g = stem_geom(B, H, W);
@@ -556,9 +617,11 @@ inline StemWs stem_ws(int B, int H, int W) {
     return r;
   };
   s.part = seg((size_t)g.nwg * SL_REC * sizeof(double));
-  s.fchunks = seg((size_t)B * 4 * std::max(g.nfr_row, g.nfr_col) * SF_REC * sizeof(float));
+  s.fchunks = seg((size_t)4 * B * g.mx * SF_REC * sizeof(float));
+  s.cells = seg((size_t)4 * B * SC_REC * sizeof(float));
   s.F = seg(SL_REC * sizeof(double));
-  s.fr = seg((size_t)B * 4 * SF_REC * sizeof(double));
+  s.fr = seg((size_t)4 * SF_REC * sizeof(double));
+  s.ce = seg((size_t)4 * SC_REC * sizeof(double));
   s.S2 = seg(147 * 147 * sizeof(double));
   s.S1 = seg(147 * sizeof(double));
   s.total = o;
@@ -572,19 +635,22 @@ int stem_bn_moments(const float* depth3, long long bstride, int B, int H, int W,
   const StemWs w = stem_ws(B, H, W);
   double* part = (double*)(ws + w.part);
   float* fch = (float*)(ws + w.fchunks);
+  float* cells = (float*)(ws + w.cells);
   double* F = (double*)(ws + w.F);
   double* fr = (double*)(ws + w.fr);
+  double* ce = (double*)(ws + w.ce);
   double* S2 = (double*)(ws + w.S2);
   double* S1 = (double*)(ws + w.S1);
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)k_stem_lag, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL_SMEM);
   if (attr != hipSuccess) return (int)attr;
   k_stem_lag<<<g.nwg, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part);
-  k_stem_frame<<<dim3(std::max(g.nfr_row, g.nfr_col), 4, B), 384, 0, s>>>(depth3, bstride, B, H, W, g.nfr_row,
-                                                                           g.nfr_col, fch);
-  k_stem_reduce<<<ceil_div(SL_REC + (long long)B * 4 * SF_REC, 256), 256, 0, s>>>(part, g.nwg, fch, B, g.nfr_row,
-                                                                                  g.nfr_col, F, fr);
-  k_stem_s2<<<ceil_div(147 * 147 + 147, 256), 256, 0, s>>>(F, fr, depth3, bstride, B, H, W, S2, S1);
+  k_stem_frame<<<dim3(g.mx, 4, B), SF_THR, 0, s>>>(depth3, bstride, B, H, W, g.nfr_row, g.nfr_col, fch, cells);
+  k_stem_sum<double><<<dim3(ceil_div(SL_REC, 16), 1), 256, 0, s>>>(part, g.nwg, SL_REC, 0, SL_REC, F);
+  k_stem_sum<float><<<dim3(ceil_div(SF_REC, 16), 4), 256, 0, s>>>(fch, B * g.mx, SF_REC, (long long)B * g.mx * SF_REC,
+                                                                  SF_REC, fr);
+  k_stem_sum<float><<<dim3(ceil_div(SC_REC, 16), 4), 256, 0, s>>>(cells, B, SC_REC, (long long)B * SC_REC, SC_REC, ce);
+  k_stem_s2<<<ceil_div(147 * 147 + 147, 256), 256, 0, s>>>(F, fr, ce, S2, S1);
   k_stem_bn<<<STEM_C, 256, 0, s>>>(S2, S1, blob, L, (double)B * H * W, momentum, bn, aff1);
   return RGBD_OK;
 }
@@ -883,6 +949,14 @@ template <int PH> constexpr size_t c2w_off_patch() {  // bf16 [3][14][40]
 }
 template <int PH> constexpr size_t c2w_smem() { return c2w_off_patch<PH>() + (size_t)3 * C2W_PH * C2W_PWP * 2 + 16; }
 static_assert(c2w_smem<1>() <= 163840, "chain v2 LDS budget");
+// Phase 1 (train: stem + fusion + fusion statistics) needs neither W3 nor W4: their space holds
+// eight copies of the depth patch shifted by 0..7 columns, [shift k][3][14][40] with element j of
+// copy k = patch column j + k, so the 8 patch values a lane feeds the stem (columns col .. col+7)
+// are ONE 16-byte-aligned ds_read_b128 from copy col % 8 (the other phases: 5 dword reads and 4
+// byte-aligns per fragment)
+constexpr size_t C2W_OFF_P8 = C2W_OFF_W3;
+constexpr int C2W_P8 = 8 * 3 * C2W_PH * C2W_PWP;  // bf16 elements
+static_assert(C2W_OFF_P8 + (size_t)C2W_P8 * 2 <= c2w_off_b<1>(), "phase-1 shifted patches fit W3 + W4");
 static_assert(2 * c2w_smem<0>() <= 163840, "chain v2 phase 0: two workgroups per CU");
 
 // Diagnostics (rgbd_debug_chain_stamps): the STAMPS instantiation records, for workgroup 0's tiles
@@ -952,6 +1026,8 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
         copy_rows_p(C2W_OFF_W2, fold + FOLD_W2, FUS_C, STEM_C, C2W_S2);
       else
         copy_rows(C2W_OFF_W2, L.w2, FUS_C, STEM_C, C2W_S2);
+    }
+    if (PHASE == 2) {  // phase 1 keeps its shifted patch copies there
       copy_rows(C2W_OFF_W3, L.w3, ATT_C, FUS_C, C2W_S3);
       copy_rows(C2W_OFF_W4, L.w4, FUS_C, ATT_C, C2W_S4);
     }
@@ -1037,6 +1113,21 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
       if (i < PATCH_N) patch[(i / C2W_PW) * C2W_PWP + i % C2W_PW] = f32_to_bf16(pre[k]);
     }
     lds_barrier();
+    if constexpr (PHASE == 1) {  // the eight shifted copies, 16 bytes at a time
+      // a lane reads copy (col & 7) at elements (col & ~7) .. +7 <= 31: chunks 0..3 of each row
+      bf16_t* p8 = (bf16_t*)(smem + C2W_OFF_P8);
+      for (int i = tid; i < 8 * 3 * C2W_PH * 4; i += 512) {
+        const int j8 = i & 3, row = (i >> 2) % (3 * C2W_PH), k = i / (3 * C2W_PH * 4);
+        const int e = 8 * j8 + k;  // first patch column of this chunk (<= 31: five words in the row)
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(patch + row * C2W_PWP + (e & ~1));
+        const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3], w4 = wp[4];
+        const uint32_t sh = (e & 1) * 2;
+        *reinterpret_cast<uint4*>(p8 + (k * 3 * C2W_PH + row) * C2W_PWP + 8 * j8) =
+            make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+      }
+      lds_barrier();
+    }
     if (STAMPS && sts) c2_stamp(sts, sidx + 1);
     fetch_patch(tile + gridDim.x);
     if (STAMPS && sts) c2_stamp(sts, sidx + 2);
@@ -1051,6 +1142,19 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
     // col & ~1 and a byte-align by 2*(col & 1).
     auto stem_b = [&](int s, Frag<bf16_t> (&bf)[2]) {
       const int q = 4 * s + g;
+      if constexpr (PHASE == 1) {  // copy (col & 7) = (r & 7) for both halves u, 16 columns apart
+        const int qc = q < 21 ? q : 20;
+        const int cq = qc / 7, dy = qc - 7 * cq;
+        const bf16_t* p8 = (const bf16_t*)(smem + C2W_OFF_P8) + (((r & 7) * 3 + cq) * C2W_PH + wave + dy) * C2W_PWP +
+                           (r & 8);
+        bf[0].v = *reinterpret_cast<const uint4*>(p8);
+        bf[1].v = *reinterpret_cast<const uint4*>(p8 + 16);
+        if (q >= 21) {
+          bf[0].zero();
+          bf[1].zero();
+        }
+        return;
+      }
       const int cq = q / 7, dy = q - 7 * cq;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -1105,16 +1209,37 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
       const float4 bb = *reinterpret_cast<const float4*>(sb1 + 16 * t + 4 * g);
       a1[t][0] = a1[t][1] = f32x4{bb.x, bb.y, bb.z, bb.w};
     }
+    if constexpr (PHASE == 1) {
+      // one K step of patch fragments in flight ahead of the MFMAs that use the current one
+      // (the scheduling fences keep the compiler from hoisting more steps: register budget)
+      Frag<bf16_t> bcur[2], bnxt[2];
+      stem_b(0, bcur);
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      Frag<bf16_t> bfr[2];
-      stem_b(s, bfr);
+      for (int s = 0; s < 6; ++s) {
+        if (s < 5) stem_b(s + 1, bnxt);
 #pragma unroll
-      for (int t = 0; t < 12; ++t) {
-        if (!stem_live(t, s)) continue;
-        const Frag<bf16_t> af = stem_w(t, s);
-        mma(a1[t][0], af, bfr[0]);
-        mma(a1[t][1], af, bfr[1]);
+        for (int t = 0; t < 12; ++t) {
+          if (!stem_live(t, s)) continue;
+          const Frag<bf16_t> af = stem_w(t, s);
+          mma(a1[t][0], af, bcur[0]);
+          mma(a1[t][1], af, bcur[1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bcur[0] = bnxt[0];
+        bcur[1] = bnxt[1];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        Frag<bf16_t> bfr[2];
+        stem_b(s, bfr);
+#pragma unroll
+        for (int t = 0; t < 12; ++t) {
+          if (!stem_live(t, s)) continue;
+          const Frag<bf16_t> af = stem_w(t, s);
+          mma(a1[t][0], af, bfr[0]);
+          mma(a1[t][1], af, bfr[1]);
+        }
       }
     }
     if (STAMPS && sts) c2_stamp(sts, sidx + 3);
@@ -1568,10 +1693,10 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y
 // weights of one step (32 KB) double-buffered.  Rows are 128 B, 16-byte chunk q stored at slot
 // q ^ (row & 6): conflict-free ds_read_b128 for 16 consecutive rows from any start row (the
 // patch rows of tap kx), pre-applied in the weight blob and on the per-lane DMA source address.
-// Pipeline (one barrier per step): in step s waves 0-3 issue the DMA of B(s+1) (or the next
-// tile's B(0)) and their piece of A (this tile's half 1 during steps 0-5, the next tile's half 0
-// during 9-14), then run their 64 MFMAs; waves 4-7 run their MFMAs first and issue their A piece
-// after them; every wave waits for its own DMA except the A piece just issued, barrier.
+// Pipeline (one barrier per step): in step s every wave issues its 4 pieces of B(s+1) (or the
+// next tile's B(0)) and one piece of A (this tile's half 1 during steps 0-5, the next tile's
+// half 0 during 9-14) — waves 0-3 before their 64 MFMAs, waves 4-7 after theirs — waits for its
+// own DMA except the A piece just issued, barrier.
 // Epilogue straight from the accumulators: y is written in a fragment-native layout
 // [tile][wave][mi][nj/2][lane][2 ch x 4 px] (1 KiB contiguous per non-temporal store instruction; read back by
 // k_rp_bn_relu_pool_frag) and the BN statistics of the float32 conv outputs (as the fp32
@@ -1651,15 +1776,16 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       src = (const char*)(x + (((long long)t.b * H + yy) * W + xx) * FUS_C + 64 * h + 8 * (q ^ (p & 6)));
     glds16(src, lds0 + h * (C3_APIX * 128) + j * 1024);
   };
-  // B pieces of step st: 32 x 1 KiB, copied by the loader waves 0-3 only (wave w: pieces
-  // 8w..8w+7): waves 4-7 open every step with their MFMAs while 0-3 issue the DMA, so the
-  // SIMD's matrix pipe is never idle behind both partners' DMA issue at once
+  // B pieces of step st: 32 x 1 KiB, wave w copies pieces 4w..4w+3.  Waves 0-3 issue theirs (and
+  // their A piece) at the top of a step, before their MFMAs; waves 4-7 open the step with their
+  // MFMAs and issue after them, so the two waves of a SIMD never stall the matrix pipe on DMA
+  // issue at the same time (their B pieces still land before the closing barrier)
   const bool loader = wave < 4;
   auto issue_b = [&](int st) {
-    const char* src = w5s + (size_t)st * (C5 * 128) + wave * 8192 + 16 * lane;
-    const uint32_t dst = lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 8192;
+    const char* src = w5s + (size_t)st * (C5 * 128) + wave * 4096 + 16 * lane;
+    const uint32_t dst = lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 4096;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) glds16(src + 1024 * k, dst + 1024 * k);
+    for (int k = 0; k < 4; ++k) glds16(src + 1024 * k, dst + 1024 * k);
   };
 
   // BN statistics per channel as (even, odd) pixel pairs: packed adds / FMAs, one instruction
@@ -1675,7 +1801,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
     const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
     for (int j = wave; j < C3_APIECES; j += 8) issue_a(t, 0, j);
-    if (loader) issue_b(0);
+    issue_b(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1733,7 +1859,8 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
         if (STAMPS && sts) c3_stamp(sts, sidx + 2 + ks);
       }
-      if (!loader) {  // the A piece lands under the barrier / next step (needed >= 3 steps later)
+      if (!loader) {  // B(st + 1) lands before the barrier; the A piece (needed >= 3 steps later) may not
+        if (b_next) issue_b(b_st);
         if (a_kind == 1) issue_a(t, 1, a_j);
         if (a_kind == 2) issue_a(tn, 0, a_j);
       }
