@@ -1693,10 +1693,10 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y
 // weights of one step (32 KB) double-buffered.  Rows are 128 B, 16-byte chunk q stored at slot
 // q ^ (row & 6): conflict-free ds_read_b128 for 16 consecutive rows from any start row (the
 // patch rows of tap kx), pre-applied in the weight blob and on the per-lane DMA source address.
-// Pipeline (one barrier per step): in step s every wave issues its 4 pieces of B(s+1) (or the
-// next tile's B(0)) and one piece of A (this tile's half 1 during steps 0-5, the next tile's
-// half 0 during 9-14) — waves 0-3 before their 64 MFMAs, waves 4-7 after theirs — waits for its
-// own DMA except the A piece just issued, barrier.
+// Pipeline (one barrier per step): in step s waves 0-3 issue the DMA of B(s+1) (or the next
+// tile's B(0)) and their piece of A (this tile's half 1 during steps 0-5, the next tile's half 0
+// during 9-14), then run their 64 MFMAs; waves 4-7 run their MFMAs first and issue their A piece
+// after them; every wave waits for its own DMA except the A piece just issued, barrier.
 // Epilogue straight from the accumulators: y is written in a fragment-native layout
 // [tile][wave][mi][nj/2][lane][2 ch x 4 px] (1 KiB contiguous per non-temporal store instruction; read back by
 // k_rp_bn_relu_pool_frag) and the BN statistics of the float32 conv outputs (as the fp32
@@ -1776,16 +1776,17 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       src = (const char*)(x + (((long long)t.b * H + yy) * W + xx) * FUS_C + 64 * h + 8 * (q ^ (p & 6)));
     glds16(src, lds0 + h * (C3_APIX * 128) + j * 1024);
   };
-  // B pieces of step st: 32 x 1 KiB, wave w copies pieces 4w..4w+3.  Waves 0-3 issue theirs (and
-  // their A piece) at the top of a step, before their MFMAs; waves 4-7 open the step with their
-  // MFMAs and issue after them, so the two waves of a SIMD never stall the matrix pipe on DMA
-  // issue at the same time (their B pieces still land before the closing barrier)
+  // B pieces of step st: 32 x 1 KiB, copied by the loader waves 0-3 only (wave w: pieces
+  // 8w..8w+7): waves 4-7 open every step with their MFMAs while 0-3 issue the DMA, so the
+  // SIMD's matrix pipe is never idle behind both partners' DMA issue at once.  (Measured, round 5:
+  // 1.7 % faster than every wave issuing 4 pieces at the step top; waves 4-7 issuing theirs
+  // after their MFMAs instead was 0.7 % slower than that — r05 ab_e.txt, conv5_stamps_e.txt.)
   const bool loader = wave < 4;
   auto issue_b = [&](int st) {
-    const char* src = w5s + (size_t)st * (C5 * 128) + wave * 4096 + 16 * lane;
-    const uint32_t dst = lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 4096;
+    const char* src = w5s + (size_t)st * (C5 * 128) + wave * 8192 + 16 * lane;
+    const uint32_t dst = lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 8192;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) glds16(src + 1024 * k, dst + 1024 * k);
+    for (int k = 0; k < 8; ++k) glds16(src + 1024 * k, dst + 1024 * k);
   };
 
   // BN statistics per channel as (even, odd) pixel pairs: packed adds / FMAs, one instruction
@@ -1801,7 +1802,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
     const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
     for (int j = wave; j < C3_APIECES; j += 8) issue_a(t, 0, j);
-    issue_b(0);
+    if (loader) issue_b(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1859,8 +1860,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
         if (STAMPS && sts) c3_stamp(sts, sidx + 2 + ks);
       }
-      if (!loader) {  // B(st + 1) lands before the barrier; the A piece (needed >= 3 steps later) may not
-        if (b_next) issue_b(b_st);
+      if (!loader) {  // the A piece lands under the barrier / next step (needed >= 3 steps later)
         if (a_kind == 1) issue_a(t, 1, a_j);
         if (a_kind == 2) issue_a(tn, 0, a_j);
       }
