@@ -7,7 +7,10 @@ attention, the point-sampled loss) runs under ``torch.nn.parallel.DistributedDat
 two 320x240 shards — gloo with both ranks on the test box's one GPU — and
 
 * every parameter that receives a gradient holds the mean of the two shards' standalone
-  gradients (1e-5 of its max), every other parameter none;
+  gradients — within 4x the run-to-run noise of one shard's standalone gradients (the float
+  atomics of the point-sampling and deformable-attention backward scatters sum in a varying
+  order), relative to the parameter's gradient scale floored at 1e-6 of the model's largest
+  gradient — every other parameter none;
 * the loss normalises by Q16's double-divided instance count: accelerate's ``reduce`` (a MEAN
   over ranks) inside HF ``get_num_masks`` (modeling_mask2former.py:781-794) and then ``/
   world_size`` again — ``HipMask2FormerLoss.get_num_masks`` defers to it whenever accelerate's
@@ -82,6 +85,15 @@ def _worker(rank, world, port, q):
                 out.loss.backward()
                 ref.append({n: (None if p.grad is None else p.grad.detach().clone()) for n, p in m.named_parameters()})
                 del m, out
+            # this rank's shard once more: the run-to-run noise of the float atomics (point-sampling
+            # and deformable-attention backward scatters) is the floor the DDP comparison is held to
+            m = model()
+            torch.manual_seed(1234 + rank)
+            out = m(pixel_values=pv[rank:rank + 1], mask_labels=mask_labels[rank:rank + 1],
+                    class_labels=class_labels[rank:rank + 1])
+            out.loss.backward()
+            again = {n: (None if p.grad is None else p.grad.detach().clone()) for n, p in m.named_parameters()}
+            del m, out
         finally:
             HipMask2FormerLoss.get_num_masks = orig
         # the Trainer's DDP step on this rank's shard, accelerate's count (the library's branch)
@@ -102,6 +114,11 @@ def _worker(rank, world, port, q):
         # of the model: some are exactly zero in exact arithmetic and only rounding noise here
         # (the self-attention key biases: softmax is invariant to a per-query constant)
         gscale = max(float(e.abs().max()) for g in ref for e in g.values() if e is not None)
+        noise = 0.0
+        for n, g in again.items():
+            if g is not None:
+                e = ref[rank][n]
+                noise = max(noise, float((g - e).abs().max() / max(float(e.abs().max()), 1e-6 * gscale)))
         worst, n_grad, bad_none, per = 0.0, 0, [], []
         for n, p in m.named_parameters():
             exp = [g[n] for g in ref]
@@ -118,7 +135,7 @@ def _worker(rank, world, port, q):
             per.append((e, n))
             worst = max(worst, e)
         q.put((rank, {"worst": worst, "n_grad": n_grad, "bad": bad_none, "num_masks": nm, "calls": len(seen),
-                      "q16": q16, "top": sorted(per, reverse=True)[:12]}))
+                      "q16": q16, "top": sorted(per, reverse=True)[:12], "noise": noise}))
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent
         import traceback
@@ -145,7 +162,9 @@ def test_whole_model_ddp_equals_shard_mean_world2():
         for e, n in got["top"]:
             print(f"    {e:.3g}  {n}")
         assert not got["bad"], got["bad"][:10]
-        assert got["worst"] < 1e-5, got
+        print(f"    run-to-run noise of one shard (same inputs, same seed): {got['noise']:.3g}")
+        # the DDP mean within 4x the run-to-run noise of the float-atomic backward scatters
+        assert got["worst"] <= 4 * got["noise"] + 1e-6, got
         # SURVEY §8(a) a12 counts 37 330 321 grad-receiving parameters for a training batch; at
         # one image per shard in eval mode 8 224 of them (one 256 -> 32 projection) get none in
         # either arm (the `bad` check above: the same set in both)
