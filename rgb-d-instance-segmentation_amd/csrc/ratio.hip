@@ -1963,217 +1963,6 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
     slab[(long long)blockIdx.x * C5 * 2 + i] = red[i] + red[C5 * 2 + i] + red[2 * C5 * 2 + i] + red[3 * C5 * 2 + i];
 }
 
-// ---- conv5 v5 (bf16): the v3 tile (8x32 px x 256 ch, same LDS image, same DMA pieces, same
-// fragment-native y and statistics) on FOUR waves, one per SIMD: wave w owns pixel rows 2w, 2w+1
-// (64 px) x all 256 channels = 4 x 16 MFMA tiles, 256 accumulators (AGPRs).  With no partner on
-// its SIMD a wave keeps the matrix pipe fed itself: the MFMAs of a k-step run B-fragment-major
-// (each B fragment feeds four MFMAs and is read three fragments ahead), the next k-step's A
-// fragments are read under the current one's MFMAs, and the step's DMA pieces (8 of B, up to 2 of
-// A per wave) are issued between MFMA groups.  One barrier per K=64 step over 4 waves.
-constexpr int C5V_ANEXT = 2;  // A pieces per wave per loading step (43 per half over 6 steps x 4 waves)
-constexpr size_t C5V_STAT_OFF = C3_SMEM, C5V_SMEM = C5V_STAT_OFF + 4 * C5 * 2 * 4;
-static_assert(C5V_SMEM <= 163840, "conv5 v5 LDS budget");
-
-__global__ __launch_bounds__(256, 1) void k_rp_conv3x3_v5(const bf16_t* __restrict__ x, int B, int H, int W,
-                                                          const char* __restrict__ blob, Layout L,
-                                                          bf16_t* __restrict__ y, float* __restrict__ slab) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int wm = wave;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  const char* w5s = blob + L.w5s;
-  const char* zero16 = blob + L.zero;
-  float* sbias = (float*)(smem + C3_BIAS_OFF);
-  for (int i = tid; i < C5; i += 256) sbias[i] = ((const float*)(blob + L.b5))[i];
-  const int tiles_x = (W + C3_TW - 1) / C3_TW, tiles_y = (H + C3_TH - 1) / C3_TH;
-  const long long ntiles = (long long)B * tiles_x * tiles_y;
-
-  auto issue_a = [&](const C3Tile& t, int h, int j) {  // A piece j of channel half h (as v3)
-    const int p = 8 * j + (lane >> 3), q = lane & 7;
-    const int hy = p / C3_PW, hx = p % C3_PW;
-    const int yy = t.y0 + hy - 1, xx = t.x0 + hx - 1;
-    const char* src = zero16;
-    if (p < C3_NPIX && yy >= 0 && yy < H && xx >= 0 && xx < W)
-      src = (const char*)(x + (((long long)t.b * H + yy) * W + xx) * FUS_C + 64 * h + 8 * (q ^ (p & 6)));
-    glds16(src, lds0 + h * (C3_APIX * 128) + j * 1024);
-  };
-  // B piece k (of this wave's 8) of step st
-  auto issue_b1 = [&](int st, int k) {
-    glds16(w5s + (size_t)st * (C5 * 128) + wave * 8192 + 1024 * k + 16 * lane,
-           lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 8192 + 1024 * k);
-  };
-
-  // BN statistics: per tile reduced over the lane groups, then added in tile order into this
-  // wave's LDS rows [wm][n][2] (no registers held across tiles: all 256 AGPRs hold accumulators)
-  float* sst = (float*)(smem + C5V_STAT_OFF);
-  for (int i = tid; i < 4 * C5 * 2; i += 256) sst[i] = 0.f;
-
-  long long tile = blockIdx.x;
-  if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
-    const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
-    for (int j = wave; j < C3_APIECES; j += 4) issue_a(t, 0, j);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) issue_b1(0, k);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (; tile < ntiles; tile += gridDim.x) {
-    const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
-    const long long ntile = tile + gridDim.x;
-    const bool has_next = ntile < ntiles;
-    const C3Tile tn = c3_tile(has_next ? ntile : tile, tiles_x, tiles_y);
-    f32x4 acc[4][16];
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int nj = 0; nj < 16; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll 1
-    for (int st = 0; st < C3_STEPS; ++st) {
-      const bool b_next = st + 1 < C3_STEPS || has_next;
-      const int b_st = st + 1 < C3_STEPS ? st + 1 : 0;
-      // A pieces of this step: this tile's half 1 during steps 0-5, the next tile's half 0 during 9-14
-      const int sa_st = st < 6 ? st : st - 9;
-      const bool a_load = (st < 6) || (st >= 9 && st < 15 && has_next);
-      const int h = st >= 9, tap = st - 9 * h, ky = tap / 3, kx = tap % 3;
-      const char* sa = smem + h * (C3_APIX * 128);
-      const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
-      int a_issued = 0;
-      Frag<bf16_t> fa[4], fan[4];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int p = (2 * wm + (mi >> 1) + ky) * C3_PW + (mi & 1) * 16 + r + kx;
-        fa[mi].v = *reinterpret_cast<const uint4*>(sa + c3_off(p, g));
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        Frag<bf16_t> fb[16];
-#pragma unroll
-        for (int nj = 0; nj < 3; ++nj)
-          fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(16 * nj + r, 4 * ks + g));
-#pragma unroll
-        for (int nj = 0; nj < 16; ++nj) {
-          // program order = issue order (the fences keep the compiler from hoisting every read
-          // of the k-step to its top): read B fragment nj + 3, then the four MFMAs of fragment nj
-          __builtin_amdgcn_sched_barrier(0);
-          if (nj + 3 < 16)
-            fb[nj + 3].v = *reinterpret_cast<const uint4*>(sb + c3_off(16 * (nj + 3) + r, 4 * ks + g));
-          if (ks == 0 && nj == 12) {  // the next k-step's A fragments under the last MFMA groups
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-              const int p = (2 * wm + (mi >> 1) + ky) * C3_PW + (mi & 1) * 16 + r + kx;
-              fan[mi].v = *reinterpret_cast<const uint4*>(sa + c3_off(p, 4 + g));
-            }
-          }
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) mma(acc[mi][nj], fa[mi], fb[nj]);
-          // this step's DMA between MFMA groups: B(st + 1) during k-step 0, the A pieces in k-step 1
-          if (ks == 0 && (nj & 1) && b_next) issue_b1(b_st, nj >> 1);
-          if (ks == 1 && nj < C5V_ANEXT && a_load) {
-            const int a_j = wave + 4 * (C5V_ANEXT * sa_st + nj);
-            if (a_j < C3_APIECES) {
-              if (st < 6)
-                issue_a(t, 1, a_j);
-              else
-                issue_a(tn, 0, a_j);
-              ++a_issued;
-            }
-          }
-        }
-        if (ks == 0) {
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) fa[mi] = fan[mi];
-        }
-      }
-      // own B pieces landed (the A pieces just issued may still be in flight), reads done, barrier
-      if (a_issued == 2)
-        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (a_issued == 1)
-        asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    // ---- epilogue: y in v3's fragment-native layout ([tile][v3 wave = wm + 4 (nj >> 3)][mi][nj/2]
-    // [lane][8]) for k_rp_bn_relu_pool_*, statistics of the float32 conv outputs
-    const bool interior = t.y0 + C3_TH <= H && t.x0 + C3_TW <= W;
-#pragma unroll
-    for (int np = 0; np < 8; ++np) {
-      const int wn = np >> 2, npl = np & 3;
-      bf16_t* yt = y + (((tile * 8 + wm + 4 * wn) * 4) * 4) * 512;
-      const float b0 = sbias[32 * np + r], b1 = sbias[32 * np + 16 + r];
-      f32x2 ts0 = {0.f, 0.f}, tq0 = {0.f, 0.f}, ts1 = {0.f, 0.f}, tq1 = {0.f, 0.f};
-      if (interior) {
-        const f32x2 bb0 = {b0, b0}, bb1 = {b1, b1};
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const f32x4 v = acc[mi][2 * np], w = acc[mi][2 * np + 1];
-          const f32x2 a0 = f32x2{v[0], v[1]} + bb0, a1 = f32x2{v[2], v[3]} + bb0;
-          const f32x2 c0 = f32x2{w[0], w[1]} + bb1, c1 = f32x2{w[2], w[3]} + bb1;
-          const u32x4 pk = {pack_bf16x2(a0.x, a0.y), pack_bf16x2(a1.x, a1.y), pack_bf16x2(c0.x, c0.y),
-                            pack_bf16x2(c1.x, c1.y)};
-          __builtin_nontemporal_store(pk, reinterpret_cast<u32x4*>(yt + ((mi * 4 + npl) * 64 + lane) * 8));
-          ts0 += a0 + a1;
-          tq0 = __builtin_elementwise_fma(a0, a0, __builtin_elementwise_fma(a1, a1, tq0));
-          ts1 += c0 + c1;
-          tq1 = __builtin_elementwise_fma(c0, c0, __builtin_elementwise_fma(c1, c1, tq1));
-        }
-      } else {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const bool row_ok = t.y0 + 2 * wm + (mi >> 1) < H;
-          const int xb = t.x0 + (mi & 1) * 16 + 4 * g;
-          uint32_t hv[8];
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int nj = 2 * np + hh;
-            const float bias = hh ? b1 : b0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float av = acc[mi][nj][j] + bias;
-              hv[4 * hh + j] = (uint32_t)f32_to_bf16(av);
-              if (row_ok && xb + j < W) {
-                if (hh) {
-                  ts1.x += av;
-                  tq1.x = __builtin_fmaf(av, av, tq1.x);
-                } else {
-                  ts0.x += av;
-                  tq0.x = __builtin_fmaf(av, av, tq0.x);
-                }
-              }
-            }
-          }
-          *reinterpret_cast<uint4*>(yt + ((mi * 4 + npl) * 64 + lane) * 8) =
-              make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16));
-        }
-      }
-      // this tile's sums of channels 32 np + r and 32 np + 16 + r over the wave's 64 px, lane
-      // groups combined in fixed order, added into the wave's own LDS rows (one writer per word)
-      float v[4] = {ts0.x + ts0.y, tq0.x + tq0.y, ts1.x + ts1.y, tq1.x + tq1.y};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] += __shfl_xor(v[e], 16);
-        v[e] += __shfl_xor(v[e], 32);
-      }
-      if (g == 0) {
-        float* row0 = sst + (wm * C5 + 32 * np + r) * 2;
-        float* row1 = sst + (wm * C5 + 32 * np + 16 + r) * 2;
-        row0[0] += v[0];
-        row0[1] += v[1];
-        row1[0] += v[2];
-        row1[1] += v[3];
-      }
-    }
-  }
-  // ---- statistics: the 4 row-pair waves' rows in fixed order
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int i = tid; i < C5 * 2; i += 256)
-    slab[(long long)blockIdx.x * C5 * 2 + i] = sst[i] + sst[C5 * 2 + i] + sst[2 * C5 * 2 + i] + sst[3 * C5 * 2 + i];
-}
-
 // BN + ReLU + AdaptiveAvgPool(4) partial sums over the fragment-native y of k_rp_conv3x3_v3.
 // grid: (16 regions * POOL_SPLIT, B); 256 threads = 128 channel pairs (c, c + 16) x 2 quad lanes;
 // a quad is 4 x-consecutive pixels (never straddles a 32-px tile); one 16-byte load (one lane of
@@ -2674,23 +2463,18 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
           (const void*)k_rp_conv3x3_v3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
       if (attr != hipSuccess) return (int)attr;
       gcv = conv3_grid(B, H, W);
-      [[maybe_unused]] auto go = [&](auto kern) {
+      auto go = [&](auto kern) {
         static const hipError_t sattr =
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
         (void)sattr;
         kern<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
       };
 #ifdef RGBD_DIAG
-      if (c3_stamps_on) {
+      if (c3_stamps_on)
         go(k_rp_conv3x3_v3<true>);
-      } else
+      else
 #endif
-      {
-        static const hipError_t vattr = hipFuncSetAttribute((const void*)k_rp_conv3x3_v5,
-                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)C5V_SMEM);
-        if (vattr != hipSuccess) return (int)vattr;
-        k_rp_conv3x3_v5<<<gcv, 256, C5V_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
-      }
+        go(k_rp_conv3x3_v3<false>);
     } else {
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
