@@ -25,6 +25,10 @@ int rgbd_debug_chain_stamps(void* buf);
  * hand-off done, epilogue done; steps | chunks << 16 | chunk << 24; the item word.  (NULL, 0)
  * stops. */
 int rgbd_debug_dsam_stamps(void* buf, int launches);
+/* The stem statistics' lag kernel (k_stem_lag): buf (device, >= workgroups * 8 * 6 uint64)
+ * receives, for every workgroup and wave of each later launch, s_memtime at entry, window staged,
+ * lag loop done, waves joined, correlations written, plane sums written.  NULL stops. */
+int rgbd_debug_stem_lag_stamps(void* buf);
 
 #ifdef __cplusplus
 }

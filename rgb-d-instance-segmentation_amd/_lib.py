@@ -128,6 +128,7 @@ DIAG_SIGNATURES = {
     "rgbd_debug_conv5_stamps": (_I, [_P]),
     "rgbd_debug_chain_stamps": (_I, [_P]),
     "rgbd_debug_dsam_stamps": (_I, [_P, _I]),
+    "rgbd_debug_stem_lag_stamps": (_I, [_P]),
 }
 
 _lib = None

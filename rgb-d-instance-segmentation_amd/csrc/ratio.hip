@@ -295,9 +295,24 @@ __device__ __forceinline__ float stem_sel(float v, int H, int W, int y, int x) {
   return (y >= 0 && y < H && x >= 0 && x < W) ? bf16_to_f32(f32_to_bf16(v)) : 0.f;
 }
 
+// Diagnostics (rgbd_debug_stem_lag_stamps, diagnostic build only): every workgroup's waves record
+// s_memtime at: kernel entry, window staged (after the barrier), lag loop done, waves joined,
+// correlations written, plane sums written: stamps[(wg * 8 + wave) * 6 + point].
+__device__ unsigned long long* g_sl_stamps = nullptr;
+static bool sl_stamps_on = false;
+__device__ __forceinline__ void sl_stamp(long long idx) {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) g_sl_stamps[idx] = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool STAMPS = false>
 __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ depth3, long long bstride, int B, int H,
                                                   int W, int nband, int ncol, double* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long long sbase = ((long long)blockIdx.x * 8 + (threadIdx.x >> 6)) * 6;
+  if constexpr (STAMPS) sl_stamp(sbase + 0);
   bf16_t* X = (bf16_t*)smem;  // [3][SL_ROWS][SL_LD]: rows u0-6 .., columns cv0-8 ..
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -348,6 +363,7 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
     }
   }
   __syncthreads();
+  if constexpr (STAMPS) sl_stamp(sbase + 1);
   // per-lane fragment bases: A rows m = (c1, Ly), B columns n = (c2, Lx); m, n >= 39 are zero
   int abase[3], bbase[3];
   bool aval[3];
@@ -385,8 +401,10 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
 #pragma unroll
       for (int j = 0; j < 3; ++j) mma(acc[i][j], fa[i], fb[j]);
   }
+  if constexpr (STAMPS) sl_stamp(sbase + 2);
   // the 8 waves' tiles summed in double, in wave order
   __syncthreads();
+  if constexpr (STAMPS) sl_stamp(sbase + 3);
   double* red = (double*)smem;
   for (int w = 0; w < 8; ++w) {
     if (wave == w) {
@@ -408,6 +426,7 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
   double* out = part + (long long)wg * SL_REC;
   for (int i = tid; i < SL_NF; i += 512) out[i] = red[i];
   __syncthreads();
+  if constexpr (STAMPS) sl_stamp(sbase + 4);
   // plane sums: per channel over the block's threads, fixed order
   for (int c = 0; c < 3; ++c) {
     red[tid] = (double)tsum[c];
@@ -419,6 +438,7 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
     if (tid == 0) out[SL_NF + c] = red[0];
     __syncthreads();
   }
+  if constexpr (STAMPS) sl_stamp(sbase + 5);
 }
 
 // Border rows / columns of every image: for the anchors of the three top (bottom) rows, per
@@ -654,9 +674,17 @@ int stem_bn_moments(const float* depth3, long long bstride, int B, int H, int W,
   double* S2 = (double*)(ws + w.S2);
   double* S1 = (double*)(ws + w.S1);
   static const hipError_t attr =
-      hipFuncSetAttribute((const void*)k_stem_lag, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL_SMEM);
+      hipFuncSetAttribute((const void*)k_stem_lag<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL_SMEM);
   if (attr != hipSuccess) return (int)attr;
-  k_stem_lag<<<g.nwg, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part);
+#ifdef RGBD_DIAG
+  if (sl_stamps_on) {
+    static const hipError_t dattr =
+        hipFuncSetAttribute((const void*)k_stem_lag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL_SMEM);
+    (void)dattr;
+    k_stem_lag<true><<<g.nwg, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part);
+  } else
+#endif
+    k_stem_lag<false><<<g.nwg, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part);
   k_stem_frame<<<dim3(g.mx, 4, B), SF_THR, 0, s>>>(depth3, bstride, B, H, W, g.nfr_row, g.nfr_col, fch, cells);
   k_stem_sum<double><<<dim3(ceil_div(SL_REC, 16), 1), 256, 0, s>>>(part, g.nwg, SL_REC, 0, SL_REC, F);
   k_stem_sum<float><<<dim3(ceil_div(SF_REC, 16), 4), 256, 0, s>>>(fch, B * g.mx, SF_REC, (long long)B * g.mx * SF_REC,
@@ -2508,6 +2536,14 @@ int rgbd_debug_chain_stamps(void* buf) {
   const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_c2_stamps), &p, sizeof(p));
   if (e != hipSuccess) return (int)e;
   c2_stamps_on = p != nullptr;
+  return RGBD_OK;
+}
+
+int rgbd_debug_stem_lag_stamps(void* buf) {
+  unsigned long long* p = (unsigned long long*)buf;
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_sl_stamps), &p, sizeof(p));
+  if (e != hipSuccess) return (int)e;
+  sl_stamps_on = p != nullptr;
   return RGBD_OK;
 }
 
