@@ -368,11 +368,29 @@ int rgbd_point_sample(const float* maps, int nmaps, int h, int w, const float* c
  * the model produces under autocast are sampled without a float32 copy); f32 output */
 int rgbd_point_sample_t(int dtype, const void* maps, int nmaps, int h, int w, const float* coords, int maps_per_coord,
                         int P, float* out, void* stream);
+/* the same with the point set of map m given per map: coords [S][P][2], set_of_map int [nmaps]
+ * (device) — every image's target masks against that image's points in one launch (the matcher
+ * draws one point set per image, modeling_mask2former.py:459-463) */
+int rgbd_point_sample_sets(int dtype, const void* maps, int nmaps, int h, int w, const float* coords,
+                           const int* set_of_map, int P, float* out, void* stream);
 int rgbd_point_sample_bwd(const float* gout, int nmaps, int h, int w, const float* coords, int maps_per_coord,
                           int P, float* gmaps, void* stream);
 int rgbd_match_cost(const float* pred, int B, int Q, int P, const float* tgt, const int* toff,
                     const float* class_cost, const long long* coff, float w_mask, float w_class, float w_dice,
                     float* cost, void* stream);
+/* rgbd_match_cost with the class cost read from the matcher's softmax instead of a gathered
+ * table: class_cost[b][q][t] = -probs[b][q][labels[toff[b] + t]], probs float32 [B][Q][C],
+ * labels int64 [sum T_b] (every image's class labels, concatenated) (:448-450). */
+int rgbd_match_cost_probs(const float* pred, int B, int Q, int P, const float* tgt, const int* toff,
+                          const float* probs, int C, const long long* labels, const long long* coff, float w_mask,
+                          float w_class, float w_dice, float* cost, void* stream);
+/* rgbd_topk_rows: idx [rows][k] int64 = the indices of the k largest of each row of x [rows][n]
+ *   float32 — loss_masks' uncertainty selection torch.topk(unc, k, dim=1, sorted=False)
+ *   (modeling_mask2former.py:711): every element above the k-th largest, then the lowest-index
+ *   elements equal to it; NaN ranks largest (torch's key order).  The set only: indices are
+ *   written in increasing order.  n <= rgbd_topk_rows_max_n() (the row is held in LDS). */
+size_t rgbd_topk_rows_max_n(void);
+int rgbd_topk_rows(const float* x, int rows, int n, int k, long long* idx, void* stream);
 int rgbd_point_losses(const float* logits, const float* labels, int N, int P, float* ce, float* dice,
                       float* sums, void* stream);
 int rgbd_point_losses_bwd(const float* logits, const float* labels, int N, int P, const float* sums,
@@ -493,7 +511,9 @@ int rgbd_mask_intersections(const unsigned long long* a, int na, const unsigned 
  *   forward Y = X W^T + b: (0, 0); dX = dY W: (0, 1); dW = dY^T X: (1, 1)
  *   act RGBD_ACT_RELU_GRAD: C = acc where R > 0 else 0 (ReLU backward; bias must be NULL).
  *   A and B share dtype (RGBD_F32 / RGBD_BF16); C is that dtype, or float32 with c_f32 = 1
- *   (weight gradients of bf16 GEMMs, autocast's float32 residual streams); R has C's dtype.  bias: float32 [N] or NULL.  batch strides sa / sb / sr / sc
+ *   (weight gradients of bf16 GEMMs, autocast's float32 residual streams); R has C's dtype.
+ *   c_f32 = 2 (bf16): C float32 holding the bf16-rounded results, R in bf16 — a bf16 GEMM's
+ *   output widened for a float32 consumer (autocast's dX of a float32 input) in the store.  bias: float32 [N] or NULL.  batch strides sa / sb / sr / sc
  *   in elements.  splits > 1: split-K with float32 partials in ws (rgbd_gemm_workspace_size),
  *   summed in split order (deterministic).  bf16: float32 accumulation; f32: exact f32 MFMA. */
 #define RGBD_ACT_NONE 0
@@ -525,6 +545,17 @@ int rgbd_colsum(int dtype, const void* y, int rows, int N, long long ld, float* 
  *   per-block partials in ws summed in block order: deterministic). */
 int rgbd_layernorm_fwd(int x_dtype, const void* x, const float* gamma, const float* beta, int rows, int C,
                        float eps, int y_dtype, void* y, float* mean, float* rstd, void* stream);
+/* rgbd_add_layernorm_fwd: the post-norm residual LN(x + r) of the decoder / pixel-decoder encoder
+ *   layers (modeling_mask2former.py:1094-1101 / :1661-1683 `layer_norm(residual + hidden)`) in one
+ *   pass: s = x + r in float32 arithmetic, rounded to the promoted dtype (float32 when either is
+ *   float32, else bf16), written to s_out (the input the backward's rgbd_layernorm_bwd takes),
+ *   and y = LN(s) as rgbd_layernorm_fwd; y2 (optional, bf16) receives y rounded to bf16 as well —
+ *   the operand the consuming bf16 GEMMs would otherwise cast from y.  C % 4 == 0, C <= 1536,
+ *   16-byte aligned x / r / s_out / y / y2 (RGBD_E_SHAPE otherwise: the caller adds and
+ *   normalises separately). */
+int rgbd_add_layernorm_fwd(int x_dtype, const void* x, int r_dtype, const void* r, const float* gamma,
+                           const float* beta, int rows, int C, float eps, int y_dtype, void* s_out, void* y,
+                           void* y2, float* mean, float* rstd, void* stream);
 size_t rgbd_layernorm_bwd_workspace_size(int rows, int C);
 int rgbd_layernorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy, const float* gamma,
                        const float* mean, const float* rstd, int rows, int C, void* dx, float* dgamma,

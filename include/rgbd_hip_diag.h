@@ -14,6 +14,10 @@ extern "C" {
  * conv5 launch (k_rp_conv3x3_v3), s_memtime stamps per wave and K step of its first two tiles
  * (step top, after the DMA issue, after k-step 0 / 1's MFMAs, after the closing wait); NULL stops. */
 int rgbd_debug_conv5_stamps(void* buf);
+/* conv5 variants for timing only (wrong results): mode bit 0 drops the in-loop weight (B) copies,
+ * bit 1 the in-loop input (A) copies, bit 2 the per-step barrier, bit 3 the LDS fragment reads;
+ * modes 0, 1, 2, 3, 7, 15 exist (others: RGBD_E_ARG); 0 restores the kernel. */
+int rgbd_debug_conv5_mode(int mode);
 /* The same for the bf16 chain kernels (k_rp_chain_v2 phases 0 and 1): buf (device, >= 2 * 4 * 8 * 7
  * uint64) receives workgroup 0's stamps for its tiles 8-11 (tile top, patch staged, next
  * patch issued, stem MFMAs issued, stem ReLU/pack, fusion MFMAs issued, tile end), phase-major

@@ -83,8 +83,13 @@ SIGNATURES = {
     "rgbd_dsam_bwd_weight_planned_multi": (_I, [_I, _P, _P, _P]),
     "rgbd_point_sample": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P]),
     "rgbd_point_sample_t": (_I, [_I, _P, _I, _I, _I, _P, _I, _I, _P, _P]),
+    "rgbd_point_sample_sets": (_I, [_I, _P, _I, _I, _I, _P, _P, _I, _P, _P]),
+    "rgbd_topk_rows_max_n": (_SZ, []),
+    "rgbd_topk_rows": (_I, [_P, _I, _I, _I, _P, _P]),
     "rgbd_point_sample_bwd": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P]),
     "rgbd_match_cost": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P]),
+    "rgbd_match_cost_probs": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P, _P, ctypes.c_float, ctypes.c_float,
+                                   ctypes.c_float, _P, _P]),
     "rgbd_point_losses": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "rgbd_point_losses_bwd": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_msda_fwd": (_I, [_I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
@@ -105,6 +110,7 @@ SIGNATURES = {
     "rgbd_colsum_workspace_size": (_SZ, [_I, _I]),
     "rgbd_colsum": (_I, [_I, _P, _I, _I, _LL, _P, _P, _P]),
     "rgbd_layernorm_fwd": (_I, [_I, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P]),
+    "rgbd_add_layernorm_fwd": (_I, [_I, _P, _I, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P, _P, _P]),
     "rgbd_layernorm_bwd_workspace_size": (_SZ, [_I, _I]),
     "rgbd_layernorm_bwd": (_I, [_I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_groupnorm_workspace_size": (_SZ, [_I, _I]),
@@ -129,6 +135,7 @@ DIAG_SIGNATURES = {
     "rgbd_debug_chain_stamps": (_I, [_P]),
     "rgbd_debug_dsam_stamps": (_I, [_P, _I]),
     "rgbd_debug_stem_lag_stamps": (_I, [_P]),
+    "rgbd_debug_conv5_mode": (_I, [_I]),
 }
 
 _lib = None

@@ -174,7 +174,9 @@ struct GArgs {
   long long ldr, sr;
   void* C;
   long long ldc, sc;
-  int c_f32;
+  int c_f32;    // C stored as float32
+  int r_f32;    // R read as float32
+  int c_round;  // values rounded to bf16 before the float32 store (c_f32 = 2)
   int splits, kchunk;
   float* part;  // split-K partials [batch*splits][M][N]
   int vec_a, vec_b;
@@ -189,7 +191,7 @@ __device__ __forceinline__ float g_act(float v, int act) {
 // R in C's dtype: float32 when C is written as float32, else the operand dtype
 template <typename T>
 __device__ __forceinline__ float g_r(const GArgs& a, long long ridx) {
-  return a.c_f32 ? reinterpret_cast<const float*>(a.R)[ridx] : Num<T>::to_f(reinterpret_cast<const T*>(a.R)[ridx]);
+  return a.r_f32 ? reinterpret_cast<const float*>(a.R)[ridx] : Num<T>::to_f(reinterpret_cast<const T*>(a.R)[ridx]);
 }
 
 // epilogue of one value: act(v + bias) (+ R) | v * (R > 0); bias indexed by n (nn.Linear) or,
@@ -208,11 +210,14 @@ __device__ __forceinline__ void g_store(const GArgs& a, int bz, int m, int n0, c
   // four consecutive n of row m
   if (a.c_f32) {
     float* c = reinterpret_cast<float*>(a.C) + (long long)bz * a.sc + (long long)m * a.ldc + n0;
+    float w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = a.c_round ? bf16_to_f32(f32_to_bf16(v[e])) : v[e];
     if (n0 + 3 < a.N && ((a.ldc | n0) & 3) == 0 && (((uintptr_t)a.C) & 15) == 0 && (a.sc & 3) == 0)
-      *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(c) = make_float4(w[0], w[1], w[2], w[3]);
     else
       for (int e = 0; e < 4; ++e)
-        if (n0 + e < a.N) c[e] = v[e];
+        if (n0 + e < a.N) c[e] = w[e];
   } else {
     T* c = reinterpret_cast<T*>(a.C) + (long long)bz * a.sc + (long long)m * a.ldc + n0;
     if constexpr (sizeof(T) == 2) {
@@ -255,7 +260,7 @@ __device__ __forceinline__ void g_store8(const GArgs& a, int b, int bz, int m, i
     // g_epi.  (vec_c implies 16-byte aligned R rows.)
     float rr[8], bb[8];
     if (a.R) {
-      if (a.c_f32) {
+      if (a.r_f32) {
         const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.R) + rbase);
         const float4 y = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.R) + rbase + 4);
         rr[0] = x.x; rr[1] = x.y; rr[2] = x.z; rr[3] = x.w; rr[4] = y.x; rr[5] = y.y; rr[6] = y.z; rr[7] = y.w;
@@ -285,6 +290,10 @@ __device__ __forceinline__ void g_store8(const GArgs& a, int b, int bz, int m, i
   }
   if (a.c_f32) {
     float* c = reinterpret_cast<float*>(a.C) + (long long)b * a.sc + (long long)m * a.ldc + n0;
+    if (a.c_round) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bf16_to_f32(f32_to_bf16(v[e]));
+    }
     if (vec_c && n0 + 8 <= a.N) {
       *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -821,7 +830,10 @@ int rgbd_gemm(int dtype, int a_t, int b_t, int M, int N, int K, const void* A, l
   a.B = B; a.ldb = ldb; a.sb = sb;
   a.bias = bias; a.act = act; a.bias_m = bias_m;
   a.R = R; a.ldr = ldr; a.sr = sr;
+  RGBD_REQUIRE(c_f32 >= 0 && c_f32 <= 2, RGBD_E_ARG);
   a.C = C; a.ldc = ldc; a.sc = sc; a.c_f32 = c_f32 || dtype == RGBD_F32;
+  a.r_f32 = a.c_f32 && !(c_f32 == 2 && dtype == RGBD_BF16);
+  a.c_round = c_f32 == 2 && dtype == RGBD_BF16;
   a.splits = splits;
   a.kchunk = ((K + splits - 1) / splits + ks - 1) / ks * ks;
   a.part = (float*)ws;

@@ -207,6 +207,68 @@ __global__ __launch_bounds__(256) void k_ln_fwd_v(const void* __restrict__ x, co
   }
 }
 
+// The post-norm residual of the decoder / pixel-decoder encoder layers in one pass:
+//   s = x + r (float32 arithmetic, rounded to s's dtype, as torch's add of the two), y = LN(s);
+// s is written for the backward (rgbd_layernorm_bwd on s).  Same row grouping as k_ln_fwd_v.
+template <typename TX, typename TR, typename TS, typename TY, int T, int NCH>
+__global__ __launch_bounds__(256) void k_add_ln_fwd_v(const void* __restrict__ x, const void* __restrict__ r,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      int rows, int C, float eps, void* __restrict__ s_out,
+                                                      void* __restrict__ y, bf16_t* __restrict__ y2,
+                                                      float* __restrict__ mean, float* __restrict__ rstd) {
+  const int j = threadIdx.x % T;
+  const int row = blockIdx.x * (256 / T) + threadIdx.x / T;
+  const bool live = row < rows;
+  const long long base = (long long)(live ? row : 0) * C;
+  float v[NCH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * (j + T * k);
+    if (c < C) {
+      float a[4], b[4];
+      ld4<TX>(x, base + c, a);
+      ld4<TR>(r, base + c, b);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] = a[e] + b[e];
+      if constexpr (sizeof(TS) == 2) {  // the bf16 sum is what the norm sees
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[k][e] = bf16_to_f32(f32_to_bf16(v[k][e]));
+      }
+    } else {
+      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0.f;
+    }
+    s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+  }
+  const float mu = group_sum<T>(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+    if (4 * (j + T * k) < C)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q += (v[k][e] - mu) * (v[k][e] - mu);
+  const float var = group_sum<T>(q) / (float)C;
+  const float rs = 1.f / sqrtf(var + eps);
+  if (!live) return;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = 4 * (j + T * k);
+    if (c < C) {
+      st4<TS>(s_out, base + c, v[k]);
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = (v[k][e] - mu) * rs * (gamma ? gamma[c + e] : 1.f) + (beta ? beta[c + e] : 0.f);
+      st4<TY>(y, base + c, o);
+      if (y2) st4<bf16_t>(y2, base + c, o);
+    }
+  }
+  if (j == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
 // dx per row; dgamma / dbeta partials per block: part[blk][2][C].  A block's groups take rows
 // r0 + g, r0 + g + G, ... (G = groups per block), two rows per group in flight; the groups'
 // partials are summed in a fixed order through LDS: deterministic for a given shape.
@@ -382,6 +444,29 @@ void lnv_bwd(const void* x, const void* dy, const float* gamma, const float* mea
   else lnv_bwd_launch<TX, TD, 64, 6>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
 }
 
+template <typename TX, typename TR, typename TS, typename TY, int T, int NCH>
+void add_lnv_launch(const void* x, const void* r, const float* gamma, const float* beta, int rows, int C, float eps,
+                    void* s_out, void* y, bf16_t* y2, float* mean, float* rstd, hipStream_t s) {
+  hipLaunchKernelGGL((k_add_ln_fwd_v<TX, TR, TS, TY, T, NCH>), dim3(ceil_div(rows, 256 / T)), dim3(256), 0, s, x, r,
+                     gamma, beta, rows, C, eps, s_out, y, y2, mean, rstd);
+}
+template <typename TX, typename TR, typename TS, typename TY>
+void add_lnv(const void* x, const void* r, const float* gamma, const float* beta, int rows, int C, float eps,
+             void* s_out, void* y, bf16_t* y2, float* mean, float* rstd, hipStream_t s) {
+  const int T = lnv_group(C), nch = ceil_div(C / 4, T);
+#define ADD_LNV(TT, NN) \
+  add_lnv_launch<TX, TR, TS, TY, TT, NN>(x, r, gamma, beta, rows, C, eps, s_out, y, y2, mean, rstd, s)
+  if (T == 16) ADD_LNV(16, 1);
+  else if (T == 32) ADD_LNV(32, 1);
+  else if (nch == 1) ADD_LNV(64, 1);
+  else if (nch == 2) ADD_LNV(64, 2);
+  else if (nch == 3) ADD_LNV(64, 3);
+  else if (nch == 4) ADD_LNV(64, 4);
+  else if (nch == 5) ADD_LNV(64, 5);
+  else ADD_LNV(64, 6);
+#undef ADD_LNV
+}
+
 template <typename TX>
 void ln_fwd_t(int y_dtype, const void* x, const float* gamma, const float* beta, int rows, int C, float eps, void* y,
               float* mean, float* rstd, hipStream_t s) {
@@ -431,6 +516,35 @@ int rgbd_layernorm_fwd(int x_dtype, const void* x, const float* gamma, const flo
     ln_fwd_t<bf16_t>(y_dtype, x, gamma, beta, rows, C, eps, y, mean, rstd, s);
   else
     ln_fwd_t<float>(y_dtype, x, gamma, beta, rows, C, eps, y, mean, rstd, s);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_add_layernorm_fwd(int x_dtype, const void* x, int r_dtype, const void* r, const float* gamma,
+                           const float* beta, int rows, int C, float eps, int y_dtype, void* s_out, void* y,
+                           void* y2, float* mean, float* rstd, void* stream) {
+  RGBD_REQUIRE(x && r && s_out && y && mean && rstd && rows > 0 && C > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(lnv_ok(C), RGBD_E_SHAPE);
+  RGBD_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)r & 15) == 0 && ((uintptr_t)s_out & 15) == 0 &&
+                   ((uintptr_t)y & 15) == 0 && ((uintptr_t)y2 & 15) == 0,
+               RGBD_E_SHAPE);
+  RGBD_REQUIRE((x_dtype == RGBD_F32 || x_dtype == RGBD_BF16) && (r_dtype == RGBD_F32 || r_dtype == RGBD_BF16) &&
+                   (y_dtype == RGBD_F32 || y_dtype == RGBD_BF16),
+               RGBD_E_DTYPE);
+  hipStream_t s = (hipStream_t)stream;
+  // s in the promoted dtype of x + r: float32 when either is
+#define ADD_LN(TX, TR, TS)                                                                      \
+  do {                                                                                          \
+    if (y_dtype == RGBD_BF16)                                                                   \
+      add_lnv<TX, TR, TS, bf16_t>(x, r, gamma, beta, rows, C, eps, s_out, y, (bf16_t*)y2, mean, rstd, s); \
+    else                                                                                        \
+      add_lnv<TX, TR, TS, float>(x, r, gamma, beta, rows, C, eps, s_out, y, (bf16_t*)y2, mean, rstd, s);  \
+  } while (0)
+  if (x_dtype == RGBD_F32 && r_dtype == RGBD_F32) ADD_LN(float, float, float);
+  else if (x_dtype == RGBD_F32) ADD_LN(float, bf16_t, float);
+  else if (r_dtype == RGBD_F32) ADD_LN(bf16_t, float, float);
+  else ADD_LN(bf16_t, bf16_t, bf16_t);
+#undef ADD_LN
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -54,15 +54,17 @@ __device__ __forceinline__ Taps taps(float cx, float cy, int h, int w) {
 }
 
 // out[m][p] = bilinear sample of map m at coords[m / per][p] (x = width, y = height): a point set
-// per group of `per` consecutive maps
+// per group of `per` consecutive maps, or per map the set set_of_map[m] when that is given
 template <typename T>
 __global__ __launch_bounds__(256) void k_point_sample(const T* __restrict__ maps, int nmaps, int h, int w,
-                                                      const float* __restrict__ coords, int per, int P,
+                                                      const float* __restrict__ coords, int per,
+                                                      const int* __restrict__ set_of_map, int P,
                                                       float* __restrict__ out) {
   const long long i = blockIdx.x * 256ll + threadIdx.x;
   if (i >= (long long)nmaps * P) return;
   const int m = (int)(i / P), p = (int)(i % P);
-  const float2 c = reinterpret_cast<const float2*>(coords)[(long long)(m / per) * P + p];
+  const int set = set_of_map ? set_of_map[m] : m / per;
+  const float2 c = reinterpret_cast<const float2*>(coords)[(long long)set * P + p];
   const Taps t = taps(c.x, c.y, h, w);
   const T* mp = maps + (long long)m * h * w;
   auto in = [&](int y, int x) { return x >= 0 && x < w && y >= 0 && y < h; };
@@ -118,12 +120,16 @@ __device__ __forceinline__ T block_sum(T v, T* red) {  // 256 threads, fixed ord
 // cost[b][q][t] = w_mask * CE(q, t) + w_class * class_cost[b][q][t] + w_dice * DICE(q, t), then
 // clamped to [-1e10, 1e10] and NaN -> 0 (the reference's post-processing of the matrix).
 // pred [B][Q][P], tgt rows of image b at tgt + toff[b] * P ([T_b][P]); class_cost / cost of image b
-// at coff[b] ([Q][T_b]).  Grid (Q, B); T is processed in chunks of 8 targets.
+// at coff[b] ([Q][T_b]).  Grid (Q, B); T is processed in chunks of 8 targets.  With probs set, the
+// class cost is read as -probs[b][q][labels[toff[b] + t]] (probs [B][Q][C], the matcher's softmax)
+// instead of from class_cost.
 constexpr int MC_TC = 8;
 __global__ __launch_bounds__(256) void k_match_cost(const float* __restrict__ pred, int Q, int P,
                                                     const float* __restrict__ tgt, const int* __restrict__ toff,
                                                     const float* __restrict__ class_cost, const long long* __restrict__ coff,
-                                                    float w_mask, float w_class, float w_dice, float* __restrict__ cost) {
+                                                    const float* __restrict__ probs, int C,
+                                                    const long long* __restrict__ labels, float w_mask,
+                                                    float w_class, float w_dice, float* __restrict__ cost) {
   __shared__ float red[4];
   const int q = blockIdx.x, b = blockIdx.y;
   const int t0 = toff[b], T = toff[b + 1] - t0;
@@ -161,7 +167,8 @@ __global__ __launch_bounds__(256) void k_match_cost(const float* __restrict__ pr
         const float ce = cp / (float)P + cn / (float)P;
         const float dice = 1.f - (2.f * cs + 1.f) / (S + cy + 1.f);
         const long long o = coff[b] + (long long)q * T + tc + k;
-        float c = w_mask * ce + w_class * class_cost[o] + w_dice * dice;
+        const float cc = probs ? -probs[((long long)b * Q + q) * C + labels[t0 + tc + k]] : class_cost[o];
+        float c = w_mask * ce + w_class * cc + w_dice * dice;
         // torch.minimum / maximum propagate NaN, then nan_to_num(., 0) zeroes it
         cost[o] = isnan(c) ? 0.f : fmaxf(fminf(c, 1e10f), -1e10f);
       }
@@ -217,6 +224,91 @@ __global__ __launch_bounds__(256) void k_point_losses_bwd(const float* __restric
   gx[i] = g_ce[n] * (sg - yv) / (float)P + g_dice[n] * ddice;
 }
 
+// The k largest of every row (loss_masks' uncertainty selection, torch.topk(unc, k, dim=1,
+// sorted=False) :711): one workgroup per row, the row's order-preserving keys resident in LDS
+// (torch's TopKTypeConfig<float>: x ^ (sign ? ~0 : 0x80000000), NaN the largest), a 4-pass
+// 8-bit radix select of the k-th key T (per-wave histograms), then every key > T and the
+// lowest-index keys == T up to k, written in index order.
+constexpr int TK_THR = 512;
+constexpr int TK_HIST = (TK_THR / 64) * 256;
+constexpr int TK_MAXN = (163840 - (TK_HIST + 2 * TK_THR + 8) * 4) / 4;
+__device__ __forceinline__ uint32_t tk_key(float v) {
+  const uint32_t x = __float_as_uint(v);
+  return v == v ? (x ^ ((x & 0x80000000u) ? 0xffffffffu : 0x80000000u)) : 0xffffffffu;
+}
+// exclusive prefix sum of v over the workgroup's 512 threads (Hillis-Steele in LDS); total in *tot
+__device__ __forceinline__ uint32_t tk_scan(uint32_t v, uint32_t* buf, uint32_t* tot) {
+  const int t = threadIdx.x;
+  buf[t] = v;
+  __syncthreads();
+  for (int o = 1; o < TK_THR; o <<= 1) {
+    const uint32_t a = t >= o ? buf[t - o] : 0u;
+    __syncthreads();
+    buf[t] += a;
+    __syncthreads();
+  }
+  const uint32_t incl = buf[t];
+  if (tot) *tot = buf[TK_THR - 1];
+  __syncthreads();
+  return incl - v;
+}
+__global__ __launch_bounds__(TK_THR) void k_topk_rows(const float* __restrict__ x, int n, int k,
+                                                      long long* __restrict__ out) {
+  extern __shared__ uint32_t tk_sm[];
+  uint32_t* keys = tk_sm;
+  uint32_t* hist = tk_sm + n;               // [8 waves][256]
+  uint32_t* buf = hist + TK_HIST;           // scan buffer [512]
+  uint32_t* misc = buf + TK_THR;            // [0] digit, [1] remaining
+  const int t = threadIdx.x, wave = t >> 6;
+  const float* xr = x + (long long)blockIdx.x * n;
+  for (int i = t; i < n; i += TK_THR) keys[i] = tk_key(xr[i]);
+  uint32_t prefix = 0u, pmask = 0u;
+  int kr = k;  // keys still to take among those matching the prefix
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = t; i < TK_HIST; i += TK_THR) hist[i] = 0u;
+    __syncthreads();
+    for (int i = t; i < n; i += TK_THR) {
+      const uint32_t kv = keys[i];
+      if ((kv & pmask) == prefix) atomicAdd(&hist[wave * 256 + ((kv >> shift) & 255u)], 1u);
+    }
+    __syncthreads();
+    // suffix counts over the digits, high digit first: thread t < 256 owns digit 255 - t
+    uint32_t c = 0u;
+    if (t < 256) {
+#pragma unroll
+      for (int w = 0; w < TK_THR / 64; ++w) c += hist[w * 256 + (255 - t)];
+    }
+    const uint32_t before = tk_scan(c, buf, nullptr);  // keys with a larger digit
+    if (t < 256 && before < (uint32_t)kr && before + c >= (uint32_t)kr) {
+      misc[0] = 255u - t;
+      misc[1] = (uint32_t)kr - before;
+    }
+    __syncthreads();
+    prefix |= misc[0] << shift;
+    pmask |= 255u << shift;
+    kr = (int)misc[1];
+    __syncthreads();
+  }
+  // every key > prefix, then the first kr keys == prefix in index order
+  const int chunk = (n + TK_THR - 1) / TK_THR, c0 = min(n, t * chunk), c1 = min(n, c0 + chunk);
+  uint32_t gt = 0u, eq = 0u;
+  for (int i = c0; i < c1; ++i) {
+    const uint32_t kv = keys[i];
+    gt += kv > prefix;
+    eq += kv == prefix;
+  }
+  const uint32_t eq_before = tk_scan(eq, buf, nullptr);
+  const uint32_t take_eq = (uint32_t)kr > eq_before ? min(eq, (uint32_t)kr - eq_before) : 0u;
+  uint32_t pos = tk_scan(gt + take_eq, buf, nullptr);
+  long long* o = out + (long long)blockIdx.x * k;
+  uint32_t eq_seen = 0u;
+  for (int i = c0; i < c1; ++i) {
+    const uint32_t kv = keys[i];
+    if (kv > prefix || (kv == prefix && eq_seen++ < take_eq)) o[pos++] = i;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -229,7 +321,7 @@ int rgbd_point_sample(const float* maps, int nmaps, int h, int w, const float* c
   if (n == 0) return RGBD_OK;
   RGBD_REQUIRE(maps && coords && out, RGBD_E_ARG);
   k_point_sample<float><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(maps, nmaps, h, w, coords,
-                                                                                      maps_per_coord, P, out);
+                                                                                      maps_per_coord, nullptr, P, out);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -244,7 +336,25 @@ int rgbd_point_sample_t(int dtype, const void* maps, int nmaps, int h, int w, co
   if (n == 0) return RGBD_OK;
   RGBD_REQUIRE(maps && coords && out, RGBD_E_ARG);
   k_point_sample<bf16_t><<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      (const bf16_t*)maps, nmaps, h, w, coords, maps_per_coord, P, out);
+      (const bf16_t*)maps, nmaps, h, w, coords, maps_per_coord, nullptr, P, out);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_point_sample_sets(int dtype, const void* maps, int nmaps, int h, int w, const float* coords,
+                           const int* set_of_map, int P, float* out, void* stream) {
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  RGBD_REQUIRE(nmaps >= 0 && h > 0 && w > 0 && P >= 0, RGBD_E_ARG);
+  const long long n = (long long)nmaps * P;
+  if (n == 0) return RGBD_OK;
+  RGBD_REQUIRE(maps && coords && set_of_map && out, RGBD_E_ARG);
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  if (dtype == RGBD_F32)
+    k_point_sample<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)maps, nmaps, h, w, coords, 1,
+                                                                 set_of_map, P, out);
+  else
+    k_point_sample<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)maps, nmaps, h, w, coords, 1,
+                                                                  set_of_map, P, out);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }
@@ -265,8 +375,35 @@ int rgbd_match_cost(const float* pred, int B, int Q, int P, const float* tgt, co
                     const float* class_cost, const long long* coff, float w_mask, float w_class, float w_dice,
                     float* cost, void* stream) {
   RGBD_REQUIRE(pred && tgt && toff && class_cost && coff && cost && B > 0 && Q > 0 && P > 0, RGBD_E_ARG);
-  k_match_cost<<<dim3(Q, B), 256, 0, (hipStream_t)stream>>>(pred, Q, P, tgt, toff, class_cost, coff, w_mask, w_class,
-                                                            w_dice, cost);
+  k_match_cost<<<dim3(Q, B), 256, 0, (hipStream_t)stream>>>(pred, Q, P, tgt, toff, class_cost, coff, nullptr, 0,
+                                                            nullptr, w_mask, w_class, w_dice, cost);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+size_t rgbd_topk_rows_max_n() { return (size_t)TK_MAXN; }
+
+int rgbd_topk_rows(const float* x, int rows, int n, int k, long long* idx, void* stream) {
+  RGBD_REQUIRE(rows >= 0 && n > 0 && k > 0 && k <= n, RGBD_E_ARG);
+  RGBD_REQUIRE(n <= TK_MAXN, RGBD_E_SHAPE);
+  if (rows == 0) return RGBD_OK;
+  RGBD_REQUIRE(x && idx, RGBD_E_ARG);
+  const size_t smem = ((size_t)n + TK_HIST + TK_THR + 8) * 4;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)k_topk_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  if (attr != hipSuccess) return (int)attr;
+  k_topk_rows<<<rows, TK_THR, smem, (hipStream_t)stream>>>(x, n, k, idx);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_match_cost_probs(const float* pred, int B, int Q, int P, const float* tgt, const int* toff,
+                          const float* probs, int C, const long long* labels, const long long* coff, float w_mask,
+                          float w_class, float w_dice, float* cost, void* stream) {
+  RGBD_REQUIRE(pred && tgt && toff && probs && labels && coff && cost && B > 0 && Q > 0 && P > 0 && C > 0,
+               RGBD_E_ARG);
+  k_match_cost<<<dim3(Q, B), 256, 0, (hipStream_t)stream>>>(pred, Q, P, tgt, toff, nullptr, coff, probs, C, labels,
+                                                            w_mask, w_class, w_dice, cost);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void k_bn_affine_stem(const float* __restrict_
 // and 3 border columns), so the whole Gram matrix costs 1 521 correlations instead of a stem
 // convolution: 9 MFMAs per 32 pixels (k_stem_lag: D[(c1,Ly)][(c2,Lx)] += X_c1(u - Ly, v)
 // X_c2(u, v + Lx) over rows u and 32-pixel blocks v, bf16 products exact, f32 accumulation per
-// wave, double across waves / workgroups), the border rows / columns by k_stem_frame, and
+// wave, double across waves / workgroups), the border rows / columns by its trailing workgroups, and
 // k_stem_s2 / k_stem_bn assemble S2, S1 and the BN affines in double.  This replaces the former
 // statistics pass over the stem (126 MFMAs per 32 pixels, 181 us per bench step).
 constexpr int SL_R = 32, SL_CW = 256, SL_PADL = 8;          // B rows per band, columns per chunk
@@ -262,12 +262,13 @@ constexpr int SL_REC = SL_NF + 3;                            // + the three plan
 constexpr size_t SL_SMEM = (size_t)3 * SL_ROWS * SL_LD * 2;
 constexpr int SL_GRP = 3 * SL_ROWS * (SL_LD / 4), SL_GPT = (SL_GRP + 511) / 512;  // 4-pixel groups staged
 static_assert(SL_GPT % 6 == 0, "k_stem_lag staging rounds");
-static_assert(SL_SMEM >= SL_NF * sizeof(double), "k_stem_lag: LDS reused for the wave reduction");
-constexpr int SF_CH = 64;                                    // k_stem_frame: pixels per chunk
+static_assert(SL_SMEM >= 8 * SL_NF * sizeof(float) + 8 + 24 * sizeof(double), "k_stem_lag: LDS reused for the wave reduction");
+constexpr int SF_CH = 64;                                    // stem_frame_body: pixels per chunk
 constexpr int SF_T = 351, SF_REC = SF_T * 13 + 9;            // sums per (kind, image, chunk)
 constexpr int SF_THR = 512;  // >= SF_T + 9 + 27: the sum threads, the plain sums, the plain corner values
 constexpr int SF_AL = SF_CH + 12, SF_N = 3 * 15 * SF_AL, SF_PT = (SF_N + SF_THR - 1) / SF_THR;
-static_assert(SF_THR >= SF_T + 9 + 27, "k_stem_frame thread roles");
+static_assert(SF_THR >= SF_T + 9 + 27 && SF_THR == 512, "stem_frame_body thread roles (k_stem_lag workgroups)");
+static_assert(SL_SMEM >= sizeof(float) * 3 * 15 * SF_AL, "stem_frame_body strip in k_stem_lag LDS");
 constexpr int SC_REC = SF_T * 39 + 27;                       // corner cells per (row kind, side, image)
 
 struct StemGeom {
@@ -295,6 +296,102 @@ __device__ __forceinline__ float stem_sel(float v, int H, int W, int y, int x) {
   return (y >= 0 && y < H && x >= 0 && x < W) ? bf16_to_f32(f32_to_bf16(v)) : 0.f;
 }
 
+// Border rows / columns of every image: for the anchors of the three top (bottom) rows, per
+// (c1, c2, Ly) and anchor row j the 13 row sums over Lx of X_c1(u1, v) X_c2(u1 + Ly, v + Lx)
+// over this chunk's 64 columns; the column kinds likewise with the roles of the axes swapped; plus
+// the plain sums of X_c over the anchor rows / columns.  Workgroup = (chunk, kind, image), kind 0
+// top rows, 1 bottom rows, 2 left columns, 3 right columns: out [kind][image][chunk][SF_REC] f32
+// (a kind's chunks past its own count write zeros).  The row kinds' first / last chunk also write
+// the corner cells of the three left / right columns: cells [row kind][side][image][SC_REC] =
+// the products [t][Lx][column] and the plain values [c][row][column].
+// (run by the trailing workgroups of k_stem_lag: wid = (image * 4 + kind) * mx + chunk)
+__device__ __forceinline__ void stem_frame_body(const float* __restrict__ depth3, long long bstride, int B, int H, int W,
+                                                int nfr_row, int nfr_col, float* __restrict__ out,
+                                                float* __restrict__ cells, int wid, char* smem) {
+  float(*S)[15][SF_AL] = reinterpret_cast<float(*)[15][SF_AL]>(smem);  // strip: 15 lines across, 64 + 12 along
+  const int mx0 = max(nfr_row, nfr_col);
+  const int chunk = wid % mx0, kind = (wid / mx0) % 4, b = wid / (4 * mx0);
+  const bool rows = kind < 2;
+  const int nch = rows ? nfr_row : nfr_col, mx = max(nfr_row, nfr_col);
+  float* o = out + (((long long)kind * B + b) * mx + chunk) * SF_REC;
+  if (chunk >= nch) {
+    for (int i = threadIdx.x; i < SF_REC; i += SF_THR) o[i] = 0.f;
+    return;
+  }
+  const long long HW = (long long)H * W;
+  const int a0 = chunk * SF_CH;                                      // first anchor along the strip
+  const int line0 = kind == 0 ? 0 : (kind == 1 ? H - 3 : (kind == 2 ? 0 : W - 3));  // first anchor line
+  float pre[SF_PT];
+#pragma unroll
+  for (int k = 0; k < SF_PT; ++k) {
+    const int i = min((int)threadIdx.x + SF_THR * k, SF_N - 1);
+    const int c = i / (15 * SF_AL), li = (i / SF_AL) % 15, al = i % SF_AL;
+    const int ln = line0 - 6 + li, at = a0 - 6 + al;                // across, along
+    pre[k] = rows ? stem_ld(depth3, bstride, HW, b, c, H, W, ln, at) : stem_ld(depth3, bstride, HW, b, c, H, W, at, ln);
+  }
+#pragma unroll
+  for (int k = 0; k < SF_PT; ++k) {
+    const int i = threadIdx.x + SF_THR * k;
+    if (i < SF_N) {
+      const int c = i / (15 * SF_AL), li = (i / SF_AL) % 15, al = i % SF_AL;
+      const int ln = line0 - 6 + li, at = a0 - 6 + al;
+      S[c][li][al] = rows ? stem_sel(pre[k], H, W, ln, at) : stem_sel(pre[k], H, W, at, ln);
+    }
+  }
+  __syncthreads();
+  const int along_n = rows ? W : H;
+  const int nal = min(SF_CH, along_n - a0);
+  const int t = threadIdx.x;
+  if (t < SF_T) {  // t = ((c1 * 3 + c2) * 13 + s1) * 3 + j: s1 the across lag, 13 along lags
+    const int j = t % 3, s1 = (t / 3) % 13, c2 = (t / 39) % 3, c1 = t / 117;
+    float acc[13];
+#pragma unroll
+    for (int q = 0; q < 13; ++q) acc[q] = 0.f;
+    float win[13];
+#pragma unroll
+    for (int q = 0; q < 13; ++q) win[q] = S[c2][j + s1][q];  // along positions a - 6 .. a + 6 of a = 0
+    for (int a = 0; a < nal; ++a) {
+      const float x1 = S[c1][6 + j][6 + a];
+#pragma unroll
+      for (int q = 0; q < 13; ++q) acc[q] = __builtin_fmaf(x1, win[q], acc[q]);
+#pragma unroll
+      for (int q = 0; q < 12; ++q) win[q] = win[q + 1];
+      win[12] = S[c2][j + s1][min(a + 13, SF_AL - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < 13; ++q) o[t * 13 + q] = acc[q];
+    if (rows) {  // corner cells: the three left (first chunk) / right (last chunk) anchor columns
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
+        if (!mine) continue;
+        float* cl = cells + (((long long)kind * 2 + side) * B + b) * SC_REC;
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) {
+          const int a = side == 0 ? ci : W - 3 + ci - a0;
+          const float x1 = S[c1][6 + j][6 + a];
+#pragma unroll
+          for (int q = 0; q < 13; ++q) cl[(t * 13 + q) * 3 + ci] = x1 * S[c2][j + s1][a + q];
+        }
+      }
+    }
+  } else if (t < SF_T + 9) {  // plain sums of X_c over anchor line j
+    const int c = (t - SF_T) / 3, j = (t - SF_T) % 3;
+    float s = 0.f;
+    for (int a = 0; a < nal; ++a) s += S[c][6 + j][6 + a];
+    o[SF_T * 13 + c * 3 + j] = s;
+  } else if (rows && t < SF_T + 9 + 27) {  // plain corner values [c][row][column]
+    const int e = t - SF_T - 9, c = e / 9, j = (e / 3) % 3, ci = e % 3;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
+      if (!mine) continue;
+      const int a = side == 0 ? ci : W - 3 + ci - a0;
+      cells[(((long long)kind * 2 + side) * B + b) * SC_REC + SF_T * 39 + e] = S[c][6 + j][6 + a];
+    }
+  }
+}
+
 // Diagnostics (rgbd_debug_stem_lag_stamps, diagnostic build only): every workgroup's waves record
 // s_memtime at: kernel entry, window staged (after the barrier), lag loop done, waves joined,
 // correlations written, plane sums written: stamps[(wg * 8 + wave) * 6 + point].
@@ -307,10 +404,17 @@ __device__ __forceinline__ void sl_stamp(long long idx) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// grid: the nwg lag workgroups, then 4 * B * mx border workgroups (stem_frame_body), which fill
+// the CU slots the lag workgroups leave free instead of following them in a second launch
 template <bool STAMPS = false>
 __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ depth3, long long bstride, int B, int H,
-                                                  int W, int nband, int ncol, double* __restrict__ part) {
+                                                  int W, int nband, int ncol, double* __restrict__ part, int nfr_row,
+                                                  int nfr_col, float* __restrict__ fch, float* __restrict__ cells) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if ((int)blockIdx.x >= B * nband * ncol) {
+    stem_frame_body(depth3, bstride, B, H, W, nfr_row, nfr_col, fch, cells, (int)blockIdx.x - B * nband * ncol, smem);
+    return;
+  }
   const long long sbase = ((long long)blockIdx.x * 8 + (threadIdx.x >> 6)) * 6;
   if constexpr (STAMPS) sl_stamp(sbase + 0);
   bf16_t* X = (bf16_t*)smem;  // [3][SL_ROWS][SL_LD]: rows u0-6 .., columns cv0-8 ..
@@ -402,147 +506,55 @@ __global__ __launch_bounds__(512) void k_stem_lag(const float* __restrict__ dept
       for (int j = 0; j < 3; ++j) mma(acc[i][j], fa[i], fb[j]);
   }
   if constexpr (STAMPS) sl_stamp(sbase + 2);
-  // the 8 waves' tiles summed in double, in wave order
+  // the 8 waves' tiles summed in double, in wave order: every wave parks its f32 tile in LDS
+  // (8 x 1 521 floats), then each correlation is summed by one thread
   __syncthreads();
   if constexpr (STAMPS) sl_stamp(sbase + 3);
-  double* red = (double*)smem;
-  for (int w = 0; w < 8; ++w) {
-    if (wave == w) {
+  float* redf = (float*)smem;  // [8 wave][SL_NF]
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < 3; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int m = 16 * i + 4 * g + e, n = 16 * j + r;
-            if (m < SL_NL && n < SL_NL) {
-              const double v = (double)acc[i][j][e];
-              red[m * SL_NL + n] = w == 0 ? v : red[m * SL_NL + n] + v;
-            }
-          }
-    }
-    __syncthreads();
-  }
-  double* out = part + (long long)wg * SL_REC;
-  for (int i = tid; i < SL_NF; i += 512) out[i] = red[i];
-  __syncthreads();
-  if constexpr (STAMPS) sl_stamp(sbase + 4);
-  // plane sums: per channel over the block's threads, fixed order
-  for (int c = 0; c < 3; ++c) {
-    red[tid] = (double)tsum[c];
-    __syncthreads();
-    for (int o = 256; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
-    }
-    if (tid == 0) out[SL_NF + c] = red[0];
-    __syncthreads();
-  }
-  if constexpr (STAMPS) sl_stamp(sbase + 5);
-}
-
-// Border rows / columns of every image: for the anchors of the three top (bottom) rows, per
-// (c1, c2, Ly) and anchor row j the 13 row sums over Lx of X_c1(u1, v) X_c2(u1 + Ly, v + Lx)
-// over this chunk's 64 columns; the column kinds likewise with the roles of the axes swapped; plus
-// the plain sums of X_c over the anchor rows / columns.  Workgroup = (chunk, kind, image), kind 0
-// top rows, 1 bottom rows, 2 left columns, 3 right columns: out [kind][image][chunk][SF_REC] f32
-// (a kind's chunks past its own count write zeros).  The row kinds' first / last chunk also write
-// the corner cells of the three left / right columns: cells [row kind][side][image][SC_REC] =
-// the products [t][Lx][column] and the plain values [c][row][column].
-__global__ __launch_bounds__(SF_THR) void k_stem_frame(const float* __restrict__ depth3, long long bstride, int B, int H,
-                                                    int W, int nfr_row, int nfr_col, float* __restrict__ out,
-                                                    float* __restrict__ cells) {
-  __shared__ float S[3][15][SF_AL];  // strip: 15 lines across (anchor lines +-6), 64 + 12 along
-  const int kind = blockIdx.y, b = blockIdx.z, chunk = blockIdx.x;
-  const bool rows = kind < 2;
-  const int nch = rows ? nfr_row : nfr_col, mx = max(nfr_row, nfr_col);
-  float* o = out + (((long long)kind * B + b) * mx + chunk) * SF_REC;
-  if (chunk >= nch) {
-    for (int i = threadIdx.x; i < SF_REC; i += SF_THR) o[i] = 0.f;
-    return;
-  }
-  const long long HW = (long long)H * W;
-  const int a0 = chunk * SF_CH;                                      // first anchor along the strip
-  const int line0 = kind == 0 ? 0 : (kind == 1 ? H - 3 : (kind == 2 ? 0 : W - 3));  // first anchor line
-  float pre[SF_PT];
-#pragma unroll
-  for (int k = 0; k < SF_PT; ++k) {
-    const int i = min((int)threadIdx.x + SF_THR * k, SF_N - 1);
-    const int c = i / (15 * SF_AL), li = (i / SF_AL) % 15, al = i % SF_AL;
-    const int ln = line0 - 6 + li, at = a0 - 6 + al;                // across, along
-    pre[k] = rows ? stem_ld(depth3, bstride, HW, b, c, H, W, ln, at) : stem_ld(depth3, bstride, HW, b, c, H, W, at, ln);
-  }
-#pragma unroll
-  for (int k = 0; k < SF_PT; ++k) {
-    const int i = threadIdx.x + SF_THR * k;
-    if (i < SF_N) {
-      const int c = i / (15 * SF_AL), li = (i / SF_AL) % 15, al = i % SF_AL;
-      const int ln = line0 - 6 + li, at = a0 - 6 + al;
-      S[c][li][al] = rows ? stem_sel(pre[k], H, W, ln, at) : stem_sel(pre[k], H, W, at, ln);
-    }
-  }
-  __syncthreads();
-  const int along_n = rows ? W : H;
-  const int nal = min(SF_CH, along_n - a0);
-  const int t = threadIdx.x;
-  if (t < SF_T) {  // t = ((c1 * 3 + c2) * 13 + s1) * 3 + j: s1 the across lag, 13 along lags
-    const int j = t % 3, s1 = (t / 3) % 13, c2 = (t / 39) % 3, c1 = t / 117;
-    float acc[13];
-#pragma unroll
-    for (int q = 0; q < 13; ++q) acc[q] = 0.f;
-    float win[13];
-#pragma unroll
-    for (int q = 0; q < 13; ++q) win[q] = S[c2][j + s1][q];  // along positions a - 6 .. a + 6 of a = 0
-    for (int a = 0; a < nal; ++a) {
-      const float x1 = S[c1][6 + j][6 + a];
-#pragma unroll
-      for (int q = 0; q < 13; ++q) acc[q] = __builtin_fmaf(x1, win[q], acc[q]);
-#pragma unroll
-      for (int q = 0; q < 12; ++q) win[q] = win[q + 1];
-      win[12] = S[c2][j + s1][min(a + 13, SF_AL - 1)];
-    }
-#pragma unroll
-    for (int q = 0; q < 13; ++q) o[t * 13 + q] = acc[q];
-    if (rows) {  // corner cells: the three left (first chunk) / right (last chunk) anchor columns
-#pragma unroll
-      for (int side = 0; side < 2; ++side) {
-        const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
-        if (!mine) continue;
-        float* cl = cells + (((long long)kind * 2 + side) * B + b) * SC_REC;
-#pragma unroll
-        for (int ci = 0; ci < 3; ++ci) {
-          const int a = side == 0 ? ci : W - 3 + ci - a0;
-          const float x1 = S[c1][6 + j][6 + a];
-#pragma unroll
-          for (int q = 0; q < 13; ++q) cl[(t * 13 + q) * 3 + ci] = x1 * S[c2][j + s1][a + q];
-        }
+      for (int e = 0; e < 4; ++e) {
+        const int m = 16 * i + 4 * g + e, n = 16 * j + r;
+        if (m < SL_NL && n < SL_NL) redf[wave * SL_NF + m * SL_NL + n] = acc[i][j][e];
       }
-    }
-  } else if (t < SF_T + 9) {  // plain sums of X_c over anchor line j
-    const int c = (t - SF_T) / 3, j = (t - SF_T) % 3;
-    float s = 0.f;
-    for (int a = 0; a < nal; ++a) s += S[c][6 + j][6 + a];
-    o[SF_T * 13 + c * 3 + j] = s;
-  } else if (rows && t < SF_T + 9 + 27) {  // plain corner values [c][row][column]
-    const int e = t - SF_T - 9, c = e / 9, j = (e / 3) % 3, ci = e % 3;
+  // plane sums: per wave in double (lane order fixed by the butterfly), parked after the tiles
+  double* wsum = (double*)(smem + 8 * SL_NF * sizeof(float) + 8);  // [8 wave][3], 8-byte aligned
 #pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
-      if (!mine) continue;
-      const int a = side == 0 ? ci : W - 3 + ci - a0;
-      cells[(((long long)kind * 2 + side) * B + b) * SC_REC + SF_T * 39 + e] = S[c][6 + j][6 + a];
-    }
+  for (int c = 0; c < 3; ++c) {
+    double v = (double)tsum[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) wsum[wave * 3 + c] = v;
   }
+  __syncthreads();
+  double* out = part + (long long)wg * SL_REC;
+  for (int i = tid; i < SL_NF; i += 512) {
+    double t = (double)redf[i];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) t += (double)redf[w * SL_NF + i];
+    out[i] = t;
+  }
+  if (tid < 3) {
+    double t = wsum[tid];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) t += wsum[w * 3 + tid];
+    out[SL_NF + tid] = t;
+  }
+  if constexpr (STAMPS) sl_stamp(sbase + 4);
+  if constexpr (STAMPS) sl_stamp(sbase + 5);
 }
 
 // dst[s][e] = sum_k src[s * seg_stride + k * stride + e] (k < n, fixed order: 16 groups of every
 // 16th k, then the groups in order): workgroup = 16 consecutive elements x 16 groups.
 template <typename T>
-__global__ __launch_bounds__(256) void k_stem_sum(const T* __restrict__ src, int n, long long stride,
-                                                  long long seg_stride, int seg_len, double* __restrict__ dst) {
-  __shared__ double red[16][17];
-  const int s = blockIdx.y, el = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int e = blockIdx.x * 16 + el;
+__device__ __forceinline__ void stem_sum_body(const T* __restrict__ src, int n, long long stride, long long seg_stride,
+                                              int seg_len, double* __restrict__ dst, int bx, int s,
+                                              double (*red)[17]) {
+  const int el = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int e = bx * 16 + el;
   double acc = 0.0;
   if (e < seg_len) {
     const T* p = src + s * seg_stride + e;
@@ -565,6 +577,33 @@ __global__ __launch_bounds__(256) void k_stem_sum(const T* __restrict__ src, int
     for (int q = 0; q < 16; ++q) t += red[q][el];
     dst[(long long)s * seg_len + e] = t;
   }
+}
+
+// The three reductions of the stem moments in one launch (1-D grid): the lag partials -> F
+// (double), the border chunks -> fr [kind] and the corner cells -> ce [row kind][side] (float).
+struct StemSums {
+  const double* part;
+  const float *fch, *cells;
+  double *F, *fr, *ce;
+  int nwg, nfch, B;
+};
+constexpr int SS_B0 = (SL_REC + 15) / 16, SS_B1 = 4 * ((SF_REC + 15) / 16), SS_B2 = 4 * ((SC_REC + 15) / 16);
+__global__ __launch_bounds__(256) void k_stem_sums(const StemSums a) {
+  __shared__ double red[16][17];
+  int bx = blockIdx.x;
+  if (bx < SS_B0) {
+    stem_sum_body<double>(a.part, a.nwg, SL_REC, 0, SL_REC, a.F, bx, 0, red);
+    return;
+  }
+  bx -= SS_B0;
+  if (bx < SS_B1) {
+    const int per = SS_B1 / 4;
+    stem_sum_body<float>(a.fch, a.nfch, SF_REC, (long long)a.nfch * SF_REC, SF_REC, a.fr, bx % per, bx / per, red);
+    return;
+  }
+  bx -= SS_B1;
+  const int per = SS_B2 / 4;
+  stem_sum_body<float>(a.cells, a.B, SC_REC, (long long)a.B * SC_REC, SC_REC, a.ce, bx % per, bx / per, red);
 }
 
 // S2 [147][147] and S1 [147] (k = c * 49 + ay * 7 + ax, the window offset a = (ay, ax) of
@@ -676,20 +715,20 @@ int stem_bn_moments(const float* depth3, long long bstride, int B, int H, int W,
   static const hipError_t attr =
       hipFuncSetAttribute((const void*)k_stem_lag<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL_SMEM);
   if (attr != hipSuccess) return (int)attr;
+  const int nall = g.nwg + 4 * B * g.mx;
 #ifdef RGBD_DIAG
   if (sl_stamps_on) {
     static const hipError_t dattr =
         hipFuncSetAttribute((const void*)k_stem_lag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SL_SMEM);
     (void)dattr;
-    k_stem_lag<true><<<g.nwg, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part);
+    k_stem_lag<true><<<nall, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part, g.nfr_row, g.nfr_col,
+                                               fch, cells);
   } else
 #endif
-    k_stem_lag<false><<<g.nwg, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part);
-  k_stem_frame<<<dim3(g.mx, 4, B), SF_THR, 0, s>>>(depth3, bstride, B, H, W, g.nfr_row, g.nfr_col, fch, cells);
-  k_stem_sum<double><<<dim3(ceil_div(SL_REC, 16), 1), 256, 0, s>>>(part, g.nwg, SL_REC, 0, SL_REC, F);
-  k_stem_sum<float><<<dim3(ceil_div(SF_REC, 16), 4), 256, 0, s>>>(fch, B * g.mx, SF_REC, (long long)B * g.mx * SF_REC,
-                                                                  SF_REC, fr);
-  k_stem_sum<float><<<dim3(ceil_div(SC_REC, 16), 4), 256, 0, s>>>(cells, B, SC_REC, (long long)B * SC_REC, SC_REC, ce);
+    k_stem_lag<false><<<nall, 512, SL_SMEM, s>>>(depth3, bstride, B, H, W, g.nband, g.ncol, part, g.nfr_row,
+                                                g.nfr_col, fch, cells);
+  StemSums ss{part, fch, cells, F, fr, ce, g.nwg, B * g.mx, B};
+  k_stem_sums<<<SS_B0 + SS_B1 + SS_B2, 256, 0, s>>>(ss);
   k_stem_s2<<<ceil_div(147 * 147 + 147, 256), 256, 0, s>>>(F, fr, ce, S2, S1);
   k_stem_bn<<<STEM_C, 256, 0, s>>>(S2, S1, blob, L, (double)B * H * W, momentum, bn, aff1);
   return RGBD_OK;
@@ -1782,6 +1821,7 @@ __device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y)
 // only while a buffer is set: the production kernel's code is unchanged.
 __device__ unsigned long long* g_c3_stamps = nullptr;
 [[maybe_unused]] static bool c3_stamps_on = false;
+[[maybe_unused]] static int c3_mode = 0;
 __device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) {
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -1789,7 +1829,10 @@ __device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) 
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool STAMPS>
+// NODMA (diagnostic build only, rgbd_debug_conv5_mode): bit 0 drops the in-loop B copies, bit 1
+// the in-loop A copies, bit 2 the per-step barrier, bit 3 the fragment reads (constant operands)
+// — wrong results; isolates the DMA's, the lockstep's and the fragment stream's costs.
+template <bool STAMPS, int NODMA = 0>
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
                                                        bf16_t* __restrict__ y, float* __restrict__ slab) {
@@ -1822,11 +1865,11 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   // 1.7 % faster than every wave issuing 4 pieces at the step top; waves 4-7 issuing theirs
   // after their MFMAs instead was 0.7 % slower than that — r05 ab_e.txt, conv5_stamps_e.txt.)
   const bool loader = wave < 4;
-  auto issue_b = [&](int st) {
+  auto issue_b = [&](int st, int k0, int k1) {
     const char* src = w5s + (size_t)st * (C5 * 128) + wave * 8192 + 16 * lane;
     const uint32_t dst = lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 8192;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) glds16(src + 1024 * k, dst + 1024 * k);
+    for (int k = k0; k < k1; ++k) glds16(src + 1024 * k, dst + 1024 * k);
   };
 
   // BN statistics per channel as (even, odd) pixel pairs: packed adds / FMAs, one instruction
@@ -1842,7 +1885,7 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
     const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
     for (int j = wave; j < C3_APIECES; j += 8) issue_a(t, 0, j);
-    if (loader) issue_b(0);
+    if (loader) issue_b(0, 0, 8);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1874,11 +1917,13 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       const int a_kind = (st < 6 && a_j < C3_APIECES) ? 1 : ((st >= 9 && st < 15 && has_next && a_j < C3_APIECES) ? 2 : 0);
       // loaders: B(st + 1) and their A piece before their MFMAs; waves 4-7: their A piece after
       if (loader) {
-        if (b_next) issue_b(b_st);
-        if (a_kind == 1) issue_a(t, 1, a_j);
-        if (a_kind == 2) issue_a(tn, 0, a_j);
+        if (b_next && !(NODMA & 1)) issue_b(b_st, 0, 8);
+        if (!(NODMA & 2)) {
+          if (a_kind == 1) issue_a(t, 1, a_j);
+          if (a_kind == 2) issue_a(tn, 0, a_j);
+        }
       }
-      a_issued = a_kind != 0;
+      a_issued = (NODMA & 2) ? 0 : a_kind != 0;
       const int h = st >= 9, tap = st - 9 * h, ky = tap / 3, kx = tap % 3;
       const char* sa = smem + h * (C3_APIX * 128);
       const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
@@ -1886,21 +1931,28 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         Frag<bf16_t> fa[4], fb[8];
+        if constexpr (!(NODMA & 8)) {
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const int p = (2 * wm + (mi >> 1) + ky) * C3_PW + (mi & 1) * 16 + r + kx;
-          fa[mi].v = *reinterpret_cast<const uint4*>(sa + c3_off(p, 4 * ks + g));
+          for (int mi = 0; mi < 4; ++mi) {
+            const int p = (2 * wm + (mi >> 1) + ky) * C3_PW + (mi & 1) * 16 + r + kx;
+            fa[mi].v = *reinterpret_cast<const uint4*>(sa + c3_off(p, 4 * ks + g));
+          }
+#pragma unroll
+          for (int nj = 0; nj < 8; ++nj)
+            fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, 4 * ks + g));
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) fa[mi].v = make_uint4(lane, ks, st, mi);
+#pragma unroll
+          for (int nj = 0; nj < 8; ++nj) fb[nj].v = make_uint4(nj, lane, ks, st);
         }
-#pragma unroll
-        for (int nj = 0; nj < 8; ++nj)
-          fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, 4 * ks + g));
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
         if (STAMPS && sts) c3_stamp(sts, sidx + 2 + ks);
       }
-      if (!loader) {  // the A piece lands under the barrier / next step (needed >= 3 steps later)
+      if (!loader && !(NODMA & 2)) {  // the A piece lands under the barrier / next step (needed >= 3 steps later)
         if (a_kind == 1) issue_a(t, 1, a_j);
         if (a_kind == 2) issue_a(tn, 0, a_j);
       }
@@ -1911,7 +1963,9 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
         else
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         if (sts) c3_stamp(sts, sidx + 4);
-        __builtin_amdgcn_s_barrier();
+        if constexpr (!(NODMA & 4)) __builtin_amdgcn_s_barrier();
+      } else if constexpr (NODMA & 4) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       } else {
         if (a_issued == 1)
           asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -2498,9 +2552,18 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
         kern<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
       };
 #ifdef RGBD_DIAG
-      if (c3_stamps_on)
-        go(k_rp_conv3x3_v3<true>);
-      else
+      if (c3_stamps_on || c3_mode) {
+        const int md = c3_mode;
+#define C3_MODE(M)                                     \
+  if (md == M) {                                       \
+    if (c3_stamps_on)                                  \
+      go(k_rp_conv3x3_v3<true, M>);                    \
+    else                                               \
+      go(k_rp_conv3x3_v3<false, M>);                   \
+  }
+        C3_MODE(0) C3_MODE(1) C3_MODE(2) C3_MODE(3) C3_MODE(7) C3_MODE(15)
+#undef C3_MODE
+      } else
 #endif
         go(k_rp_conv3x3_v3<false>);
     } else {
@@ -2544,6 +2607,12 @@ int rgbd_debug_stem_lag_stamps(void* buf) {
   const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_sl_stamps), &p, sizeof(p));
   if (e != hipSuccess) return (int)e;
   sl_stamps_on = p != nullptr;
+  return RGBD_OK;
+}
+
+int rgbd_debug_conv5_mode(int mode) {
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 3 && mode != 7 && mode != 15) return RGBD_E_ARG;
+  c3_mode = mode;
   return RGBD_OK;
 }
 

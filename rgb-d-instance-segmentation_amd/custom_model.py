@@ -155,6 +155,8 @@ class CustomMask2FormerForUniversalSegmentation(Mask2FormerForUniversalSegmentat
         # f3: the loss's point-sampled mask terms and its matcher's costs on the HIP kernels, the
         # Hungarian assignments solved on the GPU (no host round trip)
         point_loss.install(self.criterion)
+        # f1: the class head (built by the HF constructor after the model body was installed)
+        dense.install(self.class_predictor)
 
     def set_compute_dtype(self, dtype):
         self.model.pixel_level_module.set_compute_dtype(dtype)

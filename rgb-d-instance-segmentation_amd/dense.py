@@ -95,7 +95,8 @@ def gemm(A, B, a_t, b_t, M, N, K, bias=None, act=ACT_NONE, R=None, c_f32=False, 
     with the given batch strides); returns C contiguous."""
     dt = A.dtype
     c_dt = torch.float32 if (c_f32 or dt == torch.float32) else dt
-    if B.dtype != dt or dt not in _CODE or (R is not None and R.dtype != c_dt):
+    r_dt = dt if c_f32 == 2 else c_dt  # c_f32 = 2: bf16-rounded results stored as float32, R in dt
+    if B.dtype != dt or dt not in _CODE or (R is not None and R.dtype != r_dt):
         raise TypeError(f"gemm: A / B must share float32 / bfloat16 and R must have C's dtype, got {A.dtype}, "
                         f"{B.dtype}, {None if R is None else R.dtype}")
     for t in (A, B, R):
@@ -127,9 +128,20 @@ def colsum(y2):
 
 
 def _rows(x, dt):
+    """x as contiguous [rows, C] in dt.  A cast is made once per tensor (and version): it is
+    kept on x, so the projections that share an input (q / k of the self-attention, the sampling
+    offsets / attention weights of the deformable attention) and a fused LayerNorm's bf16 twin
+    (add_layer_norm) are not cast again."""
+    if x.dtype != dt:
+        hit = getattr(x, "_rgbd_rows", None)
+        if hit is not None and hit[0] == (x._version, dt) and hit[1].shape[-1] == x.shape[-1]:
+            return hit[1]
     x2 = x.reshape(-1, x.shape[-1])
     if x2.dtype != dt:
         x2 = x2.to(dt)
+        x2 = x2.contiguous()
+        x._rgbd_rows = ((x._version, dt), x2)
+        return x2
     return x2.contiguous()
 
 
@@ -140,13 +152,16 @@ def _fwd(x2, wc, b, act, M, N, K):
     return gemm(x2, wc, 0, 0, M, N, K, bias=b, act=act)
 
 
-def _dx(g2, wc, M, K, N, act=ACT_NONE, R=None):
+def _dx(g2, wc, M, K, N, act=ACT_NONE, R=None, out_dtype=None):
     """dX [M][K] = dY [M][N] W [N][K] (act ACT_RELU_GRAD: times R > 0).  bf16 with many rows: W
     transposed once (a [K][N] copy, 0.1-2 MB) so both operands are K-contiguous for the LDS-DMA
-    kernel (csrc/gemm.hip k_gemm_lds); otherwise the transposed-operand layout (0, 1)."""
+    kernel (csrc/gemm.hip k_gemm_lds); otherwise the transposed-operand layout (0, 1).
+    out_dtype float32 for bf16 operands: the bf16-rounded results stored as float32 by the GEMM
+    (the cast autograd would make for a float32 input, without its own pass)."""
+    c_f32 = 2 if (out_dtype == torch.float32 and g2.dtype == torch.bfloat16) else 0
     if g2.dtype == torch.bfloat16 and M >= 1024 and K % 8 == 0 and N % 8 == 0:
-        return gemm(g2, wc.t().contiguous(), 0, 0, M, K, N, act=act, R=R)
-    return gemm(g2, wc, 0, 1, M, K, N, act=act, R=R)
+        return gemm(g2, wc.t().contiguous(), 0, 0, M, K, N, act=act, R=R, c_f32=c_f32)
+    return gemm(g2, wc, 0, 1, M, K, N, act=act, R=R, c_f32=c_f32)
 
 
 class LinearFunction(torch.autograd.Function):
@@ -174,7 +189,7 @@ class LinearFunction(torch.autograd.Function):
             g2 = g2 * (y > 0)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _dx(g2, wc, M, K, N).to(ctx.x_dtype).view(*gy.shape[:-1], K)
+            dx = _dx(g2, wc, M, K, N, out_dtype=ctx.x_dtype).to(ctx.x_dtype).view(*gy.shape[:-1], K)
         if ctx.needs_input_grad[1]:
             dw = gemm(g2, x2, 1, 1, N, K, M, c_f32=True).to(ctx.w_dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
@@ -207,7 +222,7 @@ class FFNFunction(torch.autograd.Function):
         dh = _dx(g2, w2c, M, F_, N, act=ACT_RELU_GRAD, R=h)
         dw2 = gemm(g2, h, 1, 1, N, F_, M, c_f32=True).to(ctx.w_dtypes[1])
         db2 = colsum(g2)
-        dx = _dx(dh, w1c, M, K, F_).to(ctx.x_dtype).view(*gy.shape[:-1], K)
+        dx = _dx(dh, w1c, M, K, F_, out_dtype=ctx.x_dtype).to(ctx.x_dtype).view(*gy.shape[:-1], K)
         dw1 = gemm(dh, x2, 1, 1, F_, K, M, c_f32=True).to(ctx.w_dtypes[0])
         db1 = colsum(dh)
         return dx, dw1, db1, dw2, db2, None
@@ -250,6 +265,57 @@ class LayerNormFunction(torch.autograd.Function):
         check(L.rgbd_layernorm_bwd(_CODE[x2.dtype], _p(x2), _CODE[g2.dtype], _p(g2), _p(g32), _p(mean), _p(rstd),
                                    rows, C, _p(dx), _p(dg), _p(db), _p(ws), _stream(x2.device)), "rgbd_layernorm_bwd")
         return (dx.to(ctx.x_dtype).view(gy.shape), dg if ctx.has_g else None, db if ctx.has_b else None, None, None)
+
+
+class AddLayerNormFunction(torch.autograd.Function):
+    """y = LayerNorm(x + r): the sum and the norm in one kernel (rgbd_add_layernorm_fwd), the sum
+    kept for the backward; its gradient goes to x and r in their own dtypes (what autograd's add
+    backward hands each: the same values, cast once)."""
+
+    @staticmethod
+    def forward(ctx, x, r, gamma, beta, eps, y_dtype, twin):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        r2 = r.reshape(-1, C).contiguous()
+        x2 = x2 if x2.data_ptr() % 16 == 0 else x2.clone()  # the kernel's 16-byte row accesses
+        r2 = r2 if r2.data_ptr() % 16 == 0 else r2.clone()
+        rows = x2.shape[0]
+        s_dtype = torch.promote_types(x2.dtype, r2.dtype)
+        s = torch.empty((rows, C), dtype=s_dtype, device=x.device)
+        y = torch.empty((rows, C), dtype=y_dtype, device=x.device)
+        y2 = torch.empty((rows, C), dtype=torch.bfloat16, device=x.device) if twin else None
+        mean = torch.empty((rows,), dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        g32 = None if gamma is None else gamma.detach().float().contiguous()
+        b32 = None if beta is None else beta.detach().float().contiguous()
+        check(_lib.lib().rgbd_add_layernorm_fwd(_CODE[x2.dtype], _p(x2), _CODE[r2.dtype], _p(r2), _p(g32), _p(b32),
+                                                rows, C, float(eps), _CODE[y_dtype], _p(s), _p(y), _p(y2), _p(mean),
+                                                _p(rstd), _stream(x.device)), "rgbd_add_layernorm_fwd")
+        ctx.save_for_backward(s, g32, mean, rstd)
+        ctx.dtypes, ctx.has_g, ctx.has_b = (x.dtype, r.dtype), gamma is not None, beta is not None
+        if y2 is None:
+            y2 = torch.empty((0,), dtype=torch.bfloat16, device=x.device)
+        ctx.mark_non_differentiable(y2)
+        return y.view(x.shape), y2
+
+    @staticmethod
+    def backward(ctx, gy, _gy2):
+        s, g32, mean, rstd = ctx.saved_tensors
+        rows, C = s.shape
+        g2 = gy.reshape(rows, C)
+        if g2.dtype not in _CODE:
+            g2 = g2.float()
+        g2 = g2.contiguous()
+        ds = torch.empty_like(s)
+        dg = torch.empty((C,), dtype=torch.float32, device=s.device)
+        db = torch.empty_like(dg)
+        L = _lib.lib()
+        ws = _workspace(s.device, L.rgbd_layernorm_bwd_workspace_size(rows, C), "ln_bwd")
+        check(L.rgbd_layernorm_bwd(_CODE[s.dtype], _p(s), _CODE[g2.dtype], _p(g2), _p(g32), _p(mean), _p(rstd),
+                                   rows, C, _p(ds), _p(dg), _p(db), _p(ws), _stream(s.device)), "rgbd_layernorm_bwd")
+        ds = ds.view(gy.shape)
+        return (ds.to(ctx.dtypes[0]), ds.to(ctx.dtypes[1]), dg if ctx.has_g else None, db if ctx.has_b else None,
+                None, None, None)
 
 
 class GroupNormFunction(torch.autograd.Function):
@@ -327,6 +393,26 @@ def layer_norm(x, ln):
     return LayerNormFunction.apply(x, ln.weight, ln.bias, ln.eps, y_dtype)
 
 
+def add_layer_norm(x, r, ln):
+    """ln(x + r) for the post-norm residual of a covered layer: one fused kernel where the shapes
+    allow it (HipLayerNorm's coverage, C % 4 == 0, 16-byte aligned rows), else the add and the
+    module."""
+    C = x.shape[-1]
+    if (isinstance(ln, HipLayerNorm) and x.is_cuda and r.is_cuda and x.shape == r.shape and x.numel() > 0
+            and len(ln.normalized_shape) == 1 and ln.normalized_shape[0] == C and C % 4 == 0 and C <= 1536
+            and x.dtype in _CODE and r.dtype in _CODE):
+        amp = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+        y_dtype = torch.float32 if torch.is_autocast_enabled("cuda") else torch.promote_types(x.dtype, r.dtype)
+        # under bf16 autocast the consumers are bf16 GEMMs: the kernel also writes y in bf16 and
+        # _rows serves that instead of casting y again (the same RNE rounding of the same float)
+        twin = amp and y_dtype == torch.float32
+        y, y2 = AddLayerNormFunction.apply(x, r, ln.weight, ln.bias, ln.eps, y_dtype, twin)
+        if twin:
+            y._rgbd_rows = ((y._version, torch.bfloat16), y2)
+        return y
+    return ln(x + r)
+
+
 def _cuda_ok(x):
     return x.is_cuda and compute_dtype(x) is not None and x.numel() > 0
 
@@ -391,13 +477,13 @@ def _make_decoder_layer_class():
                 query=self.with_pos_embed(hidden_states, query_position_embeddings),
                 key=self.with_pos_embed(encoder_hidden_states[level_index], position_embeddings[level_index]),
                 value=encoder_hidden_states[level_index], attn_mask=encoder_attention_mask, key_padding_mask=None)
-            hidden_states = self.cross_attn_layer_norm(residual + hidden_states)
+            hidden_states = add_layer_norm(residual, hidden_states, self.cross_attn_layer_norm)
             residual = hidden_states
             hidden_states = self_attention(self.self_attn, hidden_states, query_position_embeddings)
-            hidden_states = self.self_attn_layer_norm(residual + hidden_states)
+            hidden_states = add_layer_norm(residual, hidden_states, self.self_attn_layer_norm)
             residual = hidden_states
             hidden_states = ffn(hidden_states, self.fc1, self.fc2)
-            hidden_states = self.final_layer_norm(residual + hidden_states)
+            hidden_states = add_layer_norm(residual, hidden_states, self.final_layer_norm)
             return (hidden_states,)
 
     return _L, HipMaskedAttentionDecoderLayer
@@ -419,10 +505,10 @@ def _make_encoder_layer_class():
                 encoder_attention_mask=attention_mask, position_embeddings=position_embeddings,
                 reference_points=reference_points, spatial_shapes_list=spatial_shapes_list,
                 level_start_index=level_start_index, output_attentions=output_attentions)
-            hidden_states = self.self_attn_layer_norm(residual + hidden_states)
+            hidden_states = add_layer_norm(residual, hidden_states, self.self_attn_layer_norm)
             residual = hidden_states
             hidden_states = ffn(hidden_states, self.fc1, self.fc2)
-            hidden_states = self.final_layer_norm(residual + hidden_states)
+            hidden_states = add_layer_norm(residual, hidden_states, self.final_layer_norm)
             if self.training:
                 # the reference clamps when any value is non-finite (:1094-1097, a host sync per
                 # layer); clamping unconditionally is the same map (identity on finite float32,

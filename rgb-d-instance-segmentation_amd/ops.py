@@ -724,6 +724,13 @@ def mask_attention(logits: torch.Tensor, size, heads: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ f3 matcher assignment
+class LsaResult(list):
+    """The per-matrix [(row_ind, col_ind)] list, plus ``rows_all`` / ``cols_all`` (every matrix's
+    indices concatenated, views of the kernel's output: no copy) and ``counts`` (host ints)."""
+    rows_all = cols_all = None
+    counts = ()
+
+
 def linear_sum_assignment_batch(costs, validate=False, return_status=False):
     """scipy.optimize.linear_sum_assignment for a list of 2-D float32 CUDA cost matrices in one
     launch (rgbd_lsa_batch).  Returns [(row_ind, col_ind)] as int64 CUDA tensors, scipy's order
@@ -763,11 +770,13 @@ def linear_sum_assignment_batch(costs, validate=False, return_status=False):
                 raise ValueError("cost matrix is infeasible")
             if s == 2:
                 raise ValueError("matrix contains invalid numeric entries")
-    out, o = [], 0
+    out, o, counts = LsaResult(), 0, []
     for i in range(len(costs)):
         n = int(min(meta[4 * i + 1], meta[4 * i + 2]))
         out.append((rows[o:o + n], cols[o:o + n]))
+        counts.append(n)
         o += n
+    out.rows_all, out.cols_all, out.counts = rows[:o], cols[:o], tuple(counts)
     return (out, status) if return_status else out
 
 

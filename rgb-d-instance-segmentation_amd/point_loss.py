@@ -22,12 +22,69 @@ from transformers.models.mask2former.modeling_mask2former import Mask2FormerHung
 
 from . import _lib
 from ._lib import RGBD_BF16, RGBD_F32, check
-from .ops import _need_cuda, _p, _stream, device_const
+from .ops import LsaResult, _need_cuda, _p, _stream, device_const
 
 # loss_masks' uncertainty top-k: unsorted by default (the loss terms are sums over the point set,
 # so only the float summation order changes; the segmented sort cost ~2.4 ms per whole-model
 # step); True — or RGBD_SORTED_TOPK=1 — takes the reference's sorted selection (parity runs)
 SORTED_TOPK = os.environ.get("RGBD_SORTED_TOPK", "0") == "1"
+
+
+# one entry each, shared by the loss and its matcher (the final and the nine auxiliary outputs of a
+# step see the same label tensors): the cache holds the label tensors themselves and matches them
+# by identity (+ version counters), so their storage cannot be recycled under a stale entry
+_ROWS_CACHE = []
+_LABELS_CACHE = []
+
+
+def target_rows(mask_labels, dtype):
+    """Every image's target masks cast like the reference (``.to(pred_masks)``), as float32 rows
+    [sum T, H, W] and their image offsets — built once per set of labels, None when the images
+    differ in size (then the reference's zero-padded batch is used)."""
+    versions = tuple(m._version for m in mask_labels)
+    if _ROWS_CACHE:
+        c_dtype, c_labels, c_versions, rows, offs = _ROWS_CACHE[0]
+        if (c_dtype == dtype and len(c_labels) == len(mask_labels)
+                and all(a is b for a, b in zip(c_labels, mask_labels)) and c_versions == versions):
+            return rows, offs
+    rows = offs = None
+    if mask_labels and len({tuple(m.shape[-2:]) for m in mask_labels}) == 1:
+        rows = torch.cat([m.reshape(-1, *m.shape[-2:]) for m in mask_labels]).to(dtype).float()
+        offs, o = [], 0
+        for m in mask_labels:
+            offs.append(o)
+            o += m.shape[0]
+    _ROWS_CACHE[:] = [(dtype, tuple(mask_labels), versions, rows, offs)]
+    return rows, offs
+
+
+def labels_all(class_labels, device):
+    """Every image's class labels concatenated (int64, on device), built once per set of labels."""
+    versions = tuple(c._version for c in class_labels)
+    if _LABELS_CACHE:
+        c_labels, c_versions, t = _LABELS_CACHE[0]
+        if (len(c_labels) == len(class_labels) and all(a is b for a, b in zip(c_labels, class_labels))
+                and c_versions == versions):
+            return t
+    t = (torch.cat([c.reshape(-1) for c in class_labels]).to(device=device, dtype=torch.long) if class_labels
+         else torch.zeros((0,), dtype=torch.long, device=device))
+    _LABELS_CACHE[:] = [(tuple(class_labels), versions, t)]
+    return t
+
+
+def topk_indices(unc, k):
+    """``torch.topk(unc, k, dim=1, sorted=False)[1]`` as a set: rgbd_topk_rows (one LDS radix
+    select per row, every element above the k-th largest and then the lowest-index ties, in
+    increasing index order).  SORTED_TOPK, or rows longer than the kernel's LDS holds, take
+    torch.topk itself."""
+    N, n = unc.shape
+    L = _lib.lib()
+    if SORTED_TOPK or n > L.rgbd_topk_rows_max_n() or k > n or k <= 0:
+        return torch.topk(unc, k=k, dim=1, sorted=SORTED_TOPK)[1]
+    u = unc.float().contiguous()
+    idx = torch.empty((N, k), dtype=torch.long, device=unc.device)
+    check(L.rgbd_topk_rows(_p(u), N, n, k, _p(idx), _stream(unc.device)), "rgbd_topk_rows")
+    return idx
 
 
 def point_sample(maps: torch.Tensor, coords: torch.Tensor) -> torch.Tensor:
@@ -111,7 +168,47 @@ def match_costs(matcher, masks_queries_logits, class_queries_logits, mask_labels
     """The matcher's cost matrices of every image ([Q, T_b] each), as
     Mask2FormerHungarianMatcher.forward builds them (:445-470): one ``torch.rand(1, P, 2)`` per
     image in image order, then the point sampling and the pair-wise CE / dice reduction on the
-    GPU (all images' costs in one launch)."""
+    GPU.  Batched: one softmax over all images (row-wise, the same rows), every image's targets
+    sampled against its own points in one launch (the cached target rows: the labels rounded to
+    the logits' dtype, as ``.to(pred)``), and the class cost read from the softmax inside the
+    cost kernel — a handful of launches per output instead of several per image."""
+    B, Q, h, w = masks_queries_logits.shape
+    P = matcher.num_points
+    dev = masks_queries_logits.device
+    rows, _ = target_rows(mask_labels, masks_queries_logits.dtype)
+    if rows is None:
+        return _match_costs_per_image(matcher, masks_queries_logits, class_queries_logits, mask_labels, class_labels)
+    probs = class_queries_logits.softmax(-1).float().contiguous()
+    pts = torch.cat([torch.rand(1, P, 2, device=dev) for _ in range(B)])
+    toff, coff, set_of_map = [0], [0], []
+    for i in range(B):
+        T = mask_labels[i].shape[0]
+        toff.append(toff[-1] + T)
+        coff.append(coff[-1] + Q * T)
+        set_of_map += [i] * T
+    pred = _sample(masks_queries_logits.reshape(B * Q, h, w), pts)
+    if toff[-1]:
+        tgt = torch.empty((toff[-1], P), dtype=torch.float32, device=dev)
+        th, tw = rows.shape[-2:]
+        check(_lib.lib().rgbd_point_sample_sets(RGBD_F32, _p(rows), toff[-1], th, tw, _p(pts.contiguous()),
+                                                _p(device_const(set_of_map, torch.int32, dev)), P, _p(tgt),
+                                                _stream(dev)), "rgbd_point_sample_sets")
+    else:
+        tgt = torch.zeros((1, P), device=dev)
+    labels = labels_all(class_labels, dev)
+    if labels.numel() == 0:
+        labels = torch.zeros((1,), dtype=torch.long, device=dev)
+    cost = torch.empty((max(coff[-1], 1),), dtype=torch.float32, device=dev)
+    toff_t = device_const(toff, torch.int32, dev)
+    coff_t = device_const(coff[:-1], torch.int64, dev)
+    check(_lib.lib().rgbd_match_cost_probs(_p(pred), B, Q, P, _p(tgt), _p(toff_t), _p(probs), probs.shape[-1],
+                                           _p(labels), _p(coff_t), float(matcher.cost_mask), float(matcher.cost_class),
+                                           float(matcher.cost_dice), _p(cost), _stream(dev)), "rgbd_match_cost_probs")
+    return [cost[coff[i]:coff[i + 1]].view(Q, toff[i + 1] - toff[i]) for i in range(B)]
+
+
+def _match_costs_per_image(matcher, masks_queries_logits, class_queries_logits, mask_labels, class_labels):
+    """match_costs with the targets cast and sampled image by image (images of different sizes)."""
     B, Q, h, w = masks_queries_logits.shape
     P = matcher.num_points
     dev = masks_queries_logits.device
@@ -175,30 +272,47 @@ class HipMask2FormerLoss(Mask2FormerLoss):
         return torch.clamp(num_masks, min=1)
 
     def _target_rows(self, mask_labels, dtype):
-        """Every image's target masks cast like the reference (``.to(pred_masks)``), as float32
-        rows [sum T, H, W] and their image offsets — built once per set of labels (the final and
-        the nine auxiliary outputs share them), None when the images differ in size (then the
-        reference's zero-padded batch is used)."""
-        # the cache holds the label tensors themselves and matches them by identity: while they
-        # are cached their storage cannot be freed, so a later batch's labels can never reuse the
-        # same addresses and be mistaken for them (a (data_ptr, _version) key could be)
-        cached = getattr(self, "_rgbd_targets", None)
-        if cached is not None:
-            c_dtype, c_labels, c_versions, rows, offs = cached
-            if (c_dtype == dtype and len(c_labels) == len(mask_labels)
-                    and all(a is b for a, b in zip(c_labels, mask_labels))
-                    and c_versions == tuple(m._version for m in mask_labels)):
-                return rows, offs
-        rows = offs = None
-        if mask_labels and len({tuple(m.shape[-2:]) for m in mask_labels}) == 1:
-            rows = torch.cat([m.reshape(-1, *m.shape[-2:]) for m in mask_labels]).to(dtype).float()
-            offs, o = [], 0
-            for m in mask_labels:
-                offs.append(o)
-                o += m.shape[0]
-        self._rgbd_targets = (dtype, tuple(mask_labels), tuple(m._version for m in mask_labels),
-                              rows, offs)
-        return rows, offs
+        return target_rows(mask_labels, dtype)
+
+    def _get_predictions_permutation_indices(self, indices):
+        """(:642-646) from the batched assignment's concatenated indices: the image index of
+        every match is a cached constant of the per-image counts, the query indices a view."""
+        if isinstance(indices, LsaResult) and indices.rows_all is not None:
+            dev = indices.rows_all.device
+            batch = device_const([i for i, n in enumerate(indices.counts) for _ in range(n)] or [0], torch.long, dev)
+            return batch[:len(indices.rows_all)], indices.rows_all
+        return super()._get_predictions_permutation_indices(indices)
+
+    def _target_flat(self, indices, offs, dev):
+        """Row index of every match's target among all images' targets (image offset + column)."""
+        if isinstance(indices, LsaResult) and indices.cols_all is not None:
+            shift = device_const([offs[i] for i, n in enumerate(indices.counts) for _ in range(n)] or [0],
+                                 torch.long, dev)
+            return indices.cols_all + shift[:len(indices.cols_all)]
+        return (torch.cat([j.to(dev) + offs[i] for i, (_, j) in enumerate(indices)]) if indices else
+                torch.zeros((0,), dtype=torch.long, device=dev))
+
+    def loss_labels(self, class_queries_logits, class_labels, indices):
+        """Mask2FormerLoss.loss_labels (:548-578) with the matched targets' classes gathered from
+        the concatenated labels in one index (the reference: one gather per image + cat) and
+        scattered into the no-object fill by flat index (the matches are distinct)."""
+        if not (isinstance(indices, LsaResult) and indices.rows_all is not None):
+            return super().loss_labels(class_queries_logits, class_labels, indices)
+        pred_logits = class_queries_logits
+        batch_size, num_queries, _ = pred_logits.shape
+        criterion = nn.CrossEntropyLoss(weight=self.empty_weight)
+        dev = pred_logits.device
+        offs, o = [], 0
+        for c in class_labels:
+            offs.append(o)
+            o += c.shape[0]
+        target_classes_o = labels_all(class_labels, dev).index_select(0, self._target_flat(indices, offs, dev))
+        target_classes = torch.full((batch_size, num_queries), fill_value=self.num_labels, dtype=torch.int64,
+                                    device=dev)
+        b_idx, q_idx = self._get_predictions_permutation_indices(indices)
+        target_classes.view(-1).index_copy_(0, b_idx * num_queries + q_idx, target_classes_o)
+        loss_ce = criterion(pred_logits.transpose(1, 2), target_classes)
+        return {"loss_cross_entropy": loss_ce}
 
     def loss_masks(self, masks_queries_logits, mask_labels, indices, num_masks):
         src_idx = self._get_predictions_permutation_indices(indices)
@@ -207,8 +321,7 @@ class HipMask2FormerLoss(Mask2FormerLoss):
         rows, offs = self._target_rows(mask_labels, masks_queries_logits.dtype)
         if rows is not None:
             dev = masks_queries_logits.device
-            tflat = torch.cat([j.to(dev) + offs[i] for i, (_, j) in enumerate(indices)]) if indices else \
-                torch.zeros((0,), dtype=torch.long, device=dev)
+            tflat = self._target_flat(indices, offs, dev)
             target_masks = rows.index_select(0, tflat)  # float32, already rounded to the logits' dtype
         else:
             tgt_idx = self._get_targets_permutation_indices(indices)
@@ -232,7 +345,7 @@ class HipMask2FormerLoss(Mask2FormerLoss):
             # of the selection (~2.4 ms per whole-model step, rocprim merge sort) is skipped
             # deliberate deviation: unsorted; SORTED_TOPK restores the reference's
             # sorted selection for parity runs (the same set up to ties, the reference's order)
-            idx = torch.topk(unc, k=k, dim=1, sorted=SORTED_TOPK)[1]
+            idx = topk_indices(unc, k)
             shift = n_over * torch.arange(N, dtype=torch.long, device=pred_masks.device)
             idx += shift[:, None]
             coords = coords.view(-1, 2)[idx.view(-1), :].view(N, k, 2)

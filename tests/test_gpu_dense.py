@@ -210,6 +210,59 @@ def test_layernorm_fwd_bwd(dt, C, rows):
     assert _rel(ln.bias.grad, b64.grad) < 1e-5
 
 
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1)])
+@pytest.mark.parametrize("M,N,K,act", [(4096, 256, 1024, 3), (800, 256, 256, 0), (37, 130, 72, 0), (50400, 256, 256, 0)])
+def test_gemm_bf16_rounded_float32_store(a_t, b_t, M, N, K, act):
+    """c_f32 = 2: a bf16 GEMM's results rounded to bf16 and stored as float32 (the dX a float32
+    input receives under autocast) — the bits of the bf16 output widened, R read in bf16."""
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn((K, M) if a_t else (M, K), generator=g).to(DEV, torch.bfloat16)
+    B = torch.randn((K, N) if b_t else (N, K), generator=g).to(DEV, torch.bfloat16)
+    R = torch.randn((M, N), generator=g).to(DEV, torch.bfloat16) if act == 3 else None
+    ref = dense.gemm(A, B, a_t, b_t, M, N, K, act=act, R=R)
+    got = dense.gemm(A, B, a_t, b_t, M, N, K, act=act, R=R, c_f32=2)
+    assert got.dtype == torch.float32 and torch.equal(got, ref.float())
+
+
+@pytest.mark.parametrize("xdt,rdt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.bfloat16)], ids=["f32+f32", "f32+bf16", "bf16+bf16"])
+@pytest.mark.parametrize("C,rows", [(256, 800), (256, 50400), (96, 333), (1536, 70)])
+def test_add_layernorm_fused(xdt, rdt, C, rows):
+    """LN(x + r) in one kernel (the decoder / encoder layers' post-norm residual): the sum in the
+    promoted dtype exactly as torch's add (bitwise), the norm and every gradient against float64
+    (x and r each get the sum's gradient in their own dtype)."""
+    from rgbd_amd import dense
+    g = torch.Generator(device="cpu").manual_seed(C + rows)
+    ln = dense.HipLayerNorm(C, eps=1e-5).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(C, generator=g))
+        ln.bias.copy_(torch.randn(C, generator=g))
+    x = (torch.randn((rows, C), generator=g) * 3 + 1).to(DEV, xdt).requires_grad_()
+    r = torch.randn((rows, C), generator=g).to(DEV, rdt).requires_grad_()
+    y = dense.add_layer_norm(x, r, ln)
+    sdt = torch.promote_types(xdt, rdt)
+    assert y.dtype == sdt
+    gy = torch.randn(y.shape, generator=g).to(DEV, sdt)
+    y.backward(gy)
+    assert x.grad.dtype == xdt and r.grad.dtype == rdt
+    s = (x.detach() + r.detach())  # torch's add: the sum the norm must see
+    s64 = s.double().requires_grad_()
+    w64, b64 = ln.weight.detach().double().requires_grad_(), ln.bias.detach().double().requires_grad_()
+    y64 = torch.nn.functional.layer_norm(s64, (C,), w64, b64, 1e-5)
+    y64.backward(gy.double())
+    tol = 1e-5 if sdt == torch.float32 else 1e-2
+    assert _rel(y, y64) < tol
+    assert _rel(x.grad, s64.grad) < tol * 2 + (1e-2 if xdt == torch.bfloat16 else 0)
+    assert _rel(r.grad, s64.grad) < tol * 2 + (1e-2 if rdt == torch.bfloat16 else 0)
+    assert _rel(ln.weight.grad, w64.grad) < 1e-5
+    assert _rel(ln.bias.grad, b64.grad) < 1e-5
+    # the unfused path (torch add + the HIP norm) gives the same bits
+    ln2 = dense.HipLayerNorm(C, eps=1e-5).to(DEV)
+    ln2.load_state_dict(ln.state_dict())
+    assert torch.equal(dense.layer_norm(s, ln2), y.detach())
+
+
 def _grads(m):
     return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
 

@@ -109,7 +109,7 @@ def test_bf16_train_mode_batchnorm_stats(H, W):
 @pytest.mark.parametrize("H,W", [(240, 320), (90, 125), (480, 640), (7, 9)])
 def test_bf16_stem_bn_batch_stats_exact(H, W):
     """The stem BatchNorms' batch statistics in bf16 train mode come from the moments of the 7x7x3
-    depth windows (k_stem_lag / k_stem_frame / k_stem_s2 / k_stem_bn: lag correlations + border
+    depth windows (k_stem_lag with its border workgroups / k_stem_sums / k_stem_s2 / k_stem_bn: lag correlations + border
     corrections, double), not from a pass over the stem — against float64 arithmetic on the same
     bf16-rounded depth and stem weights: batch mean to 2e-6 of the channel scale, unbiased
     variance to 2e-5 relative (read back from the running-stat update, momentum 0.1).  (7, 9):

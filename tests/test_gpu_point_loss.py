@@ -167,3 +167,84 @@ def test_loss_all_images_empty_matches_reference():
     sum(h.values()).backward()
     sum(r.values()).backward()
     assert torch.equal(mh.grad, mr.grad)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_match_costs_batched_equals_per_image(dt):
+    """The batched cost construction (one softmax, every image's targets against its own points
+    in one launch from the cached target rows, the class cost read from the softmax in the cost
+    kernel) gives the bits of the image-by-image construction, with an image without targets."""
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerHungarianMatcher
+    m = Mask2FormerHungarianMatcher(cost_class=2.0, cost_mask=5.0, cost_dice=5.0, num_points=12544)
+    masks, classes, ml, cl = _case(7, B=4, counts=(5, 0, 23, 1))
+    masks = masks.to(dt)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dt == torch.bfloat16):
+        torch.manual_seed(3)
+        ref = point_loss._match_costs_per_image(m, masks, classes, ml, cl)
+        torch.manual_seed(3)
+        got = point_loss.match_costs(m, masks, classes, ml, cl)
+    assert len(ref) == len(got)
+    for r, h in zip(ref, got):
+        assert r.shape == h.shape and torch.equal(r, h)
+
+
+def test_whole_loss_matches_reference():
+    """Mask2FormerLoss.forward end to end (matcher, batched permutation indices, loss_labels from
+    the concatenated labels, loss_masks) vs HF's, every term and the gradients."""
+    from transformers import Mask2FormerConfig
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerLoss
+    cfg = Mask2FormerConfig(num_labels=48)
+    wd = {"loss_cross_entropy": 2.0, "loss_mask": 5.0, "loss_dice": 5.0}
+    ref_loss, hip_loss = Mask2FormerLoss(cfg, weight_dict=wd).to(DEV), Mask2FormerLoss(cfg, weight_dict=wd).to(DEV)
+    holder = torch.nn.Module()
+    holder.criterion = hip_loss
+    assert point_loss.install(holder) == 1
+    masks, classes, ml, cl = _case(12, B=3, L=49, counts=(4, 0, 9))
+    mr, mh = masks.clone().requires_grad_(True), masks.clone().requires_grad_(True)
+    cr, ch = classes.clone().requires_grad_(True), classes.clone().requires_grad_(True)
+    torch.manual_seed(13)
+    r = ref_loss(mr, cr, ml, cl)
+    torch.manual_seed(13)
+    h = holder.criterion(mh, ch, ml, cl)
+    assert set(r) == set(h)
+    for k in r:
+        assert abs(float(h[k]) - float(r[k])) <= 1e-5 * abs(float(r[k])) + 1e-7, (k, float(h[k]), float(r[k]))
+    sum(r.values()).backward()
+    sum(h.values()).backward()
+    assert _rel(mh.grad, mr.grad) <= 1e-4
+    assert _rel(ch.grad, cr.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("N,n,k", [(41, 37632, 9408), (3, 1000, 1), (5, 777, 777), (2, 37632, 30000), (0, 100, 5)])
+@pytest.mark.parametrize("kind", ["distinct", "ties", "nan"])
+def test_topk_rows_matches_torch_set(N, n, k, kind):
+    """rgbd_topk_rows (loss_masks' uncertainty selection) gives torch.topk's index set when the
+    values are distinct, and with ties at the k-th value the same multiset of values, taking the
+    lowest indices among the tied (NaN ranks largest, as in torch)."""
+    g = torch.Generator(device=DEV).manual_seed(n + k)
+    x = -torch.rand((N, n), generator=g, device=DEV).abs()
+    if kind == "ties":
+        x = torch.round(x * 8) / 8
+    if kind == "nan" and N:
+        x[:, ::97] = float("nan")
+    got = point_loss.topk_indices(x, k)
+    assert got.shape == (N, k) and got.dtype == torch.long
+    if N == 0:
+        return
+    ref_v, ref_i = torch.topk(x, k, dim=1, sorted=True)
+    gs = torch.sort(got, dim=1).values
+    assert torch.equal(gs, got)                                        # increasing index order
+    assert (gs[:, 1:] != gs[:, :-1]).all()                             # distinct
+    gv = torch.gather(x, 1, got)
+    assert torch.equal(torch.sort(gv, dim=1, descending=True).values.nan_to_num(9.0),
+                       ref_v.nan_to_num(9.0))                          # the same values
+    if kind == "distinct":
+        assert torch.equal(gs, torch.sort(ref_i, dim=1).values)
+    else:  # the tied k-th value: the lowest indices
+        kth = ref_v[:, -1:]
+        for r in range(N):
+            if torch.isnan(kth[r]).item():
+                continue
+            tied = torch.nonzero(x[r] == kth[r]).flatten()
+            taken = got[r][x[r][got[r]] == kth[r]]
+            assert torch.equal(taken, tied[:len(taken)])

@@ -1,9 +1,11 @@
 """Where the whole-model step's torch glue comes from (diagnostic): one eager bf16 training step of
 bench.full_model's model under torch.profiler with stacks and shapes, and for every aten op with
 device time (copies, adds, fills, index ops, ...) the call site that issued it — the innermost
-frame of this repository or transformers for forward ops, the autograd node for backward ops —
+line of this repository or transformers for forward ops (a TorchFunctionMode wraps each call in
+a record_function: this torch build records no Python stacks), the autograd node for backward ops —
 with its launches, device time and input shapes.  Writes the table to argv[1] (default stdout)."""
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -11,7 +13,8 @@ _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [_R]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from torch.profiler import ProfilerActivity, profile  # noqa: E402
+from torch.overrides import TorchFunctionMode  # noqa: E402
+from torch.profiler import ProfilerActivity, profile, record_function  # noqa: E402
 
 import _rgbd_import  # noqa: E402,F401
 from rgbd_amd import init as winit, ops, synthetic  # noqa: E402
@@ -45,8 +48,40 @@ def step():
 for _ in range(3):
     step()
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
-    step()
+OURS = ("rgb-d-instance-segmentation_amd", "rgbd_amd", "transformers/", "bench.py")
+
+
+class SiteMode(TorchFunctionMode):
+    """Wraps every torch function called from this repository or transformers (forward) in a
+    record_function named after the calling line, so the profiler's tree carries the call site
+    (this torch build records no Python stacks)."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        f = sys._getframe(1)
+        while f is not None:
+            fn = f.f_code.co_filename
+            if any(o in fn for o in OURS) and "/tools/" not in fn:
+                short = re.sub(r"^.*?(rgb-d-instance-segmentation_amd|transformers)/", "", fn)
+                with record_function(f"@{short}:{f.f_lineno}"):
+                    return func(*args, **kwargs)
+            f = f.f_back
+        return func(*args, **kwargs)
+
+
+def step_sited():
+    pv = ops.assemble_pixel_values(depth, rgb)
+    with SiteMode(), torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(pixel_values=pv, mask_labels=mask_labels, class_labels=class_labels)
+    out.loss.backward()
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+
+
+step_sited()
+torch.cuda.synchronize()
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    step_sited()
     torch.cuda.synchronize()
 
 GLUE = ("aten::copy_", "aten::add", "aten::add_", "aten::mul", "aten::mul_", "aten::fill_", "aten::zero_",
@@ -61,16 +96,15 @@ GLUE = ("aten::copy_", "aten::add", "aten::add_", "aten::mul", "aten::mul_", "at
 
 
 def site(ev):
-    """The innermost repository / transformers frame of a forward op, or the autograd node."""
+    """The autograd node of a backward op; for a forward op the innermost call-site range."""
     p = ev
     while p is not None:
         if p.name.startswith("autograd::engine::evaluate_function"):
             return "bwd " + p.name.split(": ", 1)[-1]
+        if p.name.startswith("@"):
+            return p.name[1:]
         p = p.cpu_parent
-    for fr in ev.stack or []:
-        if (fr.startswith(_R) and "/tools/" not in fr) or "transformers/" in fr:
-            return fr.replace(_R + "/", "")
-    return "(no python frame)"
+    return "(no call site)"
 
 
 def device_us(ev):
