@@ -411,6 +411,16 @@ int rgbd_msda_bwd(int dtype, const void* value, int B, int L, const int* shapes_
                   int P, const float* loc, const float* attw, const void* gout, float* gvalue, float* gloc,
                   float* gattw, void* stream);
 
+/* The sampling locations of two-coordinate reference points (:990-994) in one pass:
+ *   loc[b][q][h][l][p][c] = ref[b][q][l][c] + off[b][q][h][l][p][c] / norm[l][c]
+ * ref float32 [B][Q][L][2]; off dtype [B][Q][NH][L][P][2] (the sampling-offset projection);
+ * norm float32 [L][2] = (W_l, H_l); the division in off's dtype (torch's bf16 / int64), the sum
+ * in float32.  _bwd: goff = (gloc rounded to off's dtype) / norm, rounded to off's dtype. */
+int rgbd_msda_locations(int dtype, const float* ref, const void* off, const float* norm, int B, int Q, int NH,
+                        int L, int P, float* loc, void* stream);
+int rgbd_msda_locations_bwd(int dtype, const float* gloc, const float* norm, int B, int Q, int NH, int L, int P,
+                            void* goff, void* stream);
+
 /* ---------------------------------------------------------------- f3 matcher assignment
  * Replaces scipy.optimize.linear_sum_assignment(cost_matrix.cpu()) in
  * Mask2FormerHungarianMatcher.forward (transformers 5.15 modeling_mask2former.py:474): a batch of
@@ -550,12 +560,19 @@ int rgbd_layernorm_fwd(int x_dtype, const void* x, const float* gamma, const flo
  *   pass: s = x + r in float32 arithmetic, rounded to the promoted dtype (float32 when either is
  *   float32, else bf16), written to s_out (the input the backward's rgbd_layernorm_bwd takes),
  *   and y = LN(s) as rgbd_layernorm_fwd; y2 (optional, bf16) receives y rounded to bf16 as well —
- *   the operand the consuming bf16 GEMMs would otherwise cast from y.  C % 4 == 0, C <= 1536,
- *   16-byte aligned x / r / s_out / y / y2 (RGBD_E_SHAPE otherwise: the caller adds and
- *   normalises separately). */
+ *   the operand the consuming bf16 GEMMs would otherwise cast from y.  clamp > 0: y =
+ *   clamp(LN(s), -clamp, clamp) (the encoder layer's clamp in training, :1094-1097; NaN kept).
+ *   C % 4 == 0, C <= 1536, 16-byte aligned x / r / s_out / y / y2 (RGBD_E_SHAPE otherwise: the
+ *   caller adds and normalises separately).
+ * rgbd_add_layernorm_bwd: rgbd_layernorm_bwd on s with the forward's clamp undone in the
+ *   gradient (zero where clamp(y) != y, y recomputed in the forward's order) and ds_bf16
+ *   (optional) = ds rounded to bf16 — the gradient the bf16 branch r receives. */
 int rgbd_add_layernorm_fwd(int x_dtype, const void* x, int r_dtype, const void* r, const float* gamma,
-                           const float* beta, int rows, int C, float eps, int y_dtype, void* s_out, void* y,
-                           void* y2, float* mean, float* rstd, void* stream);
+                           const float* beta, int rows, int C, float eps, float clamp, int y_dtype, void* s_out,
+                           void* y, void* y2, float* mean, float* rstd, void* stream);
+int rgbd_add_layernorm_bwd(int s_dtype, const void* s_in, int dy_dtype, const void* dy, const float* gamma,
+                           const float* beta, const float* mean, const float* rstd, int rows, int C, float clamp,
+                           void* ds, void* ds_bf16, float* dgamma, float* dbeta, void* ws, void* stream);
 size_t rgbd_layernorm_bwd_workspace_size(int rows, int C);
 int rgbd_layernorm_bwd(int x_dtype, const void* x, int dy_dtype, const void* dy, const float* gamma,
                        const float* mean, const float* rstd, int rows, int C, void* dx, float* dgamma,

@@ -94,6 +94,8 @@ SIGNATURES = {
     "rgbd_point_losses_bwd": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_msda_fwd": (_I, [_I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rgbd_msda_bwd": (_I, [_I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "rgbd_msda_locations": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "rgbd_msda_locations_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "rgbd_lsa_lds_bytes": (_SZ, [_I, _I]),
     "rgbd_lsa_batch": (_I, [_I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "rgbd_mask_logits": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
@@ -110,7 +112,10 @@ SIGNATURES = {
     "rgbd_colsum_workspace_size": (_SZ, [_I, _I]),
     "rgbd_colsum": (_I, [_I, _P, _I, _I, _LL, _P, _P, _P]),
     "rgbd_layernorm_fwd": (_I, [_I, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P]),
-    "rgbd_add_layernorm_fwd": (_I, [_I, _P, _I, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P, _P, _P]),
+    "rgbd_add_layernorm_fwd": (_I, [_I, _P, _I, _P, _P, _P, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P, _P, _P,
+                                    _P, _P, _P]),
+    "rgbd_add_layernorm_bwd": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P, _P, _P, _P,
+                                    _P]),
     "rgbd_layernorm_bwd_workspace_size": (_SZ, [_I, _I]),
     "rgbd_layernorm_bwd": (_I, [_I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_groupnorm_workspace_size": (_SZ, [_I, _I]),

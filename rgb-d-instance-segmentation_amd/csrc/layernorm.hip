@@ -213,9 +213,10 @@ __global__ __launch_bounds__(256) void k_ln_fwd_v(const void* __restrict__ x, co
 template <typename TX, typename TR, typename TS, typename TY, int T, int NCH>
 __global__ __launch_bounds__(256) void k_add_ln_fwd_v(const void* __restrict__ x, const void* __restrict__ r,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                      int rows, int C, float eps, void* __restrict__ s_out,
-                                                      void* __restrict__ y, bf16_t* __restrict__ y2,
-                                                      float* __restrict__ mean, float* __restrict__ rstd) {
+                                                      int rows, int C, float eps, float clampc,
+                                                      void* __restrict__ s_out, void* __restrict__ y,
+                                                      bf16_t* __restrict__ y2, float* __restrict__ mean,
+                                                      float* __restrict__ rstd) {
   const int j = threadIdx.x % T;
   const int row = blockIdx.x * (256 / T) + threadIdx.x / T;
   const bool live = row < rows;
@@ -259,6 +260,10 @@ __global__ __launch_bounds__(256) void k_add_ln_fwd_v(const void* __restrict__ x
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         o[e] = (v[k][e] - mu) * rs * (gamma ? gamma[c + e] : 1.f) + (beta ? beta[c + e] : 0.f);
+      if (clampc > 0.f) {  // torch.clamp(y, -c, c): NaN stays NaN
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = o[e] < -clampc ? -clampc : (o[e] > clampc ? clampc : o[e]);
+      }
       st4<TY>(y, base + c, o);
       if (y2) st4<bf16_t>(y2, base + c, o);
     }
@@ -272,11 +277,19 @@ __global__ __launch_bounds__(256) void k_add_ln_fwd_v(const void* __restrict__ x
 // dx per row; dgamma / dbeta partials per block: part[blk][2][C].  A block's groups take rows
 // r0 + g, r0 + g + G, ... (G = groups per block), two rows per group in flight; the groups'
 // partials are summed in a fixed order through LDS: deterministic for a given shape.
+// Ext (rgbd_add_layernorm_bwd): with clampc > 0 the upstream gradient is masked where the
+// forward's clamp(y, -c, c) was not the identity (y recomputed from x, mean, rstd, gamma, beta in
+// the forward's operation order: the same bits); dx2 (optional) receives dx rounded to bf16.
+struct LnBwdExt {
+  const float* beta;
+  float clampc;
+  bf16_t* dx2;
+};
 template <typename TX, typename TD, int T, int NCH>
 __global__ __launch_bounds__(256) void k_ln_bwd_v(const void* __restrict__ x, const void* __restrict__ dy,
                                                   const float* __restrict__ gamma, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, int rows, int C, int rb,
-                                                  void* __restrict__ dx, float* __restrict__ part) {
+                                                  void* __restrict__ dx, float* __restrict__ part, LnBwdExt ext) {
   constexpr int G = 256 / T;
   extern __shared__ float red[];  // [G][2][C]
   const int j = threadIdx.x % T, grp = threadIdx.x / T;
@@ -320,6 +333,11 @@ __global__ __launch_bounds__(256) void k_ln_bwd_v(const void* __restrict__ x, co
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float xh = (xv[u][k][e] - mu) * rs;
+          if (ext.clampc > 0.f) {  // torch.clamp's backward: the gradient where min <= y <= max
+            const int c = 4 * (j + T * k) + e;
+            const float yv = xh * gm[k][e] + (c < C && ext.beta ? ext.beta[c] : 0.f);
+            if (!(yv >= -ext.clampc && yv <= ext.clampc)) dv[u][k][e] = 0.f;
+          }
           const float g = dv[u][k][e] * gm[k][e];
           xv[u][k][e] = xh;
           if (ok) {
@@ -340,6 +358,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd_v(const void* __restrict__ x, co
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = rs * (dv[u][k][e] * gm[k][e] - ma - xv[u][k][e] * mb);
           st4<TX>(dx, base + c, o);
+          if (ext.dx2) st4<bf16_t>(ext.dx2, base + c, o);
         }
       }
     }
@@ -424,38 +443,38 @@ void lnv_fwd(const void* x, const float* gamma, const float* beta, int rows, int
 }
 template <typename TX, typename TD, int T, int NCH>
 void lnv_bwd_launch(const void* x, const void* dy, const float* gamma, const float* mean, const float* rstd, int rows,
-                    int C, void* dx, float* part, hipStream_t s) {
+                    int C, void* dx, float* part, hipStream_t s, LnBwdExt ext = LnBwdExt{nullptr, 0.f, nullptr}) {
   const int rb = lnv_rows_per_block(rows);
   const size_t smem = (size_t)(256 / T) * 2 * C * sizeof(float);
   hipLaunchKernelGGL((k_ln_bwd_v<TX, TD, T, NCH>), dim3(ceil_div(rows, rb)), dim3(256), smem, s, x, dy, gamma, mean,
-                     rstd, rows, C, rb, dx, part);
+                     rstd, rows, C, rb, dx, part, ext);
 }
 template <typename TX, typename TD>
 void lnv_bwd(const void* x, const void* dy, const float* gamma, const float* mean, const float* rstd, int rows, int C,
-             void* dx, float* part, hipStream_t s) {
+             void* dx, float* part, hipStream_t s, LnBwdExt ext = LnBwdExt{nullptr, 0.f, nullptr}) {
   const int T = lnv_group(C), nch = ceil_div(C / 4, T);
-  if (T == 16) lnv_bwd_launch<TX, TD, 16, 1>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
-  else if (T == 32) lnv_bwd_launch<TX, TD, 32, 1>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
-  else if (nch == 1) lnv_bwd_launch<TX, TD, 64, 1>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
-  else if (nch == 2) lnv_bwd_launch<TX, TD, 64, 2>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
-  else if (nch == 3) lnv_bwd_launch<TX, TD, 64, 3>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
-  else if (nch == 4) lnv_bwd_launch<TX, TD, 64, 4>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
-  else if (nch == 5) lnv_bwd_launch<TX, TD, 64, 5>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
-  else lnv_bwd_launch<TX, TD, 64, 6>(x, dy, gamma, mean, rstd, rows, C, dx, part, s);
+  if (T == 16) lnv_bwd_launch<TX, TD, 16, 1>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
+  else if (T == 32) lnv_bwd_launch<TX, TD, 32, 1>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
+  else if (nch == 1) lnv_bwd_launch<TX, TD, 64, 1>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
+  else if (nch == 2) lnv_bwd_launch<TX, TD, 64, 2>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
+  else if (nch == 3) lnv_bwd_launch<TX, TD, 64, 3>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
+  else if (nch == 4) lnv_bwd_launch<TX, TD, 64, 4>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
+  else if (nch == 5) lnv_bwd_launch<TX, TD, 64, 5>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
+  else lnv_bwd_launch<TX, TD, 64, 6>(x, dy, gamma, mean, rstd, rows, C, dx, part, s, ext);
 }
 
 template <typename TX, typename TR, typename TS, typename TY, int T, int NCH>
 void add_lnv_launch(const void* x, const void* r, const float* gamma, const float* beta, int rows, int C, float eps,
-                    void* s_out, void* y, bf16_t* y2, float* mean, float* rstd, hipStream_t s) {
+                    float clampc, void* s_out, void* y, bf16_t* y2, float* mean, float* rstd, hipStream_t s) {
   hipLaunchKernelGGL((k_add_ln_fwd_v<TX, TR, TS, TY, T, NCH>), dim3(ceil_div(rows, 256 / T)), dim3(256), 0, s, x, r,
-                     gamma, beta, rows, C, eps, s_out, y, y2, mean, rstd);
+                     gamma, beta, rows, C, eps, clampc, s_out, y, y2, mean, rstd);
 }
 template <typename TX, typename TR, typename TS, typename TY>
 void add_lnv(const void* x, const void* r, const float* gamma, const float* beta, int rows, int C, float eps,
-             void* s_out, void* y, bf16_t* y2, float* mean, float* rstd, hipStream_t s) {
+             float clampc, void* s_out, void* y, bf16_t* y2, float* mean, float* rstd, hipStream_t s) {
   const int T = lnv_group(C), nch = ceil_div(C / 4, T);
 #define ADD_LNV(TT, NN) \
-  add_lnv_launch<TX, TR, TS, TY, TT, NN>(x, r, gamma, beta, rows, C, eps, s_out, y, y2, mean, rstd, s)
+  add_lnv_launch<TX, TR, TS, TY, TT, NN>(x, r, gamma, beta, rows, C, eps, clampc, s_out, y, y2, mean, rstd, s)
   if (T == 16) ADD_LNV(16, 1);
   else if (T == 32) ADD_LNV(32, 1);
   else if (nch == 1) ADD_LNV(64, 1);
@@ -521,8 +540,8 @@ int rgbd_layernorm_fwd(int x_dtype, const void* x, const float* gamma, const flo
 }
 
 int rgbd_add_layernorm_fwd(int x_dtype, const void* x, int r_dtype, const void* r, const float* gamma,
-                           const float* beta, int rows, int C, float eps, int y_dtype, void* s_out, void* y,
-                           void* y2, float* mean, float* rstd, void* stream) {
+                           const float* beta, int rows, int C, float eps, float clamp, int y_dtype, void* s_out,
+                           void* y, void* y2, float* mean, float* rstd, void* stream) {
   RGBD_REQUIRE(x && r && s_out && y && mean && rstd && rows > 0 && C > 0, RGBD_E_ARG);
   RGBD_REQUIRE(lnv_ok(C), RGBD_E_SHAPE);
   RGBD_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)r & 15) == 0 && ((uintptr_t)s_out & 15) == 0 &&
@@ -536,15 +555,42 @@ int rgbd_add_layernorm_fwd(int x_dtype, const void* x, int r_dtype, const void* 
 #define ADD_LN(TX, TR, TS)                                                                      \
   do {                                                                                          \
     if (y_dtype == RGBD_BF16)                                                                   \
-      add_lnv<TX, TR, TS, bf16_t>(x, r, gamma, beta, rows, C, eps, s_out, y, (bf16_t*)y2, mean, rstd, s); \
+      add_lnv<TX, TR, TS, bf16_t>(x, r, gamma, beta, rows, C, eps, clamp, s_out, y, (bf16_t*)y2, mean, rstd, s); \
     else                                                                                        \
-      add_lnv<TX, TR, TS, float>(x, r, gamma, beta, rows, C, eps, s_out, y, (bf16_t*)y2, mean, rstd, s);  \
+      add_lnv<TX, TR, TS, float>(x, r, gamma, beta, rows, C, eps, clamp, s_out, y, (bf16_t*)y2, mean, rstd, s);  \
   } while (0)
   if (x_dtype == RGBD_F32 && r_dtype == RGBD_F32) ADD_LN(float, float, float);
   else if (x_dtype == RGBD_F32) ADD_LN(float, bf16_t, float);
   else if (r_dtype == RGBD_F32) ADD_LN(bf16_t, float, float);
   else ADD_LN(bf16_t, bf16_t, bf16_t);
 #undef ADD_LN
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+int rgbd_add_layernorm_bwd(int s_dtype, const void* s_in, int dy_dtype, const void* dy, const float* gamma,
+                           const float* beta, const float* mean, const float* rstd, int rows, int C, float clamp,
+                           void* ds, void* ds_bf16, float* dgamma, float* dbeta, void* ws, void* stream) {
+  RGBD_REQUIRE(s_in && dy && mean && rstd && ds && dgamma && dbeta && ws && rows > 0 && C > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(lnv_ok(C), RGBD_E_SHAPE);
+  RGBD_REQUIRE(((uintptr_t)s_in & 15) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)ds & 15) == 0 &&
+                   ((uintptr_t)ds_bf16 & 15) == 0,
+               RGBD_E_SHAPE);
+  RGBD_REQUIRE((s_dtype == RGBD_F32 || s_dtype == RGBD_BF16) && (dy_dtype == RGBD_F32 || dy_dtype == RGBD_BF16),
+               RGBD_E_DTYPE);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)ws;
+  const LnBwdExt ext{beta, clamp, (bf16_t*)ds_bf16};
+  if (s_dtype == RGBD_BF16) {
+    if (dy_dtype == RGBD_BF16) lnv_bwd<bf16_t, bf16_t>(s_in, dy, gamma, mean, rstd, rows, C, ds, part, s, ext);
+    else lnv_bwd<bf16_t, float>(s_in, dy, gamma, mean, rstd, rows, C, ds, part, s, ext);
+  } else {
+    if (dy_dtype == RGBD_BF16) lnv_bwd<float, bf16_t>(s_in, dy, gamma, mean, rstd, rows, C, ds, part, s, ext);
+    else lnv_bwd<float, float>(s_in, dy, gamma, mean, rstd, rows, C, ds, part, s, ext);
+  }
+  RGBD_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_ln_param_reduce_v, dim3(ceil_div(2 * C, 64)), dim3(1024), 0, s, part,
+                     ceil_div(rows, lnv_rows_per_block(rows)), C, dgamma, dbeta);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -365,6 +365,35 @@ int launch_bwd(const void* value, const MsdaLevels& lv, int B, int S, int Q, int
   return RGBD_OK;
 }
 
+// Sampling locations of the two-coordinate reference points (:990-994):
+//   loc[b][q][h][l][p][c] = ref[b][q][l][c] + (off[b][q][h][l][p][c] / norm[l][c])
+// with the division in the offsets' dtype (torch: bf16 / int64 -> bf16, computed in float and
+// rounded), the sum in float32; backward: goff = (float(round(gloc)) / norm) rounded to the offsets'
+// dtype (the add's gradient cast to that dtype, then the division's).
+template <typename T>
+__global__ __launch_bounds__(256) void k_msda_loc(const float* __restrict__ ref, const T* __restrict__ off,
+                                                  const float* __restrict__ norm, long long n, int NH, int L, int P,
+                                                  float* __restrict__ loc) {
+  const long long i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i & 1);
+  const long long j = i >> 1;                        // (b, q, h, l, p)
+  const int l = (int)((j / P) % L);
+  const long long bq = j / ((long long)P * L * NH);
+  const float q = Num<T>::to_f(Num<T>::from_f(Num<T>::to_f(off[i]) / norm[2 * l + c]));
+  loc[i] = ref[(bq * L + l) * 2 + c] + q;
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_msda_loc_bwd(const float* __restrict__ gloc, const float* __restrict__ norm,
+                                                      long long n, int L, int P, T* __restrict__ goff) {
+  const long long i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i & 1);
+  const int l = (int)(((i >> 1) / P) % L);
+  const float g = Num<T>::to_f(Num<T>::from_f(gloc[i]));
+  goff[i] = Num<T>::from_f(g / norm[2 * l + c]);
+}
+
 }  // namespace
 }  // namespace rgbd
 
@@ -420,6 +449,34 @@ extern "C" int rgbd_msda_bwd(int dtype, const void* value, int B, int L, const i
     else r = launch_bwd<bf16_t, 16>(value, lv, B, S, Q, NH, P, loc, attw, gout, gvalue, gloc, gattw, s);
   }
   if (r != RGBD_OK) return r;
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+extern "C" int rgbd_msda_locations(int dtype, const float* ref, const void* off, const float* norm, int B, int Q,
+                                   int NH, int L, int P, float* loc, void* stream) {
+  RGBD_REQUIRE(ref && off && norm && loc && B > 0 && Q > 0 && NH > 0 && L > 0 && P > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  const long long n = (long long)B * Q * NH * L * P * 2;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  if (dtype == RGBD_F32)
+    k_msda_loc<float><<<grid, 256, 0, (hipStream_t)stream>>>(ref, (const float*)off, norm, n, NH, L, P, loc);
+  else
+    k_msda_loc<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>(ref, (const bf16_t*)off, norm, n, NH, L, P, loc);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+extern "C" int rgbd_msda_locations_bwd(int dtype, const float* gloc, const float* norm, int B, int Q, int NH, int L,
+                                       int P, void* goff, void* stream) {
+  RGBD_REQUIRE(gloc && norm && goff && B > 0 && Q > 0 && NH > 0 && L > 0 && P > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  const long long n = (long long)B * Q * NH * L * P * 2;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  if (dtype == RGBD_F32)
+    k_msda_loc_bwd<float><<<grid, 256, 0, (hipStream_t)stream>>>(gloc, norm, n, L, P, (float*)goff);
+  else
+    k_msda_loc_bwd<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>(gloc, norm, n, L, P, (bf16_t*)goff);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

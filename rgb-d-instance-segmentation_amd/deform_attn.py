@@ -16,7 +16,10 @@ from torch import nn
 from transformers.models.mask2former.modeling_mask2former import (
     Mask2FormerPixelDecoderEncoderMultiscaleDeformableAttention as _HFMSDA)
 
-from . import ops
+from . import _lib, ops
+from ._lib import RGBD_BF16, RGBD_F32, check
+
+_CODE = {torch.float32: RGBD_F32, torch.bfloat16: RGBD_BF16}
 
 
 class MSDeformAttnFunction(torch.autograd.Function):
@@ -32,6 +35,35 @@ class MSDeformAttnFunction(torch.autograd.Function):
         value, loc, attw = ctx.saved_tensors
         gv, gl, ga = ops.msda_backward(value, ctx.shapes, loc, attw, gout)
         return gv.to(value.dtype), None, gl.to(ctx.loc_dtype), ga.to(ctx.attw_dtype)
+
+
+class MSDALocationsFunction(torch.autograd.Function):
+    """ref[:, :, None, :, None, :] + offsets / norm[None, None, None, :, None, :] (:990-994) in
+    one kernel (rgbd_msda_locations): the division in the offsets' dtype, the sum in float32, as
+    torch evaluates the expression; its backward forms the offsets' gradient the same way."""
+
+    @staticmethod
+    def forward(ctx, ref, offsets, norm):
+        B, Q, NH, L, P, _ = offsets.shape
+        off = offsets.contiguous()
+        r = ref.detach().float().contiguous()
+        loc = torch.empty(off.shape, dtype=torch.float32, device=off.device)
+        check(_lib.lib().rgbd_msda_locations(_CODE[off.dtype], ops._p(r), ops._p(off), ops._p(norm), B, Q, NH, L, P,
+                                             ops._p(loc), ops._stream(off.device)), "rgbd_msda_locations")
+        ctx.save_for_backward(norm)
+        ctx.dims, ctx.off_dtype = (B, Q, NH, L, P), off.dtype
+        return loc
+
+    @staticmethod
+    def backward(ctx, gloc):
+        (norm,) = ctx.saved_tensors
+        B, Q, NH, L, P = ctx.dims
+        g = gloc.float().contiguous()
+        goff = torch.empty(g.shape, dtype=ctx.off_dtype, device=g.device)
+        check(_lib.lib().rgbd_msda_locations_bwd(_CODE[ctx.off_dtype], ops._p(g), ops._p(norm), B, Q, NH, L, P,
+                                                 ops._p(goff), ops._stream(g.device)), "rgbd_msda_locations_bwd")
+        gref = g.sum(dim=(2, 4)) if ctx.needs_input_grad[0] else None
+        return gref, goff, None
 
 
 def multi_scale_deformable_attention(value, value_spatial_shapes, sampling_locations, attention_weights):
@@ -56,7 +88,11 @@ class HipMSDeformAttn(_HFMSDA):
         offsets = self.sampling_offsets(hidden_states).view(B, Q, self.n_heads, self.n_levels, self.n_points, 2)
         weights = self.attention_weights(hidden_states).view(B, Q, self.n_heads, self.n_levels * self.n_points)
         weights = nn.functional.softmax(weights, -1).view(B, Q, self.n_heads, self.n_levels, self.n_points)
-        if reference_points.shape[-1] == 2:
+        if reference_points.shape[-1] == 2 and offsets.dtype in (torch.float32, torch.bfloat16):
+            norm = ops.device_const([[float(w), float(h)] for h, w in spatial_shapes_list], torch.float32,
+                                    reference_points.device)
+            loc = MSDALocationsFunction.apply(reference_points, offsets, norm)
+        elif reference_points.shape[-1] == 2:
             norm = ops.device_const([[w, h] for h, w in spatial_shapes_list], torch.long, reference_points.device)
             loc = reference_points[:, :, None, :, None, :] + offsets / norm[None, None, None, :, None, :]
         elif reference_points.shape[-1] == 4:

@@ -268,12 +268,15 @@ class LayerNormFunction(torch.autograd.Function):
 
 
 class AddLayerNormFunction(torch.autograd.Function):
-    """y = LayerNorm(x + r): the sum and the norm in one kernel (rgbd_add_layernorm_fwd), the sum
-    kept for the backward; its gradient goes to x and r in their own dtypes (what autograd's add
-    backward hands each: the same values, cast once)."""
+    """y = LayerNorm(x + r) (then clamp(y, -clamp, clamp) when clamp > 0): the sum, the norm and
+    the clamp in one kernel (rgbd_add_layernorm_fwd), the sum kept for the backward; its gradient
+    goes to x and r in their own dtypes (what autograd's add backward hands each: the same values,
+    the bf16 one written by the backward kernel itself).  With ``twin`` a second, non-
+    differentiable output holds y in bf16 (the consuming GEMMs' operand)."""
 
     @staticmethod
-    def forward(ctx, x, r, gamma, beta, eps, y_dtype, twin):
+    def forward(ctx, x, r, gamma, beta, eps, y_dtype, twin, clamp):
+        ctx.set_materialize_grads(False)
         C = x.shape[-1]
         x2 = x.reshape(-1, C).contiguous()
         r2 = r.reshape(-1, C).contiguous()
@@ -289,10 +292,11 @@ class AddLayerNormFunction(torch.autograd.Function):
         g32 = None if gamma is None else gamma.detach().float().contiguous()
         b32 = None if beta is None else beta.detach().float().contiguous()
         check(_lib.lib().rgbd_add_layernorm_fwd(_CODE[x2.dtype], _p(x2), _CODE[r2.dtype], _p(r2), _p(g32), _p(b32),
-                                                rows, C, float(eps), _CODE[y_dtype], _p(s), _p(y), _p(y2), _p(mean),
-                                                _p(rstd), _stream(x.device)), "rgbd_add_layernorm_fwd")
-        ctx.save_for_backward(s, g32, mean, rstd)
-        ctx.dtypes, ctx.has_g, ctx.has_b = (x.dtype, r.dtype), gamma is not None, beta is not None
+                                                rows, C, float(eps), float(clamp), _CODE[y_dtype], _p(s), _p(y),
+                                                _p(y2), _p(mean), _p(rstd), _stream(x.device)),
+              "rgbd_add_layernorm_fwd")
+        ctx.save_for_backward(s, g32, b32, mean, rstd)
+        ctx.dtypes, ctx.has_g, ctx.has_b, ctx.clamp = (x.dtype, r.dtype), gamma is not None, beta is not None, clamp
         if y2 is None:
             y2 = torch.empty((0,), dtype=torch.bfloat16, device=x.device)
         ctx.mark_non_differentiable(y2)
@@ -300,22 +304,30 @@ class AddLayerNormFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, _gy2):
-        s, g32, mean, rstd = ctx.saved_tensors
+        s, g32, b32, mean, rstd = ctx.saved_tensors
         rows, C = s.shape
+        if gy is None:
+            return None, None, None, None, None, None, None, None
         g2 = gy.reshape(rows, C)
         if g2.dtype not in _CODE:
             g2 = g2.float()
         g2 = g2.contiguous()
+        if g2.data_ptr() % 16:
+            g2 = g2.clone()
         ds = torch.empty_like(s)
+        twin = s.dtype == torch.float32 and ctx.dtypes[1] == torch.bfloat16
+        ds2 = torch.empty((rows, C), dtype=torch.bfloat16, device=s.device) if twin else None
         dg = torch.empty((C,), dtype=torch.float32, device=s.device)
         db = torch.empty_like(dg)
         L = _lib.lib()
         ws = _workspace(s.device, L.rgbd_layernorm_bwd_workspace_size(rows, C), "ln_bwd")
-        check(L.rgbd_layernorm_bwd(_CODE[s.dtype], _p(s), _CODE[g2.dtype], _p(g2), _p(g32), _p(mean), _p(rstd),
-                                   rows, C, _p(ds), _p(dg), _p(db), _p(ws), _stream(s.device)), "rgbd_layernorm_bwd")
+        check(L.rgbd_add_layernorm_bwd(_CODE[s.dtype], _p(s), _CODE[g2.dtype], _p(g2), _p(g32), _p(b32), _p(mean),
+                                       _p(rstd), rows, C, float(ctx.clamp), _p(ds), _p(ds2), _p(dg), _p(db), _p(ws),
+                                       _stream(s.device)), "rgbd_add_layernorm_bwd")
         ds = ds.view(gy.shape)
-        return (ds.to(ctx.dtypes[0]), ds.to(ctx.dtypes[1]), dg if ctx.has_g else None, db if ctx.has_b else None,
-                None, None, None)
+        dr = ds2.view(gy.shape) if twin else ds.to(ctx.dtypes[1])
+        return (ds.to(ctx.dtypes[0]), dr, dg if ctx.has_g else None, db if ctx.has_b else None,
+                None, None, None, None)
 
 
 class GroupNormFunction(torch.autograd.Function):
@@ -393,10 +405,11 @@ def layer_norm(x, ln):
     return LayerNormFunction.apply(x, ln.weight, ln.bias, ln.eps, y_dtype)
 
 
-def add_layer_norm(x, r, ln):
-    """ln(x + r) for the post-norm residual of a covered layer: one fused kernel where the shapes
-    allow it (HipLayerNorm's coverage, C % 4 == 0, 16-byte aligned rows), else the add and the
-    module."""
+def add_layer_norm(x, r, ln, clamp=False):
+    """ln(x + r) for the post-norm residual of a covered layer (with ``clamp`` then
+    clamp(., -c, c), c = finfo(dtype).max - 1000, the encoder layer's training clamp): one fused
+    kernel where the shapes allow it (HipLayerNorm's coverage, C % 4 == 0), else the add, the
+    module and the clamp."""
     C = x.shape[-1]
     if (isinstance(ln, HipLayerNorm) and x.is_cuda and r.is_cuda and x.shape == r.shape and x.numel() > 0
             and len(ln.normalized_shape) == 1 and ln.normalized_shape[0] == C and C % 4 == 0 and C <= 1536
@@ -406,11 +419,16 @@ def add_layer_norm(x, r, ln):
         # under bf16 autocast the consumers are bf16 GEMMs: the kernel also writes y in bf16 and
         # _rows serves that instead of casting y again (the same RNE rounding of the same float)
         twin = amp and y_dtype == torch.float32
-        y, y2 = AddLayerNormFunction.apply(x, r, ln.weight, ln.bias, ln.eps, y_dtype, twin)
+        c = torch.finfo(y_dtype).max - 1000 if clamp else 0.0
+        y, y2 = AddLayerNormFunction.apply(x, r, ln.weight, ln.bias, ln.eps, y_dtype, twin, float(c))
         if twin:
             y._rgbd_rows = ((y._version, torch.bfloat16), y2)
         return y
-    return ln(x + r)
+    y = ln(x + r)
+    if clamp:
+        c = torch.finfo(y.dtype).max - 1000
+        y = torch.clamp(y, min=-c, max=c)
+    return y
 
 
 def _cuda_ok(x):
@@ -508,13 +526,11 @@ def _make_encoder_layer_class():
             hidden_states = add_layer_norm(residual, hidden_states, self.self_attn_layer_norm)
             residual = hidden_states
             hidden_states = ffn(hidden_states, self.fc1, self.fc2)
-            hidden_states = add_layer_norm(residual, hidden_states, self.final_layer_norm)
-            if self.training:
-                # the reference clamps when any value is non-finite (:1094-1097, a host sync per
-                # layer); clamping unconditionally is the same map (identity on finite float32,
-                # +-inf -> +-(max - 1000) = +-max, NaN kept) without the sync
-                c = torch.finfo(hidden_states.dtype).max - 1000
-                hidden_states = torch.clamp(hidden_states, min=-c, max=c)
+            # in training the reference clamps when any value is non-finite (:1094-1097, a host
+            # sync per layer); clamping unconditionally is the same map (identity on finite
+            # float32, +-inf -> +-(max - 1000) = +-max, NaN kept) without the sync, done by the
+            # fused norm kernel (its backward masks the gradient where the clamp was not the identity)
+            hidden_states = add_layer_norm(residual, hidden_states, self.final_layer_norm, clamp=self.training)
             outputs = (hidden_states,)
             if output_attentions:
                 outputs += (attn_weights.transpose(1, 0),)

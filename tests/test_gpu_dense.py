@@ -263,6 +263,51 @@ def test_add_layernorm_fused(xdt, rdt, C, rows):
     assert torch.equal(dense.layer_norm(s, ln2), y.detach())
 
 
+@pytest.mark.parametrize("rdt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_add_layernorm_clamp(rdt):
+    """The encoder layer's training clamp folded into the fused norm: values that overflow to
+    +-inf (one channel with gamma 1e38, large there in every third row) come out as +-max, and the
+    backward zeroes the gradient exactly there (torch.clamp's backward) — the clamp pattern and
+    values against torch's float32 add + layer_norm + clamp, the gradients against float64."""
+    from rgbd_amd import dense
+    C, rows = 256, 333
+    g = torch.Generator(device="cpu").manual_seed(5)
+    ln = dense.HipLayerNorm(C, eps=1e-5).to(DEV)
+    with torch.no_grad():
+        w = torch.randn(C, generator=g)
+        w[7] = 1e38  # channel 7 overflows where its normalised value exceeds ~3.4
+        ln.weight.copy_(w)
+        ln.bias.copy_(torch.randn(C, generator=g))
+    x0 = torch.randn((rows, C), generator=g)
+    x0[::3, 7] = 10.0 * torch.sign(torch.randn(len(range(0, rows, 3)), generator=g))
+    x = x0.to(DEV).requires_grad_()
+    r = torch.randn((rows, C), generator=g).to(DEV, rdt).requires_grad_()
+    y = dense.add_layer_norm(x, r, ln, clamp=True)
+    c = torch.finfo(torch.float32).max - 1000
+    assert torch.isfinite(y).all() and int((y.abs() == torch.finfo(torch.float32).max).sum()) >= rows // 3
+    gy = torch.randn(y.shape, generator=g).to(DEV)
+    y.backward(gy)
+    # reference: torch's float32 forward decides where the clamp acts (the same overflow pattern as
+    # the kernel, checked below); the gradient is the float64 LayerNorm backward of the masked dy
+    s32 = x.detach() + r.detach()
+    w, b = ln.weight.detach(), ln.bias.detach()
+    y32 = torch.nn.functional.layer_norm(s32, (C,), w, b, 1e-5)
+    big = torch.finfo(torch.float32).max
+    yr = torch.clamp(y32, min=-c, max=c)
+    assert torch.equal(y.detach().abs() == big, yr.abs() == big)
+    fin = torch.isfinite(y32)
+    assert _rel(y.detach()[fin], yr[fin]) < 1e-5
+    s64 = s32.double().requires_grad_()
+    w64, b64 = w.double().requires_grad_(), b.double().requires_grad_()
+    torch.nn.functional.layer_norm(s64, (C,), w64, b64, 1e-5).backward(gy.double() * fin.double())
+    # the clamped rows (every third): there the mask removes channel 7's 1e38-weighted gradient and
+    # the input gradients are ordinary numbers (elsewhere they are ~1e35-1e38)
+    assert torch.isfinite(x.grad[::3]).all() and float(x.grad[::3].abs().max()) < 1e6
+    assert _rel(x.grad[::3], s64.grad[::3]) < 1e-4
+    assert _rel(r.grad[::3].float(), s64.grad[::3]) < (1e-4 if rdt == torch.float32 else 1e-2)
+    assert _rel(ln.bias.grad, b64.grad) < 1e-5
+
+
 def _grads(m):
     return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
 
