@@ -35,6 +35,7 @@ the timed region.
 import argparse
 import ctypes
 import json
+import re
 import os
 import socket
 import subprocess
@@ -95,8 +96,9 @@ def profile_avg_ns(kernel, default_shape):
         with open(path, newline="") as f:
             for row in csv.DictReader(f):
                 name = row.get("Name", "").replace("(anonymous namespace)::", "")
-                base = name.split("(")[0].split()[-1].split("::")[-1] if name.split("(")[0].split() else ""
-                if base == kernel or base.split("<")[0] == kernel:
+                head = re.sub(r"<.*>", "", name.split("(")[0])  # template arguments may hold spaces
+                base = head.split()[-1].split("::")[-1] if head.split() else ""
+                if base == kernel:
                     best = (float(row["AverageNs"]), str(path.relative_to(REPO)), int(row["Calls"]))
                     break
     return best

@@ -26,7 +26,7 @@ planes, _, _ = synthetic.make_batch(3, 8, 480, 640)
 d = torch.from_numpy(planes[:, 3:6].copy()).cuda()
 L = _lib.lib()
 ROUNDS, ITERS = 6, 8
-MODES = (0, 3, 7, 15)
+MODES = tuple(int(m) for m in sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 3, 7, 15)
 res = {md: [] for md in MODES}
 for rnd in range(ROUNDS + 1):
     for md in MODES:
