@@ -396,6 +396,18 @@ int rgbd_point_losses(const float* logits, const float* labels, int N, int P, fl
 int rgbd_point_losses_bwd(const float* logits, const float* labels, int N, int P, const float* sums,
                           const float* g_ce, const float* g_dice, float* glogits, void* stream);
 
+/* The decoder memory of one feature level (Mask2FormerTransformerModule.forward :2095-2109):
+ *   out[p][b][c] = proj[b][c][p] + embed[c]   (proj dtype [B][C][HW]: the input projection's
+ *   output; embed float32 [C]: level_embed.weight[level]; out float32 [HW][B][C]: the permuted
+ *   memory, contiguous).  _bwd from g float32 [HW][B][C]: dproj[b][c][p] = g[p][b][c] in proj's
+ *   dtype, dembed[c] = sum over pixels and images (fixed order; ws:
+ *   rgbd_level_memory_workspace_size bytes). */
+size_t rgbd_level_memory_workspace_size(int B, int C, int HW);
+int rgbd_level_memory_fwd(int dtype, const void* proj, const float* embed, int B, int C, int HW, float* out,
+                          void* stream);
+int rgbd_level_memory_bwd(int dtype, const float* g, int B, int C, int HW, void* dproj, float* dembed, void* ws,
+                          void* stream);
+
 /* ---------------------------------------------------------------- f2 deformable attention
  * Replaces multi_scale_deformable_attention (transformers 5.15 modeling_mask2former.py:798-837),
  * the core of each pixel-decoder encoder layer (:1011).  value: dtype [B][S][NH][D] with

@@ -94,6 +94,9 @@ SIGNATURES = {
     "rgbd_point_losses_bwd": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "rgbd_msda_fwd": (_I, [_I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "rgbd_msda_bwd": (_I, [_I, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "rgbd_level_memory_workspace_size": (_SZ, [_I, _I, _I]),
+    "rgbd_level_memory_fwd": (_I, [_I, _P, _P, _I, _I, _I, _P, _P]),
+    "rgbd_level_memory_bwd": (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P]),
     "rgbd_msda_locations": (_I, [_I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "rgbd_msda_locations_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "rgbd_lsa_lds_bytes": (_SZ, [_I, _I]),

@@ -224,6 +224,67 @@ __global__ __launch_bounds__(256) void k_mask_attention(const T* __restrict__ lo
   }
 }
 
+// The masked-attention decoder's memory of one feature level (Mask2FormerTransformerModule.forward,
+// modeling_mask2former.py:2095-2109): proj [B][C][HW] (the input projection's output) + level
+// embedding e[c], then permuted to [HW][B][C] — written in that layout directly, in float32 (the
+// promoted dtype of proj + e), so the decoder's key / value projections read contiguous rows.
+// Tiles of 64 pixels x 64 channels of one image, transposed through LDS.  Backward: dproj[b][c][p]
+// = g[p][b][c] in proj's dtype, and per (image, pixel tile) the channel sums of g (summed by
+// k_level_embed_sum over the partials in a fixed order: d e).
+constexpr int LM_T = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void k_level_mem_fwd(const T* __restrict__ proj, const float* __restrict__ e, int B,
+                                                       int C, int HW, float* __restrict__ out) {
+  __shared__ float t[LM_T][LM_T + 1];
+  const int p0 = blockIdx.x * LM_T, c0 = blockIdx.y * LM_T, b = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int ci = ty; ci < LM_T; ci += 4) {  // coalesced along pixels
+    const int c = c0 + ci, p = p0 + tx;
+    t[ci][tx] = (c < C && p < HW) ? Num<T>::to_f(proj[((long long)b * C + c) * HW + p]) : 0.f;
+  }
+  __syncthreads();
+  const float ev = c0 + tx < C ? e[c0 + tx] : 0.f;
+#pragma unroll 4
+  for (int pi = ty; pi < LM_T; pi += 4) {  // coalesced along channels
+    const int p = p0 + pi, c = c0 + tx;
+    if (p < HW && c < C) out[((long long)p * B + b) * C + c] = t[tx][pi] + ev;
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_level_mem_bwd(const float* __restrict__ g, int B, int C, int HW,
+                                                       T* __restrict__ dproj, float* __restrict__ part) {
+  __shared__ float t[LM_T][LM_T + 1];
+  __shared__ float cs[4][LM_T];
+  const int p0 = blockIdx.x * LM_T, c0 = blockIdx.y * LM_T, b = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  float acc = 0.f;
+#pragma unroll 4
+  for (int pi = ty; pi < LM_T; pi += 4) {  // coalesced along channels; channel sums in pixel order
+    const int p = p0 + pi, c = c0 + tx;
+    const float v = (p < HW && c < C) ? g[((long long)p * B + b) * C + c] : 0.f;
+    t[tx][pi] = v;
+    acc += v;
+  }
+  cs[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && c0 + tx < C)
+    part[((long long)b * gridDim.x + blockIdx.x) * C + c0 + tx] = (cs[0][tx] + cs[1][tx]) + (cs[2][tx] + cs[3][tx]);
+#pragma unroll 4
+  for (int ci = ty; ci < LM_T; ci += 4) {  // coalesced along pixels
+    const int c = c0 + ci, p = p0 + tx;
+    if (c < C && p < HW) dproj[((long long)b * C + c) * HW + p] = Num<T>::from_f(t[ci][tx]);
+  }
+}
+__global__ __launch_bounds__(256) void k_level_embed_sum(const float* __restrict__ part, int n, int C,
+                                                         float* __restrict__ de) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += part[(long long)i * C + c];
+  de[c] = s;
+}
+
 }  // namespace
 }  // namespace rgbd
 
@@ -267,6 +328,38 @@ extern "C" int rgbd_mask_attention(int dtype, const void* logits, int B, int Q, 
     k_mask_attention<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)logits, B * Q, Q, H, W, th, tw, heads, rh, rw, attn);
   else
     return RGBD_E_DTYPE;
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+extern "C" size_t rgbd_level_memory_workspace_size(int B, int C, int HW) {
+  return (size_t)B * ((HW + LM_T - 1) / LM_T) * C * sizeof(float);
+}
+
+extern "C" int rgbd_level_memory_fwd(int dtype, const void* proj, const float* embed, int B, int C, int HW, float* out,
+                                     void* stream) {
+  RGBD_REQUIRE(proj && embed && out && B > 0 && C > 0 && HW > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  const dim3 grid((HW + LM_T - 1) / LM_T, (C + LM_T - 1) / LM_T, B);
+  if (dtype == RGBD_F32)
+    k_level_mem_fwd<float><<<grid, 256, 0, (hipStream_t)stream>>>((const float*)proj, embed, B, C, HW, out);
+  else
+    k_level_mem_fwd<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)proj, embed, B, C, HW, out);
+  RGBD_CHECK_LAUNCH();
+  return RGBD_OK;
+}
+
+extern "C" int rgbd_level_memory_bwd(int dtype, const float* g, int B, int C, int HW, void* dproj, float* dembed,
+                                     void* ws, void* stream) {
+  RGBD_REQUIRE(g && dproj && dembed && ws && B > 0 && C > 0 && HW > 0, RGBD_E_ARG);
+  RGBD_REQUIRE(dtype == RGBD_F32 || dtype == RGBD_BF16, RGBD_E_DTYPE);
+  const dim3 grid((HW + LM_T - 1) / LM_T, (C + LM_T - 1) / LM_T, B);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RGBD_F32)
+    k_level_mem_bwd<float><<<grid, 256, 0, s>>>(g, B, C, HW, (float*)dproj, (float*)ws);
+  else
+    k_level_mem_bwd<bf16_t><<<grid, 256, 0, s>>>(g, B, C, HW, (bf16_t*)dproj, (float*)ws);
+  k_level_embed_sum<<<(C + 255) / 256, 256, 0, s>>>((const float*)ws, B * (int)grid.x, C, dembed);
   RGBD_CHECK_LAUNCH();
   return RGBD_OK;
 }

@@ -111,3 +111,63 @@ def test_mask_ops_reject_bad_input():
         ops.mask_logits(emb[:, :, :32], pix)
     with pytest.raises(RuntimeError):
         ops.mask_logits(emb.cpu(), pix.cpu())
+
+
+@gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("B,C,H,W", [(8, 256, 60, 80), (2, 256, 15, 20), (3, 192, 7, 9)])
+def test_level_memory_matches_torch(dt, B, C, H, W):
+    """One level's decoder memory (input projection output + level embedding, permuted to
+    [HW, B, C], :2102-2109): the values bitwise, the projection's gradient bitwise, the
+    embedding's gradient (a sum over pixels and images in another order) to 1e-5."""
+    g = torch.Generator(device="cuda").manual_seed(C + H)
+    proj = torch.randn((B, C, H, W), generator=g, device="cuda").to(dt)
+    emb = torch.randn((4, C), generator=g, device="cuda")
+    p1, e1 = proj.clone().requires_grad_(), emb.clone().requires_grad_()
+    want = (p1.flatten(2) + e1[2][None, :, None]).permute(2, 0, 1)
+    gy = torch.randn(want.shape, generator=g, device="cuda")
+    want.backward(gy)
+    p2, e2 = proj.clone().requires_grad_(), emb.clone().requires_grad_()
+    got = mask_predictor.level_memory(p2, e2[2])
+    got.backward(gy)
+    assert got.dtype == want.dtype and got.shape == want.shape and got.is_contiguous()
+    assert torch.equal(got, want)
+    assert p2.grad.dtype == dt and torch.equal(p2.grad, p1.grad)
+    assert float((e2.grad - e1.grad).abs().max()) <= 1e-5 * float(e1.grad.abs().max())
+
+
+@gpu
+def test_transformer_module_matches_hf():
+    """HipTransformerModule (the fused level memory) inside the installed decoder gives the HF
+    module's outputs, with every parameter's gradient, on a C2-shaped call (float32)."""
+    import copy
+    from transformers.models.mask2former.modeling_mask2former import Mask2FormerTransformerModule
+    from rgbd_amd import dense, masked_attention
+    from rgbd_amd.config import standard_config
+    torch.manual_seed(3)
+    cfg = standard_config(48)
+    ref = Mask2FormerTransformerModule(in_features=256, config=cfg).cuda().train()
+    hip = copy.deepcopy(ref)
+    mask_predictor.install(hip)
+    assert type(hip) is mask_predictor.HipTransformerModule
+    feats = [torch.randn((2, 256, h, w), device="cuda") for h, w in ((8, 10), (15, 20), (30, 40))]
+    mf = torch.randn((2, 256, 60, 80), device="cuda")
+    outs = []
+    for m in (ref, hip):
+        fs = [f.clone().requires_grad_() for f in feats]
+        o = m(fs, mf)
+        loss = (sum(m_.float().square().mean() for m_ in o.masks_queries_logits)
+                + sum(h.float().square().mean() for h in o.intermediate_hidden_states))
+        loss.backward()
+        outs.append((torch.stack([m_.detach() for m_ in o.masks_queries_logits]), [f.grad for f in fs],
+                     {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}))
+    (a, fa, ga), (b, fb, gb) = outs
+    assert float((a - b).abs().max()) <= 1e-5 * float(a.abs().max())
+    for x, y in zip(fa, fb):
+        assert float((x - y).abs().max()) <= 1e-4 * float(x.abs().max())
+    assert ga.keys() == gb.keys()
+    # floored at 1e-6 of the largest gradient: the self-attention key biases' gradients are zero in
+    # exact arithmetic (softmax is invariant to a per-query constant) and rounding noise in both arms
+    scale = max(float(v.abs().max()) for v in ga.values())
+    for n in ga:
+        assert float((ga[n] - gb[n]).abs().max()) <= 1e-4 * float(ga[n].abs().max()) + 1e-6 * scale, n
