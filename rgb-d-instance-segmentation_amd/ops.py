@@ -5,6 +5,7 @@ memory is plumbing), passes raw pointers + the current HIP stream to the C ABI a
 ``RgbdHipError`` on a non-zero return.  Nothing here synchronises with the device except
 ``decode_info`` (explicitly a host read-back for tests/diagnostics).
 """
+import collections
 import contextlib
 import threading
 import ctypes
@@ -69,7 +70,12 @@ def _workspace(dev, nbytes: int, tag: str, zeroed: bool = False):
 # blocking host->device copy — torch synchronises the stream behind a pageable copy, draining the
 # GPU queue — and cannot be captured into a graph.  They are the same numbers step after step,
 # so each distinct value is copied once and the device tensor reused (read-only by contract).
-_consts = {}
+# Values that change with the batch (the matcher's per-image target counts) would make the table
+# grow without bound over a training run, so it is least-recently-used with a cap; a constant a
+# captured graph reads is pinned (the graph holds its address, not a reference).
+_consts = collections.OrderedDict()
+_pinned = set()
+_CONST_CAP = 512
 
 
 def capturing() -> bool:
@@ -93,11 +99,19 @@ def device_const(values, dtype, device):
         device = torch.device("cuda", torch.cuda.current_device())
     key = (_freeze(values), dtype, device)
     t = _consts.get(key)
+    cap = device.type == "cuda" and capturing()
     if t is None:
-        if device.type == "cuda" and capturing():
+        if cap:
             raise RuntimeError("device_const: a new constant during graph capture (run the step eagerly first)")
         t = torch.tensor(values, dtype=dtype).to(device)
         _consts[key] = t
+        if len(_consts) > _CONST_CAP:
+            for old in [k for k in _consts if k not in _pinned][:len(_consts) - _CONST_CAP]:
+                del _consts[old]
+    else:
+        _consts.move_to_end(key)
+    if cap:
+        _pinned.add(key)
     return t
 
 

@@ -56,3 +56,23 @@ def test_host_constants_only_in_the_entering_thread(monkeypatch):
         t.join()
     assert seen == [(1, 2)]
     assert other["r"] != "const"
+
+
+def test_device_const_table_is_bounded_and_keeps_pinned_entries():
+    """Per-batch values (the matcher's target counts) must not grow the table without bound: it
+    is least-recently-used with a cap, and entries a captured graph read are never evicted."""
+    ops._consts.clear()
+    ops._pinned.clear()
+    keep = ops.device_const([12345, 1], torch.long, "cpu")
+    key = next(iter(ops._consts))
+    ops._pinned.add(key)  # as if read during a capture
+    hot = ops.device_const([7, 7, 7], torch.int32, "cpu")
+    for i in range(ops._CONST_CAP + 100):
+        ops.device_const([i, i + 1], torch.long, "cpu")
+        if i % 50 == 0:
+            assert ops.device_const([7, 7, 7], torch.int32, "cpu") is hot  # recently used: kept
+    assert len(ops._consts) <= ops._CONST_CAP
+    assert ops.device_const([12345, 1], torch.long, "cpu") is keep
+    assert ops.device_const([0, 1], torch.long, "cpu").tolist() == [0, 1]  # evicted, rebuilt
+    ops._consts.clear()
+    ops._pinned.clear()
