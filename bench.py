@@ -851,7 +851,11 @@ def main():
     timings = read_timings(L)
     L.rgbd_timing_enable(0)
     use_graph = bool(args.graph) and world == 1
-    dt = timed(make_step(ctx, world, graph=True), args.steps, args.warmup, world) if use_graph else dt_eager
+    # the line's number: the captured step at N = 1; at N > 1 the eager step timed again with the
+    # per-kernel HIP events off (they cost ~0.3 ms of host time per step: 3.23 vs 2.92 ms,
+    # profiles/r05_v2/prof_host.txt)
+    dt = (timed(make_step(ctx, world, graph=True), args.steps, args.warmup, world) if use_graph
+          else timed(step, args.steps, 1, world))
     # the same captured step software-pipelined across batches (make_parts ``pipeline``)
     dt_pipe = timed(make_step(ctx, world, graph=True, pipeline=True), args.steps, args.warmup, world) \
         if use_graph and args.pipeline_report else None
@@ -904,6 +908,8 @@ def main():
                       "model's gradients (37.3 M parameters, most of them outside this path)"),
         "graph": use_graph,
         "eager_img_s": round(B * world * args.steps / dt_eager, 2),
+        "eager_note": ("eager_img_s: the eager pass with the per-kernel HIP events on (the kernel_ms figures); at "
+                       "N > 1 the line's value is the eager step timed again with them off"),
         "pipelined_img_s": None if dt_pipe is None else round(B * world * args.steps / dt_pipe, 2),
         "pipelined_note": ("the captured step with the next batch's ratio predictor on a second stream beside this "
                            "batch's DSAM / DGGM forward, backward and AdamW (bitwise the sequential schedule's "
