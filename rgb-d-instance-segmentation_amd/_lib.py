@@ -144,6 +144,7 @@ DIAG_SIGNATURES = {
     "rgbd_debug_dsam_stamps": (_I, [_P, _I]),
     "rgbd_debug_stem_lag_stamps": (_I, [_P]),
     "rgbd_debug_conv5_mode": (_I, [_I]),
+    "rgbd_debug_dsam_mode": (_I, [_I]),
 }
 
 _lib = None

@@ -1381,8 +1381,11 @@ __device__ __forceinline__ void ld_stamp(unsigned long long* st, int f) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// NODMA (diagnostic build only, rgbd_debug_dsam_mode; timing only, the results are garbage):
+// bit 0 drops the in-loop B copies, bit 1 the in-loop A copies, bit 2 the per-step barrier (each
+// wave still waits for its own copies), bit 3 the fragment reads (constant MFMA operands).
 // One (tile, chunk) item of k_dsam_lds for N tile ntile (of ntn).
-template <int KC>
+template <int KC, int NODMA = 0>
 __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, int chunk, int ntile, int ntn,
                                         int* next_s, int nitems, unsigned long long* st = nullptr) {
   using Cfg = LdCfg<KC>;
@@ -1472,7 +1475,7 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   const int s0 = (int)((long long)chunk * total / nc), s1 = (int)((long long)(chunk + 1) * total / nc);
   const int nst = s1 - s0;
   if (st && threadIdx.x == 0) st[6] = (unsigned long long)(nst | (nc << 16) | (chunk << 24));
-  auto issue = [&](int slot, int s) {  // step s (absolute)
+  auto issue = [&](int slot, int s, bool inloop = false) {  // step s (absolute)
     const int e = __builtin_amdgcn_readfirstlane(steptab[s]);
     const int t = e & 15, cg = (e >> 4) & 255, code = e >> 12;
     int ky, kx, dy, dx;
@@ -1482,8 +1485,10 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     const uint32_t rc = (t < 8 ? alo >> (4 * t) : ahi) & 15u;
     const bool live = ((aval >> t) & 1u) && rc == (uint32_t)code;
     const bf16_t* asrc = live ? xp + (long long)(aorg + delta) * a.C + cg * 32 * KC + achk : zrow;
+    if (!((NODMA & 2) && inloop))
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) dma_lds16(live ? asrc + kc * 32 : zrow, sb + kc * LD_A1 + wave * 1024);
+      for (int kc = 0; kc < KC; ++kc) dma_lds16(live ? asrc + kc * 32 : zrow, sb + kc * LD_A1 + wave * 1024);
+    if ((NODMA & 1) && inloop) return;
     const long long tstride = (long long)a.N * 32;  // one (code, tap, chunk) tile, elements
     const bf16_t* bsrc = wp + ((long long)(code * 9 + tap) * (a.C / 32) + cg * KC) * tstride + (long long)n0 * 32 + lane * 8;
 #pragma unroll
@@ -1507,11 +1512,18 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
   ld_stamp(st, 2);
 #pragma unroll 1
   for (int s = 0; s < nst; ++s) {
-    if (s + S - 1 < nst) issue((s + S - 1) % S, s0 + s + S - 1);
+    if (s + S - 1 < nst) issue((s + S - 1) % S, s0 + s + S - 1, true);
     const char* sa = smem + (s % S) * Cfg::STAGE;
     // fragments of chunk kc+1 are read while chunk kc's 12 MFMAs run
     Frag<bf16_t> fa[2][4], fb[2][3];
     auto rd = [&](int kc, int q) {
+      if constexpr (NODMA & 8) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) fa[q][mi].v = make_uint4(lane, kc, s, mi);
+#pragma unroll
+        for (int nj = 0; nj < 3; ++nj) fb[q][nj].v = make_uint4(nj, lane, kc, s);
+        return;
+      }
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int row = wm * 64 + 16 * mi + r;
@@ -1534,7 +1546,8 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     }
     // own DMA of step s+1 landed (only later steps' may stay in flight), LDS reads done, barrier
     const int ahead = (nst - 1 < s + S - 1 ? nst - 1 : s + S - 1) - (s + 1);
-    if (ahead <= 0) vm_wait_barrier<0>();
+    if constexpr (NODMA & 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if (ahead <= 0) vm_wait_barrier<0>();
     else vm_wait_barrier_dyn(ahead * cnt);
   }
   ld_stamp(st, 3);
@@ -1778,10 +1791,15 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
 // Persistent: grid (workgroups, N tiles); each workgroup takes the next item of its N tile's list
 // from a counter (items differ up to ~5x in steps: dynamic assignment balances the tail; the
 // multi-chunk reductions stay in chunk order, so results do not depend on who ran what).
-template <int KC, bool STAMPS = false>
+template <int KC, bool STAMPS = false, int NODMA = 0>
 __global__ __launch_bounds__(512, 1) void k_dsam_lds(ConvArgs a) {
   using Cfg = LdCfg<KC>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  if constexpr (NODMA != 0) {  // the ring starts zeroed: slots the modes never fill hold finite values
+    for (int e = threadIdx.x; e < Cfg::S * Cfg::STAGE / 16; e += 512)
+      reinterpret_cast<uint4*>(smem)[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+  }
   int* next_s = (int*)(smem + Cfg::TMASK + 216);  // free bytes behind the per-tap code lists: item, word
   const int nitems = *a.nitems;
   const int ntile = blockIdx.y;
@@ -1815,7 +1833,7 @@ __global__ __launch_bounds__(512, 1) void k_dsam_lds(ConvArgs a) {
     ld_stamp(st, 0);
     if (st && threadIdx.x == 0) st[7] = (unsigned long long)v;
     // next_s is rewritten only after the item's K loop, behind its prologue barrier
-    ld_item<KC>(a, v & 3, v >> 5, (v >> 2) & 7, ntile, gridDim.y, next_s, nitems, st);
+    ld_item<KC, NODMA>(a, v & 3, v >> 5, (v >> 2) & 7, ntile, gridDim.y, next_s, nitems, st);
   }
 }
 
@@ -1906,6 +1924,15 @@ hipError_t plan_convs(int n, const ConvArgs* legs, hipStream_t s) {
 // stamped so far
 unsigned long long* g_ld_stamps = nullptr;
 int g_ld_stamp_cap = 0, g_ld_stamp_n = 0;
+int g_ld_mode = 0;  // rgbd_debug_dsam_mode: NODMA bits of the stamped KC = 3 instantiation
+template <int KC, int M>
+hipError_t launch_ld_stamped(const ConvArgs& c, dim3 grid, hipStream_t s) {
+  static const hipError_t sattr = hipFuncSetAttribute((const void*)k_dsam_lds<KC, true, M>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)LdCfg<KC>::SMEM);
+  if (sattr != hipSuccess) return sattr;
+  k_dsam_lds<KC, true, M><<<grid, 512, LdCfg<KC>::SMEM, s>>>(c);
+  return hipSuccess;
+}
 #endif
 template <int KC>
 hipError_t launch_ld(const ConvArgs& b, dim3 grid, hipStream_t s) {
@@ -1913,14 +1940,21 @@ hipError_t launch_ld(const ConvArgs& b, dim3 grid, hipStream_t s) {
       hipFuncSetAttribute((const void*)k_dsam_lds<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LdCfg<KC>::SMEM);
   if (attr != hipSuccess) return attr;
 #ifdef RGBD_DIAG
-  static const hipError_t sattr = hipFuncSetAttribute((const void*)k_dsam_lds<KC, true>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)LdCfg<KC>::SMEM);
   if (g_ld_stamps && g_ld_stamp_n < g_ld_stamp_cap && grid.x * grid.y <= 256) {
-    if (sattr != hipSuccess) return sattr;
     ConvArgs c = b;
     c.stamps = g_ld_stamps + (size_t)g_ld_stamp_n++ * 256 * LD_STAMP_ITEMS * 8;
-    k_dsam_lds<KC, true><<<grid, 512, LdCfg<KC>::SMEM, s>>>(c);
-    return hipSuccess;
+    if constexpr (KC == 3) {
+      switch (g_ld_mode) {
+        case 1: return launch_ld_stamped<KC, 1>(c, grid, s);
+        case 2: return launch_ld_stamped<KC, 2>(c, grid, s);
+        case 3: return launch_ld_stamped<KC, 3>(c, grid, s);
+        case 7: return launch_ld_stamped<KC, 7>(c, grid, s);
+        case 15: return launch_ld_stamped<KC, 15>(c, grid, s);
+        case 8: return launch_ld_stamped<KC, 8>(c, grid, s);
+        default: break;
+      }
+    }
+    return launch_ld_stamped<KC, 0>(c, grid, s);
   }
 #endif
   k_dsam_lds<KC><<<grid, 512, LdCfg<KC>::SMEM, s>>>(b);
@@ -2482,6 +2516,11 @@ int rgbd_debug_dsam_stamps(void* buf, int launches) {
   g_ld_stamps = (unsigned long long*)buf;
   g_ld_stamp_cap = buf ? launches : 0;
   g_ld_stamp_n = 0;
+  return RGBD_OK;
+}
+int rgbd_debug_dsam_mode(int mode) {
+  RGBD_REQUIRE(mode == 0 || mode == 1 || mode == 2 || mode == 3 || mode == 7 || mode == 8 || mode == 15, RGBD_E_ARG);
+  g_ld_mode = mode;
   return RGBD_OK;
 }
 #endif
