@@ -3,7 +3,9 @@ graph per value (the setting is read while the step is captured), replayed in al
 prints the median ms per step per value.  Tuple settings take comma-separated values ("-" = empty):
 
     python tools/ab_hotpath_knob.py PREPACK 0,1 0 -
-    python tools/ab_hotpath_knob.py PREPARE_ORDER modes,nhwc,packs packs,modes,nhwc
+
+(profiles/r05_v2/ab_order_ze.txt came from a temporary PREPARE_ORDER tuple in prepare(): the
+order of its side-stream launches; the current order measured fastest and the knob was removed.)
 """
 import argparse
 import os
