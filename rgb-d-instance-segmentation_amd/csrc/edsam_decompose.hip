@@ -299,10 +299,14 @@ __device__ __forceinline__ Windows windows_of(rgbd_decomp_info* info, const floa
   Windows w;
   w.n = info[b].n_modes;
   const float rr = ratio[b];
+  float cen[RGBD_MAX_MODES];  // loaded unconditionally: one round trip, not one per mode
+#pragma unroll
+  for (int m = 0; m < RGBD_MAX_MODES; ++m) cen[m] = info[b].center[m];
+#pragma unroll
   for (int m = 0; m < RGBD_MAX_MODES; ++m) {
     float lo = 0.f, hi = 0.f;
     if (m < w.n) {
-      const float c = info[b].center[m];
+      const float c = cen[m];
       const float half = __fmul_rn(__fmul_rn(c, rr), 0.5f);  // c * r / 2 (:768)
       lo = __fsub_rn(c, half);
       if (!(lo > 0.f)) lo = 0.f;                             // max(0, .) (:769)
@@ -319,11 +323,15 @@ __device__ __forceinline__ Windows windows_of(rgbd_decomp_info* info, const floa
   return w;
 }
 
+// The window loop runs to the fixed RGBD_MAX_MODES (t < n predicated) so lo / hi stay in
+// registers: a loop to the run-time n indexed them dynamically, which put the two arrays in LDS
+// and cost two dependent LDS reads per window per pixel.
 __device__ __forceinline__ uint32_t pixel_code(float g, int n, const float* lo, const float* hi) {
   if (n == 0) return 0u;  // no mode: four all-zero masks (:676-678)
   uint32_t c = 0u;
-  for (int t = 0; t < n; ++t)
-    if (g >= lo[t] && g <= hi[t]) c |= 1u << t;  // (d >= lo) & (d <= hi) (:790)
+#pragma unroll
+  for (int t = 0; t < RGBD_MAX_MODES; ++t)
+    if (t < n && g >= lo[t] && g <= hi[t]) c |= 1u << t;  // (d >= lo) & (d <= hi) (:790)
   if (c == 0u) c = 1u << n;                      // remaining region ~union (:795)
   return c;
 }
@@ -368,22 +376,25 @@ __global__ __launch_bounds__(256) void k_codes_pyramid(const float* __restrict__
   __shared__ uint32_t smask[3];
   const int b = blockIdx.z, tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int i = blockIdx.y * 16 + ty, j = blockIdx.x * 16 + tx;
+  const int fy = H / oh0, fx = W / ow0;
+  const long long HW = (long long)H * W;
+  const float* d = depth3 + b * bstride;
+  const bool in0 = i < oh0 && j < ow0;
+  // the cell's grey rows are loaded before the windows are known (they do not depend on them),
+  // so the loads and the windows' record reads are in flight together
+  float4 v[4];
+  if (kF4 && in0)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) v[y] = *reinterpret_cast<const float4*>(d + (long long)(4 * i + y) * W + 4 * j);
   const Windows win =
       windows_of(info, ratio, b, blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0);
   const int n = win.n;
   const float* lo = win.lo;
   const float* hi = win.hi;
   if (threadIdx.x < 3) smask[threadIdx.x] = 0u;
-  const int fy = H / oh0, fx = W / ow0;
-  const long long HW = (long long)H * W;
-  const float* d = depth3 + b * bstride;
   uint32_t c = 0u;
-  const bool in0 = i < oh0 && j < ow0;
   if (kF4) {  // the grey plane, 4 x 4-pixel cells (the Swin stride): one 16-byte load per cell row
     if (in0 && n > 0) {
-      float4 v[4];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) v[y] = *reinterpret_cast<const float4*>(d + (long long)(4 * i + y) * W + 4 * j);
 #pragma unroll
       for (int y = 0; y < 4; ++y)
         c |= pixel_code(v[y].x, n, lo, hi) | pixel_code(v[y].y, n, lo, hi) | pixel_code(v[y].z, n, lo, hi) |

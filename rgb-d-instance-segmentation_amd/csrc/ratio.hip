@@ -396,8 +396,8 @@ __device__ __forceinline__ void stem_frame_body(const float* __restrict__ depth3
 // s_memtime at: kernel entry, window staged (after the barrier), lag loop done, waves joined,
 // correlations written, plane sums written: stamps[(wg * 8 + wave) * 6 + point].
 __device__ unsigned long long* g_sl_stamps = nullptr;
-static bool sl_stamps_on = false;
-__device__ __forceinline__ void sl_stamp(long long idx) {
+[[maybe_unused]] static bool sl_stamps_on = false;
+[[maybe_unused]] __device__ __forceinline__ void sl_stamp(long long idx) {
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0) g_sl_stamps[idx] = t;
@@ -2358,7 +2358,10 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
                                                       const char* __restrict__ blob, Layout L,
                                                       unsigned long long seed, unsigned long long* seed_ctr,
                                                       float* __restrict__ ratio) {
-  __shared__ float w8t[128][64], w9t[64][32];
+  // the weights stay row-major in LDS with one float of row padding: the staging writes and the
+  // per-output row reads (lanes = outputs, rows 129 / 65 floats apart) are both conflict-free
+  // (the transposed images this replaced took 32-way conflicts on every staging write)
+  __shared__ float w8s[64][129], w9s[32][65];
   const unsigned long long ctr = seed_ctr ? *seed_ctr : 0ull;
   seed += ctr;
   __shared__ float h1[32][128], h2[32][64], h3[32][32];
@@ -2368,14 +2371,14 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
   const float* b9 = (const float*)(blob + L.b9);
   const float* w10 = (const float*)(blob + L.w10);
   const float* b10 = (const float*)(blob + L.b10);
-  for (int i = threadIdx.x; i < 64 * 128; i += 512) w8t[i % 128][i / 128] = w8[i];
-  for (int i = threadIdx.x; i < 32 * 64; i += 512) w9t[i % 64][i / 64] = w9[i];
+  for (int i = threadIdx.x; i < 64 * 128; i += 512) w8s[i / 128][i % 128] = w8[i];
+  for (int i = threadIdx.x; i < 32 * 64; i += 512) w9s[i / 64][i % 64] = w9[i];
   for (int i = threadIdx.x; i < B * 128; i += 512) h1[i / 128][i % 128] = h1g[i];
   __syncthreads();
   for (int e = threadIdx.x; e < B * 64; e += 512) {
     const int bb = e / 64, o = e % 64;
     float s = b8[o];
-    for (int k = 0; k < 128; ++k) s += w8t[k][o] * h1[bb][k];
+    for (int k = 0; k < 128; ++k) s += w8s[o][k] * h1[bb][k];
     s = fmaxf(s, 0.f);
     if (training) s = hash_uniform(seed ^ 0x5555ull, e) < 0.2f ? 0.f : s / 0.8f;  // Dropout(0.2)
     h2[bb][o] = s;
@@ -2384,7 +2387,7 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
   for (int e = threadIdx.x; e < B * 32; e += 512) {
     const int bb = e / 32, o = e % 32;
     float s = b9[o];
-    for (int k = 0; k < 64; ++k) s += w9t[k][o] * h2[bb][k];
+    for (int k = 0; k < 64; ++k) s += w9s[o][k] * h2[bb][k];
     h3[bb][o] = fmaxf(s, 0.f);
   }
   __syncthreads();
