@@ -206,11 +206,24 @@ __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, i
                                                float2* __restrict__ affine) {
   __shared__ double red[2][256];
   double s = 0.0, q = 0.0;
-  if (training)
-    for (int i = threadIdx.x; i < nslab; i += 256) {
+  if (training) {
+    // eight slab rows per thread in flight at once, summed in the same (row) order
+    int i = threadIdx.x;
+    for (; i + 256 * 7 < nslab; i += 256 * 8) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(slab + ((long long)(i + 256 * u) * row + c_off + c) * 2);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += (double)v[u].x;
+        q += (double)v[u].y;
+      }
+    }
+    for (; i < nslab; i += 256) {
       s += (double)slab[((long long)i * row + c_off + c) * 2 + 0];
       q += (double)slab[((long long)i * row + c_off + c) * 2 + 1];
     }
+  }
   red[0][threadIdx.x] = s;
   red[1][threadIdx.x] = q;
   __syncthreads();
@@ -652,8 +665,15 @@ __global__ __launch_bounds__(256) void k_stem_bn(const double* __restrict__ S2, 
   double a = 0.0, q = 0.0;
   if (t < 147) {
     a = w[t] * S1[t];
-#pragma unroll 7
-    for (int l = 0; l < 147; ++l) q += w[l] * S2[l * 147 + t];  // S2 symmetric: coalesced rows
+    // S2 symmetric: coalesced rows.  49 rows per batch in flight together, summed in row order
+    // (seven loads per round trip made the 147 serial L2 round trips most of the kernel)
+    for (int l0 = 0; l0 < 147; l0 += 49) {
+      double sv[49];
+#pragma unroll
+      for (int u = 0; u < 49; ++u) sv[u] = S2[(l0 + u) * 147 + t];
+#pragma unroll
+      for (int u = 0; u < 49; ++u) q += w[l0 + u] * sv[u];
+    }
     q *= w[t];
   }
   red[0][t] = a;
@@ -2208,19 +2228,40 @@ __global__ __launch_bounds__(256) void k_rp_tail_conv(const float* __restrict__ 
   __shared__ float sp[TC_C * TC_IMG * 36];
   const float* w6 = (const float*)(blob + L.w6);
   const int o0 = blockIdx.x * TC_O, c0 = blockIdx.y * TC_C;
-  for (int i = threadIdx.x; i < TC_O * TC_C * 9; i += 256) {
-    const int ol = i / (TC_C * 9), r = i % (TC_C * 9);  // r = cl * 9 + tap: contiguous per o
-    sw[r * TC_O + ol] = w6[((long long)(o0 + ol) * C5 + c0) * 9 + r];
+  // staging: every thread's loads issued together, then the LDS writes (a load -> store loop
+  // waited for each load in turn: ~18 dependent memory round trips per stage)
+  constexpr int TC_NW = TC_O * TC_C * 9 / 256;
+  static_assert(TC_O * TC_C * 9 % 256 == 0 && TC_C * TC_IMG * 36 % 256 == 0, "tail conv staging");
+  {
+    float wv[TC_NW];
+#pragma unroll
+    for (int q = 0; q < TC_NW; ++q) {
+      const int i = threadIdx.x + 256 * q, ol = i / (TC_C * 9), r = i % (TC_C * 9);  // r = cl * 9 + tap
+      wv[q] = w6[((long long)(o0 + ol) * C5 + c0) * 9 + r];
+    }
+#pragma unroll
+    for (int q = 0; q < TC_NW; ++q) {
+      const int i = threadIdx.x + 256 * q, ol = i / (TC_C * 9), r = i % (TC_C * 9);
+      sw[r * TC_O + ol] = wv[q];
+    }
   }
   const int og = threadIdx.x >> 5, im = (threadIdx.x & 31) >> 2, py = threadIdx.x & 3;
   for (int b0 = 0; b0 < B; b0 += TC_IMG) {
     __syncthreads();
-    for (int i = threadIdx.x; i < TC_C * TC_IMG * 36; i += 256) {
-      const int cl = i / (TC_IMG * 36), r = i % (TC_IMG * 36), j = r / 36, q = r % 36;
-      const int yy = q / 6 - 1, xx = q % 6 - 1, b = b0 + j;
-      float v = 0.f;
-      if (b < B && yy >= 0 && yy < 4 && xx >= 0 && xx < 4) v = pooled[((long long)b * C5 + c0 + cl) * 16 + yy * 4 + xx];
-      sp[i] = v;
+    {
+      constexpr int TC_NP = TC_C * TC_IMG * 36 / 256;
+      float pv[TC_NP];
+#pragma unroll
+      for (int e = 0; e < TC_NP; ++e) {
+        const int i = threadIdx.x + 256 * e;
+        const int cl = i / (TC_IMG * 36), r = i % (TC_IMG * 36), j = r / 36, q = r % 36;
+        const int yy = q / 6 - 1, xx = q % 6 - 1, b = b0 + j;
+        const bool in = b < B && yy >= 0 && yy < 4 && xx >= 0 && xx < 4;
+        const float v = pooled[in ? ((long long)b * C5 + c0 + cl) * 16 + yy * 4 + xx : 0];  // unconditional load
+        pv[e] = in ? v : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < TC_NP; ++e) sp[threadIdx.x + 256 * e] = pv[e];
     }
     __syncthreads();
     float acc[4][4];
@@ -2336,11 +2377,21 @@ __global__ __launch_bounds__(256) void k_rp_tail_fc1(const float* __restrict__ f
   const int o = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const float* w7 = (const float*)(blob + L.w7);
   const float wa = w7[o * 512 + t], wb = w7[o * 512 + t + 256];
-  for (int b = 0; b < B; ++b) {
-    float s = wa * feat[(long long)b * C6 + t] + wb * feat[(long long)b * C6 + t + 256];
-    s = wave_sum(s);
-    if (lane == 0) red[wv][b] = s;
-  }
+  // all images' feature loads in flight before the reductions (B <= 32)
+  float fa[32], fb[32];
+#pragma unroll
+  for (int b = 0; b < 32; ++b)
+    if (b < B) {
+      fa[b] = feat[(long long)b * C6 + t];
+      fb[b] = feat[(long long)b * C6 + t + 256];
+    }
+#pragma unroll
+  for (int b = 0; b < 32; ++b)
+    if (b < B) {
+      float s = wa * fa[b] + wb * fb[b];
+      s = wave_sum(s);
+      if (lane == 0) red[wv][b] = s;
+    }
   __syncthreads();
   if (t < B) {
     const float* b7 = (const float*)(blob + L.b7);
@@ -2353,7 +2404,7 @@ __global__ __launch_bounds__(256) void k_rp_tail_fc1(const float* __restrict__ f
 }
 
 // Linear 128 -> 64 + ReLU + Dropout(0.2), Linear 64 -> 32 + ReLU, Linear 32 -> 1, sigmoid range
-// map; one workgroup, weights transposed into LDS (lanes walk output columns: conflict-free).
+// map; one workgroup, the weights row-major in LDS (padded rows: lanes walk output rows).
 __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ h1g, int B, int training,
                                                       const char* __restrict__ blob, Layout L,
                                                       unsigned long long seed, unsigned long long* seed_ctr,
@@ -2371,9 +2422,31 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
   const float* b9 = (const float*)(blob + L.b9);
   const float* w10 = (const float*)(blob + L.w10);
   const float* b10 = (const float*)(blob + L.b10);
-  for (int i = threadIdx.x; i < 64 * 128; i += 512) w8s[i / 128][i % 128] = w8[i];
-  for (int i = threadIdx.x; i < 32 * 64; i += 512) w9s[i / 64][i % 64] = w9[i];
-  for (int i = threadIdx.x; i < B * 128; i += 512) h1[i / 128][i % 128] = h1g[i];
+  {  // every staging load in flight together, then the LDS writes
+    float a8[16], a9[4], ah[8];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a8[q] = w8[threadIdx.x + 512 * q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a9[q] = w9[threadIdx.x + 512 * q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (threadIdx.x + 512 * q < B * 128) ah[q] = h1g[threadIdx.x + 512 * q];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = threadIdx.x + 512 * q;
+      w8s[i / 128][i % 128] = a8[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = threadIdx.x + 512 * q;
+      w9s[i / 64][i % 64] = a9[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = threadIdx.x + 512 * q;
+      if (i < B * 128) h1[i / 128][i % 128] = ah[q];
+    }
+  }
   __syncthreads();
   for (int e = threadIdx.x; e < B * 64; e += 512) {
     const int bb = e / 64, o = e % 64;
