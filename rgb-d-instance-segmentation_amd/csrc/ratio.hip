@@ -26,6 +26,12 @@
 #include "mfma.hpp"
 #include "timing.hpp"
 
+// RP_ORDER 1: the gate last-to-first, conv5 first-to-last, the pool's images last-to-first;
+// 0: the gate and the pool forward, conv5 last-to-first
+#ifndef RP_ORDER
+#define RP_ORDER 1
+#endif
+
 using namespace rgbd;
 
 namespace {
@@ -1530,7 +1536,8 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
   uint2 nxt[8][2];
   auto fetch = [&](int tl) {
     if (tl >= ntiles) return;
-    const bf16_t* ft = fus + (((long long)tl * 8 + wave) * 16) * 256;
+    const int tp = RP_ORDER ? ntiles - 1 - tl : tl;  // physical tile (see c3_phys)
+    const bf16_t* ft = fus + (((long long)tp * 8 + wave) * 16) * 256;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // read once: non-temporal, 16 B per lane (1 KiB per wave load)
       const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ft + (t * 64 + lane) * 8));
@@ -1540,7 +1547,7 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
   };
   fetch(blockIdx.x);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const TileDec td = tile_dec((unsigned)tile, per, (unsigned)tiles_x, C2W_TH, C2W_TW);
+    const TileDec td = tile_dec((unsigned)(RP_ORDER ? ntiles - 1 - tile : tile), per, (unsigned)tiles_x, C2W_TH, C2W_TW);
     const int b = td.b, y0 = td.y0, x0 = td.x0;
     const int py = y0 + wave;
     uint2 raw[8][2];
@@ -1852,6 +1859,9 @@ __device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) 
 // NODMA (diagnostic build only, rgbd_debug_conv5_mode): bit 0 drops the in-loop B copies, bit 1
 // the in-loop A copies, bit 2 the per-step barrier, bit 3 the fragment reads (constant operands)
 // — wrong results; isolates the DMA's, the lockstep's and the fragment stream's costs.
+__device__ __forceinline__ long long c3_phys(long long tile, long long ntiles) {
+  return RP_ORDER ? tile : ntiles - 1 - tile;
+}
 template <bool STAMPS, int NODMA = 0>
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
@@ -1901,12 +1911,13 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   // static priority for the second-dispatched half of the workgroup (the arbitration loser of
   // every step with two waves per SIMD; MI355X_MICROARCH "two waves per SIMD", item 4)
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-  // tiles in reverse order: the gate kernel before this one wrote the attention features in
-  // increasing tile order, so the last ones written (still in the Infinity Cache) are read first
-  // (conv5 1.078 -> 1.064 ms, ratio forward -18 us; profiles/r05_v2/ab_w.txt)
+  // tile order: each kernel of the chain -> gate -> conv5 -> pool sequence reads first what the
+  // previous one wrote last (still in the Infinity Cache): the chain writes in increasing tile
+  // order, the gate walks its tiles last-to-first, conv5 first-to-last, the pool the images
+  // last-to-first (RP_ORDER; conv5 alone reversed: ratio forward -18 us, profiles/r05_v2/ab_w.txt)
   long long tile = blockIdx.x;
   if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
-    const C3Tile t = c3_tile(ntiles - 1 - tile, tiles_x, tiles_y);
+    const C3Tile t = c3_tile(c3_phys(tile, ntiles), tiles_x, tiles_y);
     for (int j = wave; j < C3_APIECES; j += 8) issue_a(t, 0, j);
     if (loader) issue_b(0, 0, 8);
   }
@@ -1916,12 +1927,12 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   unsigned long long* const stamps = (STAMPS && blockIdx.x == 0) ? g_c3_stamps : nullptr;
   int tcount = 0;
   for (; tile < ntiles; tile += gridDim.x, ++tcount) {
-    const long long tphys = ntiles - 1 - tile;
+    const long long tphys = c3_phys(tile, ntiles);
     const C3Tile t = c3_tile(tphys, tiles_x, tiles_y);
     const long long ntile = tile + gridDim.x;
     unsigned long long* const sts = (STAMPS && stamps && tcount < 2) ? stamps : nullptr;
     const bool has_next = ntile < ntiles;
-    const C3Tile tn = c3_tile(ntiles - 1 - (has_next ? ntile : tile), tiles_x, tiles_y);
+    const C3Tile tn = c3_tile(c3_phys(has_next ? ntile : tile, ntiles), tiles_x, tiles_y);
     f32x4 acc[4][8];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -2149,7 +2160,8 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_tiles(const bf16_t* __r
                                                                const float2* __restrict__ aff,
                                                                float* __restrict__ part) {
   __shared__ float red[C5];
-  const int b = blockIdx.y, reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
+  const int b = RP_ORDER ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;  // see c3_phys
+  const int reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
   const int i = reg / 4, j = reg % 4;
   const int tiles_x = W / C3_TW, tiles_y = H / C3_TH;
   const int rty = tiles_y / 4, rtx = tiles_x / 4;  // region size in tiles
