@@ -1383,7 +1383,10 @@ __device__ __forceinline__ void ld_stamp(unsigned long long* st, int f) {
 
 // NODMA (diagnostic build only, rgbd_debug_dsam_mode; timing only, the results are garbage):
 // bit 0 drops the in-loop B copies, bit 1 the in-loop A copies, bit 2 the per-step barrier (each
-// wave still waits for its own copies), bit 3 the fragment reads (constant MFMA operands).
+// wave still waits for its own copies), bit 3 the fragment reads (constant MFMA operands); bit 5
+// copies every step's weights from its code's first filter tile and bit 6 every step's input rows from
+// one fixed pixel block (the copies stay, their sources become L2-resident: the ceiling of
+// locality work).
 // One (tile, chunk) item of k_dsam_lds for N tile ntile (of ntn).
 template <int KC, int NODMA = 0>
 __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, int chunk, int ntile, int ntn,
@@ -1485,12 +1488,16 @@ __device__ __forceinline__ void ld_item(const ConvArgs& a, int cls, int tile, in
     const uint32_t rc = (t < 8 ? alo >> (4 * t) : ahi) & 15u;
     const bool live = ((aval >> t) & 1u) && rc == (uint32_t)code;
     const bf16_t* asrc = live ? xp + (long long)(aorg + delta) * a.C + cg * 32 * KC + achk : zrow;
+    if constexpr ((NODMA & 64) != 0)  // timing only: every step's rows from one fixed 128-pixel block
+      if (inloop) asrc = xp + (long long)R * a.C + achk;
     if (!((NODMA & 2) && inloop))
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) dma_lds16(live ? asrc + kc * 32 : zrow, sb + kc * LD_A1 + wave * 1024);
     if ((NODMA & 1) && inloop) return;
     const long long tstride = (long long)a.N * 32;  // one (code, tap, chunk) tile, elements
     const bf16_t* bsrc = wp + ((long long)(code * 9 + tap) * (a.C / 32) + cg * KC) * tstride + (long long)n0 * 32 + lane * 8;
+    if constexpr ((NODMA & 32) != 0)  // timing only: every step's weights from its code's first tile
+      if (inloop) bsrc = wp + (long long)(code * 9) * (a.C / 32) * tstride + (long long)n0 * 32 + lane * 8;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const bf16_t* tbk = bsrc + kc * tstride;
@@ -1950,6 +1957,9 @@ hipError_t launch_ld(const ConvArgs& b, dim3 grid, hipStream_t s) {
         case 3: return launch_ld_stamped<KC, 3>(c, grid, s);
         case 7: return launch_ld_stamped<KC, 7>(c, grid, s);
         case 15: return launch_ld_stamped<KC, 15>(c, grid, s);
+        case 32: return launch_ld_stamped<KC, 32>(c, grid, s);
+        case 64: return launch_ld_stamped<KC, 64>(c, grid, s);
+        case 96: return launch_ld_stamped<KC, 96>(c, grid, s);
         case 8: return launch_ld_stamped<KC, 8>(c, grid, s);
         default: break;
       }
@@ -2519,7 +2529,9 @@ int rgbd_debug_dsam_stamps(void* buf, int launches) {
   return RGBD_OK;
 }
 int rgbd_debug_dsam_mode(int mode) {
-  RGBD_REQUIRE(mode == 0 || mode == 1 || mode == 2 || mode == 3 || mode == 7 || mode == 8 || mode == 15, RGBD_E_ARG);
+  RGBD_REQUIRE(mode == 0 || mode == 1 || mode == 2 || mode == 3 || mode == 7 || mode == 8 || mode == 15 || mode == 32 ||
+                   mode == 64 || mode == 96,
+               RGBD_E_ARG);
   g_ld_mode = mode;
   return RGBD_OK;
 }

@@ -2,7 +2,8 @@
 640x480, bf16) with the five DSAM conv launches (forward dsam0 / dsam1 / dsam2, dX of dsam2 /
 dsam1) run as the stamped kernel under rgbd_debug_dsam_mode 0 (the kernel), 1 (no in-loop weight
 copies), 2 (no in-loop input copies), 3 (no copies), 7 (and no per-step barrier), 8 (no fragment
-reads, copies kept), 15 (none of them: the MFMA stream and the loop's bookkeeping) — modes other
+reads, copies kept), 15 (none of them: the MFMA stream and the loop's bookkeeping), 32 / 64 / 96
+(the weight / input / both copies kept but sourced from one L2-resident block) — modes other
 than 0 compute garbage and are for timing only (their ring starts zeroed, so values stay finite).
 Modes alternate over rounds; per mode and launch it prints the median over rounds of the mean
 cycles per K step and of the longest workgroup span (the launch's length)."""
@@ -59,7 +60,7 @@ for rnd in range(ROUNDS):
                     lens.append(max(r[5], r[4], r[3]) - S[w, 0, 0])
             span[md][li].append(float(max(lens)))
 mname = {0: "kernel", 1: "no B copies", 2: "no A copies", 3: "no copies", 7: "+ no barrier", 8: "no frag reads",
-         15: "MFMAs only"}
+         15: "MFMAs only", 32: "B L2-resident", 64: "A L2-resident", 96: "A, B L2-resident"}
 print("cycles per K step (mean over items) / longest workgroup span (K cycles); median of", ROUNDS, "rounds")
 print(f"{'mode':22s}" + "".join(f"{n:>22s}" for n in names) + f"{'sum of spans':>14s}")
 for md in MODES:
