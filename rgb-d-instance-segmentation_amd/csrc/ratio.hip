@@ -26,12 +26,6 @@
 #include "mfma.hpp"
 #include "timing.hpp"
 
-// RP_ORDER 1: the gate last-to-first, conv5 first-to-last, the pool's images last-to-first;
-// 0: the gate and the pool forward, conv5 last-to-first
-#ifndef RP_ORDER
-#define RP_ORDER 1
-#endif
-
 using namespace rgbd;
 
 namespace {
@@ -1536,7 +1530,7 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
   uint2 nxt[8][2];
   auto fetch = [&](int tl) {
     if (tl >= ntiles) return;
-    const int tp = RP_ORDER ? ntiles - 1 - tl : tl;  // physical tile (see c3_phys)
+    const int tp = ntiles - 1 - tl;  // physical tile: last-to-first (see the conv5 kernel)
     const bf16_t* ft = fus + (((long long)tp * 8 + wave) * 16) * 256;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // read once: non-temporal, 16 B per lane (1 KiB per wave load)
@@ -1547,7 +1541,7 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
   };
   fetch(blockIdx.x);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const TileDec td = tile_dec((unsigned)(RP_ORDER ? ntiles - 1 - tile : tile), per, (unsigned)tiles_x, C2W_TH, C2W_TW);
+    const TileDec td = tile_dec((unsigned)(ntiles - 1 - tile), per, (unsigned)tiles_x, C2W_TH, C2W_TW);
     const int b = td.b, y0 = td.y0, x0 = td.x0;
     const int py = y0 + wave;
     uint2 raw[8][2];
@@ -1859,9 +1853,6 @@ __device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) 
 // NODMA (diagnostic build only, rgbd_debug_conv5_mode): bit 0 drops the in-loop B copies, bit 1
 // the in-loop A copies, bit 2 the per-step barrier, bit 3 the fragment reads (constant operands)
 // — wrong results; isolates the DMA's, the lockstep's and the fragment stream's costs.
-__device__ __forceinline__ long long c3_phys(long long tile, long long ntiles) {
-  return RP_ORDER ? tile : ntiles - 1 - tile;
-}
 template <bool STAMPS, int NODMA = 0>
 __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
                                                        const char* __restrict__ blob, Layout L,
@@ -1914,10 +1905,10 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   // tile order: each kernel of the chain -> gate -> conv5 -> pool sequence reads first what the
   // previous one wrote last (still in the Infinity Cache): the chain writes in increasing tile
   // order, the gate walks its tiles last-to-first, conv5 first-to-last, the pool the images
-  // last-to-first (RP_ORDER; conv5 alone reversed: ratio forward -18 us, profiles/r05_v2/ab_w.txt)
+  // last-to-first (profiles/r05_v2/ab_w.txt, ab_x.txt, ab_zk.txt, ab_zk2.txt)
   long long tile = blockIdx.x;
   if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
-    const C3Tile t = c3_tile(c3_phys(tile, ntiles), tiles_x, tiles_y);
+    const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
     for (int j = wave; j < C3_APIECES; j += 8) issue_a(t, 0, j);
     if (loader) issue_b(0, 0, 8);
   }
@@ -1927,12 +1918,12 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
   unsigned long long* const stamps = (STAMPS && blockIdx.x == 0) ? g_c3_stamps : nullptr;
   int tcount = 0;
   for (; tile < ntiles; tile += gridDim.x, ++tcount) {
-    const long long tphys = c3_phys(tile, ntiles);
+    const long long tphys = tile;
     const C3Tile t = c3_tile(tphys, tiles_x, tiles_y);
     const long long ntile = tile + gridDim.x;
     unsigned long long* const sts = (STAMPS && stamps && tcount < 2) ? stamps : nullptr;
     const bool has_next = ntile < ntiles;
-    const C3Tile tn = c3_tile(c3_phys(has_next ? ntile : tile, ntiles), tiles_x, tiles_y);
+    const C3Tile tn = c3_tile(has_next ? ntile : tile, tiles_x, tiles_y);
     f32x4 acc[4][8];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -2160,7 +2151,7 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_tiles(const bf16_t* __r
                                                                const float2* __restrict__ aff,
                                                                float* __restrict__ part) {
   __shared__ float red[C5];
-  const int b = RP_ORDER ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;  // see c3_phys
+  const int b = (int)gridDim.y - 1 - (int)blockIdx.y;  // images last-to-first (see the conv5 kernel)
   const int reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
   const int i = reg / 4, j = reg % 4;
   const int tiles_x = W / C3_TW, tiles_y = H / C3_TH;
