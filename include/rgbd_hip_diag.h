@@ -31,7 +31,9 @@ int rgbd_debug_chain_stamps(void* buf);
 int rgbd_debug_dsam_stamps(void* buf, int launches);
 /* Timing-only variants of the stamped DSAM conv kernel (KC = 3 legs; results are garbage): mode
  * bit 0 drops the in-loop weight copies, bit 1 the in-loop input copies, bit 2 the per-step
- * barrier, bit 3 the fragment reads.  Valid: 0, 1, 2, 3, 7, 8, 15; applies while stamps are on. */
+ * barrier, bit 3 the fragment reads; bit 5 sources every step's weight copies from its code's
+ * first filter tile, bit 6 every step's input copies from one fixed pixel block (L2-resident).
+ * Valid: 0, 1, 2, 3, 7, 8, 15, 32, 64, 96; applies while stamps are on. */
 int rgbd_debug_dsam_mode(int mode);
 /* The stem statistics' lag kernel (k_stem_lag): buf (device, >= workgroups * 8 * 6 uint64)
  * receives, for every workgroup and wave of each later launch, s_memtime at entry, window staged,
