@@ -23,7 +23,7 @@ WORLD_SIZE from the environment.  8 images per rank (scaling "weak").
 
 Prints ONE JSON line (rank 0).  ``value`` = images processed by all ranks / max-over-ranks
 time.  ``roofline`` is for the dominant kernel (the ratio predictor's 3x3 128->256 conv,
-k_rp_conv3x3), timed with HIP events on its launch stream inside the timed region;
+k_rp_conv3x3), timed with HIP events on its launch stream over this run's eager timed steps;
 ``kernels`` carries the same for K5 and the whole step's t_ideal / t_measured.
 ``cpu_baseline`` = the oracle (PyTorch-CPU fp32 restatement of the reference, tests-only
 code) on bounded samples of the same workloads on this host's cores (BASELINE.md plan).
@@ -67,41 +67,42 @@ K3_BYTES_PER_PX = 12.04
 ADAMW_BYTES_PER_PARAM = 28        # fused AdamW: read p, g, m, v; write p, m, v (f32)
 
 
+# The committed evidence of this tree's default bench step (rocprofv3 kernel trace + PMC passes,
+# see its README): named explicitly, updated with each evidence commit, never picked by sort order.
+EVIDENCE_DIR = "profiles/r05_v6"
+
+
 def pmc_traffic(kernel, default_shape):
-    """HBM bytes per launch of ``kernel`` from the newest committed PMC table
-    (profiles/*/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 correction, plus
-    WRITE_SIZE, one pass each, over this bench's default step).  rocprofv3 cannot run inside
-    this process, so the counters come from their own passes; null for a non-default shape."""
-    if not default_shape:
+    """HBM bytes per launch of ``kernel`` from EVIDENCE_DIR/pmc_traffic.json (FETCH_SIZE doubled
+    per the gfx950 correction, plus WRITE_SIZE, one pass each, over this bench's default step).
+    rocprofv3 cannot run inside this process, so the counters come from their own passes; null
+    for a non-default shape or when the evidence has no such row."""
+    path = REPO / EVIDENCE_DIR / "pmc_traffic.json"
+    if not default_shape or not path.exists():
         return None
-    best = None
-    for path in sorted((REPO / "profiles").glob("*/pmc_traffic.json")):
-        for key, row in json.loads(path.read_text()).items():
-            name = key.split(" grid=")[0]  # a template argument list (e.g. "<false>") aside
-            if (name == kernel or name.split("<")[0] == kernel) and "hbm_bytes" in row:
-                best = (row["hbm_bytes"], str(path.relative_to(REPO)))
-    return best
+    for key, row in json.loads(path.read_text()).items():
+        name = key.split(" grid=")[0]  # a template argument list (e.g. "<false>") aside
+        if (name == kernel or name.split("<")[0] == kernel) and "hbm_bytes" in row:
+            return row["hbm_bytes"], str(path.relative_to(REPO))
+    return None
 
 
 def profile_avg_ns(kernel, default_shape):
-    """(average ns per launch, source) of ``kernel`` from the newest committed bench-step kernel
-    trace (profiles/*/kernel_stats.csv: ``rocprofv3 --kernel-trace --stats`` of this bench's
-    default step, see each directory's README), looked up like pmc_traffic; None for a
-    non-default shape or when no trace has the kernel."""
-    if not default_shape:
-        return None
+    """(average ns per launch, source, calls) of ``kernel`` in EVIDENCE_DIR/kernel_stats.csv
+    (``rocprofv3 --kernel-trace --stats`` of this bench's default step); None for a non-default
+    shape or when the trace has no such kernel."""
     import csv
-    best = None
-    for path in sorted((REPO / "profiles").glob("*/kernel_stats.csv")):
-        with open(path, newline="") as f:
-            for row in csv.DictReader(f):
-                name = row.get("Name", "").replace("(anonymous namespace)::", "")
-                head = re.sub(r"<.*>", "", name.split("(")[0])  # template arguments may hold spaces
-                base = head.split()[-1].split("::")[-1] if head.split() else ""
-                if base == kernel:
-                    best = (float(row["AverageNs"]), str(path.relative_to(REPO)), int(row["Calls"]))
-                    break
-    return best
+    path = REPO / EVIDENCE_DIR / "kernel_stats.csv"
+    if not default_shape or not path.exists():
+        return None
+    with open(path, newline="") as f:
+        for row in csv.DictReader(f):
+            name = row.get("Name", "").replace("(anonymous namespace)::", "")
+            head = re.sub(r"<.*>", "", name.split("(")[0])  # template arguments may hold spaces
+            base = head.split()[-1].split("::")[-1] if head.split() else ""
+            if base == kernel:
+                return float(row["AverageNs"]), str(path.relative_to(REPO)), int(row["Calls"])
+    return None
 
 
 def parse(argv=None):
@@ -116,6 +117,9 @@ def parse(argv=None):
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
+    ap.add_argument("--ddp", type=int, default=None,
+                    help="run the data-parallel path (process group, overlapped all-reduce, buffer broadcast) "
+                         "even at N=1 (default: only for N > 1); --ddp 1 --gpus 1 executes the RCCL code on one GPU")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--inference", type=int, default=1, help="also report forward-only img/s")
     ap.add_argument("--c5-stream", type=int, default=1,
@@ -217,7 +221,7 @@ def build(args, dev, rank=0):
                 gouts=gouts, scenes=scenes, sizes=sizes)
 
 
-def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False):
+def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, ddp=None):
     """(forward_backward, optimizer_step, reducer, broadcaster) of one training step.
     forward_backward() leaves the (all-reduced, for N > 1) gradients in p.grad;
     optimizer_step.opt is the AdamW instance (``capturable`` for graph capture).
@@ -241,8 +245,9 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False):
     params = [p for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
     groups = hot_path_grad_groups(ctx["dsams"], ctx["dg"])
     # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
-    reducer = OverlappedGradReducer(groups) if world > 1 else None
-    bcast = BufferBroadcaster([ctx["rp"]]) if world > 1 else None
+    ddp = world > 1 if ddp is None else bool(ddp)
+    reducer = OverlappedGradReducer(groups) if ddp else None
+    bcast = BufferBroadcaster([ctx["rp"]]) if ddp else None
     hook = None if reducer is None else reducer.ready
     if overlap_opt:
         # dsam2's update as soon as its gradients are in (under the rest of the backward), the
@@ -303,7 +308,7 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False):
     return forward_backward, optimizer_step, reducer, bcast
 
 
-def make_step(ctx, world, inference=False, graph=False, pipeline=False):
+def make_step(ctx, world, inference=False, graph=False, pipeline=False, ddp=None):
     from rgbd_amd import ops
     from rgbd_amd.hot_path import hot_path, prepare
     if inference:
@@ -316,7 +321,7 @@ def make_step(ctx, world, inference=False, graph=False, pipeline=False):
         return istep
     if graph:  # single process: the whole step replayed from a HIP graph, captured on first use
         from rgbd_amd.train_graph import CapturedTrainStep
-        fb, ostep, _, _ = make_parts(ctx, world, capturable=True, overlap_opt=True, pipeline=pipeline)
+        fb, ostep, _, _ = make_parts(ctx, world, capturable=True, overlap_opt=True, pipeline=pipeline, ddp=ddp)
         held = {}
 
         def gstep():
@@ -324,7 +329,7 @@ def make_step(ctx, world, inference=False, graph=False, pipeline=False):
                 held["g"] = CapturedTrainStep(fb, ostep.opt, opts=ostep.opts, clear=ostep)
             return held["g"]()
         return gstep
-    fb, ostep, _, _ = make_parts(ctx, world, overlap_opt=True)
+    fb, ostep, _, _ = make_parts(ctx, world, overlap_opt=True, ddp=ddp)
 
     def step():
         feats = fb()
@@ -333,24 +338,25 @@ def make_step(ctx, world, inference=False, graph=False, pipeline=False):
     return step
 
 
-def timed(step, steps, warmup, world, on_start=None):
+def timed(step, steps, warmup, world, on_start=None, ddp=None):
+    ddp = world > 1 if ddp is None else ddp
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     if on_start is not None:
         on_start()
-    if world > 1:
+    if ddp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if ddp:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if ddp:
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -831,10 +837,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ddp = world > 1 if args.ddp is None else bool(args.ddp)
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if ddp:
+        if world == 1:  # one rank without a launcher: a local rendezvous
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -843,25 +855,25 @@ def main():
     from rgbd_amd.distributed import broadcast_parameters
     L = _lib.lib()
     ctx = build(args, dev, rank)
-    if world > 1:  # DDP construction: rank 0's parameters and buffers everywhere
+    if ddp:  # DDP construction: rank 0's parameters and buffers everywhere
         broadcast_parameters([ctx["rp"], ctx["dg"]] + ctx["dsams"])
-    step = make_step(ctx, world)
+    step = make_step(ctx, world, ddp=ddp)
     # eager pass: per-kernel HIP-event timing over its timed steps only
-    dt_eager = timed(step, args.steps, args.warmup, world, on_start=lambda: L.rgbd_timing_enable(1))
+    dt_eager = timed(step, args.steps, args.warmup, world, on_start=lambda: L.rgbd_timing_enable(1), ddp=ddp)
     timings = read_timings(L)
     L.rgbd_timing_enable(0)
-    use_graph = bool(args.graph) and world == 1
+    use_graph = bool(args.graph) and not ddp
     # the line's number: the captured step at N = 1; at N > 1 the eager step timed again with the
     # per-kernel HIP events off (they cost ~0.3 ms of host time per step: 3.23 vs 2.92 ms,
     # profiles/r05_v2/prof_host.txt)
     dt = (timed(make_step(ctx, world, graph=True), args.steps, args.warmup, world) if use_graph
-          else timed(step, args.steps, 1, world))
+          else timed(step, args.steps, 1, world, ddp=ddp))
     # the same captured step software-pipelined across batches (make_parts ``pipeline``)
     dt_pipe = timed(make_step(ctx, world, graph=True, pipeline=True), args.steps, args.warmup, world) \
         if use_graph and args.pipeline_report else None
     # N > 1 runs eagerly (the overlapped RCCL reducer is not captured): the same eager step with
     # no collective on every rank at once gives the line's own scaling reference
-    dt_local = timed(make_step(ctx, 1), args.steps, args.warmup, world) if world > 1 else None
+    dt_local = timed(make_step(ctx, 1), args.steps, args.warmup, world, ddp=ddp) if ddp else None
     B = args.batch
     step_ms = dt / args.steps * 1e3
     raw, per, fracs = kernel_fractions(timings, ctx, B, args.height, args.width, step_ms, world, args.steps)
@@ -870,7 +882,7 @@ def main():
     inf = None
     if args.inference:
         istep = make_step(ctx, world, inference=True)
-        idt = timed(istep, args.steps, args.warmup, world)
+        idt = timed(istep, args.steps, args.warmup, world, ddp=ddp)
         inf = round(B * world * args.steps / idt, 2)
         for m in [ctx["rp"], ctx["dg"]] + ctx["dsams"]:
             m.train()
@@ -881,7 +893,6 @@ def main():
     traffic = pmc_traffic(CONV5_KERNEL, default_shape)
     prof = profile_avg_ns(CONV5_KERNEL, default_shape)
     achieved_prof = None if prof is None else flop / (prof[0] * 1e-9) / 1e12
-    achieved_line = achieved if achieved_prof is None else achieved_prof
     out = {
         "metric": "NYUv2 640x480 RGB-D img/s (fwd+bwd) of the DGGM+E-DSAM hot path",
         "value": round(value, 2),
@@ -899,10 +910,10 @@ def main():
                                f"DGGM, fwd+bwd + AdamW), {args.width}x{args.height}, batch {B}/GPU",
                    "global_batch": B * world, "height": args.height, "width": args.width,
                    "parallelism": f"dp{world}"},
-        "distributed": {"world_size": dist.get_world_size() if world > 1 else 1,
-                        "backend": (dist.get_backend() if world > 1 else None),
+        "distributed": {"world_size": dist.get_world_size() if ddp else 1,
+                        "backend": (dist.get_backend() if ddp else None),
                         "collectives_per_step": ("3 async all-reduce (grad buckets dsam2, dsam1, dsam0+DGGM) + "
-                                                 "2 broadcasts (ratio-predictor BN buffers)") if world > 1 else None},
+                                                 "2 broadcasts (ratio-predictor BN buffers)") if ddp else None},
         "optimizer": ("AdamW (lr 1e-5, weight_decay 0.0, betas (0.9, 0.999), eps 1e-8: HF TrainingArguments defaults) on the hot-path parameters, stepped inside the backward; "
                       "no gradient-norm clip: the reference Trainer's max_grad_norm=1.0 clips the norm of the whole "
                       "model's gradients (37.3 M parameters, most of them outside this path)"),
@@ -922,22 +933,22 @@ def main():
         "inference_img_s": inf,
         "kernel_ms": per,
         "roofline": {"bound": "mfma", "kernel": "k_rp_conv3x3 (3x3 128->256, custom_model.py:1413)",
-                     "achieved": round(achieved_line, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved_line / MFMA_BF16_PEAK_TFLOPS, 4),
+                     "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
+                     "events_avg_us": round(conv_avg_ms * 1e3, 2), "events_launches": conv_launches,
                      "frac_profile": None if achieved_prof is None else round(achieved_prof / MFMA_BF16_PEAK_TFLOPS, 4),
                      "profile_avg_us": None if prof is None else round(prof[0] / 1e3, 2),
                      "profile_source": None if prof is None else prof[1],
-                     "achieved_events": round(achieved, 1),
-                     "frac_events": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
-                     "events_avg_us": round(conv_avg_ms * 1e3, 2),
+                     "profile_vs_events": None if prof is None else round(prof[0] / 1e6 / conv_avg_ms, 4),
                      "traffic": None if traffic is None else round(traffic[0]),
                      "traffic_unit": "bytes/launch", "traffic_source": None if traffic is None else traffic[1],
                      "algorithmic_bytes": (128 + 256) * 2 * B * args.height * args.width,
-                     "timing": ("achieved / frac: conv5's algorithmic FLOP per launch over its average duration in "
-                                "the newest committed rocprofv3 kernel trace of this bench step (profile_source; "
-                                "reproducible from profiles/); *_events: HIP events around each conv5 launch on "
-                                "its stream over this run's eager timed steps, no profiler attached (the "
-                                "profiler costs the kernel ~5 %, DESIGN.md §5.8.1)")},
+                     "timing": ("achieved / frac: conv5's algorithmic FLOP per launch over its average duration "
+                                "measured in THIS run by HIP events around each conv5 launch on its stream over the "
+                                "eager timed steps (events_launches launches, no profiler attached); frac_profile: "
+                                "the same FLOP over the average in the committed rocprofv3 trace of this tree's "
+                                "bench step (profile_source, bench.EVIDENCE_DIR; the profiler costs the kernel a "
+                                "few per cent, DESIGN.md §5.8.1); profile_vs_events = the two averages' ratio")},
         "kernels": fracs,
     }
     if rank == 0 and args.parity:
@@ -959,7 +970,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(ctx, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if ddp:
         dist.barrier()
         dist.destroy_process_group()
 

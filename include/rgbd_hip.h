@@ -346,6 +346,13 @@ size_t rgbd_ratio_features_offset(int dtype, int B, int H, int W);
 int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        unsigned long long* seed_counter, float* ratio, void* ws, void* stream);
+/* The same with option bits: RGBD_RATIO_F_PHASE2 runs the bf16 train mode's gated features
+ * through the phase-2 recompute (stem + fusion) instead of the gate kernel over phase 1's stored
+ * fusion output — the same values by another route, for tests that compare the two. */
+#define RGBD_RATIO_F_PHASE2 1
+int rgbd_ratio_forward_ex(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
+                          int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
+                          unsigned long long* seed_counter, float* ratio, void* ws, int flags, void* stream);
 
 /* ---------------------------------------------------------------- f3 point-sampled mask terms
  * The mask terms of the Mask2Former matcher and loss (transformers 5.15 modeling_mask2former.py,

@@ -134,6 +134,8 @@ SIGNATURES = {
     "rgbd_ratio_features_offset": (_SZ, [_I, _I, _I, _I]),
     "rgbd_ratio_forward": (_I, [_I, _I, ctypes.c_float, _P, _LL, _I, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P,
                                 _P, _P]),
+    "rgbd_ratio_forward_ex": (_I, [_I, _I, ctypes.c_float, _P, _LL, _I, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P,
+                                   _P, _I, _P]),
 }
 
 # the diagnostic build's extra entry points (include/rgbd_hip_diag.h; librgbd_hip_diag.so via

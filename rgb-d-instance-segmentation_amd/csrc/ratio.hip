@@ -298,6 +298,11 @@ inline StemGeom stem_geom(int B, int H, int W) {
   return g;
 }
 inline bool stem_moments_ok(int H, int W) { return H >= 8 && W >= 8; }
+// The row-kind chunk that writes the right corner cells: the one holding anchor column W - 3.
+// Its strip (columns a0 - 6 .. a0 + SF_CH + 5) then covers every in-image column the three
+// right anchors' lag windows reach (W - 9 .. W - 1); the last chunk does not when it holds
+// fewer than three columns (W % 64 in {1, 2}).
+__host__ __device__ __forceinline__ int stem_right_chunk(int W) { return (W - 3) / SF_CH; }
 
 // bf16-rounded depth value (c, y, x) of image b, 0 outside: the load always reads an in-range
 // element (clamped) and the value is selected after it, so loads issued together stay in flight
@@ -373,18 +378,18 @@ __device__ __forceinline__ void stem_frame_body(const float* __restrict__ depth3
     }
 #pragma unroll
     for (int q = 0; q < 13; ++q) o[t * 13 + q] = acc[q];
-    if (rows) {  // corner cells: the three left (first chunk) / right (last chunk) anchor columns
+    if (rows) {  // corner cells: the three left (first chunk) / right anchor columns
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
-        const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
-        if (!mine) continue;
+        if (chunk != (side == 0 ? 0 : stem_right_chunk(W))) continue;
         float* cl = cells + (((long long)kind * 2 + side) * B + b) * SC_REC;
 #pragma unroll
         for (int ci = 0; ci < 3; ++ci) {
           const int a = side == 0 ? ci : W - 3 + ci - a0;
           const float x1 = S[c1][6 + j][6 + a];
+          // strip index a + q = column a0 + a + q - 6; past the strip's end the column is >= W (0)
 #pragma unroll
-          for (int q = 0; q < 13; ++q) cl[(t * 13 + q) * 3 + ci] = x1 * S[c2][j + s1][a + q];
+          for (int q = 0; q < 13; ++q) cl[(t * 13 + q) * 3 + ci] = a + q < SF_AL ? x1 * S[c2][j + s1][a + q] : 0.f;
         }
       }
     }
@@ -397,8 +402,7 @@ __device__ __forceinline__ void stem_frame_body(const float* __restrict__ depth3
     const int e = t - SF_T - 9, c = e / 9, j = (e / 3) % 3, ci = e % 3;
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
-      const bool mine = side == 0 ? chunk == 0 : a0 + nal == W;
-      if (!mine) continue;
+      if (chunk != (side == 0 ? 0 : stem_right_chunk(W))) continue;
       const int a = side == 0 ? ci : W - 3 + ci - a0;
       cells[(((long long)kind * 2 + side) * B + b) * SC_REC + SF_T * 39 + e] = S[c][6 + j][6 + a];
     }
@@ -2542,7 +2546,7 @@ inline Ws make_ws(int es, int B, int H, int W) {
 template <typename T>
 int ratio_forward(int training, float momentum, const float* depth3, long long bstride, int B, int H, int W,
                   const char* blob, const BnPtrs& bn, unsigned long long seed, unsigned long long* seed_ctr,
-                  float* ratio, char* ws, hipStream_t s) {
+                  float* ratio, char* ws, int flags, hipStream_t s) {
   const Layout L = make_layout(sizeof(T));
   const Ws w = make_ws(sizeof(T), B, H, W);
   float2* aff1 = (float2*)(ws + w.aff1);
@@ -2597,10 +2601,9 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate
-  // RGBD_RATIO_PHASE2=1 (read per call): train mode through phase 2 instead of the gate kernel
-  // (a test compares the two paths' gated features)
-  const char* ph2 = getenv("RGBD_RATIO_PHASE2");
-  const bool gate = v2 && training && !(ph2 && atoi(ph2) != 0);
+  // flags & RGBD_RATIO_F_PHASE2: train mode through phase 2 instead of the gate kernel (a test
+  // compares the two paths' gated features)
+  const bool gate = v2 && training && !(flags & RGBD_RATIO_F_PHASE2);
   bf16_t* fus = (bf16_t*)y;
   if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, gate ? (void*)fus : nullptr);
   k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, nslab_ch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
@@ -2739,6 +2742,14 @@ size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W) {
 int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        unsigned long long* seed_counter, float* ratio, void* ws, void* stream) {
+  return rgbd_ratio_forward_ex(dtype, training, momentum, depth3, batch_stride, B, H, W, packed, bn_host, seed,
+                               seed_counter, ratio, ws, 0, stream);
+}
+
+int rgbd_ratio_forward_ex(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
+                          int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
+                          unsigned long long* seed_counter, float* ratio, void* ws, int flags, void* stream) {
+  RGBD_REQUIRE((flags & ~RGBD_RATIO_F_PHASE2) == 0, RGBD_E_ARG);
   RGBD_REQUIRE(depth3 && packed && bn_host && ratio && ws, RGBD_E_ARG);
   RGBD_REQUIRE(B > 0 && H > 0 && W > 0, RGBD_E_ARG);
   RGBD_REQUIRE(B <= 32, RGBD_E_SHAPE);  // k_rp_tail_fc1 / k_rp_tail_head hold the batch in LDS
@@ -2751,10 +2762,10 @@ int rgbd_ratio_forward(int dtype, int training, float momentum, const float* dep
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RGBD_F32)
     return ratio_forward<float>(training, momentum, depth3, batch_stride, B, H, W, (const char*)packed, bn, seed,
-                                seed_counter, ratio, (char*)ws, s);
+                                seed_counter, ratio, (char*)ws, flags, s);
   if (dtype == RGBD_BF16)
     return ratio_forward<bf16_t>(training, momentum, depth3, batch_stride, B, H, W, (const char*)packed, bn, seed,
-                                 seed_counter, ratio, (char*)ws, s);
+                                 seed_counter, ratio, (char*)ws, flags, s);
   return RGBD_E_DTYPE;
 }
 

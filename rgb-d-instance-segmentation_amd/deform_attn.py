@@ -66,6 +66,15 @@ class MSDALocationsFunction(torch.autograd.Function):
         return gref, goff, None
 
 
+def location_norm(spatial_shapes_list, dtype, device):
+    """The (w, h) normaliser of every level as float32 for rgbd_msda_locations.  The reference
+    divides the offsets by an int64 tensor (modeling_mask2former.py:994-1001), which torch first
+    casts to the offsets' dtype: for bf16 offsets a level size bf16 cannot hold (odd sizes above
+    256) is rounded to bf16 the same way here."""
+    rnd = (lambda v: float(torch.tensor(float(v)).to(dtype)))
+    return ops.device_const([[rnd(w), rnd(h)] for h, w in spatial_shapes_list], torch.float32, device)
+
+
 def multi_scale_deformable_attention(value, value_spatial_shapes, sampling_locations, attention_weights):
     """Drop-in for the reference function of the same name (same arguments, same output)."""
     return MSDeformAttnFunction.apply(value, value_spatial_shapes, sampling_locations, attention_weights)
@@ -89,8 +98,7 @@ class HipMSDeformAttn(_HFMSDA):
         weights = self.attention_weights(hidden_states).view(B, Q, self.n_heads, self.n_levels * self.n_points)
         weights = nn.functional.softmax(weights, -1).view(B, Q, self.n_heads, self.n_levels, self.n_points)
         if reference_points.shape[-1] == 2 and offsets.dtype in (torch.float32, torch.bfloat16):
-            norm = ops.device_const([[float(w), float(h)] for h, w in spatial_shapes_list], torch.float32,
-                                    reference_points.device)
+            norm = location_norm(spatial_shapes_list, offsets.dtype, reference_points.device)
             loc = MSDALocationsFunction.apply(reference_points, offsets, norm)
         elif reference_points.shape[-1] == 2:
             norm = ops.device_const([[w, h] for h, w in spatial_shapes_list], torch.long, reference_points.device)

@@ -8,44 +8,24 @@ sync and one CPU solve per image per output.
 
 ``HipHungarianMatcher`` draws the same ``torch.rand`` points in the same order, builds every
 image's cost on the GPU kernels of point_loss.py (sampling, pair-wise CE / dice, clamping in one
-launch for all images; ``matching_cost`` keeps the reference's torch form as the checker) and
+launch for all images; tests/checkers/matching_cost.py keeps the reference's torch form as the
+checker) and
 solves all images' matrices in one ``rgbd_lsa_batch`` launch (csrc/lsap.hip: scipy's algorithm in float64, same
 optimum including ties).  The matched indices stay on the GPU as int64 tensors, which the loss
 indexes with directly.  ``install(model)`` swaps the class of every HF matcher in place.
 """
 import torch
 from torch import nn
-from transformers.models.mask2former.modeling_mask2former import (Mask2FormerHungarianMatcher,
-                                                                  pair_wise_dice_loss,
-                                                                  pair_wise_sigmoid_cross_entropy_loss,
-                                                                  sample_point)
+from transformers.models.mask2former.modeling_mask2former import Mask2FormerHungarianMatcher
 
 from . import ops
-
-
-def matching_cost(matcher, masks_queries_logits, class_queries_logits, mask_labels, class_labels, i):
-    """Cost matrix of image i, as the reference builds it (modeling_mask2former.py:445-470)."""
-    probs = class_queries_logits[i].softmax(-1)
-    pred = masks_queries_logits[i]
-    c_class = -probs[:, class_labels[i]]
-    tgt = mask_labels[i].to(pred)[:, None]
-    pred = pred[:, None]
-    pts = torch.rand(1, matcher.num_points, 2, device=pred.device)
-    tgt = sample_point(tgt, pts.repeat(tgt.shape[0], 1, 1), align_corners=False).squeeze(1)
-    pred = sample_point(pred, pts.repeat(pred.shape[0], 1, 1), align_corners=False).squeeze(1)
-    c_mask = pair_wise_sigmoid_cross_entropy_loss(pred, tgt)
-    c_dice = pair_wise_dice_loss(pred, tgt)
-    cost = matcher.cost_mask * c_mask + matcher.cost_class * c_class + matcher.cost_dice * c_dice
-    cost = torch.minimum(cost, torch.tensor(1e10))
-    cost = torch.maximum(cost, torch.tensor(-1e10))
-    return torch.nan_to_num(cost, 0)
 
 
 class HipHungarianMatcher(Mask2FormerHungarianMatcher):
     @torch.no_grad()
     def forward(self, masks_queries_logits, class_queries_logits, mask_labels, class_labels):
         # point sampling + pair-wise CE / dice of all images on the GPU kernels (point_loss.py),
-        # the same torch.rand draws as the reference; matching_cost above is the torch form
+        # the same torch.rand draws as the reference (the torch form: tests/checkers/matching_cost.py)
         from .point_loss import match_costs
         costs = match_costs(self, masks_queries_logits, class_queries_logits, mask_labels, class_labels)
         return ops.linear_sum_assignment_batch(costs)

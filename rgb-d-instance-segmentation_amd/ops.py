@@ -48,6 +48,9 @@ def _need_cuda(*ts):
             raise RuntimeError("rgbd_amd ops expect contiguous tensors")
 
 
+_ws_zeroed = set()  # keys of the workspaces whose contents calls rely on (counters left at zero)
+
+
 def _workspace(dev, nbytes: int, tag: str, zeroed: bool = False):
     """Scratch buffer for one entry point, one per (device, tag, stream): launches on two
     streams never share one, and launches on one stream are ordered.  Never freed (see
@@ -61,6 +64,8 @@ def _workspace(dev, nbytes: int, tag: str, zeroed: bool = False):
         alloc = torch.zeros if zeroed else torch.empty
         buf = alloc(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
         _ws_cache[key] = buf
+    if zeroed:
+        _ws_zeroed.add(key)
     return buf
 
 
@@ -113,6 +118,21 @@ def device_const(values, dtype, device):
     if cap:
         _pinned.add(key)
     return t
+
+
+def device_vec(values, dtype, device):
+    """A device tensor of ``values`` (a number or a flat list) that change from call to call
+    (per-batch counts and offsets):
+    copied from pinned memory without blocking the host or draining the stream.  Under graph
+    capture a copy from host memory would replay stale bytes, so there the shared constant of
+    the same values (device_const, made by the eager warm-up step) is used."""
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    if device.type != "cuda" or capturing():
+        return device_const(values, dtype, device)
+    # the caching host allocator keeps the pinned block until the copy has run
+    return torch.tensor(values, dtype=dtype).pin_memory().to(device, non_blocking=True)
 
 
 _hc_local = threading.local()

@@ -22,7 +22,7 @@ from transformers.models.mask2former.modeling_mask2former import Mask2FormerHung
 
 from . import _lib
 from ._lib import RGBD_BF16, RGBD_F32, check
-from .ops import LsaResult, _need_cuda, _p, _stream, device_const
+from .ops import LsaResult, _need_cuda, _p, _stream, device_const, device_vec
 
 # loss_masks' uncertainty top-k: unsorted by default (the loss terms are sums over the point set,
 # so only the float summation order changes; the segmented sort cost ~2.4 ms per whole-model
@@ -190,17 +190,17 @@ def match_costs(matcher, masks_queries_logits, class_queries_logits, mask_labels
     if toff[-1]:
         tgt = torch.empty((toff[-1], P), dtype=torch.float32, device=dev)
         th, tw = rows.shape[-2:]
+        som = device_vec(set_of_map, torch.int32, dev)  # held until the launch is enqueued
         check(_lib.lib().rgbd_point_sample_sets(RGBD_F32, _p(rows), toff[-1], th, tw, _p(pts.contiguous()),
-                                                _p(device_const(set_of_map, torch.int32, dev)), P, _p(tgt),
-                                                _stream(dev)), "rgbd_point_sample_sets")
+                                                _p(som), P, _p(tgt), _stream(dev)), "rgbd_point_sample_sets")
     else:
         tgt = torch.zeros((1, P), device=dev)
     labels = labels_all(class_labels, dev)
     if labels.numel() == 0:
         labels = torch.zeros((1,), dtype=torch.long, device=dev)
     cost = torch.empty((max(coff[-1], 1),), dtype=torch.float32, device=dev)
-    toff_t = device_const(toff, torch.int32, dev)
-    coff_t = device_const(coff[:-1], torch.int64, dev)
+    toff_t = device_vec(toff, torch.int32, dev)
+    coff_t = device_vec(coff[:-1], torch.int64, dev)
     check(_lib.lib().rgbd_match_cost_probs(_p(pred), B, Q, P, _p(tgt), _p(toff_t), _p(probs), probs.shape[-1],
                                            _p(labels), _p(coff_t), float(matcher.cost_mask), float(matcher.cost_class),
                                            float(matcher.cost_dice), _p(cost), _stream(dev)), "rgbd_match_cost_probs")
@@ -226,8 +226,8 @@ def _match_costs_per_image(matcher, masks_queries_logits, class_queries_logits, 
     tgt = torch.cat(tgts) if toff[-1] else torch.zeros((1, P), device=dev)
     cls = torch.cat(ccls) if coff[-1] else torch.zeros((1,), device=dev)
     cost = torch.empty((max(coff[-1], 1),), dtype=torch.float32, device=dev)
-    toff_t = device_const(toff, torch.int32, dev)
-    coff_t = device_const(coff[:-1], torch.int64, dev)
+    toff_t = device_vec(toff, torch.int32, dev)
+    coff_t = device_vec(coff[:-1], torch.int64, dev)
     check(_lib.lib().rgbd_match_cost(_p(pred), B, Q, P, _p(tgt), _p(toff_t), _p(cls), _p(coff_t),
                                      float(matcher.cost_mask), float(matcher.cost_class), float(matcher.cost_dice),
                                      _p(cost), _stream(dev)), "rgbd_match_cost")
@@ -268,7 +268,7 @@ class HipMask2FormerLoss(Mask2FormerLoss):
             distributed = False
         if distributed:
             return super().get_num_masks(class_labels, device)
-        num_masks = device_const(float(sum(len(c) for c in class_labels)), torch.float32, device)
+        num_masks = device_vec(float(sum(len(c) for c in class_labels)), torch.float32, device)
         return torch.clamp(num_masks, min=1)
 
     def _target_rows(self, mask_labels, dtype):
@@ -279,15 +279,14 @@ class HipMask2FormerLoss(Mask2FormerLoss):
         every match is a cached constant of the per-image counts, the query indices a view."""
         if isinstance(indices, LsaResult) and indices.rows_all is not None:
             dev = indices.rows_all.device
-            batch = device_const([i for i, n in enumerate(indices.counts) for _ in range(n)] or [0], torch.long, dev)
+            batch = device_vec([i for i, n in enumerate(indices.counts) for _ in range(n)] or [0], torch.long, dev)
             return batch[:len(indices.rows_all)], indices.rows_all
         return super()._get_predictions_permutation_indices(indices)
 
     def _target_flat(self, indices, offs, dev):
         """Row index of every match's target among all images' targets (image offset + column)."""
         if isinstance(indices, LsaResult) and indices.cols_all is not None:
-            shift = device_const([offs[i] for i, n in enumerate(indices.counts) for _ in range(n)] or [0],
-                                 torch.long, dev)
+            shift = device_vec([offs[i] for i, n in enumerate(indices.counts) for _ in range(n)] or [0], torch.long, dev)
             return indices.cols_all + shift[:len(indices.cols_all)]
         return (torch.cat([j.to(dev) + offs[i] for i, (_, j) in enumerate(indices)]) if indices else
                 torch.zeros((0,), dtype=torch.long, device=dev))

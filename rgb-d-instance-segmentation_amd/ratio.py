@@ -92,7 +92,9 @@ def ratio_predictor_forward(module, depth_image: torch.Tensor) -> torch.Tensor:
         # increments them before normalising; here ahead of the kernels, off the ratio's critical path)
         with torch.no_grad():
             torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
-    check(L.rgbd_ratio_forward(code, int(training), ctypes.c_float(momentum), ctypes.c_void_p(d.data_ptr()),
-                               d.stride(0), B, H, W, _p(blob), bn_arr, ctypes.c_ulonglong(module._rgbd_dropout_seed),
-                               _p(ctr), _p(ratio), _p(ws), _stream(d.device)), "rgbd_ratio_forward")
+    # test hook: "phase2" computes the bf16 train-mode gated features by the phase-2 recompute
+    flags = 1 if getattr(module, "train_route", "gate") == "phase2" else 0  # RGBD_RATIO_F_PHASE2
+    check(L.rgbd_ratio_forward_ex(code, int(training), ctypes.c_float(momentum), ctypes.c_void_p(d.data_ptr()),
+                                  d.stride(0), B, H, W, _p(blob), bn_arr, ctypes.c_ulonglong(module._rgbd_dropout_seed),
+                                  _p(ctr), _p(ratio), _p(ws), flags, _stream(d.device)), "rgbd_ratio_forward_ex")
     return ratio.reshape(B, 1)

@@ -4,7 +4,7 @@ from pathlib import Path
 import pytest
 
 REPO = Path(__file__).resolve().parents[1]
-for p in (str(REPO), str(REPO / "tests" / "golden")):
+for p in (str(REPO), str(REPO / "tests"), str(REPO / "tests" / "golden")):
     if p not in sys.path:
         sys.path.insert(0, p)
 import _rgbd_import  # noqa: E402,F401

@@ -25,6 +25,8 @@ REPO = Path(__file__).resolve().parents[1]
 
 
 def _need_devices(backend, world=2):
+    if world == 1 and backend != "nccl":
+        pytest.skip("world 1 exercises the RCCL path only")
     if backend == "nccl" and torch.cuda.device_count() < world:
         pytest.skip(f"RCCL needs one device per rank: this box shows fewer than {world} GPUs")
 
@@ -34,14 +36,16 @@ BACKENDS = ["gloo", "nccl"]
 
 @pytest.mark.timeout(400)
 @pytest.mark.parametrize("backend", BACKENDS)
-@pytest.mark.parametrize("world,H,W", [(2, 96, 128), (2, 480, 640), (8, 96, 128), (8, 480, 640)],
-                         ids=["w2_96x128", "C3_w2_640x480", "w8_96x128", "C4_w8_640x480"])
+@pytest.mark.parametrize("world,H,W", [(1, 480, 640), (2, 96, 128), (2, 480, 640), (8, 96, 128), (8, 480, 640)],
+                         ids=["w1_640x480", "w2_96x128", "C3_w2_640x480", "w8_96x128", "C4_w8_640x480"])
 def test_bench_launcher_json(world, H, W, backend):
     """bench.py --gpus N end to end (its own launcher, 8 images per rank) at BASELINE's C3 (2 ranks,
     global batch 16) and C4 (8 ranks, global batch 64); gloo with every rank on the test box's one
-    GPU, or RCCL with one rank per GPU."""
+    GPU, or RCCL with one rank per GPU.  World 1 over RCCL (``--ddp 1``): the process group, the
+    overlapped all-reduces and their stream waits and the buffer broadcasts on a one-GPU box."""
     _need_devices(backend, world)
-    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", str(world), "--backend", backend, "--steps", "2",
+    extra = ["--ddp", "1"] if world == 1 else []
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", str(world), *extra, "--backend", backend, "--steps", "2",
                         "--warmup", "1", "--cpu-baseline", "0", "--c5-stream", "0", "--inference", "0", "--parity", "0",
                         "--height", str(H), "--width", str(W)],
                        capture_output=True, text=True, timeout=380, cwd=REPO)
@@ -90,7 +94,7 @@ def _worker(rank, world, port, q, shape, backend):
         # the DDP step of this rank
         ctx = bench.build(args, dev, rank=rank)
         ctx["rp"].eval()
-        fb, _, _, _ = bench.make_parts(ctx, world)
+        fb, _, _, _ = bench.make_parts(ctx, world, ddp=True)
         fb()
         got = [p.grad for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
         grad_err = max(float(((a - e).abs().max() / (e.abs().max() + 1e-12))) for a, e in zip(got, mean))
@@ -104,7 +108,7 @@ def _worker(rank, world, port, q, shape, backend):
                     b.add_(0.5 * rank)
         seen = {}
         ctx["rp"].register_forward_pre_hook(lambda m, a: seen.__setitem__("bufs", [b.clone() for b in m.buffers()]))
-        fb, _, _, _ = bench.make_parts(ctx, world)
+        fb, _, _, _ = bench.make_parts(ctx, world, ddp=True)
         fb()
         flat = torch.cat([b.double().reshape(-1) for b in seen["bufs"]])
         flat = flat.to(dev) if backend == "nccl" else flat.cpu()
@@ -117,7 +121,7 @@ def _worker(rank, world, port, q, shape, backend):
         for overlap in (False, True):
             ctx = bench.build(args, dev, rank=rank)
             ctx["rp"].eval()
-            fb, ostep, _, _ = bench.make_parts(ctx, world, overlap_opt=overlap)
+            fb, ostep, _, _ = bench.make_parts(ctx, world, overlap_opt=overlap, ddp=True)
             for _ in range(2):
                 fb()
                 ostep()
@@ -133,8 +137,9 @@ def _worker(rank, world, port, q, shape, backend):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("backend", BACKENDS)
-@pytest.mark.parametrize("world,shape", [(2, (96, 128, 3)), (2, (480, 640, 8)), (8, (96, 128, 3)), (8, (480, 640, 8))],
-                         ids=["w2_96x128_b3", "C3_w2_640x480_b8", "w8_96x128_b3", "C4_w8_640x480_b8"])
+@pytest.mark.parametrize("world,shape", [(1, (480, 640, 8)), (2, (96, 128, 3)), (2, (480, 640, 8)), (8, (96, 128, 3)),
+                                         (8, (480, 640, 8))],
+                         ids=["w1_640x480_b8", "w2_96x128_b3", "C3_w2_640x480_b8", "w8_96x128_b3", "C4_w8_640x480_b8"])
 def test_ddp_step_gradients_and_buffers(world, shape, backend):
     """Small shape, and BASELINE configs[2] / [3] (C3 / C4) at their workload: 640x480, 8 images per
     rank, bf16, world size 2 / 8 (global batch 16 / 64) — gloo with every rank on the one GPU of the

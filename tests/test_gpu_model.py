@@ -14,6 +14,7 @@ from rgbd_amd import deform_attn, init as winit, mask_predictor, masked_attentio
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+BF16_UNFORCED_REL_TOL = 4.5e-2  # G5 bf16 hot path, own attention masks
 PRE = "model.pixel_level_module.ratio_predictor."
 
 
@@ -106,14 +107,16 @@ def test_bf16_train_mode_batchnorm_stats(H, W):
             assert rel <= 5e-2, (k, rel)
 
 
-@pytest.mark.parametrize("H,W", [(240, 320), (90, 125), (480, 640), (7, 9)])
+@pytest.mark.parametrize("H,W", [(240, 320), (90, 125), (480, 640), (7, 9), (90, 129), (66, 130), (40, 65)])
 def test_bf16_stem_bn_batch_stats_exact(H, W):
     """The stem BatchNorms' batch statistics in bf16 train mode come from the moments of the 7x7x3
     depth windows (k_stem_lag with its border workgroups / k_stem_sums / k_stem_s2 / k_stem_bn: lag correlations + border
     corrections, double), not from a pass over the stem — against float64 arithmetic on the same
     bf16-rounded depth and stem weights: batch mean to 2e-6 of the channel scale, unbiased
     variance to 2e-5 relative (read back from the running-stat update, momentum 0.1).  (7, 9):
-    below the moments path's minimum size, the former statistics pass."""
+    below the moments path's minimum size, the former statistics pass.  (90, 129), (66, 130),
+    (40, 65): W % 64 in {1, 2}, where the last 64-column border chunk holds fewer than three
+    columns and the right corner cells come from the chunk holding column W - 3."""
     import torch.nn.functional as F
     pv = gi.pixel_values(8, 2, H, W)[:, 3:6]
     m = _ratio_module()
@@ -145,22 +148,22 @@ def test_bf16_stem_bn_batch_stats_exact(H, W):
 
 @pytest.mark.parametrize("H,W", [(64, 96), (90, 125), (240, 320)])
 @pytest.mark.parametrize("path", ["gate", "phase2"])
-def test_bf16_train_mode_gated_features(H, W, path, monkeypatch):
+def test_bf16_train_mode_gated_features(H, W, path):
     """The train-mode gated features (fused * attention(fused), custom_model.py:1469-1470, the
     conv5 input) read from the ratio workspace, against the PyTorch-CPU fp32 module tree in
     train mode, for both bf16 routes: k_rp_gate over phase 1's stored raw fusion output (the
-    default) and phase 2's stem + fusion recompute (RGBD_RATIO_PHASE2=1).  Aligned (64x96,
+    default) and phase 2's stem + fusion recompute (RGBD_RATIO_F_PHASE2).  Aligned (64x96,
     240x320) and ragged (90x125) shapes.  Tolerance on the features themselves: bf16 operands
     and a bf16-stored fusion output against f32 — max |diff| <= 3e-2 of max |ref|, mean |diff|
     <= 1e-2 of mean |ref| (a fragment-order slip moves whole channel/pixel blocks and fails
     both by orders of magnitude)."""
     from rgbd_amd import _lib, ops
-    monkeypatch.setenv("RGBD_RATIO_PHASE2", "1" if path == "phase2" else "0")
     B = 2
     pv = gi.pixel_values(12, B, H, W)
     m_cpu = _ratio_module().train()
     m = copy.deepcopy(m_cpu)
     m.compute_dtype = torch.bfloat16
+    m.train_route = path
     m = m.to(DEV).train()
     x = torch.from_numpy(pv).to(DEV)[:, 3:6]
     m(x)
@@ -309,7 +312,8 @@ def test_full_model_mask_logits_bf16(golden):
           f"{first['unexplained']} unexplained)")
     assert runs[True][0] < bench.BF16_LOGIT_REL_TOL  # the bench line's bound (parity.bf16.tolerance_rel)
     assert first["unexplained"] == 0
-    assert runs[False][0] < 5 * bench.BF16_LOGIT_REL_TOL
+    # measured 2.11e-2 (7 flipped bits at the first flipped call, all explained): ~2x headroom
+    assert runs[False][0] < BF16_UNFORCED_REL_TOL
 
 
 def test_full_model_grads_fp32(golden):

@@ -131,14 +131,16 @@ def test_hip_msda_module_matches_hf():
         assert float((gp_h[n] - gp_r[n]).abs().max()) / (float(gp_r[n].abs().max()) + 1e-12) < 1e-4, n
 
 
+@pytest.mark.parametrize("shapes", [[(60, 80), (30, 40), (15, 20)], [(257, 515), (129, 258), (65, 129)]],
+                         ids=["c1", "wide"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-def test_msda_locations_bitwise(dt):
+def test_msda_locations_bitwise(dt, shapes):
     """rgbd_msda_locations: ref + offsets / norm (the two-coordinate reference points, :990-994)
     with torch's dtype rules — the same bits forward, and the offsets' gradient of torch's
-    expression bitwise."""
+    expression bitwise.  "wide": level sizes above 256 that bf16 cannot hold (257, 515, 258 ...),
+    which torch rounds to bf16 before dividing bf16 offsets (deform_attn.location_norm)."""
     g = torch.Generator(device=DEV).manual_seed(4)
     B, Q, NH, L, P = 2, 777, 8, 3, 4
-    shapes = [(60, 80), (30, 40), (15, 20)]
     ref = torch.rand((B, Q, L, 2), generator=g, device=DEV)
     off = (torch.randn((B, Q, NH, L, P, 2), generator=g, device=DEV) * 3).to(dt)
     norm_l = ops.device_const([[w, h] for h, w in shapes], torch.long, DEV)
@@ -147,7 +149,7 @@ def test_msda_locations_bitwise(dt):
     gl = torch.randn(want.shape, generator=g, device=DEV)
     want.backward(gl)
     o2 = off.clone().requires_grad_()
-    norm_f = ops.device_const([[float(w), float(h)] for h, w in shapes], torch.float32, DEV)
+    norm_f = deform_attn.location_norm(shapes, dt, DEV)
     got = deform_attn.MSDALocationsFunction.apply(ref, o2, norm_f)
     got.backward(gl)
     assert got.dtype == want.dtype == torch.float32

@@ -1,7 +1,7 @@
 """f3: the point-sampled mask terms on the GPU kernels (csrc/point_loss.hip, rgbd_amd/point_loss.py)
 against the library code the reference trains through (transformers 5.15
 modeling_mask2former.py): sample_point (:245-275) and its autograd, the matcher's cost matrices
-(:445-470, restated op for op in matcher.matching_cost) and Mask2FormerLoss.loss_masks
+(:445-470, restated op for op in tests/checkers/matching_cost.py) and Mask2FormerLoss.loss_masks
 (:580-630) with its gradient.  Same torch RNG state on both sides, so the same random points.
 Tolerances: float32 reductions in a different order — 1e-5 relative on sampled values, 1e-5 relative on
 costs and losses, 1e-4 relative on gradients."""
@@ -63,7 +63,8 @@ def test_match_costs_match_reference(seed):
     m = Mask2FormerHungarianMatcher(cost_class=2.0, cost_mask=5.0, cost_dice=5.0, num_points=12544)
     masks, classes, ml, cl = _case(seed)
     torch.manual_seed(21 + seed)
-    ref = [matcher.matching_cost(m, masks, classes, ml, cl, i) for i in range(masks.shape[0])]
+    from checkers.matching_cost import matching_cost
+    ref = [matching_cost(m, masks, classes, ml, cl, i) for i in range(masks.shape[0])]
     torch.manual_seed(21 + seed)
     got = point_loss.match_costs(m, masks, classes, ml, cl)
     for r, h in zip(ref, got):
