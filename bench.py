@@ -508,20 +508,23 @@ FLIP_EXPLAIN_FACTOR = 4.0  # a flipped attention bit is explained when |ref logi
 class ReferenceMasks:
     """The reference's attention masks at every mask-predictor call of the masked-attention
     decoder (tests/golden/g9_attn_masks.npz, made by importing the reference: make_golden.py
-    attn), for the G5 (320x240) or G7 (640x480) input.  ``attach(model, force)`` hooks the
-    model's mask predictor (HF modeling_mask2former.py:1896-1933 feeds its second output to the
-    next decoder layer) and records per call the model's own mask (head 0) and its
+    attn; tag "g6": the G6 training forward's, stored in g6_grads.npz), for the G5 (320x240),
+    G7 (640x480) or G6 (320x240, batch 2) input.  ``attach(model, force)`` hooks the model's mask
+    predictor (HF modeling_mask2former.py:1896-1933 feeds its second output to the next decoder
+    layer) and records per call the model's own mask (head 0 of every image) and its
     interpolated logits at the fixture's near-threshold positions; with ``force`` the reference's
     mask replaces the model's, so every decoder layer sees the reference's attention pattern and
     the remaining logit error is arithmetic only."""
 
-    def __init__(self, tag):
-        z = np.load(G9_ATTN, allow_pickle=False)
-        self.input_sha = str(z[f"{tag}_input_sha"])
+    def __init__(self, tag, path=None):
+        path = path or (REPO / "tests" / "golden" / "g6_grads.npz" if tag == "g6" else G9_ATTN)
+        z = np.load(path, allow_pickle=False)
+        self.input_sha = str(z[f"{tag}_input_sha"]) if f"{tag}_input_sha" in z else str(z["input_sha"])
         self.calls = []
         for c in range(int(z[f"{tag}_ncalls"])):
-            Q, L = (int(v) for v in z[f"{tag}_c{c}_shape"])
-            bits = np.unpackbits(z[f"{tag}_c{c}_bits"], count=Q * L).astype(bool).reshape(Q, L)
+            shape = tuple(int(v) for v in z[f"{tag}_c{c}_shape"])
+            shape = shape if len(shape) == 3 else (1,) + shape  # [B][Q][L]
+            bits = np.unpackbits(z[f"{tag}_c{c}_bits"], count=int(np.prod(shape))).astype(bool).reshape(shape)
             self.calls.append({"mask": bits, "size": tuple(int(v) for v in z[f"{tag}_c{c}_size"]),
                                "near_idx": z[f"{tag}_c{c}_near_idx"], "near_val": z[f"{tag}_c{c}_near_val"]})
 
@@ -535,17 +538,18 @@ class ReferenceMasks:
                 raise RuntimeError("more mask-predictor calls than the fixture holds")
             ref = self.calls[c]
             logits, attn = out[0], out[1]
-            if logits.shape[0] != 1:
-                raise ValueError("ReferenceMasks: batch 1 only")
+            B = logits.shape[0]
+            if B != ref["mask"].shape[0]:
+                raise ValueError(f"ReferenceMasks: batch {B}, fixture {ref['mask'].shape[0]}")
             val = F.interpolate(logits.detach().float(), size=ref["size"], mode="bilinear",
-                                align_corners=False).flatten(2)[0].reshape(-1)
+                                align_corners=False).flatten(2).reshape(-1)
             near = torch.from_numpy(ref["near_idx"]).to(val.device)
-            nh = attn.shape[0]
-            rec.append((attn.view(nh, *attn.shape[1:])[0].cpu().numpy(), val[near].cpu().numpy()))
+            nh = attn.shape[0] // B
+            rec.append((attn.view(B, nh, *attn.shape[1:])[:, 0].cpu().numpy(), val[near].cpu().numpy()))
             if not force:
                 return None
             m = torch.from_numpy(ref["mask"]).to(attn.device)
-            return logits, m[None].expand(nh, *m.shape).contiguous()
+            return logits, m[:, None].expand(B, nh, *m.shape[1:]).reshape(B * nh, *m.shape[1:]).contiguous()
         return mp.register_forward_hook(hook)
 
     def flips(self, rec, deltas=None, upto_first=False):

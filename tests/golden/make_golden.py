@@ -20,7 +20,9 @@ Fixtures (SURVEY.md §8(c) "Golden vectors"):
   g3_dggm.npz        a9: DepthGradientInjectionResidual forward at channels [4,8,16,32]
   g4_ratio.npz       a3: EnhancedDepthImageRatioPredictor eval at 240x320, B=2
   g5_model.npz       a1+a12: full model eval forward at 320x240 (ratio, logits, sampled features)
-  g6_grads.npz       one loss.backward() at 320x240 B=2 (eval mode): hot-path grad stats
+  g6_grads.npz       one loss.backward() at 320x240 B=2 (eval mode): loss + terms, the loss's
+                     torch.rand draws (sha256), matches, attention masks, sampled gradients of
+                     every grad-receiving parameter (make_golden.py g6)
   g8_resize.npz      a11 for frames not at model resolution: the processor's resize (PIL)
   g9_attn_masks.npz  the masked-attention decoder's attention masks at G5 / G7's inputs: per
                      mask-predictor call the reference's binarised mask (bit-packed, one head:
@@ -189,29 +191,7 @@ def main():
             g5[f"{tag}{k}_abs"] = np.array(np.abs(t.astype(np.float64)).sum())
     np.savez_compressed(OUT / "g5_model.npz", **g5)
 
-    pv2 = golden_inputs.pixel_values(6, 2, 240, 320)
-    labels = golden_inputs.labels(6, 2, 240, 320)
-    model.zero_grad()
-    torch.manual_seed(1234)  # the loss samples points with torch.rand (importance sampling)
-    out = model(pixel_values=torch.from_numpy(pv2),
-                mask_labels=[torch.from_numpy(m) for m in labels[0]],
-                class_labels=[torch.from_numpy(c) for c in labels[1]])
-    out.loss.backward()
-    g6 = {"input_sha": np.array(sha(pv2)), "loss": np.array(out.loss.item())}
-    names = []
-    for n, p in model.named_parameters():
-        if ".dsam" in n or "depth_gradient_injection" in n:
-            names.append(n)
-            g = p.grad.numpy().ravel()
-            idx = golden_inputs.sample_index("g6." + n, g.size, 1024)
-            g6[n + "|norm"] = np.array(float(np.linalg.norm(g.astype(np.float64))))
-            g6[n + "|sum"] = np.array(float(g.astype(np.float64).sum()))
-            g6[n + "|idx"] = idx
-            g6[n + "|val"] = g[idx]
-        elif ("ratio_predictor" in n or "pixel_level_module.encoder." in n) and p.grad is not None:
-            raise AssertionError(f"unexpected grad on {n} (Q1/Q2)")
-    g6["names"] = np.array(names)
-    np.savez_compressed(OUT / "g6_grads.npz", **g6)
+    g6_fixture(model)
 
     # ------------------------------------------------------------------ G7 (C2 shape)
     pv7 = golden_inputs.pixel_values(7, 1, 480, 640)
@@ -234,6 +214,112 @@ def main():
 
     processor_fixture()
     print("golden fixtures written to", OUT)
+
+class RandRecorder(torch.overrides.TorchFunctionMode):
+    """Records every torch.rand call of the reference's matcher and loss (the importance-sampled
+    points, modeling_mask2former.py:455, :705, :721): shape and sha256 of the values, so the GPU
+    test can replay the same draws from a CPU generator with the same seed and prove it did."""
+
+    def __init__(self):
+        super().__init__()
+        self.calls = []
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        if func is torch.rand:
+            self.calls.append((tuple(out.shape), sha(out.numpy())))
+        return out
+
+
+def record_attn_masks(model, tag, calls, out):
+    """The binarised attention mask of every mask-predictor call (one head per image: the heads
+    repeat it), bit-packed [B][Q][L], and the interpolated logits within 2e-2 of the threshold."""
+    for c, (logits, attn, size) in enumerate(calls):
+        B = logits.shape[0]
+        nh = attn.shape[0] // B
+        a = attn.view(B, nh, *attn.shape[1:])
+        assert bool((a == a[:, :1]).all()), "heads differ"
+        a0 = a[:, 0].numpy()  # [B, Q, L]
+        val = F.interpolate(logits, size=size, mode="bilinear", align_corners=False).flatten(2).numpy()
+        assert np.array_equal(a0, val < 0) or np.array_equal(a0, 1 / (1 + np.exp(-val)) < 0.5)
+        near = np.flatnonzero(np.abs(val.ravel()) < 2e-2)
+        out[f"{tag}_c{c}_shape"] = np.array(a0.shape if B > 1 else a0.shape[1:])
+        out[f"{tag}_c{c}_size"] = np.array(size)
+        out[f"{tag}_c{c}_bits"] = np.packbits(a0.ravel())
+        out[f"{tag}_c{c}_near_idx"] = near.astype(np.int64)
+        out[f"{tag}_c{c}_near_val"] = val.ravel()[near].astype(np.float32)
+    out[f"{tag}_ncalls"] = np.array(len(calls))
+
+
+def g6_fixture(model):
+    """G6: one loss.backward() of the whole model at 320x240, B=2, eval mode (no dropout, no drop
+    path, no layer drop: the only random numbers are the loss's point draws, torch.manual_seed(1234)):
+      * the loss and each of its 30 terms (3 per output, final + 9 auxiliary);
+      * every torch.rand draw (shape + sha256, RandRecorder) for the GPU test's replay;
+      * the ratio (injected on the GPU: it feeds discrete window decisions), the matched indices of
+        every matcher call and the attention masks of every mask-predictor call (tag g6);
+      * per grad-receiving parameter: norm, sum and sampled values (1 024 for the hot path's
+        DSAM / DGGM parameters, 256 for the rest) at golden_inputs.sample_index positions."""
+    pv2 = golden_inputs.pixel_values(6, 2, 240, 320)
+    labels = golden_inputs.labels(6, 2, 240, 320)
+    model.eval()
+    model.zero_grad()
+    caps, attn_calls, matches, terms = {}, [], [], {}
+    plm = model.model.pixel_level_module
+    hooks = [plm.ratio_predictor.register_forward_hook(lambda m, i, o: caps.__setitem__("ratio", o.detach().clone())),
+             model.model.transformer_module.decoder.mask_predictor.register_forward_hook(
+                 lambda m, inp, out: attn_calls.append((out[0].detach().clone(), out[1].detach().clone(), inp[2]))),
+             model.criterion.matcher.register_forward_hook(
+                 lambda m, inp, out: matches.append([(np.asarray(i), np.asarray(j)) for i, j in out]))]
+    get_loss = model.get_loss
+
+    def get_loss_rec(loss_dict):
+        terms.update({k: float(v.detach()) for k, v in loss_dict.items()})
+        return get_loss(loss_dict)
+    model.get_loss = get_loss_rec
+    rec = RandRecorder()
+    torch.manual_seed(1234)  # the loss samples points with torch.rand (importance sampling)
+    try:
+        with rec:
+            out = model(pixel_values=torch.from_numpy(pv2),
+                        mask_labels=[torch.from_numpy(m) for m in labels[0]],
+                        class_labels=[torch.from_numpy(c) for c in labels[1]])
+    finally:
+        for h in hooks:
+            h.remove()
+        del model.get_loss
+    out.loss.backward()
+    g6 = {"input_sha": np.array(sha(pv2)), "loss": np.array(out.loss.item()), "ratio": caps["ratio"].numpy(),
+          "rand_seed": np.array(1234), "rand_shapes": np.array([str(list(s)) for s, _ in rec.calls]),
+          "rand_sha": np.array([h for _, h in rec.calls]),
+          "term_names": np.array(sorted(terms)), "term_vals": np.array([terms[k] for k in sorted(terms)])}
+    g6["match_calls"] = np.array(len(matches))
+    for c, per_img in enumerate(matches):
+        for b, (i, j) in enumerate(per_img):
+            g6[f"match_{c}_{b}"] = np.stack([i, j]).astype(np.int64)
+    record_attn_masks(model, "g6", attn_calls, g6)
+    names, hot = [], []
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            if ".dsam" in n or "depth_gradient_injection" in n:
+                raise AssertionError(f"{n}: no gradient")
+            continue
+        if "ratio_predictor" in n or "pixel_level_module.encoder." in n:
+            raise AssertionError(f"unexpected grad on {n} (Q1/Q2)")
+        names.append(n)
+        is_hot = ".dsam" in n or "depth_gradient_injection" in n
+        hot.append(is_hot)
+        g = p.grad.numpy().ravel()
+        idx = golden_inputs.sample_index("g6." + n, g.size, 1024 if is_hot else 256)
+        g6[n + "|norm"] = np.array(float(np.linalg.norm(g.astype(np.float64))))
+        g6[n + "|sum"] = np.array(float(g.astype(np.float64).sum()))
+        g6[n + "|idx"] = idx
+        g6[n + "|val"] = g[idx]
+    g6["names"] = np.array([n for n, h in zip(names, hot) if h])  # the hot path's (DSAM / DGGM)
+    g6["all_names"] = np.array(names)                               # every grad-receiving parameter
+    np.savez_compressed(OUT / "g6_grads.npz", **g6)
+    model.zero_grad()
+    return g6
 
 
 def reference_processor(h, w):
@@ -383,6 +469,10 @@ if __name__ == "__main__":
     import golden_inputs  # noqa: E402
     if len(sys.argv) > 1 and sys.argv[1] == "resize":
         resize_fixture()
+    elif len(sys.argv) > 1 and sys.argv[1] == "g6":
+        torch.manual_seed(0)
+        torch.set_num_threads(8)
+        g6_fixture(build_model(import_reference()))
     elif len(sys.argv) > 1 and sys.argv[1] == "attn":
         torch.manual_seed(0)
         torch.set_num_threads(8)

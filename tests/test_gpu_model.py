@@ -15,6 +15,9 @@ from rgbd_amd import deform_attn, init as winit, mask_predictor, masked_attentio
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 BF16_UNFORCED_REL_TOL = 4.5e-2  # G5 bf16 hot path, own attention masks
+# G6 (whole-model gradients vs the reference), non-zero-class tensors: the CPU oracle (the reference
+# HF stages around the restated hot path) reaches norm 8.8e-5, sample L2 1.3e-3, max 1.4e-2 rms
+G6_NORM_REL, G6_SAMPLE_L2, G6_SAMPLE_MAX = 1e-4, 5e-3, 5e-2
 PRE = "model.pixel_level_module.ratio_predictor."
 
 
@@ -316,21 +319,111 @@ def test_full_model_mask_logits_bf16(golden):
     assert runs[False][0] < BF16_UNFORCED_REL_TOL
 
 
-def test_full_model_grads_fp32(golden):
-    g6 = golden("g6_grads")
-    m = _full_model().eval()
-    pv = torch.from_numpy(gi.pixel_values(6, 2, 240, 320)).to(DEV)
-    masks, classes = gi.labels(6, 2, 240, 320)
-    torch.manual_seed(1234)
-    out = m(pixel_values=pv, mask_labels=[torch.from_numpy(x).to(DEV) for x in masks],
-            class_labels=[torch.from_numpy(c).to(DEV) for c in classes])
+def _g6_run(m, g6, refm, force, pv, masks, classes):
+    """One G6 training forward + backward of the fp32 drop-in model on the GPU with the
+    reference's torch.rand draws replayed (tests/checkers/rand_replay.py) and, with ``force``,
+    the reference's attention masks forced into every decoder layer (bench.ReferenceMasks "g6")."""
+    from checkers.rand_replay import CpuRandReplay
+    terms, matches, rec = {}, [], []
+    get_loss = m.get_loss
+
+    def get_loss_rec(loss_dict):
+        terms.update({k: float(v.detach()) for k, v in loss_dict.items()})
+        return get_loss(loss_dict)
+    m.get_loss = get_loss_rec
+    hm = m.criterion.matcher.register_forward_hook(
+        lambda mod, inp, out: matches.append([(i.cpu().numpy(), j.cpu().numpy()) for i, j in out]))
+    h = refm.attach(m, force, rec)
+    m.zero_grad(set_to_none=True)
+    rr = CpuRandReplay(int(g6["rand_seed"]))
+    try:
+        with rr:
+            out = m(pixel_values=pv, mask_labels=[torch.from_numpy(x).to(DEV) for x in masks],
+                    class_labels=[torch.from_numpy(c).to(DEV) for c in classes])
+    finally:
+        h.remove()
+        hm.remove()
+        del m.get_loss
+    rr.check(g6)
     out.loss.backward()
-    named = dict(m.named_parameters())
-    for n in g6["names"]:
-        n = str(n)
-        g = named[n].grad.float().cpu().numpy().ravel()
-        ref_norm = float(g6[n + "|norm"])
-        assert abs(np.linalg.norm(g.astype(np.float64)) - ref_norm) <= 2e-2 * ref_norm + 1e-9, n
-    for n, p in named.items():
+    grads = {n: p.grad.detach().double().cpu().numpy().ravel() for n, p in m.named_parameters() if p.grad is not None}
+    return float(out.loss), terms, matches, grads, rec
+
+
+def test_full_model_grads_fp32(golden):
+    """The whole drop-in model's training step pinned to the reference's (G6: one loss.backward()
+    of the reference model at 320x240, B=2, eval mode, made by importing the reference:
+    make_golden.py g6), everything on the GPU in float32.
+
+    The reference's loss draws its sample points with torch.rand on the CPU generator; they are
+    replayed here (checkers/rand_replay.py, checked call by call against the fixture's sha256).
+    The ratio is compared (rtol 1e-5) and the reference's injected, as in the G5 test (a 1e-7
+    ratio difference can move a pixel across a window bound).  Two runs:
+    * reference attention masks forced into every decoder layer (arithmetic only): the loss
+      (rtol 1e-5) and each of its 30 terms (rtol 2e-5), every matcher call's assignment
+      (identical), and for EVERY grad-receiving parameter (363 tensors, 37.3 M values;
+      checkers/g6_compare.py) the gradient norm (rtol G6_NORM_REL) and the fixture's sampled
+      values (1 024 per DSAM / DGGM tensor, 256 per other tensor): relative L2 error
+      <= G6_SAMPLE_L2, every sample within G6_SAMPLE_MAX x the tensor's rms; the nine decoder
+      self-attention key biases, whose gradient is zero in exact arithmetic (the reference's is
+      1e-10 of the largest rms), as negligible as the reference's;
+    * the model's own masks: the same bounds when no attention bit flips; flipped bits must be
+      explained by the arithmetic (bench.ReferenceMasks.flips) and the loss stays within 1e-3.
+    Q1/Q2: the Swin encoder and the ratio predictor receive no gradient."""
+    import bench
+    g6 = golden("g6_grads")
+    refm = bench.ReferenceMasks("g6")
+    m = _full_model().eval()
+    pv_np = gi.pixel_values(6, 2, 240, 320)
+    assert hashlib.sha256(pv_np.tobytes()).hexdigest() == str(g6["input_sha"])
+    pv = torch.from_numpy(pv_np).to(DEV)
+    masks, classes = gi.labels(6, 2, 240, 320)
+    plm = m.model.pixel_level_module
+    with torch.no_grad():
+        r = plm.ratio_predictor(pv[:, 3:6])
+    np.testing.assert_allclose(r.cpu().numpy(), g6["ratio"], rtol=1e-5)
+    ref_ratio = torch.from_numpy(g6["ratio"]).to(DEV)
+    h1 = plm.ratio_predictor.register_forward_hook(lambda mod, inp, out: ref_ratio.clone())
+    try:
+        runs = {force: _g6_run(m, g6, refm, force, pv, masks, classes) for force in (True, False)}
+    finally:
+        h1.remove()
+    names = [str(n) for n in g6["all_names"]]
+    term_ref = dict(zip([str(k) for k in g6["term_names"]], [float(v) for v in g6["term_vals"]]))
+
+    def compare(run):
+        from checkers.g6_compare import compare_grads
+        loss, terms, matches, grads, _ = run
+        assert sorted(terms) == sorted(term_ref)
+        assert sorted(grads) == sorted(names), set(grads) ^ set(names)
+        rep = compare_grads(grads, g6)
+        rep.update(loss_rel=abs(loss - float(g6["loss"])) / abs(float(g6["loss"])),
+                   term_rel=max(abs(terms[k] - v) / max(abs(v), 1e-12) for k, v in term_ref.items()),
+                   matches_equal=len(matches) == int(g6["match_calls"]) and all(
+                       np.array_equal(np.stack([i, j]), g6[f"match_{c}_{b}"])
+                       for c, per in enumerate(matches) for b, (i, j) in enumerate(per)))
+        del rep["zero_class"]
+        return rep
+
+    def within(rep):
+        from checkers.g6_compare import ZERO_FLOOR
+        return (rep["loss_rel"] <= 1e-5 and rep["term_rel"] <= 2e-5 and rep["norm_rel"][0] <= G6_NORM_REL
+                and rep["sample_l2"][0] <= G6_SAMPLE_L2 and rep["sample_max_over_rms"][0] <= G6_SAMPLE_MAX
+                and rep["zero_class_worst"] <= ZERO_FLOOR)
+    forced, own = compare(runs[True]), compare(runs[False])
+    fl = refm.flips(runs[True][4])
+    fl_own = refm.flips(runs[False][4], deltas=fl["deltas"])
+    first = refm.flips(runs[False][4], deltas=fl["deltas"], upto_first=True)
+    print(f"G6 forced masks: {forced}")
+    print(f"G6 own masks: {own}; own-mask flips {fl_own['flips']} (first call {first['first_call']}, "
+          f"{first['unexplained']} unexplained)")
+    assert forced["matches_equal"]
+    assert within(forced), forced
+    assert fl["unexplained"] == 0 and first["unexplained"] == 0
+    if fl_own["flips"] == 0:
+        assert own["matches_equal"] and within(own), own
+    else:
+        assert own["loss_rel"] <= 1e-3, own
+    for n, p in m.named_parameters():
         if "ratio_predictor" in n or "pixel_level_module.encoder." in n:
             assert p.grad is None, f"{n} must not receive gradients (Q1/Q2)"

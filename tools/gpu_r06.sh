@@ -3,7 +3,7 @@
 # chain stops at the first failure), then optionally the default bench line.
 cd "$GRAFT_REPO_ROOT" || exit 1
 O="$GRAFT_REPO_ROOT/gpurun_out/r06/${TAG:-x}"; mkdir -p "$O"
-timeout -k 10 ${TT:-900} python -u -m pytest tests -m gpu -v -rf -p no:cacheprovider --timeout 400 --timeout-method thread -k "$1" > "$O/tests.log" 2>&1
+timeout -k 10 ${TT:-900} python -u -m pytest tests -m gpu -v -rf -p no:cacheprovider --timeout 400 --timeout-method thread $PY -k "$1" > "$O/tests.log" 2>&1
 rc=$?; grep -E "passed|failed|error" "$O/tests.log" | tail -3; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" "$O/tests.log" | head; exit $rc; }
 if [ -n "$BENCH" ]; then
   timeout -k 10 600 python bench.py $BENCH > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
