@@ -12,7 +12,7 @@ tail -1 "$O/smoke.log"
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 400 --timeout-method thread -p no:cacheprovider > "$O/tests_full.log" 2>&1
 rc=$?; tail -3 "$O/tests_full.log"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
-python3 -c "import json;d=json.load(open('$O/bench.json'));print('bench',d['value'],d['ms_per_step'],d['roofline']['frac_events'],d['kernels']['k5_dsam']['ms_per_step'])"
+python3 -c "import json;d=json.load(open('$O/bench.json'));print('bench',d['value'],d['ms_per_step'],d['roofline']['frac'],d['roofline']['events_avg_us'],d['kernels']['k5_dsam']['ms_per_step'])"
 B="$R/bench.py --steps 5 --warmup 2 --cpu-baseline 0 --inference 0 --c5-stream 0 --parity 0 --full-model 0"
 ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 $B > "$O/prof.log" 2>&1 ) || { tail -5 "$O/prof.log"; exit 1; }
 f=$(find "$O/prof" -name '*kernel_trace.csv' | head -1)
