@@ -23,7 +23,7 @@ WORLD_SIZE from the environment.  8 images per rank (scaling "weak").
 
 Prints ONE JSON line (rank 0).  ``value`` = images processed by all ranks / max-over-ranks
 time.  ``roofline`` is for the dominant kernel (the ratio predictor's 3x3 128->256 conv,
-k_rp_conv3x3), timed with HIP events on its launch stream over this run's eager timed steps;
+k_rp_conv5_v4), timed with HIP events on its launch stream over this run's eager timed steps;
 ``kernels`` carries the same for K5 and the whole step's t_ideal / t_measured.
 ``cpu_baseline`` = the oracle (PyTorch-CPU fp32 restatement of the reference, tests-only
 code) on bounded samples of the same workloads on this host's cores (BASELINE.md plan).
@@ -55,7 +55,7 @@ import _rgbd_import  # noqa: E402,F401
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip table)
 HBM_PEAK_GBS = 8000.0
 CONV5_FLOP_PER_PX = 2 * 128 * 9 * 256  # 3x3 128->256 (custom_model.py:1413)
-CONV5_KERNEL = "k_rp_conv3x3_v3"
+CONV5_KERNEL = "k_rp_conv5_v4"
 DSAM_CH = [(96, 192), (192, 384), (384, 768)]
 # SURVEY §8(d), per input pixel of the batch (P = B*H*W): reference-algorithmic work
 K4_FLOP_PER_PX = 703_616          # ratio predictor forward
@@ -69,7 +69,7 @@ ADAMW_BYTES_PER_PARAM = 28        # fused AdamW: read p, g, m, v; write p, m, v 
 
 # The committed evidence of this tree's default bench step (rocprofv3 kernel trace + PMC passes,
 # see its README): named explicitly, updated with each evidence commit, never picked by sort order.
-EVIDENCE_DIR = "profiles/r05_v6"
+EVIDENCE_DIR = "profiles/r06_v1"
 
 
 def pmc_traffic(kernel, default_shape):
@@ -936,7 +936,7 @@ def main():
                                   "N=1 line replays a HIP graph (its eager_img_s is the eager N=1 rate)"),
         "inference_img_s": inf,
         "kernel_ms": per,
-        "roofline": {"bound": "mfma", "kernel": "k_rp_conv3x3 (3x3 128->256, custom_model.py:1413)",
+        "roofline": {"bound": "mfma", "kernel": "k_rp_conv5_v4 (3x3 128->256, custom_model.py:1413)",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
                      "events_avg_us": round(conv_avg_ms * 1e3, 2), "events_launches": conv_launches,

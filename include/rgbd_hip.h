@@ -341,8 +341,13 @@ int rgbd_ratio_pack(int dtype, const float* const* weights_host, void* packed, v
 size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W);
 /* Byte offset in the workspace of the gated attention features x * sigmoid(attention(x))
  * (the input of feature_extractor, custom_model.py:1468-1471) as rgbd_ratio_forward leaves
- * them: dtype NHWC [B][H][W][128], valid until the workspace is reused (diagnostics / tests). */
+ * them: float32 NHWC [B][H][W][128]; bf16 channel-quarter-major [B][4][H][W][32] (channel
+ * 32q + k at [b][q][y][x][k]); valid until the workspace is reused (diagnostics / tests). */
 size_t rgbd_ratio_features_offset(int dtype, int B, int H, int W);
+/* Byte offset in the workspace of the AdaptiveAvgPool(4) output of feature_extractor[0:4]
+ * (conv5 -> BN -> ReLU -> pool, custom_model.py:1412-1416) as rgbd_ratio_forward leaves it:
+ * float32 [B][256][4][4] (diagnostics / tests). */
+size_t rgbd_ratio_pooled_offset(int dtype, int B, int H, int W);
 int rgbd_ratio_forward(int dtype, int training, float momentum, const float* depth3, long long batch_stride,
                        int B, int H, int W, const void* packed, float* const* bn_host, unsigned long long seed,
                        unsigned long long* seed_counter, float* ratio, void* ws, void* stream);

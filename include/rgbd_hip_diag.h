@@ -10,14 +10,13 @@
 extern "C" {
 #endif
 
-/* Diagnostics: buf (device, >= 2 * 18 * 8 * 5 uint64) receives, for workgroup 0 of every later
- * conv5 launch (k_rp_conv3x3_v3), s_memtime stamps per wave and K step of its first two tiles
- * (step top, after the DMA issue, after k-step 0 / 1's MFMAs, after the closing wait); NULL stops. */
+/* Diagnostics: buf (device, >= 2 * 12 * 8 * 5 uint64) receives, for workgroup 0 of every later
+ * bf16 conv5 launch (k_rp_conv5_v4), s_memtime stamps per K step and wave of its first two items
+ * (step top, after the weight-copy issue, after the first kx group + input-copy issue, after the
+ * last MFMAs, after the closing wait + barrier): [item][step][wave][5]; NULL stops.  conv5's
+ * timing-only variants (copies, barrier or fragment reads removed) are compile-time:
+ * tools/build_variant.sh NAME -DC4_NODMA=bits. */
 int rgbd_debug_conv5_stamps(void* buf);
-/* conv5 variants for timing only (wrong results): mode bit 0 drops the in-loop weight (B) copies,
- * bit 1 the in-loop input (A) copies, bit 2 the per-step barrier, bit 3 the LDS fragment reads;
- * modes 0, 1, 2, 3, 7, 15 exist (others: RGBD_E_ARG); 0 restores the kernel. */
-int rgbd_debug_conv5_mode(int mode);
 /* The same for the bf16 chain kernels (k_rp_chain_v2 phases 0 and 1): buf (device, >= 2 * 4 * 8 * 7
  * uint64) receives workgroup 0's stamps for its tiles 8-11 (tile top, patch staged, next
  * patch issued, stem MFMAs issued, stem ReLU/pack, fusion MFMAs issued, tile end), phase-major

@@ -132,6 +132,7 @@ SIGNATURES = {
     "rgbd_ratio_pack": (_I, [_I, _P, _P, _P]),
     "rgbd_ratio_workspace_size": (_SZ, [_I, _I, _I, _I]),
     "rgbd_ratio_features_offset": (_SZ, [_I, _I, _I, _I]),
+    "rgbd_ratio_pooled_offset": (_SZ, [_I, _I, _I, _I]),
     "rgbd_ratio_forward": (_I, [_I, _I, ctypes.c_float, _P, _LL, _I, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P,
                                 _P, _P]),
     "rgbd_ratio_forward_ex": (_I, [_I, _I, ctypes.c_float, _P, _LL, _I, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P,

@@ -10,10 +10,11 @@
 //                     and the gate (:1404-1470).  Each GEMM's accumulator (channel in the
 //                     registers, pixel on the lane) is directly the next GEMM's B operand; the
 //                     packed weights use the matching k permutation, so nothing touches LDS.
-//   conv5  : 3x3 128->256 (:1413), 84 % of the FLOPs, LDS-tiled implicit GEMM (k_rp_conv3x3):
-//            a 4x32-pixel tile and its 6x34 halo are staged per 32-channel chunk and reused by
-//            all 9 taps; output y (NHWC) + per-workgroup BN partial sums.
-//   pool   : BN + ReLU + AdaptiveAvgPool(4) streamed over y (k_rp_bn_relu_pool)
+//   conv5  : 3x3 128->256 (:1413), 84 % of the FLOPs, LDS-tiled implicit GEMM (bf16:
+//            k_rp_conv5_v4, 16x32-pixel tiles x 128-channel halves over 32-channel quarters, the
+//            halo of a quarter staged once for all 9 taps; float32: k_rp_conv3x3): output y +
+//            per-workgroup BN partial sums (train), or BN + ReLU + pool in the epilogue (eval)
+//   pool   : BN + ReLU + AdaptiveAvgPool(4) streamed over y (k_rp_bn_relu_pool*)
 //   tail   : 3x3 256->512 on 4x4 + BN + ReLU + GAP (k_rp_tail_conv), MLP + dropout + sigmoid
 //            (k_rp_tail_mlp), ratio = 0.01 + 0.49 sigmoid(raw) (:1485).
 // BatchNorm: eval mode uses running stats (folded into per-channel scale/shift); train mode
@@ -38,7 +39,8 @@ constexpr float BN_EPS = 1e-5f;
 
 struct Layout {  // byte offsets into the packed blob
   size_t w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, w6, b6, w7, b7, w8, b8, w9, b9, w10, b10;
-  size_t w5s, zero;  // bf16: conv5 weights in LDS-DMA step order; 256 zero bytes (padding source)
+  size_t zero;       // 256 zero bytes
+  size_t w5q;        // bf16: conv5 weights in k_rp_conv5_v4's step order
   size_t w1s;        // bf16: stem weights in the chain v2 K order
   size_t w1f, w2f;   // bf16 blobs: f32 stem (w1s order) and fusion (chain order) weights, the BN-fold sources
   size_t total;
@@ -72,11 +74,11 @@ inline Layout make_layout(int es) {
   L.b9 = seg(32 * 4);
   L.w10 = seg(32 * 4);
   L.b10 = seg(4);
-  L.w5s = seg(es == 2 ? (size_t)C5 * 9 * FUS_C * 2 : 0);
   L.zero = seg(256);
   L.w1s = seg(es == 2 ? (size_t)STEM_C * STEM_K2 * 2 : 0);
   L.w1f = seg(es == 2 ? (size_t)STEM_C * STEM_K2 * 4 : 0);
   L.w2f = seg(es == 2 ? (size_t)FUS_C * STEM_C * 4 : 0);
+  L.w5q = seg(es == 2 ? (size_t)C5 * 9 * FUS_C * 2 : 0);
   L.total = o;
   return L;
 }
@@ -146,14 +148,14 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
       const int o = e / STEM_C, kk = e % STEM_C, s = kk / 32, g = (kk % 32) / 8, ee = kk % 8;
       ((float*)(blob + L.w2f))[e] = w.p[6][o * STEM_C + 32 * s + chain_perm(g, ee)];
     }
-    // K-step order for k_rp_conv3x3_v3: [step = half*9 + tap][n][64 ch], each 128-byte row
-    // holding its 16-byte chunks in the LDS swizzle order (slot q <- chunk q ^ (n & 6)), so one
-    // LDS-DMA copy of a step is linear.
-    bf16_t* w5s = (bf16_t*)(blob + L.w5s);
+    // k_rp_conv5_v4: [half][step = quarter*3 + ky][kx][n][32 ch] (64-byte rows, chunk slot s <-
+    // chunk s ^ ((n >> 1) & 2)): one step of one channel half is one linear 24 KiB copy
+    bf16_t* w5q = (bf16_t*)(blob + L.w5q);
     for (int e = tid; e < C5 * 9 * FUS_C; e += nth) {
-      const int st = e / (C5 * 64), n = (e / 64) % C5, q = (e % 64) / 8, k = e % 8;
-      const int half = st / 9, tap = st % 9, c = 64 * half + 8 * (q ^ (n & 6)) + k;
-      w5s[e] = f32_to_bf16(w.p[12][(n * FUS_C + c) * 9 + tap]);
+      const int k8 = e % 8, sl = (e / 8) % 4, n = (e / 32) % 128, kx = (e / 4096) % 3, st = (e / 12288) % 12,
+                nh = e / 147456;
+      const int qt = st / 3, ky = st % 3, c = 32 * qt + 8 * (sl ^ ((n >> 1) & 2)) + k8;
+      w5q[e] = f32_to_bf16(w.p[12][((nh * 128 + n) * FUS_C + c) * 9 + ky * 3 + kx]);
     }
   }
   for (int e = tid; e < 64; e += nth) ((float*)(blob + L.zero))[e] = 0.f;
@@ -1082,6 +1084,15 @@ __device__ __forceinline__ void c2_stamp(unsigned long long* st, long long idx) 
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// conv5 v4's input (bf16): channel-quarter-major, zero-padded planes [B][4][PH][PW][32]: pixel
+// (y, x) at plane row y + 1, column x + 1, PH / PW = the 16x32 tile grid + a one-pixel border, so
+// every halo read of every tile is in bounds and reads zeros outside the image.
+__host__ __device__ __forceinline__ int c4_ph(int H) { return (H + 15) / 16 * 16 + 2; }
+__host__ __device__ __forceinline__ int c4_pw(int W) { return (W + 31) / 32 * 32 + 2; }
+__host__ __device__ __forceinline__ long long c4_att_idx(int b, int q, int y, int x, int H, int W) {
+  return (((long long)b * 4 + q) * c4_ph(H) + y + 1) * c4_pw(W) * 32 + (long long)(x + 1) * 32;
+}
+
 template <int PHASE, bool STAMPS = false>
 __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const float* __restrict__ depth3, long long bstride, int B,
                                                      int H, int W, const char* __restrict__ blob, Layout L,
@@ -1454,8 +1465,9 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
           float o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = a2[t][u][j] * sigmoid_fast(a4[u][j]);
-          *reinterpret_cast<uint2*>(att + ((long long)b * HW + (long long)py * W + x0 + 16 * u + r) * FUS_C + 16 * t +
-                                    4 * g) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+          // conv5 v4's padded channel-quarter-major planes (c4_att_idx)
+          *reinterpret_cast<uint2*>(att + c4_att_idx(b, t >> 1, py, x0 + 16 * u + r, H, W) + 16 * (t & 1) + 4 * g) =
+              make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
         }
       }
     }
@@ -1527,14 +1539,13 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
   const int tiles_x = (W + C2W_TW - 1) / C2W_TW, tiles_y = (H + C2W_TH - 1) / C2W_TH;
   const unsigned per = (unsigned)(tiles_x * tiles_y);
   const int ntiles = B * tiles_x * tiles_y;
-  const long long HW = (long long)H * W;
   // this wave's raw fusion output of a tile ([t][lane][u][4 px]): lane (r, g) has channel 16t + r,
   // pixels 16u + 4g + j;
   // the next tile's 8 KB are loaded while the current one computes
   uint2 nxt[8][2];
   auto fetch = [&](int tl) {
     if (tl >= ntiles) return;
-    const int tp = ntiles - 1 - tl;  // physical tile: last-to-first (see the conv5 kernel)
+    const int tp = ntiles - 1 - tl;  // physical tile: last-to-first (see conv5 v4's tile order)
     const bf16_t* ft = fus + (((long long)tp * 8 + wave) * 16) * 256;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {  // read once: non-temporal, 16 B per lane (1 KiB per wave load)
@@ -1629,17 +1640,16 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
         *cell = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
       }
     }
-    // NHWC store of the wave's 32 pixels from the image: 16 lanes per 256-byte pixel row, four
-    // consecutive pixels (1 KB contiguous) per store instruction
+    // store into conv5 v4's padded channel-quarter-major planes (c4_att_idx) of the wave's 32 pixels
+    // from the image: per store instruction one quarter of 16 consecutive pixels (1 KB contiguous)
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bf16_t* orow = att + ((long long)b * HW + (long long)py * W + x0) * FUS_C;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int pr = 4 * k + (lane >> 4), q = lane & 15;
+      const int qt = k >> 1, pr = 16 * (k & 1) + (lane >> 2), q = lane & 3;
       if (x0 + pr < W)
-        *reinterpret_cast<uint4*>(orow + (long long)pr * FUS_C + 8 * q) =
-            *reinterpret_cast<const uint4*>(img + pr * GT_S + 8 * q);
+        *reinterpret_cast<uint4*>(att + c4_att_idx(b, qt, py, x0 + pr, H, W) + 8 * q) =
+            *reinterpret_cast<const uint4*>(img + pr * GT_S + 32 * qt + 8 * q);
     }
   }
 }
@@ -1790,33 +1800,6 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool(const T* __restrict__ y
   part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = s;
 }
 
-// ---- conv5 v3 (bf16): 256 px (8x32) x 256 ch per workgroup, 8 waves as 4 (pixel-row pairs) x
-// 2 (128-channel halves); wave tile 64 px x 128 ch = 4x8 MFMA 16x16x32, K step 64 (18 steps of
-// (channel half, tap)).  All LDS staging is LDS-DMA (global_load_lds_dwordx4, no VGPR round
-// trip): the whole 10x34 halo patch of one channel half (43 KB) is resident per half and the
-// weights of one step (32 KB) double-buffered.  Rows are 128 B, 16-byte chunk q stored at slot
-// q ^ (row & 6): conflict-free ds_read_b128 for 16 consecutive rows from any start row (the
-// patch rows of tap kx), pre-applied in the weight blob and on the per-lane DMA source address.
-// Pipeline (one barrier per step): in step s waves 0-3 issue the DMA of B(s+1) (or the next
-// tile's B(0)) and their piece of A (this tile's half 1 during steps 0-5, the next tile's half 0
-// during 9-14), then run their 64 MFMAs; waves 4-7 run their MFMAs first and issue their A piece
-// after them; every wave waits for its own DMA except the A piece just issued, barrier.
-// Epilogue straight from the accumulators: y is written in a fragment-native layout
-// [tile][wave][mi][nj/2][lane][2 ch x 4 px] (1 KiB contiguous per non-temporal store instruction; read back by
-// k_rp_bn_relu_pool_frag) and the BN statistics of the float32 conv outputs (as the fp32
-// reference takes them) accumulate in registers across tiles.
-constexpr int C3_TH = 8, C3_TW = 32;
-constexpr int C3_PW = C3_TW + 2, C3_NPIX = (C3_TH + 2) * C3_PW;  // 340 halo pixels
-constexpr int C3_APIX = 344, C3_APIECES = C3_APIX / 8;            // whole 1 KiB DMA pieces
-constexpr int C3_STEPS = 18;
-constexpr int C3_A_BYTES = 2 * C3_APIX * 128;
-constexpr int C3_B_OFF = C3_A_BYTES, C3_B_BYTES = 2 * C5 * 128;
-constexpr int C3_BIAS_OFF = C3_B_OFF + C3_B_BYTES;
-constexpr size_t C3_SMEM = C3_BIAS_OFF + C5 * 4;
-static_assert(C3_SMEM <= 163840, "conv5 v3 LDS budget");
-
-__device__ __forceinline__ uint32_t c3_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 6)); }
-
 // one LDS-DMA wave instruction: 64 lanes x 16 B from per-lane sources to lds_base + 16 * lane
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
@@ -1826,108 +1809,202 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
                : "memory");
 }
 
-struct C3Tile {
+// ---- conv5 v4 (bf16): a work item is a 16x32-pixel tile x one 128-channel half of the output
+// (512 px x 128 ch; the two halves of a tile run at the same time on two workgroups of one XCD,
+// so the second one's input copies hit the L2 the first one filled).  8 waves, wave w = tile
+// rows 2w, 2w+1 (64 px) x all 128 channels = 4x8 MFMA 16x16x32 tiles (the v3 wave tile).  K is
+// walked in 12 steps of (input-channel quarter qt, kernel row ky), each step the 3 taps kx of
+// that row over the quarter's 32 channels (K 96: 96 MFMAs per wave between two barriers).
+// Against v3's 256 px x 256 ch items this halves the weight copies per FLOP (the weights of a
+// step serve 512 pixels) at a slightly larger input share: 445 KB of LDS-DMA per item instead of
+// 2 x 332 KB for the same FLOPs (-33 %), ~4.6 one-KiB pieces per wave and step instead of 9
+// per loader wave.
+// LDS: two input slots (quarter qt in slot qt & 1: the whole 18x34 halo x 32 channels, 64-byte
+// rows, 16-byte chunk c at slot c ^ ((row >> 1) & 2): ds_read_b128 conflict-free for 16
+// consecutive rows from any start row), two weight buffers of one step ([kx][n][32 ch], the same
+// swizzle, pre-applied in the blob so a step is one linear 24 KiB copy).
+// Pipeline: in step st waves 0-3 issue the weights of step st+1 (the next item's step 0 after
+// the last: a workgroup always owns the same channel half) before their MFMAs; waves 4-7 issue
+// a third of the next quarter's input (the next item's quarter 0 during quarter 3) after their
+// first 32 MFMAs; every wave waits for its own copies, then the step's one barrier.
+// MODE 0 (train): y stored fragment-native per item [item = 2 tile + half][wave][mi][np][lane][8]
+//   (1 KiB contiguous per store instruction) and the BN statistics of the float32 conv outputs
+//   kept in registers across items -> slab[workgroup][256][2] (the other half's rows zero).
+// MODE 1 (eval, H % 4 == 0, W % 64 == 0, H >= 64, W >= 128: every 16-px fragment row lies in one
+//   AdaptiveAvgPool(4) bin): BN (running statistics, `aff`) + ReLU of the bf16-rounded outputs
+//   summed per pool bin in the epilogue -> out[item][4 bin slots][128]; no y.
+// MODE 2 (eval, other shapes): y only.
+// Tile order: every kernel of the chain -> gate -> conv5 -> pool sequence reads first what the
+// previous one wrote last (still in the Infinity Cache): the chain writes its tiles first to last,
+// the gate walks them last to first, conv5 first to last, the pool the images last to first
+// (round 5: profiles/r05_v2/ab_w.txt, ab_zk.txt).
+constexpr int C4_TH = 16, C4_TW = 32, C4_PW = C4_TW + 2;
+constexpr int C4_NPIX = (C4_TH + 2) * C4_PW;  // 612 halo pixels
+constexpr int C4_APIECES = 39;                // 624 rows of 64 B, 16 rows per 1 KiB piece
+constexpr int C4_A_BYTES = C4_APIECES * 1024;
+constexpr int C4_STEPS = 12;
+constexpr int C4_B_BYTES = 3 * 128 * 64;  // one step: [kx][n][32 ch]
+constexpr int C4_B_OFF = 2 * C4_A_BYTES;
+constexpr int C4_RED_OFF = C4_B_OFF + 2 * C4_B_BYTES;
+constexpr int C4_RED_BYTES = 8 * 4 * 128 * 4;  // MODE 1: per (wave, mi) bin sums of 128 channels
+constexpr int C4_PAR_OFF = C4_RED_OFF + C4_RED_BYTES;
+constexpr size_t C4_SMEM = C4_PAR_OFF + 128 * 4 + 128 * 8 + 32 * 4;  // bias, BN affine, bin slots
+static_assert(C4_SMEM <= 163840, "conv5 v4 LDS budget");
+static_assert(C4_APIECES * 16 >= C4_NPIX && C4_APIECES % 3 == 0, "conv5 v4 input pieces");
+constexpr int C4_AK = (C4_APIECES + 3) / 4;  // input pieces per copying wave and quarter
+static_assert(2 * C4_A_BYTES >= 8 * 128 * 2 * 4, "conv5 v4 statistics scratch");
+
+__device__ __forceinline__ uint32_t c4_off(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 1) & 2)); }
+
+struct C4Tile {
   int b, y0, x0;
 };
-__device__ __forceinline__ C3Tile c3_tile(long long t, int tiles_x, int tiles_y) {
-  C3Tile o;
+__device__ __forceinline__ C4Tile c4_tile(long long t, int tiles_x, int tiles_y) {
+  C4Tile o;
   const long long per = (long long)tiles_x * tiles_y;
   o.b = (int)(t / per);
   const int rem = (int)(t % per);
-  o.y0 = (rem / tiles_x) * C3_TH;
-  o.x0 = (rem % tiles_x) * C3_TW;
+  o.y0 = (rem / tiles_x) * C4_TH;
+  o.x0 = (rem % tiles_x) * C4_TW;
   return o;
 }
 
-// Diagnostics (rgbd_debug_conv5_stamps): when set, workgroup 0 records per step of its first two
-// tiles, per wave (lane 0, vector stores), s_memtime at: step top (after the barrier), after the
-// DMA issue, after k-step 0's MFMAs are issued, after k-step 1's, after the closing wait:
-// stamps[(tile * 18 + step) * 8 + wave][5].  A separate instantiation (STAMPS = true), launched
-// only while a buffer is set: the production kernel's code is unchanged.
-__device__ unsigned long long* g_c3_stamps = nullptr;
-[[maybe_unused]] static bool c3_stamps_on = false;
-[[maybe_unused]] static int c3_mode = 0;
-__device__ __forceinline__ void c3_stamp(unsigned long long* st, long long idx) {
+// C4_NODMA (experiment builds only, -DC4_NODMA=bits; results wrong, timing only): bit 0 drops the
+// in-loop weight copies, bit 1 the in-loop input copies, bit 2 the step barrier, bit 3 the
+// fragment reads (constant operands)
+#ifndef C4_NODMA
+#define C4_NODMA 0
+#endif
+#ifndef C4_PREF
+#define C4_PREF 0
+#endif
+
+// Stamps (the diagnostic build, RGBD_DIAG: rgbd_debug_conv5_stamps): workgroup 0 records, per step
+// and wave of its first two items, s_memtime at the step top, after the weight-copy issue, after
+// the first kx group (+ the input-copy issue), after the last MFMAs, after the closing wait +
+// barrier: stamps[((item * 12 + step) * 8 + wave) * 5 + k].  The product build has no stamp code.
+#if defined(RGBD_DIAG) && !defined(C4_STAMPS)
+#define C4_STAMPS
+#endif
+#ifdef C4_STAMPS
+__device__ unsigned long long* g_c4_stamps = nullptr;
+__device__ __forceinline__ void c4_stamp(unsigned long long* st, long long idx) {
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0) st[idx] = t;
   __builtin_amdgcn_sched_barrier(0);
 }
-
-// NODMA (diagnostic build only, rgbd_debug_conv5_mode): bit 0 drops the in-loop B copies, bit 1
-// the in-loop A copies, bit 2 the per-step barrier, bit 3 the fragment reads (constant operands)
-// — wrong results; isolates the DMA's, the lockstep's and the fragment stream's costs.
-template <bool STAMPS, int NODMA = 0>
-__global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict__ x, int B, int H, int W,
-                                                       const char* __restrict__ blob, Layout L,
-                                                       bf16_t* __restrict__ y, float* __restrict__ slab) {
+#define C4_STAMP(k) \
+  if (sts) c4_stamp(sts, (((long long)tcount * C4_STEPS + st) * 8 + wave) * 5 + (k))
+#else
+#define C4_STAMP(k)
+#endif
+template <int MODE>
+__global__ __launch_bounds__(512) void k_rp_conv5_v4(const bf16_t* __restrict__ x, int B, int H, int W,
+                                                     const char* __restrict__ blob, Layout L,
+                                                     const float2* __restrict__ aff, bf16_t* __restrict__ y,
+                                                     float* __restrict__ out, int xcd_pairs) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
-  const int wm = wave & 3, wn = wave >> 2;
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  const char* w5s = blob + L.w5s;
-  const char* zero16 = blob + L.zero;
-  float* sbias = (float*)(smem + C3_BIAS_OFF);
-  for (int i = tid; i < C5; i += 512) sbias[i] = ((const float*)(blob + L.b5))[i];
-  const int tiles_x = (W + C3_TW - 1) / C3_TW, tiles_y = (H + C3_TH - 1) / C3_TH;
+  // workgroups b and b + 8 (one XCD under round-robin placement: speed only) share the tiles
+  int pair, nh;
+  if (xcd_pairs) {
+    nh = (blockIdx.x >> 3) & 1;
+    pair = (blockIdx.x & 7) | ((blockIdx.x >> 4) << 3);
+  } else {
+    nh = blockIdx.x & 1;
+    pair = blockIdx.x >> 1;
+  }
+  const int npairs = gridDim.x >> 1;
+  const char* w5q = blob + L.w5q + (size_t)nh * C4_STEPS * C4_B_BYTES;
+  float* sbias = (float*)(smem + C4_PAR_OFF);
+  float2* saff = (float2*)(smem + C4_PAR_OFF + 512);
+  int* sslot = (int*)(smem + C4_PAR_OFF + 512 + 1024);
+  for (int i = tid; i < 128; i += 512) {
+    sbias[i] = ((const float*)(blob + L.b5))[nh * 128 + i];
+    if constexpr (MODE == 1) saff[i] = aff[nh * 128 + i];
+  }
+  const int tiles_x = (W + C4_TW - 1) / C4_TW, tiles_y = (H + C4_TH - 1) / C4_TH;
   const long long ntiles = (long long)B * tiles_x * tiles_y;
 
-  // A piece j of channel half h for tile t: pixel p = 8j + lane/8, slot lane%8
-  auto issue_a = [&](const C3Tile& t, int h, int j) {
-    const int p = 8 * j + (lane >> 3), q = lane & 7;
-    const int hy = p / C3_PW, hx = p % C3_PW;
-    const int yy = t.y0 + hy - 1, xx = t.x0 + hx - 1;
-    const char* src = zero16;
-    if (p < C3_NPIX && yy >= 0 && yy < H && xx >= 0 && xx < W)
-      src = (const char*)(x + (((long long)t.b * H + yy) * W + xx) * FUS_C + 64 * h + 8 * (q ^ (p & 6)));
-    glds16(src, lds0 + h * (C3_APIX * 128) + j * 1024);
-  };
-  // B pieces of step st: 32 x 1 KiB, copied by the loader waves 0-3 only (wave w: pieces
-  // 8w..8w+7): waves 4-7 open every step with their MFMAs while 0-3 issue the DMA, so the
-  // SIMD's matrix pipe is never idle behind both partners' DMA issue at once.  (Measured, round 5:
-  // 1.7 % faster than every wave issuing 4 pieces at the step top; waves 4-7 issuing theirs
-  // after their MFMAs instead was 0.7 % slower than that — r05 ab_e.txt, conv5_stamps_e.txt.)
-  const bool loader = wave < 4;
-  auto issue_b = [&](int st, int k0, int k1) {
-    const char* src = w5s + (size_t)st * (C5 * 128) + wave * 8192 + 16 * lane;
-    const uint32_t dst = lds0 + C3_B_OFF + (st & 1) * (C5 * 128) + wave * 8192;
+  // input piece j (rows 16j .. 16j+15 of the halo image) of quarter qt of tile t into slot sl:
+  // the copying waves (4-7) own pieces j = w4 + 4k (k < 10); a lane's source offset from the
+  // tile's padded origin depends on the piece and the plane width only, so it is computed once
+  const int PW = c4_pw(W);
+  const long long plane = (long long)c4_ph(H) * PW * 32;  // elements
+  uint32_t aoff[C4_AK];
 #pragma unroll
+  for (int k = 0; k < C4_AK; ++k) {
+    const int row = 16 * ((wave & 3) + 4 * k) + (lane >> 2), q = lane & 3;
+    const int hy = row / C4_PW, hx = row - hy * C4_PW;
+    aoff[k] = row < C4_NPIX ? (uint32_t)((hy * PW + hx) * 64 + 16 * (q ^ ((row >> 1) & 2))) : 0u;
+  }
+  auto issue_a = [&](const C4Tile& t, int qt, int sl, int k) {
+    const char* base = (const char*)(x + ((long long)t.b * 4 + qt) * plane + ((long long)t.y0 * PW + t.x0) * 32);
+    glds16(base + aoff[k], lds0 + sl * C4_A_BYTES + ((wave & 3) + 4 * k) * 1024);
+  };
+#if C4_PREF
+  // L2 prefetch of a quarter's halo two quarters ahead (loaders, one dword per halo pixel through
+  // LDS-DMA into a scratch strip: no register is written): touch instruction m = w + 4k of 10
+  uint32_t poff[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int p = 64 * ((wave & 3) + 4 * k) + lane, hy = p / C4_PW, hx = p - hy * C4_PW;
+    poff[k] = p < C4_NPIX ? (uint32_t)((hy * PW + hx) * 64) : 0u;
+  }
+  auto touch = [&](const C4Tile& t, int qt, int k) {
+    const char* base = (const char*)(x + ((long long)t.b * 4 + qt) * plane + ((long long)t.y0 * PW + t.x0) * 32);
+    const uint32_t dst = lds0 + C4_RED_OFF + (wave & 3) * 256;
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(base + poff[k]), "s"(dst)
+                 : "memory");
+  };
+#endif
+  // weight pieces k0..k1-1 (of 24) of step st into buffer st & 1
+  auto issue_b = [&](int st, int k0, int k1) {
+    const char* src = w5q + (size_t)st * C4_B_BYTES + 16 * lane;
+    const uint32_t dst = lds0 + C4_B_OFF + (st & 1) * C4_B_BYTES;
     for (int k = k0; k < k1; ++k) glds16(src + 1024 * k, dst + 1024 * k);
   };
+  const bool loader = wave < 4;
 
-  // BN statistics per channel as (even, odd) pixel pairs: packed adds / FMAs, one instruction
-  // per value for the sum and the sum of squares together
   f32x2 ssum[8], ssq[8];
 #pragma unroll
   for (int nj = 0; nj < 8; ++nj) ssum[nj] = ssq[nj] = f32x2{0.f, 0.f};
+  const int rh = H >> 2, rw = W >> 2;  // MODE 1: pool bin size
 
-  // static priority for the second-dispatched half of the workgroup (the arbitration loser of
-  // every step with two waves per SIMD; MI355X_MICROARCH "two waves per SIMD", item 4)
+#ifndef C4_NOPRIO
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-  // tile order: each kernel of the chain -> gate -> conv5 -> pool sequence reads first what the
-  // previous one wrote last (still in the Infinity Cache): the chain writes in increasing tile
-  // order, the gate walks its tiles last-to-first, conv5 first-to-last, the pool the images
-  // last-to-first (profiles/r05_v2/ab_w.txt, ab_x.txt, ab_zk.txt, ab_zk2.txt)
-  long long tile = blockIdx.x;
-  if (tile < ntiles) {  // prologue: half 0 + B(0) of the first tile
-    const C3Tile t = c3_tile(tile, tiles_x, tiles_y);
-    for (int j = wave; j < C3_APIECES; j += 8) issue_a(t, 0, j);
-    if (loader) issue_b(0, 0, 8);
+#endif
+  long long tile = pair;
+  if (tile < ntiles) {  // prologue: quarter 0 (waves 4-7) + the weights of step 0
+    const C4Tile t = c4_tile(tile, tiles_x, tiles_y);
+    if (!loader) {
+#pragma unroll
+      for (int k = 0; k < C4_AK; ++k)
+        if ((wave & 3) + 4 * k < C4_APIECES) issue_a(t, 0, 0, k);
+    }
+    issue_b(0, 3 * wave, 3 * wave + 3);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  unsigned long long* const stamps = (STAMPS && blockIdx.x == 0) ? g_c3_stamps : nullptr;
+#ifdef C4_STAMPS
   int tcount = 0;
-  for (; tile < ntiles; tile += gridDim.x, ++tcount) {
-    const long long tphys = tile;
-    const C3Tile t = c3_tile(tphys, tiles_x, tiles_y);
-    const long long ntile = tile + gridDim.x;
-    unsigned long long* const sts = (STAMPS && stamps && tcount < 2) ? stamps : nullptr;
+#endif
+  for (; tile < ntiles; tile += npairs) {
+#ifdef C4_STAMPS
+    unsigned long long* const sts = (blockIdx.x == 0 && tcount < 2) ? g_c4_stamps : nullptr;
+#endif
+    const C4Tile t = c4_tile(tile, tiles_x, tiles_y);
+    const long long ntile = tile + npairs;
     const bool has_next = ntile < ntiles;
-    const C3Tile tn = c3_tile(has_next ? ntile : tile, tiles_x, tiles_y);
+    const C4Tile tn = c4_tile(has_next ? ntile : tile, tiles_x, tiles_y);
     f32x4 acc[4][8];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -1935,169 +2012,260 @@ __global__ __launch_bounds__(512) void k_rp_conv3x3_v3(const bf16_t* __restrict_
       for (int nj = 0; nj < 8; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
-    for (int st = 0; st < C3_STEPS; ++st) {
-      const long long sidx = ((long long)(tcount * C3_STEPS + st) * 8 + wave) * 5;
-      if (STAMPS && sts) c3_stamp(sts, sidx + 0);
-      // this step's DMA: B(st + 1) (or the next tile's B(0)), plus a piece of A (this tile's half 1
-      // during steps 0-5, the next tile's half 0 during 9-14)
-      int a_issued = 0;
-      const bool b_next = st + 1 < C3_STEPS || has_next;
-      const int b_st = st + 1 < C3_STEPS ? st + 1 : 0;
-      const int a_j = st < 6 ? wave + 8 * st : wave + 8 * (st - 9);
-      const int a_kind = (st < 6 && a_j < C3_APIECES) ? 1 : ((st >= 9 && st < 15 && has_next && a_j < C3_APIECES) ? 2 : 0);
-      // loaders: B(st + 1) and their A piece before their MFMAs; waves 4-7: their A piece after
-      if (loader) {
-        if (b_next && !(NODMA & 1)) issue_b(b_st, 0, 8);
-        if (!(NODMA & 2)) {
-          if (a_kind == 1) issue_a(t, 1, a_j);
-          if (a_kind == 2) issue_a(tn, 0, a_j);
-        }
-      }
-      a_issued = (NODMA & 2) ? 0 : a_kind != 0;
-      const int h = st >= 9, tap = st - 9 * h, ky = tap / 3, kx = tap % 3;
-      const char* sa = smem + h * (C3_APIX * 128);
-      const char* sb = smem + C3_B_OFF + (st & 1) * (C5 * 128);
-      if (STAMPS && sts) c3_stamp(sts, sidx + 1);
+    for (int st = 0; st < C4_STEPS; ++st) {
+      const int qt = st / 3, ky = st - 3 * qt;
+      C4_STAMP(0);
+      if (!(C4_NODMA & 1) && loader && (st + 1 < C4_STEPS || has_next))
+        issue_b(st + 1 < C4_STEPS ? st + 1 : 0, 6 * wave, 6 * wave + 6);
+      C4_STAMP(1);
+      const int qn = qt + 1;  // the quarter copied during this one (4: the next item's quarter 0)
+      const bool a_go = !(C4_NODMA & 2) && !loader && (qn < 4 || has_next);
+      const char* sa = smem + (qt & 1) * C4_A_BYTES;
+      const char* sb = smem + C4_B_OFF + (st & 1) * C4_B_BYTES;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int kx = 0; kx < 3; ++kx) {
         Frag<bf16_t> fa[4], fb[8];
-        if constexpr (!(NODMA & 8)) {
+        if constexpr (!(C4_NODMA & 8)) {
 #pragma unroll
           for (int mi = 0; mi < 4; ++mi) {
-            const int p = (2 * wm + (mi >> 1) + ky) * C3_PW + (mi & 1) * 16 + r + kx;
-            fa[mi].v = *reinterpret_cast<const uint4*>(sa + c3_off(p, 4 * ks + g));
+            const int p = (2 * wave + (mi >> 1) + ky) * C4_PW + (mi & 1) * 16 + r + kx;
+            fa[mi].v = *reinterpret_cast<const uint4*>(sa + c4_off(p, g));
           }
 #pragma unroll
-          for (int nj = 0; nj < 8; ++nj)
-            fb[nj].v = *reinterpret_cast<const uint4*>(sb + c3_off(wn * 128 + 16 * nj + r, 4 * ks + g));
+          for (int nj = 0; nj < 8; ++nj) fb[nj].v = *reinterpret_cast<const uint4*>(sb + c4_off(kx * 128 + 16 * nj + r, g));
         } else {
 #pragma unroll
-          for (int mi = 0; mi < 4; ++mi) fa[mi].v = make_uint4(lane, ks, st, mi);
+          for (int mi = 0; mi < 4; ++mi) fa[mi].v = make_uint4(lane, kx, st, mi);
 #pragma unroll
-          for (int nj = 0; nj < 8; ++nj) fb[nj].v = make_uint4(nj, lane, ks, st);
+          for (int nj = 0; nj < 8; ++nj) fb[nj].v = make_uint4(nj, lane, kx, st);
         }
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int nj = 0; nj < 8; ++nj) mma(acc[mi][nj], fa[mi], fb[nj]);
-        if (STAMPS && sts) c3_stamp(sts, sidx + 2 + ks);
-      }
-      if (!loader && !(NODMA & 2)) {  // the A piece lands under the barrier / next step (needed >= 3 steps later)
-        if (a_kind == 1) issue_a(t, 1, a_j);
-        if (a_kind == 2) issue_a(tn, 0, a_j);
-      }
-      // own DMA landed (except the A pieces just issued), own LDS reads done, then the barrier
-      if constexpr (STAMPS) {
-        if (a_issued == 1)
-          asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        if (sts) c3_stamp(sts, sidx + 4);
-        if constexpr (!(NODMA & 4)) __builtin_amdgcn_s_barrier();
-      } else if constexpr (NODMA & 4) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      } else {
-        if (a_issued == 1)
-          asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      }
-    }
-    // ---- epilogue: bias, bf16, fragment-native y store (16 B per lane: the 4 px of channel
-    // pair (16*nj + r, 16*(nj+1) + r), nj even), statistics of the float32 conv outputs
-    bf16_t* yt = y + (((tphys * 8 + wave) * 4) * 4) * 512;  // [mi][nj/2][lane][8]
-    const bool interior = t.y0 + C3_TH <= H && t.x0 + C3_TW <= W;
+        if (kx == 0 && a_go) {  // this step's 13 pieces [13 ky, 13 ky + 13) of the next quarter
 #pragma unroll
-    for (int np = 0; np < 4; ++np) {
-      const float b0 = sbias[wn * 128 + 32 * np + r], b1 = sbias[wn * 128 + 32 * np + 16 + r];
-      if (interior) {
-        // every tile at 640x480: no bounds selects; per pixel pair one packed bias add, one packed
-        // conversion, one packed add (sum) and one packed FMA (sum of squares)
-        const f32x2 bb0 = {b0, b0}, bb1 = {b1, b1};
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const f32x4 v = acc[mi][2 * np], w = acc[mi][2 * np + 1];
-          const f32x2 a0 = f32x2{v[0], v[1]} + bb0, a1 = f32x2{v[2], v[3]} + bb0;
-          const f32x2 c0 = f32x2{w[0], w[1]} + bb1, c1 = f32x2{w[2], w[3]} + bb1;
-          const u32x4 pk = {pack_bf16x2(a0.x, a0.y), pack_bf16x2(a1.x, a1.y), pack_bf16x2(c0.x, c0.y),
-                            pack_bf16x2(c1.x, c1.y)};
-          __builtin_nontemporal_store(pk, reinterpret_cast<u32x4*>(yt + ((mi * 4 + np) * 64 + lane) * 8));
-          ssum[2 * np] += a0 + a1;
-          ssq[2 * np] = __builtin_elementwise_fma(a0, a0, __builtin_elementwise_fma(a1, a1, ssq[2 * np]));
-          ssum[2 * np + 1] += c0 + c1;
-          ssq[2 * np + 1] = __builtin_elementwise_fma(c0, c0, __builtin_elementwise_fma(c1, c1, ssq[2 * np + 1]));
+          for (int k = 0; k < C4_AK; ++k) {
+            const int j = (wave & 3) + 4 * k;
+            if (j >= 13 * ky && j < 13 * ky + 13 && j < C4_APIECES) issue_a(qn < 4 ? t : tn, qn & 3, qn & 1, k);
+          }
         }
-      } else {
+        if (kx == 0) C4_STAMP(2);
+      }
+      C4_STAMP(3);
+#if C4_PREF
+      if (loader && (wave & 3) + 4 * ky < 10) {
+        const int qp = qt + 2;  // 4, 5: the next item's quarters 0, 1
+        if (qp < 4 || has_next) {
+          touch(qp < 4 ? t : tn, qp & 3, ky);
+          asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          C4_STAMP(4);
+          continue;
+        }
+      }
+#endif
+      if constexpr (C4_NODMA & 4)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      C4_STAMP(4);
+    }
+#ifdef C4_STAMPS
+    ++tcount;
+#endif
+
+    // ---- epilogue
+    const long long item = 2 * tile + nh;
+    if constexpr (MODE != 1) {
+      bf16_t* yt = y + ((item * 8 + wave) * 16) * 512;  // [mi][np][lane][8]
+      const bool interior = t.y0 + C4_TH <= H && t.x0 + C4_TW <= W;
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const bool row_ok = t.y0 + 2 * wm + (mi >> 1) < H;
-          const int xb = t.x0 + (mi & 1) * 16 + 4 * g;
-          uint32_t hv[8];
+      for (int np = 0; np < 4; ++np) {
+        const float b0 = sbias[32 * np + r], b1 = sbias[32 * np + 16 + r];
+        if (interior) {
+          const f32x2 bb0 = {b0, b0}, bb1 = {b1, b1};
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int nj = 2 * np + h;
-            const float bias = h ? b1 : b0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float av = acc[mi][nj][j] + bias;
-              hv[4 * h + j] = (uint32_t)f32_to_bf16(av);
-              if (row_ok && xb + j < W) {
-                ssum[nj].x += av;
-                ssq[nj].x = __builtin_fmaf(av, av, ssq[nj].x);
-              }
+          for (int mi = 0; mi < 4; ++mi) {
+            const f32x4 v = acc[mi][2 * np], w = acc[mi][2 * np + 1];
+            const f32x2 a0 = f32x2{v[0], v[1]} + bb0, a1 = f32x2{v[2], v[3]} + bb0;
+            const f32x2 c0 = f32x2{w[0], w[1]} + bb1, c1 = f32x2{w[2], w[3]} + bb1;
+            const u32x4 pk = {pack_bf16x2(a0.x, a0.y), pack_bf16x2(a1.x, a1.y), pack_bf16x2(c0.x, c0.y),
+                              pack_bf16x2(c1.x, c1.y)};
+            __builtin_nontemporal_store(pk, reinterpret_cast<u32x4*>(yt + ((mi * 4 + np) * 64 + lane) * 8));
+            if constexpr (MODE == 0) {
+              ssum[2 * np] += a0 + a1;
+              ssq[2 * np] = __builtin_elementwise_fma(a0, a0, __builtin_elementwise_fma(a1, a1, ssq[2 * np]));
+              ssum[2 * np + 1] += c0 + c1;
+              ssq[2 * np + 1] = __builtin_elementwise_fma(c0, c0, __builtin_elementwise_fma(c1, c1, ssq[2 * np + 1]));
             }
           }
-          *reinterpret_cast<uint4*>(yt + ((mi * 4 + np) * 64 + lane) * 8) =
-              make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16));
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) {
+            const bool row_ok = t.y0 + 2 * wave + (mi >> 1) < H;
+            const int xb = t.x0 + (mi & 1) * 16 + 4 * g;
+            uint32_t hv[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int nj = 2 * np + h;
+              const float bias = h ? b1 : b0;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const float av = acc[mi][nj][j] + bias;
+                hv[4 * h + j] = (uint32_t)f32_to_bf16(av);
+                if (MODE == 0 && row_ok && xb + j < W) {
+                  ssum[nj].x += av;
+                  ssq[nj].x = __builtin_fmaf(av, av, ssq[nj].x);
+                }
+              }
+            }
+            *reinterpret_cast<uint4*>(yt + ((mi * 4 + np) * 64 + lane) * 8) =
+                make_uint4(hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16));
+          }
         }
+      }
+    } else {
+      // BN + ReLU of the bf16-rounded outputs (what the pool kernels read back from y), summed
+      // per 16-px fragment row, then per pool bin in a fixed (wave, mi) order
+      float* red = (float*)(smem + C4_RED_OFF);  // [wave][mi][128]
+      if (tid < 32) {  // bin slot of fragment (wave, mi) = tid: (row bin - first) * 2 + (col bin - first), -1 off image
+        const int row = t.y0 + 2 * (tid >> 2) + ((tid & 3) >> 1), col = t.x0 + 16 * (tid & 1);
+        sslot[tid] = row < H ? (row / rh - t.y0 / rh) * 2 + (col / rw - t.x0 / rw) : -1;
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 8; ++nj) {
+          const float bias = sbias[16 * nj + r];
+          const float2 a = saff[16 * nj + r];
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float vb = bf16_to_f32(f32_to_bf16(acc[mi][nj][j] + bias));
+            s += fmaxf(vb * a.x + a.y, 0.f);
+          }
+          s += __shfl_xor(s, 16);
+          s += __shfl_xor(s, 32);
+          if (g == 0) red[(wave * 4 + mi) * 128 + 16 * nj + r] = s;
+        }
+      __syncthreads();
+      {
+        const int slot = tid >> 7, c = tid & 127;
+        float s = 0.f;
+        for (int f = 0; f < 32; ++f)
+          if (sslot[f] == slot) s += red[f * 128 + c];
+        out[(item * 4 + slot) * 128 + c] = s;
+      }
+      // red / sslot are rewritten only after the next item's 12 step barriers
+    }
+  }
+  if constexpr (MODE == 0) {
+    // statistics: lanes of equal r, then the 8 waves in fixed order (the A slots are free: no
+    // copy is in flight after the last item)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* red = (float*)smem;  // [8 wave][128 n][2]
+#pragma unroll
+    for (int nj = 0; nj < 8; ++nj) {
+      float a = ssum[nj].x + ssum[nj].y, q = ssq[nj].x + ssq[nj].y;
+      a += __shfl_xor(a, 16);
+      a += __shfl_xor(a, 32);
+      q += __shfl_xor(q, 16);
+      q += __shfl_xor(q, 32);
+      if (g == 0) {
+        red[(wave * 128 + 16 * nj + r) * 2] = a;
+        red[(wave * 128 + 16 * nj + r) * 2 + 1] = q;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < C5 * 2; i += 512) {
+      const int c = i >> 1, k = i & 1;
+      float v = 0.f;
+      if ((c >> 7) == nh)
+        for (int w = 0; w < 8; ++w) v += red[(w * 128 + (c & 127)) * 2 + k];
+      out[(long long)blockIdx.x * C5 * 2 + i] = v;
+    }
+  }
+}
+
+// BN + ReLU + AdaptiveAvgPool(4) partial sums over v4's y, 8-row half tiles: when every half tile
+// lies inside one pool bin and no bins overlap (H % 32 == 0, W % 128 == 0).  A half tile of one
+// channel half is 64 KiB contiguous (waves 4h .. 4h+3 of the item); thread t reads 16-byte chunk
+// t + 256k (k = wave x mi), so it keeps channels (np, r) of both h of its lane's chunk -> with
+// both channel halves 4 sums; the 4 pixel-quad lanes fold by shuffles at the end.  Split sp of
+// bin reg takes the bin's half tiles sp, sp + POOL_SPLIT, ... (raster order).
+__global__ __launch_bounds__(256) void k_rp_bn_relu_pool_v4_tiles(const bf16_t* __restrict__ y, int H, int W,
+                                                                  const float2* __restrict__ aff,
+                                                                  float* __restrict__ part) {
+  __shared__ float red[C5];
+  const int b = (int)gridDim.y - 1 - (int)blockIdx.y;  // images last-to-first (see conv5 v4's tile order)
+  const int reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
+  const int i = reg / 4, j = reg % 4;
+  const int tiles_x = W / C4_TW, tiles_y = H / C4_TH;
+  const int rhy = H / 32, rtx = W / 128;  // bin size in half tiles (8 rows) and tiles (32 cols)
+  const int t = threadIdx.x, lane = t & 63, np = t >> 6, r = lane & 15;
+  float2 af[2][2];
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) af[nh][h] = aff[nh * 128 + 32 * np + 16 * h + r];
+  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  for (int q = sp; q < rhy * rtx; q += POOL_SPLIT) {
+    const int hy = i * rhy + q / rtx, tx = j * rtx + q % rtx;  // global half-tile row, tile column
+    const long long tile = ((long long)b * tiles_y + (hy >> 1)) * tiles_x + tx;
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh) {
+      const uint4* src = reinterpret_cast<const uint4*>(y + ((2 * tile + nh) * 8 + 4 * (hy & 1)) * 16 * 512) + t;
+      uint4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const u32x4 xv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 256 * u));
+        v[u] = make_uint4(xv.x, xv.y, xv.z, xv.w);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float lo = __uint_as_float(w[2 * h + e] << 16), hi = __uint_as_float(w[2 * h + e] & 0xffff0000u);
+            acc[nh][h] += fmaxf(lo * af[nh][h].x + af[nh][h].y, 0.f);
+            acc[nh][h] += fmaxf(hi * af[nh][h].x + af[nh][h].y, 0.f);
+          }
       }
     }
   }
-  // ---- statistics: lanes of equal r, then the 4 row-pair waves in fixed order
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float* red = (float*)smem;  // [4 wm][256 n][2]
 #pragma unroll
-  for (int nj = 0; nj < 8; ++nj) {
-    float a = ssum[nj].x + ssum[nj].y, q = ssq[nj].x + ssq[nj].y;
-    a += __shfl_xor(a, 16);
-    a += __shfl_xor(a, 32);
-    q += __shfl_xor(q, 16);
-    q += __shfl_xor(q, 32);
-    if (g == 0) {
-      const int n = wn * 128 + 16 * nj + r;
-      red[(wm * C5 + n) * 2] = a;
-      red[(wm * C5 + n) * 2 + 1] = q;
+  for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v = acc[nh][h];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) red[nh * 128 + 32 * np + 16 * h + r] = v;
     }
-  }
   __syncthreads();
-  for (int i = tid; i < C5 * 2; i += 512)
-    slab[(long long)blockIdx.x * C5 * 2 + i] = red[i] + red[C5 * 2 + i] + red[2 * C5 * 2 + i] + red[3 * C5 * 2 + i];
+  part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + t] = red[t];
 }
 
-// BN + ReLU + AdaptiveAvgPool(4) partial sums over the fragment-native y of k_rp_conv3x3_v3.
-// grid: (16 regions * POOL_SPLIT, B); 256 threads = 128 channel pairs (c, c + 16) x 2 quad lanes;
-// a quad is 4 x-consecutive pixels (never straddles a 32-px tile); one 16-byte load (one lane of
-// the conv's store) = 2 channels x 4 px.
-__global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __restrict__ y, int H, int W,
-                                                              const float2* __restrict__ aff,
-                                                              float* __restrict__ part) {
+// The same over v4's y for any shape (bins may overlap, tiles may be ragged): as
+// k_rp_bn_relu_pool_frag with v4's item addressing.
+__global__ __launch_bounds__(256) void k_rp_bn_relu_pool_v4_frag(const bf16_t* __restrict__ y, int H, int W,
+                                                                 const float2* __restrict__ aff,
+                                                                 float* __restrict__ part) {
   __shared__ float red[2][C5];
   const int b = blockIdx.y, reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
   const int i = reg / 4, j = reg % 4;
   const int cp = threadIdx.x & 127, ql = threadIdx.x >> 7;
-  const int wn = cp >> 6, np = (cp >> 4) & 3, r = cp & 15, n0 = wn * 128 + 32 * np + r, n1 = n0 + 16;
+  const int nh = cp >> 6, np = (cp >> 4) & 3, r = cp & 15, n0 = nh * 128 + 32 * np + r, n1 = n0 + 16;
   const int ya = (i * H) / 4, yb = ((i + 1) * H + 3) / 4, xa = (j * W) / 4, xb = ((j + 1) * W + 3) / 4;
   const int rows = yb - ya;
   const int r0 = ya + (rows * sp) / POOL_SPLIT, r1 = ya + (rows * (sp + 1)) / POOL_SPLIT;
   const int qa = xa >> 2, nq = ((xb + 3) >> 2) - qa;
-  const int tiles_x = (W + C3_TW - 1) / C3_TW, tiles_y = (H + C3_TH - 1) / C3_TH;
+  const int tiles_x = (W + C4_TW - 1) / C4_TW, tiles_y = (H + C4_TH - 1) / C4_TH;
   const float2 a0 = aff[n0], a1 = aff[n1];
   float s0 = 0.f, s1 = 0.f;
-  // The thread walks its quads (row yy, quad k of the row, k += 2) with counters instead of
-  // divisions and keeps PU independent 16-byte loads in flight per batch (addresses clamped to a
-  // valid quad past the end, contributions masked): one load per iteration left the loop
-  // latency-bound at ~4 TB/s.
   constexpr int PU = 8;
   int yy = r0, k = ql;
   while (k >= nq) {
@@ -2113,10 +2281,10 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __re
       ok[u] = yy < r1;
       const int ry = ok[u] ? yy : r1 - 1, xq = (qa + (ok[u] ? k : 0)) * 4;
       xqs[u] = xq;
-      const long long tile = ((long long)b * tiles_y + ry / C3_TH) * tiles_x + xq / C3_TW;
-      const int ly = ry % C3_TH, lx = xq % C3_TW;
-      const int wave = wn * 4 + (ly >> 1), mi = (ly & 1) * 2 + (lx >> 4), g = (lx & 15) >> 2;
-      v[u] = *reinterpret_cast<const uint4*>(y + ((((tile * 8 + wave) * 4 + mi) * 4 + np) * 64 + g * 16 + r) * 8);
+      const long long tile = ((long long)b * tiles_y + ry / C4_TH) * tiles_x + xq / C4_TW;
+      const int ly = ry % C4_TH, lx = xq % C4_TW;
+      const int wave = ly >> 1, mi = (ly & 1) * 2 + (lx >> 4), g = (lx & 15) >> 2;
+      v[u] = *reinterpret_cast<const uint4*>(y + (((((2 * tile + nh) * 8 + wave) * 4 + mi) * 4 + np) * 64 + g * 16 + r) * 8);
       k += 2;
       while (k >= nq) {
         k -= nq;
@@ -2145,67 +2313,24 @@ __global__ __launch_bounds__(256) void k_rp_bn_relu_pool_frag(const bf16_t* __re
   part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + c] = red[0][c] + red[1][c];
 }
 
-// The same pool over whole 8x32-px conv tiles, when every tile lies inside one pool region and no
-// regions overlap (H % 32 == 0, W % 128 == 0: 640x480).  A tile's 128 KiB of y is one contiguous
-// stream; thread t reads 16-byte chunk t + 256k (k = wave x mi of the conv tile), so a wave load
-// is 1 KiB contiguous and the thread keeps fixed channels: (np, r) of the chunk lane, both wn
-// halves -> 4 channel sums; the 4 pixel-quad lanes of a channel fold by shuffles at the end.
-// Split sp of region reg takes the region's tiles sp, sp + POOL_SPLIT, ... (raster order).
-__global__ __launch_bounds__(256) void k_rp_bn_relu_pool_tiles(const bf16_t* __restrict__ y, int H, int W,
-                                                               const float2* __restrict__ aff,
-                                                               float* __restrict__ part) {
-  __shared__ float red[C5];
-  const int b = (int)gridDim.y - 1 - (int)blockIdx.y;  // images last-to-first (see the conv5 kernel)
-  const int reg = blockIdx.x / POOL_SPLIT, sp = blockIdx.x % POOL_SPLIT;
-  const int i = reg / 4, j = reg % 4;
-  const int tiles_x = W / C3_TW, tiles_y = H / C3_TH;
-  const int rty = tiles_y / 4, rtx = tiles_x / 4;  // region size in tiles
-  const int t = threadIdx.x, lane = t & 63, np = t >> 6, r = lane & 15;
-  float2 af[2][2];
-#pragma unroll
-  for (int wn = 0; wn < 2; ++wn)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) af[wn][h] = aff[wn * 128 + 32 * np + 16 * h + r];
-  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-  for (int q = sp; q < rty * rtx; q += POOL_SPLIT) {
-    const int ty = i * rty + q / rtx, tx = j * rtx + q % rtx;
-    const long long tile = ((long long)b * tiles_y + ty) * tiles_x + tx;
-    const uint4* src = reinterpret_cast<const uint4*>(y + tile * (8 * 4 * 4 * 512)) + t;
-#pragma unroll
-    for (int k0 = 0; k0 < 32; k0 += 16) {
-      uint4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 256 * (k0 + u)));
-        v[u] = make_uint4(x.x, x.y, x.z, x.w);
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int wn = (k0 + u) >> 4;  // k = wv * 4 + mi, wv = wn * 4 + row pair
-        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const float lo = __uint_as_float(w[2 * h + e] << 16), hi = __uint_as_float(w[2 * h + e] & 0xffff0000u);
-            acc[wn][h] += fmaxf(lo * af[wn][h].x + af[wn][h].y, 0.f);
-            acc[wn][h] += fmaxf(hi * af[wn][h].x + af[wn][h].y, 0.f);
-          }
-      }
+// MODE 1's pool: pooled[b][c][bin] = the sum of the bin's item partials (tiles in raster order)
+// / the bin's pixel count.  grid (16 bins, B), thread = channel.
+__global__ __launch_bounds__(256) void k_rp_pool_finish_v4(const float* __restrict__ ip, int B, int H, int W,
+                                                           float* __restrict__ pooled) {
+  const int b = blockIdx.y, reg = blockIdx.x, i = reg / 4, j = reg % 4, c = threadIdx.x;
+  const int nh = c >> 7, cc = c & 127;
+  const int rh = H >> 2, rw = W >> 2;
+  const int tiles_x = W / C4_TW, tiles_y = (H + C4_TH - 1) / C4_TH;
+  const int ty0 = (i * rh) / C4_TH, ty1 = ((i + 1) * rh - 1) / C4_TH;
+  const int tx0 = (j * rw) / C4_TW, tx1 = ((j + 1) * rw - 1) / C4_TW;
+  float s = 0.f;
+  for (int ty = ty0; ty <= ty1; ++ty)
+    for (int tx = tx0; tx <= tx1; ++tx) {
+      const int slot = (i - (ty * C4_TH) / rh) * 2 + (j - (tx * C4_TW) / rw);
+      const long long tile = ((long long)b * tiles_y + ty) * tiles_x + tx;
+      s += ip[((2 * tile + nh) * 4 + slot) * 128 + cc];
     }
-  }
-  // the 4 pixel-quad lanes (g) of each (np, r) -> one sum per channel, fixed order
-#pragma unroll
-  for (int wn = 0; wn < 2; ++wn)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v = acc[wn][h];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (lane < 16) red[wn * 128 + 32 * np + 16 * h + r] = v;
-    }
-  __syncthreads();
-  part[(((long long)b * 16 + reg) * POOL_SPLIT + sp) * C5 + t] = red[t];
+  pooled[((long long)b * C5 + c) * 16 + reg] = s / (float)(rh * rw);
 }
 
 // ------------------------------------------------------------------ tail: conv 256->512 on 4x4
@@ -2482,6 +2607,28 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
   }
 }
 
+// zero the padding of conv5 v4's input planes (everything of [PH][PW] outside the image):
+// grid (8, B * 4 planes), 16 bytes per thread and iteration
+__global__ __launch_bounds__(256) void k_c4_pad_zero(bf16_t* __restrict__ att, int H, int W) {
+  const int PH = c4_ph(H), PW = c4_pw(W);
+  bf16_t* pl = att + (long long)blockIdx.y * PH * PW * 32;
+  const int edge_rows = PH - H, side = PW - W;  // full pad rows (top + bottom), pad pixels per image row
+  const long long full = (long long)edge_rows * PW * 4, part = (long long)H * side * 4;  // 16-byte chunks
+  for (long long i = blockIdx.x * 256 + threadIdx.x; i < full + part; i += 256LL * gridDim.x) {
+    long long px;
+    if (i < full) {
+      const long long c = i >> 2;
+      const int rr = (int)(c / PW), cc = (int)(c % PW);
+      px = (long long)(rr == 0 ? 0 : H + rr) * PW + cc;
+    } else {
+      const long long c = (i - full) >> 2;
+      const int rr = (int)(c / side), k = (int)(c % side);
+      px = (long long)(rr + 1) * PW + (k == 0 ? 0 : W + k);
+    }
+    *reinterpret_cast<uint4*>(pl + px * 32 + 8 * (i & 3)) = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 struct Ws {  // workspace carve
   size_t aff1, aff2, aff5, slab, att, y, part, pooled, zpart, feat, h1, fold, stem, total;
 };
@@ -2499,9 +2646,6 @@ inline int conv_grid(int B, int H, int W) {
   const long long nt = (long long)B * ((W + CV_TW - 1) / CV_TW) * ((H + CV_TH - 1) / CV_TH);
   return (int)std::min<long long>(nt, 512);
 }
-inline long long conv3_tiles(int B, int H, int W) {
-  return (long long)B * ((W + C3_TW - 1) / C3_TW) * ((H + C3_TH - 1) / C3_TH);
-}
 inline int device_cus() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -2511,9 +2655,19 @@ inline int device_cus() {
   }();
   return n;
 }
-inline int conv3_grid(int B, int H, int W) {  // persistent, one 161 KB-LDS workgroup per CU
-  return (int)std::min<long long>(conv3_tiles(B, H, W), device_cus());
+// k_rp_gate: persistent, one 512-thread workgroup per CU over 8x32-pixel tiles
+inline int gate_grid(int B, int H, int W) {
+  return (int)std::min<long long>((long long)B * ((W + 31) / 32) * ((H + 7) / 8), device_cus());
 }
+
+inline long long conv4_tiles(int B, int H, int W) {
+  return (long long)B * ((W + C4_TW - 1) / C4_TW) * ((H + C4_TH - 1) / C4_TH);
+}
+// persistent, one 147 KB-LDS workgroup per CU, in pairs (the two channel halves of a tile)
+inline int conv4_grid(int B, int H, int W) { return 2 * (int)std::min<long long>(conv4_tiles(B, H, W), device_cus() / 2); }
+// eval: BN + ReLU + AdaptiveAvgPool(4) in conv5's epilogue when the pool bins do not overlap and
+// every 16-px fragment row of a 16x32 tile lies in one bin, a tile in at most 2 x 2 bins
+inline bool conv4_pool_fused(int H, int W) { return H % 4 == 0 && W % 64 == 0 && H >= 64 && W >= 128; }
 
 inline Ws make_ws(int es, int B, int H, int W) {
   Ws w;
@@ -2525,13 +2679,13 @@ inline Ws make_ws(int es, int B, int H, int W) {
   };
   const size_t P = (size_t)B * H * W;
   const int slab_rows = std::max(std::max(chain_grid(B, H, W), 8 * chain_grid_v2(B, H, W, 0)),
-                                 std::max(conv_grid(B, H, W), conv3_grid(B, H, W)));
+                                 std::max(conv_grid(B, H, W), conv4_grid(B, H, W)));
   w.aff1 = seg(STEM_C * sizeof(float2));
   w.aff2 = seg(FUS_C * sizeof(float2));
   w.aff5 = seg(C5 * sizeof(float2));
   w.slab = seg((size_t)slab_rows * C5 * 2 * sizeof(float));
-  w.att = seg(P * FUS_C * es);
-  w.y = seg(es == 2 ? (size_t)conv3_tiles(B, H, W) * C3_TH * C3_TW * C5 * 2 : P * C5 * es);
+  w.att = seg(es == 2 ? (size_t)B * c4_ph(H) * c4_pw(W) * FUS_C * 2 : P * FUS_C * es);
+  w.y = seg(es == 2 ? (size_t)conv4_tiles(B, H, W) * C4_TH * C4_TW * C5 * 2 : P * C5 * es);
   w.part = seg((size_t)B * 16 * POOL_SPLIT * C5 * sizeof(float));
   w.pooled = seg((size_t)B * C5 * 16 * sizeof(float));
   w.zpart = seg((size_t)TC_CHUNKS * B * C6 * 16 * sizeof(float));
@@ -2599,6 +2753,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
     k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
   }
   if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
+  if (v2) k_c4_pad_zero<<<dim3(8, B * 4), 256, 0, s>>>((bf16_t*)att, H, W);
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate
   // flags & RGBD_RATIO_F_PHASE2: train mode through phase 2 instead of the gate kernel (a test
@@ -2616,57 +2771,58 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
       static const hipError_t gattr =
           hipFuncSetAttribute((const void*)k_rp_gate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GT_SMEM);
       if (gattr != hipSuccess) return (int)gattr;
-      const int gg = (int)std::min<long long>(conv3_tiles(B, H, W), device_cus());
+      const int gg = gate_grid(B, H, W);
       k_rp_gate<<<gg, 512, GT_SMEM, s>>>(fus, B, H, W, blob, L, aff2, (bf16_t*)att);
     } else {
       CHAIN_LAUNCH(2, aff1, aff2, nullptr, att);
     }
   }
-  // conv5 + its BN statistics
+  // conv5 + its BN statistics (train) / BN + ReLU + pool (eval, v4 MODE 1)
   int gcv;
-  {
-    TimerScope ts("rp_conv3x3", s);
-    if constexpr (sizeof(T) == 2) {
-      static const hipError_t attr = hipFuncSetAttribute(
-          (const void*)k_rp_conv3x3_v3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
-      if (attr != hipSuccess) return (int)attr;
-      gcv = conv3_grid(B, H, W);
-      auto go = [&](auto kern) {
+  if constexpr (sizeof(T) == 2) {
+    // eval: the BN affine from the running statistics first (the fused epilogue applies it)
+    const int mode = training ? 0 : (conv4_pool_fused(H, W) ? 1 : 2);
+    if (!training)
+      k_bn_affine<<<C5, 256, 0, s>>>(slab, 0, C5, 0, C5, P, 0, momentum, bn.p[16], bn.p[17], bn.p[18], bn.p[19],
+                                     aff5);
+    {
+      TimerScope ts("rp_conv3x3", s);
+      gcv = conv4_grid(B, H, W);
+      const int xcd = gcv % 16 == 0;
+      float* ip = (float*)y;  // MODE 1: per-item bin partials (y is not written)
+      auto go = [&](auto kern, float* out) {
         static const hipError_t sattr =
-            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM);
-        (void)sattr;
-        kern<<<gcv, 512, C3_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, (bf16_t*)y, slab);
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C4_SMEM);
+        if (sattr != hipSuccess) return (int)sattr;
+        kern<<<gcv, 512, C4_SMEM, s>>>((const bf16_t*)att, B, H, W, blob, L, aff5, (bf16_t*)y, out, xcd);
+        return (int)hipSuccess;
       };
-#ifdef RGBD_DIAG
-      if (c3_stamps_on || c3_mode) {
-        const int md = c3_mode;
-#define C3_MODE(M)                                     \
-  if (md == M) {                                       \
-    if (c3_stamps_on)                                  \
-      go(k_rp_conv3x3_v3<true, M>);                    \
-    else                                               \
-      go(k_rp_conv3x3_v3<false, M>);                   \
-  }
-        C3_MODE(0) C3_MODE(1) C3_MODE(2) C3_MODE(3) C3_MODE(7) C3_MODE(15)
-#undef C3_MODE
-      } else
-#endif
-        go(k_rp_conv3x3_v3<false>);
+      const int e = mode == 0 ? go(k_rp_conv5_v4<0>, slab) : mode == 1 ? go(k_rp_conv5_v4<1>, ip) : go(k_rp_conv5_v4<2>, nullptr);
+      if (e != hipSuccess) return e;
+    }
+    if (training)
+      k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
+                                     bn.p[19], aff5);
+    if (mode == 1) {
+      k_rp_pool_finish_v4<<<dim3(16, B), 256, 0, s>>>((const float*)y, B, H, W, pooled);
     } else {
+      if (H % 32 == 0 && W % 128 == 0)
+        k_rp_bn_relu_pool_v4_tiles<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
+      else
+        k_rp_bn_relu_pool_v4_frag<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
+      k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
+    }
+  } else {
+    {
+      TimerScope ts("rp_conv3x3", s);
       gcv = conv_grid(B, H, W);
       k_rp_conv3x3<T><<<dim3(gcv, C5 / CV_BN), 256, 0, s>>>(att, B, H, W, blob, L, y, slab);
     }
-  }
-  k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
-                                bn.p[19], aff5);
-  if constexpr (sizeof(T) == 2)
-    if (H % (4 * C3_TH) == 0 && W % (4 * C3_TW) == 0)
-      k_rp_bn_relu_pool_tiles<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
-    else
-      k_rp_bn_relu_pool_frag<<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>((const bf16_t*)y, H, W, aff5, part);
-  else
+    k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
+                                   bn.p[19], aff5);
     k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
-  k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
+    k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
+  }
   k_rp_tail_conv<<<dim3(C6 / TC_O, TC_CHUNKS), 256, 0, s>>>(pooled, B, blob, L, zpart);
   k_rp_tail_bn<<<C6 / 4, 256, 0, s>>>(zpart, B, training, momentum, blob, L, bn, feat);
   k_rp_tail_fc1<<<128, 256, 0, s>>>(feat, B, training, blob, L, seed, seed_ctr, h1);
@@ -2696,18 +2852,9 @@ int rgbd_debug_stem_lag_stamps(void* buf) {
   return RGBD_OK;
 }
 
-int rgbd_debug_conv5_mode(int mode) {
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 3 && mode != 7 && mode != 15) return RGBD_E_ARG;
-  c3_mode = mode;
-  return RGBD_OK;
-}
-
 int rgbd_debug_conv5_stamps(void* buf) {
   unsigned long long* p = (unsigned long long*)buf;
-  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_c3_stamps), &p, sizeof(p));
-  if (e != hipSuccess) return (int)e;
-  c3_stamps_on = p != nullptr;
-  return RGBD_OK;
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_c4_stamps), &p, sizeof(p));
 }
 #endif
 
@@ -2733,6 +2880,11 @@ int rgbd_ratio_pack(int dtype, const float* const* weights_host, void* packed, v
 
 size_t rgbd_ratio_features_offset(int dtype, int B, int H, int W) {
   return make_ws(dtype == RGBD_BF16 ? 2 : 4, B > 0 ? B : 1, H > 0 ? H : 1, W > 0 ? W : 1).att;
+}
+
+
+size_t rgbd_ratio_pooled_offset(int dtype, int B, int H, int W) {
+  return make_ws(dtype == RGBD_BF16 ? 2 : 4, B > 0 ? B : 1, H > 0 ? H : 1, W > 0 ? W : 1).pooled;
 }
 
 size_t rgbd_ratio_workspace_size(int dtype, int B, int H, int W) {

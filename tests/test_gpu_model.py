@@ -9,6 +9,7 @@ import pytest
 import torch
 
 import golden_inputs as gi
+from checkers import ratio_ws
 from oracle import ratio as ratio_o
 from rgbd_amd import deform_attn, init as winit, mask_predictor, masked_attention
 
@@ -174,8 +175,7 @@ def test_bf16_train_mode_gated_features(H, W, path):
     L = _lib.lib()
     ws = ops._workspace(x.device, L.rgbd_ratio_workspace_size(1, B, H, W), "ratio")
     off = L.rgbd_ratio_features_offset(1, B, H, W)
-    att = ws[off:off + B * H * W * 128 * 2].view(torch.bfloat16).reshape(B, H, W, 128)
-    got = att.permute(0, 3, 1, 2).float().cpu()
+    got = ratio_ws.ratio_features_bf16(ws, off, B, H, W).float().cpu()
     ref = {}
     m_cpu.feature_extractor.register_forward_pre_hook(lambda mod, a: ref.__setitem__("x", a[0].detach().clone()))
     with torch.no_grad():

@@ -1,20 +1,18 @@
-"""Where conv5's cycles go per K step (diagnostic): runs the bench-shape ratio predictor (train
-mode, B = 8, 640x480) with rgbd_debug_conv5_stamps set, so workgroup 0 of the conv5 launch records
-s_memtime per wave and step of its first two tiles (the stamped instantiation of
-k_rp_conv3x3_v3), and prints the mean cycles of each segment:
-  dma    step top (after the barrier) -> DMA pieces issued
-  ks0    -> k-step 0's 32 MFMAs issued (includes waiting for its fragments)
-  ks1    -> k-step 1's 32 MFMAs issued
-  wait   -> the closing s_waitcnt (own DMA landed, own LDS reads done)
-  bar    -> the next step's top (the barrier)
-for waves 0-3 (channel half 0, priority 0) and 4-7 (channel half 1, priority 1)."""
+"""Per-step s_memtime stamps of conv5 (k_rp_conv5_v4; workgroup 0, its first two items) from the
+diagnostic build (make -C rgb-d-instance-segmentation_amd/csrc diag) or an experiment build made
+with -DC4_STAMPS (tools/build_variant.sh NAME -DC4_STAMPS [...]):
+
+    python tools/conv5_stamps.py rgb-d-instance-segmentation_amd/librgbd_hip_diag.so
+
+Prints, per step, the cycles of each segment averaged over the loader waves (0-3) and the
+compute waves (4-7): top -> weights issued -> first kx group (+ input issue) -> last MFMAs ->
+wait + barrier, and the step period."""
+import ctypes
 import os
 import sys
 
 _R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [_R]
-# the stamped kernels live in the diagnostic build only (make -C rgb-d-instance-segmentation_amd/csrc diag)
-os.environ.setdefault("RGBD_HIP_LIB", os.path.join(_R, "rgb-d-instance-segmentation_amd", "librgbd_hip_diag.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -22,35 +20,34 @@ import _rgbd_import  # noqa: E402,F401
 from rgbd_amd import _lib, init as winit, synthetic  # noqa: E402
 from rgbd_amd.modules import EnhancedDepthImageRatioPredictor  # noqa: E402
 
+h = ctypes.CDLL(os.path.join(_R, sys.argv[1]))
+for name, (res, args) in _lib.SIGNATURES.items():
+    if hasattr(h, name):
+        fn = getattr(h, name)
+        fn.restype, fn.argtypes = res, args
+h.rgbd_debug_conv5_stamps.argtypes = [ctypes.c_void_p]
+_lib._lib = h
 m = EnhancedDepthImageRatioPredictor(3)
 winit.init_deterministic(m, prefix="model.pixel_level_module.ratio_predictor.")
 m.compute_dtype = torch.bfloat16
 m = m.cuda().train()
 planes, _, _ = synthetic.make_batch(3, 8, 480, 640)
 d = torch.from_numpy(planes[:, 3:6].copy()).cuda()
-for _ in range(3):
+for _ in range(5):
     m(d)
 torch.cuda.synchronize()
-STEPS, WAVES = 18, 8
-buf = torch.zeros(2 * STEPS * WAVES * 5, dtype=torch.int64, device="cuda")
-L = _lib.lib()
-assert L.rgbd_debug_conv5_stamps(buf.data_ptr()) == 0
+buf = torch.zeros(2 * 12 * 8 * 5, dtype=torch.int64, device="cuda")
+assert h.rgbd_debug_conv5_stamps(ctypes.c_void_p(buf.data_ptr())) == 0
 m(d)
 torch.cuda.synchronize()
-assert L.rgbd_debug_conv5_stamps(None) == 0
-s = buf.cpu().numpy().reshape(2, STEPS, WAVES, 5).astype(np.int64)
-names = ["dma", "ks0", "ks1", "wait", "bar"]
-for half, waves in (("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
-    seg = np.zeros((2, STEPS - 1, 4, 5))
-    for t in range(2):
-        for st in range(STEPS - 1):
-            for wi, w in enumerate(range(WAVES)[waves]):
-                v = s[t, st, w]
-                nxt = s[t, st + 1, w, 0]
-                seg[t, st, wi] = [v[1] - v[0], v[2] - v[1], v[3] - v[2], v[4] - v[3], nxt - v[4]]
-    mean = seg.reshape(-1, 5).mean(0)
-    print(f"{half}: " + "  ".join(f"{n} {x:7.1f}" for n, x in zip(names, mean)) + f"  | step {mean.sum():7.1f} cycles")
-tot = (s[1, STEPS - 1, :, 4] - s[1, 0, :, 0]).mean() / (STEPS - 1)
-print(f"tile 1, steps 0-17: {tot:.1f} cycles per step (mean over waves); MFMA floor per SIMD 2048")
-per_step = np.diff(s[1, :, 0, 0])
-print("wave 0 step-top deltas, tile 1:", per_step.tolist())
+h.rgbd_debug_conv5_stamps(None)
+s = buf.cpu().numpy().reshape(2, 12, 8, 5).astype(np.int64)
+names = ["B issue", "kx0(+A)", "kx1-2", "wait+bar"]
+for it in range(2):
+    print(f"item {it}")
+    for st in range(12):
+        seg = np.diff(s[it, st], axis=1)  # [8 waves][4]
+        per = (s[it, st + 1, :, 0] - s[it, st, :, 0]).mean() if st < 11 else float("nan")
+        lo, hi = seg[:4].mean(0), seg[4:].mean(0)
+        print(f"  st {st:2d} period {per:7.0f} | w0-3 " + " ".join(f"{n} {v:6.0f}" for n, v in zip(names, lo))
+              + " | w4-7 " + " ".join(f"{v:6.0f}" for v in hi))
