@@ -1875,9 +1875,7 @@ __device__ __forceinline__ C4Tile c4_tile(long long t, int tiles_x, int tiles_y)
 #ifndef C4_NODMA
 #define C4_NODMA 0
 #endif
-#ifndef C4_PREF
-#define C4_PREF 0
-#endif
+
 
 // Stamps (the diagnostic build, RGBD_DIAG: rgbd_debug_conv5_stamps): workgroup 0 records, per step
 // and wave of its first two items, s_memtime at the step top, after the weight-copy issue, after
@@ -1946,25 +1944,6 @@ __global__ __launch_bounds__(512) void k_rp_conv5_v4(const bf16_t* __restrict__ 
     const char* base = (const char*)(x + ((long long)t.b * 4 + qt) * plane + ((long long)t.y0 * PW + t.x0) * 32);
     glds16(base + aoff[k], lds0 + sl * C4_A_BYTES + ((wave & 3) + 4 * k) * 1024);
   };
-#if C4_PREF
-  // L2 prefetch of a quarter's halo two quarters ahead (loaders, one dword per halo pixel through
-  // LDS-DMA into a scratch strip: no register is written): touch instruction m = w + 4k of 10
-  uint32_t poff[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int p = 64 * ((wave & 3) + 4 * k) + lane, hy = p / C4_PW, hx = p - hy * C4_PW;
-    poff[k] = p < C4_NPIX ? (uint32_t)((hy * PW + hx) * 64) : 0u;
-  }
-  auto touch = [&](const C4Tile& t, int qt, int k) {
-    const char* base = (const char*)(x + ((long long)t.b * 4 + qt) * plane + ((long long)t.y0 * PW + t.x0) * 32);
-    const uint32_t dst = lds0 + C4_RED_OFF + (wave & 3) * 256;
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(base + poff[k]), "s"(dst)
-                 : "memory");
-  };
-#endif
   // weight pieces k0..k1-1 (of 24) of step st into buffer st & 1
   auto issue_b = [&](int st, int k0, int k1) {
     const char* src = w5q + (size_t)st * C4_B_BYTES + 16 * lane;
@@ -1979,6 +1958,8 @@ __global__ __launch_bounds__(512) void k_rp_conv5_v4(const bf16_t* __restrict__ 
   const int rh = H >> 2, rw = W >> 2;  // MODE 1: pool bin size
 
 #ifndef C4_NOPRIO
+  // the copying waves' partners compute first (static priority; loaders at equal priority
+  // measured +20 %, loaders at priority +12 %)
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
   long long tile = pair;
@@ -2053,17 +2034,6 @@ __global__ __launch_bounds__(512) void k_rp_conv5_v4(const bf16_t* __restrict__ 
         if (kx == 0) C4_STAMP(2);
       }
       C4_STAMP(3);
-#if C4_PREF
-      if (loader && (wave & 3) + 4 * ky < 10) {
-        const int qp = qt + 2;  // 4, 5: the next item's quarters 0, 1
-        if (qp < 4 || has_next) {
-          touch(qp < 4 ? t : tn, qp & 3, ky);
-          asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          C4_STAMP(4);
-          continue;
-        }
-      }
-#endif
       if constexpr (C4_NODMA & 4)
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       else
