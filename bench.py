@@ -221,7 +221,7 @@ def build(args, dev, rank=0):
                 gouts=gouts, scenes=scenes, sizes=sizes)
 
 
-def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, ddp=None):
+def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, ddp=None, serial_ddp=False):
     """(forward_backward, optimizer_step, reducer, broadcaster) of one training step.
     forward_backward() leaves the (all-reduced, for N > 1) gradients in p.grad;
     optimizer_step.opt is the AdamW instance (``capturable`` for graph capture).
@@ -236,7 +236,10 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
     custom_model.py:339-351, Q2) and nothing of batch k's backward feeds batch k+1's predictor,
     so every parameter, BatchNorm buffer and dropout draw is bitwise that of the sequential
     schedule (tests/test_gpu_train_graph.py).  The hot path then keeps all its own launches on the
-    main stream (two concurrent branches when captured)."""
+    main stream (two concurrent branches when captured).
+    ``serial_ddp`` (with ddp): the gradient exchange after the backward on the main stream
+    (distributed.SerialGradReducer) and one AdamW step after it — the form a HIP graph can hold
+    with the collectives inside (the N > 1 captured step)."""
     from rgbd_amd import ops
     from rgbd_amd.distributed import (BufferBroadcaster, InBackwardOptimizer, OverlappedGradReducer,
                                       hot_path_grad_groups)
@@ -246,7 +249,12 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
     groups = hot_path_grad_groups(ctx["dsams"], ctx["dg"])
     # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
     ddp = world > 1 if ddp is None else bool(ddp)
-    reducer = OverlappedGradReducer(groups) if ddp else None
+    serial = None
+    if ddp and serial_ddp:
+        from rgbd_amd.distributed import SerialGradReducer
+        serial, reducer, overlap_opt = SerialGradReducer(groups), None, False
+    else:
+        reducer = OverlappedGradReducer(groups) if ddp else None
     bcast = BufferBroadcaster([ctx["rp"]]) if ddp else None
     hook = None if reducer is None else reducer.ready
     if overlap_opt:
@@ -294,6 +302,8 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
         torch.autograd.backward(feats, ctx["gouts"])
         if reducer is not None and not overlap_opt:  # DDP gradient exchange (RCCL over xGMI)
             reducer.finish()
+        if serial is not None:  # the same exchange after the backward, capturable
+            serial.finish()
         return feats
 
     def optimizer_step():
@@ -306,6 +316,25 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
     optimizer_step.opts = inb.opts if overlap_opt else [opt]
 
     return forward_backward, optimizer_step, reducer, bcast
+
+
+def captured_ddp_step(ctx, world, dev):
+    """N > 1: the data-parallel step with its collectives inside one HIP graph (make_parts
+    ``serial_ddp``: buffer broadcast, forward, backward, gradient all-reduce, AdamW), or None
+    when any rank could not capture it (every rank agrees before any replay, so no rank waits in
+    a collective the others never issue).  Returns (step, None) or (None, reason)."""
+    from rgbd_amd.train_graph import CapturedTrainStep
+    fb, ostep, _, _ = make_parts(ctx, world, capturable=True, ddp=True, serial_ddp=True)
+    cs, why = None, None
+    try:
+        cs = CapturedTrainStep(fb, ostep.opt, clear=lambda: ostep.opt.zero_grad(set_to_none=True))
+    except Exception as e:  # noqa: BLE001 - reported in the line, the eager step stays the value
+        why = f"{type(e).__name__}: {e}"[:300]
+    ok = torch.tensor([0 if cs is None else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        return None, why or "another rank could not capture the step"
+    return cs, None
 
 
 def make_step(ctx, world, inference=False, graph=False, pipeline=False, ddp=None):
@@ -838,6 +867,12 @@ def main():
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     if args.launcher_selftest:
         return launcher_selftest()
+    # stdout carries exactly the one JSON line: everything else the process (and the libraries it
+    # loads: RCCL prints its version banner on stdout at communicator init) writes to fd 1 goes
+    # to stderr
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -875,8 +910,19 @@ def main():
     # the same captured step software-pipelined across batches (make_parts ``pipeline``)
     dt_pipe = timed(make_step(ctx, world, graph=True, pipeline=True), args.steps, args.warmup, world) \
         if use_graph and args.pipeline_report else None
-    # N > 1 runs eagerly (the overlapped RCCL reducer is not captured): the same eager step with
-    # no collective on every rank at once gives the line's own scaling reference
+    # N > 1 (RCCL): the step with its collectives inside one HIP graph (serial exchange after the
+    # backward), timed beside the eager overlapped step; the line takes the faster of the two
+    dt_capt, capt_why = None, None
+    if ddp and args.graph and dist.get_backend() == "nccl":
+        cstep, capt_why = captured_ddp_step(ctx, world, dev)
+        if cstep is not None:
+            dt_capt = timed(cstep, args.steps, args.warmup, world, ddp=ddp)
+            for p in cstep.params:  # the graph's gradient tensors: not the next eager step's
+                p.grad = None
+    dt_overlap_eager = dt if ddp else None
+    if dt_capt is not None and dt_capt < dt:
+        dt, use_graph = dt_capt, True
+    # the same eager step with no collective on every rank at once: the line's own scaling reference
     dt_local = timed(make_step(ctx, 1), args.steps, args.warmup, world, ddp=ddp) if ddp else None
     B = args.batch
     step_ms = dt / args.steps * 1e3
@@ -916,7 +962,8 @@ def main():
                    "parallelism": f"dp{world}"},
         "distributed": {"world_size": dist.get_world_size() if ddp else 1,
                         "backend": (dist.get_backend() if ddp else None),
-                        "collectives_per_step": ("3 async all-reduce (grad buckets dsam2, dsam1, dsam0+DGGM) + "
+                        "collectives_per_step": ("3 all-reduce (grad buckets dsam2, dsam1, dsam0+DGGM; async under "
+                                                 "the backward in the eager step, after it in the captured one) + "
                                                  "2 broadcasts (ratio-predictor BN buffers)") if ddp else None},
         "optimizer": ("AdamW (lr 1e-5, weight_decay 0.0, betas (0.9, 0.999), eps 1e-8: HF TrainingArguments defaults) on the hot-path parameters, stepped inside the backward; "
                       "no gradient-norm clip: the reference Trainer's max_grad_norm=1.0 clips the norm of the whole "
@@ -930,10 +977,18 @@ def main():
                            "batch's DSAM / DGGM forward, backward and AdamW (bitwise the sequential schedule's "
                            "parameters: the predictor is forward-only and frozen, Q2)"),
         "scaling_baseline_img_s": (None if dt_local is None else round(B * world * args.steps / dt_local, 2)),
-        "scaling_baseline_note": ("N > 1: the step is eager (collectives not captured); scaling_baseline_img_s = "
-                                  "the same eager step with no all-reduce / broadcast on every rank at once, so "
-                                  "value / scaling_baseline_img_s is the cost of the data-parallel exchange; the "
-                                  "N=1 line replays a HIP graph (its eager_img_s is the eager N=1 rate)"),
+        "scaling_baseline_note": ("N > 1: scaling_baseline_img_s = the eager step with no all-reduce / broadcast on "
+                                  "every rank at once, so value / scaling_baseline_img_s is the cost of the "
+                                  "data-parallel exchange; the N=1 line replays a HIP graph (its eager_img_s is the "
+                                  "eager N=1 rate)"),
+        "ddp_captured_img_s": None if dt_capt is None else round(B * world * args.steps / dt_capt, 2),
+        "ddp_overlapped_eager_img_s": (None if dt_overlap_eager is None
+                                       else round(B * world * args.steps / dt_overlap_eager, 2)),
+        "ddp_captured_note": ("N > 1 over RCCL: the step captured with its collectives (BN-buffer broadcasts, one "
+                              "all-reduce per gradient bucket after the backward, then AdamW) and replayed "
+                              "(ddp_captured_img_s), beside the eager step with the all-reduces overlapped with the "
+                              "backward and AdamW inside it (ddp_overlapped_eager_img_s); value is the faster, "
+                              "'graph' says which" + ("" if capt_why is None else f"; not captured: {capt_why}")),
         "inference_img_s": inf,
         "kernel_ms": per,
         "roofline": {"bound": "mfma", "kernel": "k_rp_conv5_v4 (3x3 128->256, custom_model.py:1413)",
@@ -973,7 +1028,7 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, args)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=line_out, flush=True)
     if ddp:
         dist.barrier()
         dist.destroy_process_group()

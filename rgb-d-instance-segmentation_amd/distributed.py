@@ -143,6 +143,37 @@ class OverlappedGradReducer:
         return out
 
 
+class SerialGradReducer:
+    """The same exchange as ``OverlappedGradReducer`` in a form a HIP graph can hold: after the
+    backward (every side stream joined), on the current stream, one flat float32 bucket per group
+    (cascade order), its all-reduce (RCCL: captured as a kernel node on the process group's stream,
+    joined back before the next kernel), the division by the world size and the copy of the means
+    into ``p.grad``.  Nothing of the backward runs beside a collective, so the captured step keeps
+    the hot path's two concurrent branches (graph_guard); the price is the exchange's exposed
+    time.  Unlike ``GradBucket`` it also issues the collective at world size 1 (the RCCL path on a
+    one-GPU box).  Every parameter must have received a gradient (the hot path's all do)."""
+
+    def __init__(self, groups, group=None):
+        self.groups = [list(g) for g in groups]
+        self.pg = group
+        dev = self.groups[0][0].device
+        self.flats = [torch.empty(sum(p.numel() for p in g), dtype=torch.float32, device=dev) for g in self.groups]
+
+    def finish(self):
+        world = dist.get_world_size(self.pg)
+        for g, flat in zip(self.groups, self.flats):
+            if any(p.grad is None for p in g):
+                raise RuntimeError("SerialGradReducer: a parameter received no gradient")
+            torch.cat([p.grad.reshape(-1).float() for p in g], out=flat)
+            dist.all_reduce(flat, group=self.pg)
+            flat.div_(world)
+            views, off = [], 0
+            for p in g:
+                views.append(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+            torch._foreach_copy_([p.grad for p in g], views)
+
+
 class InBackwardOptimizer:
     """Optimizer steps of the hot-path parameter groups issued from inside the backward, through
     ``hot_path(..., grad_hook=opt.hook)``.  ``steps`` partitions the groups (in the order the

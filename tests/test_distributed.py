@@ -191,3 +191,56 @@ def test_gpu_hot_path_ddp_overlap_world2():
     for r in (0, 1):
         assert isinstance(res[r], float), res[r]
         assert res[r] < 1e-6, res
+
+
+def _worker_serial(rank, world, port, q):
+    """SerialGradReducer (the captured N > 1 step's exchange) on CPU tensors: every group's
+    gradients replaced by their mean over the ranks; a missing gradient fails loudly."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import _rgbd_import  # noqa: F401
+    from rgbd_amd.distributed import SerialGradReducer, hot_path_grad_groups
+    from rgbd_amd.modules import DSAModule, DepthGradientInjectionResidual
+    torch.manual_seed(0)
+    dsams = [DSAModule(4, 8), DSAModule(8, 16), DSAModule(16, 32)]
+    dg = DepthGradientInjectionResidual([4, 8, 16, 32], 3)
+    groups = hot_path_grad_groups(dsams, dg)
+    red = SerialGradReducer(groups)
+    ok = True
+    for step in range(2):  # the flat buckets are reused
+        exp = []
+        for gi, g in enumerate(groups):
+            for i, p in enumerate(g):
+                t = torch.randn(p.shape, generator=torch.Generator().manual_seed(1000 * step + 100 * gi + i))
+                p.grad = t * (rank + 1)
+                exp.append(t * (world + 1) / 2)
+        red.finish()
+        got = [p.grad for g in groups for p in g]
+        tol = 4 * world * torch.finfo(torch.float32).eps
+        errs = [float((a - b).abs().max() / (b.abs().max() + 1e-30)) for a, b in zip(got, exp)]
+        ok = ok and max(errs) <= tol
+    groups[1][0].grad = None
+    try:
+        red.finish()
+        ok = False
+    except RuntimeError:
+        pass
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_serial_reducer_world(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_serial, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}

@@ -50,13 +50,16 @@ def test_bench_launcher_json(world, H, W, backend):
                         "--height", str(H), "--width", str(W)],
                        capture_output=True, text=True, timeout=380, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]  # stdout: the one JSON line only
     out = json.loads(lines[0])
     assert out["n_gpus"] == world and out["config"]["global_batch"] == 8 * world
     assert out["distributed"]["world_size"] == world and out["config"]["parallelism"] == f"dp{world}"
     assert out["distributed"]["backend"] == backend
     assert out["value"] > 0
+    if backend == "nccl":  # the captured step with its collectives replayed beside the eager one
+        assert out["ddp_captured_img_s"] is not None, out["ddp_captured_note"]
+        assert out["ddp_overlapped_eager_img_s"] is not None
 
 
 def _free_port():
@@ -162,3 +165,75 @@ def test_ddp_step_gradients_and_buffers(world, shape, backend):
         assert grad_err < 1e-5, res
         assert buf_err == 0.0, res
         assert opt_err == 0.0, res
+
+
+def _captured_worker(port, q, shape, steps):
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        sys.path.insert(0, str(REPO))
+        import bench
+        H, W, B = shape
+        args = bench.parse(["--height", str(H), "--width", str(W), "--batch", str(B)])
+
+        def state(ctx):
+            return ([p.detach().clone() for m in ctx["dsams"] + [ctx["dg"]] for p in m.parameters()]
+                    + [b.detach().clone() for b in ctx["rp"].buffers()])
+        # CapturedTrainStep's two warmup steps + `steps` replays = 2 + steps training steps, against
+        # the same schedule run eagerly (serial exchange, one AdamW after it) and the eager bench
+        # step (all-reduces overlapped with the backward, AdamW inside it)
+        def build():  # ratio predictor in eval: the same ratio in every run (its dropout draws
+            ctx = bench.build(args, dev)  # come from a process-wide counter)
+            ctx["rp"].eval()
+            return ctx
+
+        def eager(**kw):
+            ctx = build()
+            fb, ostep, _, _ = bench.make_parts(ctx, 1, ddp=True, **kw)
+            for _ in range(2 + steps):
+                fb()
+                ostep()
+            return state(ctx)
+        ref_serial = eager(serial_ddp=True)
+        ref_overlap = eager(overlap_opt=True)
+        ctx = build()
+        cs, why = bench.captured_ddp_step(ctx, 1, dev)
+        assert cs is not None, why
+        for _ in range(steps):
+            cs()
+        torch.cuda.synchronize()
+        got = state(ctx)
+        diff = [i for i, (a, e) in enumerate(zip(got, ref_serial)) if not torch.equal(a, e)]
+        rel = max(float((a.double() - e.double()).abs().max() / (e.double().abs().max() + 1e-30))
+                  for a, e in zip(ref_serial, ref_overlap) if a.is_floating_point())
+        print(f"captured vs eager serial: {len(diff)} tensors differ; eager serial vs overlapped: max rel {rel:.3g}")
+        q.put((0, (diff, cs.width, rel)))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((0, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.timeout(400)
+def test_captured_rccl_step_bitwise_eager_world1():
+    """The N > 1 captured step (bench.captured_ddp_step: BN-buffer broadcasts, forward, backward,
+    one RCCL all-reduce per gradient bucket after the backward, AdamW — all inside one HIP graph)
+    at world 1 over RCCL on the box's one GPU: the graph captures and instantiates (at most two
+    concurrent branches), its replays run the collectives, and the parameters and ratio-predictor
+    buffers after 2 warmup steps + 3 replays are bitwise those of the eager run of the same schedule; against the eager bench step (all-reduces overlapped with the
+    backward, AdamW inside it) within 1e-6 relative (finetuning.py:98-113)."""
+    _need_devices("nccl", 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_captured_worker, args=(_free_port(), q, (96, 128, 3), 3))
+    p.start()
+    rank, res = q.get(timeout=380)
+    p.join(timeout=60)
+    assert isinstance(res, tuple), res
+    diff, width, rel = res
+    assert width <= 2
+    assert diff == [], f"state tensors differ: {diff}"
+    assert rel <= 1e-6, rel  # the two exchange schedules: the same means, the same AdamW
