@@ -239,7 +239,9 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
     main stream (two concurrent branches when captured).
     ``serial_ddp`` (with ddp): the gradient exchange after the backward on the main stream
     (distributed.SerialGradReducer) and one AdamW step after it — the form a HIP graph can hold
-    with the collectives inside (the N > 1 captured step)."""
+    with the collectives inside (the N > 1 captured step); ``serial_ddp="overlap"``: the backward's
+    launches all on the main stream and the overlapped reducer + in-backward AdamW beside them
+    (the all-reduces are then the graph's second branch)."""
     from rgbd_amd import ops
     from rgbd_amd.distributed import (BufferBroadcaster, InBackwardOptimizer, OverlappedGradReducer,
                                       hot_path_grad_groups)
@@ -250,7 +252,10 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
     # DDP: one bucket per DSAM module, all-reduced asynchronously while the backward cascade runs
     ddp = world > 1 if ddp is None else bool(ddp)
     serial = None
-    if ddp and serial_ddp:
+    bwd_side = not (ddp and serial_ddp == "overlap")
+    if ddp and serial_ddp == "overlap":
+        reducer, overlap_opt = OverlappedGradReducer(groups), True
+    elif ddp and serial_ddp:
         from rgbd_amd.distributed import SerialGradReducer
         serial, reducer, overlap_opt = SerialGradReducer(groups), None, False
     else:
@@ -298,7 +303,7 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
         prep = prepare(pv, ctx["colors"], ctx["dtype"], dsam_modules=ctx["dsams"])  # beside the ratio predictor
         ratio = ctx["rp"](pv[:, 3:6])
         feats = hot_path(pv, ratio, ctx["colors"], ctx["dsams"], ctx["dg"], dtype=ctx["dtype"], grad_hook=hook,
-                         prepared=prep)
+                         prepared=prep, overlap_bwd=bwd_side)
         torch.autograd.backward(feats, ctx["gouts"])
         if reducer is not None and not overlap_opt:  # DDP gradient exchange (RCCL over xGMI)
             reducer.finish()
@@ -318,16 +323,19 @@ def make_parts(ctx, world, capturable=False, overlap_opt=False, pipeline=False, 
     return forward_backward, optimizer_step, reducer, bcast
 
 
-def captured_ddp_step(ctx, world, dev):
+def captured_ddp_step(ctx, world, dev, serial_ddp=True):
     """N > 1: the data-parallel step with its collectives inside one HIP graph (make_parts
     ``serial_ddp``: buffer broadcast, forward, backward, gradient all-reduce, AdamW), or None
     when any rank could not capture it (every rank agrees before any replay, so no rank waits in
     a collective the others never issue).  Returns (step, None) or (None, reason)."""
     from rgbd_amd.train_graph import CapturedTrainStep
-    fb, ostep, _, _ = make_parts(ctx, world, capturable=True, ddp=True, serial_ddp=True)
+    fb, ostep, _, _ = make_parts(ctx, world, capturable=True, ddp=True, serial_ddp=serial_ddp)
     cs, why = None, None
     try:
-        cs = CapturedTrainStep(fb, ostep.opt, clear=lambda: ostep.opt.zero_grad(set_to_none=True))
+        if ostep.opt is None:  # in-backward AdamW: the step's optimizers, cleared by ostep()
+            cs = CapturedTrainStep(fb, None, opts=ostep.opts, clear=ostep)
+        else:
+            cs = CapturedTrainStep(fb, ostep.opt, clear=lambda: ostep.opt.zero_grad(set_to_none=True))
     except Exception as e:  # noqa: BLE001 - reported in the line, the eager step stays the value
         why = f"{type(e).__name__}: {e}"[:300]
     ok = torch.tensor([0 if cs is None else 1], dtype=torch.int32, device=dev)
@@ -912,16 +920,26 @@ def main():
         if use_graph and args.pipeline_report else None
     # N > 1 (RCCL): the step with its collectives inside one HIP graph (serial exchange after the
     # backward), timed beside the eager overlapped step; the line takes the faster of the two
-    dt_capt, capt_why = None, None
+    dt_capt, capt_why, dt_capt_ov, capt_ov_why = None, None, None, None
     if ddp and args.graph and dist.get_backend() == "nccl":
-        cstep, capt_why = captured_ddp_step(ctx, world, dev)
-        if cstep is not None:
-            dt_capt = timed(cstep, args.steps, args.warmup, world, ddp=ddp)
-            for p in cstep.params:  # the graph's gradient tensors: not the next eager step's
-                p.grad = None
+        for form in (True, "overlap"):
+            cstep, why = captured_ddp_step(ctx, world, dev, serial_ddp=form)
+            dtc = None
+            if cstep is not None:
+                dtc = timed(cstep, args.steps, args.warmup, world, ddp=ddp)
+                for p in cstep.params:  # the graph's gradient tensors: not the next eager step's
+                    p.grad = None
+                del cstep
+            if form is True:
+                dt_capt, capt_why = dtc, why
+            else:
+                dt_capt_ov, capt_ov_why = dtc, why
     dt_overlap_eager = dt if ddp else None
-    if dt_capt is not None and dt_capt < dt:
-        dt, use_graph = dt_capt, True
+    ddp_form = "eager, all-reduces overlapped" if ddp else None
+    for dtc, form in ((dt_capt, "captured, all-reduces after the backward"),
+                      (dt_capt_ov, "captured, all-reduces overlapped")):
+        if dtc is not None and dtc < dt:
+            dt, use_graph, ddp_form = dtc, True, form
     # the same eager step with no collective on every rank at once: the line's own scaling reference
     dt_local = timed(make_step(ctx, 1), args.steps, args.warmup, world, ddp=ddp) if ddp else None
     B = args.batch
@@ -981,14 +999,19 @@ def main():
                                   "every rank at once, so value / scaling_baseline_img_s is the cost of the "
                                   "data-parallel exchange; the N=1 line replays a HIP graph (its eager_img_s is the "
                                   "eager N=1 rate)"),
+        "ddp_form": ddp_form,
         "ddp_captured_img_s": None if dt_capt is None else round(B * world * args.steps / dt_capt, 2),
+        "ddp_captured_overlap_img_s": None if dt_capt_ov is None else round(B * world * args.steps / dt_capt_ov, 2),
         "ddp_overlapped_eager_img_s": (None if dt_overlap_eager is None
                                        else round(B * world * args.steps / dt_overlap_eager, 2)),
-        "ddp_captured_note": ("N > 1 over RCCL: the step captured with its collectives (BN-buffer broadcasts, one "
-                              "all-reduce per gradient bucket after the backward, then AdamW) and replayed "
-                              "(ddp_captured_img_s), beside the eager step with the all-reduces overlapped with the "
-                              "backward and AdamW inside it (ddp_overlapped_eager_img_s); value is the faster, "
-                              "'graph' says which" + ("" if capt_why is None else f"; not captured: {capt_why}")),
+        "ddp_captured_note": ("N > 1 over RCCL, three forms of the same step, value the fastest (ddp_form): captured "
+                              "with its collectives (BN-buffer broadcasts, one all-reduce per gradient bucket after "
+                              "the backward, then AdamW; ddp_captured_img_s); captured with the backward on one "
+                              "stream and the all-reduces + AdamW steps overlapped beside it "
+                              "(ddp_captured_overlap_img_s); eager with the all-reduces overlapped with the "
+                              "backward's two streams (ddp_overlapped_eager_img_s)"
+                              + ("" if capt_why is None else f"; serial form not captured: {capt_why}")
+                              + ("" if capt_ov_why is None else f"; overlapped form not captured: {capt_ov_why}")),
         "inference_img_s": inf,
         "kernel_ms": per,
         "roofline": {"bound": "mfma", "kernel": "k_rp_conv5_v4 (3x3 128->256, custom_model.py:1413)",

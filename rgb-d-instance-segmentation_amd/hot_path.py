@@ -316,7 +316,7 @@ class HotPathFunction(torch.autograd.Function):
         # bf16 on the GPU: the main stream runs dX2 -> dX1 -> dW1 + dW0 (one launch); the DGGM backward
         # and the dW of dsam2 run beside it on the side stream (their persistent kernels take CUs as the
         # other stream's work drains; every kernel assigns its work dynamically)
-        side = _Side(G[0].device, bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True))
+        side = _Side(G[0].device, bf16 and G[0].is_cuda and ctx.cfg.get("overlap", True) and ctx.cfg.get("overlap_bwd", True))
 
         def dggm_bwd():
             out = []
@@ -379,7 +379,7 @@ class HotPathFunction(torch.autograd.Function):
 
 
 def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch.float32, check_status=False,
-             grad_hook=None, status_sink=None, prepared=None, overlap=True):
+             grad_hook=None, status_sink=None, prepared=None, overlap=True, overlap_bwd=True):
     """Run the fused hot path.  ``dsam_modules``: the three DSAModule instances;
     ``dggm_module``: the DepthGradientInjectionResidual instance.  ``check_status`` raises the
     reference's ValueError for a degenerate depth histogram right away (synchronising);
@@ -390,6 +390,8 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
     reducer uses it to overlap the gradient all-reduce with the rest of the backward.
     ``prepared``: ``prepare(pixel_values, colors, dtype)``, launched before the ratio predictor
     (the same pixel_values / colours), so the ratio-free work overlaps it; None = inline.
+    ``overlap_bwd`` False keeps only the backward's launches on the current stream (a captured
+    data-parallel step overlaps its gradient all-reduces there instead: graph_guard's two branches).
     ``overlap`` False keeps every launch on the current stream (no side stream of the hot path's
     own: a caller that runs other work beside it on a stream of its own, e.g. the next batch's
     ratio predictor, stays within two concurrent branches when captured)."""
@@ -402,7 +404,8 @@ def hot_path(pixel_values, ratio, colors, dsam_modules, dggm_module, dtype=torch
         conv = dggm_module.depth_enhancement_layers[i][0]
         params += [conv.weight, conv.bias]
     cfg = {"dtype": dtype, "check_status": check_status, "grad_hook": grad_hook, "status_sink": status_sink,
-           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": overlap, "prepared": prepared}
+           "pack_cache": [m._pack_cache for m in dsam_modules], "overlap": overlap, "overlap_bwd": overlap_bwd,
+           "prepared": prepared}
     if prepared is not None:
         prepared.check(pixel_values, colors)
     pv = prepared.pixel_values if prepared is not None else pixel_values.detach().float().contiguous()

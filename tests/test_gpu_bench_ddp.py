@@ -59,6 +59,7 @@ def test_bench_launcher_json(world, H, W, backend):
     assert out["value"] > 0
     if backend == "nccl":  # the captured step with its collectives replayed beside the eager one
         assert out["ddp_captured_img_s"] is not None, out["ddp_captured_note"]
+        assert out["ddp_captured_overlap_img_s"] is not None, out["ddp_captured_note"]
         assert out["ddp_overlapped_eager_img_s"] is not None
 
 
@@ -199,18 +200,24 @@ def _captured_worker(port, q, shape, steps):
             return state(ctx)
         ref_serial = eager(serial_ddp=True)
         ref_overlap = eager(overlap_opt=True)
-        ctx = build()
-        cs, why = bench.captured_ddp_step(ctx, 1, dev)
-        assert cs is not None, why
-        for _ in range(steps):
-            cs()
-        torch.cuda.synchronize()
-        got = state(ctx)
+        ref_ov1 = eager(serial_ddp="overlap")
+
+        def captured(form):
+            ctx = build()
+            cs, why = bench.captured_ddp_step(ctx, 1, dev, serial_ddp=form)
+            assert cs is not None, why
+            for _ in range(steps):
+                cs()
+            torch.cuda.synchronize()
+            return state(ctx), cs.width
+        got, width = captured(True)
+        got_ov, width_ov = captured("overlap")
         diff = [i for i, (a, e) in enumerate(zip(got, ref_serial)) if not torch.equal(a, e)]
+        diff += [100 + i for i, (a, e) in enumerate(zip(got_ov, ref_ov1)) if not torch.equal(a, e)]
         rel = max(float((a.double() - e.double()).abs().max() / (e.double().abs().max() + 1e-30))
                   for a, e in zip(ref_serial, ref_overlap) if a.is_floating_point())
         print(f"captured vs eager serial: {len(diff)} tensors differ; eager serial vs overlapped: max rel {rel:.3g}")
-        q.put((0, (diff, cs.width, rel)))
+        q.put((0, (diff, max(width, width_ov), rel)))
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent
         import traceback
@@ -223,8 +230,10 @@ def test_captured_rccl_step_bitwise_eager_world1():
     one RCCL all-reduce per gradient bucket after the backward, AdamW — all inside one HIP graph)
     at world 1 over RCCL on the box's one GPU: the graph captures and instantiates (at most two
     concurrent branches), its replays run the collectives, and the parameters and ratio-predictor
-    buffers after 2 warmup steps + 3 replays are bitwise those of the eager run of the same schedule; against the eager bench step (all-reduces overlapped with the
-    backward, AdamW inside it) within 1e-6 relative (finetuning.py:98-113)."""
+    buffers after 2 warmup steps + 3 replays are bitwise those of the eager run of the same
+    schedule, and against the eager bench step (all-reduces overlapped with the backward, AdamW
+    inside it) within 1e-6 relative.  The same for the captured form with the backward on one
+    stream and the all-reduces + in-backward AdamW overlapped beside it (finetuning.py:98-113)."""
     _need_devices("nccl", 1)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
