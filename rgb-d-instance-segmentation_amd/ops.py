@@ -96,7 +96,7 @@ def _freeze(v):
     raise TypeError("device_const: numbers or nested lists / tuples of numbers only")
 
 
-def device_const(values, dtype, device):
+def device_const(values, dtype, device, _nonblocking=False):
     """A device tensor holding ``values`` (numbers, nested lists / tuples), copied once per
     distinct (values, dtype, device) and shared: callers must not modify it."""
     device = torch.device(device)
@@ -108,7 +108,11 @@ def device_const(values, dtype, device):
     if t is None:
         if cap:
             raise RuntimeError("device_const: a new constant during graph capture (run the step eagerly first)")
-        t = torch.tensor(values, dtype=dtype).to(device)
+        if _nonblocking and device.type == "cuda":
+            # the caching host allocator keeps the pinned block until the copy has run
+            t = torch.tensor(values, dtype=dtype).pin_memory().to(device, non_blocking=True)
+        else:
+            t = torch.tensor(values, dtype=dtype).to(device)
         _consts[key] = t
         if len(_consts) > _CONST_CAP:
             for old in [k for k in _consts if k not in _pinned][:len(_consts) - _CONST_CAP]:
@@ -122,17 +126,12 @@ def device_const(values, dtype, device):
 
 def device_vec(values, dtype, device):
     """A device tensor of ``values`` (a number or a flat list) that change from call to call
-    (per-batch counts and offsets):
-    copied from pinned memory without blocking the host or draining the stream.  Under graph
-    capture a copy from host memory would replay stale bytes, so there the shared constant of
-    the same values (device_const, made by the eager warm-up step) is used."""
-    device = torch.device(device)
-    if device.type == "cuda" and device.index is None:
-        device = torch.device("cuda", torch.cuda.current_device())
-    if device.type != "cuda" or capturing():
-        return device_const(values, dtype, device)
-    # the caching host allocator keeps the pinned block until the copy has run
-    return torch.tensor(values, dtype=dtype).pin_memory().to(device, non_blocking=True)
+    (per-batch counts and offsets): device_const's shared tensor when these values were seen
+    before (no copy at all), else a copy from pinned memory that neither blocks the host nor
+    drains the stream, kept in device_const's cache — so a graph capture after an eager warm-up
+    step of the same batch finds it (a capture cannot copy from host memory: replays would read
+    stale bytes)."""
+    return device_const(values, dtype, device, _nonblocking=True)
 
 
 _hc_local = threading.local()
