@@ -315,6 +315,79 @@ __device__ __forceinline__ void g_store8(const GArgs& a, int b, int bz, int m, i
   }
 }
 
+// The staged accumulator tile's epilogue for one batch entry, no split: thread = 8 columns of NR
+// rows.  The bias (the same 8 columns for every row) and every row's residual are loaded before
+// any use, then g_store8's arithmetic (bias, act, + R) and 16-byte stores.  One row at a time,
+// each row's bias / residual loads were a memory round trip of their own (the bias epilogue took
+// a (50400 x 1024, K 256) forward from 69 to 130 us).  Returns false (nothing done) outside the
+// vector shape: the caller's per-row path then runs.
+template <typename T, int TM, int TN, int NT>
+__device__ __forceinline__ bool g_epi_rows(const GArgs& a, const char* smem, int tid, int b, int m_base, int n_base,
+                                           bool vec_c) {
+  constexpr int TPR = TN / 8, RPP = NT / TPR, NR = TM / RPP;
+  const int nl = (tid % TPR) * 8, n0 = n_base + nl;
+  if (!(a.splits == 1 && vec_c && !a.bias_m && n0 + 8 <= a.N && (((uintptr_t)a.bias) & 15) == 0)) return false;
+  float bb[8];
+  if (a.bias && a.act != RGBD_ACT_RELU_GRAD) {
+    const float4 x = *reinterpret_cast<const float4*>(a.bias + n0), y = *reinterpret_cast<const float4*>(a.bias + n0 + 4);
+    bb[0] = x.x; bb[1] = x.y; bb[2] = x.z; bb[3] = x.w; bb[4] = y.x; bb[5] = y.y; bb[6] = y.z; bb[7] = y.w;
+  }
+  float rr[NR][8];
+  if (a.R) {
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const int m = m_base + tid / TPR + q * RPP;
+      const long long rb = (long long)b * a.sr + (long long)(m < a.M ? m : 0) * a.ldr + n0;
+      if (a.r_f32) {
+        const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.R) + rb);
+        const float4 y = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.R) + rb + 4);
+        rr[q][0] = x.x; rr[q][1] = x.y; rr[q][2] = x.z; rr[q][3] = x.w;
+        rr[q][4] = y.x; rr[q][5] = y.y; rr[q][6] = y.z; rr[q][7] = y.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rr[q][e] = Num<T>::to_f(reinterpret_cast<const T*>(a.R)[rb + e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    const int ml = tid / TPR + q * RPP, m = m_base + ml;
+    if (m >= a.M) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4));
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + coff<TN>(ml, nl / 4 + 1));
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (a.act == RGBD_ACT_RELU_GRAD) {
+        v[e] = rr[q][e] > 0.f ? v[e] : 0.f;
+        continue;
+      }
+      if (a.bias) v[e] += bb[e];
+      v[e] = g_act(v[e], a.act);
+      if (a.R) v[e] += rr[q][e];
+    }
+    if (a.c_f32) {
+      float* c = reinterpret_cast<float*>(a.C) + (long long)b * a.sc + (long long)m * a.ldc + n0;
+      if (a.c_round) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = bf16_to_f32(f32_to_bf16(v[e]));
+      }
+      *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      T* c = reinterpret_cast<T*>(a.C) + (long long)b * a.sc + (long long)m * a.ldc + n0;
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(c) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                  pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c[e] = Num<T>::from_f(v[e]);
+      }
+    }
+  }
+  return true;
+}
+
 template <typename T, int TM, int TN, bool AT, bool BT, bool VEC>
 __global__ __launch_bounds__(G_THREADS) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_gemm(GArgs a) {
   using Cfg = GCfg<T>;
@@ -405,6 +478,7 @@ __global__ __launch_bounds__(G_THREADS) __attribute__((amdgpu_waves_per_eu(2, 4)
   const bool vec_c = a.splits > 1 ? (a.N % 4 == 0)
                                   : ((a.N % 8 == 0) && (((uintptr_t)a.C) % 16 == 0) && (a.ldc % 8 == 0) &&
                                      (a.sc % 8 == 0) && (!a.R || (a.ldr % 8 == 0 && a.sr % 8 == 0 && ((uintptr_t)a.R) % 16 == 0)));
+  if (g_epi_rows<T, TM, TN, G_THREADS>(a, smem, tid, b, m_base, n_base, vec_c)) return;
   constexpr int TPR = TN / 8, RPP = G_THREADS / TPR;  // threads per row, rows per pass
   const int nl = (tid % TPR) * 8;
 #pragma unroll 1
@@ -719,6 +793,7 @@ __global__ __launch_bounds__(GL_THREADS, S == 2 ? 2 : 1) void k_gemm_lds(GArgs a
                                      (!a.R || (a.ldr % 8 == 0 && ((uintptr_t)a.R) % 16 == 0)));
   constexpr int TPR = TN / 8, RPP = GL_THREADS / TPR;
   const int nl = (tid % TPR) * 8;
+  if (g_epi_rows<bf16_t, TM, TN, GL_THREADS>(a, smem, tid, 0, m_base, n_base, vec_c)) return;
 #pragma unroll 1
   for (int ml = tid / TPR; ml < TM; ml += RPP) {
     const int m = m_base + ml, n0 = n_base + nl;
