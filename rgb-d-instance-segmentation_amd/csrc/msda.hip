@@ -322,7 +322,11 @@ __global__ __launch_bounds__(256) void k_msda_bwd_runs(const T* __restrict__ val
   }
 }
 
-constexpr int MSDA_RUN = 8;  // queries per run of k_msda_bwd_runs
+// queries per run of k_msda_bwd_runs: longer runs carry more taps but hold more registers
+// (measured at C2, bf16, tools/micro_msda_bwd.py: R = 2/3/4/5/6/8/16 -> 1398/1084/1003/973/938/
+// 1107/2077 us; 6 is the longest run at 3 waves per SIMD without spills; forcing the taps to be
+// recomputed after the loads instead of held saves ~30 registers but measured slower at R = 4-8)
+constexpr int MSDA_RUN = 6;
 
 int msda_levels(int L, const int* shapes_host, MsdaLevels& lv, int& S) {
   if (L < 1 || L > MSDA_MAX_L || !shapes_host) return RGBD_E_SHAPE;
