@@ -182,9 +182,16 @@ __global__ void k_rp_pack(WPtrs w, char* blob, Layout L) {
 // fixed-shape tree reduction: deterministic for a given nslab.
 // BatchNorm from the batch sums (s, q) = (sum, sum of squares) over `count` values (train) or the
 // running stats (eval): per-channel affine, running stats updated like torch (unbiased variance)
-__device__ __forceinline__ void bn_finish(double s, double q, double count, int training, float momentum,
-                                          const float* gamma, const float* beta, float* run_mean, float* run_var,
-                                          int c, float2* __restrict__ affine) {
+struct BnVals {  // one channel's gamma, beta and running statistics, loaded ahead of its sums
+  float g, b, rm, rv;
+};
+__device__ __forceinline__ BnVals bn_vals(const float* gamma, const float* beta, const float* run_mean,
+                                          const float* run_var, int c) {
+  return BnVals{gamma[c], beta[c], run_mean[c], run_var[c]};
+}
+__device__ __forceinline__ float2 bn_finish_v(double s, double q, double count, int training, float momentum,
+                                              const BnVals& p, float* run_mean, float* run_var, int c,
+                                              float2* __restrict__ affine) {
   float mean, var;
   if (training) {
     const double m = s / count;
@@ -193,20 +200,37 @@ __device__ __forceinline__ void bn_finish(double s, double q, double count, int 
     mean = (float)m;
     var = (float)v;
     const double unb = count > 1.0 ? v * count / (count - 1.0) : v;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    run_mean[c] = (1.f - momentum) * p.rm + momentum * mean;
+    run_var[c] = (1.f - momentum) * p.rv + momentum * (float)unb;
   } else {
-    mean = run_mean[c];
-    var = run_var[c];
+    mean = p.rm;
+    var = p.rv;
   }
-  const float sc = gamma[c] / sqrtf(var + BN_EPS);
-  affine[c] = make_float2(sc, beta[c] - mean * sc);
+  const float sc = p.g / sqrtf(var + BN_EPS);
+  const float2 af = make_float2(sc, p.b - mean * sc);
+  affine[c] = af;
+  return af;
 }
+__device__ __forceinline__ float2 bn_finish(double s, double q, double count, int training, float momentum,
+                                            const float* gamma, const float* beta, float* run_mean, float* run_var,
+                                            int c, float2* __restrict__ affine) {
+  return bn_finish_v(s, q, count, training, momentum, bn_vals(gamma, beta, run_mean, run_var, c), run_mean, run_var,
+                     c, affine);
+}
+__device__ __forceinline__ double wave_sum_dbl(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// the channel's parameters load with the slab rows (thread 0), the sums reduce per wave by
+// shuffles, then the four wave sums in order: one barrier instead of the eight of a tree
 __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, int nslab, int row, int c_off, int c,
                                                double count, int training, float momentum, const float* gamma,
                                                const float* beta, float* run_mean, float* run_var,
                                                float2* __restrict__ affine) {
-  __shared__ double red[2][256];
+  __shared__ double red[2][4];
+  BnVals pv{};
+  if (threadIdx.x == 0) pv = bn_vals(gamma, beta, run_mean, run_var, c);
   double s = 0.0, q = 0.0;
   if (training) {
     // eight slab rows per thread in flight at once, summed in the same (row) order
@@ -226,18 +250,16 @@ __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, i
       q += (double)slab[((long long)i * row + c_off + c) * 2 + 1];
     }
   }
-  red[0][threadIdx.x] = s;
-  red[1][threadIdx.x] = q;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + o];
-      red[1][threadIdx.x] += red[1][threadIdx.x + o];
-    }
-    __syncthreads();
+  s = wave_sum_dbl(s);
+  q = wave_sum_dbl(q);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s;
+    red[1][threadIdx.x >> 6] = q;
   }
+  __syncthreads();
   if (threadIdx.x != 0) return;
-  bn_finish(red[0][0], red[1][0], count, training, momentum, gamma, beta, run_mean, run_var, c, affine);
+  bn_finish_v(((red[0][0] + red[0][1]) + red[0][2]) + red[0][3], ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3],
+              count, training, momentum, pv, run_mean, run_var, c, affine);
 }
 __global__ __launch_bounds__(256) void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off,
                                                    int C, double count, int training, float momentum,
@@ -578,13 +600,12 @@ __device__ __forceinline__ void stem_sum_body(const T* __restrict__ src, int n, 
   if (e < seg_len) {
     const T* p = src + s * seg_stride + e;
     int k = grp;
-    for (; k + 48 < n; k += 64) {
-      const double a0 = (double)p[k * stride], a1 = (double)p[(k + 16) * stride];
-      const double a2 = (double)p[(k + 32) * stride], a3 = (double)p[(k + 48) * stride];
-      acc += a0;
-      acc += a1;
-      acc += a2;
-      acc += a3;
+    for (; k + 112 < n; k += 128) {  // eight loads in flight, added in k order
+      double a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = (double)p[(k + 16 * u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += a[u];
     }
     for (; k < n; k += 16) acc += (double)p[k * stride];
   }
@@ -645,27 +666,63 @@ __global__ __launch_bounds__(256) void k_stem_s2(const double* __restrict__ F, c
   const double* ck = fr + (long long)ckind * SF_REC;
   const double* cc = ce + ((long long)rkind * 2 + (ckind - 2)) * SC_REC;
   const int trow = ((c1 * 3 + c2) * 13 + ly + 6) * 3, tcol = ((c1 * 3 + c2) * 13 + lx + 6) * 3;
+  // every load in flight together (j = 0..2 index valid rows whatever the bounds; the loops over
+  // the data-dependent bounds waited for each load in turn), applied in the same order as before
   double s = is_s1 ? F[SL_NF + c1] : F[(c1 * 13 + ly + 6) * SL_NL + c2 * 13 + lx + 6];
-  for (int j = rlo; j < rhi; ++j) s -= is_s1 ? rk[SF_T * 13 + c1 * 3 + j] : rk[(trow + j) * 13 + lx + 6];
-  for (int j = clo; j < chi; ++j) s -= is_s1 ? ck[SF_T * 13 + c1 * 3 + j] : ck[(tcol + j) * 13 + ly + 6];
-  for (int jr = rlo; jr < rhi; ++jr)  // corners: excluded in both, subtracted twice
-    for (int jc = clo; jc < chi; ++jc)
-      s += is_s1 ? cc[SF_T * 39 + (c1 * 3 + jr) * 3 + jc] : cc[((trow + jr) * 13 + lx + 6) * 3 + jc];
+  double rv[3], cv[3], xv[3][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    rv[j] = is_s1 ? rk[SF_T * 13 + c1 * 3 + j] : rk[(trow + j) * 13 + lx + 6];
+    cv[j] = is_s1 ? ck[SF_T * 13 + c1 * 3 + j] : ck[(tcol + j) * 13 + ly + 6];
+#pragma unroll
+    for (int jc = 0; jc < 3; ++jc)
+      xv[j][jc] = is_s1 ? cc[SF_T * 39 + (c1 * 3 + j) * 3 + jc] : cc[((trow + j) * 13 + lx + 6) * 3 + jc];
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    if (j >= rlo && j < rhi) s -= rv[j];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    if (j >= clo && j < chi) s -= cv[j];
+#pragma unroll
+  for (int jr = 0; jr < 3; ++jr)  // corners: excluded in both, subtracted twice
+#pragma unroll
+    for (int jc = 0; jc < 3; ++jc)
+      if (jr >= rlo && jr < rhi && jc >= clo && jc < chi) s += xv[jr][jc];
   if (is_s1)
     S1[k] = s;
   else
     S2[i] = s;
 }
 
+// fold: [W1' 192 x 168 bf16][W2' 128 x 192 bf16][b1' 192 f32][b2' 128 f32] (BN folding below)
+constexpr size_t FOLD_W1 = 0, FOLD_W2 = FOLD_W1 + (size_t)STEM_C * STEM_K2 * 2;
+constexpr size_t FOLD_B1 = FOLD_W2 + (size_t)FUS_C * STEM_C * 2, FOLD_B2 = FOLD_B1 + STEM_C * 4;
+constexpr size_t FOLD_BYTES = FOLD_B2 + FUS_C * 4;
+
 // Per stem channel o (one block each): sum y = N b + w.S1, sum y^2 = N b^2 + 2 b w.S1 + w S2 w^T,
-// then the BatchNorm of bn_affine_body (train mode) from the double sums.
+// then the BatchNorm of bn_affine_body (train mode) from the double sums, and the block folds
+// its affine into W1' / b1' row o as k_rp_fold (which 1) does.  Blocks STEM_C .. STEM_C + 32 B - 1
+// zero conv5 v4's input padding (k_c4_pad_zero's work: grid (8, 4 B) flattened), so neither
+// small kernel is a launch of its own on the predictor's critical path.
+__device__ void c4_pad_body(bf16_t* __restrict__ att, int H, int W, int bx, int plane, int nbx);
 __global__ __launch_bounds__(256) void k_stem_bn(const double* __restrict__ S2, const double* __restrict__ S1,
                                                  const char* __restrict__ blob, Layout L, double count, float momentum,
-                                                 BnPtrs bn, float2* __restrict__ affine) {
+                                                 BnPtrs bn, float2* __restrict__ affine, char* __restrict__ fold,
+                                                 bf16_t* __restrict__ att, int H, int W) {
+  if ((int)blockIdx.x >= STEM_C) {  // block-uniform
+    const int p = (int)blockIdx.x - STEM_C;
+    c4_pad_body(att, H, W, p % 8, p / 8, 8);
+    return;
+  }
   __shared__ double red[2][256];
   __shared__ double w[147];
+  __shared__ float2 s_aff;
   const int o = blockIdx.x, t = threadIdx.x;
   const bf16_t* w1s = (const bf16_t*)(blob + L.w1s);
+  // the fold's source row, loaded now (in flight through the reduction)
+  const float wf = t < STEM_K2 ? ((const float*)(blob + L.w1f))[(size_t)o * STEM_K2 + t] : 0.f;
+  const float bf = ((const float*)(blob + L.b1))[o];
   if (t < 147) w[t] = (double)bf16_to_f32(w1s[o * STEM_K2 + ((t / 49) * 7 + (t % 49) / 7) * 8 + t % 7]);
   __syncthreads();
   double a = 0.0, q = 0.0;
@@ -692,13 +749,19 @@ __global__ __launch_bounds__(256) void k_stem_bn(const double* __restrict__ S2, 
     }
     __syncthreads();
   }
-  if (t != 0) return;
-  const double bias = (double)((const float*)(blob + L.b1))[o];
-  const double sy = count * bias + red[0][0];
-  const double sq = count * bias * bias + 2.0 * bias * red[0][0] + red[1][0];
-  const int l = o / 64, c = o % 64;
-  bn_finish(sy, sq, count, 1, momentum, bn.p[4 * l], bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], c,
-            affine + 64 * l);
+  if (t == 0) {
+    const double bias = (double)bf;
+    const double sy = count * bias + red[0][0];
+    const double sq = count * bias * bias + 2.0 * bias * red[0][0] + red[1][0];
+    const int l = o / 64, c = o % 64;
+    s_aff = bn_finish(sy, sq, count, 1, momentum, bn.p[4 * l], bn.p[4 * l + 1], bn.p[4 * l + 2], bn.p[4 * l + 3], c,
+                      affine + 64 * l);
+  }
+  __syncthreads();
+  // BN1 -> W1', b1' (k_rp_fold's arithmetic)
+  const float2 af = s_aff;
+  if (t < STEM_K2) ((bf16_t*)(fold + FOLD_W1))[(size_t)o * STEM_K2 + t] = f32_to_bf16(wf * af.x);
+  if (t == 0) ((float*)(fold + FOLD_B1))[o] = __builtin_fmaf(bf, af.x, af.y);
 }
 
 struct StemWs {
@@ -727,7 +790,7 @@ inline StemWs stem_ws(int B, int H, int W) {
 
 // the moments of every window and the stem BN affines (aff1) + running stats, train mode
 int stem_bn_moments(const float* depth3, long long bstride, int B, int H, int W, const char* blob, const Layout& L,
-                    float momentum, const BnPtrs& bn, float2* aff1, char* ws, hipStream_t s) {
+                    float momentum, const BnPtrs& bn, float2* aff1, char* fold, bf16_t* att, char* ws, hipStream_t s) {
   const StemGeom g = stem_geom(B, H, W);
   const StemWs w = stem_ws(B, H, W);
   double* part = (double*)(ws + w.part);
@@ -756,7 +819,7 @@ int stem_bn_moments(const float* depth3, long long bstride, int B, int H, int W,
   StemSums ss{part, fch, cells, F, fr, ce, g.nwg, B * g.mx, B};
   k_stem_sums<<<SS_B0 + SS_B1 + SS_B2, 256, 0, s>>>(ss);
   k_stem_s2<<<ceil_div(147 * 147 + 147, 256), 256, 0, s>>>(F, fr, ce, S2, S1);
-  k_stem_bn<<<STEM_C, 256, 0, s>>>(S2, S1, blob, L, (double)B * H * W, momentum, bn, aff1);
+  k_stem_bn<<<STEM_C + 32 * B, 256, 0, s>>>(S2, S1, blob, L, (double)B * H * W, momentum, bn, aff1, fold, att, H, W);
   return RGBD_OK;
 }
 
@@ -998,10 +1061,7 @@ __device__ __forceinline__ void reduce_scatter16(float (&v)[N], int r) {
 // ------------------------------------------------------------------ BN folding (bf16 chain)
 // Once the statistics of a BN layer are known, fold its affine (sc, sh) into the producing
 // layer: W' = bf16(sc * W_f32) row-wise, b' = sc * b + sh, so the chain applies only the ReLU.
-// fold: [W1' 192 x 168 bf16][W2' 128 x 192 bf16][b1' 192 f32][b2' 128 f32].  which = 1 | 2.
-constexpr size_t FOLD_W1 = 0, FOLD_W2 = FOLD_W1 + (size_t)STEM_C * STEM_K2 * 2;
-constexpr size_t FOLD_B1 = FOLD_W2 + (size_t)FUS_C * STEM_C * 2, FOLD_B2 = FOLD_B1 + STEM_C * 4;
-constexpr size_t FOLD_BYTES = FOLD_B2 + FUS_C * 4;
+// (fold layout: FOLD_W1 .. FOLD_BYTES above)  which = 1 | 2.
 __global__ __launch_bounds__(256) void k_rp_fold(const char* __restrict__ blob, Layout L,
                                                  const float2* __restrict__ aff, int which, char* __restrict__ fold) {
   const int c = blockIdx.x;
@@ -1554,6 +1614,7 @@ __global__ __launch_bounds__(512) void k_rp_gate(const bf16_t* __restrict__ fus,
       nxt[t][1] = make_uint2(q[2], q[3]);
     }
   };
+  // (one tile ahead: two and three tiles ahead measured the same, 0.252-0.258 ms, round 6)
   fetch(blockIdx.x);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const TileDec td = tile_dec((unsigned)(ntiles - 1 - tile), per, (unsigned)tiles_x, C2W_TH, C2W_TW);
@@ -2579,12 +2640,12 @@ __global__ __launch_bounds__(512) void k_rp_tail_head(const float* __restrict__ 
 
 // zero the padding of conv5 v4's input planes (everything of [PH][PW] outside the image):
 // grid (8, B * 4 planes), 16 bytes per thread and iteration
-__global__ __launch_bounds__(256) void k_c4_pad_zero(bf16_t* __restrict__ att, int H, int W) {
+__device__ void c4_pad_body(bf16_t* __restrict__ att, int H, int W, int bx, int plane, int nbx) {
   const int PH = c4_ph(H), PW = c4_pw(W);
-  bf16_t* pl = att + (long long)blockIdx.y * PH * PW * 32;
+  bf16_t* pl = att + (long long)plane * PH * PW * 32;
   const int edge_rows = PH - H, side = PW - W;  // full pad rows (top + bottom), pad pixels per image row
   const long long full = (long long)edge_rows * PW * 4, part = (long long)H * side * 4;  // 16-byte chunks
-  for (long long i = blockIdx.x * 256 + threadIdx.x; i < full + part; i += 256LL * gridDim.x) {
+  for (long long i = bx * 256 + threadIdx.x; i < full + part; i += 256LL * nbx) {
     long long px;
     if (i < full) {
       const long long c = i >> 2;
@@ -2597,6 +2658,10 @@ __global__ __launch_bounds__(256) void k_c4_pad_zero(bf16_t* __restrict__ att, i
     }
     *reinterpret_cast<uint4*>(pl + px * 32 + 8 * (i & 3)) = make_uint4(0u, 0u, 0u, 0u);
   }
+}
+
+__global__ __launch_bounds__(256) void k_c4_pad_zero(bf16_t* __restrict__ att, int H, int W) {
+  c4_pad_body(att, H, W, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 struct Ws {  // workspace carve
@@ -2716,14 +2781,16 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   } while (0)
   // stem BNs (scale1/2/3, 64 channels each, concatenated :1463)
   if (training && v2 && stem_moments_ok(H, W)) {  // bf16 train: the moments of the windows (no stem pass)
-    const int e = stem_bn_moments(depth3, bstride, B, H, W, blob, L, momentum, bn, aff1, ws + w.stem, s);
+    // (+ the BN1 fold and conv5 v4's input padding)
+    const int e = stem_bn_moments(depth3, bstride, B, H, W, blob, L, momentum, bn, aff1, fold, (bf16_t*)att,
+                                  ws + w.stem, s);
     if (e != RGBD_OK) return e;
   } else {
     if (training) CHAIN_LAUNCH(0, nullptr, nullptr, slab, nullptr);
     k_bn_affine_stem<<<STEM_C, 256, 0, s>>>(slab, nslab_ch0, P, training, momentum, bn, aff1);
+    if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
+    if (v2) k_c4_pad_zero<<<dim3(8, B * 4), 256, 0, s>>>((bf16_t*)att, H, W);
   }
-  if (v2) k_rp_fold<<<STEM_C, 256, 0, s>>>(blob, L, aff1, 1, fold);  // BN1 -> W1', b1'
-  if (v2) k_c4_pad_zero<<<dim3(8, B * 4), 256, 0, s>>>((bf16_t*)att, H, W);
   // fusion BN; train + bf16: phase 1 also stores its raw fusion output (in the conv5 output
   // buffer, which is dead until conv5) for k_rp_gate
   // flags & RGBD_RATIO_F_PHASE2: train mode through phase 2 instead of the gate kernel (a test
