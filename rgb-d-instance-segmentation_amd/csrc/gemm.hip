@@ -32,6 +32,7 @@
 #include "mfma.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rgbd {
 namespace {
@@ -413,11 +414,14 @@ __global__ __launch_bounds__(G_THREADS) __attribute__((amdgpu_waves_per_eu(2, 4)
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // K stages through two register sets and two LDS buffers: the loads of stage kt + 2 are issued
-  // while stage kt is multiplied, and land in LDS one stage later (two stages of latency cover);
-  // the barrier between stages waits for LDS traffic only (loads stay in flight across it)
-  SA ra0, ra1;
-  SB rb0, rb1;
+  // K stages through PD register sets and two LDS buffers: the loads of stage kt + PD are issued
+  // while stage kt is multiplied and are stored to LDS PD - 1 stages later (the barrier between
+  // stages waits for LDS traffic only; loads stay in flight across it).  PD = 2 for the 128 x 128
+  // tiles (register budget); PD = 4 for the 64 x 64 tiles of small GEMMs, whose stages are short
+  // and otherwise each wait for a load issued only one stage earlier.
+  constexpr int PD = TM == 64 ? 4 : 2;
+  SA ra[PD];
+  SB rb[PD];
   const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
   auto load = [&](SA& ra, SB& rb, int kt) {
     const int k0 = kbeg + kt * KS;
@@ -446,20 +450,30 @@ __global__ __launch_bounds__(G_THREADS) __attribute__((amdgpu_waves_per_eu(2, 4)
         for (int i = 0; i < FM; ++i) mma(acc[j][i], fn[j], fm[i]);
     }
   };
-  if (nk > 0) load(ra0, rb0, 0);
-  if (nk > 1) load(ra1, rb1, 1);
-  if (nk > 0) put(ra0, rb0, 0);
+#pragma unroll
+  for (int j = 0; j < PD; ++j)
+    if (j < nk) load(ra[j], rb[j], j);
+  if (nk > 0) put(ra[0], rb[0], 0);
   lds_barrier();
-  for (int kt = 0; kt < nk; kt += 2) {
-    if (kt + 2 < nk) load(ra0, rb0, kt + 2);
-    compute(0);
-    if (kt + 1 < nk) put(ra1, rb1, 1);
+  // step kt: register set kt % PD went to LDS buffer kt % 2 before the last barrier and takes
+  // stage kt + PD now; set (kt + 1) % PD goes to the other buffer after the multiply
+  auto step = [&](auto J, int kt) {
+    constexpr int j = decltype(J)::value;
+    if (kt + PD < nk) load(ra[j], rb[j], kt + PD);
+    compute(j & 1);
+    if (kt + 1 < nk) put(ra[(j + 1) % PD], rb[(j + 1) % PD], (j + 1) & 1);
     lds_barrier();
+  };
+  for (int kt = 0; kt < nk; kt += PD) {
+    step(std::integral_constant<int, 0>{}, kt);
     if (kt + 1 >= nk) break;
-    if (kt + 3 < nk) load(ra1, rb1, kt + 3);
-    compute(1);
-    if (kt + 2 < nk) put(ra0, rb0, 0);
-    lds_barrier();
+    step(std::integral_constant<int, 1>{}, kt + 1);
+    if constexpr (PD == 4) {
+      if (kt + 2 >= nk) break;
+      step(std::integral_constant<int, 2>{}, kt + 2);
+      if (kt + 3 >= nk) break;
+      step(std::integral_constant<int, 3>{}, kt + 3);
+    }
   }
 
   // epilogue: accumulators -> LDS (float32 tile) -> rows of 8 outputs per thread, coalesced
