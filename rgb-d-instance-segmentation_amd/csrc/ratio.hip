@@ -2377,122 +2377,131 @@ __global__ void k_rp_pool_finish(const float* __restrict__ part, int B, int H, i
   pooled[e] = s / (float)cnt;
 }
 
-// Tail conv 256->512 (3x3 pad 1 on the 4x4 pooled map) as K-split partial sums: workgroup =
-// (32 output channels, 16 input channels); the filter slice [16 c][9 tap][32 o] and a zero-padded
-// 6x6 copy of 8 images' pooled planes sit in LDS; thread = 4 outputs x one 4-pixel row of one
-// image (4x4 register tile).  zpart[chunk][b][o][16]; the sum over the 16 chunks (fixed order)
-// happens in k_rp_tail_bn.
-constexpr int TC_O = 32, TC_C = 16, TC_IMG = 8, TC_CHUNKS = C5 / TC_C;
+// Tail conv chunks: the 16-channel groups whose partial sums the fused kernel adds in order.
+constexpr int TC_C = 16, TC_CHUNKS = C5 / TC_C;
 
-__global__ __launch_bounds__(256) void k_rp_tail_conv(const float* __restrict__ pooled, int B,
-                                                      const char* __restrict__ blob, Layout L,
-                                                      float* __restrict__ zpart) {
-  __shared__ float sw[TC_C * 9 * TC_O];
-  __shared__ float sp[TC_C * TC_IMG * 36];
+__device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned long long idx) {
+  unsigned long long z = seed + idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// Tail conv 256->512 + BN(512) + ReLU + AdaptiveAvgPool2d(1) in one launch (k_rp_tail_conv +
+// k_rp_tail_bn, bitwise the same values): workgroup = two output channels over ALL 256 input
+// channels, so the BN of its channels needs no other workgroup.  LDS holds 8 images' pooled maps
+// unpadded [256 c][8 b][16] (128 KB: out-of-map taps read 0.f, the padded copy's value) and the
+// two channels' filters [256 c][3 ky][2 o][4]; 512 threads, thread = (chunk k, image b, row py): 2 o x
+// 4 px of the 16-channel chunk k, accumulated in tail_conv's order
+// (cl, ky, kx; mul then add); then z = b6 + the 16 chunk partials in chunk order (tail_bn's
+// zval) and tail_bn's statistics / running-stat update / ReLU / mean over the 16 positions, one
+// wave per channel.  256 workgroups (one per CU), eight waves each (two per SIMD: the LDS reads of
+// one wave under the other's arithmetic).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int TB_SP = C5 * 8 * 16;                  // floats: pooled, 8 images
+constexpr int TB_SW = C5 * 3 * 2 * 4;               // floats: filters of 2 channels
+constexpr int TB_ZS = 2 * 32 * 16;                  // floats: z of the 2 channels, B <= 32
+constexpr size_t TB_SMEM = (size_t)(TB_SP + TB_SW + TB_ZS) * 4;
+static_assert(TB_SMEM <= 163840 && TC_CHUNKS * 2 * 8 * 16 <= TB_SP, "tail conv+bn LDS");
+__global__ __launch_bounds__(512) void k_rp_tail_convbn(const float* __restrict__ pooled, int B, int training,
+                                                        float momentum, const char* __restrict__ blob, Layout L,
+                                                        BnPtrs bn, float* __restrict__ feat) {
+  extern __shared__ __attribute__((aligned(16))) float tsm[];
+  float* sp = tsm;                  // [256 c][8 b][16]; later the chunk partials [16 k][2 o][8 b][16]
+  float* sw = tsm + TB_SP;          // [256 c][3 ky][2 o][4]
+  float* zs = sw + TB_SW;           // [2 o][B * 16]
+  const int tid = threadIdx.x, o0 = blockIdx.x * 2;
   const float* w6 = (const float*)(blob + L.w6);
-  const int o0 = blockIdx.x * TC_O, c0 = blockIdx.y * TC_C;
-  // staging: every thread's loads issued together, then the LDS writes (a load -> store loop
-  // waited for each load in turn: ~18 dependent memory round trips per stage)
-  constexpr int TC_NW = TC_O * TC_C * 9 / 256;
-  static_assert(TC_O * TC_C * 9 % 256 == 0 && TC_C * TC_IMG * 36 % 256 == 0, "tail conv staging");
   {
-    float wv[TC_NW];
+    float wv[2 * C5 * 9 / 512];
 #pragma unroll
-    for (int q = 0; q < TC_NW; ++q) {
-      const int i = threadIdx.x + 256 * q, ol = i / (TC_C * 9), r = i % (TC_C * 9);  // r = cl * 9 + tap
-      wv[q] = w6[((long long)(o0 + ol) * C5 + c0) * 9 + r];
-    }
+    for (int q = 0; q < 2 * C5 * 9 / 512; ++q) wv[q] = w6[(long long)o0 * C5 * 9 + tid + 512 * q];
 #pragma unroll
-    for (int q = 0; q < TC_NW; ++q) {
-      const int i = threadIdx.x + 256 * q, ol = i / (TC_C * 9), r = i % (TC_C * 9);
-      sw[r * TC_O + ol] = wv[q];
+    for (int q = 0; q < 2 * C5 * 9 / 512; ++q) {
+      const int i = tid + 512 * q, ol = i / (C5 * 9), r = i % (C5 * 9), c = r / 9, tap = r % 9;
+      sw[((c * 3 + tap / 3) * 2 + ol) * 4 + tap % 3] = wv[q];
     }
   }
-  const int og = threadIdx.x >> 5, im = (threadIdx.x & 31) >> 2, py = threadIdx.x & 3;
-  for (int b0 = 0; b0 < B; b0 += TC_IMG) {
-    __syncthreads();
+  const int ck = tid >> 5, bl = (tid >> 2) & 7, py = tid & 3;
+  for (int b0 = 0; b0 < B; b0 += 8) {
+    __syncthreads();  // previous group's partial sums consumed
     {
-      constexpr int TC_NP = TC_C * TC_IMG * 36 / 256;
-      float pv[TC_NP];
+      constexpr int NQ = TB_SP / 4 / 512;  // float4 per thread
+      float4 pv[NQ];
 #pragma unroll
-      for (int e = 0; e < TC_NP; ++e) {
-        const int i = threadIdx.x + 256 * e;
-        const int cl = i / (TC_IMG * 36), r = i % (TC_IMG * 36), j = r / 36, q = r % 36;
-        const int yy = q / 6 - 1, xx = q % 6 - 1, b = b0 + j;
-        const bool in = b < B && yy >= 0 && yy < 4 && xx >= 0 && xx < 4;
-        const float v = pooled[in ? ((long long)b * C5 + c0 + cl) * 16 + yy * 4 + xx : 0];  // unconditional load
-        pv[e] = in ? v : 0.f;
+      for (int u = 0; u < NQ; ++u) {
+        const int e = tid + 512 * u, q = e & 3, c = (e >> 2) & (C5 - 1), b = b0 + (e >> 10);
+        pv[u] = b < B ? *reinterpret_cast<const float4*>(pooled + ((long long)b * C5 + c) * 16 + 4 * q)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int e = 0; e < TC_NP; ++e) sp[threadIdx.x + 256 * e] = pv[e];
+      for (int u = 0; u < NQ; ++u) {
+        const int e = tid + 512 * u, q = e & 3, c = (e >> 2) & (C5 - 1), b = e >> 10;
+        *reinterpret_cast<float4*>(sp + (c * 8 + b) * 16 + 4 * q) = pv[u];
+      }
     }
     __syncthreads();
-    float acc[4][4];
+    // pixel pairs in two-wide vectors: packed multiplies and adds (v_pk_mul_f32 / v_pk_add_f32),
+    // each lane's arithmetic the scalar mul-then-add of tail_conv
+    f32x2 acc[2][2];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int ol = 0; ol < 2; ++ol)
 #pragma unroll
-      for (int x = 0; x < 4; ++x) acc[a][x] = 0.f;
-#pragma unroll 2
+      for (int x = 0; x < 2; ++x) acc[ol][x] = f32x2{0.f, 0.f};
+#pragma unroll 4
     for (int cl = 0; cl < TC_C; ++cl) {
+      const int c = ck * TC_C + cl;
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
-        const float* row = &sp[(cl * TC_IMG + im) * 36 + (py + ky) * 6];
-        float r[6];
-#pragma unroll
-        for (int x = 0; x < 6; ++x) r[x] = row[x];
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const float4 wv = *(const float4*)&sw[(cl * 9 + ky * 3 + kx) * TC_O + 4 * og];
-#pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            acc[0][x] += wv.x * r[x + kx];
-            acc[1][x] += wv.y * r[x + kx];
-            acc[2][x] += wv.z * r[x + kx];
-            acc[3][x] += wv.w * r[x + kx];
-          }
+        const int y = py + ky - 1;
+        float r[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (y >= 0 && y < 4) {
+          const float4 v = *reinterpret_cast<const float4*>(sp + (c * 8 + bl) * 16 + 4 * y);
+          r[1] = v.x; r[2] = v.y; r[3] = v.z; r[4] = v.w;
         }
+        const float4 w0 = *reinterpret_cast<const float4*>(sw + ((c * 3 + ky) * 2 + 0) * 4);
+        const float4 w1 = *reinterpret_cast<const float4*>(sw + ((c * 3 + ky) * 2 + 1) * 4);
+        const float wa[3] = {w0.x, w0.y, w0.z}, wb[3] = {w1.x, w1.y, w1.z};
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int x = 0; x < 2; ++x) {
+            const f32x2 rv = f32x2{r[2 * x + kx], r[2 * x + 1 + kx]};
+            acc[0][x] += f32x2{wa[kx], wa[kx]} * rv;
+            acc[1][x] += f32x2{wb[kx], wb[kx]} * rv;
+          }
       }
     }
-    const int b = b0 + im;
-    if (b < B) {
+    __syncthreads();  // every thread's pooled reads done: the region takes the chunk partials
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-        *(float4*)&zpart[(((long long)blockIdx.y * B + b) * C6 + o0 + 4 * og + a) * 16 + py * 4] =
-            make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
+    for (int ol = 0; ol < 2; ++ol)
+      *reinterpret_cast<float4*>(sp + ((ck * 2 + ol) * 8 + bl) * 16 + 4 * py) =
+          make_float4(acc[ol][0].x, acc[ol][0].y, acc[ol][1].x, acc[ol][1].y);
+    __syncthreads();
+    if (tid < 256) {  // z = b6 + the chunk partials in chunk order: thread = (o, image, position)
+      const int ol = tid >> 7, b = (tid >> 4) & 7, pos = tid & 15;
+      float z = ((const float*)(blob + L.b6))[o0 + ol];
+#pragma unroll
+      for (int k = 0; k < TC_CHUNKS; ++k) z += sp[((k * 2 + ol) * 8 + b) * 16 + pos];
+      if (b0 + b < B) zs[ol * (B * 16) + (b0 + b) * 16 + pos] = z;
     }
   }
-}
-
-__device__ __forceinline__ double wave_sum_d(double v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
-// z6 = b6 + sum of the conv partials; BN(512) with batch statistics (train: running stats
-// updated, unbiased variance) or running statistics; ReLU; AdaptiveAvgPool2d(1).  One wave per
-// channel, lane = (b, pos) pairs strided by 64.
-__global__ __launch_bounds__(256) void k_rp_tail_bn(const float* __restrict__ zpart, int B, int training,
-                                                    float momentum, const char* __restrict__ blob, Layout L,
-                                                    BnPtrs bn, float* __restrict__ feat) {
-  const int lane = threadIdx.x & 63, c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const float bc = ((const float*)(blob + L.b6))[c];
-  const int n = B * 16;
-  auto zval = [&](int bp) {
-    const int b = bp >> 4, pos = bp & 15;
-    float z = bc;
-    for (int k = 0; k < TC_CHUNKS; ++k) z += zpart[(((long long)k * B + b) * C6 + c) * 16 + pos];
-    return z;
-  };
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  if (wave >= 2) return;
+  const int c = o0 + wave, n = B * 16;
+  const float* zc = zs + wave * n;
   float mean, var;
   if (training) {
     double s = 0.0, q = 0.0;
     for (int bp = lane; bp < n; bp += 64) {
-      const double v = zval(bp);
+      const double v = zc[bp];
       s += v;
       q += v * v;
     }
-    s = wave_sum_d(s);
-    q = wave_sum_d(q);
+    s = wave_sum_dbl(s);
+    q = wave_sum_dbl(q);
     const double nn = (double)n, m = s / nn;
     double v = q / nn - m * m;
     if (v < 0.0) v = 0.0;
@@ -2512,21 +2521,13 @@ __global__ __launch_bounds__(256) void k_rp_tail_bn(const float* __restrict__ zp
   const float sc = bn.p[5 * 4 + 0][c] / sqrtf(var + BN_EPS), sh = bn.p[5 * 4 + 1][c] - mean * sc;
   for (int base = 0; base < n; base += 64) {  // n is a multiple of 16: 16-lane groups are whole images
     const int bp = base + lane;
-    float r = bp < n ? fmaxf(zval(bp) * sc + sh, 0.f) : 0.f;
+    float r = bp < n ? fmaxf(zc[bp] * sc + sh, 0.f) : 0.f;
     r += __shfl_xor(r, 8);
     r += __shfl_xor(r, 4);
     r += __shfl_xor(r, 2);
     r += __shfl_xor(r, 1);
     if (bp < n && (lane & 15) == 0) feat[(long long)(bp >> 4) * C6 + c] = r / 16.f;
   }
-}
-
-__device__ __forceinline__ float hash_uniform(unsigned long long seed, unsigned long long idx) {
-  unsigned long long z = seed + idx * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
 
 // Linear 512 -> 128 + ReLU + Dropout(0.3): one workgroup per output o, thread = 2 k's for all
@@ -2665,7 +2666,7 @@ __global__ __launch_bounds__(256) void k_c4_pad_zero(bf16_t* __restrict__ att, i
 }
 
 struct Ws {  // workspace carve
-  size_t aff1, aff2, aff5, slab, att, y, part, pooled, zpart, feat, h1, fold, stem, total;
+  size_t aff1, aff2, aff5, slab, att, y, part, pooled, feat, h1, fold, stem, total;
 };
 
 inline int chain_grid(int B, int H, int W) {
@@ -2723,7 +2724,6 @@ inline Ws make_ws(int es, int B, int H, int W) {
   w.y = seg(es == 2 ? (size_t)conv4_tiles(B, H, W) * C4_TH * C4_TW * C5 * 2 : P * C5 * es);
   w.part = seg((size_t)B * 16 * POOL_SPLIT * C5 * sizeof(float));
   w.pooled = seg((size_t)B * C5 * 16 * sizeof(float));
-  w.zpart = seg((size_t)TC_CHUNKS * B * C6 * 16 * sizeof(float));
   w.feat = seg((size_t)B * C6 * sizeof(float));
   w.h1 = seg((size_t)B * 128 * sizeof(float));
   w.fold = seg(es == 2 ? FOLD_BYTES : 0);
@@ -2746,7 +2746,6 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   T* y = (T*)(ws + w.y);
   float* part = (float*)(ws + w.part);
   float* pooled = (float*)(ws + w.pooled);
-  float* zpart = (float*)(ws + w.zpart);
   float* feat = (float*)(ws + w.feat);
   float* h1 = (float*)(ws + w.h1);
   char* fold = ws + w.fold;
@@ -2860,8 +2859,12 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
     k_rp_bn_relu_pool<T><<<dim3(16 * POOL_SPLIT, B), 256, 0, s>>>(y, H, W, aff5, part);
     k_rp_pool_finish<<<ceil_div((long long)B * C5 * 16, 256), 256, 0, s>>>(part, B, H, W, pooled);
   }
-  k_rp_tail_conv<<<dim3(C6 / TC_O, TC_CHUNKS), 256, 0, s>>>(pooled, B, blob, L, zpart);
-  k_rp_tail_bn<<<C6 / 4, 256, 0, s>>>(zpart, B, training, momentum, blob, L, bn, feat);
+  {
+    static const hipError_t tattr =
+        hipFuncSetAttribute((const void*)k_rp_tail_convbn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TB_SMEM);
+    if (tattr != hipSuccess) return (int)tattr;
+    k_rp_tail_convbn<<<C6 / 2, 512, TB_SMEM, s>>>(pooled, B, training, momentum, blob, L, bn, feat);
+  }
   k_rp_tail_fc1<<<128, 256, 0, s>>>(feat, B, training, blob, L, seed, seed_ctr, h1);
   k_rp_tail_head<<<1, 512, 0, s>>>(h1, B, training, blob, L, seed, seed_ctr, ratio);
   RGBD_CHECK_LAUNCH();
