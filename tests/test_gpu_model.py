@@ -54,6 +54,24 @@ def test_ratio_predictor_eval_bf16_ragged(H, W):
     np.testing.assert_allclose(r, np.asarray(ref, dtype=np.float32).reshape(r.shape), atol=5e-3)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ratio_predictor_eval_batch_over_eight(dtype):
+    """Eval ratio at B = 11 (the fused tail's second, partial group of eight images) against the
+    fp32 CPU module tree: 1e-5 in fp32, the stated bf16 tolerance in bf16."""
+    pv = gi.pixel_values(6, 11, 64, 96)
+    m_cpu = _ratio_module().eval()
+    m = copy.deepcopy(m_cpu)
+    m.compute_dtype = dtype
+    m = m.to(DEV).eval()
+    r = m(torch.from_numpy(pv).to(DEV)[:, 3:6]).cpu().numpy()
+    with torch.no_grad():
+        ref = np.asarray(ratio_o.ratio_forward_modules(m_cpu, torch.from_numpy(pv[:, 3:6])), dtype=np.float32)
+    if dtype == torch.float32:
+        np.testing.assert_allclose(r, ref.reshape(r.shape), rtol=1e-5, atol=1e-6)
+    else:
+        np.testing.assert_allclose(r, ref.reshape(r.shape), atol=5e-3)
+
+
 def test_ratio_predictor_eval_bf16(golden):
     g4 = golden("g4_ratio")
     pv = gi.pixel_values(4, 2, 240, 320)
@@ -62,10 +80,12 @@ def test_ratio_predictor_eval_bf16(golden):
     np.testing.assert_allclose(r, g4["ratio"], atol=5e-3)  # stated bf16 tolerance on the ratio
 
 
-@pytest.mark.parametrize("H,W", [(240, 320), (96, 128)])
-def test_ratio_predictor_train_batchnorm(H, W):
-    """Train mode: batch-statistics BatchNorm; every running stat updated like torch."""
-    pv = gi.pixel_values(8, 3, H, W)
+@pytest.mark.parametrize("H,W,B", [(240, 320, 3), (96, 128, 3), (64, 96, 11)])
+def test_ratio_predictor_train_batchnorm(H, W, B):
+    """Train mode: batch-statistics BatchNorm; every running stat updated like torch.  B = 11:
+    the fused tail conv + BN stages its pooled maps eight images at a time (two groups, the second
+    partial)."""
+    pv = gi.pixel_values(8, B, H, W)
     m_cpu = _ratio_module().train()
     m = copy.deepcopy(m_cpu).to(DEV).train()
     m(torch.from_numpy(pv).to(DEV)[:, 3:6])
