@@ -88,13 +88,14 @@ def ratio_predictor_forward(module, depth_image: torch.Tensor) -> torch.Tensor:
     if ctr is None or ctr.device != d.device:
         ctr = module._rgbd_dropout_ctr = torch.zeros((1,), dtype=torch.int64, device=d.device)
         module._rgbd_dropout_seed = (torch.initial_seed() * 1000003 + next(_seed_counter) * 0x10000) & 0xFFFFFFFFFFFF
-    if training:  # one multi-tensor launch for the six BatchNorm counters (as torch's BatchNorm2d
-        # increments them before normalising; here ahead of the kernels, off the ratio's critical path)
-        with torch.no_grad():
-            torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
     # test hook: "phase2" computes the bf16 train-mode gated features by the phase-2 recompute
     flags = 1 if getattr(module, "train_route", "gate") == "phase2" else 0  # RGBD_RATIO_F_PHASE2
     check(L.rgbd_ratio_forward_ex(code, int(training), ctypes.c_float(momentum), ctypes.c_void_p(d.data_ptr()),
                                   d.stride(0), B, H, W, _p(blob), bn_arr, ctypes.c_ulonglong(module._rgbd_dropout_seed),
                                   _p(ctr), _p(ratio), _p(ws), flags, _stream(d.device)), "rgbd_ratio_forward_ex")
+    if training:  # one multi-tensor launch for the six BatchNorm counters (torch's BatchNorm2d
+        # increments them before normalising; with a set momentum nothing reads them, so they follow
+        # the kernels: queued ahead of them the launch delayed the predictor's first kernel)
+        with torch.no_grad():
+            torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
     return ratio.reshape(B, 1)
