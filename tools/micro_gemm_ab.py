@@ -20,7 +20,7 @@ from rgbd_amd import _lib, dense  # noqa: E402
 dev = torch.device("cuda")
 new = _lib.lib()
 libs = {"new": new}
-for other in sys.argv[1:]:
+for other in [v for v in sys.argv[1:] if not v.startswith("--")]:
     h = ctypes.CDLL(os.path.join(_R, other))
     for name, (res, args) in _lib.SIGNATURES.items():
         if hasattr(h, name):
@@ -36,16 +36,23 @@ shapes = [(800, 256, 256, 0, 0, 0, torch.bfloat16), (800, 256, 256, 0, 1, 1, tor
           (800, 49, 256, 0, 0, 0, torch.bfloat16), (49, 256, 800, 1, 1, 1, torch.bfloat16),
           (2400, 256, 256, 0, 0, 0, torch.bfloat16), (9600, 256, 256, 0, 0, 0, torch.bfloat16),
           (256, 256, 2400, 1, 1, 1, torch.bfloat16), (800, 256, 256, 0, 1, 1, torch.float32)]
+if "--big" in sys.argv:  # the pixel decoder's / Swin's many-tile forward products, with bias
+    sys.argv.remove("--big")
+    shapes = [(50400, 1024, 256, 0, 0, 0, torch.bfloat16), (50400, 256, 256, 0, 0, 0, torch.bfloat16),
+              (50400, 256, 1024, 0, 0, 0, torch.bfloat16), (50400, 192, 256, 0, 0, 0, torch.bfloat16),
+              (38400, 256, 256, 0, 0, 0, torch.bfloat16), (50400, 256, 256, 0, 0, 1, torch.bfloat16),
+              (153600, 384, 96, 0, 0, 0, torch.bfloat16)]
 n, rounds = 20, 5
 for M, N, K, at, bt, cf, dt in shapes:
     A = torch.randn((K, M) if at else (M, K), device=dev).to(dt)
     Bm = torch.randn((K, N) if bt else (N, K), device=dev).to(dt)
+    bias = torch.randn(N, device=dev) if M >= 38400 else None
     times = {k: [] for k in libs}
     outs, graphs = {}, {}
     for rnd in range(rounds + 1):
         for tag, L in libs.items():
             _lib._lib = L
-            fn = lambda: dense.gemm(A, Bm, at, bt, M, N, K, c_f32=bool(cf))  # noqa: E731
+            fn = lambda: dense.gemm(A, Bm, at, bt, M, N, K, c_f32=bool(cf), bias=bias)  # noqa: E731
             outs[tag] = fn()
             torch.cuda.synchronize()
             if rnd == 0:  # the n calls captured once per build: replays time the device alone
