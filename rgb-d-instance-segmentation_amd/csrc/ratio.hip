@@ -224,10 +224,13 @@ __device__ __forceinline__ double wave_sum_dbl(double v) {
 }
 // the channel's parameters load with the slab rows (thread 0), the sums reduce per wave by
 // shuffles, then the four wave sums in order: one barrier instead of the eight of a tree
+// slab layouts: row-major [nslab][row][2] (cm = 0), or channel-major [channel][nslab][2] (cm = 1:
+// the bf16 chain's phase 1 and conv5 v4 write it, so a block's reads are contiguous; the rows are
+// summed in the same order either way)
 __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, int nslab, int row, int c_off, int c,
                                                double count, int training, float momentum, const float* gamma,
                                                const float* beta, float* run_mean, float* run_var,
-                                               float2* __restrict__ affine) {
+                                               float2* __restrict__ affine, int cm = 0) {
   __shared__ double red[2][4];
   BnVals pv{};
   if (threadIdx.x == 0) pv = bn_vals(gamma, beta, run_mean, run_var, c);
@@ -238,7 +241,9 @@ __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, i
     for (; i + 256 * 7 < nslab; i += 256 * 8) {
       float2 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float2*>(slab + ((long long)(i + 256 * u) * row + c_off + c) * 2);
+      for (int u = 0; u < 8; ++u)
+        v[u] = *reinterpret_cast<const float2*>(
+            slab + (cm ? (long long)(c_off + c) * nslab + i + 256 * u : (long long)(i + 256 * u) * row + c_off + c) * 2);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         s += (double)v[u].x;
@@ -246,8 +251,9 @@ __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, i
       }
     }
     for (; i < nslab; i += 256) {
-      s += (double)slab[((long long)i * row + c_off + c) * 2 + 0];
-      q += (double)slab[((long long)i * row + c_off + c) * 2 + 1];
+      const long long e = cm ? (long long)(c_off + c) * nslab + i : (long long)i * row + c_off + c;
+      s += (double)slab[e * 2 + 0];
+      q += (double)slab[e * 2 + 1];
     }
   }
   s = wave_sum_dbl(s);
@@ -264,9 +270,10 @@ __device__ __forceinline__ void bn_affine_body(const float* __restrict__ slab, i
 __global__ __launch_bounds__(256) void k_bn_affine(const float* __restrict__ slab, int nslab, int row, int c_off,
                                                    int C, double count, int training, float momentum,
                                                    const float* gamma, const float* beta, float* run_mean,
-                                                   float* run_var, float2* __restrict__ affine) {
+                                                   float* run_var, float2* __restrict__ affine, int cm = 0) {
   if ((int)blockIdx.x >= C) return;
-  bn_affine_body(slab, nslab, row, c_off, blockIdx.x, count, training, momentum, gamma, beta, run_mean, run_var, affine);
+  bn_affine_body(slab, nslab, row, c_off, blockIdx.x, count, training, momentum, gamma, beta, run_mean, run_var, affine,
+                 cm);
 }
 // the three stem BNs (scale1/2/3, 64 channels each, concatenated :1463) in one launch
 __global__ __launch_bounds__(256) void k_bn_affine_stem(const float* __restrict__ slab, int nslab, double count,
@@ -1544,8 +1551,10 @@ __global__ __launch_bounds__(512, PHASE == 0 ? 4 : 2) void k_rp_chain_v2(const f
       a += __shfl_xor(a, 32);
       q += __shfl_xor(q, 32);
       if (g == 0) {
-        slab[(row * NC + 16 * t + r) * 2 + 0] = a;
-        slab[(row * NC + 16 * t + r) * 2 + 1] = q;
+        // phase 1: channel-major (k_bn_affine cm = 1); phase 0: row-major (k_bn_affine_stem)
+        const long long e = PHASE == 1 ? (long long)(16 * t + r) * (gridDim.x * 8) + row : row * NC + 16 * t + r;
+        slab[e * 2 + 0] = a;
+        slab[e * 2 + 1] = q;
       }
     }
   }
@@ -1890,7 +1899,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
 // first 32 MFMAs; every wave waits for its own copies, then the step's one barrier.
 // MODE 0 (train): y stored fragment-native per item [item = 2 tile + half][wave][mi][np][lane][8]
 //   (1 KiB contiguous per store instruction) and the BN statistics of the float32 conv outputs
-//   kept in registers across items -> slab[workgroup][256][2] (the other half's rows zero).
+//   kept in registers across items -> slab[256][workgroup][2] (the other half's entries zero).
 // MODE 1 (eval, H % 4 == 0, W % 64 == 0, H >= 64, W >= 128: every 16-px fragment row lies in one
 //   AdaptiveAvgPool(4) bin): BN (running statistics, `aff`) + ReLU of the bf16-rounded outputs
 //   summed per pool bin in the epilogue -> out[item][4 bin slots][128]; no y.
@@ -2209,12 +2218,12 @@ __global__ __launch_bounds__(512) void k_rp_conv5_v4(const bf16_t* __restrict__ 
       }
     }
     __syncthreads();
-    for (int i = tid; i < C5 * 2; i += 512) {
+    for (int i = tid; i < C5 * 2; i += 512) {  // channel-major [256][gridDim.x][2] (k_bn_affine cm = 1)
       const int c = i >> 1, k = i & 1;
       float v = 0.f;
       if ((c >> 7) == nh)
         for (int w = 0; w < 8; ++w) v += red[(w * 128 + (c & 127)) * 2 + k];
-      out[(long long)blockIdx.x * C5 * 2 + i] = v;
+      out[((long long)c * gridDim.x + blockIdx.x) * 2 + k] = v;
     }
   }
 }
@@ -2798,7 +2807,7 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
   bf16_t* fus = (bf16_t*)y;
   if (training) CHAIN_LAUNCH(1, aff1, nullptr, slab, gate ? (void*)fus : nullptr);
   k_bn_affine<<<FUS_C, 256, 0, s>>>(slab, nslab_ch, FUS_C, 0, FUS_C, P, training, momentum, bn.p[12], bn.p[13], bn.p[14],
-                                bn.p[15], aff2);
+                                bn.p[15], aff2, v2 ? 1 : 0);  // chain v2 phase 1: channel-major
   if (v2 && !gate) k_rp_fold<<<FUS_C, 256, 0, s>>>(blob, L, aff2, 2, fold);  // BN2 -> W2', b2'
   // gated attention features
   {
@@ -2836,9 +2845,9 @@ int ratio_forward(int training, float momentum, const float* depth3, long long b
       const int e = mode == 0 ? go(k_rp_conv5_v4<0>, slab) : mode == 1 ? go(k_rp_conv5_v4<1>, ip) : go(k_rp_conv5_v4<2>, nullptr);
       if (e != hipSuccess) return e;
     }
-    if (training)
+    if (training)  // conv5 v4 MODE 0: channel-major
       k_bn_affine<<<C5, 256, 0, s>>>(slab, gcv, C5, 0, C5, P, training, momentum, bn.p[16], bn.p[17], bn.p[18],
-                                     bn.p[19], aff5);
+                                     bn.p[19], aff5, 1);
     if (mode == 1) {
       k_rp_pool_finish_v4<<<dim3(16, B), 256, 0, s>>>((const float*)y, B, H, W, pooled);
     } else {
