@@ -69,7 +69,7 @@ ADAMW_BYTES_PER_PARAM = 28        # fused AdamW: read p, g, m, v; write p, m, v 
 
 # The committed evidence of this tree's default bench step (rocprofv3 kernel trace + PMC passes,
 # see its README): named explicitly, updated with each evidence commit, never picked by sort order.
-EVIDENCE_DIR = "profiles/r06_v3"
+EVIDENCE_DIR = "profiles/r06_v4"
 
 
 def pmc_traffic(kernel, default_shape):
