@@ -15,7 +15,7 @@ from rgbd_amd import deform_attn, init as winit, mask_predictor, masked_attentio
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-BF16_UNFORCED_REL_TOL = 4.5e-2  # G5 bf16 hot path, own attention masks
+BF16_UNFORCED_REL_TOL = 4.2e-2  # G5 bf16 hot path, own attention masks: 2x the measured 2.11e-2
 # G6 (whole-model gradients vs the reference), non-zero-class tensors: the CPU oracle (the reference
 # HF stages around the restated hot path) reaches norm 8.8e-5, sample L2 1.3e-3, max 1.4e-2 rms
 G6_NORM_REL, G6_SAMPLE_L2, G6_SAMPLE_MAX = 1e-4, 5e-3, 5e-2
@@ -335,7 +335,7 @@ def test_full_model_mask_logits_bf16(golden):
           f"{first['unexplained']} unexplained)")
     assert runs[True][0] < bench.BF16_LOGIT_REL_TOL  # the bench line's bound (parity.bf16.tolerance_rel)
     assert first["unexplained"] == 0
-    # measured 2.11e-2 (7 flipped bits at the first flipped call, all explained): ~2x headroom
+    # measured 2.11e-2 (7 flipped bits at the first flipped call, all explained): 2x headroom
     assert runs[False][0] < BF16_UNFORCED_REL_TOL
 
 
