@@ -54,11 +54,12 @@ def test_ratio_predictor_eval_bf16_ragged(H, W):
     np.testing.assert_allclose(r, np.asarray(ref, dtype=np.float32).reshape(r.shape), atol=5e-3)
 
 
+@pytest.mark.parametrize("B", [1, 11])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_ratio_predictor_eval_batch_over_eight(dtype):
-    """Eval ratio at B = 11 (the fused tail's second, partial group of eight images) against the
-    fp32 CPU module tree: 1e-5 in fp32, the stated bf16 tolerance in bf16."""
-    pv = gi.pixel_values(6, 11, 64, 96)
+def test_ratio_predictor_eval_batch_over_eight(dtype, B):
+    """Eval ratio at B = 11 (the fused tail's second, partial group of eight images) and B = 1
+    against the fp32 CPU module tree: 1e-5 in fp32, the stated bf16 tolerance in bf16."""
+    pv = gi.pixel_values(6, B, 64, 96)
     m_cpu = _ratio_module().eval()
     m = copy.deepcopy(m_cpu)
     m.compute_dtype = dtype
@@ -80,7 +81,7 @@ def test_ratio_predictor_eval_bf16(golden):
     np.testing.assert_allclose(r, g4["ratio"], atol=5e-3)  # stated bf16 tolerance on the ratio
 
 
-@pytest.mark.parametrize("H,W,B", [(240, 320, 3), (96, 128, 3), (64, 96, 11)])
+@pytest.mark.parametrize("H,W,B", [(240, 320, 3), (96, 128, 3), (64, 96, 11), (64, 96, 1)])
 def test_ratio_predictor_train_batchnorm(H, W, B):
     """Train mode: batch-statistics BatchNorm; every running stat updated like torch.  B = 11:
     the fused tail conv + BN stages its pooled maps eight images at a time (two groups, the second
